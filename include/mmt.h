@@ -1,0 +1,116 @@
+/* include/mmt.h -- C-ABI of libmmt, the MI355X-native per-frame front end of the
+ * cule/multimot_track multi-motion tracker (ORB extraction -> flow/semantic association ->
+ * per-motion pose solves).
+ *
+ * Plain pointers and sizes only; no OpenCV/Eigen/torch types.  Every entry point returns 0 on
+ * success and a negative errno-style code on failure (never exit()); mmt_last_error() gives the
+ * message.  One context per host thread, bound to one HIP device.  Inputs are caller-owned and
+ * read-only (the reference mutates depthmap in place, Tracking.cc:447-456; we do not).
+ *
+ * Reference interfaces replaced (paths relative to the reference checkout):
+ *   mmt_create          <- ORB_SLAM2::System::System(voc, settings, RGBD, viewer)  System.h:62,
+ *                          Tracking::Tracking settings parse Tracking.cc:135-238,
+ *                          ORBextractor::ORBextractor  ORBextractor.cc:410-470
+ *   mmt_orb_extract     <- ORBextractor::operator()(image, mask, keypoints, descriptors)
+ *                          ORBextractor.h:59-61 / ORBextractor.cc:1046-1109
+ *   mmt_orb_extract_batch / _device
+ *                       <- the same, over many frames (ORB extraction is stateless per frame)
+ *   mmt_track_rgbd      <- System::TrackRGBD(im, depthmap, flowmap, masksem, ...) System.h:73-75,
+ *                          System.cc:169-220 -> Tracking::GrabImageRGBD Tracking.cc:438-919
+ *   mmt_pose_flow_solve <- Optimizer::PoseOptimizationFlow2Cam / PoseOptimizationFlow2
+ *                          Optimizer.h:43-56, Optimizer.cc:396-601 / 2170-2377
+ *   mmt_destroy         <- System::Shutdown / delete
+ */
+#ifndef MMT_H
+#define MMT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMT_OK 0
+#define MMT_EINVAL (-22)
+#define MMT_ENOMEM (-12)
+#define MMT_ENOSPC (-28)
+#define MMT_EDEVICE (-5)
+#define MMT_ESTATE (-77)
+
+/* Settings of kitti03.yaml (Camera.*, ThDepth, ORBextractor.*) plus build-side knobs. */
+typedef struct mmt_config {
+  int width, height;              /* Camera.width / Camera.height                       */
+  float fx, fy, cx, cy;           /* Camera.fx fy cx cy                                  */
+  float k1, k2, p1, p2, k3;       /* distortion (must be 0 on this path)                 */
+  float bf;                       /* Camera.bf                                           */
+  float th_depth;                 /* ThDepth (baseline units, Tracking.cc:225)          */
+  int rgb;                        /* Camera.RGB (1: cvtColor RGB2GRAY on the input)      */
+  int orb_nfeatures;              /* ORBextractor.nFeatures                              */
+  float orb_scale_factor;         /* ORBextractor.scaleFactor                            */
+  int orb_nlevels;                /* ORBextractor.nLevels                                */
+  int orb_ini_th_fast;            /* ORBextractor.iniThFAST                              */
+  int orb_min_th_fast;            /* ORBextractor.minThFAST                              */
+  uint32_t noise_seed;            /* replaces cv::RNG(time(NULL)), Frame.cc:1246         */
+  int device_id;                  /* HIP device ordinal                                  */
+  int max_batch;                  /* frames in flight for batched ORB extraction         */
+} mmt_config;
+
+/* cv::KeyPoint, same field order and size (28 bytes). */
+typedef struct mmt_kp {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} mmt_kp;
+
+/* One recovered object motion (Tracking.cc:2127-2129: vObjMod = Tcw^-1 * X). */
+typedef struct mmt_motion {
+  int32_t label;        /* nModLabel (track id)                     */
+  int32_t sem_label;    /* semantic label (nSemPosition)            */
+  int32_t n_points;     /* flow vertices in the solve              */
+  int32_t n_inliers;    /* inliers after the solve                 */
+  float world_motion[16]; /* row-major 4x4 world-frame motion      */
+  float cam_pose[16];     /* row-major 4x4 camera-frame object pose X */
+} mmt_motion;
+
+typedef struct mmt_ctx mmt_ctx;
+
+int mmt_version(void);
+const char* mmt_last_error(const mmt_ctx* ctx);
+
+mmt_ctx* mmt_create(const mmt_config* cfg);
+void mmt_destroy(mmt_ctx* ctx);
+
+/* Per-level ORB tables derived exactly as ORBextractor's ctor (sizes nlevels). */
+int mmt_orb_levels(const mmt_ctx* ctx, float* scale, float* sigma2, int* n_per_level,
+                   int* level_w, int* level_h);
+
+/* ORBextractor::operator() on one 8-bit gray image (host pointers). keypoints/descriptors are
+ * level-major exactly as the reference.  *n receives the count; MMT_ENOSPC if cap is short. */
+int mmt_orb_extract(mmt_ctx* ctx, const uint8_t* gray, int w, int h, int stride, mmt_kp* kps,
+                    uint8_t* desc, int cap, int* n);
+
+/* Same over `nframes` host frames (each w x h, row stride `stride`), processed as one batch
+ * of device launches.  Outputs are frame-major with `cap_per_frame` slots per frame. */
+int mmt_orb_extract_batch(mmt_ctx* ctx, const uint8_t* const* grays, int nframes, int stride,
+                          mmt_kp* kps, uint8_t* desc, int cap_per_frame, int* n_per_frame);
+
+/* Device-resident variant: d_gray holds nframes gray frames (pitch frame_pitch bytes, rows of
+ * `width` bytes, tightly packed); all outputs are device pointers; runs on `stream`
+ * (hipStream_t, may be NULL for the context stream).  No host synchronisation. */
+int mmt_orb_extract_device(mmt_ctx* ctx, const uint8_t* d_gray, int nframes, size_t frame_pitch,
+                           mmt_kp* d_kps, uint8_t* d_desc, int cap_per_frame, int* d_n,
+                           void* stream);
+
+/* Debug: copy an intermediate device buffer of the last ORB run (frame 0..max_batch-1) to the
+ * host.  what: 0 pyramid, 1 blurred pyramid (both level-major, unpadded), 2 FAST per-cell
+ * counts (int), 3 FAST candidate keys (packed u32), 4 octree output keys (packed u32),
+ * 5 octree per-level counts (int), 6 device error flags (int).  Returns bytes written or <0. */
+long mmt_debug_fetch(mmt_ctx* ctx, int what, int frame, void* out, size_t cap);
+
+/* Upper bound on keypoints per frame (sum over levels of quota + 3). */
+int mmt_orb_capacity(const mmt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMT_H */

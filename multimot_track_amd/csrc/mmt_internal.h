@@ -1,0 +1,131 @@
+// multimot_track_amd/csrc/mmt_internal.h -- shared host-side declarations of libmmt.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/mmt.h"
+
+namespace mmt {
+
+#define MMT_HIP(call)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (call);                                                        \
+    if (e_ != hipSuccess) throw mmt::DeviceError(std::string(#call) + ": " +        \
+                                                 hipGetErrorString(e_));           \
+  } while (0)
+
+struct DeviceError {
+  std::string msg;
+  explicit DeviceError(std::string m) : msg(std::move(m)) {}
+};
+struct ArgError {
+  std::string msg;
+  explicit ArgError(std::string m) : msg(std::move(m)) {}
+};
+
+// ORB tables, computed on the host exactly like ORBextractor's ctor (ORBextractor.cc:410-470).
+struct OrbTables {
+  int nfeatures = 0, nlevels = 0, iniTh = 0, minTh = 0;
+  std::vector<float> scale, invScale, sigma2, invSigma2;
+  std::vector<int> nPerLevel, umax;
+  void init(int nfeatures, float scaleFactor, int nlevels, int iniTh, int minTh);
+};
+
+// Device-side geometry records (POD, uploaded once per context).
+struct LevelInfo {
+  int w, h;            // level size
+  int off;             // byte offset of the level inside one frame's pyramid
+  int nIni;            // DistributeOctTree initial node count (ORBextractor.cc:543)
+  float hX;            // initial node width (ORBextractor.cc:545)
+  int N;               // mnFeaturesPerLevel
+  int cell_begin, cell_end;  // cell index range (row-major cells of this level)
+  int key_off, key_cap;      // candidate-key slot range (per frame)
+  int out_off, out_cap;      // octree output slot range (per frame)
+  float scale;               // mvScaleFactor[level]
+  float size;                // (float)(int)(31 * scale)  (ORBextractor.cc:837)
+};
+
+struct CellInfo {
+  int level;
+  int r0, c0;          // tile origin in level coordinates (= iniY, iniX)
+  int rows, cols;      // tile size ((maxY-iniY) x (maxX-iniX))
+  int slot_off, slot_cap;
+  int pad;
+};
+
+struct ResizeX {  // horizontal INTER_LINEAR coefficients of one destination column
+  int sx;
+  short a0, a1;
+};
+struct ResizeY {
+  int sy0, sy1;
+  short b0, b1;
+};
+
+struct BlurTile {
+  int level, x0, y0, pad;
+};
+
+// Batched ORB extraction engine for one image size.
+class OrbEngine {
+ public:
+  OrbEngine() = default;
+  ~OrbEngine();
+  void setup(int w, int h, const OrbTables& t, int max_batch);
+  // d_gray: nframes x frame_pitch bytes, row pitch = width.  Outputs device pointers.
+  void run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_kp* d_kps,
+           uint8_t* d_desc, int cap_per_frame, int* d_n, hipStream_t stream);
+  int capacity() const { return cap_frame_; }
+  int width() const { return w_; }
+  int height() const { return h_; }
+  const std::vector<LevelInfo>& levels() const { return lv_; }
+  // Device pyramid of the last run (frame-major, pyr_stride_ bytes per frame).
+  const uint8_t* pyramid() const { return d_pyr_; }
+  size_t pyramid_stride() const { return pyr_stride_; }
+  long debug_fetch(int what, int frame, void* out, size_t cap, hipStream_t stream);
+
+ private:
+  void release();
+  int w_ = 0, h_ = 0, nlevels_ = 0, max_batch_ = 0, ncells_ = 0, ntiles_ = 0;
+  int total_slots_ = 0, out_slots_ = 0, cap_frame_ = 0, node_cap_ = 0;
+  int iniTh_ = 20, minTh_ = 7;
+  size_t pyr_stride_ = 0;
+  std::vector<LevelInfo> lv_;
+  std::vector<CellInfo> cells_;
+  std::vector<int> xtab_off_, ytab_off_;
+  LevelInfo* d_lv_ = nullptr;
+  CellInfo* d_cells_ = nullptr;
+  ResizeX* d_xtab_ = nullptr;
+  ResizeY* d_ytab_ = nullptr;
+  BlurTile* d_tiles_ = nullptr;
+  int* d_umax_ = nullptr;
+  uint8_t* d_pyr_ = nullptr;
+  uint8_t* d_blur_ = nullptr;
+  uint32_t* d_keys_ = nullptr;   // candidate keys, per frame total_slots_
+  uint32_t* d_lkeys_ = nullptr;  // per-level gathered keys
+  uint32_t* d_knode_ = nullptr;  // key -> node
+  int* d_cellcnt_ = nullptr;
+  uint32_t* d_okeys_ = nullptr;  // octree output, per frame out_slots_
+  int* d_ocount_ = nullptr;      // per frame nlevels
+  int* d_err_ = nullptr;
+};
+
+}  // namespace mmt
+
+struct mmt_ctx {
+  mmt_config cfg;
+  mmt::OrbTables orb;
+  mmt::OrbEngine engine;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // staging for the host-pointer entry points
+  uint8_t* d_in = nullptr;
+  size_t d_in_bytes = 0;
+  mmt_kp* d_kps = nullptr;
+  uint8_t* d_desc = nullptr;
+  int* d_n = nullptr;
+  int staged_frames = 0;
+};

@@ -1,0 +1,1018 @@
+// multimot_track_amd/csrc/mmt_orb.hip -- batched, bit-exact ORB extraction for gfx950.
+//
+// Replaces ORBextractor::operator() (reference src/ORBextractor.cc:1046-1109).  Pipeline per
+// batch of frames (every launch covers all frames of the batch):
+//   k_resize x (nlevels-1)   ComputePyramid, cv::resize INTER_LINEAR fixed point   (:1111-1136)
+//   k_fast                   per-cell FAST-9 + cell-local NMS + iniTh/minTh fallback (:765-829)
+//   k_octree                 DistributeOctTree, data-parallel pass formulation      (:539-763)
+//   k_blur                   GaussianBlur 7x7 sigma 2 bit-exact fixed point          (:1089-1090)
+//   k_orient_desc            IC_Angle + rotated BRIEF + level-major assembly  (:77-147, :1079-1108)
+// k_blur depends only on the pyramid; it is issued after k_octree on the same stream (a
+// second stream would overlap it with FAST/octree).
+//
+// All arithmetic that feeds an output is integer, or fp32 with contraction disabled
+// (-ffp-contract=off) and correctly rounded division, so results equal the CPU oracle bit for bit.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "mmt_internal.h"
+
+namespace mmt {
+
+static const int kEdge = 19;       // EDGE_THRESHOLD
+static const int kMinBorder = 16;  // EDGE_THRESHOLD - 3
+
+__constant__ int c_pattern[1024] = {
+#include "orb_pattern.inc"
+};
+
+static inline int host_round(float v) { return (int)lrintf(v); }
+static inline int host_floor(float v) {
+  int i = (int)v;
+  return i - (i > v);
+}
+static inline int host_ceil(float v) {
+  int i = (int)v;
+  return i + (i < v);
+}
+
+void OrbTables::init(int nf, float scaleFactorF, int nl, int ini, int mn) {
+  nfeatures = nf;
+  nlevels = nl;
+  iniTh = ini;
+  minTh = mn;
+  const double sf = (double)scaleFactorF;
+  scale.assign(nl, 1.f);
+  sigma2.assign(nl, 1.f);
+  for (int i = 1; i < nl; i++) {
+    scale[i] = (float)((double)scale[i - 1] * sf);
+    sigma2[i] = scale[i] * scale[i];
+  }
+  invScale.resize(nl);
+  invSigma2.resize(nl);
+  for (int i = 0; i < nl; i++) {
+    invScale[i] = 1.0f / scale[i];
+    invSigma2[i] = 1.0f / sigma2[i];
+  }
+  nPerLevel.assign(nl, 0);
+  const float factor = (float)(1.0f / sf);
+  float nd = nf * (1 - factor) / (1 - (float)pow((double)factor, (double)nl));
+  int sum = 0;
+  for (int l = 0; l < nl - 1; l++) {
+    nPerLevel[l] = host_round(nd);
+    sum += nPerLevel[l];
+    nd *= factor;
+  }
+  nPerLevel[nl - 1] = std::max(nf - sum, 0);
+  umax.assign(16, 0);
+  const int vmax = host_floor(15 * sqrtf(2.f) / 2 + 1), vmin = host_ceil(15 * sqrtf(2.f) / 2);
+  const double hp2 = 225.0;
+  int v, v0;
+  for (v = 0; v <= vmax; ++v) umax[v] = (int)lrint(sqrt(hp2 - v * v));
+  for (v = 15, v0 = 0; v >= vmin; --v) {
+    while (umax[v0] == umax[v0 + 1]) ++v0;
+    umax[v] = v0;
+    ++v0;
+  }
+}
+
+// ======================================================================== kernels
+
+// ---- pyramid level l from level l-1 (cv::resize INTER_LINEAR 8U, scalar fixed point) ----
+__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                int src_off, int sw, int dst_off, int dw,
+                                                const ResizeX* __restrict__ xt,
+                                                const ResizeY* __restrict__ yt) {
+  const int dx = blockIdx.x * 256 + threadIdx.x;
+  const int dy = blockIdx.y;
+  if (dx >= dw) return;
+  uint8_t* base = pyr + (size_t)blockIdx.z * pyr_stride;
+  const uint8_t* src = base + src_off;
+  const ResizeX cx = xt[dx];
+  const ResizeY cy = yt[dy];
+  const uint8_t* s0 = src + (size_t)cy.sy0 * sw + cx.sx;
+  const uint8_t* s1 = src + (size_t)cy.sy1 * sw + cx.sx;
+  // a1 == 0 marks the clamped right edge (dx >= xmax): only S[sx]*2048 contributes.
+  const int h0 = cx.a1 ? s0[0] * cx.a0 + s0[1] * cx.a1 : s0[0] * cx.a0;
+  const int h1 = cx.a1 ? s1[0] * cx.a0 + s1[1] * cx.a1 : s1[0] * cx.a0;
+  int v = (cy.b0 * h0 + cy.b1 * h1 + (1 << 21)) >> 22;
+  v = v < 0 ? 0 : (v > 255 ? 255 : v);
+  base[dst_off + (size_t)dy * dw + dx] = (uint8_t)v;
+}
+
+// ---- FAST arc strength: max over 9-arcs of min(v - p) (dark) and min(p - v) (bright). ----
+// A pixel is a FAST-9 corner at threshold t iff M > t, and OpenCV's cornerScore<16> returns
+// M - 1 for every corner (derivation in DESIGN.md), so one M per pixel serves both thresholds.
+__device__ __forceinline__ int arc_strength(const uint8_t* t, int stride, int r, int c) {
+  const int v = t[r * stride + c];
+  int d[16];
+  d[0] = v - t[(r + 3) * stride + c];
+  d[1] = v - t[(r + 3) * stride + c + 1];
+  d[2] = v - t[(r + 2) * stride + c + 2];
+  d[3] = v - t[(r + 1) * stride + c + 3];
+  d[4] = v - t[r * stride + c + 3];
+  d[5] = v - t[(r - 1) * stride + c + 3];
+  d[6] = v - t[(r - 2) * stride + c + 2];
+  d[7] = v - t[(r - 3) * stride + c + 1];
+  d[8] = v - t[(r - 3) * stride + c];
+  d[9] = v - t[(r - 3) * stride + c - 1];
+  d[10] = v - t[(r - 2) * stride + c - 2];
+  d[11] = v - t[(r - 1) * stride + c - 3];
+  d[12] = v - t[r * stride + c - 3];
+  d[13] = v - t[(r + 1) * stride + c - 3];
+  d[14] = v - t[(r + 2) * stride + c - 2];
+  d[15] = v - t[(r + 3) * stride + c - 1];
+  int mn2[16], mx2[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int a = d[k], b = d[(k + 1) & 15];
+    mn2[k] = min(a, b);
+    mx2[k] = max(a, b);
+  }
+  int mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+  }
+  int best = -1000;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+    const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+    best = max(best, max(mn9, -mx9));
+  }
+  return best;
+}
+
+#define FAST_TILE_MAX 5184  // 72 x 72 tile
+#define FAST_WIN_MAX 4356   // 66 x 66 window
+
+// One workgroup per (cell, frame).  Cell = the submatrix the reference hands to cv::FAST.
+__global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                              const LevelInfo* __restrict__ lv,
+                                              const CellInfo* __restrict__ cells, int ncells,
+                                              uint32_t* __restrict__ keys, int total_slots,
+                                              int* __restrict__ cellcnt, int iniTh, int minTh) {
+  __shared__ uint8_t tile[FAST_TILE_MAX];
+  __shared__ uint8_t arcm[FAST_WIN_MAX];
+  __shared__ uint8_t score[FAST_WIN_MAX];
+  __shared__ int s_wave[4];
+  __shared__ int s_total;
+  const CellInfo ci = cells[blockIdx.x];
+  const int frame = blockIdx.y;
+  const LevelInfo L = lv[ci.level];
+  const uint8_t* img = pyr + (size_t)frame * pyr_stride + L.off;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rows = ci.rows, cols = ci.cols;
+  for (int i = tid; i < rows * cols; i += 256) {
+    const int r = i / cols, c = i - r * cols;
+    tile[i] = img[(size_t)(ci.r0 + r) * L.w + ci.c0 + c];
+  }
+  __syncthreads();
+  const int R = rows - 6, C = cols - 6;  // detection window: tile rows 3..rows-4, cols 3..cols-4
+  const int npx = R * C;
+  for (int p = tid; p < npx; p += 256) {
+    const int r = p / C, c = p - r * C;
+    const int m = arc_strength(tile, cols, r + 3, c + 3);
+    arcm[p] = (uint8_t)(m < 0 ? 0 : m);
+  }
+  __syncthreads();
+  uint32_t* out = keys + (size_t)frame * total_slots + ci.slot_off;
+  int count = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
+    for (int p = tid; p < npx; p += 256) {
+      const int m = arcm[p];
+      score[p] = (uint8_t)(m > th ? m - 1 : 0);
+    }
+    __syncthreads();
+    // order-preserving compaction of NMS survivors, 256 pixels per round
+    int base = 0;
+    for (int p0 = 0; p0 < npx; p0 += 256) {
+      const int p = p0 + tid;
+      bool keep = false;
+      int s = 0;
+      if (p < npx && arcm[p] > th) {
+        const int r = p / C, c = p - r * C;
+        s = score[p];
+        keep = true;
+#pragma unroll
+        for (int dr = -1; dr <= 1; dr++)
+#pragma unroll
+          for (int dc = -1; dc <= 1; dc++) {
+            if (dr == 0 && dc == 0) continue;
+            const int rr = r + dr, cc = c + dc;
+            const int ns = (rr >= 0 && rr < R && cc >= 0 && cc < C) ? score[rr * C + cc] : 0;
+            keep = keep && (s > ns);
+          }
+      }
+      const unsigned long long bal = __ballot(keep);
+      const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) s_wave[wave] = __popcll(bal);
+      __syncthreads();
+      int woff = 0;
+      for (int w = 0; w < wave; w++) woff += s_wave[w];
+      const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+      if (keep) {
+        const int r = p / C, c = p - r * C;
+        const uint32_t x = (uint32_t)(ci.c0 - kMinBorder + c + 3);
+        const uint32_t y = (uint32_t)(ci.r0 - kMinBorder + r + 3);
+        const int slot = base + woff + rank;
+        if (slot < ci.slot_cap) out[slot] = (y << 20) | (x << 8) | (uint32_t)s;
+      }
+      base += tot;
+      __syncthreads();
+    }
+    count = base;
+    if (count > 0) break;
+  }
+  if (tid == 0) cellcnt[(size_t)frame * ncells + blockIdx.x] = min(count, ci.slot_cap);
+  (void)s_total;
+}
+
+// ---------------------------------------------------------------- octree helpers
+// In-place exclusive scan of LDS ints a[0..n) by the whole workgroup; returns the total.
+__device__ int wg_scan_excl(int* a, int n, int* s_tmp /*[17]*/) {
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
+  const int per = (n + nt - 1) / nt;
+  const int b = min(tid * per, n), e = min(b + per, n);
+  int local = 0;
+  for (int i = b; i < e; i++) local += a[i];
+  int incl = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_tmp[wave] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    const int nw = nt >> 6;
+    for (int w = 0; w < nw; w++) {
+      const int t = s_tmp[w];
+      s_tmp[w] = acc;
+      acc += t;
+    }
+    s_tmp[16] = acc;
+  }
+  __syncthreads();
+  int run = s_tmp[wave] + incl - local;
+  for (int i = b; i < e; i++) {
+    const int t = a[i];
+    a[i] = run;
+    run += t;
+  }
+  const int total = s_tmp[16];
+  __syncthreads();
+  return total;
+}
+
+__device__ __forceinline__ uint32_t key_x(uint32_t k) { return (k >> 8) & 0xFFFu; }
+__device__ __forceinline__ uint32_t key_y(uint32_t k) { return k >> 20; }
+__device__ __forceinline__ uint32_t key_s(uint32_t k) { return k & 0xFFu; }
+
+struct OctLDS {
+  uint16_t* x0[2];
+  uint16_t* y0[2];
+  uint16_t* x1[2];
+  uint16_t* y1[2];
+  uint32_t* cnt[2];
+  uint32_t* seq[2];
+  int* prank;
+  int* order;
+  int* gst;    // group start of processed rank r, later reused
+  int* cumnc;  // exclusive prefix of child counts
+  int* krank;  // kept-node rank
+  uint32_t* cc;          // 4 per processed rank (aliases sortkey / best)
+  unsigned long long* sortkey;
+  uint32_t* best;
+};
+
+// One division pass: nodes order[0..D) (processing order) are divided; every other node is kept.
+// Children of the last processed node go to the front (std::list::push_front semantics).
+// If `limitN` > 0 the pass stops after the first node whose division makes size >= limitN.
+__device__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D, int limitN,
+                         const uint32_t* __restrict__ lk, uint32_t* __restrict__ knode,
+                         uint8_t* __restrict__ kq, int n, int* s_tmp, int* s_ctl) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int c = cur;
+  for (int i = tid; i < 4 * D; i += nt) S.cc[i] = 0;
+  __syncthreads();
+  // 1) child counts per processed node
+  for (int i = tid; i < n; i += nt) {
+    const uint32_t nd = knode[i];
+    const int r = S.prank[nd];
+    if (r >= 0) {
+      const uint32_t k = lk[i];
+      const int hx = (int)ceilf((float)(S.x1[c][nd] - S.x0[c][nd]) / 2.f);
+      const int hy = (int)ceilf((float)(S.y1[c][nd] - S.y0[c][nd]) / 2.f);
+      const int mx = S.x0[c][nd] + hx, my = S.y0[c][nd] + hy;
+      const int q = ((int)key_x(k) < mx) ? (((int)key_y(k) < my) ? 0 : 2)
+                                         : (((int)key_y(k) < my) ? 1 : 3);
+      kq[i] = (uint8_t)q;
+      atomicAdd(&S.cc[r * 4 + q], 1u);
+    }
+  }
+  __syncthreads();
+  // 2) children per processed node; optional break at limitN (phase 2, ORBextractor.cc:730)
+  for (int r = tid; r < D; r += nt) {
+    int nc = 0;
+    for (int k = 0; k < 4; k++) nc += S.cc[r * 4 + k] > 0;
+    S.cumnc[r] = nc;
+  }
+  if (tid == 0) s_ctl[0] = D;
+  __syncthreads();
+  if (limitN > 0) {
+    for (int r = tid; r < D; r += nt) S.gst[r] = S.cumnc[r] - 1;
+    __syncthreads();
+    wg_scan_excl(S.gst, D, s_tmp);
+    for (int r = tid; r < D; r += nt) {
+      const int incl = S.gst[r] + S.cumnc[r] - 1;
+      if (L + incl >= limitN) atomicMin(&s_ctl[0], r + 1);
+    }
+    __syncthreads();
+  }
+  const int Dt = s_ctl[0];
+  for (int r = tid + Dt; r < D; r += nt) S.prank[S.order[r]] = -1;  // not divided this pass
+  __syncthreads();
+  const int T = wg_scan_excl(S.cumnc, Dt, s_tmp);  // cumnc = sum_{q<r} nc
+  for (int r = tid; r < Dt; r += nt) {
+    int nc = 0;
+    for (int k = 0; k < 4; k++) nc += S.cc[r * 4 + k] > 0;
+    S.gst[r] = T - S.cumnc[r] - nc;  // sum_{q>r} nc
+  }
+  for (int s = tid; s < L; s += nt) S.krank[s] = S.prank[s] < 0 ? 1 : 0;
+  __syncthreads();
+  const int K = wg_scan_excl(S.krank, L, s_tmp);
+  const int o = c ^ 1;
+  // 3) new node list: processed children (n4..n1 per group, last group first), then kept nodes
+  for (int r = tid; r < Dt; r += nt) {
+    const int nd = S.order[r];
+    const int X0 = S.x0[c][nd], Y0 = S.y0[c][nd], X1 = S.x1[c][nd], Y1 = S.y1[c][nd];
+    const int mx = X0 + (int)ceilf((float)(X1 - X0) / 2.f);
+    const int my = Y0 + (int)ceilf((float)(Y1 - Y0) / 2.f);
+    const int rx0[4] = {X0, mx, X0, mx}, ry0[4] = {Y0, Y0, my, my};
+    const int rx1[4] = {mx, X1, mx, X1}, ry1[4] = {my, my, Y1, Y1};
+    uint32_t cnts[4];
+    for (int k = 0; k < 4; k++) cnts[k] = S.cc[r * 4 + k];
+    int before = 0;
+    for (int k = 0; k < 4; k++) {
+      if (!cnts[k]) continue;
+      int after = 0;
+      for (int k2 = k + 1; k2 < 4; k2++) after += cnts[k2] > 0;
+      const int slot = S.gst[r] + after;
+      S.x0[o][slot] = (uint16_t)rx0[k];
+      S.y0[o][slot] = (uint16_t)ry0[k];
+      S.x1[o][slot] = (uint16_t)rx1[k];
+      S.y1[o][slot] = (uint16_t)ry1[k];
+      S.cnt[o][slot] = cnts[k];
+      S.seq[o][slot] = seqBase + (uint32_t)(S.cumnc[r] + before);
+      before++;
+    }
+  }
+  for (int s = tid; s < L; s += nt) {
+    if (S.prank[s] < 0) {
+      const int slot = T + S.krank[s];
+      S.x0[o][slot] = S.x0[c][s];
+      S.y0[o][slot] = S.y0[c][s];
+      S.x1[o][slot] = S.x1[c][s];
+      S.y1[o][slot] = S.y1[c][s];
+      S.cnt[o][slot] = S.cnt[c][s];
+      S.seq[o][slot] = S.seq[c][s];
+    }
+  }
+  __syncthreads();
+  // 4) key -> new node
+  for (int i = tid; i < n; i += nt) {
+    const uint32_t nd = knode[i];
+    const int r = S.prank[nd];
+    if (r >= 0) {
+      const int q = kq[i];
+      int after = 0;
+      for (int k2 = q + 1; k2 < 4; k2++) after += S.cc[r * 4 + k2] > 0;
+      knode[i] = (uint32_t)(S.gst[r] + after);
+    } else {
+      knode[i] = (uint32_t)(T + S.krank[nd]);
+    }
+  }
+  __syncthreads();
+  cur = o;
+  L = T + K;
+  seqBase += (uint32_t)T;
+}
+
+// Nodes with cnt > 1, in list order, into S.order; sets prank; returns their count.
+__device__ int oct_expandable_in_order(OctLDS& S, int cur, int L, int* s_tmp) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int s = tid; s < L; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
+  __syncthreads();
+  const int D = wg_scan_excl(S.gst, L, s_tmp);
+  for (int s = tid; s < L; s += nt) {
+    if (S.cnt[cur][s] > 1) {
+      S.order[S.gst[s]] = s;
+      S.prank[s] = S.gst[s];
+    } else {
+      S.prank[s] = -1;
+    }
+  }
+  __syncthreads();
+  return D;
+}
+
+// Phase-2 order: expandable nodes sorted by (size, creation seq) descending (ORBextractor.cc:684
+// sorts pair<size, ExtractorNode*> ascending and walks it backwards; pointer order is pinned to
+// creation order).
+__device__ int oct_expandable_sorted(OctLDS& S, int cur, int L, int ncap, int* s_tmp) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int s = tid; s < L; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
+  __syncthreads();
+  const int D = wg_scan_excl(S.gst, L, s_tmp);
+  int P = 1;
+  while (P < D) P <<= 1;
+  for (int i = tid; i < P; i += nt) S.sortkey[i] = 0ull;
+  __syncthreads();
+  for (int s = tid; s < L; s += nt) {
+    if (S.cnt[cur][s] > 1)
+      S.sortkey[S.gst[s]] = ((unsigned long long)S.cnt[cur][s] << 40) |
+                            ((unsigned long long)(S.seq[cur][s] & 0xFFFFFFu) << 16) |
+                            (unsigned long long)s;
+  }
+  __syncthreads();
+  // bitonic sort, descending
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += nt) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = S.sortkey[i], b = S.sortkey[ixj];
+          const bool desc = (i & k) == 0;
+          if (desc ? (a < b) : (a > b)) {
+            S.sortkey[i] = b;
+            S.sortkey[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int s = tid; s < L; s += nt) S.prank[s] = -1;
+  __syncthreads();
+  for (int r = tid; r < D; r += nt) {
+    const int s = (int)(S.sortkey[r] & 0xFFFFull);
+    S.order[r] = s;
+    S.prank[s] = r;
+  }
+  __syncthreads();
+  (void)ncap;
+  return D;
+}
+
+// One workgroup per (level, frame).  Gathers the level's FAST candidates in cell order and runs
+// DistributeOctTree.  Output: selected keys in list order, level coordinates.
+__global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ lv,
+                                                 const CellInfo* __restrict__ cells, int ncells,
+                                                 const uint32_t* __restrict__ keys,
+                                                 const int* __restrict__ cellcnt, int total_slots,
+                                                 uint32_t* __restrict__ lkeys,
+                                                 uint32_t* __restrict__ knode_g,
+                                                 uint32_t* __restrict__ okeys, int out_slots,
+                                                 int* __restrict__ ocount, int nlevels,
+                                                 int ncap, int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int s_tmp[17];
+  __shared__ int s_ctl[4];
+  const int level = blockIdx.x, frame = blockIdx.y;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const LevelInfo L0 = lv[level];
+  // ---- carve LDS (all offsets multiples of 16)
+  OctLDS S;
+  unsigned char* p = smem;
+  auto carve = [&](size_t bytes) {
+    unsigned char* r = p;
+    p += (bytes + 15) & ~(size_t)15;
+    return r;
+  };
+  for (int b = 0; b < 2; b++) {
+    S.x0[b] = (uint16_t*)carve(2 * ncap);
+    S.y0[b] = (uint16_t*)carve(2 * ncap);
+    S.x1[b] = (uint16_t*)carve(2 * ncap);
+    S.y1[b] = (uint16_t*)carve(2 * ncap);
+    S.cnt[b] = (uint32_t*)carve(4 * ncap);
+    S.seq[b] = (uint32_t*)carve(4 * ncap);
+  }
+  S.prank = (int*)carve(4 * ncap);
+  S.order = (int*)carve(4 * ncap);
+  S.gst = (int*)carve(4 * ncap);
+  S.cumnc = (int*)carve(4 * ncap);
+  S.krank = (int*)carve(4 * ncap);
+  S.cc = (uint32_t*)carve(16 * ncap);
+  S.sortkey = (unsigned long long*)S.cc;
+  S.best = S.cc;
+
+  // ---- gather candidates of this level in cell order
+  const int nc = L0.cell_end - L0.cell_begin;
+  const int* cnt = cellcnt + (size_t)frame * ncells + L0.cell_begin;
+  int* coff = (int*)S.cc;  // reuse as scratch (nc <= 4 * ncap checked on host)
+  for (int i = tid; i < nc; i += nt) coff[i] = cnt[i];
+  __syncthreads();
+  const int n = wg_scan_excl(coff, nc, s_tmp);
+  uint32_t* lk = lkeys + (size_t)frame * total_slots + L0.key_off;
+  uint32_t* knode = knode_g + (size_t)frame * total_slots + L0.key_off;
+  // quadrant scratch lives in the upper bytes of this level's gathered-key region of `lkeys`?
+  // no: use a dedicated byte view after knode's slots (total_slots*4 bytes per frame reserved).
+  uint8_t* kq = (uint8_t*)(knode_g + (size_t)gridDim.y * total_slots) +
+                (size_t)frame * total_slots + L0.key_off;
+  const uint32_t* fk = keys + (size_t)frame * total_slots;
+  for (int ci = 0; ci < nc; ci++) {
+    const CellInfo cell = cells[L0.cell_begin + ci];
+    const int m = cnt[ci], o = coff[ci];
+    for (int j = tid; j < m; j += nt) lk[o + j] = fk[cell.slot_off + j];
+  }
+  __syncthreads();
+  uint32_t* outp = okeys + (size_t)frame * out_slots + L0.out_off;
+  if (n == 0) {
+    if (tid == 0) ocount[frame * nlevels + level] = 0;
+    return;
+  }
+  // ---- initial nodes (ORBextractor.cc:552-585)
+  const int nIni = L0.nIni;
+  const float hX = L0.hX;
+  const int H = (L0.h - kEdge + 3) - kMinBorder;  // maxBorderY - minBorderY
+  for (int i = tid; i < nIni; i += nt) S.cnt[0][i] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += nt) {
+    const int idx = (int)((float)key_x(lk[i]) / hX);
+    knode[i] = (uint32_t)idx;
+    atomicAdd(&S.cnt[0][idx], 1u);
+  }
+  __syncthreads();
+  for (int i = tid; i < nIni; i += nt) S.krank[i] = S.cnt[0][i] > 0 ? 1 : 0;
+  __syncthreads();
+  int Lsz = wg_scan_excl(S.krank, nIni, s_tmp);
+  for (int i = tid; i < nIni; i += nt) {
+    if (S.cnt[0][i] > 0) {
+      const int s = S.krank[i];
+      S.x0[1][s] = (uint16_t)(int)(hX * (float)i);
+      S.x1[1][s] = (uint16_t)(int)(hX * (float)(i + 1));
+      S.y0[1][s] = 0;
+      S.y1[1][s] = (uint16_t)H;
+      S.cnt[1][s] = S.cnt[0][i];
+      S.seq[1][s] = (uint32_t)i;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += nt) knode[i] = (uint32_t)S.krank[knode[i]];
+  __syncthreads();
+  int cur = 1;
+  uint32_t seqBase = (uint32_t)nIni;
+  const int N = L0.N;
+  // ---- main loop (ORBextractor.cc:594-739)
+  bool finish = false;
+  int guard = 0;
+  while (!finish) {
+    if (++guard > 4096) {
+      if (tid == 0) atomicOr(err, 1);
+      break;
+    }
+    const int prevSize = Lsz;
+    const int D = oct_expandable_in_order(S, cur, Lsz, s_tmp);
+    oct_pass(S, cur, Lsz, seqBase, D, 0, lk, knode, kq, n, s_tmp, s_ctl);
+    // nToExpand = nodes with more than one key
+    for (int s = tid; s < Lsz; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
+    __syncthreads();
+    const int nToExpand = wg_scan_excl(S.gst, Lsz, s_tmp);
+    if (Lsz >= N || Lsz == prevSize) {
+      finish = true;
+    } else if (Lsz + nToExpand * 3 > N) {
+      while (!finish) {
+        if (++guard > 4096) {
+          if (tid == 0) atomicOr(err, 1);
+          finish = true;
+          break;
+        }
+        const int prev2 = Lsz;
+        const int D2 = oct_expandable_sorted(S, cur, Lsz, ncap, s_tmp);
+        oct_pass(S, cur, Lsz, seqBase, D2, N, lk, knode, kq, n, s_tmp, s_ctl);
+        if (Lsz >= N || Lsz == prev2) finish = true;
+      }
+    }
+    if (Lsz + 4 > ncap) {  // capacity guard (cannot happen for N + 8 <= ncap)
+      if (tid == 0) atomicOr(err, 2);
+      finish = true;
+    }
+  }
+  // ---- retain the best key per node: max response, first in key order (:744-760)
+  for (int s = tid; s < Lsz; s += nt) S.best[s] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += nt)
+    atomicMax(&S.best[knode[i]], (key_s(lk[i]) << 24) | (0xFFFFFFu - (uint32_t)i));
+  __syncthreads();
+  const int nout = min(Lsz, L0.out_cap);
+  for (int s = tid; s < nout; s += nt) {
+    const uint32_t i = 0xFFFFFFu - (S.best[s] & 0xFFFFFFu);
+    const uint32_t k = lk[i];
+    const uint32_t x = key_x(k) + kMinBorder, y = key_y(k) + kMinBorder;
+    outp[s] = (y << 20) | (x << 8) | key_s(k);
+  }
+  if (tid == 0) {
+    ocount[frame * nlevels + level] = nout;
+    if (Lsz > L0.out_cap) atomicOr(err, 4);
+  }
+}
+
+// ---- GaussianBlur 7x7 sigma 2, 8U bit-exact, BORDER_REFLECT_101 ---------------------------
+__device__ __forceinline__ int reflect101(int p, int n) {
+  p = p < 0 ? -p : p;
+  p = p >= n ? 2 * n - 2 - p : p;
+  return p;
+}
+
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
+                                              uint8_t* __restrict__ blur, size_t pyr_stride,
+                                              const LevelInfo* __restrict__ lv,
+                                              const BlurTile* __restrict__ tiles) {
+  // taps of getGaussianKernelBitExact(7, 2) quantised to Q8 with error diffusion
+  const int T0 = 18, T1 = 34, T2 = 48, T3 = 56;
+  __shared__ uint8_t src[22][72];
+  __shared__ uint16_t hs[22][64];
+  const BlurTile t = tiles[blockIdx.x];
+  const LevelInfo L = lv[t.level];
+  const size_t fo = (size_t)blockIdx.y * pyr_stride + L.off;
+  const uint8_t* img = pyr + fo;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 22 * 70; i += 256) {
+    const int r = i / 70, c = i - r * 70;
+    const int y = reflect101(min(t.y0 + r - 3, L.h + 2), L.h);
+    const int x = reflect101(min(t.x0 + c - 3, L.w + 2), L.w);
+    src[r][c] = img[(size_t)y * L.w + x];
+  }
+  __syncthreads();
+  for (int i = tid; i < 22 * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    const uint8_t* s = &src[r][c];
+    hs[r][c] = (uint16_t)(T0 * (s[0] + s[6]) + T1 * (s[1] + s[5]) + T2 * (s[2] + s[4]) + T3 * s[3]);
+  }
+  __syncthreads();
+  for (int i = tid; i < 16 * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    const int y = t.y0 + r, x = t.x0 + c;
+    if (y >= L.h || x >= L.w) continue;
+    const uint32_t v = T0 * ((uint32_t)hs[r][c] + hs[r + 6][c]) +
+                       T1 * ((uint32_t)hs[r + 1][c] + hs[r + 5][c]) +
+                       T2 * ((uint32_t)hs[r + 2][c] + hs[r + 4][c]) + T3 * (uint32_t)hs[r + 3][c];
+    blur[fo + (size_t)y * L.w + x] = (uint8_t)min((v + 32768u) >> 16, 255u);
+  }
+}
+
+// ---- fastAtan2 (OpenCV core), fp32 without contraction -------------------------------------
+__device__ __forceinline__ float fast_atan2_deg(float y, float x) {
+  const float k = (float)(180.0 / 3.14159265358979323846);
+  const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
+  const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+  const float eps = (float)2.220446049250313e-16;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + eps);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + eps);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+// One wave per output keypoint slot: IC_Angle on the level (:77-104), rotated BRIEF on the
+// blurred level (:108-147), level-major assembly with coordinate scaling (:1079-1108).
+__global__ __launch_bounds__(256) void k_orient_desc(
+    const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur, size_t pyr_stride,
+    const LevelInfo* __restrict__ lv, int nlevels, const int* __restrict__ umax,
+    const uint32_t* __restrict__ okeys, int out_slots, const int* __restrict__ ocount,
+    mmt_kp* __restrict__ kps, uint8_t* __restrict__ desc, int cap_frame, int* __restrict__ nkp,
+    int nframes) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int frame = g / out_slots;
+  if (frame >= nframes) return;
+  const int local = g - frame * out_slots;
+  const int* oc = ocount + frame * nlevels;
+  if (local == 0 && lane == 0) {
+    int tot = 0;
+    for (int l = 0; l < nlevels; l++) tot += oc[l];
+    nkp[frame] = min(tot, cap_frame);
+  }
+  int level = 0, before = 0;
+  while (level + 1 < nlevels && local >= lv[level + 1].out_off) {
+    before += oc[level];
+    level++;
+  }
+  const LevelInfo L = lv[level];
+  const int s = local - L.out_off;
+  if (s >= oc[level]) return;
+  const int outi = before + s;
+  if (outi >= cap_frame) return;
+  const uint32_t k = okeys[(size_t)frame * out_slots + local];
+  const int kx = (int)((k >> 8) & 0xFFFu), ky = (int)(k >> 20);
+  const float response = (float)(k & 0xFFu);
+  const size_t fo = (size_t)frame * pyr_stride + L.off;
+  // --- IC_Angle: lane u+15 owns column u of the radius-15 disc
+  const uint8_t* img = pyr + fo;
+  int m10 = 0, m01 = 0;
+  if (lane < 31) {
+    const int u = lane - 15;
+    const int au = u < 0 ? -u : u;
+    const uint8_t* col = img + (size_t)ky * L.w + kx + u;
+    int colsum = col[0];
+    int vs = 0;
+    for (int v = 1; v <= 15; v++) {
+      if (au <= umax[v]) {
+        const int vp = col[(size_t)v * L.w], vm = col[-(ptrdiff_t)v * L.w];
+        colsum += vp + vm;
+        vs += v * (vp - vm);
+      }
+    }
+    m10 = u * colsum;
+    m01 = vs;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    m10 += __shfl_xor(m10, o, 64);
+    m01 += __shfl_xor(m01, o, 64);
+  }
+  const float angle = fast_atan2_deg((float)m01, (float)m10);
+  // --- rotated BRIEF; cos/sin pinned to (float)cos((double)angle) (parity hazards)
+  const float factorPI = (float)(3.14159265358979323846 / 180.0);
+  const float ang = angle * factorPI;
+  const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+  const uint8_t* center = blur + fo + (size_t)ky * L.w + kx;
+  const int step = L.w;
+  uint8_t* dout = desc + ((size_t)frame * cap_frame + outi) * 32;
+  for (int j = 0; j < 4; j++) {
+    const int t = j * 64 + lane;
+    const float x0 = (float)c_pattern[4 * t], y0 = (float)c_pattern[4 * t + 1];
+    const float x1 = (float)c_pattern[4 * t + 2], y1 = (float)c_pattern[4 * t + 3];
+    const float ry0 = x0 * b + y0 * a, rx0 = x0 * a - y0 * b;
+    const float ry1 = x1 * b + y1 * a, rx1 = x1 * a - y1 * b;
+    const int v0 = center[__float2int_rn(ry0) * step + __float2int_rn(rx0)];
+    const int v1 = center[__float2int_rn(ry1) * step + __float2int_rn(rx1)];
+    const unsigned long long bal = __ballot(v0 < v1);
+    if (lane == j) *(unsigned long long*)(dout + 8 * j) = bal;
+  }
+  if (lane == 0) {
+    mmt_kp kp;
+    kp.x = level == 0 ? (float)kx : (float)kx * L.scale;
+    kp.y = level == 0 ? (float)ky : (float)ky * L.scale;
+    kp.size = L.size;
+    kp.angle = angle;
+    kp.response = response;
+    kp.octave = level;
+    kp.class_id = -1;
+    kps[(size_t)frame * cap_frame + outi] = kp;
+  }
+}
+
+// ======================================================================== host engine
+
+static size_t octree_lds_bytes(int ncap) {
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  size_t b = 0;
+  for (int i = 0; i < 2; i++) b += 4 * r16(2 * ncap) + 2 * r16(4 * ncap);
+  b += 5 * r16(4 * ncap) + r16(16 * ncap);
+  return b;
+}
+
+OrbEngine::~OrbEngine() { release(); }
+
+void OrbEngine::release() {
+  void* ptrs[] = {d_lv_,   d_cells_,   d_xtab_,  d_ytab_,   d_tiles_, d_umax_, d_pyr_, d_blur_,
+                  d_keys_, d_lkeys_, d_knode_, d_cellcnt_, d_okeys_, d_ocount_, d_err_};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  d_lv_ = nullptr;
+  d_cells_ = nullptr;
+  d_xtab_ = nullptr;
+  d_ytab_ = nullptr;
+  d_tiles_ = nullptr;
+  d_umax_ = nullptr;
+  d_pyr_ = d_blur_ = nullptr;
+  d_keys_ = d_lkeys_ = d_knode_ = d_okeys_ = nullptr;
+  d_cellcnt_ = d_ocount_ = d_err_ = nullptr;
+}
+
+template <typename T>
+static void upload(T** dptr, const std::vector<T>& v) {
+  MMT_HIP(hipMalloc((void**)dptr, std::max<size_t>(1, v.size()) * sizeof(T)));
+  if (!v.empty()) MMT_HIP(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+
+void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
+  release();
+  if (w > 4000 || h > 4000) throw ArgError("image larger than 4000 px is not supported");
+  w_ = w;
+  h_ = h;
+  nlevels_ = t.nlevels;
+  max_batch_ = std::max(1, max_batch);
+  iniTh_ = t.iniTh;
+  minTh_ = t.minTh;
+  lv_.assign(nlevels_, LevelInfo());
+  cells_.clear();
+  int off = 0, key_off = 0, out_off = 0, maxN = 0;
+  std::vector<ResizeX> xt;
+  std::vector<ResizeY> yt;
+  xtab_off_.assign(nlevels_, 0);
+  ytab_off_.assign(nlevels_, 0);
+  std::vector<BlurTile> tiles;
+  for (int l = 0; l < nlevels_; l++) {
+    LevelInfo& L = lv_[l];
+    L.w = host_round((float)w * t.invScale[l]);
+    L.h = host_round((float)h * t.invScale[l]);
+    if (L.w - 2 * kMinBorder < 30 || L.h - 2 * kMinBorder < 30)
+      throw ArgError("image too small for the requested pyramid (level " + std::to_string(l) + ")");
+    L.off = off;
+    off += L.w * L.h;
+    // FAST cells (ORBextractor.cc:769-806)
+    const int maxBorderX = L.w - kEdge + 3, maxBorderY = L.h - kEdge + 3;
+    const float width = (float)(maxBorderX - kMinBorder), height = (float)(maxBorderY - kMinBorder);
+    const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
+    const int wCell = (int)ceil(width / nCols), hCell = (int)ceil(height / nRows);
+    L.cell_begin = (int)cells_.size();
+    L.key_off = key_off;
+    for (int i = 0; i < nRows; i++) {
+      const float iniY = (float)(kMinBorder + i * hCell);
+      float maxY = iniY + hCell + 6;
+      if (iniY >= maxBorderY - 3) continue;
+      if (maxY > maxBorderY) maxY = (float)maxBorderY;
+      for (int j = 0; j < nCols; j++) {
+        const float iniX = (float)(kMinBorder + j * wCell);
+        float maxX = iniX + wCell + 6;
+        if (iniX >= maxBorderX - 6) continue;
+        if (maxX > maxBorderX) maxX = (float)maxBorderX;
+        CellInfo c;
+        c.level = l;
+        c.r0 = (int)iniY;
+        c.c0 = (int)iniX;
+        c.rows = (int)maxY - (int)iniY;
+        c.cols = (int)maxX - (int)iniX;
+        if (c.rows * c.cols > FAST_TILE_MAX || (c.rows - 6) * (c.cols - 6) > FAST_WIN_MAX)
+          throw ArgError("FAST cell larger than the LDS tile");
+        const int R = std::max(c.rows - 6, 0), C = std::max(c.cols - 6, 0);
+        c.slot_cap = ((R + 1) / 2) * ((C + 1) / 2);  // max strict-NMS survivors
+        c.slot_off = key_off;
+        c.pad = 0;
+        key_off += c.slot_cap;
+        cells_.push_back(c);
+      }
+    }
+    L.cell_end = (int)cells_.size();
+    L.key_cap = key_off - L.key_off;
+    // octree geometry (ORBextractor.cc:543-545)
+    const int minX = kMinBorder, maxX = maxBorderX, minY = kMinBorder, maxY = maxBorderY;
+    L.nIni = (int)round(static_cast<float>(maxX - minX) / (maxY - minY));
+    if (L.nIni < 1) throw ArgError("degenerate octree geometry (nIni < 1)");
+    L.hX = static_cast<float>(maxX - minX) / L.nIni;
+    L.N = t.nPerLevel[l];
+    maxN = std::max(maxN, L.N);
+    L.out_off = out_off;
+    L.out_cap = L.N + 8;
+    out_off += L.out_cap;
+    L.scale = t.scale[l];
+    L.size = (float)(int)(31 * t.scale[l]);
+    // resize tables for level l (from l-1)
+    if (l > 0) {
+      const LevelInfo& S = lv_[l - 1];
+      const int sw = S.w, sh = S.h, dw = L.w, dh = L.h;
+      const double isx = (double)dw / sw, isy = (double)dh / sh;
+      const double scx = 1. / isx, scy = 1. / isy;
+      xtab_off_[l] = (int)xt.size();
+      for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scx - 0.5);
+        int sx = host_floor(fx);
+        fx -= sx;
+        bool clampR = false;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+          clampR = true;
+          if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        ResizeX r;
+        r.sx = sx;
+        r.a0 = (short)std::min(std::max(host_round((1.f - fx) * 2048), -32768), 32767);
+        r.a1 = (short)std::min(std::max(host_round(fx * 2048), -32768), 32767);
+        if (clampR) { r.a0 = 2048; r.a1 = 0; }
+        xt.push_back(r);
+      }
+      ytab_off_[l] = (int)yt.size();
+      for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scy - 0.5);
+        int sy = host_floor(fy);
+        fy -= sy;
+        auto clip = [&](int v) { return v >= 0 ? (v < sh ? v : sh - 1) : 0; };
+        ResizeY r;
+        r.sy0 = clip(sy);
+        r.sy1 = clip(sy + 1);
+        r.b0 = (short)std::min(std::max(host_round((1.f - fy) * 2048), -32768), 32767);
+        r.b1 = (short)std::min(std::max(host_round(fy * 2048), -32768), 32767);
+        yt.push_back(r);
+      }
+    }
+    for (int y0 = 0; y0 < L.h; y0 += 16)
+      for (int x0 = 0; x0 < L.w; x0 += 64) tiles.push_back(BlurTile{l, x0, y0, 0});
+  }
+  ncells_ = (int)cells_.size();
+  ntiles_ = (int)tiles.size();
+  total_slots_ = key_off;
+  out_slots_ = out_off;
+  cap_frame_ = out_off;
+  pyr_stride_ = ((size_t)off + 255) & ~(size_t)255;
+  node_cap_ = 256;
+  while (node_cap_ < maxN + 16) node_cap_ <<= 1;
+  for (auto& L : lv_) {
+    while (L.cell_end - L.cell_begin > 4 * node_cap_) node_cap_ <<= 1;  // gather scratch
+    if (L.nIni > node_cap_) throw ArgError("too many initial octree nodes");
+  }
+  if (node_cap_ > 2048) throw ArgError("ORB nfeatures too large for the LDS octree (max ~9000)");
+  MMT_HIP(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)octree_lds_bytes(node_cap_)));
+  upload(&d_lv_, lv_);
+  upload(&d_cells_, cells_);
+  upload(&d_xtab_, xt);
+  upload(&d_ytab_, yt);
+  upload(&d_tiles_, tiles);
+  upload(&d_umax_, t.umax);
+  const size_t B = (size_t)max_batch_;
+  MMT_HIP(hipMalloc((void**)&d_pyr_, B * pyr_stride_));
+  MMT_HIP(hipMalloc((void**)&d_blur_, B * pyr_stride_));
+  MMT_HIP(hipMalloc((void**)&d_keys_, B * total_slots_ * sizeof(uint32_t)));
+  MMT_HIP(hipMalloc((void**)&d_lkeys_, B * total_slots_ * sizeof(uint32_t)));
+  // knode (u32 per slot) followed by the per-key quadrant bytes (u8 per slot)
+  MMT_HIP(hipMalloc((void**)&d_knode_, B * total_slots_ * (sizeof(uint32_t) + 1) + 16));
+  MMT_HIP(hipMalloc((void**)&d_cellcnt_, B * ncells_ * sizeof(int)));
+  MMT_HIP(hipMalloc((void**)&d_okeys_, B * out_slots_ * sizeof(uint32_t)));
+  MMT_HIP(hipMalloc((void**)&d_ocount_, B * nlevels_ * sizeof(int)));
+  MMT_HIP(hipMalloc((void**)&d_err_, sizeof(int)));
+  MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
+}
+
+void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_kp* d_kps,
+                    uint8_t* d_desc, int cap_per_frame, int* d_n, hipStream_t stream) {
+  if (nframes < 1 || nframes > max_batch_) throw ArgError("nframes outside [1, max_batch]");
+  if (cap_per_frame < cap_frame_) throw ArgError("cap_per_frame below mmt_orb_capacity()");
+  const size_t lvl0 = (size_t)w_ * h_;
+  // level 0: copy the gray frames into the pyramid buffer
+  MMT_HIP(hipMemcpy2DAsync(d_pyr_, pyr_stride_, d_gray, frame_pitch, lvl0, nframes,
+                           hipMemcpyDeviceToDevice, stream));
+  for (int l = 1; l < nlevels_; l++) {
+    const LevelInfo& S = lv_[l - 1];
+    const LevelInfo& L = lv_[l];
+    dim3 grid((L.w + 255) / 256, L.h, nframes);
+    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, d_pyr_, pyr_stride_, S.off, S.w,
+                       L.off, L.w, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l]);
+  }
+  hipLaunchKernelGGL(k_fast, dim3(ncells_, nframes), dim3(256), 0, stream, d_pyr_, pyr_stride_,
+                     d_lv_, d_cells_, ncells_, d_keys_, total_slots_, d_cellcnt_, iniTh_, minTh_);
+  const size_t lds = octree_lds_bytes(node_cap_);
+  hipLaunchKernelGGL(k_octree, dim3(nlevels_, nframes), dim3(1024), lds, stream, d_lv_, d_cells_,
+                     ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,
+                     out_slots_, d_ocount_, nlevels_, node_cap_, d_err_);
+  hipLaunchKernelGGL(k_blur, dim3(ntiles_, nframes), dim3(256), 0, stream, d_pyr_, d_blur_,
+                     pyr_stride_, d_lv_, d_tiles_);
+  const int waves = nframes * out_slots_;
+  hipLaunchKernelGGL(k_orient_desc, dim3((waves + 3) / 4), dim3(256), 0, stream, d_pyr_, d_blur_,
+                     pyr_stride_, d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_,
+                     d_kps, d_desc, cap_per_frame, d_n, nframes);
+  MMT_HIP(hipGetLastError());
+}
+
+long OrbEngine::debug_fetch(int what, int frame, void* out, size_t cap, hipStream_t stream) {
+  if (frame < 0 || frame >= max_batch_) throw ArgError("bad frame");
+  const void* src = nullptr;
+  size_t bytes = 0;
+  size_t P = 0;
+  for (auto& L : lv_) P += (size_t)L.w * L.h;
+  switch (what) {
+    case 0: src = d_pyr_ + frame * pyr_stride_; bytes = P; break;
+    case 1: src = d_blur_ + frame * pyr_stride_; bytes = P; break;
+    case 2: src = d_cellcnt_ + (size_t)frame * ncells_; bytes = sizeof(int) * ncells_; break;
+    case 3: src = d_keys_ + (size_t)frame * total_slots_; bytes = 4 * (size_t)total_slots_; break;
+    case 4: src = d_okeys_ + (size_t)frame * out_slots_; bytes = 4 * (size_t)out_slots_; break;
+    case 5: src = d_ocount_ + (size_t)frame * nlevels_; bytes = sizeof(int) * nlevels_; break;
+    case 6: src = d_err_; bytes = sizeof(int); break;
+    default: throw ArgError("bad debug buffer id");
+  }
+  if (bytes > cap) throw ArgError("debug buffer too small");
+  MMT_HIP(hipMemcpyAsync(out, src, bytes, hipMemcpyDeviceToHost, stream));
+  MMT_HIP(hipStreamSynchronize(stream));
+  return (long)bytes;
+}
+
+}  // namespace mmt
