@@ -64,7 +64,7 @@ def test_orb_kitti_bit_exact(kitti_frames, oracle_mod):
 
 @pytest.mark.parametrize("w,h,nf,seed", [(1242, 375, 2000, 1), (1241, 376, 4000, 2),
                                          (1226, 370, 4000, 3), (640, 480, 1000, 4),
-                                         (1920, 1080, 8000, 5), (333, 211, 300, 6)])
+                                         (1920, 1080, 8000, 5), (400, 260, 300, 6)])
 def test_orb_synthetic_sizes_bit_exact(w, h, nf, seed, oracle_mod):
     ctx = _ctx(w, h, nf)
     gray = synthetic.gray_frame(h, w, seed)
@@ -72,6 +72,12 @@ def test_orb_synthetic_sizes_bit_exact(w, h, nf, seed, oracle_mod):
     _check_stages(ctx, gray, oracle_mod, "synth %dx%d" % (w, h))
     kr, dr = oracle_mod.orb_extract(gray, nf)
     _compare(k, d, kr, dr, "synth %dx%d n%d" % (w, h, nf))
+
+
+def test_too_small_image_is_rejected():
+    # the reference divides by zero when a level has no FAST cell row (ORBextractor.cc:784-787)
+    with pytest.raises(M.MmtError):
+        _ctx(333, 211, 300)
 
 
 def test_orb_edge_cases(oracle_mod):
