@@ -64,13 +64,29 @@ typedef struct mmt_kp {
 
 /* One recovered object motion (Tracking.cc:2127-2129: vObjMod = Tcw^-1 * X). */
 typedef struct mmt_motion {
-  int32_t label;        /* nModLabel (track id)                     */
-  int32_t sem_label;    /* semantic label (nSemPosition)            */
-  int32_t n_points;     /* flow vertices in the solve              */
-  int32_t n_inliers;    /* inliers after the solve                 */
-  float world_motion[16]; /* row-major 4x4 world-frame motion      */
-  float cam_pose[16];     /* row-major 4x4 camera-frame object pose X */
+  int32_t label;            /* nModLabel (track id)                                   */
+  int32_t sem_label;        /* semantic label (nSemPosition)                          */
+  int32_t n_points;         /* object samples (ObjIdNew[i].size())                    */
+  int32_t n_inliers;        /* solve edges with chi2 <= 0.01 after PoseOptimizationFlow2 */
+  int32_t n_ransac_inliers; /* solvePnPRansac inliers                                 */
+  int32_t n_mm_inliers;     /* motion-model inliers (-1: no previous motion)          */
+  int32_t n_solve;          /* flow vertices in the solve (ObjIdTest_in.size())        */
+  int32_t iterations;       /* LM iterations                                          */
+  float world_motion[16];   /* row-major 4x4 vObjMod = Tcw^-1 * X                      */
+  float cam_pose[16];       /* row-major 4x4 X (PoseOptimizationFlow2 output)          */
+  float init_pose[16];      /* row-major 4x4 mInitModel (PnP or motion model)          */
 } mmt_motion;
+
+/* Per-frame tracking result (the Tcw cv::Mat returned by System::TrackRGBD + counters). */
+typedef struct mmt_frame_result {
+  float Tcw[16];            /* row-major camera pose (world -> camera)                 */
+  int32_t initialized;      /* tracking state OK (StereoInitialization done)           */
+  int32_t n_keypoints;      /* ORB keypoints of the frame                              */
+  int32_t n_obj_samples;    /* object samples carried from the last frame              */
+  int32_t ego_iterations;   /* LM iterations of PoseOptimizationFlow2Cam               */
+  int32_t ego_inliers;      /* its inliers (chi2 <= 0.04)                              */
+  int32_t n_objects;        /* dynamic objects solved this frame                       */
+} mmt_frame_result;
 
 typedef struct mmt_ctx mmt_ctx;
 
@@ -106,6 +122,52 @@ int mmt_orb_extract_device(mmt_ctx* ctx, const uint8_t* d_gray, int nframes, siz
  * counts (int), 3 FAST candidate keys (packed u32), 4 octree output keys (packed u32),
  * 5 octree per-level counts (int), 6 device error flags (int).  Returns bytes written or <0. */
 long mmt_debug_fetch(mmt_ctx* ctx, int what, int frame, void* out, size_t cap);
+
+/* System::TrackRGBD on one frame (host buffers): bgr 8UC3 (w*h*3), disparity*256 u16 (w*h),
+ * flow t->t+1 (w*h*2 float), semantic labels (w*h int32, LoadMask-filtered).  Fills `res` and up
+ * to objs_cap object motions.  The first call with > 500 keypoints initialises (Tcw = I). */
+int mmt_track_rgbd(mmt_ctx* ctx, const uint8_t* bgr, const uint16_t* disp256,
+                   const float* flow_uv, const int32_t* mask, double timestamp,
+                   mmt_frame_result* res, mmt_motion* objs, int objs_cap);
+
+/* Device-resident chunk of consecutive frames of the context's sequence (pitches in bytes):
+ * ORB extraction is batched over the chunk, tracking then runs frame by frame.  res[nframes],
+ * objs[nframes * objs_cap] are host arrays. */
+int mmt_track_rgbd_chunk_device(mmt_ctx* ctx, int nframes, const uint8_t* d_bgr,
+                                size_t bgr_pitch, const uint16_t* d_disp, size_t disp_pitch,
+                                const float* d_flow, size_t flow_pitch, const int32_t* d_mask,
+                                size_t mask_pitch, mmt_frame_result* res, mmt_motion* objs,
+                                int objs_cap, void* stream);
+
+/* One flow-refined pose solve (probe of PoseOptimizationFlow2Cam / PoseOptimizationFlow2).
+ * obs/flow: n x 2 floats (last-frame sample pixel, its flow); depth: n floats. */
+typedef struct mmt_flow_problem {
+  int n;
+  const float* obs;
+  const float* flow;
+  const float* depth;
+  float Tcw_last[16];  /* row-major last camera pose; edges use its inverse (Twl)   */
+  float init[16];      /* row-major initial estimate                                */
+  float rp_thres;      /* 0.04 ego / 0.01 object (Huber delta^2)                    */
+  double prior_info;   /* 0.3 ego / 0.5 object                                      */
+  int max_iters;       /* 100 ego / 200 object                                      */
+  int use_noise;       /* ego: depth += g0 * z^2/362.5*0.15 (ObtainFlowDepthCamera) */
+  float g0;            /* the cv::RNG gaussian draw of the noise seed               */
+  float fx, fy, cx, cy;
+} mmt_flow_problem;
+int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* problem, float* pose_out,
+                        int* stats_out /* iterations, inliers, status */);
+
+/* cv::solvePnPRansac(..., SOLVEPNP_AP3P) probe as called by GetInitModelObj: pts3 n x 3,
+ * pts2 n x 2 floats.  R_out row-major 3x3 (after the Rodrigues round trip), t_out 3;
+ * inliers_out (optional, n ints) receives the RANSAC inlier indices. */
+int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, float fx,
+                   float fy, float cx, float cy, int max_iters, double reproj, double confidence,
+                   double* R_out, double* t_out, int* inliers_out, int* n_inliers,
+                   int* iters_out /* iterations run, best hypothesis */);
+
+/* Forget the sequence (Tracking::Reset). */
+int mmt_reset(mmt_ctx* ctx);
 
 /* Upper bound on keypoints per frame (sum over levels of quota + 3). */
 int mmt_orb_capacity(const mmt_ctx* ctx);

@@ -33,6 +33,51 @@ class MmtConfig(ctypes.Structure):
                 ("device_id", ctypes.c_int), ("max_batch", ctypes.c_int)]
 
 
+class MmtMotion(ctypes.Structure):
+    _fields_ = [("label", ctypes.c_int32), ("sem_label", ctypes.c_int32),
+                ("n_points", ctypes.c_int32), ("n_inliers", ctypes.c_int32),
+                ("n_ransac_inliers", ctypes.c_int32), ("n_mm_inliers", ctypes.c_int32),
+                ("n_solve", ctypes.c_int32), ("iterations", ctypes.c_int32),
+                ("world_motion", ctypes.c_float * 16), ("cam_pose", ctypes.c_float * 16),
+                ("init_pose", ctypes.c_float * 16)]
+
+
+class MmtFrameResult(ctypes.Structure):
+    _fields_ = [("Tcw", ctypes.c_float * 16), ("initialized", ctypes.c_int32),
+                ("n_keypoints", ctypes.c_int32), ("n_obj_samples", ctypes.c_int32),
+                ("ego_iterations", ctypes.c_int32), ("ego_inliers", ctypes.c_int32),
+                ("n_objects", ctypes.c_int32)]
+
+
+class MmtFlowProblem(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("obs", ctypes.c_void_p), ("flow", ctypes.c_void_p),
+                ("depth", ctypes.c_void_p), ("Tcw_last", ctypes.c_float * 16),
+                ("init", ctypes.c_float * 16), ("rp_thres", ctypes.c_float),
+                ("prior_info", ctypes.c_double), ("max_iters", ctypes.c_int),
+                ("use_noise", ctypes.c_int), ("g0", ctypes.c_float), ("fx", ctypes.c_float),
+                ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float)]
+
+
+MAX_OBJECTS = 8  # objects reported per frame (kMaxObj in csrc/mmt_tracker.h)
+
+
+def _mat(a):
+    return np.array(a[:], np.float32).reshape(4, 4)
+
+
+def _frame_dict(r, objs):
+    """Same keys as oracle.Tracker.track so tests compare like for like."""
+    out = []
+    for o in objs[:r.n_objects]:
+        out.append(dict(label=o.label, sem_label=o.sem_label, n_points=o.n_points,
+                        ransac_inliers=o.n_ransac_inliers, mm_inliers=o.n_mm_inliers,
+                        n_solve=o.n_solve, n_inliers=o.n_inliers, iterations=o.iterations,
+                        init=_mat(o.init_pose), X=_mat(o.cam_pose), motion=_mat(o.world_motion)))
+    return dict(initialized=bool(r.initialized), Tcw=_mat(r.Tcw), n_keys=r.n_keypoints,
+                n_obj_samples=r.n_obj_samples, ego_iterations=r.ego_iterations,
+                ego_inliers=r.ego_inliers, objects=out)
+
+
 class MmtError(RuntimeError):
     pass
 
@@ -59,6 +104,13 @@ def lib():
         L.mmt_orb_extract_device.argtypes = [vp, vp, i32, sz, vp, vp, i32, vp, vp]
         L.mmt_debug_fetch.restype = ctypes.c_long
         L.mmt_debug_fetch.argtypes = [vp, i32, i32, vp, sz]
+        L.mmt_reset.argtypes = [vp]
+        L.mmt_track_rgbd.argtypes = [vp, vp, vp, vp, vp, ctypes.c_double, vp, vp, i32]
+        L.mmt_track_rgbd_chunk_device.argtypes = [vp, i32, vp, sz, vp, sz, vp, sz, vp, sz, vp, vp,
+                                                  i32, vp]
+        L.mmt_pose_flow_solve.argtypes = [vp, ctypes.POINTER(MmtFlowProblem), vp, vp]
+        L.mmt_pnp_ransac.argtypes = [vp, vp, vp, i32] + [ctypes.c_float] * 4 + \
+            [i32, ctypes.c_double, ctypes.c_double] + [vp] * 5
         _LIB = L
     return _LIB
 
@@ -143,6 +195,75 @@ class Context:
         self._check(lib().mmt_orb_extract_batch(self._h, ptrs, nf, w, _p(kps), _p(desc), cap,
                                                 _p(ns)))
         return [(kps[i, :ns[i]].copy(), desc[i, :ns[i]].copy()) for i in range(nf)]
+
+    # -- tracking (System::TrackRGBD) ---------------------------------------------------------
+    def reset(self):
+        self._check(lib().mmt_reset(self._h))
+
+    def track(self, bgr, disp, flow, mask, timestamp=0.0):
+        """One RGB-D frame: BGR u8 HxWx3, disparity*256 u16 HxW, flow f32 HxWx2, labels i32 HxW."""
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        disp = np.ascontiguousarray(disp, np.uint16)
+        flow = np.ascontiguousarray(flow, np.float32)
+        mask = np.ascontiguousarray(mask, np.int32)
+        h, w = disp.shape
+        assert (w, h) == (self.cfg.width, self.cfg.height), "frame size differs from the context"
+        assert bgr.shape == (h, w, 3) and flow.shape == (h, w, 2) and mask.shape == (h, w)
+        r = MmtFrameResult()
+        objs = (MmtMotion * MAX_OBJECTS)()
+        self._check(lib().mmt_track_rgbd(self._h, _p(bgr), _p(disp), _p(flow), _p(mask),
+                                         float(timestamp), ctypes.byref(r), objs, MAX_OBJECTS))
+        return _frame_dict(r, objs)
+
+    def track_chunk_device(self, bgr, disp, flow, mask, stream=0):
+        """Device-resident chunk (torch tensors on this context's device, frame-major):
+        bgr [F,H,W,3] u8, disp [F,H,W] i16/u16 bits, flow [F,H,W,2] f32, mask [F,H,W] i32."""
+        nf = int(bgr.shape[0])
+        res = (MmtFrameResult * nf)()
+        objs = (MmtMotion * (nf * MAX_OBJECTS))()
+
+        def pitch(t):
+            return t.stride(0) * t.element_size()
+        self._check(lib().mmt_track_rgbd_chunk_device(
+            self._h, nf, bgr.data_ptr(), pitch(bgr), disp.data_ptr(), pitch(disp),
+            flow.data_ptr(), pitch(flow), mask.data_ptr(), pitch(mask), res, objs, MAX_OBJECTS,
+            ctypes.c_void_p(stream)))
+        return [_frame_dict(res[i], objs[i * MAX_OBJECTS:(i + 1) * MAX_OBJECTS])
+                for i in range(nf)]
+
+    # -- probes of single solves ------------------------------------------------------------
+    def flow_solve(self, obs, flow, depth, tcw_last, init, rp_thres, prior_info, max_iters,
+                   K, use_noise=False, g0=0.0):
+        obs = np.ascontiguousarray(obs, np.float32)
+        flow = np.ascontiguousarray(flow, np.float32)
+        depth = np.ascontiguousarray(depth, np.float32)
+        pr = MmtFlowProblem()
+        pr.n = len(depth)
+        pr.obs, pr.flow, pr.depth = obs.ctypes.data, flow.ctypes.data, depth.ctypes.data
+        pr.Tcw_last[:] = np.asarray(tcw_last, np.float32).reshape(16).tolist()
+        pr.init[:] = np.asarray(init, np.float32).reshape(16).tolist()
+        pr.rp_thres, pr.prior_info, pr.max_iters = rp_thres, prior_info, max_iters
+        pr.use_noise, pr.g0 = int(use_noise), g0
+        pr.fx, pr.fy, pr.cx, pr.cy = K
+        pose = np.zeros(16, np.float32)
+        st = np.zeros(3, np.int32)
+        self._check(lib().mmt_pose_flow_solve(self._h, ctypes.byref(pr), _p(pose), _p(st)))
+        return int(st[2]), pose.reshape(4, 4), dict(iterations=int(st[0]), inliers=int(st[1]))
+
+    def pnp_ransac(self, pts3, pts2, K, max_iters=500, reproj=0.3, conf=0.98):
+        pts3 = np.ascontiguousarray(pts3, np.float32)
+        pts2 = np.ascontiguousarray(pts2, np.float32)
+        n = len(pts3)
+        R = np.zeros(9)
+        t = np.zeros(3)
+        inl = np.zeros(max(n, 1), np.int32)
+        ninl = ctypes.c_int(0)
+        its = np.zeros(2, np.int32)
+        self._check(lib().mmt_pnp_ransac(self._h, _p(pts3), _p(pts2), n, K[0], K[1], K[2], K[3],
+                                         max_iters, reproj, conf, _p(R), _p(t), _p(inl),
+                                         ctypes.byref(ninl), _p(its)))
+        return R.reshape(3, 3), t, inl[:ninl.value].copy(), dict(iterations=int(its[0]),
+                                                                 best_iter=int(its[1]))
 
     def debug_fetch(self, what, frame=0, nbytes=1 << 26):
         buf = np.zeros(nbytes, np.uint8)

@@ -3,10 +3,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
+#include <vector>
 #include <new>
 
-#include "mmt_internal.h"
+#include "mmt_ctx.h"
+#include "mmt_pnp.h"
+#include "mmt_track.h"
 
 using mmt::ArgError;
 using mmt::DeviceError;
@@ -27,6 +31,14 @@ static int guard(mmt_ctx* ctx, F&& body) {
   }
   return MMT_OK;
 }
+
+// Scoped device allocation for the probe entry points.
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  explicit DevBuf(size_t n) { MMT_HIP(hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T))); }
+  ~DevBuf() { (void)hipFree(p); }
+};
 
 static thread_local std::string g_create_error;
 
@@ -79,6 +91,10 @@ void mmt_destroy(mmt_ctx* ctx) {
   (void)hipFree(ctx->d_kps);
   (void)hipFree(ctx->d_desc);
   (void)hipFree(ctx->d_n);
+  (void)hipFree(ctx->t_bgr);
+  (void)hipFree(ctx->t_disp);
+  (void)hipFree(ctx->t_flow);
+  (void)hipFree(ctx->t_mask);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -193,6 +209,201 @@ int mmt_orb_extract_device(mmt_ctx* ctx, const uint8_t* d_gray, int nframes, siz
   return guard(ctx, [&] {
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     ctx->engine.run(d_gray, nframes, frame_pitch, d_kps, d_desc, cap_per_frame, d_n, s);
+  });
+}
+
+static void ensure_tracker(mmt_ctx* ctx) {
+  if (ctx->tracker_ready) return;
+  const int B = ctx->cfg.max_batch > 0 ? ctx->cfg.max_batch : 1;
+  ctx->tracker.setup(ctx->cfg, &ctx->engine, B);
+  ctx->tracker_ready = true;
+}
+
+static void fill_results(const std::vector<mmt::FrameOut>& outs, mmt_frame_result* res,
+                         mmt_motion* objs, int objs_cap) {
+  for (size_t f = 0; f < outs.size(); f++) {
+    const mmt::FrameOut& o = outs[f];
+    mmt_frame_result& r = res[f];
+    memcpy(r.Tcw, o.Tcw, sizeof(r.Tcw));
+    r.initialized = o.initialized;
+    r.n_keypoints = o.n_keys;
+    r.n_obj_samples = o.n_obj_samples;
+    r.ego_iterations = o.ego_iterations;
+    r.ego_inliers = o.ego_inliers;
+    r.n_objects = (int)o.objects.size();
+    if (!objs) continue;
+    for (int i = 0; i < (int)o.objects.size() && i < objs_cap; i++) {
+      const mmt::ObjOut& s = o.objects[i];
+      mmt_motion& m = objs[f * objs_cap + i];
+      m.label = s.label;
+      m.sem_label = s.sem_label;
+      m.n_points = s.n_points;
+      m.n_inliers = s.n_inliers;
+      m.n_ransac_inliers = s.n_ransac_inliers;
+      m.n_mm_inliers = s.n_mm_inliers;
+      m.n_solve = s.n_solve;
+      m.iterations = s.iterations;
+      memcpy(m.world_motion, s.motion, 64);
+      memcpy(m.cam_pose, s.X, 64);
+      memcpy(m.init_pose, s.init, 64);
+    }
+  }
+}
+
+int mmt_reset(mmt_ctx* ctx) {
+  if (!ctx) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    ensure_tracker(ctx);
+    ctx->tracker.reset();
+  });
+}
+
+int mmt_track_rgbd_chunk_device(mmt_ctx* ctx, int nframes, const uint8_t* d_bgr,
+                                size_t bgr_pitch, const uint16_t* d_disp, size_t disp_pitch,
+                                const float* d_flow, size_t flow_pitch, const int32_t* d_mask,
+                                size_t mask_pitch, mmt_frame_result* res, mmt_motion* objs,
+                                int objs_cap, void* stream) {
+  if (!ctx || !d_bgr || !d_disp || !d_flow || !d_mask || !res || nframes < 1) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ensure_tracker(ctx);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    std::vector<mmt::FrameOut> outs;
+    ctx->tracker.track_chunk(d_bgr, bgr_pitch, d_disp, disp_pitch, d_flow, flow_pitch, d_mask,
+                             mask_pitch, nframes, outs, s);
+    fill_results(outs, res, objs, objs_cap);
+  });
+}
+
+int mmt_track_rgbd(mmt_ctx* ctx, const uint8_t* bgr, const uint16_t* disp256,
+                   const float* flow_uv, const int32_t* mask, double timestamp,
+                   mmt_frame_result* res, mmt_motion* objs, int objs_cap) {
+  (void)timestamp;
+  if (!ctx || !bgr || !disp256 || !flow_uv || !mask || !res) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ensure_tracker(ctx);
+    const size_t npix = (size_t)ctx->cfg.width * ctx->cfg.height;
+    if (!ctx->t_bgr) {
+      MMT_HIP(hipMalloc((void**)&ctx->t_bgr, npix * 3));
+      MMT_HIP(hipMalloc((void**)&ctx->t_disp, npix * 2));
+      MMT_HIP(hipMalloc((void**)&ctx->t_flow, npix * 8));
+      MMT_HIP(hipMalloc((void**)&ctx->t_mask, npix * 4));
+    }
+    hipStream_t s = ctx->stream;
+    MMT_HIP(hipMemcpyAsync(ctx->t_bgr, bgr, npix * 3, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(ctx->t_disp, disp256, npix * 2, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(ctx->t_flow, flow_uv, npix * 8, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(ctx->t_mask, mask, npix * 4, hipMemcpyHostToDevice, s));
+    std::vector<mmt::FrameOut> outs;
+    ctx->tracker.track_chunk(ctx->t_bgr, npix * 3, ctx->t_disp, npix * 2, ctx->t_flow, npix * 8,
+                             ctx->t_mask, npix * 4, 1, outs, s);
+    fill_results(outs, res, objs, objs_cap);
+  });
+}
+
+int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* pr, float* pose_out,
+                        int* stats_out) {
+  if (!ctx || !pr || !pose_out || !stats_out || pr->n < 0) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    hipStream_t s = ctx->stream;
+    const int n = pr->n, cap = std::max(n, 1);
+    DevBuf<float2> obs(cap), flow(cap);
+    DevBuf<float> depth(cap), pose(16);
+    DevBuf<double> scratch(mmt::flow_scratch_doubles(cap));
+    DevBuf<int> st(3);
+    DevBuf<mmt::FlowSolveDesc> dd(1);
+    if (n > 0) {
+      MMT_HIP(hipMemcpyAsync(obs.p, pr->obs, 8 * (size_t)n, hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(flow.p, pr->flow, 8 * (size_t)n, hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(depth.p, pr->depth, 4 * (size_t)n, hipMemcpyHostToDevice, s));
+    }
+    mmt::FlowSolveDesc d;
+    memset(&d, 0, sizeof(d));
+    d.n = n;
+    d.obs = obs.p;
+    d.flow = flow.p;
+    d.depth = depth.p;
+    memcpy(d.Tcw_last, pr->Tcw_last, 64);
+    memcpy(d.init, pr->init, 64);
+    d.rp_thres = pr->rp_thres;
+    d.use_noise = pr->use_noise;
+    d.g0 = pr->g0;
+    d.max_iters = pr->max_iters;
+    d.prior_info = pr->prior_info;
+    d.fx = pr->fx; d.fy = pr->fy; d.cx = pr->cx; d.cy = pr->cy;
+    d.scratch = scratch.p;
+    d.cap = cap;
+    d.pose_out = pose.p;
+    d.stats = st.p;
+    MMT_HIP(hipMemcpyAsync(dd.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(pose.p, pr->init, 64, hipMemcpyHostToDevice, s));
+    mmt::launch_flow_lm(dd.p, 1, s);
+    MMT_HIP(hipMemcpyAsync(pose_out, pose.p, 64, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(stats_out, st.p, 12, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, float fx,
+                   float fy, float cx, float cy, int max_iters, double reproj, double confidence,
+                   double* R_out, double* t_out, int* inliers_out, int* n_inliers,
+                   int* iters_out) {
+  if (!ctx || !pts3 || !pts2 || !R_out || !t_out || !n_inliers || !iters_out || n < 5 ||
+      max_iters < 1)
+    return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    hipStream_t s = ctx->stream;
+    const int words = (n + 63) / 64;
+    DevBuf<float> p3(3 * (size_t)n);
+    DevBuf<float2> p2(n);
+    DevBuf<int> dn(1), sub(5 * (size_t)max_iters), good(max_iters), inl(n), mm(n), subset(n),
+        nsub(1), res(8);
+    DevBuf<double> models(6 * (size_t)max_iters), Rt(12);
+    DevBuf<unsigned long long> masks((size_t)max_iters * words);
+    DevBuf<mmt::PnPObject> po(1);
+    std::vector<int> h_sub;
+    mmt::ransac_subsets(n, max_iters, h_sub);
+    MMT_HIP(hipMemcpyAsync(p3.p, pts3, 12 * (size_t)n, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(p2.p, pts2, 8 * (size_t)n, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(dn.p, &n, 4, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(sub.p, h_sub.data(), 4 * h_sub.size(), hipMemcpyHostToDevice, s));
+    mmt::PnPObject o;
+    memset(&o, 0, sizeof(o));
+    o.n = dn.p;
+    o.fx = fx; o.fy = fy; o.cx = cx; o.cy = cy;
+    o.reproj = reproj;
+    o.confidence = confidence;
+    o.subsets = sub.p;
+    o.pts3 = p3.p;
+    o.pts2 = p2.p;
+    o.models = models.p;
+    o.good = good.p;
+    o.masks = masks.p;
+    o.mask_words = words;
+    o.inliers = inl.p;
+    o.mm_inliers = mm.p;
+    o.subset = subset.p;
+    o.n_subset = nsub.p;
+    o.result = res.p;
+    o.Rt = Rt.p;
+    MMT_HIP(hipMemcpyAsync(po.p, &o, sizeof(o), hipMemcpyHostToDevice, s));
+    mmt::launch_pnp(po.p, 1, max_iters, s, false);
+    int r[8];
+    double rt[12];
+    MMT_HIP(hipMemcpyAsync(r, res.p, sizeof(r), hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(rt, Rt.p, sizeof(rt), hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+    const int ni = r[0] >= 0 ? r[3] : 0;
+    if (inliers_out && ni > 0)
+      MMT_HIP(hipMemcpy(inliers_out, inl.p, 4 * (size_t)ni, hipMemcpyDeviceToHost));
+    memcpy(R_out, rt, 72);
+    memcpy(t_out, rt + 9, 24);
+    *n_inliers = ni;
+    iters_out[0] = r[2];
+    iters_out[1] = r[0];
   });
 }
 

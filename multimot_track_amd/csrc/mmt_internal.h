@@ -115,17 +115,3 @@ class OrbEngine {
 
 }  // namespace mmt
 
-struct mmt_ctx {
-  mmt_config cfg;
-  mmt::OrbTables orb;
-  mmt::OrbEngine engine;
-  hipStream_t stream = nullptr;
-  std::string err;
-  // staging for the host-pointer entry points
-  uint8_t* d_in = nullptr;
-  size_t d_in_bytes = 0;
-  mmt_kp* d_kps = nullptr;
-  uint8_t* d_desc = nullptr;
-  int* d_n = nullptr;
-  int staged_frames = 0;
-};

@@ -1,0 +1,41 @@
+// multimot_track_amd/csrc/mmt_pnp.h -- device record of one object's D5 RANSAC problem.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mmt {
+
+struct PnPObject {
+  // inputs
+  const int* n;             // member count (device)
+  const int* members;       // ascending sample indices (ObjIdNew[i])
+  const float2* last_keys;  // last frame's own object samples (mvObjKeys of mLastFrame)
+  const float* last_depth;
+  const float2* cur_keys;   // current mvObjKeys (= last mvObjCorres)
+  float Tlast[16];
+  float fx, fy, cx, cy;
+  double reproj, confidence;
+  const int* subsets;       // [max_iters][5] RNG((uint64)-1) draws for this count
+  int use_mm;               // motion model available (PreObjID != -1)
+  float MM[16];             // Tcw * last vObjMod[PreObjID]
+  int use_mm_choice;        // set by the host after the counts are known
+  // scratch / outputs
+  float* pts3;              // [cap][3] pre_3d
+  float2* pts2;             // [cap] cur_2d
+  double* models;           // [max_iters][6] rvec, tvec
+  int* good;                // [max_iters]
+  unsigned long long* masks;  // [max_iters][mask_words]
+  int mask_words;
+  int* inliers;             // RANSAC inliers (indices into the member list)
+  int* mm_inliers;
+  int* subset;              // D3 edge -> sample index
+  int* n_subset;
+  int* result;              // best, maxGood, iterations, n_ransac_inliers, n_mm_inliers
+  double* Rt;               // R (9), t (3)
+};
+
+void launch_pnp(PnPObject* d_objs, int nobj, int max_iters, hipStream_t st, bool gather = true);
+void launch_pnp_subset(PnPObject* d_objs, int nobj, hipStream_t st);
+
+}  // namespace mmt

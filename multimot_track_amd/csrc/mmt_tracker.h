@@ -1,0 +1,117 @@
+// multimot_track_amd/csrc/mmt_tracker.h -- host tracker state (one sequence per context).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "mmt_internal.h"
+#include "mmt_pnp.h"
+#include "mmt_track.h"
+
+namespace mmt {
+
+constexpr int kMaxObj = 8;         // objects solved per frame
+constexpr int kRansacIters = 500;  // solvePnPRansac iterationsCount (Tracking.cc:4361)
+
+struct ObjOut {
+  int label = 0, sem_label = 0, n_points = 0, n_ransac_inliers = 0, n_mm_inliers = -1;
+  int ransac_iterations = 0, n_solve = 0, n_inliers = 0, iterations = 0;
+  float init[16], X[16], motion[16];
+};
+
+struct FrameOut {
+  bool initialized = false;
+  float Tcw[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  int n_keys = 0, n_obj_samples = 0, ego_iterations = 0, ego_inliers = 0;
+  std::vector<ObjOut> objects;
+};
+
+float rng_first_gaussian(uint64_t seed);
+// RANSACPointSetRegistrator::getSubset draws (5-point subsets) for a point count.
+void ransac_subsets(int count, int iters, std::vector<int>& idx);
+
+class Tracker {
+ public:
+  ~Tracker();
+  void setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk);
+  void reset();
+  // Frames of one sequence, device-resident, processed in order (ORB batched over the chunk).
+  void track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t* d_disp,
+                   size_t disp_pitch, const float* d_flow, size_t flow_pitch,
+                   const int32_t* d_mask, size_t mask_pitch, int nframes,
+                   std::vector<FrameOut>& outs, hipStream_t st);
+  int max_chunk() const { return max_chunk_; }
+  // last chunk's ORB output (device) for probes
+  const mmt_kp* kps() const { return d_kps_; }
+  const int* nkp() const { return d_nkp_; }
+  int kcap() const { return kcap_; }
+
+ private:
+  struct FrameSlot {
+    SampleSet st;
+    ObjSampleSet ob;
+    HandoffSet ho;
+    float Tcw[16];
+    std::vector<int> nModLabel, nSemPosition;
+    std::vector<std::vector<float>> vObjMod;
+  };
+  struct FrameArgs {
+    const float* depth;
+    const float2* flow;
+    const int32_t* mask;
+    const mmt_kp* kps;
+    const int* nkp;
+    int n_keys;
+  };
+  struct PnPBuf {
+    float* pts3;
+    float2* pts2;
+    int* subsets;
+    double* models;
+    int* good;
+    unsigned long long* masks;
+    int* inliers;
+    int* mm_inliers;
+    int* subset;
+    int* n_subset;
+    int* result;
+    double* Rt;
+  };
+  template <typename T>
+  T* alloc(size_t n);
+  void track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st);
+  void track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, FrameOut& out,
+                     hipStream_t st);
+  void finish_frame(FrameSlot& C, FrameOut& out, hipStream_t st);
+
+  mmt_config cfg_{};
+  OrbEngine* engine_ = nullptr;
+  int W_ = 0, H_ = 0, max_chunk_ = 0, kcap_ = 0, ocap_ = 0, lm_cap_ = 0, mask_words_ = 0;
+  float g0_ = 0;
+  int state_ = 0, cur_ = 0;
+  bool bFirstFrame_ = false, bSecondFrame_ = false, hasVelocity_ = false;
+  float V_[16] = {0};
+  FrameSlot slot_[2];
+  FrameSlot& last_ = slot_[1];
+  std::vector<void*> allocs_;
+  uint8_t* d_gray_ = nullptr;
+  float* d_depth_ = nullptr;
+  mmt_kp* d_kps_ = nullptr;
+  uint8_t* d_desc_ = nullptr;
+  int* d_nkp_ = nullptr;
+  int32_t* d_obj_label_ = nullptr;
+  int* d_members_ = nullptr;
+  LabelStats* d_stats_ = nullptr;
+  int* d_hist_ = nullptr;
+  int* d_err_ = nullptr;
+  double* d_lm_scratch_ = nullptr;
+  FlowSolveDesc* d_descs_ = nullptr;
+  float* d_poses_ = nullptr;
+  int* d_lmstats_ = nullptr;
+  PnPObject* d_pnp_ = nullptr;
+  PnPBuf pnp_[kMaxObj];
+  std::vector<int> h_subsets_;
+};
+
+}  // namespace mmt

@@ -1,0 +1,570 @@
+// multimot_track_amd/csrc/mmt_tracker.hip -- host side of System::TrackRGBD for one sequence.
+//
+// Mirrors Tracking::GrabImageRGBD / Tracking::Track (reference src/Tracking.cc:438-661, 951-2499)
+// and Tracking::StereoInitialization (:2512-2570): every per-pixel / per-sample / per-edge stage
+// runs as HIP kernels (mmt_orb.hip, mmt_track.hip, mmt_pnp.hip); the host keeps the scalar
+// state machine -- poses, motion model, label bookkeeping (B8), per-object decisions -- exactly
+// where the reference keeps it.  Deviation: the ego *initial* pose comes from the
+// constant-velocity motion model instead of ORB-SLAM2's map tracking (MapPoints/KeyFrames/
+// vocabulary are not on this path yet).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "mmt_internal.h"
+#include "mmt_pnp.h"
+#include "mmt_track.h"
+#include "mmt_tracker.h"
+
+namespace mmt {
+
+// ------------------------------------------------------------------ float cv::Mat helpers
+static void mat4_mul(const float* A, const float* B, float* C) {  // cv::gemm, CV_32F
+  float R[16];
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) {
+      double s = 0;
+      for (int k = 0; k < 4; k++) s += (double)A[4 * r + k] * (double)B[4 * k + c];
+      R[4 * r + c] = (float)s;
+    }
+  memcpy(C, R, sizeof(R));
+}
+static void inv_mat(const float* T, float* Ti) {  // Tracking::InvMatrix
+  float R[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) R[4 * r + c] = T[4 * c + r];
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)T[4 * k + 3];
+    R[4 * r + 3] = (float)(-s);
+  }
+  memcpy(Ti, R, sizeof(R));
+}
+static void mat4_eye(float* T) {
+  for (int i = 0; i < 16; i++) T[i] = (i % 5 == 0) ? 1.f : 0.f;
+}
+
+// cv::RNG(seed).gaussian(1.0) first draw (randn_0_1_32f ziggurat; Frame.cc:1246-1251)
+static inline uint64_t rng_next(uint64_t x) { return (uint64_t)(unsigned)x * 4164903690ULL + (x >> 32); }
+float rng_first_gaussian(uint64_t seed) {
+  static unsigned kn[128];
+  static float wn[128], fn[128];
+  static bool init = false;
+  if (!init) {
+    const double m1 = 2147483648.0;
+    double dn = 3.442619855899, tn = dn, vn = 9.91256303526217e-3;
+    const double q = vn / std::exp(-.5 * dn * dn);
+    kn[0] = (unsigned)((dn / q) * m1);
+    kn[1] = 0;
+    wn[0] = (float)(q / m1);
+    wn[127] = (float)(dn / m1);
+    fn[0] = 1.f;
+    fn[127] = (float)std::exp(-.5 * dn * dn);
+    for (int i = 126; i >= 1; i--) {
+      dn = std::sqrt(-2. * std::log(vn / dn + std::exp(-.5 * dn * dn)));
+      kn[i + 1] = (unsigned)((dn / tn) * m1);
+      tn = dn;
+      fn[i] = (float)std::exp(-.5 * dn * dn);
+      wn[i] = (float)(dn / m1);
+    }
+    init = true;
+  }
+  const float r = 3.442620f, rng_flt = 2.3283064365386962890625e-10f;
+  uint64_t temp = seed ? seed : 0xffffffffULL;
+  float x, y;
+  for (;;) {
+    const int hz = (int)temp;
+    temp = rng_next(temp);
+    const int iz = hz & 127;
+    x = hz * wn[iz];
+    if ((unsigned)std::abs(hz) < kn[iz]) break;
+    if (iz == 0) {
+      do {
+        x = (unsigned)temp * rng_flt;
+        temp = rng_next(temp);
+        y = (unsigned)temp * rng_flt;
+        temp = rng_next(temp);
+        x = (float)(-std::log(x + FLT_MIN) * 0.2904764);
+        y = (float)-std::log(y + FLT_MIN);
+      } while (y + y < x * x);
+      x = hz > 0 ? r + x : -r - x;
+      break;
+    }
+    y = (unsigned)temp * rng_flt;
+    temp = rng_next(temp);
+    if (fn[iz] + y * (fn[iz - 1] - fn[iz]) < std::exp(-.5 * x * x)) break;
+  }
+  return x;
+}
+
+// RANSACPointSetRegistrator::getSubset draws with RNG((uint64)-1): depends on the count only.
+void ransac_subsets(int count, int iters, std::vector<int>& idx) {
+  uint64_t state = 0xFFFFFFFFFFFFFFFFULL;
+  idx.assign((size_t)iters * 5, 0);
+  for (int it = 0; it < iters; it++) {
+    int* cur = &idx[(size_t)it * 5];
+    for (int i = 0; i < 5; i++)
+      for (;;) {
+        state = (uint64_t)(unsigned)state * 4164903690ULL + (unsigned)(state >> 32);
+        const int v = (int)((unsigned)state % (unsigned)count);
+        cur[i] = v;
+        int j = 0;
+        for (; j < i; j++)
+          if (v == cur[j]) break;
+        if (j == i) break;
+      }
+  }
+}
+
+template <typename T>
+static T* dalloc(size_t n) {
+  T* p = nullptr;
+  MMT_HIP(hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T)));
+  return p;
+}
+
+Tracker::~Tracker() {
+  for (void* p : allocs_) (void)hipFree(p);
+}
+
+template <typename T>
+T* Tracker::alloc(size_t n) {
+  T* p = dalloc<T>(n);
+  allocs_.push_back(p);
+  return p;
+}
+
+void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
+  cfg_ = cfg;
+  engine_ = engine;
+  W_ = cfg.width;
+  H_ = cfg.height;
+  max_chunk_ = max_chunk;
+  g0_ = rng_first_gaussian(cfg.noise_seed);
+  kcap_ = engine->capacity();
+  ocap_ = ((W_ + 3) / 4) * ((H_ + 3) / 4);
+  const size_t npix = (size_t)W_ * H_;
+  d_gray_ = alloc<uint8_t>(npix * max_chunk);
+  d_depth_ = alloc<float>(npix * max_chunk);
+  d_kps_ = alloc<mmt_kp>((size_t)kcap_ * max_chunk);
+  d_desc_ = alloc<uint8_t>((size_t)kcap_ * 32 * max_chunk);
+  d_nkp_ = alloc<int>(max_chunk);
+  for (int s = 0; s < 2; s++) {
+    FrameSlot& F = slot_[s];
+    F.st.keys = alloc<float2>(kcap_);
+    F.st.corres = alloc<float2>(kcap_);
+    F.st.flow = alloc<float2>(kcap_);
+    F.st.depth = alloc<float>(kcap_);
+    F.st.count = alloc<int>(1);
+    F.st.cap = kcap_;
+    F.ob.keys = alloc<float2>(ocap_);
+    F.ob.corres = alloc<float2>(ocap_);
+    F.ob.flow = alloc<float2>(ocap_);
+    F.ob.depth = alloc<float>(ocap_);
+    F.ob.label = alloc<int32_t>(ocap_);
+    F.ob.count = alloc<int>(1);
+    F.ob.cap = ocap_;
+    F.ho.skeys = alloc<float2>(kcap_);
+    F.ho.sdepth = alloc<float>(kcap_);
+    F.ho.ns = alloc<int>(1);
+    F.ho.okeys = alloc<float2>(ocap_);
+    F.ho.odepth = alloc<float>(ocap_);
+    F.ho.olabel = alloc<int32_t>(ocap_);
+    F.ho.no = alloc<int>(1);
+    MMT_HIP(hipMemset(F.st.count, 0, sizeof(int)));
+    MMT_HIP(hipMemset(F.ob.count, 0, sizeof(int)));
+  }
+  d_obj_label_ = alloc<int32_t>(ocap_);
+  d_members_ = alloc<int>((size_t)kMaxLabel * ocap_);
+  d_stats_ = alloc<LabelStats>(kMaxLabel);
+  d_hist_ = alloc<int>(kMaxLabel * kMaxLabel);
+  d_err_ = alloc<int>(1);
+  MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
+  // solves: 1 ego + up to kMaxObj objects
+  const int lmcap = std::max(kcap_, ocap_);
+  lm_cap_ = lmcap;
+  d_lm_scratch_ = alloc<double>(flow_scratch_doubles(lmcap) * (1 + kMaxObj));
+  d_descs_ = alloc<FlowSolveDesc>(1 + kMaxObj);
+  d_poses_ = alloc<float>(16 * (1 + kMaxObj));
+  d_lmstats_ = alloc<int>(3 * (1 + kMaxObj));
+  // PnP
+  mask_words_ = (ocap_ + 63) / 64;
+  d_pnp_ = alloc<PnPObject>(kMaxObj);
+  for (int o = 0; o < kMaxObj; o++) {
+    PnPBuf& b = pnp_[o];
+    b.pts3 = alloc<float>(3 * (size_t)ocap_);
+    b.pts2 = alloc<float2>(ocap_);
+    b.subsets = alloc<int>(5 * kRansacIters);
+    b.models = alloc<double>(6 * kRansacIters);
+    b.good = alloc<int>(kRansacIters);
+    b.masks = alloc<unsigned long long>((size_t)kRansacIters * mask_words_);
+    b.inliers = alloc<int>(ocap_);
+    b.mm_inliers = alloc<int>(ocap_);
+    b.subset = alloc<int>(ocap_);
+    b.n_subset = alloc<int>(1);
+    b.result = alloc<int>(8);
+    b.Rt = alloc<double>(12);
+  }
+  h_subsets_.resize(5 * kRansacIters);
+  reset();
+}
+
+void Tracker::reset() {
+  state_ = 0;
+  bFirstFrame_ = false;  // uninitialised member in the reference (Tracking.h:180): pinned false
+  bSecondFrame_ = false;
+  hasVelocity_ = false;
+  cur_ = 0;
+  last_.nModLabel.clear();
+  last_.nSemPosition.clear();
+  last_.vObjMod.clear();
+  mat4_eye(last_.Tcw);
+}
+
+void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t* d_disp,
+                          size_t disp_pitch, const float* d_flow, size_t flow_pitch,
+                          const int32_t* d_mask, size_t mask_pitch, int nframes,
+                          std::vector<FrameOut>& outs, hipStream_t st) {
+  if (nframes < 1 || nframes > max_chunk_) throw ArgError("chunk size outside [1, max_batch]");
+  const size_t npix = (size_t)W_ * H_;
+  // ---- per-frame preparation and batched ORB extraction for the whole chunk
+  launch_gray_depth(d_bgr, bgr_pitch, d_disp, disp_pitch / sizeof(uint16_t), d_gray_, npix,
+                    d_depth_, npix, (int)npix, nframes, cfg_.bf, st);
+  engine_->run(d_gray_, nframes, npix, d_kps_, d_desc_, kcap_, d_nkp_, st);
+  std::vector<int> nkp(nframes);
+  MMT_HIP(hipMemcpyAsync(nkp.data(), d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipStreamSynchronize(st));
+  outs.assign(nframes, FrameOut());
+  for (int f = 0; f < nframes; f++) {
+    FrameArgs a;
+    a.depth = d_depth_ + npix * f;
+    a.flow = (const float2*)((const uint8_t*)d_flow + flow_pitch * f);
+    a.mask = (const int32_t*)((const uint8_t*)d_mask + mask_pitch * f);
+    a.kps = d_kps_ + (size_t)kcap_ * f;
+    a.nkp = d_nkp_ + f;
+    a.n_keys = nkp[f];
+    track_frame(a, outs[f], st);
+  }
+}
+
+void Tracker::track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st) {
+  FrameSlot& C = slot_[cur_];
+  FrameSlot& Ls = slot_[cur_ ^ 1];
+  out = FrameOut();
+  out.n_keys = a.n_keys;
+  // ---- Frame(RGBD): B2 static samples, B1 object samples
+  launch_static_samples(a.kps, a.nkp, a.depth, a.flow, a.mask, W_, H_, C.st, st);
+  launch_obj_samples(a.depth, a.flow, a.mask, W_, H_, C.ob, st);
+  // ---- GrabImageRGBD hand-off (B4)
+  const bool handoff = bFirstFrame_ || bSecondFrame_;
+  if (handoff)
+    launch_handoff(Ls.st.corres, Ls.st.count, Ls.ob.corres, Ls.ob.count, a.depth, a.mask, W_, H_,
+                   C.ho, st);
+  if (state_ == 0) {
+    // ---- StereoInitialization (needs more than 500 keypoints)
+    bFirstFrame_ = true;
+    bSecondFrame_ = false;
+    if (a.n_keys > 500) {
+      mat4_eye(C.Tcw);
+      memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
+      C.nModLabel.clear();
+      C.nSemPosition.clear();
+      C.vObjMod.clear();
+      state_ = 1;
+      out.initialized = true;
+      finish_frame(C, out, st);
+    } else {
+      mat4_eye(out.Tcw);
+    }
+    return;
+  }
+  // ---- ego initial pose: motion model (deviation, see header)
+  float Tinit[16];
+  if (hasVelocity_) {
+    mat4_mul(V_, Ls.Tcw, Tinit);
+    bSecondFrame_ = false;
+  } else {
+    memcpy(Tinit, Ls.Tcw, sizeof(Tinit));
+    bSecondFrame_ = true;
+  }
+  // ---- D2 (PoseOptimizationFlow2Cam) + B6/B7 statistics in one round trip
+  FlowSolveDesc d2;
+  memset(&d2, 0, sizeof(d2));
+  d2.d_n = Ls.st.count;
+  d2.idx = nullptr;
+  d2.obs = Ls.st.keys;  // mLastFrame.mvSiftKeys (= its own mvSiftKeysTmp)
+  d2.flow = Ls.st.flow;
+  d2.depth = Ls.st.depth;
+  memcpy(d2.Tcw_last, Ls.Tcw, sizeof(d2.Tcw_last));
+  memcpy(d2.init, Tinit, sizeof(d2.init));
+  d2.rp_thres = 0.04f;
+  d2.use_noise = 1;
+  d2.g0 = g0_;
+  d2.max_iters = 100;
+  d2.prior_info = 0.3;
+  d2.fx = cfg_.fx; d2.fy = cfg_.fy; d2.cx = cfg_.cx; d2.cy = cfg_.cy;
+  d2.scratch = d_lm_scratch_;
+  d2.cap = lm_cap_;
+  d2.pose_out = d_poses_;
+  d2.stats = d_lmstats_;
+  MMT_HIP(hipMemcpyAsync(d_descs_, &d2, sizeof(d2), hipMemcpyHostToDevice, st));
+  MMT_HIP(hipMemcpyAsync(d_poses_, Tinit, sizeof(Tinit), hipMemcpyHostToDevice, st));
+  launch_flow_lm(d_descs_, 1, st);
+  float Tcw[16];
+  int lmst[3];
+  MMT_HIP(hipMemcpyAsync(Tcw, d_poses_, sizeof(Tcw), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(lmst, d_lmstats_, sizeof(lmst), hipMemcpyDeviceToHost, st));
+  int n_last_obj = 0;
+  MMT_HIP(hipMemcpyAsync(&n_last_obj, Ls.ob.count, sizeof(int), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipStreamSynchronize(st));
+  if (lmst[2] != 0) memcpy(Tcw, Tinit, sizeof(Tcw));  // < 3 correspondences: pose unchanged
+  memcpy(C.Tcw, Tcw, sizeof(Tcw));
+  out.ego_iterations = lmst[0];
+  out.ego_inliers = lmst[1];
+  {
+    float LastTwc[16];
+    inv_mat(Ls.Tcw, LastTwc);
+    mat4_mul(C.Tcw, LastTwc, V_);
+    hasVelocity_ = true;
+  }
+  memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
+  out.initialized = true;
+  C.nModLabel.clear();
+  C.nSemPosition.clear();
+  C.vObjMod.clear();
+  if (n_last_obj > 0) track_objects(C, Ls, n_last_obj, out, st);
+  finish_frame(C, out, st);
+}
+
+void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, FrameOut& out,
+                            hipStream_t st) {
+  // ---- B6 + B7 statistics
+  GroupArgs g;
+  memset(&g, 0, sizeof(g));
+  g.n = Ls.ob.count;
+  g.cur_keys = C.ho.okeys;
+  g.cur_depth = C.ho.odepth;
+  g.cur_label = C.ho.olabel;
+  g.last_keys = Ls.ob.keys;
+  g.last_depth = Ls.ob.depth;
+  g.last_label = Ls.ob.label;
+  memcpy(g.Tcur, C.Tcw, sizeof(g.Tcur));
+  memcpy(g.Tlast, Ls.Tcw, sizeof(g.Tlast));
+  g.fx = cfg_.fx; g.fy = cfg_.fy; g.cx = cfg_.cx; g.cy = cfg_.cy;
+  g.W = W_;
+  g.H = H_;
+  g.obj_label = d_obj_label_;
+  g.members = d_members_;
+  g.member_cap = ocap_;
+  g.stats = d_stats_;
+  g.hist = d_hist_;
+  g.err = d_err_;
+  launch_obj_group(g, st);
+  LabelStats stats[kMaxLabel];
+  int hist[kMaxLabel * kMaxLabel];
+  int err = 0;
+  MMT_HIP(hipMemcpyAsync(stats, d_stats_, sizeof(stats), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(hist, d_hist_, sizeof(hist), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(&err, d_err_, sizeof(int), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipStreamSynchronize(st));
+  if (err) throw ArgError("semantic label outside [0, 15] on the object path");
+  out.n_obj_samples = n_obj_samples;
+  // ---- B7 decisions (Tracking.cc:1424-1536); labels ascending = UniLab order
+  std::vector<int> objLabelsNew;  // semantic label of each kept object
+  for (int l = 1; l < kMaxLabel; l++) {
+    const LabelStats& s = stats[l];
+    if (s.cnt == 0) continue;
+    const float count = (float)s.bcnt;
+    if (count / s.cnt > 0.5f) continue;  // mostly on the image boundary
+    if (!(s.cnt > 100)) continue;        // fewer than 100 points
+    const float sf_count = (float)s.sfcnt;
+    if (sf_count / s.cnt > 0.3f) continue;            // static object
+    if (s.depth_sum / s.cnt > 25.0) continue;         // too far
+    objLabelsNew.push_back(l);
+  }
+  // ---- B8 label association (Tracking.cc:1556-1630)
+  int mx;
+  if (bSecondFrame_)
+    mx = 1;
+  else if (!Ls.nModLabel.empty())
+    mx = *std::max_element(Ls.nModLabel.begin(), Ls.nModLabel.end()) + 1;
+  else
+    mx = 1;  // uninitialised in the reference (Tracking.cc:1557): pinned 1
+  const int nobj = std::min((int)objLabelsNew.size(), kMaxObj);
+  std::vector<int> LabId(nobj);
+  for (int i = 0; i < nobj; i++) {
+    const int l = objLabelsNew[i];
+    int New_lab = 0, best = -1;
+    for (int ll = 0; ll < kMaxLabel; ll++) {  // std::map order: ascending last label
+      const int c = hist[l * kMaxLabel + ll];
+      if (c > best && c > 0) {
+        best = c;
+        New_lab = ll;
+      }
+    }
+    if (bSecondFrame_) {
+      LabId[i] = mx++;
+    } else {
+      bool exist = false;
+      for (size_t k = 0; k < Ls.nSemPosition.size(); k++)
+        if (Ls.nSemPosition[k] == New_lab) {
+          LabId[i] = Ls.nModLabel[k];
+          exist = true;
+          break;
+        }
+      if (!exist) LabId[i] = mx++;
+    }
+  }
+  C.nModLabel = LabId;
+  C.nSemPosition.assign(objLabelsNew.begin(), objLabelsNew.begin() + nobj);
+  C.vObjMod.assign(nobj, std::vector<float>(16, 0.f));
+  if (nobj == 0) return;
+  // ---- D5: PnP-RANSAC per object (GetInitModelObj)
+  std::vector<PnPObject> po(nobj);
+  for (int i = 0; i < nobj; i++) {
+    const int l = objLabelsNew[i];
+    PnPBuf& b = pnp_[i];
+    PnPObject& o = po[i];
+    memset(&o, 0, sizeof(o));
+    o.n = &d_stats_[l].members;
+    o.members = d_members_ + (size_t)l * ocap_;
+    o.last_keys = Ls.ob.keys;
+    o.last_depth = Ls.ob.depth;
+    o.cur_keys = C.ho.okeys;
+    memcpy(o.Tlast, Ls.Tcw, sizeof(o.Tlast));
+    o.fx = cfg_.fx; o.fy = cfg_.fy; o.cx = cfg_.cx; o.cy = cfg_.cy;
+    o.reproj = 0.3;
+    o.confidence = 0.98;
+    ransac_subsets(std::max(stats[l].members, 1), kRansacIters, h_subsets_);
+    MMT_HIP(hipMemcpyAsync(b.subsets, h_subsets_.data(), sizeof(int) * 5 * kRansacIters,
+                           hipMemcpyHostToDevice, st));
+    o.subsets = b.subsets;
+    int PreObjID = -1;
+    for (size_t k = 0; k < Ls.nModLabel.size(); k++)
+      if (Ls.nModLabel[k] == LabId[i]) {
+        PreObjID = (int)k;
+        break;
+      }
+    o.use_mm = PreObjID >= 0;
+    if (o.use_mm) mat4_mul(C.Tcw, Ls.vObjMod[PreObjID].data(), o.MM);
+    o.pts3 = b.pts3;
+    o.pts2 = b.pts2;
+    o.models = b.models;
+    o.good = b.good;
+    o.masks = b.masks;
+    o.mask_words = mask_words_;
+    o.inliers = b.inliers;
+    o.mm_inliers = b.mm_inliers;
+    o.subset = b.subset;
+    o.n_subset = b.n_subset;
+    o.result = b.result;
+    o.Rt = b.Rt;
+    // hipMemcpyAsync of the subsets above must complete before the host vector is reused
+    MMT_HIP(hipStreamSynchronize(st));
+  }
+  MMT_HIP(hipMemcpyAsync(d_pnp_, po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
+  launch_pnp(d_pnp_, nobj, kRansacIters, st);
+  std::vector<int> res(8 * nobj);
+  std::vector<double> Rt(12 * nobj);
+  for (int i = 0; i < nobj; i++) {
+    MMT_HIP(hipMemcpyAsync(&res[8 * i], pnp_[i].result, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipMemcpyAsync(&Rt[12 * i], pnp_[i].Rt, sizeof(double) * 12, hipMemcpyDeviceToHost, st));
+  }
+  MMT_HIP(hipStreamSynchronize(st));
+  // ---- choose RANSAC model or motion model; D3 descriptors
+  std::vector<FlowSolveDesc> descs(nobj);
+  std::vector<std::vector<float>> inits(nobj, std::vector<float>(16));
+  for (int i = 0; i < nobj; i++) {
+    const int n_ransac = res[8 * i + 0] >= 0 ? res[8 * i + 3] : 0;
+    const int n_mm = po[i].use_mm ? res[8 * i + 4] : -1;
+    float Mod[16];
+    mat4_eye(Mod);
+    for (int r = 0; r < 3; r++) {
+      for (int c = 0; c < 3; c++) Mod[4 * r + c] = (float)Rt[12 * i + 3 * r + c];
+      Mod[4 * r + 3] = (float)Rt[12 * i + 9 + r];
+    }
+    if (po[i].use_mm && !(n_ransac > n_mm)) {
+      po[i].use_mm_choice = 1;
+      memcpy(inits[i].data(), po[i].MM, 64);
+    } else {
+      po[i].use_mm_choice = 0;
+      memcpy(inits[i].data(), Mod, 64);
+    }
+    if (res[8 * i + 0] < 0 && !po[i].use_mm_choice) {
+      // RANSAC found no model: empty inlier set (D3 then returns identity)
+      res[8 * i + 3] = 0;
+    }
+    ObjOut oo;
+    oo.label = LabId[i];
+    oo.sem_label = objLabelsNew[i];
+    oo.n_points = stats[objLabelsNew[i]].members;
+    oo.n_ransac_inliers = n_ransac;
+    oo.n_mm_inliers = n_mm;
+    oo.ransac_iterations = res[8 * i + 2];
+    memcpy(oo.init, inits[i].data(), 64);
+    out.objects.push_back(oo);
+    FlowSolveDesc& d = descs[i];
+    memset(&d, 0, sizeof(d));
+    d.d_n = pnp_[i].n_subset;
+    d.idx = pnp_[i].subset;
+    d.obs = Ls.ob.keys;
+    d.flow = Ls.ob.flow;
+    d.depth = Ls.ob.depth;
+    memcpy(d.Tcw_last, Ls.Tcw, sizeof(d.Tcw_last));
+    memcpy(d.init, inits[i].data(), 64);
+    d.rp_thres = 0.01f;
+    d.use_noise = 0;
+    d.max_iters = 200;
+    d.prior_info = 0.5;
+    d.fx = cfg_.fx; d.fy = cfg_.fy; d.cx = cfg_.cx; d.cy = cfg_.cy;
+    d.scratch = d_lm_scratch_ + flow_scratch_doubles(lm_cap_) * (1 + i);
+    d.cap = lm_cap_;
+    d.pose_out = d_poses_ + 16 * (1 + i);
+    d.stats = d_lmstats_ + 3 * (1 + i);
+  }
+  MMT_HIP(hipMemcpyAsync(d_pnp_, po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
+  launch_pnp_subset(d_pnp_, nobj, st);
+  MMT_HIP(hipMemcpyAsync(d_descs_ + 1, descs.data(), sizeof(FlowSolveDesc) * nobj,
+                         hipMemcpyHostToDevice, st));
+  launch_flow_lm(d_descs_ + 1, nobj, st);
+  std::vector<float> X(16 * nobj);
+  std::vector<int> lst(3 * nobj), nsub(nobj);
+  MMT_HIP(hipMemcpyAsync(X.data(), d_poses_ + 16, sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(lst.data(), d_lmstats_ + 3, sizeof(int) * 3 * nobj, hipMemcpyDeviceToHost, st));
+  for (int i = 0; i < nobj; i++)
+    MMT_HIP(hipMemcpyAsync(&nsub[i], pnp_[i].n_subset, sizeof(int), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipStreamSynchronize(st));
+  float TcwInv[16];
+  inv_mat(C.Tcw, TcwInv);
+  for (int i = 0; i < nobj; i++) {
+    float Xi[16];
+    if (lst[3 * i + 2] != 0)
+      mat4_eye(Xi);  // fewer than 3 correspondences: PoseOptimizationFlow2 returns identity
+    else
+      memcpy(Xi, &X[16 * i], 64);
+    mat4_mul(TcwInv, Xi, C.vObjMod[i].data());
+    ObjOut& oo = out.objects[i];
+    oo.n_solve = nsub[i];
+    oo.n_inliers = lst[3 * i + 2] ? 0 : lst[3 * i + 1];
+    oo.iterations = lst[3 * i];
+    memcpy(oo.X, Xi, 64);
+    memcpy(oo.motion, C.vObjMod[i].data(), 64);
+  }
+}
+
+// B9: the current slot becomes the last frame (Tracking.cc:2463-2477): its own samples
+// (st.keys/st.depth, ob.keys/ob.depth/ob.label) already live in the slot; just swap.
+void Tracker::finish_frame(FrameSlot& C, FrameOut& out, hipStream_t st) {
+  (void)out;
+  (void)st;
+  (void)C;
+  cur_ ^= 1;
+}
+
+}  // namespace mmt

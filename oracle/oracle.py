@@ -115,3 +115,91 @@ def orb_extract(gray, nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, mi
                                   ini_th, min_th, _p(kps), _p(desc), cap, ctypes.byref(n))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+# ------------------------------------------------------------------ tracker / solves
+def rng_first_gaussian(seed):
+    L = lib()
+    L.oracle_rng_first_gaussian.restype = ctypes.c_float
+    L.oracle_rng_first_gaussian.argtypes = [ctypes.c_ulonglong]
+    return L.oracle_rng_first_gaussian(seed)
+
+
+def flow_solve(obs, flow, depth, tcw_last, init, rp_thres, prior_info, max_iters, K):
+    L = lib()
+    L.oracle_flow_solve.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 5 + [
+        ctypes.c_float, ctypes.c_double, ctypes.c_int] + [ctypes.c_float] * 4 + [ctypes.c_void_p] * 2
+    obs = np.ascontiguousarray(obs, np.float32)
+    flow = np.ascontiguousarray(flow, np.float32)
+    depth = np.ascontiguousarray(depth, np.float32)
+    tl = np.ascontiguousarray(tcw_last, np.float32).reshape(16)
+    ini = np.ascontiguousarray(init, np.float32).reshape(16)
+    pose = np.zeros(16, np.float32)
+    st = np.zeros(3, np.int32)
+    rc = L.oracle_flow_solve(len(depth), _p(obs), _p(flow), _p(depth), _p(tl), _p(ini), rp_thres,
+                             prior_info, max_iters, K[0], K[1], K[2], K[3], _p(pose), _p(st))
+    return rc, pose.reshape(4, 4), dict(iterations=int(st[0]), inliers=int(st[1]))
+
+
+def pnp_ransac(pts3, pts2, K, max_iters=500, reproj=0.3, conf=0.98):
+    L = lib()
+    L.oracle_pnp_ransac.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + \
+        [ctypes.c_double] * 4 + [ctypes.c_int, ctypes.c_double, ctypes.c_double] + [ctypes.c_void_p] * 5
+    pts3 = np.ascontiguousarray(pts3, np.float32)
+    pts2 = np.ascontiguousarray(pts2, np.float32)
+    n = len(pts3)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    inl = np.zeros(max(n, 1), np.int32)
+    ninl = ctypes.c_int(0)
+    its = np.zeros(2, np.int32)
+    rc = L.oracle_pnp_ransac(_p(pts3), _p(pts2), n, K[0], K[1], K[2], K[3], max_iters, reproj,
+                             conf, _p(R), _p(t), _p(inl), ctypes.byref(ninl), _p(its))
+    return rc, R.reshape(3, 3), t, inl[:ninl.value].copy(), dict(iterations=int(its[0]),
+                                                                 best_iter=int(its[1]))
+
+
+def ransac_subsets(count, iters):
+    out = np.zeros(iters * 5, np.int32)
+    lib().oracle_ransac_subsets(count, iters, _p(out))
+    return out.reshape(iters, 5)
+
+
+class Tracker:
+    """CPU restatement of System::TrackRGBD (oracle/track_ref.cpp)."""
+
+    def __init__(self, w, h, K, bf, seed=0, nfeatures=2000):
+        L = lib()
+        L.oracle_tracker_create.restype = ctypes.c_void_p
+        L.oracle_tracker_create.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_float] * 5 + \
+            [ctypes.c_ulonglong, ctypes.c_int]
+        L.oracle_tracker_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_tracker_track.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_int]
+        self._h = L.oracle_tracker_create(w, h, K[0], K[1], K[2], K[3], bf, seed, nfeatures)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oracle_tracker_destroy(self._h)
+            self._h = None
+
+    def track(self, bgr, disp, flow, mask):
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        disp = np.ascontiguousarray(disp, np.uint16)
+        flow = np.ascontiguousarray(flow, np.float32)
+        mask = np.ascontiguousarray(mask, np.int32)
+        tcw = np.zeros(16, np.float32)
+        info = np.zeros(7, np.int32)
+        oi = np.zeros((16, 8), np.int32)
+        of = np.zeros((16, 48), np.float32)
+        lib().oracle_tracker_track(self._h, _p(bgr), _p(disp), _p(flow), _p(mask), _p(tcw),
+                                   _p(info), _p(oi), _p(of), 16)
+        objs = []
+        for i in range(min(int(info[6]), 16)):
+            objs.append(dict(label=int(oi[i, 0]), sem_label=int(oi[i, 1]), n_points=int(oi[i, 2]),
+                             ransac_inliers=int(oi[i, 3]), mm_inliers=int(oi[i, 4]),
+                             n_solve=int(oi[i, 5]), n_inliers=int(oi[i, 6]),
+                             iterations=int(oi[i, 7]), init=of[i, :16].reshape(4, 4),
+                             X=of[i, 16:32].reshape(4, 4), motion=of[i, 32:].reshape(4, 4)))
+        return dict(initialized=bool(info[0]), Tcw=tcw.reshape(4, 4), n_keys=int(info[1]),
+                    n_static=int(info[2]), n_obj_samples=int(info[3]), ego_iterations=int(info[4]),
+                    ego_inliers=int(info[5]), objects=objs)

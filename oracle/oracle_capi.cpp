@@ -122,3 +122,103 @@ int oracle_orb_extract(const uint8_t* gray, int w, int h, int nfeatures, float s
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ tracker / solve probes
+#include "oracle_solve.h"
+#include "oracle_track.h"
+
+extern "C" {
+
+float oracle_rng_first_gaussian(unsigned long long seed) { return cv_rng_first_gaussian(seed); }
+
+// Flow-refined pose solve probe (D2 when noise already applied to depth / D3).
+int oracle_flow_solve(int n, const float* obs, const float* flow, const float* depth,
+                      const float* tcw_last, const float* init, float rp_thres, double prior_info,
+                      int max_iters, float fx, float fy, float cx, float cy, float* pose_out,
+                      int* stats3) {
+  FlowProblem p;
+  p.n = n;
+  p.obs = obs;
+  p.flow = flow;
+  p.depth = depth;
+  memcpy(p.Tcw_last, tcw_last, sizeof(p.Tcw_last));
+  memcpy(p.init, init, sizeof(p.init));
+  p.rp_thres = rp_thres;
+  p.prior_info = prior_info;
+  p.max_iters = max_iters;
+  p.fx = fx; p.fy = fy; p.cx = cx; p.cy = cy;
+  FlowSolveStats st;
+  const int rc = flow_pose_solve(p, pose_out, &st);
+  stats3[0] = st.iterations;
+  stats3[1] = st.inliers;
+  stats3[2] = st.status;
+  return rc;
+}
+
+int oracle_pnp_ransac(const float* pts3, const float* pts2, int n, double fx, double fy,
+                      double cx, double cy, int max_iters, double reproj, double conf,
+                      double* R9, double* t3, int* inliers, int* n_inliers, int* iters) {
+  PnPResult r = pnp_ransac(pts3, pts2, n, fx, fy, cx, cy, max_iters, reproj, conf);
+  memcpy(R9, r.R, sizeof(r.R));
+  memcpy(t3, r.t, sizeof(r.t));
+  *n_inliers = (int)r.inliers.size();
+  for (size_t i = 0; i < r.inliers.size(); i++) inliers[i] = r.inliers[i];
+  iters[0] = r.iterations;
+  iters[1] = r.best_iter;
+  return r.ok ? 0 : 1;
+}
+
+int oracle_ransac_subsets(int count, int iters, int* out) {
+  std::vector<int> idx;
+  ransac_subsets(count, 5, iters, idx);
+  memcpy(out, idx.data(), idx.size() * sizeof(int));
+  return 0;
+}
+
+void* oracle_tracker_create(int w, int h, float fx, float fy, float cx, float cy, float bf,
+                            unsigned long long seed, int nfeatures) {
+  OTracker* t = new OTracker();
+  TrackParams p;
+  p.width = w;
+  p.height = h;
+  p.fx = fx; p.fy = fy; p.cx = cx; p.cy = cy; p.bf = bf;
+  p.noise_seed = seed;
+  OrbConfig c;
+  orb_config_init(c, nfeatures, 1.2f, 8, 20, 7);
+  t->init(p, c);
+  return t;
+}
+
+void oracle_tracker_destroy(void* t) { delete (OTracker*)t; }
+
+// Tracks one frame.  info: [initialized, n_keys, n_static, n_obj_samples, ego_iters,
+// ego_inliers, n_objects].  objs: per object 8 ints (label, sem, n_points, ransac_inliers,
+// mm_inliers, n_solve, n_inliers, iterations) + 48 floats (init, X, motion).
+int oracle_tracker_track(void* tp, const uint8_t* bgr, const uint16_t* disp, const float* flow,
+                         const int32_t* mask, float* tcw, int* info, int* obj_i, float* obj_f,
+                         int obj_cap) {
+  OTracker* t = (OTracker*)tp;
+  FrameResult r;
+  t->track(bgr, disp, flow, mask, r);
+  memcpy(tcw, r.Tcw, sizeof(r.Tcw));
+  info[0] = r.initialized;
+  info[1] = r.n_keys;
+  info[2] = r.n_static;
+  info[3] = r.n_obj_samples;
+  info[4] = r.ego_iterations;
+  info[5] = r.ego_inliers;
+  info[6] = (int)r.objects.size();
+  for (int i = 0; i < (int)r.objects.size() && i < obj_cap; i++) {
+    const ObjectResult& o = r.objects[i];
+    int* oi = obj_i + 8 * i;
+    oi[0] = o.label; oi[1] = o.sem_label; oi[2] = o.n_points; oi[3] = o.n_ransac_inliers;
+    oi[4] = o.n_mm_inliers; oi[5] = o.n_solve; oi[6] = o.n_inliers; oi[7] = o.iterations;
+    float* of = obj_f + 48 * i;
+    memcpy(of, o.init, 64);
+    memcpy(of + 16, o.X, 64);
+    memcpy(of + 32, o.motion, 64);
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,51 @@
+// oracle/oracle_solve.h -- TEST INFRASTRUCTURE ONLY (see orb_ref.cpp header).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "oracle_common.h"
+
+namespace oracle {
+
+// One flow-refined pose solve (Optimizer::PoseOptimizationFlow2Cam / PoseOptimizationFlow2).
+struct FlowProblem {
+  int n = 0;
+  const float* obs = nullptr;    // n x (u, v): last-frame sample pixel (edge measurement)
+  const float* flow = nullptr;   // n x (fu, fv): flow init = prior measurement
+  const float* depth = nullptr;  // n: last-frame depth (noisy for the ego solve)
+  float Tcw_last[16];            // row-major last-frame camera pose (Twl = inverse)
+  float init[16];                // row-major initial estimate of the solved pose
+  float rp_thres = 0.04f;        // Huber delta^2 and outlier threshold (0.04 ego / 0.01 object)
+  double prior_info = 0.3;       // EdgeFlowPrior information (0.3 ego / 0.5 object)
+  int max_iters = 100;           // 100 ego / 200 object
+  float fx = 0, fy = 0, cx = 0, cy = 0;
+};
+struct FlowSolveStats {
+  int iterations = 0, inliers = 0, status = 0;
+};
+int flow_pose_solve(const FlowProblem& p, float pose_out[16], FlowSolveStats* st);
+
+float cv_rng_first_gaussian(uint64_t seed);
+float noisy_depth(float z, float g0);
+
+// cv::solvePnPRansac(pre_3d, cur_2d, K, 0, rvec, tvec, false, iters, reproj, conf, inliers,
+// SOLVEPNP_AP3P) as called by Tracking::GetInitModelObj (Tracking.cc:4362-4365).
+struct PnPResult {
+  bool ok = false;
+  double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  double t[3] = {0, 0, 0};
+  std::vector<int> inliers;
+  int iterations = 0;
+  int best_iter = -1;
+};
+PnPResult pnp_ransac(const float* pts3, const float* pts2, int n, double fx, double fy, double cx,
+                     double cy, int max_iters, double reproj, double confidence);
+// RANSAC subset indices exactly as RANSACPointSetRegistrator::getSubset draws them.
+void ransac_subsets(int count, int model_points, int iters, std::vector<int>& idx);
+// EPnP on n >= 4 correspondences (epnp.cpp / PnPsolver.cc:342-1022), pixel inputs.
+void epnp_pose(const float* pts3, const float* pts2, const int* sel, int n, double fx, double fy,
+               double cx, double cy, double R[9], double t[3], bool f64_points);
+void rodrigues_r2v(const double R[9], double r[3]);
+void rodrigues_v2r(const double r[3], double R[9]);
+
+}  // namespace oracle

@@ -1,0 +1,71 @@
+// oracle/oracle_track.h -- TEST INFRASTRUCTURE ONLY (see orb_ref.cpp header).
+#pragma once
+#include <array>
+#include <cstdint>
+#include <vector>
+
+#include "oracle_common.h"
+
+namespace oracle {
+
+struct P2 {
+  float x, y;
+};
+
+struct TrackParams {
+  int width = 0, height = 0;
+  float fx = 0, fy = 0, cx = 0, cy = 0, bf = 0;
+  uint64_t noise_seed = 0;
+};
+
+// The parts of ORB_SLAM2::Frame this path reads (Frame.h of the reference).
+struct OFrame {
+  std::vector<float> depth;
+  std::vector<Key> keys;
+  std::vector<uint8_t> desc;
+  std::vector<P2> siftTmp, corres, flowNext;  // mvSiftKeysTmp, mvCorres, mvFlowNext
+  std::vector<float> siftDepthTmp;            // mvSiftDepthTmp
+  std::vector<P2> siftKeys;                   // mvSiftKeys
+  std::vector<float> siftDepth;               // mvSiftDepth
+  std::vector<P2> objKeys, objCorres, objFlow;  // mvObjKeys, mvObjCorres, mvObjFlowNext
+  std::vector<float> objDepth;                // mvObjDepth
+  std::vector<int> semObjLabel, objLabel;     // vSemObjLabel, vObjLabel
+  std::vector<std::array<float, 3>> flow3d;   // vFlow_3d
+  float Tcw[16] = {0};
+  bool hasPose = false;
+  std::vector<int> nModLabel, nSemPosition;
+  std::vector<std::vector<float>> vObjMod;
+};
+
+struct ObjectResult {
+  int label = 0, sem_label = 0, n_points = 0, n_ransac_inliers = 0, n_mm_inliers = -1;
+  int n_solve = 0, n_inliers = 0, iterations = 0;
+  float init[16], X[16], motion[16];
+  std::vector<int> ids, sub;
+};
+
+struct FrameResult {
+  bool initialized = false;
+  float Tcw[16] = {0};
+  int n_keys = 0, n_static = 0, n_obj_samples = 0, ego_iterations = 0, ego_inliers = 0;
+  std::vector<ObjectResult> objects;
+};
+
+void build_frame(const TrackParams& P, const OrbConfig& orb, const uint8_t* bgr,
+                 const uint16_t* disp, const float* flow, const int32_t* mask, OFrame& F);
+
+class OTracker {
+ public:
+  void init(const TrackParams& p, const OrbConfig& orb);
+  int track(const uint8_t* bgr, const uint16_t* disp, const float* flow, const int32_t* mask,
+            FrameResult& out);
+  TrackParams P;
+  OrbConfig orbc;
+  int state = 0;
+  bool bFirstFrame = false, bSecondFrame = false, hasVelocity = false;
+  float V[16] = {0};
+  float g0 = 0;
+  OFrame L;  // mLastFrame
+};
+
+}  // namespace oracle

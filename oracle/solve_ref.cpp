@@ -1,0 +1,512 @@
+// oracle/solve_ref.cpp -- TEST INFRASTRUCTURE ONLY (checker; see orb_ref.cpp header).
+//
+// CPU restatement of the flow-refined pose solves Optimizer::PoseOptimizationFlow2Cam
+// (reference src/Optimizer.cc:396-601) and Optimizer::PoseOptimizationFlow2 (:2170-2377) as
+// executed by the vendored, modified g2o:
+//   SparseOptimizer::optimize         Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:354-400
+//   OptimizationAlgorithmLevenberg    core/optimization_algorithm_levenberg.cpp:60-185
+//   BlockSolver_6_3 (Schur)           core/block_solver.hpp:354-489, 502-604
+//   LinearSolverDense (LDLT)          solvers/linear_solver_dense.h:65-113
+//   EdgeSE3ProjectFlow2 / EdgeFlowPrior / VertexSBAFlow / SE3Quat   types/*
+// including the 2-D "landmark" in a 3x3 block quirk, restated with the
+// closed forms of its block algebra:
+//   D_i   = [[h+l, h, 0], [0, l, 0], [0, 0, l]]       (2x2 column-major map onto a 3x3 block,
+//                                                      setLambda on all 3 diagonal entries)
+//   Dinv  = [[1/(h+l), -h/((h+l)l), 0], [0, 1/l, 0], [0, 0, 1/l]]
+//   Hs    = lower(Hpp + l I - sum_i B_i Dinv2_i B_i^T)   (LDLT reads the lower triangle)
+//   x_i   = (c0/(h+l) - h c1/((h+l)l) + [i>0] c0/l,  c1/l)   (stride-2 axpy spill)
+// Double precision throughout, like g2o/Eigen.  Also: the cv::RNG gaussian that
+// Frame::ObtainFlowDepthCamera draws from a freshly seeded RNG (Frame.cc:1241-1251).
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "oracle_solve.h"
+
+namespace oracle {
+
+// ------------------------------------------------------------------ cv::RNG (Appendix A.8)
+static inline uint64_t rng_next(uint64_t x) {
+  return (uint64_t)(unsigned)x * 4164903690ULL + (x >> 32);
+}
+
+float cv_rng_first_gaussian(uint64_t seed) {
+  // randn_0_1_32f ziggurat tables (OpenCV core/src/rand.cpp)
+  static unsigned kn[128];
+  static float wn[128], fn[128];
+  static bool init = false;
+  if (!init) {
+    const double m1 = 2147483648.0;
+    double dn = 3.442619855899, tn = dn, vn = 9.91256303526217e-3;
+    double q = vn / std::exp(-.5 * dn * dn);
+    kn[0] = (unsigned)((dn / q) * m1);
+    kn[1] = 0;
+    wn[0] = (float)(q / m1);
+    wn[127] = (float)(dn / m1);
+    fn[0] = 1.f;
+    fn[127] = (float)std::exp(-.5 * dn * dn);
+    for (int i = 126; i >= 1; i--) {
+      dn = std::sqrt(-2. * std::log(vn / dn + std::exp(-.5 * dn * dn)));
+      kn[i + 1] = (unsigned)((dn / tn) * m1);
+      tn = dn;
+      fn[i] = (float)std::exp(-.5 * dn * dn);
+      wn[i] = (float)(dn / m1);
+    }
+    init = true;
+  }
+  const float r = 3.442620f;
+  const float rng_flt = 2.3283064365386962890625e-10f;
+  uint64_t temp = seed ? seed : 0xffffffffULL;
+  float x, y;
+  for (;;) {
+    int hz = (int)temp;
+    temp = rng_next(temp);
+    int iz = hz & 127;
+    x = hz * wn[iz];
+    if ((unsigned)std::abs(hz) < kn[iz]) break;
+    if (iz == 0) {
+      do {
+        x = (unsigned)temp * rng_flt;
+        temp = rng_next(temp);
+        y = (unsigned)temp * rng_flt;
+        temp = rng_next(temp);
+        x = (float)(-std::log(x + FLT_MIN) * 0.2904764);
+        y = (float)-std::log(y + FLT_MIN);
+      } while (y + y < x * x);
+      x = hz > 0 ? r + x : -r - x;
+      break;
+    }
+    y = (unsigned)temp * rng_flt;
+    temp = rng_next(temp);
+    if (fn[iz] + y * (fn[iz - 1] - fn[iz]) < std::exp(-.5 * x * x)) break;
+  }
+  return x;
+}
+
+// Frame::ObtainFlowDepthCamera(i, addnoise=1): z + RNG(seed).gaussian(z*z/(725*0.5)*0.15)
+float noisy_depth(float z, float g0) {
+  const double sigma = (double)(z * z) / (725 * 0.5) * 0.15;
+  return (float)((double)z + (double)g0 * sigma);
+}
+
+// ------------------------------------------------------------------ SE3Quat (se3quat.h)
+struct Quat {
+  double x, y, z, w;
+};
+struct SE3 {
+  Quat q;
+  double t[3];
+};
+
+static void quat_normalize_rot(Quat& q) {  // SE3Quat::normalizeRotation
+  if (q.w < 0) {
+    q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w;
+  }
+  const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  q.x /= n; q.y /= n; q.z /= n; q.w /= n;
+}
+
+static Quat quat_from_R(const double R[3][3]) {  // Eigen::Quaternion(const Matrix3&)
+  Quat q;
+  const double t = R[0][0] + R[1][1] + R[2][2];
+  if (t > 0) {
+    double s = std::sqrt(t + 1.0);
+    q.w = 0.5 * s;
+    s = 0.5 / s;
+    q.x = (R[2][1] - R[1][2]) * s;
+    q.y = (R[0][2] - R[2][0]) * s;
+    q.z = (R[1][0] - R[0][1]) * s;
+  } else {
+    int i = 0;
+    if (R[1][1] > R[0][0]) i = 1;
+    if (R[2][2] > R[i][i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    double s = std::sqrt(R[i][i] - R[j][j] - R[k][k] + 1.0);
+    double v[3];
+    v[i] = 0.5 * s;
+    s = 0.5 / s;
+    q.w = (R[k][j] - R[j][k]) * s;
+    v[j] = (R[j][i] + R[i][j]) * s;
+    v[k] = (R[k][i] + R[i][k]) * s;
+    q.x = v[0]; q.y = v[1]; q.z = v[2];
+  }
+  return q;
+}
+
+static void quat_to_R(const Quat& q, double R[3][3]) {  // Eigen toRotationMatrix
+  const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+  const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+  const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+  const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+  R[0][0] = 1 - (tyy + tzz); R[0][1] = txy - twz;       R[0][2] = txz + twy;
+  R[1][0] = txy + twz;       R[1][1] = 1 - (txx + tzz); R[1][2] = tyz - twx;
+  R[2][0] = txz - twy;       R[2][1] = tyz + twx;       R[2][2] = 1 - (txx + tyy);
+}
+
+static void quat_rotate(const Quat& q, const double v[3], double out[3]) {
+  double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
+  uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+  const double c[3] = {q.y * uv[2] - q.z * uv[1], q.z * uv[0] - q.x * uv[2], q.x * uv[1] - q.y * uv[0]};
+  for (int k = 0; k < 3; k++) out[k] = v[k] + q.w * uv[k] + c[k];
+}
+
+static Quat quat_mul(const Quat& a, const Quat& b) {
+  Quat r;
+  r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+  r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+  r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+  r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+  return r;
+}
+
+static SE3 se3_from_float(const float T[16]) {  // Converter::toSE3Quat
+  double R[3][3];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) R[r][c] = (double)T[4 * r + c];
+  SE3 s;
+  s.q = quat_from_R(R);
+  quat_normalize_rot(s.q);
+  s.t[0] = T[3]; s.t[1] = T[7]; s.t[2] = T[11];
+  return s;
+}
+
+static void se3_to_float(const SE3& s, float T[16]) {  // Converter::toCvMat(SE3Quat)
+  double R[3][3];
+  quat_to_R(s.q, R);
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) T[4 * r + c] = (float)R[r][c];
+    T[4 * r + 3] = (float)s.t[r];
+  }
+  T[12] = T[13] = T[14] = 0.f;
+  T[15] = 1.f;
+}
+
+static SE3 se3_exp(const double u[6]) {  // SE3Quat::exp
+  const double om[3] = {u[0], u[1], u[2]};
+  const double up[3] = {u[3], u[4], u[5]};
+  const double theta = std::sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+  double O[3][3] = {{0, -om[2], om[1]}, {om[2], 0, -om[0]}, {-om[1], om[0], 0}};
+  double O2[3][3];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      double s = 0;
+      for (int k = 0; k < 3; k++) s += O[r][k] * O[k][c];
+      O2[r][c] = s;
+    }
+  double R[3][3], V[3][3];
+  if (theta < 0.00001) {
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) R[r][c] = (r == c ? 1.0 : 0.0) + O[r][c] + O2[r][c];
+    memcpy(V, R, sizeof(R));
+  } else {
+    const double a = std::sin(theta) / theta, b = (1 - std::cos(theta)) / (theta * theta);
+    const double c2 = (theta - std::sin(theta)) / std::pow(theta, 3);
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) {
+        R[r][c] = (r == c ? 1.0 : 0.0) + a * O[r][c] + b * O2[r][c];
+        V[r][c] = (r == c ? 1.0 : 0.0) + b * O[r][c] + c2 * O2[r][c];
+      }
+  }
+  SE3 s;
+  s.q = quat_from_R(R);
+  for (int r = 0; r < 3; r++) s.t[r] = V[r][0] * up[0] + V[r][1] * up[1] + V[r][2] * up[2];
+  quat_normalize_rot(s.q);  // SE3Quat(const Quaterniond&, const Vector3d&) normalises
+  return s;
+}
+
+static SE3 se3_mul(const SE3& a, const SE3& b) {  // SE3Quat::operator*
+  SE3 r;
+  double rt[3];
+  quat_rotate(a.q, b.t, rt);
+  for (int k = 0; k < 3; k++) r.t[k] = a.t[k] + rt[k];
+  r.q = quat_mul(a.q, b.q);
+  quat_normalize_rot(r.q);
+  return r;
+}
+
+static void se3_map(const SE3& s, const double X[3], double out[3]) {
+  quat_rotate(s.q, X, out);
+  for (int k = 0; k < 3; k++) out[k] += s.t[k];
+}
+
+// ------------------------------------------------------------------ 6x6 LDLT (Eigen LDLT<MatrixXd>)
+// Reads the lower triangle; diagonal pivoting as Eigen's ldlt_inplace<Lower>.  Returns false when
+// the factorisation is not positive (LDLT::isPositive()).
+static bool ldlt_solve6(const double Hin[6][6], const double b[6], double x[6]) {
+  double A[6][6];
+  for (int r = 0; r < 6; r++)
+    for (int c = 0; c < 6; c++) A[r][c] = (c <= r) ? Hin[r][c] : Hin[c][r];
+  int perm[6] = {0, 1, 2, 3, 4, 5};
+  bool positive = true;
+  double D[6];
+  double L[6][6] = {{0}};
+  // symmetric pivoting: at step k choose the largest remaining |diag|
+  for (int k = 0; k < 6; k++) {
+    int p = k;
+    double best = std::fabs(A[k][k]);
+    for (int i = k + 1; i < 6; i++)
+      if (std::fabs(A[i][i]) > best) {
+        best = std::fabs(A[i][i]);
+        p = i;
+      }
+    if (p != k) {
+      for (int c = 0; c < 6; c++) std::swap(A[k][c], A[p][c]);
+      for (int r = 0; r < 6; r++) std::swap(A[r][k], A[r][p]);
+      for (int c = 0; c < k; c++) std::swap(L[k][c], L[p][c]);
+      std::swap(perm[k], perm[p]);
+    }
+    double d = A[k][k];
+    for (int c = 0; c < k; c++) d -= L[k][c] * L[k][c] * D[c];
+    D[k] = d;
+    if (d < 0) positive = false;
+    for (int i = k + 1; i < 6; i++) {
+      double s = A[i][k];
+      for (int c = 0; c < k; c++) s -= L[i][c] * L[k][c] * D[c];
+      L[i][k] = (d != 0) ? s / d : 0.0;
+    }
+    L[k][k] = 1.0;
+  }
+  if (!positive) return false;
+  double y[6];
+  for (int i = 0; i < 6; i++) y[i] = b[perm[i]];
+  for (int i = 0; i < 6; i++)
+    for (int c = 0; c < i; c++) y[i] -= L[i][c] * y[c];
+  for (int i = 0; i < 6; i++) y[i] = (D[i] != 0) ? y[i] / D[i] : 0.0;
+  for (int i = 5; i >= 0; i--)
+    for (int r = i + 1; r < 6; r++) y[i] -= L[r][i] * y[r];
+  for (int i = 0; i < 6; i++) x[perm[i]] = y[i];
+  return true;
+}
+
+// ------------------------------------------------------------------ the LM
+struct EdgeState {
+  double Xw[3];  // Twl * back-projected observation (constant per edge)
+  double obs[2], prior[2];
+};
+
+static inline void huber(double e, double dsqr, double delta, double& rho0, double& rho1) {
+  if (e <= dsqr) {
+    rho0 = e;
+    rho1 = 1.;
+  } else {
+    const double s = std::sqrt(e);
+    rho0 = 2 * s * delta - dsqr;
+    rho1 = delta / s;
+  }
+}
+
+int flow_pose_solve(const FlowProblem& P, float pose_out[16], FlowSolveStats* st) {
+  const int N = P.n;
+  const double fx = P.fx, fy = P.fy, cx = P.cx, cy = P.cy;
+  const double kInfo = 0.1;  // info_flow (Optimizer.cc:466 / 2241)
+  const double pinfo = P.prior_info;
+  const float deltaF = std::sqrt(P.rp_thres);  // const float deltaMono = sqrt(rp_thres)
+  const double delta = (double)deltaF, dsqr = delta * delta;
+  if (N < 3) {
+    if (st) {
+      st->iterations = 0;
+      st->inliers = 0;
+      st->status = 1;
+    }
+    return 1;  // caller keeps its pose (Flow2Cam) / identity (Flow2)
+  }
+  // Twl = inverse(last Tcw) built as in Optimizer.cc:473-479 (float Mat ops, then double)
+  const float* T = P.Tcw_last;
+  float Rwl[3][3], twl[3];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) Rwl[r][c] = T[4 * c + r];
+  for (int r = 0; r < 3; r++) {  // -R^T * t via cv::gemm (double accumulation for CV_32F)
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)Rwl[r][k] * (double)T[4 * k + 3];
+    twl[r] = (float)(-s);
+  }
+  std::vector<EdgeState> E(N);
+  for (int i = 0; i < N; i++) {
+    const double u = P.obs[2 * i], v = P.obs[2 * i + 1], depth = P.depth[i];
+    const double Xc[3] = {(u - cx) * depth / fx, (v - cy) * depth / fy, depth};
+    for (int r = 0; r < 3; r++)
+      E[i].Xw[r] = (double)Rwl[r][0] * Xc[0] + (double)Rwl[r][1] * Xc[1] +
+                   (double)Rwl[r][2] * Xc[2] + (double)twl[r];
+    E[i].obs[0] = u;
+    E[i].obs[1] = v;
+    E[i].prior[0] = P.flow[2 * i];
+    E[i].prior[1] = P.flow[2 * i + 1];
+  }
+  SE3 pose = se3_from_float(P.init);
+  std::vector<double> f(2 * N), fb(2 * N);
+  for (int i = 0; i < 2 * N; i++) f[i] = E[i / 2].prior[i % 2];  // vFlo->setEstimate(FloD.head(2))
+
+  // error state (g2o keeps the errors of the LAST evaluated state, accepted or not)
+  std::vector<double> err(2 * N), perr(2 * N);
+  auto compute_errors = [&](const SE3& ps, const std::vector<double>& fl) {
+    for (int i = 0; i < N; i++) {
+      double pc[3];
+      se3_map(ps, E[i].Xw, pc);
+      const double pu = pc[0] / pc[2] * fx + cx, pv = pc[1] / pc[2] * fy + cy;
+      err[2 * i] = (E[i].obs[0] + fl[2 * i]) - pu;
+      err[2 * i + 1] = (E[i].obs[1] + fl[2 * i + 1]) - pv;
+      perr[2 * i] = fl[2 * i] - E[i].prior[0];
+      perr[2 * i + 1] = fl[2 * i + 1] - E[i].prior[1];
+    }
+  };
+  auto robust_chi2 = [&]() {
+    double chi = 0;
+    for (int i = 0; i < N; i++) {
+      const double e2 = kInfo * (err[2 * i] * err[2 * i] + err[2 * i + 1] * err[2 * i + 1]);
+      double r0, r1;
+      huber(e2, dsqr, delta, r0, r1);
+      chi += r0;
+      chi += pinfo * (perr[2 * i] * perr[2 * i] + perr[2 * i + 1] * perr[2 * i + 1]);
+    }
+    return chi;
+  };
+
+  double lambda = 0, ni = 2;
+  int nBad = 0;
+  double xbuf[6] = {0, 0, 0, 0, 0, 0};  // g2o's persistent _x (stale on a failed solve)
+  std::vector<double> xl(2 * N, 0.0);
+  std::vector<double> Bm(12 * N), h(N), bl(2 * N);
+  double chi2_check = 0;
+  int it_done = 0;
+  for (int iter = 0; iter < P.max_iters; iter++) {
+    // ---- OptimizationAlgorithmLevenberg::solve
+    compute_errors(pose, f);
+    double currentChi = robust_chi2();
+    const double iniChi = currentChi;
+    // buildSystem at the current state
+    double Hpp[6][6] = {{0}}, bp[6] = {0};
+    for (int i = 0; i < N; i++) {
+      double pc[3];
+      se3_map(pose, E[i].Xw, pc);
+      const double x = pc[0], y = pc[1], z = pc[2], z2 = z * z;
+      const double J[2][6] = {
+          {x * y / z2 * fx, -(1 + (x * x / z2)) * fx, y / z * fx, -1. / z * fx, 0, x / z2 * fx},
+          {(1 + y * y / z2) * fy, -x * y / z2 * fy, -x / z * fy, 0, -1. / z * fy, y / z2 * fy}};
+      const double e2 = kInfo * (err[2 * i] * err[2 * i] + err[2 * i + 1] * err[2 * i + 1]);
+      double r0, r1;
+      huber(e2, dsqr, delta, r0, r1);
+      const double w = kInfo * r1;
+      const double om[2] = {-w * err[2 * i], -w * err[2 * i + 1]};  // rho' * (-Omega e)
+      for (int a = 0; a < 6; a++) {
+        for (int b = 0; b < 6; b++) Hpp[a][b] += J[0][a] * w * J[0][b] + J[1][a] * w * J[1][b];
+        bp[a] += J[0][a] * om[0] + J[1][a] * om[1];
+        Bm[12 * i + 2 * a] = w * J[0][a];  // B_i (6x2) = J^T * (rho' Omega) * I
+        Bm[12 * i + 2 * a + 1] = w * J[1][a];
+      }
+      h[i] = w + pinfo;
+      bl[2 * i] = om[0] - pinfo * perr[2 * i];
+      bl[2 * i + 1] = om[1] - pinfo * perr[2 * i + 1];
+    }
+    if (iter == 0) {  // computeLambdaInit: tau * max |hessian diagonal| over all vertices
+      double maxd = 0;
+      for (int a = 0; a < 6; a++) maxd = std::max(maxd, std::fabs(Hpp[a][a]));
+      for (int i = 0; i < N; i++) maxd = std::max(maxd, std::fabs(h[i]));
+      lambda = 1e-5 * maxd;
+      ni = 2;
+      nBad = 0;
+    }
+    double rho = 0;
+    int qmax = 0;
+    double lastTrialChi = 0;
+    do {
+      const SE3 pose_b = pose;
+      fb = f;
+      // ---- BlockSolver::solve with the lambda-augmented diagonals
+      double Hs[6][6], bs[6];
+      for (int a = 0; a < 6; a++) {
+        for (int b = 0; b < 6; b++) Hs[a][b] = Hpp[a][b] + (a == b ? lambda : 0.0);
+        bs[a] = bp[a];
+      }
+      for (int i = 0; i < N; i++) {
+        const double hi = h[i];
+        const double d00 = 1.0 / (hi + lambda), d01 = -hi / ((hi + lambda) * lambda),
+                     d11 = 1.0 / lambda;
+        const double* B = &Bm[12 * i];
+        const double db0 = d00 * bl[2 * i] + d01 * bl[2 * i + 1], db1 = d11 * bl[2 * i + 1];
+        for (int a = 0; a < 6; a++) {
+          const double BD0 = B[2 * a] * d00, BD1 = B[2 * a] * d01 + B[2 * a + 1] * d11;
+          for (int b = 0; b < 6; b++) Hs[a][b] -= BD0 * B[2 * b] + BD1 * B[2 * b + 1];
+          bs[a] -= B[2 * a] * db0 + B[2 * a + 1] * db1;
+        }
+      }
+      double xp[6];
+      const bool ok2 = ldlt_solve6(Hs, bs, xp);
+      if (ok2) {
+        memcpy(xbuf, xp, sizeof(xp));
+        for (int i = 0; i < N; i++) {
+          const double* B = &Bm[12 * i];
+          double c0 = bl[2 * i], c1 = bl[2 * i + 1];
+          for (int a = 0; a < 6; a++) {
+            c0 -= B[2 * a] * xp[a];
+            c1 -= B[2 * a + 1] * xp[a];
+          }
+          const double hi = h[i];
+          double x0 = c0 / (hi + lambda) - hi * c1 / ((hi + lambda) * lambda);
+          if (i > 0) x0 += c0 / lambda;  // landmark i-1's third Dinv row lands here
+          xl[2 * i] = x0;
+          xl[2 * i + 1] = c1 / lambda;
+        }
+      }
+      // SparseOptimizer::update(x) -- applied even when the solve failed (stale _x)
+      pose = se3_mul(se3_exp(xbuf), pose);
+      for (int i = 0; i < 2 * N; i++) f[i] += xl[i];
+      compute_errors(pose, f);
+      double tempChi = robust_chi2();
+      lastTrialChi = tempChi;
+      if (!ok2) tempChi = DBL_MAX;
+      rho = currentChi - tempChi;
+      double scale = 0;
+      for (int a = 0; a < 6; a++) scale += xbuf[a] * (lambda * xbuf[a] + bp[a]);
+      for (int i = 0; i < 2 * N; i++) scale += xl[i] * (lambda * xl[i] + bl[i]);
+      scale += 1e-3;
+      rho /= scale;
+      if (rho > 0 && std::isfinite(tempChi)) {
+        double alpha = 1. - std::pow((2 * rho - 1), 3);
+        alpha = std::min(alpha, 2. / 3.);
+        const double sf = std::max(1. / 3., alpha);
+        lambda *= sf;
+        ni = 2;
+        currentChi = tempChi;
+      } else {
+        lambda *= ni;
+        ni *= 2;
+        pose = pose_b;
+        f = fb;
+      }
+      qmax++;
+    } while (rho < 0 && qmax < 10);
+    bool ok = true;
+    if (qmax == 10 || rho == 0) ok = false;  // Terminate
+    if (ok) {
+      if ((iniChi - currentChi) * 1e3 < iniChi)
+        nBad++;
+      else
+        nBad = 0;
+      if (nBad >= 3) ok = false;
+    }
+    // sparse_optimizer.cpp:393-396 (modified g2o): stop when the robust chi2 increased
+    if (chi2_check < lastTrialChi && iter > 0) ok = false;
+    chi2_check = lastTrialChi;
+    it_done = iter + 1;
+    if (!ok) break;
+  }
+  se3_to_float(pose, pose_out);
+  // outlier count from the edges' last computed errors (Optimizer.cc:536-566)
+  int nBadEdges = 0;
+  for (int i = 0; i < N; i++) {
+    const float chi2 = (float)(kInfo * (err[2 * i] * err[2 * i] + err[2 * i + 1] * err[2 * i + 1]));
+    if (chi2 > P.rp_thres) nBadEdges++;
+  }
+  if (st) {
+    st->iterations = it_done;
+    st->inliers = N - nBadEdges;
+    st->status = 0;
+  }
+  return 0;
+}
+
+}  // namespace oracle

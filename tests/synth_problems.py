@@ -1,0 +1,65 @@
+"""Seeded synthetic inputs for single-solve parity tests (flow-refined pose LM, PnP-RANSAC).
+
+These are inputs only; expected outputs come from the CPU oracle (oracle/) at test time."""
+import numpy as np
+
+K_KITTI = (721.5377, 721.5377, 609.5593, 172.8540)
+
+
+def rot(axis, ang):
+    axis = np.asarray(axis, np.float64)
+    axis = axis / np.linalg.norm(axis)
+    k = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * k + (1 - np.cos(ang)) * k @ k
+
+
+def se3(R, t):
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = t
+    return T.astype(np.float32)
+
+
+def project(T, Pw, K):
+    fx, fy, cx, cy = K
+    pc = (T[:3, :3].astype(np.float64) @ Pw.T).T + T[:3, 3]
+    return np.stack([pc[:, 0] / pc[:, 2] * fx + cx, pc[:, 1] / pc[:, 2] * fy + cy], 1), pc[:, 2]
+
+
+def flow_problem(seed, n, outlier_frac=0.1, pix_noise=0.3, motion=0.05, K=K_KITTI,
+                 w=1242, h=375):
+    """A last-frame pose, a true current pose, n world points seen in both; returns
+    (obs, flow, depth, Tcw_last, init, T_true).  Flow carries pixel noise and outliers."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = K
+    Tl = se3(rot(rng.normal(size=3), 0.05 * rng.normal()), rng.normal(size=3))
+    dT = se3(rot(rng.normal(size=3), motion * 0.1 * rng.normal()),
+             np.array([0.02, 0.01, 1.0]) * motion * 20 * rng.normal(size=3))
+    Tc = (dT.astype(np.float64) @ Tl).astype(np.float32)
+    u = rng.uniform(20, w - 20, n)
+    v = rng.uniform(20, h - 20, n)
+    z = rng.uniform(3.0, 40.0, n)
+    pc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    Twl = np.linalg.inv(Tl.astype(np.float64))
+    Pw = (Twl[:3, :3] @ pc.T).T + Twl[:3, 3]
+    uv2, _ = project(Tc, Pw, K)
+    flow = uv2 - np.stack([u, v], 1) + rng.normal(scale=pix_noise, size=(n, 2))
+    nout = int(outlier_frac * n)
+    if nout:
+        flow[:nout] += rng.uniform(-30, 30, size=(nout, 2))
+    obs = np.stack([u, v], 1).astype(np.float32)
+    # initial estimate: last pose (constant position) as in the tracker's second frame
+    return (obs, flow.astype(np.float32), z.astype(np.float32), Tl, Tl.copy(), Tc)
+
+
+def pnp_problem(seed, n, outlier_frac=0.3, pix_noise=0.1, K=K_KITTI):
+    """n 3-D points in the last camera frame and their pixels in the current frame."""
+    rng = np.random.default_rng(seed)
+    T = se3(rot(rng.normal(size=3), 0.1 * rng.normal()), rng.normal(size=3) * [0.3, 0.1, 1.0])
+    p = np.stack([rng.uniform(-8, 8, n), rng.uniform(-2, 2, n), rng.uniform(6, 30, n)], 1)
+    uv, z = project(T, p, K)
+    uv += rng.normal(scale=pix_noise, size=uv.shape)
+    nout = int(outlier_frac * n)
+    if nout:
+        uv[-nout:] += rng.uniform(-40, 40, size=(nout, 2))
+    return p.astype(np.float32), uv.astype(np.float32), T

@@ -1,0 +1,114 @@
+"""GPU parity of the tracking half of the hot path
+against the CPU oracle: single solves through the probe entry points, then whole kitti_sample
+sequences through mmt_track_rgbd / mmt_track_rgbd_chunk_device.
+
+Tolerance (north_star): SE(3) poses within 1e-4 (max abs over the 4x4 entries); integer
+outputs (counts, labels, iterations, inlier sets) exact."""
+import numpy as np
+import pytest
+
+from synth_problems import K_KITTI, flow_problem, pnp_problem
+
+pytestmark = pytest.mark.gpu
+POSE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import multimot_track_amd as M
+    c = M.Context(M.kitti03_config(nfeatures=2000, max_batch=8))
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("seed,n,out,ego", [(0, 400, 0.0, True), (1, 600, 0.1, True),
+                                             (2, 1500, 0.2, True), (3, 300, 0.15, False),
+                                             (4, 3000, 0.3, False), (5, 3, 0.0, False),
+                                             (6, 37, 0.3, True)])
+def test_flow_solve_matches_oracle(ctx, oracle_mod, seed, n, out, ego):
+    obs, flow, depth, Tl, init, _ = flow_problem(seed, n, outlier_frac=out)
+    args = (0.04, 0.3, 100) if ego else (0.01, 0.5, 200)
+    rc, pose_o, st_o = oracle_mod.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    status, pose_g, st_g = ctx.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    assert status == rc
+    assert st_g["iterations"] == st_o["iterations"]
+    assert st_g["inliers"] == st_o["inliers"]
+    if rc == 0:
+        assert np.abs(pose_g - pose_o).max() < POSE_TOL
+
+
+def test_flow_solve_too_few_edges(ctx):
+    obs, flow, depth, Tl, init, _ = flow_problem(8, 2)
+    status, _, st = ctx.flow_solve(obs, flow, depth, Tl, init, 0.04, 0.3, 100, K_KITTI)
+    assert status == 1 and st["iterations"] == 0
+
+
+@pytest.mark.parametrize("seed,n,out", [(0, 200, 0.3), (1, 1000, 0.5), (2, 5, 0.0),
+                                        (3, 64, 0.2), (4, 3000, 0.6), (5, 130, 0.9)])
+def test_pnp_ransac_matches_oracle(ctx, oracle_mod, seed, n, out):
+    p3, p2, _ = pnp_problem(seed, n, outlier_frac=out, pix_noise=0.05)
+    rc, R_o, t_o, inl_o, info_o = oracle_mod.pnp_ransac(p3, p2, K_KITTI)
+    R_g, t_g, inl_g, info_g = ctx.pnp_ransac(p3, p2, K_KITTI)
+    assert info_g["iterations"] == info_o["iterations"]
+    assert info_g["best_iter"] == info_o["best_iter"]
+    assert sorted(inl_g.tolist()) == sorted(inl_o.tolist())
+    if rc == 0:
+        assert np.abs(R_g - R_o).max() < POSE_TOL
+        assert np.abs(t_g - t_o).max() < POSE_TOL
+
+
+def _compare_frame(g, o, i):
+    assert g["initialized"] == o["initialized"], i
+    assert g["n_keys"] == o["n_keys"], i
+    assert g["n_obj_samples"] == o["n_obj_samples"], i
+    assert g["ego_iterations"] == o["ego_iterations"], i
+    assert g["ego_inliers"] == o["ego_inliers"], i
+    assert np.abs(g["Tcw"] - o["Tcw"]).max() < POSE_TOL, (i, g["Tcw"], o["Tcw"])
+    assert len(g["objects"]) == len(o["objects"]), i
+    for a, b in zip(g["objects"], o["objects"]):
+        for k in ("label", "sem_label", "n_points", "ransac_inliers", "mm_inliers", "n_solve",
+                  "n_inliers", "iterations"):
+            assert a[k] == b[k], (i, k, a[k], b[k])
+        for k in ("init", "X", "motion"):
+            assert np.abs(a[k] - b[k]).max() < POSE_TOL, (i, k, a[k], b[k])
+
+
+def test_track_kitti_sequence_matches_oracle(ctx, oracle_mod, kitti_frames):
+    ctx.reset()
+    tr = oracle_mod.Tracker(1242, 375, K_KITTI, 387.5744, 0, 2000)
+    for i, f in enumerate(kitti_frames):
+        o = tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+        g = ctx.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+        _compare_frame(g, o, i)
+
+
+def test_track_chunk_device_equals_per_frame(ctx, kitti_frames):
+    import torch
+    ctx.reset()
+    per = [ctx.track(f["bgr"], f["disp"], f["flow"], f["sem"]) for f in kitti_frames]
+    ctx.reset()
+    dev = torch.device("cuda:0")
+    bgr = torch.from_numpy(np.stack([f["bgr"] for f in kitti_frames])).to(dev)
+    disp = torch.from_numpy(np.stack([f["disp"].view(np.int16) for f in kitti_frames])).to(dev)
+    flow = torch.from_numpy(np.stack([f["flow"] for f in kitti_frames])).to(dev)
+    mask = torch.from_numpy(np.stack([f["sem"] for f in kitti_frames])).to(dev)
+    torch.cuda.synchronize()
+    got = ctx.track_chunk_device(bgr[:3], disp[:3], flow[:3], mask[:3])
+    got += ctx.track_chunk_device(bgr[3:], disp[3:], flow[3:], mask[3:])
+    for i, (a, b) in enumerate(zip(got, per)):
+        assert np.array_equal(a["Tcw"], b["Tcw"]), i
+        assert [o["label"] for o in a["objects"]] == [o["label"] for o in b["objects"]]
+        for x, y in zip(a["objects"], b["objects"]):
+            assert np.array_equal(x["motion"], y["motion"])
+
+
+def test_track_static_scene_without_objects(ctx, oracle_mod, kitti_frames):
+    """No semantic labels: ego-only tracking (C2-style input), objects list stays empty."""
+    ctx.reset()
+    tr = oracle_mod.Tracker(1242, 375, K_KITTI, 387.5744, 0, 2000)
+    for i, f in enumerate(kitti_frames[:3]):
+        z = np.zeros_like(f["sem"])
+        o = tr.track(f["bgr"], f["disp"], f["flow"], z)
+        g = ctx.track(f["bgr"], f["disp"], f["flow"], z)
+        _compare_frame(g, o, i)
+        assert g["objects"] == []
