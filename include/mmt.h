@@ -82,7 +82,7 @@ typedef struct mmt_frame_result {
   float Tcw[16];            /* row-major camera pose (world -> camera)                 */
   int32_t initialized;      /* tracking state OK (StereoInitialization done)           */
   int32_t n_keypoints;      /* ORB keypoints of the frame                              */
-  int32_t n_obj_samples;    /* object samples carried from the last frame              */
+  int32_t n_obj_samples;    /* mvObjKeys.size(): last frame's hand-off (own on frame 0) */
   int32_t ego_iterations;   /* LM iterations of PoseOptimizationFlow2Cam               */
   int32_t ego_inliers;      /* its inliers (chi2 <= 0.04)                              */
   int32_t n_objects;        /* dynamic objects solved this frame                       */

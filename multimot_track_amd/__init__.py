@@ -89,6 +89,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise MmtError("libmmt.so not built: run `python -c 'import __graft_entry__ as g; "
                            "g.build()'` (there is no CPU fallback)")
+        try:
+            # torch's bundled HIP runtime carries the same SONAME (libamdhip64.so.7): loading it
+            # first makes libmmt bind to it, so one runtime serves both and torch device
+            # pointers / streams are valid in libmmt.  Loaded the other way round, two HIP
+            # runtimes end up in the process and torch no longer sees the GPU.
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         L.mmt_version.restype = i32

@@ -267,6 +267,12 @@ void Tracker::track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st) {
     launch_handoff(Ls.st.corres, Ls.st.count, Ls.ob.corres, Ls.ob.count, a.depth, a.mask, W_, H_,
                    C.ho, st);
   if (state_ == 0) {
+    // mCurrentFrame.mvObjKeys: the frame's own samples, or the hand-off once bFirstFrame is set
+    int nob = 0;
+    MMT_HIP(hipMemcpyAsync(&nob, handoff ? Ls.ob.count : C.ob.count, sizeof(int),
+                           hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipStreamSynchronize(st));
+    out.n_obj_samples = nob;
     // ---- StereoInitialization (needs more than 500 keypoints)
     bFirstFrame_ = true;
     bSecondFrame_ = false;
@@ -325,6 +331,7 @@ void Tracker::track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   MMT_HIP(hipStreamSynchronize(st));
   if (lmst[2] != 0) memcpy(Tcw, Tinit, sizeof(Tcw));  // < 3 correspondences: pose unchanged
   memcpy(C.Tcw, Tcw, sizeof(Tcw));
+  out.n_obj_samples = n_last_obj;  // hand-off of the last frame's object correspondences
   out.ego_iterations = lmst[0];
   out.ego_inliers = lmst[1];
   {
