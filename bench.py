@@ -1,21 +1,25 @@
 """bench.py -- driver benchmark contract (one JSON line on rank 0).
 
-Workload (BASELINE.json configs[1]): KITTI-03 geometry 1242x375, 2000 ORB
-features, synthetic seeded frames (value noise, scene seed 1003) resident in HBM before the timed
-region.  A "step" = one pass of the hot path over one batch of `--batch` frames of one sequence.
+Workload (BASELINE.json configs[2]): KITTI-03 geometry 1242x375, 2000 ORB
+features, ego + 3 object motions.  Synthetic seeded street sequence (multimot_track_amd/scene.py:
+ray-cast ground, facades and three moving boxes with exact depth, flow and semantic labels),
+rendered straight into HBM before the timed region.  One sequence per GPU (seed 1003 + rank).
 
-Stage measured in this version: batched ORB extraction (ORBextractor::operator() for every frame
-of the batch: pyramid, FAST cells, octree, orientation, blur, BRIEF).  config.workload names the
-stage; the tracker stages are added to the timed region as they land.
+A "step" = System::TrackRGBD over one chunk of `--chunk` consecutive frames of the sequence:
+batched ORB extraction for the chunk, then per frame the association (B1-B9), the ego flow solve
+(PoseOptimizationFlow2Cam), object grouping, per-object PnP-RANSAC + PoseOptimizationFlow2 --
+everything the reference does per frame on this path (mmt_track_rgbd_chunk_device).  Frames are
+processed in order, so the tracker state carries across steps exactly as in rgbd_mmt.
 
-Multi-GPU: one process per GPU (torchrun); each rank owns an independent sequence (different seed),
-no data-path collective; barrier + cuda sync bracket the timed region; the time is the MAX over
-ranks; value = frames of all ranks / that time ("scaling": "weak").
+Multi-GPU: one process per GPU (torchrun), independent sequences, no data-path collective;
+barrier + device sync bracket the timed region; time = MAX over ranks; value = frames of all
+ranks / that time ("scaling": "weak").
 
-roofline: algorithmic bytes per ORB launch sequence (B_orb = 3WH + 4P + 60N per frame)
-/ its average duration from HIP events on the launch stream, vs the 8 TB/s HBM peak.
-cpu_baseline: the CPU oracle (oracle/, a scalar C++ restatement of the reference) on rank 0, on a
-bounded sample of the same frames, 1 core.
+roofline: the batched ORB launch sequence (B_orb = 3WH + 4P + 60N algorithmic bytes
+per frame x frames per launch) / its average duration from HIP events the library records on the
+launch stream around every ORB launch sequence (mmt_profile_*), vs the 8 TB/s HBM peak.
+cpu_baseline: the CPU oracle tracker (oracle/track_ref.cpp, a scalar C++ restatement of the
+reference's per-frame path) on rank 0 over the first frames of the same sequence, 1 core.
 """
 import argparse
 import json
@@ -29,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0
+METRIC = "KITTI RGB-D frames/sec (ego+object poses) at 1/2/4/8 GPUs; CPU ref fps"
 
 
 def b_orb(w, h, nfeat, lw, lh):
@@ -36,23 +41,34 @@ def b_orb(w, h, nfeat, lw, lh):
     return 3 * w * h + 4 * P + 60 * nfeat
 
 
+def load_traffic(path, cfg_key):
+    """HBM bytes per ORB launch sequence from a committed rocprofv3 --pmc summary (or None)."""
+    try:
+        d = json.load(open(path))
+        return d.get(cfg_key)
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--chunk", type=int, default=32, help="frames per step (ORB batch)")
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--nfeatures", type=int, default=2000)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--objects", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     import multimot_track_amd as M
-    from multimot_track_amd import synthetic
+    from multimot_track_amd import scene
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -62,89 +78,104 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    W, H, NF, B = args.width, args.height, args.nfeatures, args.batch
-    cfg = M.kitti03_config(W, H, NF, max_batch=B, device_id=local)
-    ctx = M.Context(cfg)
-    cap = ctx.capacity()
-    lv = ctx.levels()
-
-    # synthetic sequence of this rank (seed 1003 + rank), resident in HBM
-    seed0 = 1003 + 1000 * rank
-    frames = np.stack([synthetic.gray_frame(H, W, seed0 + i) for i in range(B)])
-    d_gray = torch.from_numpy(frames).to(dev)
-    d_kps = torch.empty((B, cap * 28), dtype=torch.uint8, device=dev)
-    d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
-    d_n = torch.empty(B, dtype=torch.int32, device=dev)
-    # a dedicated (non-default) stream: the library launches on it and the HIP events below are
-    # recorded on it, so they bracket exactly the kernels of the step
-    stream = torch.cuda.Stream(dev)
-
-    def step():
-        rc = M.lib().mmt_orb_extract_device(ctx.handle, d_gray.data_ptr(), B, W * H,
-                                            d_kps.data_ptr(), d_desc.data_ptr(), cap,
-                                            d_n.data_ptr(), stream.cuda_stream)
-        if rc != 0:
-            raise M.MmtError(M.lib().mmt_last_error(ctx.handle).decode())
-
-    torch.cuda.set_stream(stream)
-    for _ in range(args.warmup):
-        step()
+    W, H, NF, C = args.width, args.height, args.nfeatures, args.chunk
+    nframes = (args.warmup + args.steps) * C
+    seed = 1003 + rank
+    t_gen = time.perf_counter()
+    seq = scene.kitti_like_sequence(nframes, W, H, n_objects=args.objects, seed=seed, device=dev)
     torch.cuda.synchronize(dev)
+    t_gen = time.perf_counter() - t_gen
+
+    cfg = M.kitti03_config(W, H, NF, max_batch=C, device_id=local)
+    ctx = M.Context(cfg)
+    lv = ctx.levels()
+    # a dedicated (non-default) stream: the library launches on it and records its HIP events on
+    # it, and torch's sync below waits for it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+
+    def step(i):
+        sl = slice(i * C, (i + 1) * C)
+        return ctx.track_chunk_device(seq["bgr"][sl], seq["disp"][sl], seq["flow"][sl],
+                                      seq["mask"][sl], stream.cuda_stream, parse=False)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    ctx.profile_enable(True)
+    ctx.profile_read(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
+    results = [step(args.warmup + i) for i in range(args.steps)]
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    nkp = d_n.cpu().numpy()
+
+    # per-frame outputs of the timed region (sanity: every frame tracked, objects found)
+    res, objs = results[-1]
+    n_obj_last = int(res[C - 1].n_objects)
+    tracked = sum(int(r.initialized) for rr, _ in results for r in rr)
+    gt = seq["Tcw"][-1]
+    ego_err = float(np.abs(np.array(res[C - 1].Tcw[:]).reshape(4, 4) - gt).max())
 
     if rank == 0:
-        frames_total = args.steps * B * world
+        frames_total = args.steps * C * world
         value = frames_total / elapsed
-        bytes_per_launch = B * b_orb(W, H, NF, lv["level_w"], lv["level_h"])
+        launch_ms = prof["orb_ms"] / max(prof["orb_launches"], 1)
+        bytes_per_launch = C * b_orb(W, H, NF, lv["level_w"], lv["level_h"])
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        key = "%dx%d_n%d_b%d" % (W, H, NF, C)
+        traffic = load_traffic(args.traffic_file, key)
         cpu = None
         if not args.no_cpu:
             from oracle import oracle as O
             O.build()
-            n_done, tc0 = 0, time.perf_counter()
-            while time.perf_counter() - tc0 < args.cpu_seconds:
-                O.orb_extract(frames[n_done % B], NF)
+            K = (cfg.fx, cfg.fy, cfg.cx, cfg.cy)
+            tr = O.Tracker(W, H, K, cfg.bf, 0, NF)
+            n_done, tcpu = 0, 0.0
+            while tcpu < args.cpu_seconds and n_done < nframes:
+                f = scene.to_numpy_frames({k: seq[k][n_done:n_done + 1]
+                                           for k in ("bgr", "disp", "flow", "mask")})[0]
+                tc = time.perf_counter()
+                tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+                tcpu += time.perf_counter() - tc
                 n_done += 1
-            tcpu = time.perf_counter() - tc0
-            cpu = {"value": n_done / tcpu, "unit": "frames/s", "cores": 1, "kind": "port",
-                   "sample": "%d synthetic 1242x375 frames, ORB extraction (oracle/orb_ref.cpp), "
-                             "single thread, %.1f s" % (n_done, tcpu)}
+            cpu = {"value": round(n_done / tcpu, 3), "unit": "frames/s", "cores": 1,
+                   "kind": "port",
+                   "sample": "first %d frames of the same C3 sequence, full per-frame tracking "
+                             "(oracle/track_ref.cpp: ORB, association, ego + object solves), "
+                             "single thread, %.1f s of CPU time" % (n_done, tcpu)}
         out = {
-            "metric": "KITTI RGB-D frames/sec (ego+object poses) at 1/2/4/8 GPUs; CPU ref fps",
+            "metric": METRIC,
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u8", "data": "synthetic (seeded value-noise frames, KITTI-03 geometry)",
-            "config": {"workload": "C2 front end, stage: batched ORB extraction only "
-                                   "(tracker stages not yet in the timed region)",
-                       "width": W, "height": H, "orb_features": NF, "batch_frames": B,
-                       "keypoints_per_frame": float(nkp.mean()), "parallelism": "dp%d" % world},
+            "dtype": "u8", "data": "synthetic (seeded ray-cast street sequence, exact depth/flow/"
+                                   "labels, KITTI-03 camera), resident in HBM",
+            "config": {"workload": "C3: KITTI-03-like RGB-D, end-to-end TrackRGBD (ORB + "
+                                   "association + ego + %d object motions)" % args.objects,
+                       "width": W, "height": H, "orb_features": NF, "chunk_frames": C,
+                       "sequences_per_gpu": 1, "parallelism": "dp%d" % world,
+                       "frames_tracked": tracked, "objects_last_frame": n_obj_last,
+                       "ego_abs_err_last_frame": round(ego_err, 5),
+                       "scene_render_s": round(t_gen, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None,
-                         "kernel": "ORB launch sequence (k_resize..k_orient_desc), %d frames" % B,
-                         "launch_ms": round(launch_ms, 4), "bytes_per_launch": bytes_per_launch},
+                         "traffic": traffic,
+                         "kernel": "batched ORB launch sequence (k_resize, k_fast, k_octree, "
+                                   "k_blur, k_orient_desc) over %d frames" % C,
+                         "launch_ms": round(launch_ms, 4), "bytes_per_launch": bytes_per_launch,
+                         "orb_share_of_step": round(prof["orb_ms"] / (elapsed * 1e3), 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -166,6 +166,16 @@ int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, fl
                    double* R_out, double* t_out, int* inliers_out, int* n_inliers,
                    int* iters_out /* iterations run, best hypothesis */);
 
+/* Stage timing with HIP events on the launch stream (no reference counterpart: measurement
+ * hook for bench.py).  orb_ms sums the batched ORB launch sequences of the tracked chunks. */
+typedef struct mmt_profile {
+  double orb_ms;
+  int64_t orb_launches;
+  int64_t orb_frames;
+} mmt_profile;
+int mmt_profile_enable(mmt_ctx* ctx, int on);
+int mmt_profile_read(mmt_ctx* ctx, mmt_profile* out, int reset);
+
 /* Forget the sequence (Tracking::Reset). */
 int mmt_reset(mmt_ctx* ctx);
 

@@ -58,6 +58,11 @@ class MmtFlowProblem(ctypes.Structure):
                 ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float)]
 
 
+class MmtProfile(ctypes.Structure):
+    _fields_ = [("orb_ms", ctypes.c_double), ("orb_launches", ctypes.c_int64),
+                ("orb_frames", ctypes.c_int64)]
+
+
 MAX_OBJECTS = 8  # objects reported per frame (kMaxObj in csrc/mmt_tracker.h)
 
 
@@ -119,6 +124,8 @@ def lib():
         L.mmt_pose_flow_solve.argtypes = [vp, ctypes.POINTER(MmtFlowProblem), vp, vp]
         L.mmt_pnp_ransac.argtypes = [vp, vp, vp, i32] + [ctypes.c_float] * 4 + \
             [i32, ctypes.c_double, ctypes.c_double] + [vp] * 5
+        L.mmt_profile_enable.argtypes = [vp, i32]
+        L.mmt_profile_read.argtypes = [vp, ctypes.POINTER(MmtProfile), i32]
         _LIB = L
     return _LIB
 
@@ -223,9 +230,14 @@ class Context:
                                          float(timestamp), ctypes.byref(r), objs, MAX_OBJECTS))
         return _frame_dict(r, objs)
 
-    def track_chunk_device(self, bgr, disp, flow, mask, stream=0):
+    def track_chunk_device(self, bgr, disp, flow, mask, stream=0, parse=True):
         """Device-resident chunk (torch tensors on this context's device, frame-major):
-        bgr [F,H,W,3] u8, disp [F,H,W] i16/u16 bits, flow [F,H,W,2] f32, mask [F,H,W] i32."""
+        bgr [F,H,W,3] u8, disp [F,H,W] i16/u16 bits, flow [F,H,W,2] f32, mask [F,H,W] i32.
+        parse=False returns the raw (MmtFrameResult[F], MmtMotion[F * MAX_OBJECTS]) arrays."""
+        for t, shp in ((bgr, 3), (disp, None), (flow, 2), (mask, None)):
+            assert t.is_cuda and t.is_contiguous() and t.shape[1:3] == (self.cfg.height,
+                                                                         self.cfg.width)
+            assert shp is None or t.shape[3] == shp
         nf = int(bgr.shape[0])
         res = (MmtFrameResult * nf)()
         objs = (MmtMotion * (nf * MAX_OBJECTS))()
@@ -236,8 +248,18 @@ class Context:
             self._h, nf, bgr.data_ptr(), pitch(bgr), disp.data_ptr(), pitch(disp),
             flow.data_ptr(), pitch(flow), mask.data_ptr(), pitch(mask), res, objs, MAX_OBJECTS,
             ctypes.c_void_p(stream)))
+        if not parse:
+            return res, objs
         return [_frame_dict(res[i], objs[i * MAX_OBJECTS:(i + 1) * MAX_OBJECTS])
                 for i in range(nf)]
+
+    def profile_enable(self, on=True):
+        self._check(lib().mmt_profile_enable(self._h, int(on)))
+
+    def profile_read(self, reset=False):
+        p = MmtProfile()
+        self._check(lib().mmt_profile_read(self._h, ctypes.byref(p), int(reset)))
+        return dict(orb_ms=p.orb_ms, orb_launches=p.orb_launches, orb_frames=p.orb_frames)
 
     # -- probes of single solves ------------------------------------------------------------
     def flow_solve(self, obs, flow, depth, tcw_last, init, rp_thres, prior_info, max_iters,

@@ -250,6 +250,26 @@ static void fill_results(const std::vector<mmt::FrameOut>& outs, mmt_frame_resul
   }
 }
 
+int mmt_profile_enable(mmt_ctx* ctx, int on) {
+  if (!ctx) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ensure_tracker(ctx);
+    ctx->tracker.set_profiling(on != 0);
+  });
+}
+
+int mmt_profile_read(mmt_ctx* ctx, mmt_profile* out, int reset) {
+  if (!ctx || !out) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    ensure_tracker(ctx);
+    long long l = 0, f = 0;
+    ctx->tracker.read_profile(&out->orb_ms, &l, &f, reset != 0);
+    out->orb_launches = l;
+    out->orb_frames = f;
+  });
+}
+
 int mmt_reset(mmt_ctx* ctx) {
   if (!ctx) return MMT_EINVAL;
   return guard(ctx, [&] {
@@ -362,6 +382,7 @@ int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, fl
     DevBuf<int> dn(1), sub(5 * (size_t)max_iters), good(max_iters), inl(n), mm(n), subset(n),
         nsub(1), res(8);
     DevBuf<double> models(6 * (size_t)max_iters), Rt(12);
+    DevBuf<double> hrec((size_t)mmt::kHypRec * max_iters), hout((size_t)3 * mmt::kHypOut * max_iters);
     DevBuf<unsigned long long> masks((size_t)max_iters * words);
     DevBuf<mmt::PnPObject> po(1);
     std::vector<int> h_sub;
@@ -380,6 +401,8 @@ int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, fl
     o.pts3 = p3.p;
     o.pts2 = p2.p;
     o.models = models.p;
+    o.hrec = hrec.p;
+    o.hout = hout.p;
     o.good = good.p;
     o.masks = masks.p;
     o.mask_words = words;

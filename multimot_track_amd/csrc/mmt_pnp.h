@@ -24,6 +24,8 @@ struct PnPObject {
   float* pts3;              // [cap][3] pre_3d
   float2* pts2;             // [cap] cur_2d
   double* models;           // [max_iters][6] rvec, tvec
+  double* hrec;             // [max_iters][kHypRec] per-hypothesis EPnP state (null space, L, ...)
+  double* hout;             // [max_iters][3][kHypOut] err, R, t of the three beta estimates
   int* good;                // [max_iters]
   unsigned long long* masks;  // [max_iters][mask_words]
   int mask_words;
@@ -34,6 +36,9 @@ struct PnPObject {
   int* result;              // best, maxGood, iterations, n_ransac_inliers, n_mm_inliers
   double* Rt;               // R (9), t (3)
 };
+
+constexpr int kHypRec = 160;  // doubles per hypothesis record
+constexpr int kHypOut = 16;   // doubles per (hypothesis, beta variant) result
 
 void launch_pnp(PnPObject* d_objs, int nobj, int max_iters, hipStream_t st, bool gather = true);
 void launch_pnp_subset(PnPObject* d_objs, int nobj, hipStream_t st);

@@ -3,14 +3,17 @@
 // called by Tracking::GetInitModelObj (reference src/Tracking.cc:4324-4443).
 //
 //   k_pnp_gather   pre_3d = UnprojectStereoObject(last sample), cur_2d = current sample
-//   k_pnp_hyp      one lane per RANSAC hypothesis: 5-point EPnP (PnPsolver.cc:342-1022 lineage)
+//   k_pnp_hyp      one wave per RANSAC hypothesis: 5-point EPnP (PnPsolver.cc:342-1022 lineage)
 //                  on the subset drawn by RNG((uint64)-1) (precomputed on the host: the draw
-//                  sequence depends only on the point count), then Rodrigues -> model
-//   k_pnp_score    one workgroup per hypothesis: projectPoints + squared-error test, inlier
-//                  count by ballot/popcount, inlier bit mask
+//                  sequence depends only on the point count) up to the null space of M^T M
+//   k_pnp_beta<V>  one lane per hypothesis: beta estimate V, Gauss-Newton, R and t
+//   k_pnp_score    picks the best estimate (Rodrigues -> model), then one workgroup per
+//                  hypothesis scores it
+//                  (projectPoints + squared-error test, inlier count by ballot/popcount,
+//                  inlier bit mask)
 //   k_pnp_select   replay of RANSACPointSetRegistrator::run's best-so-far / niters logic
-//   k_pnp_refit    one workgroup per object: EPnP over all RANSAC inliers (reductions over the
-//                  points, 12x12 eigen-solve and beta estimation in one lane)
+//   k_refit_*      EPnP over all RANSAC inliers (reductions over the points, block-wide 12x12
+//                  eigen-solve, beta estimates in lanes, one Procrustes solve per wave)
 //   k_mm_inliers   motion-model check (Tracking.cc:4375-4405)
 // The dense algebra (cyclic/one-sided Jacobi) follows oracle/pnp_ref.cpp operation for
 // operation so hypothesis models agree to the last bit with the CPU checker.
@@ -25,111 +28,180 @@
 
 namespace mmt {
 
-// ---------------------------------------------------------------- dense helpers (one lane)
-__device__ void d_jacobi_eig_sym(int n, double* A, double* d, double* vt, double* V, int* ord) {
-  for (int i = 0; i < n * n; i++) V[i] = 0.0;
-  for (int i = 0; i < n; i++) V[i * n + i] = 1.0;
+// ---------------------------------------------------------------- register-resident dense algebra
+// One lane, every array index a compile-time constant after unrolling, so the matrices live in
+// VGPRs (dynamic indexing of private arrays would put them in scratch memory).  Operation order
+// follows oracle/pnp_ref.cpp exactly.
+
+// cyclic Jacobi eigen-decomposition of a small symmetric matrix; eigenvectors as rows of vt,
+// stable descending order of the eigenvalues
+template <int N>
+__device__ __forceinline__ void eig_sym_small(double (&A)[N * N], double (&d)[N],
+                                              double (&vt)[N * N]) {
+  double V[N * N];
+#pragma unroll
+  for (int i = 0; i < N * N; i++) V[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 100; sweep++) {
-    double off = 0;
-    for (int p = 0; p < n; p++)
-      for (int q = p + 1; q < n; q++) off += A[p * n + q] * A[p * n + q];
-    if (off < 1e-300) break;
-    for (int p = 0; p < n; p++)
-      for (int q = p + 1; q < n; q++) {
-        const double apq = A[p * n + q];
+    double off = 0, dsum = 0;  // convergence test of oracle/pnp_ref.cpp
+#pragma unroll
+    for (int p = 0; p < N; p++) {
+      dsum += A[p * N + p] * A[p * N + p];
+#pragma unroll
+      for (int q = p + 1; q < N; q++) off += A[p * N + q] * A[p * N + q];
+    }
+    if (off <= 1e-26 * dsum) break;
+#pragma unroll
+    for (int p = 0; p < N; p++)
+#pragma unroll
+      for (int q = p + 1; q < N; q++) {
+        const double apq = A[p * N + q];
         if (fabs(apq) < 1e-300) continue;
-        const double app = A[p * n + p], aqq = A[q * n + q];
+        const double app = A[p * N + p], aqq = A[q * N + q];
         const double theta = (aqq - app) / (2 * apq);
         const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
         const double c = 1 / sqrt(t * t + 1), s = t * c;
-        for (int k = 0; k < n; k++) {
-          const double akp = A[k * n + p], akq = A[k * n + q];
-          A[k * n + p] = c * akp - s * akq;
-          A[k * n + q] = s * akp + c * akq;
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+          const double akp = A[k * N + p], akq = A[k * N + q];
+          A[k * N + p] = c * akp - s * akq;
+          A[k * N + q] = s * akp + c * akq;
         }
-        for (int k = 0; k < n; k++) {
-          const double apk = A[p * n + k], aqk = A[q * n + k];
-          A[p * n + k] = c * apk - s * aqk;
-          A[q * n + k] = s * apk + c * aqk;
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+          const double apk = A[p * N + k], aqk = A[q * N + k];
+          A[p * N + k] = c * apk - s * aqk;
+          A[q * N + k] = s * apk + c * aqk;
         }
-        for (int k = 0; k < n; k++) {
-          const double vkp = V[k * n + p], vkq = V[k * n + q];
-          V[k * n + p] = c * vkp - s * vkq;
-          V[k * n + q] = s * vkp + c * vkq;
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+          const double vkp = V[k * N + p], vkq = V[k * N + q];
+          V[k * N + p] = c * vkp - s * vkq;
+          V[k * N + q] = s * vkp + c * vkq;
         }
       }
   }
-  // stable sort by descending eigenvalue (insertion sort == std::stable_sort order)
-  for (int i = 0; i < n; i++) ord[i] = i;
-  for (int i = 1; i < n; i++) {
-    const int v = ord[i];
-    int j = i - 1;
-    while (j >= 0 && A[ord[j] * n + ord[j]] < A[v * n + v]) {
-      ord[j + 1] = ord[j];
-      j--;
-    }
-    ord[j + 1] = v;
-  }
-  for (int r = 0; r < n; r++) {
-    d[r] = A[ord[r] * n + ord[r]];
-    for (int k = 0; k < n; k++) vt[r * n + k] = V[k * n + ord[r]];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    int rank = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++)
+      rank += (A[j * (N + 1)] > A[i * (N + 1)]) || (j < i && A[j * (N + 1)] == A[i * (N + 1)]);
+#pragma unroll
+    for (int r = 0; r < N; r++)
+      if (rank == r) {
+        d[r] = A[i * (N + 1)];
+#pragma unroll
+        for (int k = 0; k < N; k++) vt[r * N + k] = V[k * N + i];
+      }
   }
 }
 
-// thin SVD (m >= n) by one-sided Jacobi; A is overwritten
-__device__ void d_jacobi_svd(int m, int n, double* A, double* U, double* w, double* V) {
-  for (int i = 0; i < n * n; i++) V[i] = 0;
-  for (int i = 0; i < n; i++) V[i * n + i] = 1;
+// thin SVD (M >= N) by one-sided Jacobi; A is overwritten
+template <int M, int N>
+__device__ __forceinline__ void svd_small(double (&A)[M * N], double (&U)[M * N], double (&w)[N],
+                                          double (&V)[N * N]) {
+#pragma unroll
+  for (int i = 0; i < N * N; i++) V[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 100; sweep++) {
     bool changed = false;
-    for (int p = 0; p < n; p++)
-      for (int q = p + 1; q < n; q++) {
+#pragma unroll
+    for (int p = 0; p < N; p++)
+#pragma unroll
+      for (int q = p + 1; q < N; q++) {
         double a = 0, b = 0, g = 0;
-        for (int k = 0; k < m; k++) {
-          a += A[k * n + p] * A[k * n + p];
-          b += A[k * n + q] * A[k * n + q];
-          g += A[k * n + p] * A[k * n + q];
+#pragma unroll
+        for (int k = 0; k < M; k++) {
+          a += A[k * N + p] * A[k * N + p];
+          b += A[k * N + q] * A[k * N + q];
+          g += A[k * N + p] * A[k * N + q];
         }
         if (fabs(g) <= 1e-15 * sqrt(a * b) || g == 0) continue;
         changed = true;
         const double zeta = (b - a) / (2 * g);
         const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1 + zeta * zeta));
         const double c = 1 / sqrt(1 + t * t), s = c * t;
-        for (int k = 0; k < m; k++) {
-          const double x = A[k * n + p], y = A[k * n + q];
-          A[k * n + p] = c * x - s * y;
-          A[k * n + q] = s * x + c * y;
+#pragma unroll
+        for (int k = 0; k < M; k++) {
+          const double x = A[k * N + p], y = A[k * N + q];
+          A[k * N + p] = c * x - s * y;
+          A[k * N + q] = s * x + c * y;
         }
-        for (int k = 0; k < n; k++) {
-          const double x = V[k * n + p], y = V[k * n + q];
-          V[k * n + p] = c * x - s * y;
-          V[k * n + q] = s * x + c * y;
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+          const double x = V[k * N + p], y = V[k * N + q];
+          V[k * N + p] = c * x - s * y;
+          V[k * N + q] = s * x + c * y;
         }
       }
     if (!changed) break;
   }
-  for (int j = 0; j < n; j++) {
+#pragma unroll
+  for (int j = 0; j < N; j++) {
     double s = 0;
-    for (int k = 0; k < m; k++) s += A[k * n + j] * A[k * n + j];
+#pragma unroll
+    for (int k = 0; k < M; k++) s += A[k * N + j] * A[k * N + j];
     w[j] = sqrt(s);
-    for (int k = 0; k < m; k++) U[k * n + j] = w[j] > 0 ? A[k * n + j] / w[j] : 0.0;
+#pragma unroll
+    for (int k = 0; k < M; k++) U[k * N + j] = w[j] > 0 ? A[k * N + j] / w[j] : 0.0;
   }
 }
 
-__device__ void d_svd_solve(int m, int n, const double* Ain, const double* b, double* x) {
-  double A[30], U[30], w[5], V[25];
-  for (int i = 0; i < m * n; i++) A[i] = Ain[i];
-  d_jacobi_svd(m, n, A, U, w, V);
+// x = pinv(A) b (cvSolve(..., CV_SVD)); A (M x N) is overwritten
+template <int M, int N>
+__device__ __forceinline__ void svd_solve_small(double (&A)[M * N], const double (&b)[M],
+                                                double (&x)[N]) {
+  double U[M * N], w[N], V[N * N];
+  svd_small<M, N>(A, U, w, V);
   double wmax = 0;
-  for (int j = 0; j < n; j++) wmax = fmax(wmax, w[j]);
-  const double thr = DBL_EPSILON * wmax * m;
-  for (int i = 0; i < n; i++) x[i] = 0;
-  for (int j = 0; j < n; j++) {
+#pragma unroll
+  for (int j = 0; j < N; j++) wmax = fmax(wmax, w[j]);
+  const double thr = DBL_EPSILON * wmax * M;
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] = 0;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
     if (w[j] <= thr) continue;
     double ub = 0;
-    for (int k = 0; k < m; k++) ub += U[k * n + j] * b[k];
+#pragma unroll
+    for (int k = 0; k < M; k++) ub += U[k * N + j] * b[k];
     ub /= w[j];
-    for (int i = 0; i < n; i++) x[i] += V[i * n + j] * ub;
+#pragma unroll
+    for (int i = 0; i < N; i++) x[i] += V[i * N + j] * ub;
+  }
+}
+
+// pseudo-inverse of the 3x3 control-point matrix (cvInvert(CC, CC_inv, CV_SVD))
+__device__ __forceinline__ void pinv3(double (&cc)[9], double (&ci)[9]) {
+  double U[9], w[3], V[9];
+  svd_small<3, 3>(cc, U, w, V);
+  const double wmax = fmax(w[0], fmax(w[1], w[2]));
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      double s = 0;
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+        if (w[k] > DBL_EPSILON * wmax * 3) s += V[r * 3 + k] * U[c * 3 + k] / w[k];
+      ci[3 * r + c] = s;
+    }
+}
+
+// rotation from the cross-covariance abt (estimate_R_and_t)
+__device__ __forceinline__ void procrustes_R(double (&abt)[9], double (&R)[9]) {
+  double U[9], w[3], V[9];
+  svd_small<3, 3>(abt, U, w, V);
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      R[3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
+  const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] -
+                     R[2] * R[4] * R[6] - R[1] * R[3] * R[8] - R[0] * R[5] * R[7];
+  if (det < 0) {
+    R[6] = -R[6];
+    R[7] = -R[7];
+    R[8] = -R[8];
   }
 }
 
@@ -140,13 +212,17 @@ __device__ __forceinline__ double d_dist2(const double* a, const double* b) {
   return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
 }
 
-__device__ void d_compute_L_6x10(const double* ut, double* l) {
-  const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+// L_6x10 from the four null-space vectors ut rows 11, 10, 9, 8 (ut in LDS)
+__device__ __forceinline__ void compute_L_6x10(const double* ut, double (&l)[60]) {
   double dv[4][6][3];
+#pragma unroll
   for (int i = 0; i < 4; i++) {
+    const double* v = ut + 12 * (11 - i);
     int a = 0, b = 1;
+#pragma unroll
     for (int j = 0; j < 6; j++) {
-      for (int k = 0; k < 3; k++) dv[i][j][k] = v[i][3 * a + k] - v[i][3 * b + k];
+#pragma unroll
+      for (int k = 0; k < 3; k++) dv[i][j][k] = v[3 * a + k] - v[3 * b + k];
       b++;
       if (b > 3) {
         a++;
@@ -154,6 +230,7 @@ __device__ void d_compute_L_6x10(const double* ut, double* l) {
       }
     }
   }
+#pragma unroll
   for (int i = 0; i < 6; i++) {
     double* row = l + 10 * i;
     row[0] = d_dot3(dv[0][i], dv[0][i]);
@@ -169,129 +246,130 @@ __device__ void d_compute_L_6x10(const double* ut, double* l) {
   }
 }
 
-__device__ void d_betas(int which, const double* L, const double* rho, double* betas) {
-  if (which == 1) {
-    double A[24], b4[4];
-    for (int i = 0; i < 6; i++) {
-      A[4 * i] = L[10 * i];
-      A[4 * i + 1] = L[10 * i + 1];
-      A[4 * i + 2] = L[10 * i + 3];
-      A[4 * i + 3] = L[10 * i + 6];
-    }
-    d_svd_solve(6, 4, A, rho, b4);
-    if (b4[0] < 0) {
-      betas[0] = sqrt(-b4[0]);
-      betas[1] = -b4[1] / betas[0];
-      betas[2] = -b4[2] / betas[0];
-      betas[3] = -b4[3] / betas[0];
-    } else {
-      betas[0] = sqrt(b4[0]);
-      betas[1] = b4[1] / betas[0];
-      betas[2] = b4[2] / betas[0];
-      betas[3] = b4[3] / betas[0];
-    }
-  } else if (which == 2) {
-    double A[18], b3[3];
-    for (int i = 0; i < 6; i++)
-      for (int k = 0; k < 3; k++) A[3 * i + k] = L[10 * i + k];
-    d_svd_solve(6, 3, A, rho, b3);
-    if (b3[0] < 0) {
-      betas[0] = sqrt(-b3[0]);
-      betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
-    } else {
-      betas[0] = sqrt(b3[0]);
-      betas[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
-    }
-    if (b3[1] < 0) betas[0] = -betas[0];
-    betas[2] = 0.0;
-    betas[3] = 0.0;
+__device__ __forceinline__ void betas_approx_1(const double (&L)[60], const double (&rho)[6],
+                                               double (&betas)[4]) {
+  double A[24], b4[4];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    A[4 * i] = L[10 * i];
+    A[4 * i + 1] = L[10 * i + 1];
+    A[4 * i + 2] = L[10 * i + 3];
+    A[4 * i + 3] = L[10 * i + 6];
+  }
+  svd_solve_small<6, 4>(A, rho, b4);
+  if (b4[0] < 0) {
+    betas[0] = sqrt(-b4[0]);
+    betas[1] = -b4[1] / betas[0];
+    betas[2] = -b4[2] / betas[0];
+    betas[3] = -b4[3] / betas[0];
   } else {
-    double A[30], b5[5];
-    for (int i = 0; i < 6; i++)
-      for (int k = 0; k < 5; k++) A[5 * i + k] = L[10 * i + k];
-    d_svd_solve(6, 5, A, rho, b5);
-    if (b5[0] < 0) {
-      betas[0] = sqrt(-b5[0]);
-      betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
-    } else {
-      betas[0] = sqrt(b5[0]);
-      betas[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
-    }
-    if (b5[1] < 0) betas[0] = -betas[0];
-    betas[2] = b5[3] / betas[0];
-    betas[3] = 0.0;
+    betas[0] = sqrt(b4[0]);
+    betas[1] = b4[1] / betas[0];
+    betas[2] = b4[2] / betas[0];
+    betas[3] = b4[3] / betas[0];
   }
 }
 
-__device__ void d_qr_solve(double* A, double* b, double* X) {  // 6 x 4 (PnPsolver.cc:840-950)
-  const int nr = 6, nc = 4;
-  double A1[6], A2[6];
-  double *pA = A, *ppAkk = pA;
+__device__ __forceinline__ void betas_approx_2(const double (&L)[60], const double (&rho)[6],
+                                               double (&betas)[4]) {
+  double A[18], b3[3];
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) A[3 * i + k] = L[10 * i + k];
+  svd_solve_small<6, 3>(A, rho, b3);
+  if (b3[0] < 0) {
+    betas[0] = sqrt(-b3[0]);
+    betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
+  } else {
+    betas[0] = sqrt(b3[0]);
+    betas[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
+  }
+  if (b3[1] < 0) betas[0] = -betas[0];
+  betas[2] = 0.0;
+  betas[3] = 0.0;
+}
+
+__device__ __forceinline__ void betas_approx_3(const double (&L)[60], const double (&rho)[6],
+                                               double (&betas)[4]) {
+  double A[30], b5[5];
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
+    for (int k = 0; k < 5; k++) A[5 * i + k] = L[10 * i + k];
+  svd_solve_small<6, 5>(A, rho, b5);
+  if (b5[0] < 0) {
+    betas[0] = sqrt(-b5[0]);
+    betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
+  } else {
+    betas[0] = sqrt(b5[0]);
+    betas[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
+  }
+  if (b5[1] < 0) betas[0] = -betas[0];
+  betas[2] = b5[3] / betas[0];
+  betas[3] = 0.0;
+}
+
+// Householder QR solve of the 6x4 Gauss-Newton system (PnPsolver.cc:840-950, including its
+// column-max scan that starts one row early)
+__device__ __forceinline__ void qr_solve_6x4(double (&A)[24], double (&b)[6], double (&X)[4]) {
+  constexpr int nr = 6, nc = 4;
+  double A1[4], A2[4];
+#pragma unroll
   for (int k = 0; k < nc; k++) {
-    double *ppAik = ppAkk, eta = fabs(*ppAik);
+    double eta = fabs(A[k * nc + k]);
+#pragma unroll
     for (int i = k + 1; i < nr; i++) {
-      double elt = fabs(*ppAik);
+      const double elt = fabs(A[(i - 1) * nc + k]);
       if (eta < elt) eta = elt;
-      ppAik += nc;
     }
-    if (eta == 0) return;
-    double sum = 0.0, inv_eta = 1. / eta;
-    ppAik = ppAkk;
+    if (eta == 0) return;  // "A is singular": X left unchanged
+    double sum = 0.0;
+    const double inv_eta = 1. / eta;
+#pragma unroll
     for (int i = k; i < nr; i++) {
-      *ppAik *= inv_eta;
-      sum += *ppAik * *ppAik;
-      ppAik += nc;
+      A[i * nc + k] *= inv_eta;
+      sum += A[i * nc + k] * A[i * nc + k];
     }
     double sigma = sqrt(sum);
-    if (*ppAkk < 0) sigma = -sigma;
-    *ppAkk += sigma;
-    A1[k] = sigma * *ppAkk;
+    if (A[k * nc + k] < 0) sigma = -sigma;
+    A[k * nc + k] += sigma;
+    A1[k] = sigma * A[k * nc + k];
     A2[k] = -eta * sigma;
+#pragma unroll
     for (int j = k + 1; j < nc; j++) {
-      double* pp = ppAkk;
       double s = 0;
-      for (int i = k; i < nr; i++) {
-        s += *pp * pp[j - k];
-        pp += nc;
-      }
+#pragma unroll
+      for (int i = k; i < nr; i++) s += A[i * nc + k] * A[i * nc + j];
       const double tau = s / A1[k];
-      pp = ppAkk;
-      for (int i = k; i < nr; i++) {
-        pp[j - k] -= tau * *pp;
-        pp += nc;
-      }
+#pragma unroll
+      for (int i = k; i < nr; i++) A[i * nc + j] -= tau * A[i * nc + k];
     }
-    ppAkk += nc + 1;
   }
-  double *ppAjj = pA, *pb = b;
+#pragma unroll
   for (int j = 0; j < nc; j++) {
-    double *ppAij = ppAjj, tau = 0;
-    for (int i = j; i < nr; i++) {
-      tau += *ppAij * pb[i];
-      ppAij += nc;
-    }
+    double tau = 0;
+#pragma unroll
+    for (int i = j; i < nr; i++) tau += A[i * nc + j] * b[i];
     tau /= A1[j];
-    ppAij = ppAjj;
-    for (int i = j; i < nr; i++) {
-      pb[i] -= tau * *ppAij;
-      ppAij += nc;
-    }
-    ppAjj += nc + 1;
+#pragma unroll
+    for (int i = j; i < nr; i++) b[i] -= tau * A[i * nc + j];
   }
-  X[nc - 1] = pb[nc - 1] / A2[nc - 1];
+  X[nc - 1] = b[nc - 1] / A2[nc - 1];
+#pragma unroll
   for (int i = nc - 2; i >= 0; i--) {
-    double *ppAij = pA + i * nc + (i + 1), s = 0;
-    for (int j = i + 1; j < nc; j++) {
-      s += *ppAij * X[j];
-      ppAij++;
-    }
-    X[i] = (pb[i] - s) / A2[i];
+    double s = 0;
+#pragma unroll
+    for (int j = i + 1; j < nc; j++) s += A[i * nc + j] * X[j];
+    X[i] = (b[i] - s) / A2[i];
   }
 }
 
-__device__ void d_gauss_newton(const double* L, const double* rho, double* betas) {
+__device__ __forceinline__ void gauss_newton(const double (&L)[60], const double (&rho)[6],
+                                             double (&betas)[4]) {
   for (int k = 0; k < 5; k++) {
     double A[24], b[6], x[4] = {0, 0, 0, 0};
+#pragma unroll
     for (int i = 0; i < 6; i++) {
       const double* r = L + i * 10;
       double* a = A + i * 4;
@@ -305,8 +383,22 @@ __device__ void d_gauss_newton(const double* L, const double* rho, double* betas
                        r[6] * betas[0] * betas[3] + r[7] * betas[1] * betas[3] +
                        r[8] * betas[2] * betas[3] + r[9] * betas[3] * betas[3]);
     }
-    d_qr_solve(A, b, x);
+    qr_solve_6x4(A, b, x);
+#pragma unroll
     for (int i = 0; i < 4; i++) betas[i] += x[i];
+  }
+}
+
+// ccs = sum_i betas[i] * ut row (11 - i)  (compute_ccs)
+__device__ __forceinline__ void compute_ccs(const double* ut, const double (&betas)[4],
+                                            double (&ccs)[12]) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) ccs[i] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double* v = ut + 12 * (11 - i);
+#pragma unroll
+    for (int j = 0; j < 12; j++) ccs[j] += betas[i] * v[j];
   }
 }
 
@@ -358,123 +450,94 @@ __device__ void d_rodrigues_v2r(const double rv[3], double R[9]) {
   for (int i = 0; i < 9; i++) R[i] = c * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i] + s * rx[i];
 }
 
-// ---------------------------------------------------------------- EPnP over a point set
-// Points are accessed through `pw(i)`/`us(i)` loaders so the same code serves the 5-point
-// hypotheses (one lane) and, via reductions, the refit.
-struct EPnPSmall {  // n <= 5, all in lane-private storage
-  int n;
-  double fu, fv, uc, vc;
-  double pws[15], us[10], alphas[20], pcs[15];
-  double cws[4][3], ccs[4][3];
-
-  __device__ void choose_control_points() {
-    cws[0][0] = cws[0][1] = cws[0][2] = 0;
-    for (int i = 0; i < n; i++)
-      for (int j = 0; j < 3; j++) cws[0][j] += pws[3 * i + j];
-    for (int j = 0; j < 3; j++) cws[0][j] /= n;
-    double m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < n; i++) {
-      double p[3];
-      for (int j = 0; j < 3; j++) p[j] = pws[3 * i + j] - cws[0][j];
-      for (int a = 0; a < 3; a++)
-        for (int b = 0; b < 3; b++) m[3 * a + b] += p[a] * p[b];
-    }
-    double dc[3], uct[9], V[9];
-    int ord[3];
-    d_jacobi_eig_sym(3, m, dc, uct, V, ord);
-    for (int i = 1; i < 4; i++) {
-      const double k = sqrt(fmax(dc[i - 1], 0.0) / n);
-      for (int j = 0; j < 3; j++) cws[i][j] = cws[0][j] + k * uct[3 * (i - 1) + j];
-    }
-  }
-  __device__ void compute_barycentric() {
-    double cc[9];
-    for (int i = 0; i < 3; i++)
-      for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
-    double U[9], w[3], V[9], ci[9];
-    d_jacobi_svd(3, 3, cc, U, w, V);
-    const double wmax = fmax(w[0], fmax(w[1], w[2]));
-    for (int r = 0; r < 3; r++)
-      for (int c = 0; c < 3; c++) {
-        double s = 0;
-        for (int k = 0; k < 3; k++)
-          if (w[k] > DBL_EPSILON * wmax * 3) s += V[r * 3 + k] * U[c * 3 + k] / w[k];
-        ci[3 * r + c] = s;
-      }
-    for (int i = 0; i < n; i++) {
-      const double* pi = &pws[3 * i];
-      double* a = &alphas[4 * i];
-      for (int j = 0; j < 3; j++)
-        a[1 + j] = ci[3 * j] * (pi[0] - cws[0][0]) + ci[3 * j + 1] * (pi[1] - cws[0][1]) +
-                   ci[3 * j + 2] * (pi[2] - cws[0][2]);
-      a[0] = 1.0f - a[1] - a[2] - a[3];
-    }
-  }
-  __device__ double compute_R_and_t(const double* ut, const double* betas, double R[3][3],
-                                    double t[3]) {
-    for (int i = 0; i < 4; i++) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
-    for (int i = 0; i < 4; i++) {
-      const double* v = ut + 12 * (11 - i);
-      for (int j = 0; j < 4; j++)
-        for (int k = 0; k < 3; k++) ccs[j][k] += betas[i] * v[3 * j + k];
-    }
-    for (int i = 0; i < n; i++) {
-      const double* a = &alphas[4 * i];
-      for (int j = 0; j < 3; j++)
-        pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
-    }
-    if (pcs[2] < 0.0) {
-      for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 3; j++) ccs[i][j] = -ccs[i][j];
-      for (int i = 0; i < 3 * n; i++) pcs[i] = -pcs[i];
-    }
-    double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
-    for (int i = 0; i < n; i++)
-      for (int j = 0; j < 3; j++) {
-        pc0[j] += pcs[3 * i + j];
-        pw0[j] += pws[3 * i + j];
-      }
-    for (int j = 0; j < 3; j++) {
-      pc0[j] /= n;
-      pw0[j] /= n;
-    }
-    double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < n; i++) {
-      const double* pc = &pcs[3 * i];
-      const double* pw = &pws[3 * i];
-      for (int j = 0; j < 3; j++) {
-        abt[3 * j] += (pc[j] - pc0[j]) * (pw[0] - pw0[0]);
-        abt[3 * j + 1] += (pc[j] - pc0[j]) * (pw[1] - pw0[1]);
-        abt[3 * j + 2] += (pc[j] - pc0[j]) * (pw[2] - pw0[2]);
-      }
-    }
-    double U[9], w[3], V[9];
-    d_jacobi_svd(3, 3, abt, U, w, V);
-    for (int i = 0; i < 3; i++)
-      for (int j = 0; j < 3; j++) R[i][j] = d_dot3(U + 3 * i, V + 3 * j);
-    const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] +
-                       R[0][2] * R[1][0] * R[2][1] - R[0][2] * R[1][1] * R[2][0] -
-                       R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
-    if (det < 0) {
-      R[2][0] = -R[2][0];
-      R[2][1] = -R[2][1];
-      R[2][2] = -R[2][2];
-    }
-    t[0] = pc0[0] - d_dot3(R[0], pw0);
-    t[1] = pc0[1] - d_dot3(R[1], pw0);
-    t[2] = pc0[2] - d_dot3(R[2], pw0);
-    double sum2 = 0.0;
-    for (int i = 0; i < n; i++) {
-      const double* pw = &pws[3 * i];
-      const double Xc = d_dot3(R[0], pw) + t[0], Yc = d_dot3(R[1], pw) + t[1];
-      const double inv_Zc = 1.0 / (d_dot3(R[2], pw) + t[2]);
-      const double ue = uc + fu * Xc * inv_Zc, ve = vc + fv * Yc * inv_Zc;
-      const double u = us[2 * i], v = us[2 * i + 1];
-      sum2 += sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
-    }
-    return sum2 / n;
-  }
+// ---------------------------------------------------------------- 12x12 eigen-solve, block-wide
+// Parallel-order Jacobi (oracle/pnp_ref.cpp: jacobi_eig12_rr): per round 6 disjoint pairs, angles
+// from the round's start matrix, then B = A J (columns) and A = J^T B (rows), V = V J, each element
+// by its own lane.  A, B, V, V2 in LDS; `cs` holds c/s indexed by the pair's smaller index.
+struct Eig12Smem {
+  double A[144], B[144], V[144], V2[144], ut[144], c[12], s[12];
+  int done;
 };
+
+__device__ __forceinline__ void rr_partner(int r, int j, int& p, int& q) {
+  const int k = j == 11 ? r : (j == r ? 11 : (2 * r - j + 22) % 11);
+  p = min(j, k);
+  q = max(j, k);
+}
+
+// all threads of the block call this; A holds M^T M on entry; ut (rows = eigenvectors by
+// descending eigenvalue) on exit
+__device__ void eig12_block(Eig12Smem& S) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int e = tid; e < 144; e += nt) S.V[e] = (e % 13 == 0) ? 1.0 : 0.0;
+  __syncthreads();
+  double* V = S.V;
+  double* V2 = S.V2;
+  for (int sweep = 0; sweep < 100; sweep++) {
+    if (tid == 0) {
+      double off = 0, dsum = 0;
+      for (int p = 0; p < 12; p++) {
+        dsum += S.A[p * 12 + p] * S.A[p * 12 + p];
+        for (int q = p + 1; q < 12; q++) off += S.A[p * 12 + q] * S.A[p * 12 + q];
+      }
+      S.done = off <= 1e-26 * dsum;
+    }
+    __syncthreads();
+    if (S.done) break;
+    for (int r = 0; r < 11; r++) {
+      if (tid < 6) {
+        const int a = tid == 0 ? r : (r + tid) % 11, b = tid == 0 ? 11 : (r - tid + 11) % 11;
+        const int p = min(a, b), q = max(a, b);
+        const double apq = S.A[p * 12 + q];
+        if (fabs(apq) < 1e-300) {
+          S.c[p] = 1.0;
+          S.s[p] = 0.0;
+        } else {
+          const double app = S.A[p * 12 + p], aqq = S.A[q * 12 + q];
+          const double theta = (aqq - app) / (2 * apq);
+          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+          const double c = 1 / sqrt(t * t + 1);
+          S.c[p] = c;
+          S.s[p] = t * c;
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < 144; e += nt) {
+        const int k = e / 12, j = e - 12 * k;
+        int p, q;
+        rr_partner(r, j, p, q);
+        const double cc = S.c[p], ss = S.s[p];
+        if (j == p) {
+          S.B[e] = cc * S.A[k * 12 + p] - ss * S.A[k * 12 + q];
+          V2[e] = cc * V[k * 12 + p] - ss * V[k * 12 + q];
+        } else {
+          S.B[e] = ss * S.A[k * 12 + p] + cc * S.A[k * 12 + q];
+          V2[e] = ss * V[k * 12 + p] + cc * V[k * 12 + q];
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < 144; e += nt) {
+        const int i = e / 12, k = e - 12 * i;
+        int p, q;
+        rr_partner(r, i, p, q);
+        const double cc = S.c[p], ss = S.s[p];
+        S.A[e] = i == p ? cc * S.B[p * 12 + k] - ss * S.B[q * 12 + k]
+                        : ss * S.B[p * 12 + k] + cc * S.B[q * 12 + k];
+      }
+      double* tmp = V;
+      V = V2;
+      V2 = tmp;
+      __syncthreads();
+    }
+  }
+  if (tid < 12) {
+    const double di = S.A[tid * 13];
+    int rank = 0;
+    for (int j = 0; j < 12; j++) rank += (S.A[j * 13] > di) || (j < tid && S.A[j * 13] == di);
+    for (int k = 0; k < 12; k++) S.ut[rank * 12 + k] = V[k * 12 + tid];
+  }
+  __syncthreads();
+}
 
 // ---------------------------------------------------------------- kernels
 __global__ __launch_bounds__(256) void k_pnp_gather(PnPObject* objs) {
@@ -500,84 +563,220 @@ __global__ __launch_bounds__(256) void k_pnp_gather(PnPObject* objs) {
   }
 }
 
-// one lane per (object, hypothesis)
+// Hypothesis record layout (doubles): the four null-space vectors ut rows 8..11, alphas, pws,
+// us, L_6x10, rho
+constexpr int R_UT = 0, R_AL = 48, R_PW = 68, R_US = 83, R_L = 93, R_RHO = 153;
+
+// one 64-lane workgroup per (hypothesis, object): 5-point EPnP up to the null space.  Lane 0 does
+// the small dense algebra in registers, the 64 lanes build M^T M and run the 12x12 eigen-solve.
+struct HypSmem {
+  Eig12Smem eig;
+  double pws[15], us[10], alphas[20], cws[12];
+};
+
 __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) {
+  __shared__ HypSmem S;
+  const int h = blockIdx.x, tid = threadIdx.x;
+  PnPObject& o = objs[blockIdx.y];
+  const int n = *o.n;
+  if (h >= max_iters || n < 5) return;
+  const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
+  if (tid == 0) {
+    double pws[15], us[10], cws[12];
+    const double ifx = 1. / fu, ify = 1. / fv;
+    const int* sub = o.subsets + 5 * h;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int j = n == 5 ? i : sub[i];  // count == modelPoints: the kernel runs on all points
+#pragma unroll
+      for (int k = 0; k < 3; k++) pws[3 * i + k] = o.pts3[3 * j + k];
+      const float2 p = o.pts2[j];
+      const float xn = (float)(((double)p.x - uc) * ifx);
+      const float yn = (float)(((double)p.y - vc) * ify);
+      us[2 * i] = (double)xn * fu + uc;
+      us[2 * i + 1] = (double)yn * fv + vc;
+    }
+    // choose_control_points
+    cws[0] = cws[1] = cws[2] = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) cws[j] += pws[3 * i + j];
+#pragma unroll
+    for (int j = 0; j < 3; j++) cws[j] /= 5;
+    double m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      double p[3];
+#pragma unroll
+      for (int j = 0; j < 3; j++) p[j] = pws[3 * i + j] - cws[j];
+#pragma unroll
+      for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 3; b++) m[3 * a + b] += p[a] * p[b];
+    }
+    double dc[3], uct[9];
+    eig_sym_small<3>(m, dc, uct);
+#pragma unroll
+    for (int i = 1; i < 4; i++) {
+      const double k = sqrt(fmax(dc[i - 1], 0.0) / 5);
+#pragma unroll
+      for (int j = 0; j < 3; j++) cws[3 * i + j] = cws[j] + k * uct[3 * (i - 1) + j];
+    }
+    // compute_barycentric_coordinates
+    double cc[9], ci[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = cws[3 * j + i] - cws[i];
+    pinv3(cc, ci);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const double* pi = &pws[3 * i];
+      double a[4];
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+        a[1 + j] = ci[3 * j] * (pi[0] - cws[0]) + ci[3 * j + 1] * (pi[1] - cws[1]) +
+                   ci[3 * j + 2] * (pi[2] - cws[2]);
+      a[0] = 1.0f - a[1] - a[2] - a[3];
+#pragma unroll
+      for (int j = 0; j < 4; j++) S.alphas[4 * i + j] = a[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 15; i++) S.pws[i] = pws[i];
+#pragma unroll
+    for (int i = 0; i < 10; i++) S.us[i] = us[i];
+#pragma unroll
+    for (int i = 0; i < 12; i++) S.cws[i] = cws[i];
+  }
+  __syncthreads();
+  // M^T M, one entry per lane and pass, points in order (compute_pose)
+  for (int e = tid; e < 144; e += 64) {
+    const int a = e / 12, b = e - 12 * a;
+    const int qa = a / 3, ca = a - 3 * qa, qb = b / 3, cb = b - 3 * qb;
+    double acc = 0;
+    for (int i = 0; i < 5; i++) {
+      const double u = S.us[2 * i], v = S.us[2 * i + 1];
+      const double aa = S.alphas[4 * i + qa], ab = S.alphas[4 * i + qb];
+      const double m1a = ca == 0 ? aa * fu : (ca == 1 ? 0.0 : aa * (uc - u));
+      const double m1b = cb == 0 ? ab * fu : (cb == 1 ? 0.0 : ab * (uc - u));
+      const double m2a = ca == 0 ? 0.0 : (ca == 1 ? aa * fv : aa * (vc - v));
+      const double m2b = cb == 0 ? 0.0 : (cb == 1 ? ab * fv : ab * (vc - v));
+      acc += m1a * m1b + m2a * m2b;
+    }
+    S.eig.A[e] = acc;
+  }
+  __syncthreads();
+  eig12_block(S.eig);
+  double* rec = o.hrec + (size_t)kHypRec * h;
+  for (int e = tid; e < 48; e += 64) rec[R_UT + e] = S.eig.ut[96 + e];
+  if (tid < 20) rec[R_AL + tid] = S.alphas[tid];
+  if (tid < 15) rec[R_PW + tid] = S.pws[tid];
+  if (tid < 10) rec[R_US + tid] = S.us[tid];
+  if (tid == 0) {
+    double L[60];
+    compute_L_6x10(S.eig.ut, L);
+#pragma unroll
+    for (int i = 0; i < 60; i++) rec[R_L + i] = L[i];
+    const double* cws = S.cws;
+    rec[R_RHO + 0] = d_dist2(cws + 0, cws + 3);
+    rec[R_RHO + 1] = d_dist2(cws + 0, cws + 6);
+    rec[R_RHO + 2] = d_dist2(cws + 0, cws + 9);
+    rec[R_RHO + 3] = d_dist2(cws + 3, cws + 6);
+    rec[R_RHO + 4] = d_dist2(cws + 3, cws + 9);
+    rec[R_RHO + 5] = d_dist2(cws + 6, cws + 9);
+  }
+}
+
+// one lane per (hypothesis, object) for beta estimate V (betas_approx_V + gauss_newton +
+// compute_R_and_t); each variant is its own launch so a wave runs one code path
+template <int V>
+__global__ __launch_bounds__(64) void k_pnp_beta(PnPObject* objs, int max_iters) {
   const int h = blockIdx.x * 64 + threadIdx.x;
   PnPObject& o = objs[blockIdx.y];
   const int n = *o.n;
   if (h >= max_iters || n < 5) return;
-  EPnPSmall e;
-  e.n = 5;
-  e.fu = o.fx;
-  e.fv = o.fy;
-  e.uc = o.cx;
-  e.vc = o.cy;
-  const double ifx = 1. / (double)o.fx, ify = 1. / (double)o.fy;
-  const int* sub = o.subsets + 5 * h;
+  const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
+  const double* rec = o.hrec + (size_t)kHypRec * h;
+  double L[60], rho[6], betas[4];
+#pragma unroll
+  for (int i = 0; i < 60; i++) L[i] = rec[R_L + i];
+#pragma unroll
+  for (int i = 0; i < 6; i++) rho[i] = rec[R_RHO + i];
+  if (V == 1)
+    betas_approx_1(L, rho, betas);
+  else if (V == 2)
+    betas_approx_2(L, rho, betas);
+  else
+    betas_approx_3(L, rho, betas);
+  gauss_newton(L, rho, betas);
+  // compute_R_and_t: ccs, pcs, solve_for_sign, estimate_R_and_t, reprojection_error
+  double ccs[12], pcs[15], pws[15], R[9], t[3];
+#pragma unroll
+  for (int i = 0; i < 12; i++) ccs[i] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double* v = rec + R_UT + 12 * (3 - i);  // ut row 11 - i
+#pragma unroll
+    for (int j = 0; j < 12; j++) ccs[j] += betas[i] * v[j];
+  }
+#pragma unroll
   for (int i = 0; i < 5; i++) {
-    const int j = n == 5 ? i : sub[i];  // count == modelPoints: the kernel runs on all points
-    for (int k = 0; k < 3; k++) e.pws[3 * i + k] = o.pts3[3 * j + k];
-    const float2 p = o.pts2[j];
-    const float xn = (float)(((double)p.x - (double)o.cx) * ifx);
-    const float yn = (float)(((double)p.y - (double)o.cy) * ify);
-    e.us[2 * i] = (double)xn * (double)o.fx + (double)o.cx;
-    e.us[2 * i + 1] = (double)yn * (double)o.fy + (double)o.cy;
+    const double* a = rec + R_AL + 4 * i;
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      pcs[3 * i + j] = a[0] * ccs[j] + a[1] * ccs[3 + j] + a[2] * ccs[6 + j] + a[3] * ccs[9 + j];
   }
-  e.choose_control_points();
-  e.compute_barycentric();
-  double mtm[144];
-  for (int i = 0; i < 144; i++) mtm[i] = 0;
+  if (pcs[2] < 0.0) {
+#pragma unroll
+    for (int i = 0; i < 15; i++) pcs[i] = -pcs[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 15; i++) pws[i] = rec[R_PW + i];
+  double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      pc0[j] += pcs[3 * i + j];
+      pw0[j] += pws[3 * i + j];
+    }
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    pc0[j] /= 5;
+    pw0[j] /= 5;
+  }
+  double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
   for (int i = 0; i < 5; i++) {
-    const double* as = &e.alphas[4 * i];
-    const double u = e.us[2 * i], v = e.us[2 * i + 1];
-    double M1[12], M2[12];
-    for (int k = 0; k < 4; k++) {
-      M1[3 * k] = as[k] * e.fu;
-      M1[3 * k + 1] = 0.0;
-      M1[3 * k + 2] = as[k] * (e.uc - u);
-      M2[3 * k] = 0.0;
-      M2[3 * k + 1] = as[k] * e.fv;
-      M2[3 * k + 2] = as[k] * (e.vc - v);
-    }
-    for (int a = 0; a < 12; a++)
-      for (int b = 0; b < 12; b++) mtm[12 * a + b] += M1[a] * M1[b] + M2[a] * M2[b];
-  }
-  double d[12], ut[144], V[144];
-  int ord[12];
-  d_jacobi_eig_sym(12, mtm, d, ut, V, ord);
-  double L[60], rho[6];
-  d_compute_L_6x10(ut, L);
-  rho[0] = d_dist2(e.cws[0], e.cws[1]);
-  rho[1] = d_dist2(e.cws[0], e.cws[2]);
-  rho[2] = d_dist2(e.cws[0], e.cws[3]);
-  rho[3] = d_dist2(e.cws[1], e.cws[2]);
-  rho[4] = d_dist2(e.cws[1], e.cws[3]);
-  rho[5] = d_dist2(e.cws[2], e.cws[3]);
-  double best_err = 0, bR[3][3], bt[3];
-  for (int which = 1; which <= 3; which++) {
-    double betas[4], R[3][3], t[3];
-    d_betas(which, L, rho, betas);
-    d_gauss_newton(L, rho, betas);
-    const double err = e.compute_R_and_t(ut, betas, R, t);
-    if (which == 1 || err < best_err) {  // rep_errors[2] < [1]; [3] < [N]
-      best_err = err;
-      for (int r = 0; r < 3; r++) {
-        for (int c = 0; c < 3; c++) bR[r][c] = R[r][c];
-        bt[r] = t[r];
-      }
+    const double* pc = &pcs[3 * i];
+    const double* pw = &pws[3 * i];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      abt[3 * j] += (pc[j] - pc0[j]) * (pw[0] - pw0[0]);
+      abt[3 * j + 1] += (pc[j] - pc0[j]) * (pw[1] - pw0[1]);
+      abt[3 * j + 2] += (pc[j] - pc0[j]) * (pw[2] - pw0[2]);
     }
   }
-  double Rf[9], rv[3];
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 3; c++) Rf[3 * r + c] = bR[r][c];
-  d_rodrigues_r2v(Rf, rv);
-  double* m = o.models + 6 * h;
-  m[0] = rv[0];
-  m[1] = rv[1];
-  m[2] = rv[2];
-  m[3] = bt[0];
-  m[4] = bt[1];
-  m[5] = bt[2];
+  procrustes_R(abt, R);
+#pragma unroll
+  for (int r = 0; r < 3; r++) t[r] = pc0[r] - d_dot3(R + 3 * r, pw0);
+  double sum2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const double* pw = &pws[3 * i];
+    const double Xc = d_dot3(R, pw) + t[0], Yc = d_dot3(R + 3, pw) + t[1];
+    const double inv_Zc = 1.0 / (d_dot3(R + 6, pw) + t[2]);
+    const double ue = uc + fu * Xc * inv_Zc, ve = vc + fv * Yc * inv_Zc;
+    const double u = rec[R_US + 2 * i], v = rec[R_US + 2 * i + 1];
+    sum2 += sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+  }
+  double* out = o.hout + (size_t)kHypOut * (3 * h + V - 1);
+  out[0] = sum2 / 5;
+#pragma unroll
+  for (int i = 0; i < 9; i++) out[1 + i] = R[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) out[10 + i] = t[i];
 }
 
 // one workgroup per (hypothesis, object): inlier count + mask (PnPRansacCallback::computeError,
@@ -589,8 +788,25 @@ __global__ __launch_bounds__(256) void k_pnp_score(PnPObject* objs, int max_iter
   PnPObject& o = objs[blockIdx.y];
   const int n = *o.n;
   if (h >= max_iters || n < 5) return;
-  const double* m = o.models + 6 * h;
-  if (threadIdx.x == 0) d_rodrigues_v2r(m, sR);
+  double* m = o.models + 6 * h;
+  if (threadIdx.x == 0) {
+    // compute_pose's choice among the three beta estimates (rep_errors[2] < [1]; [3] < [N]),
+    // then the model as PnPRansacCallback stores it (rvec via Rodrigues, tvec)
+    const double* out = o.hout + (size_t)kHypOut * 3 * h;
+    int best = 0;
+    if (out[kHypOut] < out[0]) best = 1;
+    if (out[2 * kHypOut] < out[best * kHypOut]) best = 2;
+    const double* bo = out + best * kHypOut;
+    double rv[3];
+    d_rodrigues_r2v(bo + 1, rv);
+    m[0] = rv[0];
+    m[1] = rv[1];
+    m[2] = rv[2];
+    m[3] = bo[10];
+    m[4] = bo[11];
+    m[5] = bo[12];
+    d_rodrigues_v2r(m, sR);
+  }
   __syncthreads();
   const double tx = m[3], ty = m[4], tz = m[5];
   const float thr = (float)(o.reproj * o.reproj);
@@ -662,126 +878,144 @@ __global__ void k_pnp_select(PnPObject* objs, int max_iters) {
   o.result[2] = it;
 }
 
-// one workgroup per object: EPnP refit over the best hypothesis' inliers; also emits the
-// inlier index list (ascending) used as ObjIdTest_in
-__global__ __launch_bounds__(256) void k_pnp_refit(PnPObject* objs) {
-  __shared__ double s_red[4 * 80];
-  __shared__ double s_sum[80];
-  __shared__ double s_cws[4][3], s_ci[9], s_ut[144], s_L[60], s_rho[6], s_ccs[4][3];
-  __shared__ double s_R[3][3], s_t[3], s_pc0[3], s_pw0[3], s_bestR[9], s_bestT[3], s_best;
-  __shared__ int s_w[4], s_n;
+// EPnP refit over the best hypothesis' inliers, in three steps per object:
+//   k_refit_null    inlier index list (ascending; ObjIdTest_in), control points, M^T M
+//                   (reductions over the inliers), block-wide 12x12 eigen-solve, L_6x10, rho
+//   k_refit_beta<V> lane 0: beta estimate V + Gauss-Newton -> control points in camera frame
+//   k_refit_rt      R, t and reprojection error of the three estimates (reductions over the
+//                   inliers, one Procrustes solve per wave), best estimate -> Rodrigues round trip
+// The refit is not bit-identical to the CPU checker (its sums over the inliers are reduced in a
+// different order); RANSAC's decisions (inlier sets, iteration counts) do not depend on it.
+// Record: the hypothesis-0 slot of hrec (free once the hypotheses are scored); R_AL holds cws,
+// R_PW the pseudo-inverse ci; hout slots 0..2 hold ccs of the three estimates.
+struct RefitSmem {
+  Eig12Smem eig;
+  double red[4 * 80], sum[80];
+  double cws[12], ci[9];
+  int w[4], n;
+};
+
+__device__ __forceinline__ void refit_pw(const PnPObject& o, int k, double* p) {
+  const int j = o.inliers[k];
+  p[0] = o.pts3[3 * j];
+  p[1] = o.pts3[3 * j + 1];
+  p[2] = o.pts3[3 * j + 2];
+}
+
+// solvePnPRansac converts the inliers to CV_64F before the refit, so undistortPoints keeps the
+// normalised coordinates in double here (the hypotheses round them to float)
+__device__ __forceinline__ void refit_us(const PnPObject& o, int k, double& u, double& v) {
+  const float2 q = o.pts2[o.inliers[k]];
+  const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
+  u = (((double)q.x - uc) * (1. / fu)) * fu + uc;
+  v = (((double)q.y - vc) * (1. / fv)) * fv + vc;
+}
+
+__device__ __forceinline__ void refit_alphas(const PnPObject& o, int k, const double* cws,
+                                             const double* ci, double* a) {
+  double p[3];
+  refit_pw(o, k, p);
+  for (int j = 0; j < 3; j++)
+    a[1 + j] = ci[3 * j] * (p[0] - cws[0]) + ci[3 * j + 1] * (p[1] - cws[1]) +
+               ci[3 * j + 2] * (p[2] - cws[2]);
+  a[0] = 1.0f - a[1] - a[2] - a[3];
+}
+
+__global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
+  __shared__ RefitSmem S;
   PnPObject& o = objs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int best = o.result[0];
   if (best < 0) {
-    if (tid == 0) {
-      o.result[3] = 0;
-      for (int i = 0; i < 9; i++) o.Rt[i] = (i % 4 == 0) ? 1.0 : 0.0;
-      o.Rt[9] = o.Rt[10] = o.Rt[11] = 0.0;
-    }
+    if (tid == 0) o.result[3] = 0;
     return;
   }
   const int n = *o.n;
   const unsigned long long* mask = o.masks + (size_t)best * o.mask_words;
-  // ordered inlier list
   int base = 0;
   for (int i0 = 0; i0 < n; i0 += blockDim.x) {
     const int i = i0 + tid;
     const bool in = i < n && ((mask[i >> 6] >> (i & 63)) & 1ull);
     const unsigned long long bal = __ballot(in);
-    if (lane == 0) s_w[wave] = __popcll(bal);
+    if (lane == 0) S.w[wave] = __popcll(bal);
     __syncthreads();
     int off = 0, tot = 0;
     for (int w = 0; w < 4; w++) {
-      if (w < wave) off += s_w[w];
-      tot += s_w[w];
+      if (w < wave) off += S.w[w];
+      tot += S.w[w];
     }
     if (in) o.inliers[base + off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
     base += tot;
     __syncthreads();
   }
-  if (tid == 0) s_n = base;
+  if (tid == 0) {
+    S.n = base;
+    o.result[3] = base;
+  }
   __syncthreads();
-  const int ni = s_n;
+  const int ni = S.n;
   const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
-  const double ifx = 1. / fu, ify = 1. / fv;
-  auto pw = [&](int k, double* p) {
-    const int j = o.inliers[k];
-    p[0] = o.pts3[3 * j];
-    p[1] = o.pts3[3 * j + 1];
-    p[2] = o.pts3[3 * j + 2];
-  };
-  auto usp = [&](int k, double& u, double& v) {
-    // solvePnPRansac converts the inliers to CV_64F before the refit, so undistortPoints
-    // keeps the normalised coordinates in double here (the hypotheses round them to float)
-    const float2 q = o.pts2[o.inliers[k]];
-    u = (((double)q.x - uc) * ifx) * fu + uc;
-    v = (((double)q.y - vc) * ify) * fv + vc;
-  };
   // control points: centroid, then PCA of the centred points
   {
     double v[3] = {0, 0, 0};
     for (int k = tid; k < ni; k += blockDim.x) {
       double p[3];
-      pw(k, p);
+      refit_pw(o, k, p);
       v[0] += p[0];
       v[1] += p[1];
       v[2] += p[2];
     }
-    wg_sum<3>(v, s_red, s_sum);
+    wg_sum<3>(v, S.red, S.sum);
     if (tid == 0)
-      for (int j = 0; j < 3; j++) s_cws[0][j] = s_sum[j] / ni;
+      for (int j = 0; j < 3; j++) S.cws[j] = S.sum[j] / ni;
     __syncthreads();
     double m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int k = tid; k < ni; k += blockDim.x) {
       double p[3];
-      pw(k, p);
-      for (int j = 0; j < 3; j++) p[j] -= s_cws[0][j];
+      refit_pw(o, k, p);
+      for (int j = 0; j < 3; j++) p[j] -= S.cws[j];
+#pragma unroll
       for (int a = 0; a < 3; a++)
+#pragma unroll
         for (int b = 0; b < 3; b++) m[3 * a + b] += p[a] * p[b];
     }
-    wg_sum<9>(m, s_red, s_sum);
+    wg_sum<9>(m, S.red, S.sum);
     if (tid == 0) {
-      double mm[9], dc[3], uct[9], V[9];
-      int ord[3];
-      for (int i = 0; i < 9; i++) mm[i] = s_sum[i];
-      d_jacobi_eig_sym(3, mm, dc, uct, V, ord);
+      double mm[9], dc[3], uct[9], cws[12], cc[9], ci[9];
+#pragma unroll
+      for (int i = 0; i < 9; i++) mm[i] = S.sum[i];
+      eig_sym_small<3>(mm, dc, uct);
+#pragma unroll
+      for (int j = 0; j < 3; j++) cws[j] = S.cws[j];
+#pragma unroll
       for (int i = 1; i < 4; i++) {
         const double k = sqrt(fmax(dc[i - 1], 0.0) / ni);
-        for (int j = 0; j < 3; j++) s_cws[i][j] = s_cws[0][j] + k * uct[3 * (i - 1) + j];
+#pragma unroll
+        for (int j = 0; j < 3; j++) cws[3 * i + j] = cws[j] + k * uct[3 * (i - 1) + j];
       }
-      double cc[9], U[9], w[3];
+#pragma unroll
       for (int i = 0; i < 3; i++)
-        for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = s_cws[j][i] - s_cws[0][i];
-      d_jacobi_svd(3, 3, cc, U, w, V);
-      const double wmax = fmax(w[0], fmax(w[1], w[2]));
-      for (int r = 0; r < 3; r++)
-        for (int c = 0; c < 3; c++) {
-          double s = 0;
-          for (int k = 0; k < 3; k++)
-            if (w[k] > DBL_EPSILON * wmax * 3) s += V[r * 3 + k] * U[c * 3 + k] / w[k];
-          s_ci[3 * r + c] = s;
-        }
+#pragma unroll
+        for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = cws[3 * j + i] - cws[i];
+      pinv3(cc, ci);
+#pragma unroll
+      for (int i = 0; i < 12; i++) S.cws[i] = cws[i];
+#pragma unroll
+      for (int i = 0; i < 9; i++) S.ci[i] = ci[i];
     }
     __syncthreads();
   }
-  auto alphas = [&](int k, double* a) {
-    double p[3];
-    pw(k, p);
-    for (int j = 0; j < 3; j++)
-      a[1 + j] = s_ci[3 * j] * (p[0] - s_cws[0][0]) + s_ci[3 * j + 1] * (p[1] - s_cws[0][1]) +
-                 s_ci[3 * j + 2] * (p[2] - s_cws[0][2]);
-    a[0] = 1.0f - a[1] - a[2] - a[3];
-  };
   // M^T M (upper triangle, 78 entries)
   {
     double v[78];
+#pragma unroll
     for (int i = 0; i < 78; i++) v[i] = 0;
     for (int k = tid; k < ni; k += blockDim.x) {
       double a[4], u, vv;
-      alphas(k, a);
-      usp(k, u, vv);
+      refit_alphas(o, k, S.cws, S.ci, a);
+      refit_us(o, k, u, vv);
       double M1[12], M2[12];
+#pragma unroll
       for (int q = 0; q < 4; q++) {
         M1[3 * q] = a[q] * fu;
         M1[3 * q + 1] = 0.0;
@@ -791,133 +1025,181 @@ __global__ __launch_bounds__(256) void k_pnp_refit(PnPObject* objs) {
         M2[3 * q + 2] = a[q] * (vc - vv);
       }
       int t = 0;
+#pragma unroll
       for (int r = 0; r < 12; r++)
+#pragma unroll
         for (int c = r; c < 12; c++) v[t++] += M1[r] * M1[c] + M2[r] * M2[c];
     }
-    wg_sum<78>(v, s_red, s_sum);
-    if (tid == 0) {
-      double mtm[144], d[12], V[144];
-      int ord[12];
-      int t = 0;
-      for (int r = 0; r < 12; r++)
-        for (int c = r; c < 12; c++) {
-          mtm[12 * r + c] = s_sum[t];
-          mtm[12 * c + r] = s_sum[t];
-          t++;
-        }
-      d_jacobi_eig_sym(12, mtm, d, s_ut, V, ord);
-      d_compute_L_6x10(s_ut, s_L);
-      s_rho[0] = d_dist2(s_cws[0], s_cws[1]);
-      s_rho[1] = d_dist2(s_cws[0], s_cws[2]);
-      s_rho[2] = d_dist2(s_cws[0], s_cws[3]);
-      s_rho[3] = d_dist2(s_cws[1], s_cws[2]);
-      s_rho[4] = d_dist2(s_cws[1], s_cws[3]);
-      s_rho[5] = d_dist2(s_cws[2], s_cws[3]);
+    wg_sum<78>(v, S.red, S.sum);
+    for (int e = tid; e < 144; e += blockDim.x) {
+      const int r = e / 12, c = e - 12 * r;
+      const int lo = min(r, c), hi = max(r, c);
+      S.eig.A[e] = S.sum[lo * 12 - lo * (lo - 1) / 2 + (hi - lo)];
     }
     __syncthreads();
   }
-  for (int which = 1; which <= 3; which++) {
-    if (tid == 0) {
-      double betas[4];
-      d_betas(which, s_L, s_rho, betas);
-      d_gauss_newton(s_L, s_rho, betas);
-      for (int i = 0; i < 4; i++) s_ccs[i][0] = s_ccs[i][1] = s_ccs[i][2] = 0.0f;
-      for (int i = 0; i < 4; i++) {
-        const double* v = s_ut + 12 * (11 - i);
-        for (int j = 0; j < 4; j++)
-          for (int k = 0; k < 3; k++) s_ccs[j][k] += betas[i] * v[3 * j + k];
-      }
-      // solve_for_sign uses the first point's camera depth
-      double a[4];
-      alphas(0, a);
-      const double pc2 = a[0] * s_ccs[0][2] + a[1] * s_ccs[1][2] + a[2] * s_ccs[2][2] + a[3] * s_ccs[3][2];
-      if (pc2 < 0.0)
-        for (int i = 0; i < 4; i++)
-          for (int j = 0; j < 3; j++) s_ccs[i][j] = -s_ccs[i][j];
-    }
-    __syncthreads();
-    auto pcs = [&](int k, double* pc) {
-      double a[4];
-      alphas(k, a);
-      for (int j = 0; j < 3; j++)
-        pc[j] = a[0] * s_ccs[0][j] + a[1] * s_ccs[1][j] + a[2] * s_ccs[2][j] + a[3] * s_ccs[3][j];
-    };
-    {
-      double v[6] = {0, 0, 0, 0, 0, 0};
-      for (int k = tid; k < ni; k += blockDim.x) {
-        double pc[3], p[3];
-        pcs(k, pc);
-        pw(k, p);
-        for (int j = 0; j < 3; j++) {
-          v[j] += pc[j];
-          v[3 + j] += p[j];
-        }
-      }
-      wg_sum<6>(v, s_red, s_sum);
-      if (tid == 0)
-        for (int j = 0; j < 3; j++) {
-          s_pc0[j] = s_sum[j] / ni;
-          s_pw0[j] = s_sum[3 + j] / ni;
-        }
-      __syncthreads();
-    }
-    {
-      double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (int k = tid; k < ni; k += blockDim.x) {
-        double pc[3], p[3];
-        pcs(k, pc);
-        pw(k, p);
-        for (int j = 0; j < 3; j++)
-          for (int q = 0; q < 3; q++) v[3 * j + q] += (pc[j] - s_pc0[j]) * (p[q] - s_pw0[q]);
-      }
-      wg_sum<9>(v, s_red, s_sum);
-      if (tid == 0) {
-        double abt[9], U[9], w[3], V[9];
-        for (int i = 0; i < 9; i++) abt[i] = s_sum[i];
-        d_jacobi_svd(3, 3, abt, U, w, V);
-        for (int i = 0; i < 3; i++)
-          for (int j = 0; j < 3; j++) s_R[i][j] = d_dot3(U + 3 * i, V + 3 * j);
-        const double det = s_R[0][0] * s_R[1][1] * s_R[2][2] + s_R[0][1] * s_R[1][2] * s_R[2][0] +
-                           s_R[0][2] * s_R[1][0] * s_R[2][1] - s_R[0][2] * s_R[1][1] * s_R[2][0] -
-                           s_R[0][1] * s_R[1][0] * s_R[2][2] - s_R[0][0] * s_R[1][2] * s_R[2][1];
-        if (det < 0)
-          for (int j = 0; j < 3; j++) s_R[2][j] = -s_R[2][j];
-        for (int r = 0; r < 3; r++) s_t[r] = s_pc0[r] - d_dot3(s_R[r], s_pw0);
-      }
-      __syncthreads();
-    }
-    {
-      double v[1] = {0};
-      for (int k = tid; k < ni; k += blockDim.x) {
-        double p[3], u, vv;
-        pw(k, p);
-        usp(k, u, vv);
-        const double Xc = d_dot3(s_R[0], p) + s_t[0], Yc = d_dot3(s_R[1], p) + s_t[1];
-        const double inv_Zc = 1.0 / (d_dot3(s_R[2], p) + s_t[2]);
-        const double ue = uc + fu * Xc * inv_Zc, ve = vc + fv * Yc * inv_Zc;
-        v[0] += sqrt((u - ue) * (u - ue) + (vv - ve) * (vv - ve));
-      }
-      wg_sum<1>(v, s_red, s_sum);
-      if (tid == 0) {
-        const double err = s_sum[0] / ni;
-        if (which == 1 || err < s_best) {
-          s_best = err;
-          for (int r = 0; r < 3; r++) {
-            for (int c = 0; c < 3; c++) s_bestR[3 * r + c] = s_R[r][c];
-            s_bestT[r] = s_t[r];
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
+  eig12_block(S.eig);
+  double* rec = o.hrec;
+  for (int e = tid; e < 48; e += blockDim.x) rec[R_UT + e] = S.eig.ut[96 + e];
+  if (tid < 12) rec[R_AL + tid] = S.cws[tid];
+  if (tid < 9) rec[R_PW + tid] = S.ci[tid];
   if (tid == 0) {
-    double rv[3], R[9];
-    d_rodrigues_r2v(s_bestR, rv);
-    d_rodrigues_v2r(rv, R);
-    for (int i = 0; i < 9; i++) o.Rt[i] = R[i];
-    for (int i = 0; i < 3; i++) o.Rt[9 + i] = s_bestT[i];
-    o.result[3] = ni;
+    double L[60];
+    compute_L_6x10(S.eig.ut, L);
+#pragma unroll
+    for (int i = 0; i < 60; i++) rec[R_L + i] = L[i];
+    const double* cws = S.cws;
+    rec[R_RHO + 0] = d_dist2(cws + 0, cws + 3);
+    rec[R_RHO + 1] = d_dist2(cws + 0, cws + 6);
+    rec[R_RHO + 2] = d_dist2(cws + 0, cws + 9);
+    rec[R_RHO + 3] = d_dist2(cws + 3, cws + 6);
+    rec[R_RHO + 4] = d_dist2(cws + 3, cws + 9);
+    rec[R_RHO + 5] = d_dist2(cws + 6, cws + 9);
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(64) void k_refit_beta(PnPObject* objs) {
+  PnPObject& o = objs[blockIdx.x];
+  if (threadIdx.x != 0 || o.result[0] < 0) return;
+  const double* rec = o.hrec;
+  double L[60], rho[6], betas[4], ccs[12];
+#pragma unroll
+  for (int i = 0; i < 60; i++) L[i] = rec[R_L + i];
+#pragma unroll
+  for (int i = 0; i < 6; i++) rho[i] = rec[R_RHO + i];
+  if (V == 1)
+    betas_approx_1(L, rho, betas);
+  else if (V == 2)
+    betas_approx_2(L, rho, betas);
+  else
+    betas_approx_3(L, rho, betas);
+  gauss_newton(L, rho, betas);
+#pragma unroll
+  for (int i = 0; i < 12; i++) ccs[i] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double* v = rec + R_UT + 12 * (3 - i);  // ut row 11 - i
+#pragma unroll
+    for (int j = 0; j < 12; j++) ccs[j] += betas[i] * v[j];
+  }
+  // solve_for_sign on the first inlier's camera depth
+  double a[4];
+  refit_alphas(o, 0, rec + R_AL, rec + R_PW, a);
+  const double pc2 = a[0] * ccs[2] + a[1] * ccs[5] + a[2] * ccs[8] + a[3] * ccs[11];
+  double* out = o.hout + (size_t)kHypOut * (V - 1);
+#pragma unroll
+  for (int i = 0; i < 12; i++) out[i] = pc2 < 0.0 ? -ccs[i] : ccs[i];
+}
+
+struct RefitRtSmem {
+  double red[4 * 40], sum[40];
+  double ccs[36], cws[12], ci[9], pc0[9], pw0[3], R[27], t[9];
+};
+
+__global__ __launch_bounds__(256) void k_refit_rt(PnPObject* objs) {
+  __shared__ RefitRtSmem S;
+  PnPObject& o = objs[blockIdx.x];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (o.result[0] < 0) {
+    if (tid == 0) {
+      for (int i = 0; i < 9; i++) o.Rt[i] = (i % 4 == 0) ? 1.0 : 0.0;
+      o.Rt[9] = o.Rt[10] = o.Rt[11] = 0.0;
+    }
+    return;
+  }
+  const int ni = o.result[3];
+  for (int i = tid; i < 36; i += blockDim.x) S.ccs[i] = o.hout[(size_t)kHypOut * (i / 12) + i % 12];
+  if (tid < 12) S.cws[tid] = o.hrec[R_AL + tid];
+  if (tid < 9) S.ci[tid] = o.hrec[R_PW + tid];
+  __syncthreads();
+  const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
+  auto pcs = [&](int k, int var, double* pc) {
+    double a[4];
+    refit_alphas(o, k, S.cws, S.ci, a);
+    const double* c = S.ccs + 12 * var;
+    for (int j = 0; j < 3; j++) pc[j] = a[0] * c[j] + a[1] * c[3 + j] + a[2] * c[6 + j] + a[3] * c[9 + j];
+  };
+  {  // centroids of the three camera-frame point sets and of the world points
+    double v[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) v[i] = 0;
+    for (int k = tid; k < ni; k += blockDim.x) {
+      double p[3];
+      refit_pw(o, k, p);
+#pragma unroll
+      for (int var = 0; var < 3; var++) {
+        double pc[3];
+        pcs(k, var, pc);
+#pragma unroll
+        for (int j = 0; j < 3; j++) v[3 * var + j] += pc[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 3; j++) v[9 + j] += p[j];
+    }
+    wg_sum<12>(v, S.red, S.sum);
+    if (tid < 9) S.pc0[tid] = S.sum[tid] / ni;
+    if (tid < 3) S.pw0[tid] = S.sum[9 + tid] / ni;
+    __syncthreads();
+  }
+  {  // cross-covariances, then one Procrustes solve per wave
+    double v[27];
+#pragma unroll
+    for (int i = 0; i < 27; i++) v[i] = 0;
+    for (int k = tid; k < ni; k += blockDim.x) {
+      double p[3];
+      refit_pw(o, k, p);
+#pragma unroll
+      for (int var = 0; var < 3; var++) {
+        double pc[3];
+        pcs(k, var, pc);
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+          for (int q = 0; q < 3; q++)
+            v[9 * var + 3 * j + q] += (pc[j] - S.pc0[3 * var + j]) * (p[q] - S.pw0[q]);
+      }
+    }
+    wg_sum<27>(v, S.red, S.sum);
+    if (lane == 0 && wave < 3) {
+      double abt[9], R[9];
+#pragma unroll
+      for (int i = 0; i < 9; i++) abt[i] = S.sum[9 * wave + i];
+      procrustes_R(abt, R);
+#pragma unroll
+      for (int i = 0; i < 9; i++) S.R[9 * wave + i] = R[i];
+#pragma unroll
+      for (int r = 0; r < 3; r++) S.t[3 * wave + r] = S.pc0[3 * wave + r] - d_dot3(R + 3 * r, S.pw0);
+    }
+    __syncthreads();
+  }
+  {  // reprojection errors, best estimate
+    double v[3] = {0, 0, 0};
+    for (int k = tid; k < ni; k += blockDim.x) {
+      double p[3], u, vv;
+      refit_pw(o, k, p);
+      refit_us(o, k, u, vv);
+#pragma unroll
+      for (int var = 0; var < 3; var++) {
+        const double* R = S.R + 9 * var;
+        const double* t = S.t + 3 * var;
+        const double Xc = d_dot3(R, p) + t[0], Yc = d_dot3(R + 3, p) + t[1];
+        const double inv_Zc = 1.0 / (d_dot3(R + 6, p) + t[2]);
+        const double ue = uc + fu * Xc * inv_Zc, ve = vc + fv * Yc * inv_Zc;
+        v[var] += sqrt((u - ue) * (u - ue) + (vv - ve) * (vv - ve));
+      }
+    }
+    wg_sum<3>(v, S.red, S.sum);
+    if (tid == 0) {
+      int best = 0;
+      if (S.sum[1] / ni < S.sum[0] / ni) best = 1;
+      if (S.sum[2] / ni < S.sum[best] / ni) best = 2;
+      double rv[3], R[9];
+      d_rodrigues_r2v(S.R + 9 * best, rv);
+      d_rodrigues_v2r(rv, R);
+      for (int i = 0; i < 9; i++) o.Rt[i] = R[i];
+      for (int i = 0; i < 3; i++) o.Rt[9 + i] = S.t[3 * best + i];
+    }
   }
 }
 
@@ -972,10 +1254,18 @@ __global__ __launch_bounds__(256) void k_pnp_subset(PnPObject* objs) {
 
 void launch_pnp(PnPObject* d_objs, int nobj, int max_iters, hipStream_t st, bool gather) {
   if (gather) hipLaunchKernelGGL(k_pnp_gather, dim3(nobj), dim3(256), 0, st, d_objs);
-  hipLaunchKernelGGL(k_pnp_hyp, dim3((max_iters + 63) / 64, nobj), dim3(64), 0, st, d_objs, max_iters);
+  hipLaunchKernelGGL(k_pnp_hyp, dim3(max_iters, nobj), dim3(64), 0, st, d_objs, max_iters);
+  const dim3 gb((max_iters + 63) / 64, nobj);
+  hipLaunchKernelGGL(k_pnp_beta<1>, gb, dim3(64), 0, st, d_objs, max_iters);
+  hipLaunchKernelGGL(k_pnp_beta<2>, gb, dim3(64), 0, st, d_objs, max_iters);
+  hipLaunchKernelGGL(k_pnp_beta<3>, gb, dim3(64), 0, st, d_objs, max_iters);
   hipLaunchKernelGGL(k_pnp_score, dim3(max_iters, nobj), dim3(256), 0, st, d_objs, max_iters);
   hipLaunchKernelGGL(k_pnp_select, dim3(nobj), dim3(64), 0, st, d_objs, max_iters);
-  hipLaunchKernelGGL(k_pnp_refit, dim3(nobj), dim3(256), 0, st, d_objs);
+  hipLaunchKernelGGL(k_refit_null, dim3(nobj), dim3(256), 0, st, d_objs);
+  hipLaunchKernelGGL(k_refit_beta<1>, dim3(nobj), dim3(64), 0, st, d_objs);
+  hipLaunchKernelGGL(k_refit_beta<2>, dim3(nobj), dim3(64), 0, st, d_objs);
+  hipLaunchKernelGGL(k_refit_beta<3>, dim3(nobj), dim3(64), 0, st, d_objs);
+  hipLaunchKernelGGL(k_refit_rt, dim3(nobj), dim3(256), 0, st, d_objs);
   hipLaunchKernelGGL(k_mm_inliers, dim3(nobj), dim3(256), 0, st, d_objs);
 }
 

@@ -42,6 +42,9 @@ class Tracker {
                    const int32_t* d_mask, size_t mask_pitch, int nframes,
                    std::vector<FrameOut>& outs, hipStream_t st);
   int max_chunk() const { return max_chunk_; }
+  // HIP events around the batched ORB launch sequence of every chunk (on the launch stream)
+  void set_profiling(bool on);
+  void read_profile(double* orb_ms, long long* orb_launches, long long* orb_frames, bool reset);
   // last chunk's ORB output (device) for probes
   const mmt_kp* kps() const { return d_kps_; }
   const int* nkp() const { return d_nkp_; }
@@ -69,6 +72,8 @@ class Tracker {
     float2* pts2;
     int* subsets;
     double* models;
+    double* hrec;
+    double* hout;
     int* good;
     unsigned long long* masks;
     int* inliers;
@@ -112,6 +117,10 @@ class Tracker {
   PnPObject* d_pnp_ = nullptr;
   PnPBuf pnp_[kMaxObj];
   std::vector<int> h_subsets_;
+  bool prof_ = false;
+  hipEvent_t ev_orb_[2] = {nullptr, nullptr};
+  double orb_ms_ = 0;
+  long long orb_launches_ = 0, orb_frames_ = 0;
 };
 
 }  // namespace mmt

@@ -131,6 +131,27 @@ static T* dalloc(size_t n) {
 
 Tracker::~Tracker() {
   for (void* p : allocs_) (void)hipFree(p);
+  for (hipEvent_t& e : ev_orb_)
+    if (e) (void)hipEventDestroy(e);
+}
+
+void Tracker::set_profiling(bool on) {
+  if (on && !ev_orb_[0]) {
+    MMT_HIP(hipEventCreate(&ev_orb_[0]));
+    MMT_HIP(hipEventCreate(&ev_orb_[1]));
+  }
+  prof_ = on;
+}
+
+void Tracker::read_profile(double* orb_ms, long long* orb_launches, long long* orb_frames,
+                           bool reset) {
+  *orb_ms = orb_ms_;
+  *orb_launches = orb_launches_;
+  *orb_frames = orb_frames_;
+  if (reset) {
+    orb_ms_ = 0;
+    orb_launches_ = orb_frames_ = 0;
+  }
 }
 
 template <typename T>
@@ -202,6 +223,8 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     b.pts2 = alloc<float2>(ocap_);
     b.subsets = alloc<int>(5 * kRansacIters);
     b.models = alloc<double>(6 * kRansacIters);
+    b.hrec = alloc<double>((size_t)kHypRec * kRansacIters);
+    b.hout = alloc<double>((size_t)3 * kHypOut * kRansacIters);
     b.good = alloc<int>(kRansacIters);
     b.masks = alloc<unsigned long long>((size_t)kRansacIters * mask_words_);
     b.inliers = alloc<int>(ocap_);
@@ -236,10 +259,19 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   // ---- per-frame preparation and batched ORB extraction for the whole chunk
   launch_gray_depth(d_bgr, bgr_pitch, d_disp, disp_pitch / sizeof(uint16_t), d_gray_, npix,
                     d_depth_, npix, (int)npix, nframes, cfg_.bf, st);
+  if (prof_) MMT_HIP(hipEventRecord(ev_orb_[0], st));
   engine_->run(d_gray_, nframes, npix, d_kps_, d_desc_, kcap_, d_nkp_, st);
+  if (prof_) MMT_HIP(hipEventRecord(ev_orb_[1], st));
   std::vector<int> nkp(nframes);
   MMT_HIP(hipMemcpyAsync(nkp.data(), d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
+  if (prof_) {
+    float ms = 0;
+    MMT_HIP(hipEventElapsedTime(&ms, ev_orb_[0], ev_orb_[1]));
+    orb_ms_ += ms;
+    orb_launches_ += 1;
+    orb_frames_ += nframes;
+  }
   outs.assign(nframes, FrameOut());
   for (int f = 0; f < nframes; f++) {
     FrameArgs a;
@@ -463,6 +495,8 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, Fram
     o.pts3 = b.pts3;
     o.pts2 = b.pts2;
     o.models = b.models;
+    o.hrec = b.hrec;
+    o.hout = b.hout;
     o.good = b.good;
     o.masks = b.masks;
     o.mask_words = mask_words_;

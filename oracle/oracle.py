@@ -178,8 +178,8 @@ class Tracker:
         self._h = L.oracle_tracker_create(w, h, K[0], K[1], K[2], K[3], bf, seed, nfeatures)
 
     def __del__(self):
-        if getattr(self, "_h", None):
-            lib().oracle_tracker_destroy(self._h)
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.oracle_tracker_destroy(self._h)
             self._h = None
 
     def track(self, bgr, disp, flow, mask):

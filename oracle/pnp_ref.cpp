@@ -27,10 +27,14 @@ static void jacobi_eig_sym(int n, const double* Ain, double* d, double* vt) {
   std::vector<double> A(Ain, Ain + n * n), V(n * n, 0.0);
   for (int i = 0; i < n; i++) V[i * n + i] = 1.0;
   for (int sweep = 0; sweep < 100; sweep++) {
-    double off = 0;
-    for (int p = 0; p < n; p++)
+    // converged when the off-diagonal mass is below (1e-13)^2 of the diagonal's: rotations leave
+    // residues of order eps * |a_pp| behind, so an absolute threshold is never reached
+    double off = 0, dsum = 0;
+    for (int p = 0; p < n; p++) {
+      dsum += A[p * n + p] * A[p * n + p];
       for (int q = p + 1; q < n; q++) off += A[p * n + q] * A[p * n + q];
-    if (off < 1e-300) break;
+    }
+    if (off <= 1e-26 * dsum) break;
     for (int p = 0; p < n; p++)
       for (int q = p + 1; q < n; q++) {
         const double apq = A[p * n + q];
@@ -62,6 +66,81 @@ static void jacobi_eig_sym(int n, const double* Ain, double* d, double* vt) {
   for (int r = 0; r < n; r++) {
     d[r] = A[ord[r] * n + ord[r]];
     for (int k = 0; k < n; k++) vt[r * n + k] = V[k * n + ord[r]];
+  }
+}
+
+// 12x12 symmetric eigen-decomposition for EPnP's M^T M by PARALLEL-ORDER Jacobi: each sweep is
+// 11 rounds of 6 disjoint (p, q) pairs (round-robin schedule, player 11 fixed); all six rotations
+// of a round take their angle from the matrix at the start of the round and are applied as
+// B = A J (columns), then A' = J^T B (rows), V' = V J.  This is the same Jacobi method as above
+// with an ordering the GPU executes one round per step (mmt_pnp.hip: eig12_block); both follow
+// this loop operation for operation.  Eigenvectors as rows of `vt`, descending eigenvalues.
+static inline void rr_partner(int r, int j, int& p, int& q) {
+  const int k = j == 11 ? r : (j == r ? 11 : (2 * r - j + 22) % 11);
+  p = std::min(j, k);
+  q = std::max(j, k);
+}
+
+static void jacobi_eig12_rr(const double* Ain, double* d, double* vt) {
+  const int n = 12;
+  double A[144], B[144], V[144], V2[144], c[12], s[12];
+  memcpy(A, Ain, sizeof(A));
+  for (int i = 0; i < 144; i++) V[i] = (i % 13 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 100; sweep++) {
+    // converged when the off-diagonal mass is below (1e-13)^2 of the diagonal's: rotations leave
+    // residues of order eps * |a_pp| behind, so an absolute threshold is never reached
+    double off = 0, dsum = 0;
+    for (int p = 0; p < n; p++) {
+      dsum += A[p * n + p] * A[p * n + p];
+      for (int q = p + 1; q < n; q++) off += A[p * n + q] * A[p * n + q];
+    }
+    if (off <= 1e-26 * dsum) break;
+    for (int r = 0; r < 11; r++) {
+      for (int slot = 0; slot < 6; slot++) {
+        const int a = slot == 0 ? r : (r + slot) % 11, b = slot == 0 ? 11 : (r - slot + 11) % 11;
+        const int p = std::min(a, b), q = std::max(a, b);
+        const double apq = A[p * n + q];
+        if (std::fabs(apq) < 1e-300) {
+          c[p] = 1.0;
+          s[p] = 0.0;
+          continue;
+        }
+        const double app = A[p * n + p], aqq = A[q * n + q];
+        const double theta = (aqq - app) / (2 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1));
+        c[p] = 1 / std::sqrt(t * t + 1);
+        s[p] = t * c[p];
+      }
+      for (int k = 0; k < n; k++)
+        for (int j = 0; j < n; j++) {
+          int p, q;
+          rr_partner(r, j, p, q);
+          const double cc = c[p], ss = s[p];
+          if (j == p) {
+            B[k * n + j] = cc * A[k * n + p] - ss * A[k * n + q];
+            V2[k * n + j] = cc * V[k * n + p] - ss * V[k * n + q];
+          } else {
+            B[k * n + j] = ss * A[k * n + p] + cc * A[k * n + q];
+            V2[k * n + j] = ss * V[k * n + p] + cc * V[k * n + q];
+          }
+        }
+      for (int i = 0; i < n; i++)
+        for (int k = 0; k < n; k++) {
+          int p, q;
+          rr_partner(r, i, p, q);
+          const double cc = c[p], ss = s[p];
+          A[i * n + k] = i == p ? cc * B[p * n + k] - ss * B[q * n + k]
+                                : ss * B[p * n + k] + cc * B[q * n + k];
+        }
+      memcpy(V, V2, sizeof(V));
+    }
+  }
+  for (int i = 0; i < n; i++) {  // stable descending order
+    int rank = 0;
+    for (int j = 0; j < n; j++)
+      rank += (A[j * 13] > A[i * 13]) || (j < i && A[j * 13] == A[i * 13]);
+    d[rank] = A[i * 13];
+    for (int k = 0; k < n; k++) vt[rank * n + k] = V[k * n + i];
   }
 }
 
@@ -455,7 +534,7 @@ struct EPnP {
         for (int b = 0; b < 12; b++) mtm[12 * a + b] += M1[a] * M1[b] + M2[a] * M2[b];
     }
     double d[12], ut[144];
-    jacobi_eig_sym(12, mtm, d, ut);
+    jacobi_eig12_rr(mtm, d, ut);
     double L[60], rho[6];
     compute_L_6x10(ut, L);
     compute_rho(rho);

@@ -115,3 +115,37 @@ def test_track_static_scene_without_objects(ctx, oracle_mod, kitti_frames):
         g = ctx.track(f["bgr"], f["disp"], f["flow"], z)
         _compare_frame(g, o, i)
         assert g["objects"] == []
+
+
+def _synthetic_parity(w, h, nfeat, nobj, nframes, seed):
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    from oracle import oracle as O
+    frames = scene.to_numpy_frames(scene.kitti_like_sequence(nframes, w, h, n_objects=nobj,
+                                                             seed=seed))
+    c = M.Context(M.kitti03_config(w, h, nfeat, max_batch=4))
+    tr = O.Tracker(w, h, K_KITTI, 387.5744, 0, nfeat)
+    n_obj = 0
+    try:
+        for i, f in enumerate(frames):
+            o = tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            g = c.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            _compare_frame(g, o, i)
+            n_obj = max(n_obj, len(g["objects"]))
+    finally:
+        c.close()
+    return n_obj
+
+
+def test_track_synthetic_c3_matches_oracle(oracle_mod):
+    """BASELINE C3 geometry: ego + 3 moving boxes, 2000 features."""
+    assert _synthetic_parity(1242, 375, 2000, 3, 8, 1003) == 3
+
+
+def test_track_synthetic_c2_ego_only_matches_oracle(oracle_mod):
+    assert _synthetic_parity(1242, 375, 2000, 0, 5, 1005) == 0
+
+
+def test_track_synthetic_c5_1080p_matches_oracle(oracle_mod):
+    """BASELINE C5 geometry: 1920x1080, 8000 features, 8 moving boxes."""
+    assert _synthetic_parity(1920, 1080, 8000, 8, 4, 2000) >= 4
