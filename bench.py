@@ -68,11 +68,9 @@ def main():
     import torch
     import torch.distributed as dist
     import multimot_track_amd as M
-    from multimot_track_amd import scene
+    from multimot_track_amd import scene, shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = shard.rank_env()
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
@@ -80,7 +78,7 @@ def main():
 
     W, H, NF, C = args.width, args.height, args.nfeatures, args.chunk
     nframes = (args.warmup + args.steps) * C
-    seed = 1003 + rank
+    seed = shard.sequence_seed(1003, rank)
     t_gen = time.perf_counter()
     seq = scene.kitti_like_sequence(nframes, W, H, n_objects=args.objects, seed=seed, device=dev)
     torch.cuda.synchronize(dev)
@@ -104,21 +102,15 @@ def main():
     torch.cuda.synchronize(dev)
     ctx.profile_enable(True)
     ctx.profile_read(reset=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    shard.barrier(world, dev)
     t0 = time.perf_counter()
     results = [step(args.warmup + i) for i in range(args.steps)]
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    shard.barrier(world, dev)
     elapsed = time.perf_counter() - t0
     prof = ctx.profile_read()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(elapsed, world, dev)
+    frames_all = shard.sum_over_ranks(args.steps * C, world, dev)
 
     # per-frame outputs of the timed region (sanity: every frame tracked, objects found)
     res, objs = results[-1]
@@ -128,8 +120,7 @@ def main():
     ego_err = float(np.abs(np.array(res[C - 1].Tcw[:]).reshape(4, 4) - gt).max())
 
     if rank == 0:
-        frames_total = args.steps * C * world
-        value = frames_total / elapsed
+        value = frames_all / elapsed
         launch_ms = prof["orb_ms"] / max(prof["orb_launches"], 1)
         bytes_per_launch = C * b_orb(W, H, NF, lv["level_w"], lv["level_h"])
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9

@@ -359,7 +359,7 @@ int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* pr, float* pose_ou
     d.stats = st.p;
     MMT_HIP(hipMemcpyAsync(dd.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
     MMT_HIP(hipMemcpyAsync(pose.p, pr->init, 64, hipMemcpyHostToDevice, s));
-    mmt::launch_flow_lm(dd.p, 1, s);
+    mmt::launch_flow_lm(dd.p, 1, n, s);
     MMT_HIP(hipMemcpyAsync(pose_out, pose.p, 64, hipMemcpyDeviceToHost, s));
     MMT_HIP(hipMemcpyAsync(stats_out, st.p, 12, hipMemcpyDeviceToHost, s));
     MMT_HIP(hipStreamSynchronize(s));

@@ -19,11 +19,12 @@ __device__ __forceinline__ void dq_normalize_rot(DQuat& q) {
   if (q.w < 0) {
     q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w;
   }
-  const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
-  q.x /= n; q.y /= n; q.z /= n; q.w /= n;
+  const double in = 1.0 / sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  q.x *= in; q.y *= in; q.z *= in; q.w *= in;
 }
 
-// Eigen::Quaternion(const Matrix3&): trace branch, else largest-diagonal branch.
+// Eigen::Quaternion(const Matrix3&): trace branch, else largest-diagonal branch (the three
+// (i, j, k) cases written out so nothing is indexed at run time).
 __device__ inline DQuat dq_from_R(const double R[3][3]) {
   DQuat q;
   const double t = R[0][0] + R[1][1] + R[2][2];
@@ -37,16 +38,29 @@ __device__ inline DQuat dq_from_R(const double R[3][3]) {
   } else {
     int i = 0;
     if (R[1][1] > R[0][0]) i = 1;
-    if (R[2][2] > R[i][i]) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    double s = sqrt(R[i][i] - R[j][j] - R[k][k] + 1.0);
-    double v[3];
-    v[i] = 0.5 * s;
-    s = 0.5 / s;
-    q.w = (R[k][j] - R[j][k]) * s;
-    v[j] = (R[j][i] + R[i][j]) * s;
-    v[k] = (R[k][i] + R[i][k]) * s;
-    q.x = v[0]; q.y = v[1]; q.z = v[2];
+    if (R[2][2] > (i == 0 ? R[0][0] : R[1][1])) i = 2;
+    if (i == 0) {  // j = 1, k = 2
+      double s = sqrt(R[0][0] - R[1][1] - R[2][2] + 1.0);
+      q.x = 0.5 * s;
+      s = 0.5 / s;
+      q.w = (R[2][1] - R[1][2]) * s;
+      q.y = (R[1][0] + R[0][1]) * s;
+      q.z = (R[2][0] + R[0][2]) * s;
+    } else if (i == 1) {  // j = 2, k = 0
+      double s = sqrt(R[1][1] - R[2][2] - R[0][0] + 1.0);
+      q.y = 0.5 * s;
+      s = 0.5 / s;
+      q.w = (R[0][2] - R[2][0]) * s;
+      q.z = (R[2][1] + R[1][2]) * s;
+      q.x = (R[0][1] + R[1][0]) * s;
+    } else {  // j = 0, k = 1
+      double s = sqrt(R[2][2] - R[0][0] - R[1][1] + 1.0);
+      q.z = 0.5 * s;
+      s = 0.5 / s;
+      q.w = (R[1][0] - R[0][1]) * s;
+      q.x = (R[0][2] + R[2][0]) * s;
+      q.y = (R[1][2] + R[2][1]) * s;
+    }
   }
   return q;
 }
@@ -83,7 +97,9 @@ __device__ __forceinline__ DQuat dq_mul(const DQuat& a, const DQuat& b) {
 
 __device__ inline DSE3 dse3_from_float(const float* T) {  // Converter::toSE3Quat
   double R[3][3];
+#pragma unroll
   for (int r = 0; r < 3; r++)
+#pragma unroll
     for (int c = 0; c < 3; c++) R[r][c] = (double)T[4 * r + c];
   DSE3 s;
   s.q = dq_from_R(R);
@@ -95,7 +111,9 @@ __device__ inline DSE3 dse3_from_float(const float* T) {  // Converter::toSE3Qua
 __device__ inline void dse3_to_float(const DSE3& s, float* T) {  // Converter::toCvMat
   double R[3][3];
   dq_to_R(s.q, R);
+#pragma unroll
   for (int r = 0; r < 3; r++) {
+#pragma unroll
     for (int c = 0; c < 3; c++) T[4 * r + c] = (float)R[r][c];
     T[4 * r + 3] = (float)s.t[r];
   }
@@ -107,19 +125,27 @@ __device__ inline DSE3 dse3_exp(const double u[6]) {  // SE3Quat::exp
   const double theta = sqrt(o0 * o0 + o1 * o1 + o2 * o2);
   const double O[3][3] = {{0, -o2, o1}, {o2, 0, -o0}, {-o1, o0, 0}};
   double O2[3][3];
+#pragma unroll
   for (int r = 0; r < 3; r++)
+#pragma unroll
     for (int c = 0; c < 3; c++) O2[r][c] = O[r][0] * O[0][c] + O[r][1] * O[1][c] + O[r][2] * O[2][c];
   double R[3][3], V[3][3];
   if (theta < 0.00001) {
+#pragma unroll
     for (int r = 0; r < 3; r++)
+#pragma unroll
       for (int c = 0; c < 3; c++) {
         R[r][c] = (r == c ? 1.0 : 0.0) + O[r][c] + O2[r][c];
         V[r][c] = R[r][c];
       }
   } else {
-    const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-    const double c2 = (theta - sin(theta)) / (theta * theta * theta);
+    double st, ct;
+    sincos(theta, &st, &ct);
+    const double a = st / theta, b = (1 - ct) / (theta * theta);
+    const double c2 = (theta - st) / (theta * theta * theta);
+#pragma unroll
     for (int r = 0; r < 3; r++)
+#pragma unroll
       for (int c = 0; c < 3; c++) {
         R[r][c] = (r == c ? 1.0 : 0.0) + a * O[r][c] + b * O2[r][c];
         V[r][c] = (r == c ? 1.0 : 0.0) + b * O[r][c] + c2 * O2[r][c];
@@ -127,6 +153,7 @@ __device__ inline DSE3 dse3_exp(const double u[6]) {  // SE3Quat::exp
   }
   DSE3 s;
   s.q = dq_from_R(R);
+#pragma unroll
   for (int r = 0; r < 3; r++) s.t[r] = V[r][0] * u[3] + V[r][1] * u[4] + V[r][2] * u[5];
   dq_normalize_rot(s.q);
   return s;
@@ -144,45 +171,64 @@ __device__ inline DSE3 dse3_mul(const DSE3& a, const DSE3& b) {
   return r;
 }
 
-// 6x6 LDLT with symmetric diagonal pivoting on the LOWER triangle (Eigen LDLT<MatrixXd>).
-// Returns false when not positive (LDLT::isPositive()).
-__device__ inline bool ldlt_solve6(const double* Hl /*row-major 6x6, lower used*/, const double* b,
-                                   double* x) {
-  double A[6][6];
-  for (int r = 0; r < 6; r++)
-    for (int c = 0; c < 6; c++) A[r][c] = (c <= r) ? Hl[6 * r + c] : Hl[6 * c + r];
+// 6x6 LDLT with symmetric diagonal pivoting on the LOWER triangle (Eigen LDLT<MatrixXd>); returns
+// false when not positive (LDLT::isPositive()).  Every array index is a compile-time constant
+// (pivot swaps by predicated unrolled blocks), so the factorisation stays in registers.
+__device__ inline bool ldlt_solve6(const double (&Hl)[36], const double (&b)[6], double (&x)[6]) {
+  double A[6][6], L[6][6], D[6];
   int perm[6] = {0, 1, 2, 3, 4, 5};
-  double D[6];
-  double L[6][6];
+#pragma unroll
   for (int r = 0; r < 6; r++)
-    for (int c = 0; c < 6; c++) L[r][c] = 0.0;
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      A[r][c] = (c <= r) ? Hl[6 * r + c] : Hl[6 * c + r];
+      L[r][c] = 0.0;
+    }
   bool positive = true;
+#pragma unroll
   for (int k = 0; k < 6; k++) {
     int p = k;
     double best = fabs(A[k][k]);
+#pragma unroll
     for (int i = k + 1; i < 6; i++)
       if (fabs(A[i][i]) > best) {
         best = fabs(A[i][i]);
         p = i;
       }
-    if (p != k) {
-      for (int c = 0; c < 6; c++) {
-        const double t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t;
+#pragma unroll
+    for (int i = k + 1; i < 6; i++)
+      if (p == i) {
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          const double t = A[k][c];
+          A[k][c] = A[i][c];
+          A[i][c] = t;
+        }
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+          const double t = A[r][k];
+          A[r][k] = A[r][i];
+          A[r][i] = t;
+        }
+#pragma unroll
+        for (int c = 0; c < k; c++) {
+          const double t = L[k][c];
+          L[k][c] = L[i][c];
+          L[i][c] = t;
+        }
+        const int t = perm[k];
+        perm[k] = perm[i];
+        perm[i] = t;
       }
-      for (int r = 0; r < 6; r++) {
-        const double t = A[r][k]; A[r][k] = A[r][p]; A[r][p] = t;
-      }
-      for (int c = 0; c < k; c++) {
-        const double t = L[k][c]; L[k][c] = L[p][c]; L[p][c] = t;
-      }
-      const int t = perm[k]; perm[k] = perm[p]; perm[p] = t;
-    }
     double d = A[k][k];
+#pragma unroll
     for (int c = 0; c < k; c++) d -= L[k][c] * L[k][c] * D[c];
     D[k] = d;
     if (d < 0) positive = false;
+#pragma unroll
     for (int i = k + 1; i < 6; i++) {
       double s = A[i][k];
+#pragma unroll
       for (int c = 0; c < k; c++) s -= L[i][c] * L[k][c] * D[c];
       L[i][k] = (d != 0) ? s / d : 0.0;
     }
@@ -190,14 +236,70 @@ __device__ inline bool ldlt_solve6(const double* Hl /*row-major 6x6, lower used*
   }
   if (!positive) return false;
   double y[6];
-  for (int i = 0; i < 6; i++) y[i] = b[perm[i]];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    double v = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++)
+      if (perm[i] == j) v = b[j];
+    y[i] = v;
+  }
+#pragma unroll
   for (int i = 0; i < 6; i++)
+#pragma unroll
     for (int c = 0; c < i; c++) y[i] -= L[i][c] * y[c];
+#pragma unroll
   for (int i = 0; i < 6; i++) y[i] = (D[i] != 0) ? y[i] / D[i] : 0.0;
+#pragma unroll
   for (int i = 5; i >= 0; i--)
+#pragma unroll
     for (int r = i + 1; r < 6; r++) y[i] -= L[r][i] * y[r];
-  for (int i = 0; i < 6; i++) x[perm[i]] = y[i];
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
+    for (int j = 0; j < 6; j++)
+      if (perm[i] == j) x[j] = y[i];
   return true;
+}
+
+// Block sum of K <= 32 doubles held per thread (blockDim a multiple of 64): a butterfly
+// reduce-scatter inside each wave (32 shuffles instead of 6 per value), then one LDS pass across
+// waves.  `red` holds 32 doubles per wave; the sums land in out[0..K) (LDS), visible to every
+// thread on return.
+template <int K>
+__device__ inline void block_sum(const double (&v)[K], double* red, double* out) {
+  static_assert(K <= 32, "block_sum: at most 32 values");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  double a[16];
+  {
+    const bool hi = lane & 32;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const double x0 = j < K ? v[j] : 0.0, x1 = (16 + j) < K ? v[16 + j] : 0.0;
+      a[j] = (hi ? x1 : x0) + __shfl_xor(hi ? x0 : x1, 32, 64);
+    }
+  }
+#pragma unroll
+  for (int h = 8, bit = 16; h >= 1; h >>= 1, bit >>= 1) {
+    const bool hi = lane & bit;
+#pragma unroll
+    for (int j = 0; j < h; j++) a[j] = (hi ? a[h + j] : a[j]) + __shfl_xor(hi ? a[j] : a[h + j], bit, 64);
+  }
+  a[0] += __shfl_xor(a[0], 1, 64);
+  const int idx = lane >> 1;  // value index this lane pair holds
+  if (nw == 1) {
+    if (!(lane & 1) && idx < K) out[idx] = a[0];
+    __syncthreads();
+    return;
+  }
+  if (!(lane & 1) && idx < K) red[wave * 32 + idx] = a[0];
+  __syncthreads();
+  if (threadIdx.x < K) {
+    double s = 0;
+    for (int w = 0; w < nw; w++) s += red[w * 32 + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
 }
 
 // Workgroup sum of K doubles held per thread; result broadcast in `out` (LDS, K entries).

@@ -1,0 +1,592 @@
+// multimot_track_amd/csrc/mmt_lm.hip -- D2 / D3: the flow-refined pose solves.
+//
+// Optimizer::PoseOptimizationFlow2Cam (ego, reference src/Optimizer.cc:396-601) and
+// Optimizer::PoseOptimizationFlow2 (objects, Optimizer.cc:2170-2377): one SE(3) vertex plus one
+// 2-D "flow" vertex per correspondence, EdgeFlowCamera/EdgeFlowObj (Huber, information 0.1) and a
+// flow prior per correspondence, solved by g2o's Levenberg-Marquardt with the Schur complement over
+// the flow vertices.  The g2o behaviour reproduced here (CPU restatement in
+// oracle/solve_ref.cpp): LM damping init 1e-5 * max diagonal, rho/alpha update with the 1e-3 scale
+// term, ni doubling, 10 trials, stale-x update when the LDLT fails, "Raul" stop after three
+// iterations with under 0.1 % gain, the chi2-increase stop on the last trial's chi2, the landmark
+// back-substitution with the stride-2 spill term, inliers from the last evaluated errors.
+//
+// One workgroup per solve (ego + every object of a frame in one launch), fp64.  Per-correspondence
+// state lives in registers (IR items per thread; items beyond IR * blockDim spill to the global
+// scratch arrays).  Each LM trial is two passes over the correspondences:
+//   Schur pass   J^T W J terms of the Schur complement (27 sums)
+//   update pass  flow back-substitution, the trial's errors and chi2, and -- speculatively -- the
+//                linearisation at the trial state (H, b: 29 sums); accepted trials hand it to the
+//                next iteration, so no separate linearisation pass is needed
+// and one lane solves the 6x6 system in between.  Reductions are butterfly reduce-scatters
+// (mmt_devmath.h: block_sum).  Sums are reduced in a different order than the CPU checker's
+// sequential loops, so poses agree to rounding (1e-4 bar), not bit for bit.
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdio>
+#include <cstdlib>
+
+#include <algorithm>
+
+#include "mmt_devmath.h"
+#include "mmt_internal.h"
+#include "mmt_track.h"
+
+namespace mmt {
+
+namespace {
+
+constexpr double kInfo = 0.1;  // info_flow (Optimizer.cc:466 / 2241)
+
+struct LMItem {
+  double X[3];      // world point of the last frame's sample (Twl * unprojection)
+  double ob[2];     // measurement: last-frame pixel
+  double pr[2];     // flow prior
+  double f[2];      // flow vertex estimate
+  double xl[2];     // last flow increment (reused when the 6x6 solve fails)
+  double w, bl[2];  // robust weight, landmark gradient at the current state
+  double wn, bln[2];  // the same at the trial state
+  double e[2];      // errors of the last evaluated state
+};
+
+enum { G_X0 = 0, G_X1, G_X2, G_OB0, G_OB1, G_PR0, G_PR1, G_F0, G_F1, G_XL0, G_XL1, G_W, G_BL0,
+       G_BL1, G_WN, G_BLN0, G_BLN1, G_E0, G_E1, G_COUNT };
+
+__device__ __forceinline__ void item_load(const double* S, int cap, int i, LMItem& it) {
+  double* d = &it.X[0];
+  const double* src = S + i;
+#pragma unroll
+  for (int k = 0; k < G_COUNT; k++) d[k] = src[(size_t)k * cap];
+}
+
+__device__ __forceinline__ void item_store(double* S, int cap, int i, const LMItem& it) {
+  const double* d = &it.X[0];
+  double* dst = S + i;
+#pragma unroll
+  for (int k = 0; k < G_COUNT; k++) dst[(size_t)k * cap] = d[k];
+}
+
+static_assert(sizeof(LMItem) == G_COUNT * sizeof(double), "LMItem layout");
+
+__device__ __forceinline__ void huber(double e, double dsqr, double delta, double& r0, double& r1) {
+  if (e <= dsqr) {
+    r0 = e;
+    r1 = 1.;
+  } else {
+    const double s = sqrt(e);
+    r0 = 2 * s * delta - dsqr;
+    r1 = delta / s;
+  }
+}
+
+// projection Jacobian of EdgeFlowCamera / EdgeFlowObj (g2o's EdgeSE3ProjectXYZ form) at the
+// camera-frame point (x, y, z), written with one reciprocal of z instead of nine divisions
+__device__ __forceinline__ void jac(double x, double y, double iz, double fx, double fy,
+                                    double J[2][6]) {
+  const double iz2 = iz * iz;
+  const double xx = x * x * iz2, yy = y * y * iz2, xy = x * y * iz2;
+  J[0][0] = xy * fx;
+  J[0][1] = -(1 + xx) * fx;
+  J[0][2] = y * iz * fx;
+  J[0][3] = -iz * fx;
+  J[0][4] = 0;
+  J[0][5] = x * iz2 * fx;
+  J[1][0] = (1 + yy) * fy;
+  J[1][1] = -xy * fy;
+  J[1][2] = -x * iz * fy;
+  J[1][3] = 0;
+  J[1][4] = -iz * fy;
+  J[1][5] = y * iz2 * fy;
+}
+
+__device__ __forceinline__ void map(const DSE3& p, const double* X, double& x, double& y,
+                                    double& z) {
+  dq_rotate(p.q, X[0], X[1], X[2], x, y, z);
+  x += p.t[0];
+  y += p.t[1];
+  z += p.t[2];
+}
+
+struct Cam {
+  double fx, fy, cx, cy, pinfo, dsqr, delta;
+};
+
+// linearise at (P, flow fl): errors, chi2 term, robust weight, H/b contributions (acc[0..20] the
+// lower triangle of J^T W J, acc[21..26] J^T W (-e)), landmark gradient
+__device__ __forceinline__ void linearise(const Cam& c, const DSE3& P, const LMItem& it,
+                                          const double f0, const double f1, double* acc,
+                                          double& chi, double& e0, double& e1, double& w,
+                                          double& bl0, double& bl1, double& mh) {
+  double x, y, z;
+  map(P, it.X, x, y, z);
+  const double iz = 1.0 / z;
+  const double pu = x * iz * c.fx + c.cx, pv = y * iz * c.fy + c.cy;
+  e0 = (it.ob[0] + f0) - pu;
+  e1 = (it.ob[1] + f1) - pv;
+  const double p0 = f0 - it.pr[0], p1 = f1 - it.pr[1];
+  const double e2 = kInfo * (e0 * e0 + e1 * e1);
+  double r0, r1;
+  huber(e2, c.dsqr, c.delta, r0, r1);
+  chi += r0 + c.pinfo * (p0 * p0 + p1 * p1);
+  w = kInfo * r1;
+  double J[2][6];
+  jac(x, y, iz, c.fx, c.fy, J);
+  int k = 0;
+#pragma unroll
+  for (int a = 0; a < 6; a++)
+#pragma unroll
+    for (int b = 0; b <= a; b++) acc[k++] += J[0][a] * w * J[0][b] + J[1][a] * w * J[1][b];
+  const double o0 = -w * e0, o1 = -w * e1;
+#pragma unroll
+  for (int a = 0; a < 6; a++) acc[21 + a] += J[0][a] * o0 + J[1][a] * o1;
+  bl0 = o0 - c.pinfo * p0;
+  bl1 = o1 - c.pinfo * p1;
+  mh = fmax(mh, w + c.pinfo);
+}
+
+// Schur complement contributions of one correspondence at pose P with damping lam
+__device__ __forceinline__ void schur_terms(const Cam& c, const DSE3& P, const LMItem& it,
+                                            double lam, double ilam, double* v) {
+  double x, y, z;
+  map(P, it.X, x, y, z);
+  double J[2][6];
+  jac(x, y, 1.0 / z, c.fx, c.fy, J);
+  const double w = it.w, h = w + c.pinfo;
+  const double d00 = 1.0 / (h + lam), d01 = -h * d00 * ilam, d11 = ilam;
+  const double bl0 = it.bl[0], bl1 = it.bl[1];
+  const double db0 = d00 * bl0 + d01 * bl1, db1 = d11 * bl1;
+  int k = 0;
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+    const double B0a = w * J[0][a], B1a = w * J[1][a];
+    const double BD0 = B0a * d00, BD1 = B0a * d01 + B1a * d11;
+#pragma unroll
+    for (int b = 0; b <= a; b++) v[k++] += BD0 * (w * J[0][b]) + BD1 * (w * J[1][b]);
+    v[21 + a] += B0a * db0 + B1a * db1;
+  }
+}
+
+// back-substitution of the flow increment (when the 6x6 solve succeeded), trial errors and
+// speculative linearisation at (PN, f + xl); v[0] trial chi2, v[1] the scale term, v[2..28] H/b
+__device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const DSE3& PN,
+                                             LMItem& it, int i, bool ok2, double lam,
+                                             double ilam, const double* xb, double* v) {
+  const double bl0 = it.bl[0], bl1 = it.bl[1];
+  if (ok2) {
+    double x, y, z;
+    map(P, it.X, x, y, z);
+    double J[2][6];
+    jac(x, y, 1.0 / z, c.fx, c.fy, J);
+    const double w = it.w, h = w + c.pinfo;
+    double c0 = bl0, c1 = bl1;
+#pragma unroll
+    for (int a = 0; a < 6; a++) {
+      c0 -= w * J[0][a] * xb[a];
+      c1 -= w * J[1][a] * xb[a];
+    }
+    const double ihl = 1.0 / (h + lam);
+    double xl0 = c0 * ihl - h * c1 * ihl * ilam;
+    if (i > 0) xl0 += c0 * ilam;  // stride-2 spill of landmark i-1's third Dinv row
+    it.xl[0] = xl0;
+    it.xl[1] = c1 * ilam;
+  }
+  const double xl0 = it.xl[0], xl1 = it.xl[1];
+  const double f0 = it.f[0] + xl0, f1 = it.f[1] + xl1;
+  double mh = 0;
+  linearise(c, PN, it, f0, f1, v + 2, v[0], it.e[0], it.e[1], it.wn, it.bln[0], it.bln[1], mh);
+  v[1] += xl0 * (lam * xl0 + bl0) + xl1 * (lam * xl1 + bl1);
+}
+
+#ifdef MMT_LM_PROFILE
+#define MMT_LMPROF(k)                  \
+  do {                                 \
+    if (tid == 0) {                    \
+      const long long now = clock64(); \
+      sm.prof[k] += now - prof_t;      \
+      prof_t = now;                    \
+    }                                  \
+  } while (0)
+#else
+#define MMT_LMPROF(k) \
+  do {                \
+  } while (0)
+#endif
+
+// 6x6 LDL^T of the (symmetric positive definite) Schur complement, unpivoted, straight-line
+// code; false when a pivot is negative.  The reduced camera system H_pp + lambda I - B D^-1 B^T
+// is SPD whenever lambda > 0, so the pivoting of Eigen's LDLT only moves rounding.
+__device__ __forceinline__ bool ldlt6(const double (&H)[36], const double (&b)[6], double (&x)[6]) {
+  double L[6][6], D[6];
+  bool positive = true;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    double d = H[6 * k + k];
+#pragma unroll
+    for (int c = 0; c < k; c++) d -= L[k][c] * L[k][c] * D[c];
+    D[k] = d;
+    positive = positive && !(d < 0);
+    const double id = d != 0 ? 1.0 / d : 0.0;
+#pragma unroll
+    for (int i = k + 1; i < 6; i++) {
+      double s = H[6 * i + k];
+#pragma unroll
+      for (int c = 0; c < k; c++) s -= L[i][c] * L[k][c] * D[c];
+      L[i][k] = s * id;
+    }
+  }
+  double y[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    double v = b[i];
+#pragma unroll
+    for (int c = 0; c < i; c++) v -= L[i][c] * y[c];
+    y[i] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++) y[i] = (D[i] != 0) ? y[i] * (1.0 / D[i]) : 0.0;
+#pragma unroll
+  for (int i = 5; i >= 0; i--) {
+    double v = y[i];
+#pragma unroll
+    for (int r = i + 1; r < 6; r++) v -= L[r][i] * y[r];
+    y[i] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++) x[i] = y[i];
+  return positive;
+}
+
+// sums of one linearisation: [0] chi2, [1] scale term (trial only), [2..22] lower triangle of
+// J^T W J, [23..28] J^T W (-e)
+constexpr int kSums = 29;
+
+struct LMSmem {
+  long long prof[8];
+  double red[16 * 32];
+  double S27[32];
+  double H[2][32];  // current / trial linearisation sums (kSums)
+  double mh[16];
+  double xbuf[6];
+  DSE3 pose_new;
+  int ok2;
+};
+
+}  // namespace
+
+template <int IR, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_flow_lm(const FlowSolveDesc* __restrict__ descs) {
+  __shared__ LMSmem sm;
+  const FlowSolveDesc& D = descs[blockIdx.x];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int N = D.d_n ? min(*D.d_n, D.cap) : min(D.n, D.cap);
+  if (N < 3) {
+    if (tid == 0) {
+      D.stats[0] = 0;
+      D.stats[1] = 0;
+      D.stats[2] = 1;
+    }
+    return;
+  }
+#ifdef MMT_LM_PROFILE
+  long long prof_t = 0;
+  if (tid == 0)
+    for (int k = 0; k < 8; k++) sm.prof[k] = 0;
+#endif
+  double* G = D.scratch;  // items beyond IR * blockDim
+  const int cap = D.cap;
+  Cam c;
+  c.fx = D.fx;
+  c.fy = D.fy;
+  c.cx = D.cx;
+  c.cy = D.cy;
+  c.pinfo = D.prior_info;
+  const float deltaF = sqrtf(D.rp_thres);
+  c.delta = (double)deltaF;
+  c.dsqr = c.delta * c.delta;
+  // Twl = inverse(last Tcw): Rwl = R^T (float), twl = -R^T t via double-accumulated gemm
+  float Rwl[9], twl[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int cc = 0; cc < 3; cc++) Rwl[3 * r + cc] = D.Tcw_last[4 * cc + r];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) s += (double)Rwl[3 * r + k] * (double)D.Tcw_last[4 * k + 3];
+    twl[r] = (float)(-s);
+  }
+  auto init_item = [&](int i, LMItem& it) {
+    const int s = D.idx ? D.idx[i] : i;
+    const float2 ob = D.obs[s];
+    float z = D.depth[s];
+    if (D.use_noise) z = (float)((double)z + (double)D.g0 * ((double)(z * z) / (725 * 0.5) * 0.15));
+    const double u = ob.x, v = ob.y, dz = z;
+    const double Xc0 = (u - c.cx) * dz / c.fx, Xc1 = (v - c.cy) * dz / c.fy, Xc2 = dz;
+    it.X[0] = (double)Rwl[0] * Xc0 + (double)Rwl[1] * Xc1 + (double)Rwl[2] * Xc2 + (double)twl[0];
+    it.X[1] = (double)Rwl[3] * Xc0 + (double)Rwl[4] * Xc1 + (double)Rwl[5] * Xc2 + (double)twl[1];
+    it.X[2] = (double)Rwl[6] * Xc0 + (double)Rwl[7] * Xc1 + (double)Rwl[8] * Xc2 + (double)twl[2];
+    it.ob[0] = u;
+    it.ob[1] = v;
+    const float2 fl = D.flow[s];
+    it.pr[0] = fl.x;
+    it.pr[1] = fl.y;
+    it.f[0] = fl.x;
+    it.f[1] = fl.y;
+    it.xl[0] = it.xl[1] = 0;
+    it.e[0] = it.e[1] = 0;
+  };
+  LMItem R[IR];
+  const int n_reg = IR * nt;
+  // The LM bookkeeping below is computed redundantly by every thread from the block sums in LDS
+  // (identical inputs, identical results), so only the 6x6 solve needs a lane-0 section.
+  DSE3 P = dse3_from_float(D.init);
+  int hs = 0;  // sm.H[hs] holds the linearisation at P
+  // ---- initial linearisation (computeActiveErrors + buildSystem at the initial estimate)
+  {
+    double v[kSums];
+#pragma unroll
+    for (int k = 0; k < kSums; k++) v[k] = 0;
+    double mh = 0;
+#pragma unroll
+    for (int k = 0; k < IR; k++) {
+      const int i = tid + k * nt;
+      if (i < N) {
+        init_item(i, R[k]);
+        linearise(c, P, R[k], R[k].f[0], R[k].f[1], v + 2, v[0], R[k].e[0], R[k].e[1], R[k].w,
+                  R[k].bl[0], R[k].bl[1], mh);
+      }
+    }
+    for (int i = n_reg + tid; i < N; i += nt) {
+      LMItem it;
+      init_item(i, it);
+      linearise(c, P, it, it.f[0], it.f[1], v + 2, v[0], it.e[0], it.e[1], it.w, it.bl[0],
+                it.bl[1], mh);
+      item_store(G, cap, i, it);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mh = fmax(mh, __shfl_xor(mh, o, 64));
+    if ((tid & 63) == 0) sm.mh[tid >> 6] = mh;
+    block_sum<kSums>(v, sm.red, sm.H[0]);
+  }
+  double cur = sm.H[0][0], lam, ni = 2, chk = 0;
+  {
+    double md = 0;
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+      md = fmax(md, fabs(sm.H[0][2 + a * (a + 3) / 2]));  // diagonal (a, a) of the lower triangle
+    for (int w = 0; w < (nt >> 6); w++) md = fmax(md, sm.mh[w]);
+    lam = 1e-5 * md;
+  }
+  int nbad = 0, iters = 0;
+  if (tid == 0)
+    for (int k = 0; k < 6; k++) sm.xbuf[k] = 0;
+  for (int iter = 0; iter < D.max_iters; iter++) {
+    const double ini = cur;
+    int qmax = 0;
+    bool bad = false;
+    for (;;) {
+#ifdef MMT_LM_PROFILE
+      if (tid == 0) prof_t = clock64();
+#endif
+      const double ilam = 1.0 / lam;
+      // ---- Schur complement over the flow vertices
+      {
+        double v[27];
+#pragma unroll
+        for (int k = 0; k < 27; k++) v[k] = 0;
+#pragma unroll
+        for (int k = 0; k < IR; k++)
+          if (tid + k * nt < N) schur_terms(c, P, R[k], lam, ilam, v);
+        for (int i = n_reg + tid; i < N; i += nt) {
+          LMItem it;
+          item_load(G, cap, i, it);
+          schur_terms(c, P, it, lam, ilam, v);
+        }
+        block_sum<27>(v, sm.red, sm.S27);
+      }
+      MMT_LMPROF(0);
+      if (tid == 0) {
+        const double* Hc = sm.H[hs];
+        double Hs[36], bs[6], xp[6];
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+          for (int b = 0; b <= a; b++) {
+            Hs[6 * a + b] = Hc[2 + k] + (a == b ? lam : 0.0) - sm.S27[k];
+            Hs[6 * b + a] = Hs[6 * a + b];
+            k++;
+          }
+#pragma unroll
+        for (int a = 0; a < 6; a++) bs[a] = Hc[23 + a] - sm.S27[21 + a];
+        const bool ok2 = ldlt6(Hs, bs, xp);
+        double xu[6];
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+          xu[a] = ok2 ? xp[a] : sm.xbuf[a];  // a failed solve reuses the last increment
+          sm.xbuf[a] = xu[a];
+        }
+        sm.ok2 = ok2;
+        sm.pose_new = dse3_mul(dse3_exp(xu), P);
+      }
+      __syncthreads();
+      MMT_LMPROF(1);
+      const bool ok2 = sm.ok2;
+      const DSE3 PN = sm.pose_new;
+      double xb[6];
+#pragma unroll
+      for (int a = 0; a < 6; a++) xb[a] = sm.xbuf[a];
+      // ---- flow back-substitution, trial errors, speculative linearisation
+      {
+        double v[kSums];
+#pragma unroll
+        for (int k = 0; k < kSums; k++) v[k] = 0;
+#pragma unroll
+        for (int k = 0; k < IR; k++) {
+          const int i = tid + k * nt;
+          if (i < N) update_terms(c, P, PN, R[k], i, ok2, lam, ilam, xb, v);
+        }
+        for (int i = n_reg + tid; i < N; i += nt) {
+          LMItem it;
+          item_load(G, cap, i, it);
+          update_terms(c, P, PN, it, i, ok2, lam, ilam, xb, v);
+          item_store(G, cap, i, it);
+        }
+        block_sum<kSums>(v, sm.red, sm.H[hs ^ 1]);
+      }
+      MMT_LMPROF(2);
+      // ---- g2o LM step acceptance and termination (every thread, same values)
+      const double* Ht = sm.H[hs ^ 1];
+      const double* Hc = sm.H[hs];
+      const double lastTrialChi = Ht[0];
+      const double tempChi = ok2 ? Ht[0] : DBL_MAX;
+      double scale = Ht[1];
+#pragma unroll
+      for (int a = 0; a < 6; a++) scale += xb[a] * (lam * xb[a] + Hc[23 + a]);
+      scale += 1e-3;
+      const double rho = (cur - tempChi) / scale;
+      const bool accept = rho > 0 && isfinite(tempChi);
+      if (accept) {
+        const double t = 2 * rho - 1;
+        double alpha = 1. - t * t * t;
+        alpha = fmin(alpha, 2. / 3.);
+        lam = lam * fmax(1. / 3., alpha);
+        ni = 2;
+        cur = tempChi;
+        P = PN;
+        hs ^= 1;  // the trial's linearisation becomes the current system
+      } else {
+        lam = lam * ni;
+        ni = ni * 2;
+      }
+      qmax++;
+      const bool again = (rho < 0 && qmax < 10);
+      if (!again) {
+        bool ok = true;
+        if (qmax == 10 || rho == 0) ok = false;
+        if (ok) {
+          if ((ini - cur) * 1e3 < ini)
+            nbad++;
+          else
+            nbad = 0;
+          if (nbad >= 3) ok = false;
+        }
+        if (chk < lastTrialChi && iter > 0) ok = false;
+        chk = lastTrialChi;
+        iters = iter + 1;
+        bad = !ok;
+      }
+      if (accept) {
+#pragma unroll
+        for (int k = 0; k < IR; k++)
+          if (tid + k * nt < N) {
+            LMItem& it = R[k];
+            it.f[0] += it.xl[0];
+            it.f[1] += it.xl[1];
+            it.w = it.wn;
+            it.bl[0] = it.bln[0];
+            it.bl[1] = it.bln[1];
+          }
+        for (int i = n_reg + tid; i < N; i += nt) {
+          LMItem it;
+          item_load(G, cap, i, it);
+          it.f[0] += it.xl[0];
+          it.f[1] += it.xl[1];
+          it.w = it.wn;
+          it.bl[0] = it.bln[0];
+          it.bl[1] = it.bln[1];
+          item_store(G, cap, i, it);
+        }
+      }
+      MMT_LMPROF(3);
+      if (!again) break;
+    }
+    if (bad) break;
+  }
+  // outputs: pose, iterations, inliers from the last computed edge errors (Optimizer.cc:536-566)
+  double v[1] = {0};
+  auto outlier = [&](const LMItem& it) {
+    const float chi2 = (float)(kInfo * (it.e[0] * it.e[0] + it.e[1] * it.e[1]));
+    return chi2 > D.rp_thres ? 1.0 : 0.0;
+  };
+#pragma unroll
+  for (int k = 0; k < IR; k++)
+    if (tid + k * nt < N) v[0] += outlier(R[k]);
+  for (int i = n_reg + tid; i < N; i += nt) {
+    LMItem it;
+    item_load(G, cap, i, it);
+    v[0] += outlier(it);
+  }
+  block_sum<1>(v, sm.red, sm.S27);
+  if (tid == 0) {
+    dse3_to_float(P, D.pose_out);
+    D.stats[0] = iters;
+    D.stats[1] = N - (int)sm.S27[0];
+    D.stats[2] = 0;
+#ifdef MMT_LM_PROFILE
+    printf("lmprof N=%d iters=%d schur=%lld solve=%lld update=%lld decide=%lld\n", N, iters,
+           sm.prof[0], sm.prof[1], sm.prof[2], sm.prof[3]);
+#endif
+  }
+}
+
+void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st) {
+  // Latency-bound: one correspondence per thread where the block allows it (a trial's passes
+  // cost about one correspondence's dependency chain), up to 512 threads x 4 register items; the
+  // kernel itself handles any N (items beyond spill to the scratch arrays).
+  static const int force = [] {  // MMT_LM_CONFIG=<threads>x<items>: tuning knob for tools/
+    const char* e = getenv("MMT_LM_CONFIG");
+    int t = 0, r = 0;
+    if (e && sscanf(e, "%dx%d", &t, &r) == 2) return t * 100 + r;
+    return 0;
+  }();
+  auto r64 = [](int v) { return std::min(512, std::max(64, (v + 63) / 64 * 64)); };
+  int threads, ir;
+  if (force) {
+    threads = force / 100;
+    ir = force % 100;
+  } else if (n_hint <= 512) {
+    threads = r64(n_hint);
+    ir = 1;
+  } else if (n_hint <= 1024) {
+    threads = r64((n_hint + 3) / 4);
+    ir = 4;
+  } else {
+    threads = std::min(256, r64((n_hint + 7) / 8));
+    ir = 8;
+  }
+  if (ir == 1)
+    hipLaunchKernelGGL((k_flow_lm<1, 512>), dim3(nsolves), dim3(threads), 0, st, d_descs);
+  else if (ir == 2)
+    hipLaunchKernelGGL((k_flow_lm<2, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
+  else if (ir == 4)
+    hipLaunchKernelGGL((k_flow_lm<4, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
+  else
+    hipLaunchKernelGGL((k_flow_lm<8, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
+}
+
+size_t flow_scratch_doubles(int cap) { return (size_t)G_COUNT * cap; }
+
+}  // namespace mmt

@@ -101,7 +101,7 @@ void launch_handoff(const float2* last_corres, const int* n_last, const float2* 
                     const int* n_olast, const float* depth, const int32_t* mask, int W, int H,
                     const HandoffSet& cur, hipStream_t st);
 void launch_obj_group(const GroupArgs& a, hipStream_t st);
-void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, hipStream_t st);
+void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st);
 size_t flow_scratch_doubles(int cap);
 
 }  // namespace mmt

@@ -6,9 +6,7 @@
 //   k_handoff         B4: correspondences -> current keys + depth/label gathers (Tracking.cc:487-578)
 //   k_obj_group       B6 + B7 statistics: scene flow, per-label counts, ordered depth sums,
 //                     member lists, last-label histograms           (Tracking.cc:1389-1536, 4007-4093)
-//   k_flow_lm         D2 / D3: the whole g2o Levenberg-Marquardt of PoseOptimizationFlow2Cam /
-//                     PoseOptimizationFlow2 in one workgroup per solve, fp64 (Optimizer.cc:396-601,
-//                     2170-2377; g2o quirks as SURVEY.md Appendix B, see oracle/solve_ref.cpp)
+// (D2 / D3, the flow-refined pose solves, are in mmt_lm.hip)
 
 #include <hip/hip_runtime.h>
 
@@ -273,336 +271,6 @@ __global__ __launch_bounds__(1024) void k_obj_group(GroupArgs a) {
 // ------------------------------------------------------------------ D2 / D3 Levenberg-Marquardt
 // Edge scratch (SoA doubles, `cap` each): Xw0..2, OB0..1, PR0..1, F0..1, FS0..1, W, BL0..1,
 // XL0..1, E0..1.
-enum { S_X0 = 0, S_X1, S_X2, S_OB0, S_OB1, S_PR0, S_PR1, S_F0, S_F1, S_FS0, S_FS1, S_W, S_BL0,
-       S_BL1, S_XL0, S_XL1, S_E0, S_E1, S_COUNT };
-
-__device__ __forceinline__ void huber(double e, double dsqr, double delta, double& r0, double& r1) {
-  if (e <= dsqr) {
-    r0 = e;
-    r1 = 1.;
-  } else {
-    const double s = sqrt(e);
-    r0 = 2 * s * delta - dsqr;
-    r1 = delta / s;
-  }
-}
-
-__device__ __forceinline__ void jac(double x, double y, double z, double fx, double fy,
-                                    double J[2][6]) {
-  const double z2 = z * z;
-  J[0][0] = x * y / z2 * fx;
-  J[0][1] = -(1 + (x * x / z2)) * fx;
-  J[0][2] = y / z * fx;
-  J[0][3] = -1. / z * fx;
-  J[0][4] = 0;
-  J[0][5] = x / z2 * fx;
-  J[1][0] = (1 + y * y / z2) * fy;
-  J[1][1] = -x * y / z2 * fy;
-  J[1][2] = -x / z * fy;
-  J[1][3] = 0;
-  J[1][4] = -1. / z * fy;
-  J[1][5] = y / z2 * fy;
-}
-
-__device__ __forceinline__ void se3_map(const DSE3& p, const double* S, int cap, int i,
-                                        double& x, double& y, double& z) {
-  dq_rotate(p.q, S[S_X0 * cap + i], S[S_X1 * cap + i], S[S_X2 * cap + i], x, y, z);
-  x += p.t[0];
-  y += p.t[1];
-  z += p.t[2];
-}
-
-__global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict__ descs) {
-  __shared__ double s_red[4 * 28];
-  __shared__ double s_out[28];
-  __shared__ double s_max[4];
-  __shared__ DSE3 s_pose, s_pose_new;
-  __shared__ double s_Hpp[36], s_bp[6], s_xbuf[6];
-  __shared__ double s_lambda, s_ni, s_cur, s_ini, s_chk;
-  __shared__ int s_ok2, s_accept, s_stop, s_qmax, s_nbad, s_iters, s_bad;
-  const FlowSolveDesc D = descs[blockIdx.x];
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int N = D.d_n ? min(*D.d_n, D.cap) : min(D.n, D.cap);
-  if (N < 3) {
-    if (tid == 0) {
-      D.stats[0] = 0;
-      D.stats[1] = 0;
-      D.stats[2] = 1;
-    }
-    return;
-  }
-  double* S = D.scratch;
-  const int cap = D.cap;
-  const double fx = D.fx, fy = D.fy, cx = D.cx, cy = D.cy;
-  const double kInfo = 0.1, pinfo = D.prior_info;
-  const float deltaF = sqrtf(D.rp_thres);
-  const double delta = (double)deltaF, dsqr = delta * delta;
-  // Twl = inverse(last Tcw): Rwl = R^T (float), twl = -R^T t via double-accumulated gemm
-  float Rwl[9], twl[3];
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 3; c++) Rwl[3 * r + c] = D.Tcw_last[4 * c + r];
-  for (int r = 0; r < 3; r++) {
-    double s = 0;
-    for (int k = 0; k < 3; k++) s += (double)Rwl[3 * r + k] * (double)D.Tcw_last[4 * k + 3];
-    twl[r] = (float)(-s);
-  }
-  for (int i = tid; i < N; i += nt) {
-    const int s = D.idx ? D.idx[i] : i;
-    const float2 ob = D.obs[s];
-    float z = D.depth[s];
-    if (D.use_noise) z = (float)((double)z + (double)D.g0 * ((double)(z * z) / (725 * 0.5) * 0.15));
-    const double u = ob.x, v = ob.y, dz = z;
-    const double Xc0 = (u - cx) * dz / fx, Xc1 = (v - cy) * dz / fy, Xc2 = dz;
-    S[S_X0 * cap + i] = (double)Rwl[0] * Xc0 + (double)Rwl[1] * Xc1 + (double)Rwl[2] * Xc2 + (double)twl[0];
-    S[S_X1 * cap + i] = (double)Rwl[3] * Xc0 + (double)Rwl[4] * Xc1 + (double)Rwl[5] * Xc2 + (double)twl[1];
-    S[S_X2 * cap + i] = (double)Rwl[6] * Xc0 + (double)Rwl[7] * Xc1 + (double)Rwl[8] * Xc2 + (double)twl[2];
-    S[S_OB0 * cap + i] = u;
-    S[S_OB1 * cap + i] = v;
-    const float2 fl = D.flow[s];
-    S[S_PR0 * cap + i] = fl.x;
-    S[S_PR1 * cap + i] = fl.y;
-    S[S_F0 * cap + i] = fl.x;
-    S[S_F1 * cap + i] = fl.y;
-    S[S_XL0 * cap + i] = 0;
-    S[S_XL1 * cap + i] = 0;
-  }
-  if (tid == 0) {
-    s_pose = dse3_from_float(D.init);
-    for (int k = 0; k < 6; k++) s_xbuf[k] = 0;
-    s_chk = 0;
-    s_stop = 0;
-    s_iters = 0;
-  }
-  __syncthreads();
-  for (int iter = 0; iter < D.max_iters; iter++) {
-    // ---- linearise at the current state (computeActiveErrors + buildSystem)
-    {
-      double v[28];
-#pragma unroll
-      for (int k = 0; k < 28; k++) v[k] = 0;
-      double mh = 0;
-      const DSE3 P = s_pose;
-      for (int i = tid; i < N; i += nt) {
-        double x, y, z;
-        se3_map(P, S, cap, i, x, y, z);
-        const double pu = x / z * fx + cx, pv = y / z * fy + cy;
-        const double f0 = S[S_F0 * cap + i], f1 = S[S_F1 * cap + i];
-        const double e0 = (S[S_OB0 * cap + i] + f0) - pu, e1 = (S[S_OB1 * cap + i] + f1) - pv;
-        const double p0 = f0 - S[S_PR0 * cap + i], p1 = f1 - S[S_PR1 * cap + i];
-        const double e2 = kInfo * (e0 * e0 + e1 * e1);
-        double r0, r1;
-        huber(e2, dsqr, delta, r0, r1);
-        v[27] += r0 + pinfo * (p0 * p0 + p1 * p1);
-        const double w = kInfo * r1;
-        double J[2][6];
-        jac(x, y, z, fx, fy, J);
-        int k = 0;
-#pragma unroll
-        for (int a = 0; a < 6; a++)
-#pragma unroll
-          for (int b = 0; b <= a; b++) v[k++] += J[0][a] * w * J[0][b] + J[1][a] * w * J[1][b];
-        const double o0 = -w * e0, o1 = -w * e1;
-#pragma unroll
-        for (int a = 0; a < 6; a++) v[21 + a] += J[0][a] * o0 + J[1][a] * o1;
-        S[S_W * cap + i] = w;
-        S[S_BL0 * cap + i] = o0 - pinfo * p0;
-        S[S_BL1 * cap + i] = o1 - pinfo * p1;
-        mh = fmax(mh, w + pinfo);
-      }
-      wg_sum<28>(v, s_red, s_out);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mh = fmax(mh, __shfl_xor(mh, o, 64));
-      if ((tid & 63) == 0) s_max[tid >> 6] = mh;
-      __syncthreads();
-      if (tid == 0) {
-        int k = 0;
-        for (int a = 0; a < 6; a++)
-          for (int b = 0; b <= a; b++) {
-            s_Hpp[6 * a + b] = s_out[k];
-            s_Hpp[6 * b + a] = s_out[k];
-            k++;
-          }
-        for (int a = 0; a < 6; a++) s_bp[a] = s_out[21 + a];
-        s_cur = s_out[27];
-        s_ini = s_out[27];
-        if (iter == 0) {
-          double md = 0;
-          for (int a = 0; a < 6; a++) md = fmax(md, fabs(s_Hpp[7 * a]));
-          for (int w = 0; w < (nt >> 6); w++) md = fmax(md, s_max[w]);
-          s_lambda = 1e-5 * md;
-          s_ni = 2;
-          s_nbad = 0;
-        }
-        s_qmax = 0;
-      }
-      __syncthreads();
-    }
-    // ---- Levenberg trials
-    double lastTrialChi = 0, rho = 0;
-    for (;;) {
-      const DSE3 P = s_pose;
-      const double lam = s_lambda;
-      // Schur complement over the flow "landmarks"
-      {
-        double v[27];
-#pragma unroll
-        for (int k = 0; k < 27; k++) v[k] = 0;
-        for (int i = tid; i < N; i += nt) {
-          double x, y, z;
-          se3_map(P, S, cap, i, x, y, z);
-          double J[2][6];
-          jac(x, y, z, fx, fy, J);
-          const double w = S[S_W * cap + i], h = w + pinfo;
-          const double d00 = 1.0 / (h + lam), d01 = -h / ((h + lam) * lam), d11 = 1.0 / lam;
-          const double bl0 = S[S_BL0 * cap + i], bl1 = S[S_BL1 * cap + i];
-          const double db0 = d00 * bl0 + d01 * bl1, db1 = d11 * bl1;
-          int k = 0;
-#pragma unroll
-          for (int a = 0; a < 6; a++) {
-            const double B0a = w * J[0][a], B1a = w * J[1][a];
-            const double BD0 = B0a * d00, BD1 = B0a * d01 + B1a * d11;
-#pragma unroll
-            for (int b = 0; b <= a; b++) v[k++] += BD0 * (w * J[0][b]) + BD1 * (w * J[1][b]);
-            v[21 + a] += B0a * db0 + B1a * db1;
-          }
-        }
-        wg_sum<27>(v, s_red, s_out);
-      }
-      if (tid == 0) {
-        double Hs[36], bs[6], xp[6];
-        int k = 0;
-        for (int a = 0; a < 6; a++)
-          for (int b = 0; b <= a; b++) {
-            Hs[6 * a + b] = s_Hpp[6 * a + b] + (a == b ? lam : 0.0) - s_out[k];
-            k++;
-          }
-        for (int a = 0; a < 6; a++) bs[a] = s_bp[a] - s_out[21 + a];
-        const bool ok2 = ldlt_solve6(Hs, bs, xp);
-        if (ok2)
-          for (int a = 0; a < 6; a++) s_xbuf[a] = xp[a];
-        s_ok2 = ok2;
-        s_pose_new = dse3_mul(dse3_exp(s_xbuf), s_pose);
-      }
-      __syncthreads();
-      // landmark back-substitution, update, errors of the trial state
-      {
-        const bool ok2 = s_ok2;
-        const DSE3 PN = s_pose_new;
-        double v[2] = {0, 0};
-        for (int i = tid; i < N; i += nt) {
-          double xl0, xl1;
-          const double bl0 = S[S_BL0 * cap + i], bl1 = S[S_BL1 * cap + i];
-          if (ok2) {
-            double x, y, z;
-            se3_map(P, S, cap, i, x, y, z);
-            double J[2][6];
-            jac(x, y, z, fx, fy, J);
-            const double w = S[S_W * cap + i], h = w + pinfo;
-            double c0 = bl0, c1 = bl1;
-#pragma unroll
-            for (int a = 0; a < 6; a++) {
-              c0 -= w * J[0][a] * s_xbuf[a];
-              c1 -= w * J[1][a] * s_xbuf[a];
-            }
-            xl0 = c0 / (h + lam) - h * c1 / ((h + lam) * lam);
-            if (i > 0) xl0 += c0 / lam;  // stride-2 spill of landmark i-1's third Dinv row
-            xl1 = c1 / lam;
-            S[S_XL0 * cap + i] = xl0;
-            S[S_XL1 * cap + i] = xl1;
-          } else {
-            xl0 = S[S_XL0 * cap + i];
-            xl1 = S[S_XL1 * cap + i];
-          }
-          const double f0o = S[S_F0 * cap + i], f1o = S[S_F1 * cap + i];
-          S[S_FS0 * cap + i] = f0o;
-          S[S_FS1 * cap + i] = f1o;
-          const double f0 = f0o + xl0, f1 = f1o + xl1;
-          S[S_F0 * cap + i] = f0;
-          S[S_F1 * cap + i] = f1;
-          double x, y, z;
-          se3_map(PN, S, cap, i, x, y, z);
-          const double pu = x / z * fx + cx, pv = y / z * fy + cy;
-          const double e0 = (S[S_OB0 * cap + i] + f0) - pu, e1 = (S[S_OB1 * cap + i] + f1) - pv;
-          const double p0 = f0 - S[S_PR0 * cap + i], p1 = f1 - S[S_PR1 * cap + i];
-          S[S_E0 * cap + i] = e0;
-          S[S_E1 * cap + i] = e1;
-          const double e2 = kInfo * (e0 * e0 + e1 * e1);
-          double r0, r1;
-          huber(e2, dsqr, delta, r0, r1);
-          v[0] += r0 + pinfo * (p0 * p0 + p1 * p1);
-          v[1] += xl0 * (lam * xl0 + bl0) + xl1 * (lam * xl1 + bl1);
-        }
-        wg_sum<2>(v, s_red, s_out);
-      }
-      if (tid == 0) {
-        lastTrialChi = s_out[0];
-        double tempChi = s_ok2 ? s_out[0] : DBL_MAX;
-        double scale = s_out[1];
-        for (int a = 0; a < 6; a++) scale += s_xbuf[a] * (lam * s_xbuf[a] + s_bp[a]);
-        scale += 1e-3;
-        rho = (s_cur - tempChi) / scale;
-        if (rho > 0 && isfinite(tempChi)) {
-          double alpha = 1. - pow((2 * rho - 1), 3);
-          alpha = fmin(alpha, 2. / 3.);
-          const double sf = fmax(1. / 3., alpha);
-          s_lambda = lam * sf;
-          s_ni = 2;
-          s_cur = tempChi;
-          s_pose = s_pose_new;
-          s_accept = 1;
-        } else {
-          s_lambda = lam * s_ni;
-          s_ni = s_ni * 2;
-          s_accept = 0;
-        }
-        s_qmax = s_qmax + 1;
-        // loop condition (rho < 0 && qmax < 10) and termination bookkeeping
-        const bool again = (rho < 0 && s_qmax < 10);
-        s_stop = again ? 0 : 1;
-        if (!again) {
-          bool ok = true;
-          if (s_qmax == 10 || rho == 0) ok = false;
-          if (ok) {
-            if ((s_ini - s_cur) * 1e3 < s_ini)
-              s_nbad = s_nbad + 1;
-            else
-              s_nbad = 0;
-            if (s_nbad >= 3) ok = false;
-          }
-          if (s_chk < lastTrialChi && iter > 0) ok = false;
-          s_chk = lastTrialChi;
-          s_iters = iter + 1;
-          s_bad = ok ? 0 : 1;
-        }
-      }
-      __syncthreads();
-      if (!s_accept)
-        for (int i = tid; i < N; i += nt) {
-          S[S_F0 * cap + i] = S[S_FS0 * cap + i];
-          S[S_F1 * cap + i] = S[S_FS1 * cap + i];
-        }
-      const int stop = s_stop;
-      __syncthreads();
-      if (stop) break;
-    }
-    if (s_bad) break;
-  }
-  // outputs: pose, iterations, inliers from the last computed edge errors (Optimizer.cc:536-566)
-  double v[1] = {0};
-  for (int i = tid; i < N; i += nt) {
-    const double e0 = S[S_E0 * cap + i], e1 = S[S_E1 * cap + i];
-    const float chi2 = (float)(kInfo * (e0 * e0 + e1 * e1));
-    if (chi2 > D.rp_thres) v[0] += 1.0;
-  }
-  wg_sum<1>(v, s_red, s_out);
-  if (tid == 0) {
-    dse3_to_float(s_pose, D.pose_out);
-    D.stats[0] = s_iters;
-    D.stats[1] = N - (int)s_out[0];
-    D.stats[2] = 0;
-  }
-}
-
 // ------------------------------------------------------------------ launchers
 void launch_gray_depth(const uint8_t* bgr, size_t bgr_pitch, const uint16_t* disp,
                        size_t disp_pitch, uint8_t* gray, size_t gray_pitch, float* depth,
@@ -634,11 +302,5 @@ void launch_handoff(const float2* last_corres, const int* n_last, const float2* 
 void launch_obj_group(const GroupArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_obj_group, dim3(1), dim3(1024), 0, st, a);
 }
-
-void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, hipStream_t st) {
-  hipLaunchKernelGGL(k_flow_lm, dim3(nsolves), dim3(256), 0, st, d_descs);
-}
-
-size_t flow_scratch_doubles(int cap) { return (size_t)S_COUNT * cap; }
 
 }  // namespace mmt

@@ -56,6 +56,7 @@ class Tracker {
     ObjSampleSet ob;
     HandoffSet ho;
     float Tcw[16];
+    int n_static = 0;  // host copy of st.count (valid from the frame's first sync on)
     std::vector<int> nModLabel, nSemPosition;
     std::vector<std::vector<float>> vObjMod;
   };

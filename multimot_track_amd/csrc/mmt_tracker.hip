@@ -292,6 +292,7 @@ void Tracker::track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   out.n_keys = a.n_keys;
   // ---- Frame(RGBD): B2 static samples, B1 object samples
   launch_static_samples(a.kps, a.nkp, a.depth, a.flow, a.mask, W_, H_, C.st, st);
+  MMT_HIP(hipMemcpyAsync(&C.n_static, C.st.count, sizeof(int), hipMemcpyDeviceToHost, st));
   launch_obj_samples(a.depth, a.flow, a.mask, W_, H_, C.ob, st);
   // ---- GrabImageRGBD hand-off (B4)
   const bool handoff = bFirstFrame_ || bSecondFrame_;
@@ -353,7 +354,7 @@ void Tracker::track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   d2.stats = d_lmstats_;
   MMT_HIP(hipMemcpyAsync(d_descs_, &d2, sizeof(d2), hipMemcpyHostToDevice, st));
   MMT_HIP(hipMemcpyAsync(d_poses_, Tinit, sizeof(Tinit), hipMemcpyHostToDevice, st));
-  launch_flow_lm(d_descs_, 1, st);
+  launch_flow_lm(d_descs_, 1, Ls.n_static, st);
   float Tcw[16];
   int lmst[3];
   MMT_HIP(hipMemcpyAsync(Tcw, d_poses_, sizeof(Tcw), hipMemcpyDeviceToHost, st));
@@ -573,7 +574,10 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, Fram
   launch_pnp_subset(d_pnp_, nobj, st);
   MMT_HIP(hipMemcpyAsync(d_descs_ + 1, descs.data(), sizeof(FlowSolveDesc) * nobj,
                          hipMemcpyHostToDevice, st));
-  launch_flow_lm(d_descs_ + 1, nobj, st);
+  int n_hint = 0;
+  for (int i = 0; i < nobj; i++)
+    n_hint = std::max(n_hint, po[i].use_mm_choice ? res[8 * i + 4] : res[8 * i + 3]);
+  launch_flow_lm(d_descs_ + 1, nobj, n_hint, st);
   std::vector<float> X(16 * nobj);
   std::vector<int> lst(3 * nobj), nsub(nobj);
   MMT_HIP(hipMemcpyAsync(X.data(), d_poses_ + 16, sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
