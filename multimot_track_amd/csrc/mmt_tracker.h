@@ -56,9 +56,16 @@ class Tracker {
     ObjSampleSet ob;
     HandoffSet ho;
     float Tcw[16];
-    int n_static = 0;  // host copy of st.count (valid from the frame's first sync on)
+    bool bSecond = false;  // bSecondFrame as of this frame (label association, B8)
     std::vector<int> nModLabel, nSemPosition;
     std::vector<std::vector<float>> vObjMod;
+  };
+  // object path of a frame whose ego pose is known, run while the next frame's ego solve is in
+  // flight (the two chains only meet through the pose)
+  struct Pending {
+    bool active = false;
+    int cur = 0, last = 0, n_last_obj = 0;
+    FrameOut* out = nullptr;
   };
   struct FrameArgs {
     const float* depth;
@@ -86,20 +93,35 @@ class Tracker {
   };
   template <typename T>
   T* alloc(size_t n);
-  void track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st);
-  void track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, FrameOut& out,
-                     hipStream_t st);
-  void finish_frame(FrameSlot& C, FrameOut& out, hipStream_t st);
+  // ego part of a frame: samples, hand-off, D2 launched on `st` (no wait)
+  void ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st);
+  // waits for the ego solve, updates the motion model, queues the frame's object path
+  void ego_finish(FrameOut& out, hipStream_t st);
+  void track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStream_t st);
+  void run_pending();
 
   mmt_config cfg_{};
   OrbEngine* engine_ = nullptr;
   int W_ = 0, H_ = 0, max_chunk_ = 0, kcap_ = 0, ocap_ = 0, lm_cap_ = 0, mask_words_ = 0;
   float g0_ = 0;
-  int state_ = 0, cur_ = 0;
+  int state_ = 0, cur_ = 0, last_ = 2;
   bool bFirstFrame_ = false, bSecondFrame_ = false, hasVelocity_ = false;
   float V_[16] = {0};
-  FrameSlot slot_[2];
-  FrameSlot& last_ = slot_[1];
+  FrameSlot slot_[3];
+  // ego in flight; its device->host results land in pinned memory so the copies stay
+  // asynchronous while the host drives the previous frame's object path
+  struct EgoHost {
+    FlowSolveDesc d2;
+    float Tcw[16];
+    int st[3];
+    int nlast_obj;
+    int n_static[3];
+  };
+  bool ego_pending_ = false;
+  float ego_Tinit_[16];
+  EgoHost* eh_ = nullptr;
+  Pending pend_;
+  hipStream_t ost_ = nullptr;  // object-path stream
   std::vector<void*> allocs_;
   uint8_t* d_gray_ = nullptr;
   float* d_depth_ = nullptr;
@@ -117,7 +139,7 @@ class Tracker {
   int* d_lmstats_ = nullptr;
   PnPObject* d_pnp_ = nullptr;
   PnPBuf pnp_[kMaxObj];
-  std::vector<int> h_subsets_;
+  std::vector<int> h_subsets_[kMaxObj];
   bool prof_ = false;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
   double orb_ms_ = 0;

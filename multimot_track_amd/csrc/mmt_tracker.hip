@@ -130,7 +130,12 @@ static T* dalloc(size_t n) {
 }
 
 Tracker::~Tracker() {
+  if (ost_) {
+    (void)hipStreamSynchronize(ost_);
+    (void)hipStreamDestroy(ost_);
+  }
   for (void* p : allocs_) (void)hipFree(p);
+  if (eh_) (void)hipHostFree(eh_);
   for (hipEvent_t& e : ev_orb_)
     if (e) (void)hipEventDestroy(e);
 }
@@ -176,7 +181,7 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   d_kps_ = alloc<mmt_kp>((size_t)kcap_ * max_chunk);
   d_desc_ = alloc<uint8_t>((size_t)kcap_ * 32 * max_chunk);
   d_nkp_ = alloc<int>(max_chunk);
-  for (int s = 0; s < 2; s++) {
+  for (int s = 0; s < 3; s++) {
     FrameSlot& F = slot_[s];
     F.st.keys = alloc<float2>(kcap_);
     F.st.corres = alloc<float2>(kcap_);
@@ -234,20 +239,30 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     b.result = alloc<int>(8);
     b.Rt = alloc<double>(12);
   }
-  h_subsets_.resize(5 * kRansacIters);
+  for (int o = 0; o < kMaxObj; o++) h_subsets_[o].resize(5 * kRansacIters);
+  MMT_HIP(hipStreamCreateWithFlags(&ost_, hipStreamNonBlocking));
+  MMT_HIP(hipHostMalloc((void**)&eh_, sizeof(EgoHost), hipHostMallocDefault));
+  memset(eh_, 0, sizeof(EgoHost));
   reset();
 }
 
 void Tracker::reset() {
+  if (ost_) MMT_HIP(hipStreamSynchronize(ost_));
   state_ = 0;
   bFirstFrame_ = false;  // uninitialised member in the reference (Tracking.h:180): pinned false
   bSecondFrame_ = false;
   hasVelocity_ = false;
   cur_ = 0;
-  last_.nModLabel.clear();
-  last_.nSemPosition.clear();
-  last_.vObjMod.clear();
-  mat4_eye(last_.Tcw);
+  last_ = 2;
+  ego_pending_ = false;
+  pend_ = Pending();
+  for (FrameSlot& F : slot_) {
+    F.nModLabel.clear();
+    F.nSemPosition.clear();
+    F.vObjMod.clear();
+    F.bSecond = false;
+    mat4_eye(F.Tcw);
+  }
 }
 
 void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t* d_disp,
@@ -273,6 +288,9 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
     orb_frames_ += nframes;
   }
   outs.assign(nframes, FrameOut());
+  // Two chains per sequence: ego (samples, hand-off, D2 of frame f needs frame f-1's pose) on
+  // `st`, and objects (grouping, PnP, D3 of frame f need frame f's pose and frame f-1's objects)
+  // on ost_.  Frame f's ego solve runs on the GPU while the host drives frame f-1's object path.
   for (int f = 0; f < nframes; f++) {
     FrameArgs a;
     a.depth = d_depth_ + npix * f;
@@ -281,59 +299,54 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
     a.kps = d_kps_ + (size_t)kcap_ * f;
     a.nkp = d_nkp_ + f;
     a.n_keys = nkp[f];
-    track_frame(a, outs[f], st);
+    ego_launch(a, outs[f], st);
+    run_pending();
+    ego_finish(outs[f], st);
   }
+  run_pending();  // the chunk's results are complete on return
 }
 
-void Tracker::track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st) {
+void Tracker::run_pending() {
+  if (!pend_.active) return;
+  pend_.active = false;
+  track_objects(slot_[pend_.cur], slot_[pend_.last], *pend_.out, ost_);
+}
+
+void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   FrameSlot& C = slot_[cur_];
-  FrameSlot& Ls = slot_[cur_ ^ 1];
+  FrameSlot& Ls = slot_[last_];
   out = FrameOut();
   out.n_keys = a.n_keys;
+  C.nModLabel.clear();
+  C.nSemPosition.clear();
+  C.vObjMod.clear();
   // ---- Frame(RGBD): B2 static samples, B1 object samples
   launch_static_samples(a.kps, a.nkp, a.depth, a.flow, a.mask, W_, H_, C.st, st);
-  MMT_HIP(hipMemcpyAsync(&C.n_static, C.st.count, sizeof(int), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(&eh_->n_static[cur_], C.st.count, sizeof(int), hipMemcpyDeviceToHost, st));
   launch_obj_samples(a.depth, a.flow, a.mask, W_, H_, C.ob, st);
   // ---- GrabImageRGBD hand-off (B4)
   const bool handoff = bFirstFrame_ || bSecondFrame_;
   if (handoff)
     launch_handoff(Ls.st.corres, Ls.st.count, Ls.ob.corres, Ls.ob.count, a.depth, a.mask, W_, H_,
                    C.ho, st);
+  // mCurrentFrame.mvObjKeys: the frame's own samples, or the hand-off once bFirstFrame is set
+  MMT_HIP(hipMemcpyAsync(&eh_->nlast_obj, handoff ? Ls.ob.count : C.ob.count, sizeof(int),
+                         hipMemcpyDeviceToHost, st));
   if (state_ == 0) {
-    // mCurrentFrame.mvObjKeys: the frame's own samples, or the hand-off once bFirstFrame is set
-    int nob = 0;
-    MMT_HIP(hipMemcpyAsync(&nob, handoff ? Ls.ob.count : C.ob.count, sizeof(int),
-                           hipMemcpyDeviceToHost, st));
-    MMT_HIP(hipStreamSynchronize(st));
-    out.n_obj_samples = nob;
-    // ---- StereoInitialization (needs more than 500 keypoints)
-    bFirstFrame_ = true;
-    bSecondFrame_ = false;
-    if (a.n_keys > 500) {
-      mat4_eye(C.Tcw);
-      memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
-      C.nModLabel.clear();
-      C.nSemPosition.clear();
-      C.vObjMod.clear();
-      state_ = 1;
-      out.initialized = true;
-      finish_frame(C, out, st);
-    } else {
-      mat4_eye(out.Tcw);
-    }
+    ego_pending_ = false;
     return;
   }
   // ---- ego initial pose: motion model (deviation, see header)
-  float Tinit[16];
   if (hasVelocity_) {
-    mat4_mul(V_, Ls.Tcw, Tinit);
+    mat4_mul(V_, Ls.Tcw, ego_Tinit_);
     bSecondFrame_ = false;
   } else {
-    memcpy(Tinit, Ls.Tcw, sizeof(Tinit));
+    memcpy(ego_Tinit_, Ls.Tcw, sizeof(ego_Tinit_));
     bSecondFrame_ = true;
   }
-  // ---- D2 (PoseOptimizationFlow2Cam) + B6/B7 statistics in one round trip
-  FlowSolveDesc d2;
+  C.bSecond = bSecondFrame_;
+  // ---- D2 (PoseOptimizationFlow2Cam)
+  FlowSolveDesc& d2 = eh_->d2;  // pinned: the upload below stays asynchronous
   memset(&d2, 0, sizeof(d2));
   d2.d_n = Ls.st.count;
   d2.idx = nullptr;
@@ -341,7 +354,7 @@ void Tracker::track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   d2.flow = Ls.st.flow;
   d2.depth = Ls.st.depth;
   memcpy(d2.Tcw_last, Ls.Tcw, sizeof(d2.Tcw_last));
-  memcpy(d2.init, Tinit, sizeof(d2.init));
+  memcpy(d2.init, ego_Tinit_, sizeof(d2.init));
   d2.rp_thres = 0.04f;
   d2.use_noise = 1;
   d2.g0 = g0_;
@@ -353,37 +366,63 @@ void Tracker::track_frame(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   d2.pose_out = d_poses_;
   d2.stats = d_lmstats_;
   MMT_HIP(hipMemcpyAsync(d_descs_, &d2, sizeof(d2), hipMemcpyHostToDevice, st));
-  MMT_HIP(hipMemcpyAsync(d_poses_, Tinit, sizeof(Tinit), hipMemcpyHostToDevice, st));
-  launch_flow_lm(d_descs_, 1, Ls.n_static, st);
-  float Tcw[16];
-  int lmst[3];
-  MMT_HIP(hipMemcpyAsync(Tcw, d_poses_, sizeof(Tcw), hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(lmst, d_lmstats_, sizeof(lmst), hipMemcpyDeviceToHost, st));
-  int n_last_obj = 0;
-  MMT_HIP(hipMemcpyAsync(&n_last_obj, Ls.ob.count, sizeof(int), hipMemcpyDeviceToHost, st));
+  launch_flow_lm(d_descs_, 1, eh_->n_static[last_], st);
+  MMT_HIP(hipMemcpyAsync(eh_->Tcw, d_poses_, sizeof(eh_->Tcw), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(eh_->st, d_lmstats_, sizeof(eh_->st), hipMemcpyDeviceToHost, st));
+  ego_pending_ = true;
+}
+
+void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
+  FrameSlot& C = slot_[cur_];
+  FrameSlot& Ls = slot_[last_];
   MMT_HIP(hipStreamSynchronize(st));
-  if (lmst[2] != 0) memcpy(Tcw, Tinit, sizeof(Tcw));  // < 3 correspondences: pose unchanged
-  memcpy(C.Tcw, Tcw, sizeof(Tcw));
-  out.n_obj_samples = n_last_obj;  // hand-off of the last frame's object correspondences
-  out.ego_iterations = lmst[0];
-  out.ego_inliers = lmst[1];
-  {
+  out.n_obj_samples = eh_->nlast_obj;
+  bool advance = true;
+  if (state_ == 0) {
+    // ---- StereoInitialization (needs more than 500 keypoints)
+    bFirstFrame_ = true;
+    bSecondFrame_ = false;
+    if (out.n_keys > 500) {
+      mat4_eye(C.Tcw);
+      memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
+      state_ = 1;
+      out.initialized = true;
+    } else {
+      mat4_eye(out.Tcw);
+      advance = false;  // the reference keeps its last frame until initialisation succeeds
+    }
+  } else {
+    float Tcw[16];
+    memcpy(Tcw, eh_->Tcw, sizeof(Tcw));
+    if (eh_->st[2] != 0) memcpy(Tcw, ego_Tinit_, sizeof(Tcw));  // < 3 edges: pose unchanged
+    memcpy(C.Tcw, Tcw, sizeof(Tcw));
+    out.ego_iterations = eh_->st[0];
+    out.ego_inliers = eh_->st[1];
     float LastTwc[16];
     inv_mat(Ls.Tcw, LastTwc);
     mat4_mul(C.Tcw, LastTwc, V_);
     hasVelocity_ = true;
+    memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
+    out.initialized = true;
+    if (eh_->nlast_obj > 0) {
+      pend_.active = true;
+      pend_.cur = cur_;
+      pend_.last = last_;
+      pend_.n_last_obj = eh_->nlast_obj;
+      pend_.out = &out;
+    }
   }
-  memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
-  out.initialized = true;
-  C.nModLabel.clear();
-  C.nSemPosition.clear();
-  C.vObjMod.clear();
-  if (n_last_obj > 0) track_objects(C, Ls, n_last_obj, out, st);
-  finish_frame(C, out, st);
+  ego_pending_ = false;
+  if (advance) {
+    // B9: the current slot becomes the last frame (Tracking.cc:2463-2477); its own samples
+    // already live in the slot, so this is an index rotation over three slots (the object path
+    // of this frame still reads this slot and the previous one)
+    last_ = cur_;
+    cur_ = (cur_ + 1) % 3;
+  }
 }
 
-void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, FrameOut& out,
-                            hipStream_t st) {
+void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStream_t st) {
   // ---- B6 + B7 statistics
   GroupArgs g;
   memset(&g, 0, sizeof(g));
@@ -414,7 +453,6 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, Fram
   MMT_HIP(hipMemcpyAsync(&err, d_err_, sizeof(int), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
   if (err) throw ArgError("semantic label outside [0, 15] on the object path");
-  out.n_obj_samples = n_obj_samples;
   // ---- B7 decisions (Tracking.cc:1424-1536); labels ascending = UniLab order
   std::vector<int> objLabelsNew;  // semantic label of each kept object
   for (int l = 1; l < kMaxLabel; l++) {
@@ -430,7 +468,7 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, Fram
   }
   // ---- B8 label association (Tracking.cc:1556-1630)
   int mx;
-  if (bSecondFrame_)
+  if (C.bSecond)
     mx = 1;
   else if (!Ls.nModLabel.empty())
     mx = *std::max_element(Ls.nModLabel.begin(), Ls.nModLabel.end()) + 1;
@@ -448,7 +486,7 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, Fram
         New_lab = ll;
       }
     }
-    if (bSecondFrame_) {
+    if (C.bSecond) {
       LabId[i] = mx++;
     } else {
       bool exist = false;
@@ -481,8 +519,8 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, Fram
     o.fx = cfg_.fx; o.fy = cfg_.fy; o.cx = cfg_.cx; o.cy = cfg_.cy;
     o.reproj = 0.3;
     o.confidence = 0.98;
-    ransac_subsets(std::max(stats[l].members, 1), kRansacIters, h_subsets_);
-    MMT_HIP(hipMemcpyAsync(b.subsets, h_subsets_.data(), sizeof(int) * 5 * kRansacIters,
+    ransac_subsets(std::max(stats[l].members, 1), kRansacIters, h_subsets_[i]);
+    MMT_HIP(hipMemcpyAsync(b.subsets, h_subsets_[i].data(), sizeof(int) * 5 * kRansacIters,
                            hipMemcpyHostToDevice, st));
     o.subsets = b.subsets;
     int PreObjID = -1;
@@ -507,8 +545,6 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, Fram
     o.n_subset = b.n_subset;
     o.result = b.result;
     o.Rt = b.Rt;
-    // hipMemcpyAsync of the subsets above must complete before the host vector is reused
-    MMT_HIP(hipStreamSynchronize(st));
   }
   MMT_HIP(hipMemcpyAsync(d_pnp_, po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
   launch_pnp(d_pnp_, nobj, kRansacIters, st);
@@ -601,15 +637,6 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, int n_obj_samples, Fram
     memcpy(oo.X, Xi, 64);
     memcpy(oo.motion, C.vObjMod[i].data(), 64);
   }
-}
-
-// B9: the current slot becomes the last frame (Tracking.cc:2463-2477): its own samples
-// (st.keys/st.depth, ob.keys/ob.depth/ob.label) already live in the slot; just swap.
-void Tracker::finish_frame(FrameSlot& C, FrameOut& out, hipStream_t st) {
-  (void)out;
-  (void)st;
-  (void)C;
-  cur_ ^= 1;
 }
 
 }  // namespace mmt
