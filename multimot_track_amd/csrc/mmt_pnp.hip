@@ -212,12 +212,12 @@ __device__ __forceinline__ double d_dist2(const double* a, const double* b) {
   return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
 }
 
-// L_6x10 from the four null-space vectors ut rows 11, 10, 9, 8 (ut in LDS)
-__device__ __forceinline__ void compute_L_6x10(const double* ut, double (&l)[60]) {
+// L_6x10 from the four null-space vectors ut rows 11, 10, 9, 8 (`ut8` points at row 8)
+__device__ __forceinline__ void compute_L_6x10(const double* ut8, double (&l)[60]) {
   double dv[4][6][3];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const double* v = ut + 12 * (11 - i);
+    const double* v = ut8 + 12 * (3 - i);
     int a = 0, b = 1;
 #pragma unroll
     for (int j = 0; j < 6; j++) {
@@ -450,93 +450,74 @@ __device__ void d_rodrigues_v2r(const double rv[3], double R[9]) {
   for (int i = 0; i < 9; i++) R[i] = c * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i] + s * rx[i];
 }
 
-// ---------------------------------------------------------------- 12x12 eigen-solve, block-wide
-// Parallel-order Jacobi (oracle/pnp_ref.cpp: jacobi_eig12_rr): per round 6 disjoint pairs, angles
-// from the round's start matrix, then B = A J (columns) and A = J^T B (rows), V = V J, each element
-// by its own lane.  A, B, V, V2 in LDS; `cs` holds c/s indexed by the pair's smaller index.
-struct Eig12Smem {
-  double A[144], B[144], V[144], V2[144], ut[144], c[12], s[12];
-  int done;
-};
-
+// ---------------------------------------------------------------- 12x12 eigen-solve, one lane per column
+// One-sided parallel-order Jacobi of oracle/pnp_ref.cpp (jacobi_eig12): lane `gb + j` holds
+// column j of the matrix (a) and of the accumulated rotation (v) in registers; per round it
+// fetches its partner column with cross-lane shuffles, both lanes of a pair compute the same
+// (alpha, beta, gamma) in the same order, hence the same rotation, and each updates its own
+// column.  A 64-lane wave runs five independent solves (lanes 0-59).  On return `rank` is the
+// column's position in descending singular-value order.
 __device__ __forceinline__ void rr_partner(int r, int j, int& p, int& q) {
   const int k = j == 11 ? r : (j == r ? 11 : (2 * r - j + 22) % 11);
   p = min(j, k);
   q = max(j, k);
 }
 
-// all threads of the block call this; A holds M^T M on entry; ut (rows = eigenvectors by
-// descending eigenvalue) on exit
-__device__ void eig12_block(Eig12Smem& S) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int e = tid; e < 144; e += nt) S.V[e] = (e % 13 == 0) ? 1.0 : 0.0;
-  __syncthreads();
-  double* V = S.V;
-  double* V2 = S.V2;
+__device__ __forceinline__ void eig12_group(double (&a)[12], double (&v)[12], int gb, int j,
+                                            bool active, int& rank) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long gmask = active ? (0xFFFull << gb) : 0ull;
   for (int sweep = 0; sweep < 100; sweep++) {
-    if (tid == 0) {
-      double off = 0, dsum = 0;
-      for (int p = 0; p < 12; p++) {
-        dsum += S.A[p * 12 + p] * S.A[p * 12 + p];
-        for (int q = p + 1; q < 12; q++) off += S.A[p * 12 + q] * S.A[p * 12 + q];
-      }
-      S.done = off <= 1e-26 * dsum;
-    }
-    __syncthreads();
-    if (S.done) break;
+    bool rotated = false;
     for (int r = 0; r < 11; r++) {
-      if (tid < 6) {
-        const int a = tid == 0 ? r : (r + tid) % 11, b = tid == 0 ? 11 : (r - tid + 11) % 11;
-        const int p = min(a, b), q = max(a, b);
-        const double apq = S.A[p * 12 + q];
-        if (fabs(apq) < 1e-300) {
-          S.c[p] = 1.0;
-          S.s[p] = 0.0;
-        } else {
-          const double app = S.A[p * 12 + p], aqq = S.A[q * 12 + q];
-          const double theta = (aqq - app) / (2 * apq);
-          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
-          const double c = 1 / sqrt(t * t + 1);
-          S.c[p] = c;
-          S.s[p] = t * c;
+      int p, q;
+      rr_partner(r, j, p, q);
+      const int src = gb + (j == p ? q : p);
+      double b[12], w[12];
+#pragma unroll
+      for (int k = 0; k < 12; k++) {
+        b[k] = __shfl(a[k], src, 64);
+        w[k] = __shfl(v[k], src, 64);
+      }
+      const bool mine_p = (j == p);
+      double al = 0, be = 0, ga = 0;
+#pragma unroll
+      for (int k = 0; k < 12; k++) {
+        const double xp = mine_p ? a[k] : b[k], xq = mine_p ? b[k] : a[k];
+        al += xp * xp;
+        be += xq * xq;
+        ga += xp * xq;
+      }
+      if (active && !(fabs(ga) <= 1e-15 * sqrt(al * be) || ga == 0)) {
+        rotated = true;
+        const double zeta = (be - al) / (2 * ga);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1 + zeta * zeta));
+        const double c = 1 / sqrt(1 + t * t), s = c * t;
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+          const double xp = mine_p ? a[k] : b[k], xq = mine_p ? b[k] : a[k];
+          const double vp = mine_p ? v[k] : w[k], vq = mine_p ? w[k] : v[k];
+          a[k] = mine_p ? c * xp - s * xq : s * xp + c * xq;
+          v[k] = mine_p ? c * vp - s * vq : s * vp + c * vq;
         }
       }
-      __syncthreads();
-      for (int e = tid; e < 144; e += nt) {
-        const int k = e / 12, j = e - 12 * k;
-        int p, q;
-        rr_partner(r, j, p, q);
-        const double cc = S.c[p], ss = S.s[p];
-        if (j == p) {
-          S.B[e] = cc * S.A[k * 12 + p] - ss * S.A[k * 12 + q];
-          V2[e] = cc * V[k * 12 + p] - ss * V[k * 12 + q];
-        } else {
-          S.B[e] = ss * S.A[k * 12 + p] + cc * S.A[k * 12 + q];
-          V2[e] = ss * V[k * 12 + p] + cc * V[k * 12 + q];
-        }
-      }
-      __syncthreads();
-      for (int e = tid; e < 144; e += nt) {
-        const int i = e / 12, k = e - 12 * i;
-        int p, q;
-        rr_partner(r, i, p, q);
-        const double cc = S.c[p], ss = S.s[p];
-        S.A[e] = i == p ? cc * S.B[p * 12 + k] - ss * S.B[q * 12 + k]
-                        : ss * S.B[p * 12 + k] + cc * S.B[q * 12 + k];
-      }
-      double* tmp = V;
-      V = V2;
-      V2 = tmp;
-      __syncthreads();
     }
+    const unsigned long long any = __ballot(rotated);
+    // every group keeps shuffling until all groups of the wave have converged; a converged
+    // group's pairs are orthogonal and stay untouched, so its results do not change
+    if (!(any & 0x0FFFFFFFFFFFFFFFull)) break;
+    (void)gmask;
   }
-  if (tid < 12) {
-    const double di = S.A[tid * 13];
-    int rank = 0;
-    for (int j = 0; j < 12; j++) rank += (S.A[j * 13] > di) || (j < tid && S.A[j * 13] == di);
-    for (int k = 0; k < 12; k++) S.ut[rank * 12 + k] = V[k * 12 + tid];
+  double ss = 0;
+#pragma unroll
+  for (int k = 0; k < 12; k++) ss += a[k] * a[k];
+  const double sig = sqrt(ss);
+  rank = 0;
+  for (int i = 0; i < 12; i++) {
+    const double si = __shfl(sig, gb + i, 64);
+    rank += (si > sig) || (i < j && si == sig);
   }
-  __syncthreads();
+  (void)lane;
 }
 
 // ---------------------------------------------------------------- kernels
@@ -567,32 +548,33 @@ __global__ __launch_bounds__(256) void k_pnp_gather(PnPObject* objs) {
 // us, L_6x10, rho
 constexpr int R_UT = 0, R_AL = 48, R_PW = 68, R_US = 83, R_L = 93, R_RHO = 153;
 
-// one 64-lane workgroup per (hypothesis, object): 5-point EPnP up to the null space.  Lane 0 does
-// the small dense algebra in registers, the 64 lanes build M^T M and run the 12x12 eigen-solve.
-struct HypSmem {
-  Eig12Smem eig;
-  double pws[15], us[10], alphas[20], cws[12];
-};
+// 64-lane workgroup = five hypotheses (lanes 12g..12g+11 for hypothesis g): 5-point EPnP up to
+// the null space of M^T M.  Lane 12g does the control points in registers, every lane builds one
+// column of M^T M and runs its column of the eigen-solve.
+constexpr int kHypPerBlock = 5;
 
 __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) {
-  __shared__ HypSmem S;
-  const int h = blockIdx.x, tid = threadIdx.x;
+  __shared__ double s_al[kHypPerBlock][20], s_us[kHypPerBlock][10], s_pws[kHypPerBlock][15];
+  __shared__ double s_cws[kHypPerBlock][12], s_ut[kHypPerBlock][48];
+  const int lane = threadIdx.x, g = lane / 12, j = lane - 12 * g, gb = 12 * g;
   PnPObject& o = objs[blockIdx.y];
   const int n = *o.n;
-  if (h >= max_iters || n < 5) return;
+  if (n < 5) return;
+  const int h = blockIdx.x * kHypPerBlock + g;
+  const bool active = g < kHypPerBlock && h < max_iters;
   const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
-  if (tid == 0) {
+  if (active && j == 0) {
     double pws[15], us[10], cws[12];
     const double ifx = 1. / fu, ify = 1. / fv;
     const int* sub = o.subsets + 5 * h;
 #pragma unroll
     for (int i = 0; i < 5; i++) {
-      const int j = n == 5 ? i : sub[i];  // count == modelPoints: the kernel runs on all points
+      const int jj = n == 5 ? i : sub[i];  // count == modelPoints: the kernel runs on all points
 #pragma unroll
-      for (int k = 0; k < 3; k++) pws[3 * i + k] = o.pts3[3 * j + k];
-      const float2 p = o.pts2[j];
-      const float xn = (float)(((double)p.x - uc) * ifx);
-      const float yn = (float)(((double)p.y - vc) * ify);
+      for (int k = 0; k < 3; k++) pws[3 * i + k] = o.pts3[3 * jj + k];
+      const float2 pt = o.pts2[jj];
+      const float xn = (float)(((double)pt.x - uc) * ifx);
+      const float yn = (float)(((double)pt.y - vc) * ify);
       us[2 * i] = (double)xn * fu + uc;
       us[2 * i + 1] = (double)yn * fv + vc;
     }
@@ -601,19 +583,19 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
 #pragma unroll
     for (int i = 0; i < 5; i++)
 #pragma unroll
-      for (int j = 0; j < 3; j++) cws[j] += pws[3 * i + j];
+      for (int k = 0; k < 3; k++) cws[k] += pws[3 * i + k];
 #pragma unroll
-    for (int j = 0; j < 3; j++) cws[j] /= 5;
+    for (int k = 0; k < 3; k++) cws[k] /= 5;
     double m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 5; i++) {
-      double p[3];
+      double pp[3];
 #pragma unroll
-      for (int j = 0; j < 3; j++) p[j] = pws[3 * i + j] - cws[j];
+      for (int k = 0; k < 3; k++) pp[k] = pws[3 * i + k] - cws[k];
 #pragma unroll
-      for (int a = 0; a < 3; a++)
+      for (int x = 0; x < 3; x++)
 #pragma unroll
-        for (int b = 0; b < 3; b++) m[3 * a + b] += p[a] * p[b];
+        for (int y = 0; y < 3; y++) m[3 * x + y] += pp[x] * pp[y];
     }
     double dc[3], uct[9];
     eig_sym_small<3>(m, dc, uct);
@@ -621,64 +603,76 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
     for (int i = 1; i < 4; i++) {
       const double k = sqrt(fmax(dc[i - 1], 0.0) / 5);
 #pragma unroll
-      for (int j = 0; j < 3; j++) cws[3 * i + j] = cws[j] + k * uct[3 * (i - 1) + j];
+      for (int x = 0; x < 3; x++) cws[3 * i + x] = cws[x] + k * uct[3 * (i - 1) + x];
     }
     // compute_barycentric_coordinates
     double cc[9], ci[9];
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-      for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = cws[3 * j + i] - cws[i];
+      for (int x = 1; x < 4; x++) cc[3 * i + x - 1] = cws[3 * x + i] - cws[i];
     pinv3(cc, ci);
 #pragma unroll
     for (int i = 0; i < 5; i++) {
       const double* pi = &pws[3 * i];
-      double a[4];
+      double al[4];
 #pragma unroll
-      for (int j = 0; j < 3; j++)
-        a[1 + j] = ci[3 * j] * (pi[0] - cws[0]) + ci[3 * j + 1] * (pi[1] - cws[1]) +
-                   ci[3 * j + 2] * (pi[2] - cws[2]);
-      a[0] = 1.0f - a[1] - a[2] - a[3];
+      for (int x = 0; x < 3; x++)
+        al[1 + x] = ci[3 * x] * (pi[0] - cws[0]) + ci[3 * x + 1] * (pi[1] - cws[1]) +
+                    ci[3 * x + 2] * (pi[2] - cws[2]);
+      al[0] = 1.0f - al[1] - al[2] - al[3];
 #pragma unroll
-      for (int j = 0; j < 4; j++) S.alphas[4 * i + j] = a[j];
+      for (int x = 0; x < 4; x++) s_al[g][4 * i + x] = al[x];
     }
 #pragma unroll
-    for (int i = 0; i < 15; i++) S.pws[i] = pws[i];
+    for (int i = 0; i < 15; i++) s_pws[g][i] = pws[i];
 #pragma unroll
-    for (int i = 0; i < 10; i++) S.us[i] = us[i];
+    for (int i = 0; i < 10; i++) s_us[g][i] = us[i];
 #pragma unroll
-    for (int i = 0; i < 12; i++) S.cws[i] = cws[i];
+    for (int i = 0; i < 12; i++) s_cws[g][i] = cws[i];
   }
   __syncthreads();
-  // M^T M, one entry per lane and pass, points in order (compute_pose)
-  for (int e = tid; e < 144; e += 64) {
-    const int a = e / 12, b = e - 12 * a;
-    const int qa = a / 3, ca = a - 3 * qa, qb = b / 3, cb = b - 3 * qb;
-    double acc = 0;
-    for (int i = 0; i < 5; i++) {
-      const double u = S.us[2 * i], v = S.us[2 * i + 1];
-      const double aa = S.alphas[4 * i + qa], ab = S.alphas[4 * i + qb];
-      const double m1a = ca == 0 ? aa * fu : (ca == 1 ? 0.0 : aa * (uc - u));
-      const double m1b = cb == 0 ? ab * fu : (cb == 1 ? 0.0 : ab * (uc - u));
-      const double m2a = ca == 0 ? 0.0 : (ca == 1 ? aa * fv : aa * (vc - v));
-      const double m2b = cb == 0 ? 0.0 : (cb == 1 ? ab * fv : ab * (vc - v));
-      acc += m1a * m1b + m2a * m2b;
+  // column j of M^T M: entry (k, j) = sum_i M1[k] M1[j] + M2[k] M2[j], points in order
+  double a[12], v[12];
+  {
+    const int qb = j / 3, cb = j - 3 * qb;
+    const int gg = active ? g : 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      const int qa = k / 3, ca = k - 3 * qa;
+      double acc = 0;
+      for (int i = 0; i < 5; i++) {
+        const double u = s_us[gg][2 * i], vv = s_us[gg][2 * i + 1];
+        const double aa = s_al[gg][4 * i + qa], ab = s_al[gg][4 * i + qb];
+        const double m1a = ca == 0 ? aa * fu : (ca == 1 ? 0.0 : aa * (uc - u));
+        const double m1b = cb == 0 ? ab * fu : (cb == 1 ? 0.0 : ab * (uc - u));
+        const double m2a = ca == 0 ? 0.0 : (ca == 1 ? aa * fv : aa * (vc - vv));
+        const double m2b = cb == 0 ? 0.0 : (cb == 1 ? ab * fv : ab * (vc - vv));
+        acc += m1a * m1b + m2a * m2b;
+      }
+      a[k] = active ? acc : 0.0;
+      v[k] = (k == j) ? 1.0 : 0.0;
     }
-    S.eig.A[e] = acc;
   }
+  int rank;
+  eig12_group(a, v, gb, j, active, rank);
+  // ut rows 8..11 (the four smallest singular values) = V columns of ranks 8..11
+  if (active && rank >= 8)
+#pragma unroll
+    for (int k = 0; k < 12; k++) s_ut[g][(rank - 8) * 12 + k] = v[k];
   __syncthreads();
-  eig12_block(S.eig);
+  if (!active) return;
   double* rec = o.hrec + (size_t)kHypRec * h;
-  for (int e = tid; e < 48; e += 64) rec[R_UT + e] = S.eig.ut[96 + e];
-  if (tid < 20) rec[R_AL + tid] = S.alphas[tid];
-  if (tid < 15) rec[R_PW + tid] = S.pws[tid];
-  if (tid < 10) rec[R_US + tid] = S.us[tid];
-  if (tid == 0) {
+  for (int e = j; e < 48; e += 12) rec[R_UT + e] = s_ut[g][e];
+  for (int e = j; e < 20; e += 12) rec[R_AL + e] = s_al[g][e];
+  for (int e = j; e < 15; e += 12) rec[R_PW + e] = s_pws[g][e];
+  if (j < 10) rec[R_US + j] = s_us[g][j];
+  if (j == 0) {
     double L[60];
-    compute_L_6x10(S.eig.ut, L);
+    compute_L_6x10(s_ut[g], L);
 #pragma unroll
     for (int i = 0; i < 60; i++) rec[R_L + i] = L[i];
-    const double* cws = S.cws;
+    const double* cws = s_cws[g];
     rec[R_RHO + 0] = d_dist2(cws + 0, cws + 3);
     rec[R_RHO + 1] = d_dist2(cws + 0, cws + 6);
     rec[R_RHO + 2] = d_dist2(cws + 0, cws + 9);
@@ -691,9 +685,8 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
 // one lane per (hypothesis, object) for beta estimate V (betas_approx_V + gauss_newton +
 // compute_R_and_t); each variant is its own launch so a wave runs one code path
 template <int V>
-__global__ __launch_bounds__(64) void k_pnp_beta(PnPObject* objs, int max_iters) {
+__device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
   const int h = blockIdx.x * 64 + threadIdx.x;
-  PnPObject& o = objs[blockIdx.y];
   const int n = *o.n;
   if (h >= max_iters || n < 5) return;
   const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
@@ -777,6 +770,18 @@ __global__ __launch_bounds__(64) void k_pnp_beta(PnPObject* objs, int max_iters)
   for (int i = 0; i < 9; i++) out[1 + i] = R[i];
 #pragma unroll
   for (int i = 0; i < 3; i++) out[10 + i] = t[i];
+}
+
+// the three estimates of every hypothesis run concurrently (blockIdx.z = estimate), each block on
+// one code path
+__global__ __launch_bounds__(64) void k_pnp_beta(PnPObject* objs, int max_iters) {
+  PnPObject& o = objs[blockIdx.y];
+  if (blockIdx.z == 0)
+    pnp_beta<1>(o, max_iters);
+  else if (blockIdx.z == 1)
+    pnp_beta<2>(o, max_iters);
+  else
+    pnp_beta<3>(o, max_iters);
 }
 
 // one workgroup per (hypothesis, object): inlier count + mask (PnPRansacCallback::computeError,
@@ -889,8 +894,8 @@ __global__ void k_pnp_select(PnPObject* objs, int max_iters) {
 // Record: the hypothesis-0 slot of hrec (free once the hypotheses are scored); R_AL holds cws,
 // R_PW the pseudo-inverse ci; hout slots 0..2 hold ccs of the three estimates.
 struct RefitSmem {
-  Eig12Smem eig;
   double red[4 * 80], sum[80];
+  double A[144], ut8[48];
   double cws[12], ci[9];
   int w[4], n;
 };
@@ -1034,18 +1039,33 @@ __global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
     for (int e = tid; e < 144; e += blockDim.x) {
       const int r = e / 12, c = e - 12 * r;
       const int lo = min(r, c), hi = max(r, c);
-      S.eig.A[e] = S.sum[lo * 12 - lo * (lo - 1) / 2 + (hi - lo)];
+      S.A[e] = S.sum[lo * 12 - lo * (lo - 1) / 2 + (hi - lo)];
     }
     __syncthreads();
   }
-  eig12_block(S.eig);
+  if (wave == 0) {  // the eigen-solve runs on lanes 0..11 of wave 0
+    const bool act = lane < 12;
+    const int j = act ? lane : 0;
+    double a[12], v[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      a[k] = act ? S.A[12 * k + j] : 0.0;
+      v[k] = (act && k == j) ? 1.0 : 0.0;
+    }
+    int rank;
+    eig12_group(a, v, 0, act ? lane : 12 + (lane % 12), act, rank);
+    if (act && rank >= 8)
+#pragma unroll
+      for (int k = 0; k < 12; k++) S.ut8[(rank - 8) * 12 + k] = v[k];
+  }
+  __syncthreads();
   double* rec = o.hrec;
-  for (int e = tid; e < 48; e += blockDim.x) rec[R_UT + e] = S.eig.ut[96 + e];
+  for (int e = tid; e < 48; e += blockDim.x) rec[R_UT + e] = S.ut8[e];
   if (tid < 12) rec[R_AL + tid] = S.cws[tid];
   if (tid < 9) rec[R_PW + tid] = S.ci[tid];
   if (tid == 0) {
     double L[60];
-    compute_L_6x10(S.eig.ut, L);
+    compute_L_6x10(S.ut8, L);
 #pragma unroll
     for (int i = 0; i < 60; i++) rec[R_L + i] = L[i];
     const double* cws = S.cws;
@@ -1059,8 +1079,7 @@ __global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
 }
 
 template <int V>
-__global__ __launch_bounds__(64) void k_refit_beta(PnPObject* objs) {
-  PnPObject& o = objs[blockIdx.x];
+__device__ __forceinline__ void refit_beta(PnPObject& o) {
   if (threadIdx.x != 0 || o.result[0] < 0) return;
   const double* rec = o.hrec;
   double L[60], rho[6], betas[4], ccs[12];
@@ -1090,6 +1109,16 @@ __global__ __launch_bounds__(64) void k_refit_beta(PnPObject* objs) {
   double* out = o.hout + (size_t)kHypOut * (V - 1);
 #pragma unroll
   for (int i = 0; i < 12; i++) out[i] = pc2 < 0.0 ? -ccs[i] : ccs[i];
+}
+
+__global__ __launch_bounds__(64) void k_refit_beta(PnPObject* objs) {
+  PnPObject& o = objs[blockIdx.x];
+  if (blockIdx.y == 0)
+    refit_beta<1>(o);
+  else if (blockIdx.y == 1)
+    refit_beta<2>(o);
+  else
+    refit_beta<3>(o);
 }
 
 struct RefitRtSmem {
@@ -1254,17 +1283,14 @@ __global__ __launch_bounds__(256) void k_pnp_subset(PnPObject* objs) {
 
 void launch_pnp(PnPObject* d_objs, int nobj, int max_iters, hipStream_t st, bool gather) {
   if (gather) hipLaunchKernelGGL(k_pnp_gather, dim3(nobj), dim3(256), 0, st, d_objs);
-  hipLaunchKernelGGL(k_pnp_hyp, dim3(max_iters, nobj), dim3(64), 0, st, d_objs, max_iters);
-  const dim3 gb((max_iters + 63) / 64, nobj);
-  hipLaunchKernelGGL(k_pnp_beta<1>, gb, dim3(64), 0, st, d_objs, max_iters);
-  hipLaunchKernelGGL(k_pnp_beta<2>, gb, dim3(64), 0, st, d_objs, max_iters);
-  hipLaunchKernelGGL(k_pnp_beta<3>, gb, dim3(64), 0, st, d_objs, max_iters);
+  hipLaunchKernelGGL(k_pnp_hyp, dim3((max_iters + kHypPerBlock - 1) / kHypPerBlock, nobj), dim3(64),
+                     0, st, d_objs, max_iters);
+  hipLaunchKernelGGL(k_pnp_beta, dim3((max_iters + 63) / 64, nobj, 3), dim3(64), 0, st, d_objs,
+                     max_iters);
   hipLaunchKernelGGL(k_pnp_score, dim3(max_iters, nobj), dim3(256), 0, st, d_objs, max_iters);
   hipLaunchKernelGGL(k_pnp_select, dim3(nobj), dim3(64), 0, st, d_objs, max_iters);
   hipLaunchKernelGGL(k_refit_null, dim3(nobj), dim3(256), 0, st, d_objs);
-  hipLaunchKernelGGL(k_refit_beta<1>, dim3(nobj), dim3(64), 0, st, d_objs);
-  hipLaunchKernelGGL(k_refit_beta<2>, dim3(nobj), dim3(64), 0, st, d_objs);
-  hipLaunchKernelGGL(k_refit_beta<3>, dim3(nobj), dim3(64), 0, st, d_objs);
+  hipLaunchKernelGGL(k_refit_beta, dim3(nobj, 3), dim3(64), 0, st, d_objs);
   hipLaunchKernelGGL(k_refit_rt, dim3(nobj), dim3(256), 0, st, d_objs);
   hipLaunchKernelGGL(k_mm_inliers, dim3(nobj), dim3(256), 0, st, d_objs);
 }

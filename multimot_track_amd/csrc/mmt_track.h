@@ -29,6 +29,7 @@ struct ObjSampleSet {
   int32_t* label;
   int* count;
   int cap;
+  int* block_counts;  // per-workgroup counts of the two-pass compaction (64 ints)
 };
 
 // Current-frame arrays after the hand-off (mvSiftKeys/Depth, mvObjKeys/Depth, vSemObjLabel).

@@ -91,42 +91,106 @@ __global__ __launch_bounds__(1024) void k_static_samples(const mmt_kp* __restric
 }
 
 // B1 for one frame; single workgroup, grid positions in row-major order.
-__global__ __launch_bounds__(1024) void k_obj_samples(const float* __restrict__ depth,
-                                                      const float2* __restrict__ flow,
-                                                      const int32_t* __restrict__ mask, int W,
-                                                      int H, ObjSampleSet out) {
-  __shared__ int s_w[16];
-  const int gw = (W + 3) / 4, gh = (H + 3) / 4, n = gw * gh;
-  int base = 0;
-  for (int r0 = 0; r0 < n; r0 += blockDim.x) {
+// exclusive block-wide scan of one int per thread (thread order); returns the total
+__device__ __forceinline__ int block_scan_excl(int v, int* s_w, int& excl) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int w = 0; w < nw; w++) {
+    const int c = s_w[w];
+    if (w < wave) off += c;
+    tot += c;
+  }
+  excl = off + x - v;
+  __syncthreads();
+  return tot;
+}
+
+// B1: every 4th row/column, order-preserving, over kObjBlocks workgroups (one CU cannot pull the
+// ~2 MB of sampled rows fast enough).  Two passes: k_obj_count counts each workgroup's kept
+// samples, k_obj_write recomputes its flags, offsets by the counts of the workgroups before it
+// and writes in order.  Workgroup b owns grid positions [b*per, (b+1)*per).
+constexpr int kObjBlocks = 64;
+
+__device__ __forceinline__ bool obj_keep(const float* __restrict__ depth,
+                                         const float2* __restrict__ flow,
+                                         const int32_t* __restrict__ mask, int W, int H, int gw,
+                                         int g, int& lab, float& d, float2& fl) {
+  const int i = (g / gw) * 4, j = (g % gw) * 4;
+  const size_t p = (size_t)i * W + j;
+  lab = mask[p];
+  d = depth[p];
+  fl = flow[p];
+  if (!(lab != 0 && d < 25 && d > 0)) return false;
+  return (float)j + fl.x < (float)W && (float)j + fl.x > 0 && (float)i + fl.y < (float)H &&
+         (float)i + fl.y > 0;
+}
+
+__global__ __launch_bounds__(256) void k_obj_count(const float* __restrict__ depth,
+                                                   const float2* __restrict__ flow,
+                                                   const int32_t* __restrict__ mask, int W, int H,
+                                                   int* __restrict__ counts) {
+  __shared__ int s_w[4];
+  const int gw = (W + 3) / 4, n = gw * ((H + 3) / 4);
+  const int per = (n + kObjBlocks - 1) / kObjBlocks;
+  const int g0 = blockIdx.x * per, g1 = min(n, g0 + per);
+  int c = 0;
+  for (int g = g0 + (int)threadIdx.x; g < g1; g += blockDim.x) {
+    int lab;
+    float d;
+    float2 fl;
+    c += obj_keep(depth, flow, mask, W, H, gw, g, lab, d, fl) ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+__global__ __launch_bounds__(256) void k_obj_write(const float* __restrict__ depth,
+                                                   const float2* __restrict__ flow,
+                                                   const int32_t* __restrict__ mask, int W, int H,
+                                                   const int* __restrict__ counts,
+                                                   ObjSampleSet out) {
+  __shared__ int s_w[4];
+  __shared__ int s_base;
+  const int gw = (W + 3) / 4, n = gw * ((H + 3) / 4);
+  const int per = (n + kObjBlocks - 1) / kObjBlocks;
+  const int g0 = blockIdx.x * per, g1 = min(n, g0 + per);
+  if (threadIdx.x < 64) {
+    int b = 0;
+    for (int k = threadIdx.x; k < (int)blockIdx.x; k += 64) b += counts[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+    if (threadIdx.x == 0) s_base = b;
+  }
+  __syncthreads();
+  int base = s_base;
+  for (int r0 = g0; r0 < g1; r0 += blockDim.x) {
     const int g = r0 + threadIdx.x;
-    bool keep = false;
-    int i = 0, j = 0, lab = 0;
-    float fx = 0, fy = 0, d = 0;
-    if (g < n) {
-      i = (g / gw) * 4;
-      j = (g % gw) * 4;
-      const size_t p = (size_t)i * W + j;
-      lab = mask[p];
-      d = depth[p];
-      if (lab != 0 && d < 25 && d > 0) {
-        const float2 fl = flow[p];
-        fx = fl.x;
-        fy = fl.y;
-        keep = (float)j + fx < (float)W && (float)j + fx > 0 && (float)i + fy < (float)H &&
-               (float)i + fy > 0;
-      }
-    }
+    int lab = 0;
+    float d = 0;
+    float2 fl = make_float2(0.f, 0.f);
+    const bool keep = g < g1 && obj_keep(depth, flow, mask, W, H, gw, g, lab, d, fl);
     const int slot = wg_compact_slot(keep, s_w, base);
     if (keep && slot < out.cap) {
+      const int i = (g / gw) * 4, j = (g % gw) * 4;
       out.keys[slot] = make_float2((float)j, (float)i);
-      out.corres[slot] = make_float2((float)j + fx, (float)i + fy);
-      out.flow[slot] = make_float2(fx, fy);
+      out.corres[slot] = make_float2((float)j + fl.x, (float)i + fl.y);
+      out.flow[slot] = fl;
       out.depth[slot] = d;
       out.label[slot] = lab;
     }
   }
-  if (threadIdx.x == 0) *out.count = min(base, out.cap);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *out.count = min(base, out.cap);
 }
 
 // B4: current keys = last correspondences; depth (and label) at std::round coordinates.
@@ -188,6 +252,8 @@ __device__ __forceinline__ void unproject_world(const float* T, float fx, float 
 }
 
 // B6 + B7 statistics for one frame; single workgroup of 1024 threads.
+constexpr int kDepthChunk = 512;
+
 __global__ __launch_bounds__(1024) void k_obj_group(GroupArgs a) {
   __shared__ int s_cnt[kMaxLabel], s_bcnt[kMaxLabel], s_sfcnt[kMaxLabel];
   __shared__ int s_wl[16 * kMaxLabel];
@@ -253,17 +319,35 @@ __global__ __launch_bounds__(1024) void k_obj_group(GroupArgs a) {
     }
     __syncthreads();
   }
-  // ordered float depth sums (obj_center_depth accumulates in index order, Tracking.cc:1473)
+  // ordered float depth sums (obj_center_depth accumulates in index order, Tracking.cc:1473):
+  // float addition is not associative, so each label's sum stays sequential -- but over depths
+  // gathered into LDS in parallel, chunk by chunk, instead of dependent global loads
+  __shared__ float s_dep[kMaxLabel][kDepthChunk];
+  __shared__ int s_m[kMaxLabel];
+  if (tid < kMaxLabel) s_m[tid] = min(base[tid], a.member_cap);
+  __syncthreads();
+  int mmax = 0;
+  for (int l = 0; l < kMaxLabel; l++) mmax = max(mmax, s_m[l]);
+  float dsum = 0;
+  for (int c0 = 0; c0 < mmax; c0 += kDepthChunk) {
+    for (int e = tid; e < kMaxLabel * kDepthChunk; e += blockDim.x) {
+      const int l = e / kDepthChunk, k = e - l * kDepthChunk;
+      if (c0 + k < s_m[l]) s_dep[l][k] = a.cur_depth[a.members[l * a.member_cap + c0 + k]];
+    }
+    __syncthreads();
+    if (tid < kMaxLabel) {
+      const int m = min(s_m[tid] - c0, kDepthChunk);
+      for (int k = 0; k < m; k++) dsum = dsum + s_dep[tid][k];
+    }
+    __syncthreads();
+  }
   if (tid < kMaxLabel) {
     const int l = tid;
-    const int m = min(base[l], a.member_cap);
-    float s = 0;
-    for (int k = 0; k < m; k++) s = s + a.cur_depth[a.members[l * a.member_cap + k]];
     a.stats[l].cnt = s_cnt[l];
     a.stats[l].bcnt = s_bcnt[l];
     a.stats[l].sfcnt = s_sfcnt[l];
-    a.stats[l].depth_sum = s;
-    a.stats[l].members = m;
+    a.stats[l].depth_sum = dsum;
+    a.stats[l].members = s_m[l];
   }
   for (int i = tid; i < kMaxLabel * kMaxLabel; i += blockDim.x) a.hist[i] = s_hist[i];
 }
@@ -289,7 +373,10 @@ void launch_static_samples(const mmt_kp* kps, const int* nkp, const float* depth
 
 void launch_obj_samples(const float* depth, const float2* flow, const int32_t* mask, int W,
                         int H, const ObjSampleSet& out, hipStream_t st) {
-  hipLaunchKernelGGL(k_obj_samples, dim3(1), dim3(1024), 0, st, depth, flow, mask, W, H, out);
+  hipLaunchKernelGGL(k_obj_count, dim3(kObjBlocks), dim3(256), 0, st, depth, flow, mask, W, H,
+                     out.block_counts);
+  hipLaunchKernelGGL(k_obj_write, dim3(kObjBlocks), dim3(256), 0, st, depth, flow, mask, W, H,
+                     out.block_counts, out);
 }
 
 void launch_handoff(const float2* last_corres, const int* n_last, const float2* last_ocorres,

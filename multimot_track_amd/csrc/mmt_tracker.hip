@@ -196,6 +196,7 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     F.ob.label = alloc<int32_t>(ocap_);
     F.ob.count = alloc<int>(1);
     F.ob.cap = ocap_;
+    F.ob.block_counts = alloc<int>(64);
     F.ho.skeys = alloc<float2>(kcap_);
     F.ho.sdepth = alloc<float>(kcap_);
     F.ho.ns = alloc<int>(1);

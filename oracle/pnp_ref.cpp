@@ -69,78 +69,63 @@ static void jacobi_eig_sym(int n, const double* Ain, double* d, double* vt) {
   }
 }
 
-// 12x12 symmetric eigen-decomposition for EPnP's M^T M by PARALLEL-ORDER Jacobi: each sweep is
-// 11 rounds of 6 disjoint (p, q) pairs (round-robin schedule, player 11 fixed); all six rotations
-// of a round take their angle from the matrix at the start of the round and are applied as
-// B = A J (columns), then A' = J^T B (rows), V' = V J.  This is the same Jacobi method as above
-// with an ordering the GPU executes one round per step (mmt_pnp.hip: eig12_block); both follow
-// this loop operation for operation.  Eigenvectors as rows of `vt`, descending eigenvalues.
+// EPnP's cvSVD(MtM, D, Ut, 0, MODIFY_A | U_T) (PnPsolver.cc:392-395 lineage) by one-sided
+// (Hestenes) Jacobi in PARALLEL ORDER: each sweep is 11 rounds of 6 disjoint column pairs
+// (round-robin schedule, column 11 fixed); a pair is rotated unless its columns are already
+// orthogonal to 1e-15 relative; sweeps stop when a whole sweep rotates nothing.  Disjoint pairs
+// touch disjoint columns, so the rounds equal sequential processing in schedule order; the GPU
+// (mmt_pnp.hip: eig12_group) runs one column per lane and follows this loop operation for
+// operation.  M^T M is symmetric PSD, so its singular vectors are its eigenvectors: `vt` rows are
+// the accumulated right vectors (V columns), ordered by descending column norm (= singular value).
 static inline void rr_partner(int r, int j, int& p, int& q) {
   const int k = j == 11 ? r : (j == r ? 11 : (2 * r - j + 22) % 11);
   p = std::min(j, k);
   q = std::max(j, k);
 }
 
-static void jacobi_eig12_rr(const double* Ain, double* d, double* vt) {
+static void jacobi_eig12(const double* Ain, double* vt) {
   const int n = 12;
-  double A[144], B[144], V[144], V2[144], c[12], s[12];
+  double A[144], V[144];  // row-major: A[k * 12 + j] = row k, column j
   memcpy(A, Ain, sizeof(A));
   for (int i = 0; i < 144; i++) V[i] = (i % 13 == 0) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 100; sweep++) {
-    // converged when the off-diagonal mass is below (1e-13)^2 of the diagonal's: rotations leave
-    // residues of order eps * |a_pp| behind, so an absolute threshold is never reached
-    double off = 0, dsum = 0;
-    for (int p = 0; p < n; p++) {
-      dsum += A[p * n + p] * A[p * n + p];
-      for (int q = p + 1; q < n; q++) off += A[p * n + q] * A[p * n + q];
-    }
-    if (off <= 1e-26 * dsum) break;
-    for (int r = 0; r < 11; r++) {
+    bool rotated = false;
+    for (int r = 0; r < 11; r++)
       for (int slot = 0; slot < 6; slot++) {
-        const int a = slot == 0 ? r : (r + slot) % 11, b = slot == 0 ? 11 : (r - slot + 11) % 11;
-        const int p = std::min(a, b), q = std::max(a, b);
-        const double apq = A[p * n + q];
-        if (std::fabs(apq) < 1e-300) {
-          c[p] = 1.0;
-          s[p] = 0.0;
-          continue;
-        }
-        const double app = A[p * n + p], aqq = A[q * n + q];
-        const double theta = (aqq - app) / (2 * apq);
-        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1));
-        c[p] = 1 / std::sqrt(t * t + 1);
-        s[p] = t * c[p];
-      }
-      for (int k = 0; k < n; k++)
-        for (int j = 0; j < n; j++) {
-          int p, q;
-          rr_partner(r, j, p, q);
-          const double cc = c[p], ss = s[p];
-          if (j == p) {
-            B[k * n + j] = cc * A[k * n + p] - ss * A[k * n + q];
-            V2[k * n + j] = cc * V[k * n + p] - ss * V[k * n + q];
-          } else {
-            B[k * n + j] = ss * A[k * n + p] + cc * A[k * n + q];
-            V2[k * n + j] = ss * V[k * n + p] + cc * V[k * n + q];
-          }
-        }
-      for (int i = 0; i < n; i++)
+        const int a0 = slot == 0 ? r : (r + slot) % 11, b0 = slot == 0 ? 11 : (r - slot + 11) % 11;
+        const int p = std::min(a0, b0), q = std::max(a0, b0);
+        double al = 0, be = 0, ga = 0;
         for (int k = 0; k < n; k++) {
-          int p, q;
-          rr_partner(r, i, p, q);
-          const double cc = c[p], ss = s[p];
-          A[i * n + k] = i == p ? cc * B[p * n + k] - ss * B[q * n + k]
-                                : ss * B[p * n + k] + cc * B[q * n + k];
+          al += A[k * n + p] * A[k * n + p];
+          be += A[k * n + q] * A[k * n + q];
+          ga += A[k * n + p] * A[k * n + q];
         }
-      memcpy(V, V2, sizeof(V));
-    }
+        if (std::fabs(ga) <= 1e-15 * std::sqrt(al * be) || ga == 0) continue;
+        rotated = true;
+        const double zeta = (be - al) / (2 * ga);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1 + zeta * zeta));
+        const double c = 1 / std::sqrt(1 + t * t), s = c * t;
+        for (int k = 0; k < n; k++) {
+          const double x = A[k * n + p], y = A[k * n + q];
+          A[k * n + p] = c * x - s * y;
+          A[k * n + q] = s * x + c * y;
+          const double vx = V[k * n + p], vy = V[k * n + q];
+          V[k * n + p] = c * vx - s * vy;
+          V[k * n + q] = s * vx + c * vy;
+        }
+      }
+    if (!rotated) break;
   }
-  for (int i = 0; i < n; i++) {  // stable descending order
+  double sig[12];
+  for (int j = 0; j < n; j++) {
+    double ss = 0;
+    for (int k = 0; k < n; k++) ss += A[k * n + j] * A[k * n + j];
+    sig[j] = std::sqrt(ss);
+  }
+  for (int j = 0; j < n; j++) {  // stable descending order
     int rank = 0;
-    for (int j = 0; j < n; j++)
-      rank += (A[j * 13] > A[i * 13]) || (j < i && A[j * 13] == A[i * 13]);
-    d[rank] = A[i * 13];
-    for (int k = 0; k < n; k++) vt[rank * n + k] = V[k * n + i];
+    for (int i = 0; i < n; i++) rank += (sig[i] > sig[j]) || (i < j && sig[i] == sig[j]);
+    for (int k = 0; k < n; k++) vt[rank * n + k] = V[k * n + j];
   }
 }
 
@@ -533,8 +518,8 @@ struct EPnP {
       for (int a = 0; a < 12; a++)
         for (int b = 0; b < 12; b++) mtm[12 * a + b] += M1[a] * M1[b] + M2[a] * M2[b];
     }
-    double d[12], ut[144];
-    jacobi_eig12_rr(mtm, d, ut);
+    double ut[144];
+    jacobi_eig12(mtm, ut);
     double L[60], rho[6];
     compute_L_6x10(ut, L);
     compute_rho(rho);
