@@ -302,6 +302,45 @@ __device__ inline void block_sum(const double (&v)[K], double* red, double* out)
   __syncthreads();
 }
 
+// Block sum of K <= 32 doubles per thread by an LDS transpose: every lane stores its K partials
+// in a row of a [64][33] tile per wave, lane k of each wave then sums column k (64 LDS reads,
+// four interleaved chains), and the per-wave partials are added.  Fewer cross-lane operations
+// than a shuffle tree when K is large.  `tile` holds 64 * 33 doubles per wave, `part` 32 per wave;
+// out[0..K) is visible to every thread on return.  blockDim <= 256.
+template <int K>
+__device__ inline void block_sum_t(const double (&v)[K], double* tile, double* part, double* out) {
+  static_assert(K <= 32, "block_sum_t: at most 32 values");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  double* t = tile + (size_t)wave * 64 * 33;
+#pragma unroll
+  for (int k = 0; k < K; k++) t[lane * 33 + k] = v[k];
+  __syncthreads();
+  if (lane < K) {
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll 4
+    for (int r = 0; r < 64; r += 4) {
+      s0 += t[(r + 0) * 33 + lane];
+      s1 += t[(r + 1) * 33 + lane];
+      s2 += t[(r + 2) * 33 + lane];
+      s3 += t[(r + 3) * 33 + lane];
+    }
+    const double s = (s0 + s1) + (s2 + s3);
+    if (nw == 1)
+      out[lane] = s;
+    else
+      part[wave * 32 + lane] = s;
+  }
+  __syncthreads();
+  if (nw > 1) {
+    if (threadIdx.x < K) {
+      double s = 0;
+      for (int w = 0; w < nw; w++) s += part[w * 32 + threadIdx.x];
+      out[threadIdx.x] = s;
+    }
+    __syncthreads();
+  }
+}
+
 // Workgroup sum of K doubles held per thread; result broadcast in `out` (LDS, K entries).
 // `scratch` holds (blockDim/64) * K doubles.
 template <int K>

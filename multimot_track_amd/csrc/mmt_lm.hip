@@ -217,7 +217,7 @@ __device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const 
 // code; false when a pivot is negative.  The reduced camera system H_pp + lambda I - B D^-1 B^T
 // is SPD whenever lambda > 0, so the pivoting of Eigen's LDLT only moves rounding.
 __device__ __forceinline__ bool ldlt6(const double (&H)[36], const double (&b)[6], double (&x)[6]) {
-  double L[6][6], D[6];
+  double L[6][6], D[6], ID[6];
   bool positive = true;
 #pragma unroll
   for (int k = 0; k < 6; k++) {
@@ -227,6 +227,7 @@ __device__ __forceinline__ bool ldlt6(const double (&H)[36], const double (&b)[6
     D[k] = d;
     positive = positive && !(d < 0);
     const double id = d != 0 ? 1.0 / d : 0.0;
+    ID[k] = id;
 #pragma unroll
     for (int i = k + 1; i < 6; i++) {
       double s = H[6 * i + k];
@@ -244,7 +245,7 @@ __device__ __forceinline__ bool ldlt6(const double (&H)[36], const double (&b)[6
     y[i] = v;
   }
 #pragma unroll
-  for (int i = 0; i < 6; i++) y[i] = (D[i] != 0) ? y[i] * (1.0 / D[i]) : 0.0;
+  for (int i = 0; i < 6; i++) y[i] *= ID[i];
 #pragma unroll
   for (int i = 5; i >= 0; i--) {
     double v = y[i];
@@ -264,6 +265,7 @@ constexpr int kSums = 29;
 struct LMSmem {
   long long prof[8];
   double red[16 * 32];
+  double tile[4 * 64 * 33];  // block_sum_t transpose tiles (blockDim <= 256)
   double S27[32];
   double H[2][32];  // current / trial linearisation sums (kSums)
   double mh[16];
@@ -368,7 +370,7 @@ __global__ __launch_bounds__(MAXT) void k_flow_lm(const FlowSolveDesc* __restric
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mh = fmax(mh, __shfl_xor(mh, o, 64));
     if ((tid & 63) == 0) sm.mh[tid >> 6] = mh;
-    block_sum<kSums>(v, sm.red, sm.H[0]);
+    block_sum_t<kSums>(v, sm.tile, sm.red, sm.H[0]);
   }
   double cur = sm.H[0][0], lam, ni = 2, chk = 0;
   {
@@ -404,7 +406,8 @@ __global__ __launch_bounds__(MAXT) void k_flow_lm(const FlowSolveDesc* __restric
           item_load(G, cap, i, it);
           schur_terms(c, P, it, lam, ilam, v);
         }
-        block_sum<27>(v, sm.red, sm.S27);
+        MMT_LMPROF(4);
+        block_sum_t<27>(v, sm.tile, sm.red, sm.S27);
       }
       MMT_LMPROF(0);
       if (tid == 0) {
@@ -454,7 +457,8 @@ __global__ __launch_bounds__(MAXT) void k_flow_lm(const FlowSolveDesc* __restric
           update_terms(c, P, PN, it, i, ok2, lam, ilam, xb, v);
           item_store(G, cap, i, it);
         }
-        block_sum<kSums>(v, sm.red, sm.H[hs ^ 1]);
+        MMT_LMPROF(5);
+        block_sum_t<kSums>(v, sm.tile, sm.red, sm.H[hs ^ 1]);
       }
       MMT_LMPROF(2);
       // ---- g2o LM step acceptance and termination (every thread, same values)
@@ -521,6 +525,9 @@ __global__ __launch_bounds__(MAXT) void k_flow_lm(const FlowSolveDesc* __restric
         }
       }
       MMT_LMPROF(3);
+#ifdef MMT_LM_PROFILE
+      if (tid == 0) sm.prof[6]++;
+#endif
       if (!again) break;
     }
     if (bad) break;
@@ -546,8 +553,9 @@ __global__ __launch_bounds__(MAXT) void k_flow_lm(const FlowSolveDesc* __restric
     D.stats[1] = N - (int)sm.S27[0];
     D.stats[2] = 0;
 #ifdef MMT_LM_PROFILE
-    printf("lmprof N=%d iters=%d schur=%lld solve=%lld update=%lld decide=%lld\n", N, iters,
-           sm.prof[0], sm.prof[1], sm.prof[2], sm.prof[3]);
+    printf("lmprof N=%d T=%d iters=%d trials=%lld schur_pass=%lld schur_red=%lld solve=%lld "
+           "upd_pass=%lld upd_red=%lld decide=%lld\n", N, nt, iters, sm.prof[6], sm.prof[4],
+           sm.prof[0], sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3]);
 #endif
   }
 }
@@ -562,14 +570,17 @@ void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipSt
     if (e && sscanf(e, "%dx%d", &t, &r) == 2) return t * 100 + r;
     return 0;
   }();
-  auto r64 = [](int v) { return std::min(512, std::max(64, (v + 63) / 64 * 64)); };
+  auto r64 = [](int v) { return std::min(256, std::max(64, (v + 63) / 64 * 64)); };
   int threads, ir;
   if (force) {
     threads = force / 100;
     ir = force % 100;
-  } else if (n_hint <= 512) {
+  } else if (n_hint <= 256) {
     threads = r64(n_hint);
     ir = 1;
+  } else if (n_hint <= 512) {
+    threads = r64((n_hint + 1) / 2);
+    ir = 2;
   } else if (n_hint <= 1024) {
     threads = r64((n_hint + 3) / 4);
     ir = 4;
@@ -578,7 +589,7 @@ void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipSt
     ir = 8;
   }
   if (ir == 1)
-    hipLaunchKernelGGL((k_flow_lm<1, 512>), dim3(nsolves), dim3(threads), 0, st, d_descs);
+    hipLaunchKernelGGL((k_flow_lm<1, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
   else if (ir == 2)
     hipLaunchKernelGGL((k_flow_lm<2, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
   else if (ir == 4)

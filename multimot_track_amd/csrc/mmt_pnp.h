@@ -40,7 +40,10 @@ struct PnPObject {
 constexpr int kHypRec = 160;  // doubles per hypothesis record
 constexpr int kHypOut = 16;   // doubles per (hypothesis, beta variant) result
 
+// RANSAC + refit (everything but the motion-model check)
 void launch_pnp(PnPObject* d_objs, int nobj, int max_iters, hipStream_t st, bool gather = true);
+// motion-model inliers (needs PnPObject::MM, i.e. the previous frame's object motions)
+void launch_pnp_mm(PnPObject* d_objs, int nobj, hipStream_t st);
 void launch_pnp_subset(PnPObject* d_objs, int nobj, hipStream_t st);
 
 }  // namespace mmt

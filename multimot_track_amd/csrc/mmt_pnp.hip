@@ -1292,6 +1292,9 @@ void launch_pnp(PnPObject* d_objs, int nobj, int max_iters, hipStream_t st, bool
   hipLaunchKernelGGL(k_refit_null, dim3(nobj), dim3(256), 0, st, d_objs);
   hipLaunchKernelGGL(k_refit_beta, dim3(nobj, 3), dim3(64), 0, st, d_objs);
   hipLaunchKernelGGL(k_refit_rt, dim3(nobj), dim3(256), 0, st, d_objs);
+}
+
+void launch_pnp_mm(PnPObject* d_objs, int nobj, hipStream_t st) {
   hipLaunchKernelGGL(k_mm_inliers, dim3(nobj), dim3(256), 0, st, d_objs);
 }
 

@@ -60,12 +60,16 @@ class Tracker {
     std::vector<int> nModLabel, nSemPosition;
     std::vector<std::vector<float>> vObjMod;
   };
-  // object path of a frame whose ego pose is known, run while the next frame's ego solve is in
-  // flight (the two chains only meet through the pose)
-  struct Pending {
+  // Object work of one frame in flight.  Stage A (grouping, B7/B8, PnP-RANSAC) needs only the
+  // frame's pose and the previous frame's labels; stage B (motion-model check, D3) needs the
+  // previous frame's object motions, i.e. the previous frame's D3.  So stage A of frame f runs
+  // while D3 of frame f-1 is in flight, and both overlap the ego solve of frame f+1.
+  struct ObjFrame {
     bool active = false;
-    int cur = 0, last = 0, n_last_obj = 0;
+    int cur = 0, last = 0, par = 0, nobj = 0;
     FrameOut* out = nullptr;
+    std::vector<int> labels, LabId, PreObjID, members;
+    std::vector<PnPObject> po;
   };
   struct FrameArgs {
     const float* depth;
@@ -97,8 +101,11 @@ class Tracker {
   void ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st);
   // waits for the ego solve, updates the motion model, queues the frame's object path
   void ego_finish(FrameOut& out, hipStream_t st);
-  void track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStream_t st);
-  void run_pending();
+  void obj_stage_a(ObjFrame& F);    // grouping + B7/B8 + PnP-RANSAC launch (stream oa_)
+  void obj_stage_b(ObjFrame& F);    // MM check, model choice, D3 launch (stream ob_)
+  void obj_finish(ObjFrame& F);     // waits for D3, object motions, results
+  void obj_advance();               // one pipeline step after a frame's ego pose is known
+  void obj_flush();
 
   mmt_config cfg_{};
   OrbEngine* engine_ = nullptr;
@@ -107,7 +114,8 @@ class Tracker {
   int state_ = 0, cur_ = 0, last_ = 2;
   bool bFirstFrame_ = false, bSecondFrame_ = false, hasVelocity_ = false;
   float V_[16] = {0};
-  FrameSlot slot_[3];
+  static constexpr int kSlots = 4;  // frames f (ego), f-1 (stage A), f-2 (D3), f-3 (D3's last)
+  FrameSlot slot_[kSlots];
   // ego in flight; its device->host results land in pinned memory so the copies stay
   // asynchronous while the host drives the previous frame's object path
   struct EgoHost {
@@ -120,26 +128,27 @@ class Tracker {
   bool ego_pending_ = false;
   float ego_Tinit_[16];
   EgoHost* eh_ = nullptr;
-  Pending pend_;
-  hipStream_t ost_ = nullptr;  // object-path stream
+  ObjFrame qa_, fa_, fb_;  // queued (ego done), stage A done, stage B (D3) in flight
+  hipStream_t oa_ = nullptr, ob_ = nullptr;
   std::vector<void*> allocs_;
   uint8_t* d_gray_ = nullptr;
   float* d_depth_ = nullptr;
   mmt_kp* d_kps_ = nullptr;
   uint8_t* d_desc_ = nullptr;
   int* d_nkp_ = nullptr;
-  int32_t* d_obj_label_ = nullptr;
-  int* d_members_ = nullptr;
-  LabelStats* d_stats_ = nullptr;
-  int* d_hist_ = nullptr;
+  int32_t* d_obj_label_[2] = {nullptr, nullptr};
+  int* d_members_[2] = {nullptr, nullptr};
+  LabelStats* d_stats_[2] = {nullptr, nullptr};
+  int* d_hist_[2] = {nullptr, nullptr};
   int* d_err_ = nullptr;
   double* d_lm_scratch_ = nullptr;
   FlowSolveDesc* d_descs_ = nullptr;
   float* d_poses_ = nullptr;
   int* d_lmstats_ = nullptr;
-  PnPObject* d_pnp_ = nullptr;
-  PnPBuf pnp_[kMaxObj];
-  std::vector<int> h_subsets_[kMaxObj];
+  PnPObject* d_pnp_[2] = {nullptr, nullptr};
+  PnPBuf pnp_[2][kMaxObj];
+  std::vector<int> h_subsets_[2][kMaxObj];
+  int frame_par_ = 0;
   bool prof_ = false;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
   double orb_ms_ = 0;

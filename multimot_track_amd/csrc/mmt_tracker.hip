@@ -130,10 +130,11 @@ static T* dalloc(size_t n) {
 }
 
 Tracker::~Tracker() {
-  if (ost_) {
-    (void)hipStreamSynchronize(ost_);
-    (void)hipStreamDestroy(ost_);
-  }
+  for (hipStream_t* q : {&oa_, &ob_})
+    if (*q) {
+      (void)hipStreamSynchronize(*q);
+      (void)hipStreamDestroy(*q);
+    }
   for (void* p : allocs_) (void)hipFree(p);
   if (eh_) (void)hipHostFree(eh_);
   for (hipEvent_t& e : ev_orb_)
@@ -181,7 +182,7 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   d_kps_ = alloc<mmt_kp>((size_t)kcap_ * max_chunk);
   d_desc_ = alloc<uint8_t>((size_t)kcap_ * 32 * max_chunk);
   d_nkp_ = alloc<int>(max_chunk);
-  for (int s = 0; s < 3; s++) {
+  for (int s = 0; s < kSlots; s++) {
     FrameSlot& F = slot_[s];
     F.st.keys = alloc<float2>(kcap_);
     F.st.corres = alloc<float2>(kcap_);
@@ -207,10 +208,12 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     MMT_HIP(hipMemset(F.st.count, 0, sizeof(int)));
     MMT_HIP(hipMemset(F.ob.count, 0, sizeof(int)));
   }
-  d_obj_label_ = alloc<int32_t>(ocap_);
-  d_members_ = alloc<int>((size_t)kMaxLabel * ocap_);
-  d_stats_ = alloc<LabelStats>(kMaxLabel);
-  d_hist_ = alloc<int>(kMaxLabel * kMaxLabel);
+  for (int q = 0; q < 2; q++) {
+    d_obj_label_[q] = alloc<int32_t>(ocap_);
+    d_members_[q] = alloc<int>((size_t)kMaxLabel * ocap_);
+    d_stats_[q] = alloc<LabelStats>(kMaxLabel);
+    d_hist_[q] = alloc<int>(kMaxLabel * kMaxLabel);
+  }
   d_err_ = alloc<int>(1);
   MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
   // solves: 1 ego + up to kMaxObj objects
@@ -222,9 +225,10 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   d_lmstats_ = alloc<int>(3 * (1 + kMaxObj));
   // PnP
   mask_words_ = (ocap_ + 63) / 64;
-  d_pnp_ = alloc<PnPObject>(kMaxObj);
+  for (int q = 0; q < 2; q++) {
+  d_pnp_[q] = alloc<PnPObject>(kMaxObj);
   for (int o = 0; o < kMaxObj; o++) {
-    PnPBuf& b = pnp_[o];
+    PnPBuf& b = pnp_[q][o];
     b.pts3 = alloc<float>(3 * (size_t)ocap_);
     b.pts2 = alloc<float2>(ocap_);
     b.subsets = alloc<int>(5 * kRansacIters);
@@ -239,24 +243,35 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     b.n_subset = alloc<int>(1);
     b.result = alloc<int>(8);
     b.Rt = alloc<double>(12);
+    h_subsets_[q][o].resize(5 * kRansacIters);
   }
-  for (int o = 0; o < kMaxObj; o++) h_subsets_[o].resize(5 * kRansacIters);
-  MMT_HIP(hipStreamCreateWithFlags(&ost_, hipStreamNonBlocking));
+  }
+  // The two object stages need hardware queues of their own (streams beyond the runtime's
+  // GPU_MAX_HW_QUEUES share queues and serialise): the D3 stage, the longest chain, gets a
+  // high-priority stream, which the runtime maps to a separate queue.
+  int lo = 0, hi = 0;
+  MMT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  MMT_HIP(hipStreamCreateWithPriority(&oa_, hipStreamNonBlocking, lo));
+  MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, hi));
   MMT_HIP(hipHostMalloc((void**)&eh_, sizeof(EgoHost), hipHostMallocDefault));
   memset(eh_, 0, sizeof(EgoHost));
   reset();
 }
 
 void Tracker::reset() {
-  if (ost_) MMT_HIP(hipStreamSynchronize(ost_));
+  if (oa_) MMT_HIP(hipStreamSynchronize(oa_));
+  if (ob_) MMT_HIP(hipStreamSynchronize(ob_));
   state_ = 0;
   bFirstFrame_ = false;  // uninitialised member in the reference (Tracking.h:180): pinned false
   bSecondFrame_ = false;
   hasVelocity_ = false;
   cur_ = 0;
-  last_ = 2;
+  last_ = kSlots - 1;
   ego_pending_ = false;
-  pend_ = Pending();
+  qa_ = ObjFrame();
+  fa_ = ObjFrame();
+  fb_ = ObjFrame();
+  frame_par_ = 0;
   for (FrameSlot& F : slot_) {
     F.nModLabel.clear();
     F.nSemPosition.clear();
@@ -301,16 +316,30 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
     a.nkp = d_nkp_ + f;
     a.n_keys = nkp[f];
     ego_launch(a, outs[f], st);
-    run_pending();
+    obj_advance();
     ego_finish(outs[f], st);
   }
-  run_pending();  // the chunk's results are complete on return
+  obj_flush();  // the chunk's results are complete on return
 }
 
-void Tracker::run_pending() {
-  if (!pend_.active) return;
-  pend_.active = false;
-  track_objects(slot_[pend_.cur], slot_[pend_.last], *pend_.out, ost_);
+// One step of the object pipeline: finish D3 of the oldest frame, launch D3 of the next, run
+// stage A of the newest (whose ego pose is known).  Called while the next ego solve runs.
+void Tracker::obj_advance() {
+  if (fb_.active) obj_finish(fb_);  // D3 of frame f-2 done -> its object motions
+  if (fa_.active) {
+    obj_stage_b(fa_);  // MM check + D3 launch for frame f-1 (its RANSAC ran during the last step)
+    fb_ = fa_;
+    fa_ = ObjFrame();
+  }
+  if (qa_.active) {
+    obj_stage_a(qa_);  // grouping + RANSAC of frame f, overlapping D3 of frame f-1
+    fa_ = qa_;
+    qa_ = ObjFrame();
+  }
+}
+
+void Tracker::obj_flush() {
+  for (int k = 0; k < 3 && (qa_.active || fa_.active || fb_.active); k++) obj_advance();
 }
 
 void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
@@ -405,13 +434,16 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
     hasVelocity_ = true;
     memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
     out.initialized = true;
-    if (eh_->nlast_obj > 0) {
-      pend_.active = true;
-      pend_.cur = cur_;
-      pend_.last = last_;
-      pend_.n_last_obj = eh_->nlast_obj;
-      pend_.out = &out;
-    }
+    // queue the frame's object work (also when there are no object samples: its labels and
+    // motions must be reset for the next frame, in pipeline order)
+    qa_ = ObjFrame();
+    qa_.active = true;
+    qa_.cur = cur_;
+    qa_.last = last_;
+    qa_.par = frame_par_;
+    qa_.nobj = eh_->nlast_obj > 0 ? -1 : 0;  // -1: grouping decides
+    qa_.out = &out;
+    frame_par_ ^= 1;
   }
   ego_pending_ = false;
   if (advance) {
@@ -419,11 +451,19 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
     // already live in the slot, so this is an index rotation over three slots (the object path
     // of this frame still reads this slot and the previous one)
     last_ = cur_;
-    cur_ = (cur_ + 1) % 3;
+    cur_ = (cur_ + 1) % kSlots;
   }
 }
 
-void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStream_t st) {
+void Tracker::obj_stage_a(ObjFrame& F) {
+  FrameSlot& C = slot_[F.cur];
+  FrameSlot& Ls = slot_[F.last];
+  hipStream_t st = oa_;
+  const int q = F.par;
+  C.nModLabel.clear();
+  C.nSemPosition.clear();
+  C.vObjMod.clear();
+  if (F.nobj == 0) return;  // no object samples carried into this frame
   // ---- B6 + B7 statistics
   GroupArgs g;
   memset(&g, 0, sizeof(g));
@@ -439,18 +479,18 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStrea
   g.fx = cfg_.fx; g.fy = cfg_.fy; g.cx = cfg_.cx; g.cy = cfg_.cy;
   g.W = W_;
   g.H = H_;
-  g.obj_label = d_obj_label_;
-  g.members = d_members_;
+  g.obj_label = d_obj_label_[q];
+  g.members = d_members_[q];
   g.member_cap = ocap_;
-  g.stats = d_stats_;
-  g.hist = d_hist_;
+  g.stats = d_stats_[q];
+  g.hist = d_hist_[q];
   g.err = d_err_;
   launch_obj_group(g, st);
   LabelStats stats[kMaxLabel];
   int hist[kMaxLabel * kMaxLabel];
   int err = 0;
-  MMT_HIP(hipMemcpyAsync(stats, d_stats_, sizeof(stats), hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(hist, d_hist_, sizeof(hist), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(stats, d_stats_[q], sizeof(stats), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(hist, d_hist_[q], sizeof(hist), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(&err, d_err_, sizeof(int), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
   if (err) throw ArgError("semantic label outside [0, 15] on the object path");
@@ -503,16 +543,21 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStrea
   C.nModLabel = LabId;
   C.nSemPosition.assign(objLabelsNew.begin(), objLabelsNew.begin() + nobj);
   C.vObjMod.assign(nobj, std::vector<float>(16, 0.f));
+  F.nobj = nobj;
+  F.labels.assign(objLabelsNew.begin(), objLabelsNew.begin() + nobj);
+  F.LabId = LabId;
+  F.PreObjID.assign(nobj, -1);
+  F.members.assign(nobj, 0);
+  F.po.assign(nobj, PnPObject());
   if (nobj == 0) return;
-  // ---- D5: PnP-RANSAC per object (GetInitModelObj)
-  std::vector<PnPObject> po(nobj);
+  // ---- D5: PnP-RANSAC per object (GetInitModelObj), motion-model check deferred to stage B
   for (int i = 0; i < nobj; i++) {
     const int l = objLabelsNew[i];
-    PnPBuf& b = pnp_[i];
-    PnPObject& o = po[i];
+    PnPBuf& b = pnp_[q][i];
+    PnPObject& o = F.po[i];
     memset(&o, 0, sizeof(o));
-    o.n = &d_stats_[l].members;
-    o.members = d_members_ + (size_t)l * ocap_;
+    o.n = &d_stats_[q][l].members;
+    o.members = d_members_[q] + (size_t)l * ocap_;
     o.last_keys = Ls.ob.keys;
     o.last_depth = Ls.ob.depth;
     o.cur_keys = C.ho.okeys;
@@ -520,18 +565,17 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStrea
     o.fx = cfg_.fx; o.fy = cfg_.fy; o.cx = cfg_.cx; o.cy = cfg_.cy;
     o.reproj = 0.3;
     o.confidence = 0.98;
-    ransac_subsets(std::max(stats[l].members, 1), kRansacIters, h_subsets_[i]);
-    MMT_HIP(hipMemcpyAsync(b.subsets, h_subsets_[i].data(), sizeof(int) * 5 * kRansacIters,
+    F.members[i] = stats[l].members;
+    ransac_subsets(std::max(stats[l].members, 1), kRansacIters, h_subsets_[q][i]);
+    MMT_HIP(hipMemcpyAsync(b.subsets, h_subsets_[q][i].data(), sizeof(int) * 5 * kRansacIters,
                            hipMemcpyHostToDevice, st));
     o.subsets = b.subsets;
-    int PreObjID = -1;
     for (size_t k = 0; k < Ls.nModLabel.size(); k++)
       if (Ls.nModLabel[k] == LabId[i]) {
-        PreObjID = (int)k;
+        F.PreObjID[i] = (int)k;
         break;
       }
-    o.use_mm = PreObjID >= 0;
-    if (o.use_mm) mat4_mul(C.Tcw, Ls.vObjMod[PreObjID].data(), o.MM);
+    o.use_mm = F.PreObjID[i] >= 0;
     o.pts3 = b.pts3;
     o.pts2 = b.pts2;
     o.models = b.models;
@@ -547,42 +591,69 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStrea
     o.result = b.result;
     o.Rt = b.Rt;
   }
-  MMT_HIP(hipMemcpyAsync(d_pnp_, po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
-  launch_pnp(d_pnp_, nobj, kRansacIters, st);
+  MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice,
+                         st));
+  launch_pnp(d_pnp_[q], nobj, kRansacIters, st);
+}
+
+void Tracker::obj_stage_b(ObjFrame& F) {
+  FrameSlot& C = slot_[F.cur];
+  FrameSlot& Ls = slot_[F.last];
+  const int nobj = F.nobj, q = F.par;
+  FrameOut& out = *F.out;
+  if (nobj <= 0) return;
+  hipStream_t st = ob_;
+  // RANSAC results (stage A's stream), then the motion-model check with the previous frame's
+  // object motions, now final (Tracking.cc:4375-4405)
+  MMT_HIP(hipStreamSynchronize(oa_));
+  bool any_mm = false;
+  for (int i = 0; i < nobj; i++) {
+    PnPObject& o = F.po[i];
+    if (o.use_mm) {
+      mat4_mul(C.Tcw, Ls.vObjMod[F.PreObjID[i]].data(), o.MM);
+      any_mm = true;
+    }
+  }
+  if (any_mm) {
+    MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po.data(), sizeof(PnPObject) * nobj,
+                           hipMemcpyHostToDevice, st));
+    launch_pnp_mm(d_pnp_[q], nobj, st);
+  }
   std::vector<int> res(8 * nobj);
   std::vector<double> Rt(12 * nobj);
   for (int i = 0; i < nobj; i++) {
-    MMT_HIP(hipMemcpyAsync(&res[8 * i], pnp_[i].result, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
-    MMT_HIP(hipMemcpyAsync(&Rt[12 * i], pnp_[i].Rt, sizeof(double) * 12, hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipMemcpyAsync(&res[8 * i], pnp_[q][i].result, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipMemcpyAsync(&Rt[12 * i], pnp_[q][i].Rt, sizeof(double) * 12, hipMemcpyDeviceToHost, st));
   }
   MMT_HIP(hipStreamSynchronize(st));
   // ---- choose RANSAC model or motion model; D3 descriptors
   std::vector<FlowSolveDesc> descs(nobj);
   std::vector<std::vector<float>> inits(nobj, std::vector<float>(16));
   for (int i = 0; i < nobj; i++) {
+    PnPObject& o = F.po[i];
     const int n_ransac = res[8 * i + 0] >= 0 ? res[8 * i + 3] : 0;
-    const int n_mm = po[i].use_mm ? res[8 * i + 4] : -1;
+    const int n_mm = o.use_mm ? res[8 * i + 4] : -1;
     float Mod[16];
     mat4_eye(Mod);
     for (int r = 0; r < 3; r++) {
       for (int c = 0; c < 3; c++) Mod[4 * r + c] = (float)Rt[12 * i + 3 * r + c];
       Mod[4 * r + 3] = (float)Rt[12 * i + 9 + r];
     }
-    if (po[i].use_mm && !(n_ransac > n_mm)) {
-      po[i].use_mm_choice = 1;
-      memcpy(inits[i].data(), po[i].MM, 64);
+    if (o.use_mm && !(n_ransac > n_mm)) {
+      o.use_mm_choice = 1;
+      memcpy(inits[i].data(), o.MM, 64);
     } else {
-      po[i].use_mm_choice = 0;
+      o.use_mm_choice = 0;
       memcpy(inits[i].data(), Mod, 64);
     }
-    if (res[8 * i + 0] < 0 && !po[i].use_mm_choice) {
+    if (res[8 * i + 0] < 0 && !o.use_mm_choice) {
       // RANSAC found no model: empty inlier set (D3 then returns identity)
       res[8 * i + 3] = 0;
     }
     ObjOut oo;
-    oo.label = LabId[i];
-    oo.sem_label = objLabelsNew[i];
-    oo.n_points = stats[objLabelsNew[i]].members;
+    oo.label = F.LabId[i];
+    oo.sem_label = F.labels[i];
+    oo.n_points = F.members[i];
     oo.n_ransac_inliers = n_ransac;
     oo.n_mm_inliers = n_mm;
     oo.ransac_iterations = res[8 * i + 2];
@@ -590,8 +661,8 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStrea
     out.objects.push_back(oo);
     FlowSolveDesc& d = descs[i];
     memset(&d, 0, sizeof(d));
-    d.d_n = pnp_[i].n_subset;
-    d.idx = pnp_[i].subset;
+    d.d_n = pnp_[q][i].n_subset;
+    d.idx = pnp_[q][i].subset;
     d.obs = Ls.ob.keys;
     d.flow = Ls.ob.flow;
     d.depth = Ls.ob.depth;
@@ -607,20 +678,29 @@ void Tracker::track_objects(FrameSlot& C, FrameSlot& Ls, FrameOut& out, hipStrea
     d.pose_out = d_poses_ + 16 * (1 + i);
     d.stats = d_lmstats_ + 3 * (1 + i);
   }
-  MMT_HIP(hipMemcpyAsync(d_pnp_, po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
-  launch_pnp_subset(d_pnp_, nobj, st);
+  MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
+  launch_pnp_subset(d_pnp_[q], nobj, st);
   MMT_HIP(hipMemcpyAsync(d_descs_ + 1, descs.data(), sizeof(FlowSolveDesc) * nobj,
                          hipMemcpyHostToDevice, st));
   int n_hint = 0;
   for (int i = 0; i < nobj; i++)
-    n_hint = std::max(n_hint, po[i].use_mm_choice ? res[8 * i + 4] : res[8 * i + 3]);
+    n_hint = std::max(n_hint, F.po[i].use_mm_choice ? res[8 * i + 4] : res[8 * i + 3]);
   launch_flow_lm(d_descs_ + 1, nobj, n_hint, st);
+}
+
+void Tracker::obj_finish(ObjFrame& F) {
+  FrameSlot& C = slot_[F.cur];
+  const int nobj = F.nobj, q = F.par;
+  FrameOut& out = *F.out;
+  F.active = false;
+  if (nobj <= 0) return;
+  hipStream_t st = ob_;
   std::vector<float> X(16 * nobj);
   std::vector<int> lst(3 * nobj), nsub(nobj);
   MMT_HIP(hipMemcpyAsync(X.data(), d_poses_ + 16, sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(lst.data(), d_lmstats_ + 3, sizeof(int) * 3 * nobj, hipMemcpyDeviceToHost, st));
   for (int i = 0; i < nobj; i++)
-    MMT_HIP(hipMemcpyAsync(&nsub[i], pnp_[i].n_subset, sizeof(int), hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipMemcpyAsync(&nsub[i], pnp_[q][i].n_subset, sizeof(int), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
   float TcwInv[16];
   inv_mat(C.Tcw, TcwInv);
