@@ -276,20 +276,9 @@ struct LMSmem {
 
 }  // namespace
 
-template <int IR, int MAXT>
-__global__ __launch_bounds__(MAXT) void k_flow_lm(const FlowSolveDesc* __restrict__ descs) {
-  __shared__ LMSmem sm;
-  const FlowSolveDesc& D = descs[blockIdx.x];
+template <int IR>
+__device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSmem& sm) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  const int N = D.d_n ? min(*D.d_n, D.cap) : min(D.n, D.cap);
-  if (N < 3) {
-    if (tid == 0) {
-      D.stats[0] = 0;
-      D.stats[1] = 0;
-      D.stats[2] = 1;
-    }
-    return;
-  }
 #ifdef MMT_LM_PROFILE
   long long prof_t = 0;
   if (tid == 0)
@@ -560,42 +549,48 @@ __global__ __launch_bounds__(MAXT) void k_flow_lm(const FlowSolveDesc* __restric
   }
 }
 
-void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st) {
-  // Latency-bound: one correspondence per thread where the block allows it (a trial's passes
-  // cost about one correspondence's dependency chain), up to 512 threads x 4 register items; the
-  // kernel itself handles any N (items beyond spill to the scratch arrays).
-  static const int force = [] {  // MMT_LM_CONFIG=<threads>x<items>: tuning knob for tools/
-    const char* e = getenv("MMT_LM_CONFIG");
-    int t = 0, r = 0;
-    if (e && sscanf(e, "%dx%d", &t, &r) == 2) return t * 100 + r;
-    return 0;
-  }();
-  auto r64 = [](int v) { return std::min(256, std::max(64, (v + 63) / 64 * 64)); };
-  int threads, ir;
-  if (force) {
-    threads = force / 100;
-    ir = force % 100;
-  } else if (n_hint <= 256) {
-    threads = r64(n_hint);
-    ir = 1;
-  } else if (n_hint <= 512) {
-    threads = r64((n_hint + 1) / 2);
-    ir = 2;
-  } else if (n_hint <= 1024) {
-    threads = r64((n_hint + 3) / 4);
-    ir = 4;
-  } else {
-    threads = std::min(256, r64((n_hint + 7) / 8));
-    ir = 8;
+// One workgroup per solve; each workgroup picks the register-item count its own edge count needs,
+// so a small object solved in the same launch as a large one runs the short code path.
+template <int MAXIR>
+__global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict__ descs) {
+  __shared__ LMSmem sm;
+  const FlowSolveDesc& D = descs[blockIdx.x];
+  const int N = D.d_n ? min(*D.d_n, D.cap) : min(D.n, D.cap);
+  if (N < 3) {
+    if (threadIdx.x == 0) {
+      D.stats[0] = 0;
+      D.stats[1] = 0;
+      D.stats[2] = 1;
+    }
+    return;
   }
-  if (ir == 1)
-    hipLaunchKernelGGL((k_flow_lm<1, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
-  else if (ir == 2)
-    hipLaunchKernelGGL((k_flow_lm<2, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
-  else if (ir == 4)
-    hipLaunchKernelGGL((k_flow_lm<4, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
+  const int nt = blockDim.x;
+  if (N <= nt || MAXIR == 1)
+    flow_lm_body<1>(D, N, sm);
+  else if (N <= 2 * nt || MAXIR == 2)
+    flow_lm_body<2>(D, N, sm);
+  else if (N <= 4 * nt || MAXIR == 4)
+    flow_lm_body<4>(D, N, sm);
   else
-    hipLaunchKernelGGL((k_flow_lm<8, 256>), dim3(nsolves), dim3(std::min(threads, 256)), 0, st, d_descs);
+    flow_lm_body<8>(D, N, sm);
+}
+
+void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st) {
+  // Latency-bound: about one correspondence per thread where the block allows it (a trial's
+  // passes cost about one correspondence's dependency chain), 64..256 threads, up to 8 register
+  // items each; items beyond spill to the scratch arrays.  Each workgroup picks its own item
+  // count (k_flow_lm); n_hint (the largest edge count) only sizes the block.
+  static const int force = [] {  // MMT_LM_THREADS=<threads>: tuning knob for tools/
+    const char* e = getenv("MMT_LM_THREADS");
+    return e ? atoi(e) : 0;
+  }();
+  static const bool force8 = getenv("MMT_LM_MAXIR8") != nullptr;
+  int threads = std::min(256, std::max(64, (n_hint + 63) / 64 * 64));
+  if (force) threads = force;
+  if (n_hint <= 2 * threads && !force8)
+    hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs);
+  else
+    hipLaunchKernelGGL(k_flow_lm<8>, dim3(nsolves), dim3(threads), 0, st, d_descs);
 }
 
 size_t flow_scratch_doubles(int cap) { return (size_t)G_COUNT * cap; }

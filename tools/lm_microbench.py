@@ -1,6 +1,6 @@
 """Micro-benchmark of the flow-refined pose solve (mmt_pose_flow_solve probe) on synthetic
 problems of the sizes the tracker sees; run under rocprofv3 --kernel-trace --stats to get the
-per-launch kernel time.  MMT_LM_CONFIG=<threads>x<items> forces a launch configuration."""
+per-launch kernel time.  MMT_LM_THREADS=<threads> forces the block size."""
 import os
 import sys
 import time
