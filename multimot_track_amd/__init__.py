@@ -158,8 +158,8 @@ class Context:
         self.nlevels = cfg.orb_nlevels
 
     def close(self):
-        if getattr(self, "_h", None):
-            lib().mmt_destroy(self._h)
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.mmt_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -90,6 +90,7 @@ class OrbEngine {
  private:
   void release();
   int w_ = 0, h_ = 0, nlevels_ = 0, max_batch_ = 0, ncells_ = 0, ntiles_ = 0;
+  int fast_tile_max_ = 0, fast_win_max_ = 0;  // largest FAST cell tile / window (bytes)
   int total_slots_ = 0, out_slots_ = 0, cap_frame_ = 0, node_cap_ = 0;
   int iniTh_ = 20, minTh_ = 7;
   size_t pyr_stride_ = 0;

@@ -152,54 +152,96 @@ __device__ __forceinline__ int arc_strength(const uint8_t* t, int stride, int r,
 #define FAST_TILE_MAX 5184  // 72 x 72 tile
 #define FAST_WIN_MAX 4356   // 66 x 66 window
 
-// One workgroup per (cell, frame).  Cell = the submatrix the reference hands to cv::FAST.
+// Wave-level LDS ordering (no s_barrier): a wave's LDS writes are visible to its other lanes
+// after this point.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per (cell, frame); four cells per workgroup.  Cell = the submatrix the reference hands
+// to cv::FAST (ORBextractor.cc:791-816).  The wave stages the cell in its own LDS region, scores
+// every pixel once (arc strength M), then per threshold (iniTh, then minTh if the cell came out
+// empty) runs the cell-local 3x3 strict NMS and an order-preserving ballot compaction -- all
+// wave-synchronous, so cells of different sizes never wait for each other.
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                               const LevelInfo* __restrict__ lv,
                                               const CellInfo* __restrict__ cells, int ncells,
                                               uint32_t* __restrict__ keys, int total_slots,
-                                              int* __restrict__ cellcnt, int iniTh, int minTh) {
-  __shared__ uint8_t tile[FAST_TILE_MAX];
-  __shared__ uint8_t arcm[FAST_WIN_MAX];
-  __shared__ uint8_t score[FAST_WIN_MAX];
-  __shared__ int s_wave[4];
-  __shared__ int s_total;
-  const CellInfo ci = cells[blockIdx.x];
+                                              int* __restrict__ cellcnt, int iniTh, int minTh,
+                                              int tile_max, int win_max) {
+  extern __shared__ uint8_t fast_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cell = blockIdx.x * 4 + wave;
+  if (cell >= ncells) return;
+  const int per_wave = (tile_max + 4 * win_max + 31) & ~15;
+  uint8_t* tile = fast_lds + wave * per_wave;
+  uint8_t* arcm = tile + tile_max;
+  uint8_t* score = arcm + win_max;
+  uint16_t* cand_list = (uint16_t*)(((uintptr_t)(score + win_max) + 1) & ~(uintptr_t)1);
+  const CellInfo ci = cells[cell];
   const int frame = blockIdx.y;
   const LevelInfo L = lv[ci.level];
   const uint8_t* img = pyr + (size_t)frame * pyr_stride + L.off;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rows = ci.rows, cols = ci.cols;
-  for (int i = tid; i < rows * cols; i += 256) {
+  for (int i = lane; i < rows * cols; i += 64) {
     const int r = i / cols, c = i - r * cols;
     tile[i] = img[(size_t)(ci.r0 + r) * L.w + ci.c0 + c];
   }
-  __syncthreads();
+  wave_sync();
   const int R = rows - 6, C = cols - 6;  // detection window: tile rows 3..rows-4, cols 3..cols-4
   const int npx = R * C;
-  for (int p = tid; p < npx; p += 256) {
+  // Arc strength only where it can exceed the lower threshold: a 9-arc covers two adjacent
+  // compass points (0/4/8/12), so a pixel whose compass pairs all fail at t_lo has M <= t_lo and
+  // is no corner at either threshold (its arcm may then be stored as 0).  Candidates are
+  // compacted so the full 16-point test runs on dense lanes.
+  const int t_lo = min(min(max(iniTh, 0), 255), min(max(minTh, 0), 255));
+  int ncand = 0;
+  for (int p0 = 0; p0 < npx; p0 += 64) {
+    const int p = p0 + lane;
+    bool cand = false;
+    if (p < npx) {
+      const int r = p / C + 3, c = p - (p / C) * C + 3;
+      const int v = tile[r * cols + c];
+      const int d0 = v - tile[(r + 3) * cols + c], d4 = v - tile[r * cols + c + 3];
+      const int d8 = v - tile[(r - 3) * cols + c], d12 = v - tile[r * cols + c - 3];
+      const bool k0 = d0 > t_lo, k4 = d4 > t_lo, k8 = d8 > t_lo, k12 = d12 > t_lo;
+      const bool b0 = d0 < -t_lo, b4 = d4 < -t_lo, b8 = d8 < -t_lo, b12 = d12 < -t_lo;
+      cand = (k0 && k4) || (k4 && k8) || (k8 && k12) || (k12 && k0) || (b0 && b4) ||
+             (b4 && b8) || (b8 && b12) || (b12 && b0);
+      if (!cand) arcm[p] = 0;
+    }
+    const unsigned long long bal = __ballot(cand);
+    if (cand) cand_list[ncand + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)p;
+    ncand += __popcll(bal);
+  }
+  wave_sync();
+  for (int k = lane; k < ncand; k += 64) {
+    const int p = cand_list[k];
     const int r = p / C, c = p - r * C;
     const int m = arc_strength(tile, cols, r + 3, c + 3);
     arcm[p] = (uint8_t)(m < 0 ? 0 : m);
   }
-  __syncthreads();
+  wave_sync();
   uint32_t* out = keys + (size_t)frame * total_slots + ci.slot_off;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   int count = 0;
   for (int pass = 0; pass < 2; pass++) {
     const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
-    for (int p = tid; p < npx; p += 256) {
+    for (int p = lane; p < npx; p += 64) {
       const int m = arcm[p];
       score[p] = (uint8_t)(m > th ? m - 1 : 0);
     }
-    __syncthreads();
-    // order-preserving compaction of NMS survivors, 256 pixels per round
+    wave_sync();
     int base = 0;
-    for (int p0 = 0; p0 < npx; p0 += 256) {
-      const int p = p0 + tid;
+    for (int p0 = 0; p0 < npx; p0 += 64) {
+      const int p = p0 + lane;
       bool keep = false;
-      int s = 0;
+      int sc = 0;
       if (p < npx && arcm[p] > th) {
         const int r = p / C, c = p - r * C;
-        s = score[p];
+        sc = score[p];
         keep = true;
 #pragma unroll
         for (int dr = -1; dr <= 1; dr++)
@@ -208,31 +250,24 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
             if (dr == 0 && dc == 0) continue;
             const int rr = r + dr, cc = c + dc;
             const int ns = (rr >= 0 && rr < R && cc >= 0 && cc < C) ? score[rr * C + cc] : 0;
-            keep = keep && (s > ns);
+            keep = keep && (sc > ns);
           }
       }
       const unsigned long long bal = __ballot(keep);
-      const int rank = __popcll(bal & ((1ull << lane) - 1ull));
-      if (lane == 0) s_wave[wave] = __popcll(bal);
-      __syncthreads();
-      int woff = 0;
-      for (int w = 0; w < wave; w++) woff += s_wave[w];
-      const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
       if (keep) {
         const int r = p / C, c = p - r * C;
         const uint32_t x = (uint32_t)(ci.c0 - kMinBorder + c + 3);
         const uint32_t y = (uint32_t)(ci.r0 - kMinBorder + r + 3);
-        const int slot = base + woff + rank;
-        if (slot < ci.slot_cap) out[slot] = (y << 20) | (x << 8) | (uint32_t)s;
+        const int slot = base + __popcll(bal & lt);
+        if (slot < ci.slot_cap) out[slot] = (y << 20) | (x << 8) | (uint32_t)sc;
       }
-      base += tot;
-      __syncthreads();
+      base += __popcll(bal);
     }
     count = base;
     if (count > 0) break;
+    wave_sync();  // the next pass rewrites `score`
   }
-  if (tid == 0) cellcnt[(size_t)frame * ncells + blockIdx.x] = min(count, ci.slot_cap);
-  (void)s_total;
+  if (lane == 0) cellcnt[(size_t)frame * ncells + cell] = min(count, ci.slot_cap);
 }
 
 // ---------------------------------------------------------------- octree helpers
@@ -529,10 +564,10 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
   uint8_t* kq = (uint8_t*)(knode_g + (size_t)gridDim.y * total_slots) +
                 (size_t)frame * total_slots + L0.key_off;
   const uint32_t* fk = keys + (size_t)frame * total_slots;
-  for (int ci = 0; ci < nc; ci++) {
-    const CellInfo cell = cells[L0.cell_begin + ci];
-    const int m = cnt[ci], o = coff[ci];
-    for (int j = tid; j < m; j += nt) lk[o + j] = fk[cell.slot_off + j];
+  // one thread per cell (a cell holds at most a few dozen survivors)
+  for (int ci = tid; ci < nc; ci += nt) {
+    const int m = cnt[ci], o = coff[ci], so = cells[L0.cell_begin + ci].slot_off;
+    for (int j = 0; j < m; j++) lk[o + j] = fk[so + j];
   }
   __syncthreads();
   uint32_t* outp = okeys + (size_t)frame * out_slots + L0.out_off;
@@ -633,40 +668,61 @@ __device__ __forceinline__ int reflect101(int p, int n) {
   return p;
 }
 
+// GaussianBlur(7x7, sigma 2, REFLECT_101) of every level (ORBextractor.cc:1089-1090), bit-exact
+// 8U fixed point: horizontal Q8 taps -> 16-bit sums, vertical Q8 taps, (v + 2^15) >> 16.
+// One workgroup per (stripe of 256 columns, band of kBlurBand rows): the band is walked row by
+// row; each source row is staged once in LDS (double-buffered: one barrier per row), each thread
+// keeps the last seven horizontal sums of its column in registers and emits the vertical tap
+// sum.  Source rows are read once per band (+6 halo rows), outputs written once.
+constexpr int kBlurBand = 64;
+
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur, size_t pyr_stride,
                                               const LevelInfo* __restrict__ lv,
                                               const BlurTile* __restrict__ tiles) {
-  // taps of getGaussianKernelBitExact(7, 2) quantised to Q8 with error diffusion
-  const int T0 = 18, T1 = 34, T2 = 48, T3 = 56;
-  __shared__ uint8_t src[22][72];
-  __shared__ uint16_t hs[22][64];
+  const uint32_t T0 = 18, T1 = 34, T2 = 48, T3 = 56;
+  __shared__ uint8_t row[2][256 + 8];
   const BlurTile t = tiles[blockIdx.x];
   const LevelInfo L = lv[t.level];
   const size_t fo = (size_t)blockIdx.y * pyr_stride + L.off;
   const uint8_t* img = pyr + fo;
+  uint8_t* dst = blur + fo;
   const int tid = threadIdx.x;
-  for (int i = tid; i < 22 * 70; i += 256) {
-    const int r = i / 70, c = i - r * 70;
-    const int y = reflect101(min(t.y0 + r - 3, L.h + 2), L.h);
-    const int x = reflect101(min(t.x0 + c - 3, L.w + 2), L.w);
-    src[r][c] = img[(size_t)y * L.w + x];
+  const int x = t.x0 + tid;
+  const int y_end = min(t.y0 + kBlurBand, L.h);
+  // source columns of this stripe: x0-3 .. x0+258 (reflected at the level edges)
+  const bool edge = t.x0 == 0 || t.x0 + 259 > L.w;
+  int sx0 = 0, sx1 = 0;
+  {
+    const int c0 = t.x0 - 3 + tid;
+    sx0 = edge ? reflect101(min(c0, L.w + 2), L.w) : c0;
+    const int c1 = t.x0 - 3 + 256 + tid;
+    sx1 = tid < 6 ? (edge ? reflect101(min(c1, L.w + 2), L.w) : c1) : 0;
   }
-  __syncthreads();
-  for (int i = tid; i < 22 * 64; i += 256) {
-    const int r = i >> 6, c = i & 63;
-    const uint8_t* s = &src[r][c];
-    hs[r][c] = (uint16_t)(T0 * (s[0] + s[6]) + T1 * (s[1] + s[5]) + T2 * (s[2] + s[4]) + T3 * s[3]);
-  }
-  __syncthreads();
-  for (int i = tid; i < 16 * 64; i += 256) {
-    const int r = i >> 6, c = i & 63;
-    const int y = t.y0 + r, x = t.x0 + c;
-    if (y >= L.h || x >= L.w) continue;
-    const uint32_t v = T0 * ((uint32_t)hs[r][c] + hs[r + 6][c]) +
-                       T1 * ((uint32_t)hs[r + 1][c] + hs[r + 5][c]) +
-                       T2 * ((uint32_t)hs[r + 2][c] + hs[r + 4][c]) + T3 * (uint32_t)hs[r + 3][c];
-    blur[fo + (size_t)y * L.w + x] = (uint8_t)min((v + 32768u) >> 16, 255u);
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0, h6 = 0;
+  int buf = 0;
+  for (int r = t.y0 - 3; r < y_end + 3; r++) {
+    const int sy = reflect101(min(r, L.h + 2), L.h);
+    const uint8_t* srow = img + (size_t)sy * L.w;
+    row[buf][tid] = srow[sx0];
+    if (tid < 6) row[buf][256 + tid] = srow[sx1];
+    __syncthreads();
+    const uint8_t* s = &row[buf][tid];
+    const uint32_t hs = T0 * ((uint32_t)s[0] + s[6]) + T1 * ((uint32_t)s[1] + s[5]) +
+                        T2 * ((uint32_t)s[2] + s[4]) + T3 * (uint32_t)s[3];
+    h0 = h1;
+    h1 = h2;
+    h2 = h3;
+    h3 = h4;
+    h4 = h5;
+    h5 = h6;
+    h6 = hs;
+    const int yo = r - 3;
+    if (yo >= t.y0 && x < L.w) {
+      const uint32_t v = T0 * (h0 + h6) + T1 * (h1 + h5) + T2 * (h2 + h4) + T3 * h3;
+      dst[(size_t)yo * L.w + x] = (uint8_t)min((v + 32768u) >> 16, 255u);
+    }
+    buf ^= 1;
   }
 }
 
@@ -826,6 +882,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   minTh_ = t.minTh;
   lv_.assign(nlevels_, LevelInfo());
   cells_.clear();
+  fast_tile_max_ = fast_win_max_ = 0;
   int off = 0, key_off = 0, out_off = 0, maxN = 0;
   std::vector<ResizeX> xt;
   std::vector<ResizeY> yt;
@@ -865,6 +922,8 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
         c.cols = (int)maxX - (int)iniX;
         if (c.rows * c.cols > FAST_TILE_MAX || (c.rows - 6) * (c.cols - 6) > FAST_WIN_MAX)
           throw ArgError("FAST cell larger than the LDS tile");
+        fast_tile_max_ = std::max(fast_tile_max_, c.rows * c.cols);
+        fast_win_max_ = std::max(fast_win_max_, std::max(c.rows - 6, 0) * std::max(c.cols - 6, 0));
         const int R = std::max(c.rows - 6, 0), C = std::max(c.cols - 6, 0);
         c.slot_cap = ((R + 1) / 2) * ((C + 1) / 2);  // max strict-NMS survivors
         c.slot_off = key_off;
@@ -925,8 +984,8 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
         yt.push_back(r);
       }
     }
-    for (int y0 = 0; y0 < L.h; y0 += 16)
-      for (int x0 = 0; x0 < L.w; x0 += 64) tiles.push_back(BlurTile{l, x0, y0, 0});
+    for (int y0 = 0; y0 < L.h; y0 += kBlurBand)
+      for (int x0 = 0; x0 < L.w; x0 += 256) tiles.push_back(BlurTile{l, x0, y0, 0});
   }
   ncells_ = (int)cells_.size();
   ntiles_ = (int)tiles.size();
@@ -978,8 +1037,10 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
     hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, d_pyr_, pyr_stride_, S.off, S.w,
                        L.off, L.w, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l]);
   }
-  hipLaunchKernelGGL(k_fast, dim3(ncells_, nframes), dim3(256), 0, stream, d_pyr_, pyr_stride_,
-                     d_lv_, d_cells_, ncells_, d_keys_, total_slots_, d_cellcnt_, iniTh_, minTh_);
+  const int fast_per_wave = (fast_tile_max_ + 4 * fast_win_max_ + 31) & ~15;
+  hipLaunchKernelGGL(k_fast, dim3((ncells_ + 3) / 4, nframes), dim3(256), 4 * fast_per_wave, stream,
+                     d_pyr_, pyr_stride_, d_lv_, d_cells_, ncells_, d_keys_, total_slots_,
+                     d_cellcnt_, iniTh_, minTh_, fast_tile_max_, fast_win_max_);
   const size_t lds = octree_lds_bytes(node_cap_);
   hipLaunchKernelGGL(k_octree, dim3(nlevels_, nframes), dim3(1024), lds, stream, d_lv_, d_cells_,
                      ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,

@@ -8,8 +8,11 @@ import sys
 
 src, out = sys.argv[1], sys.argv[2]
 rows = []
-dbs = glob.glob(os.path.join(src, "**", "*.db"), recursive=True)
-csvs = glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True)
+# newest first: an output directory may hold earlier runs
+dbs = sorted(glob.glob(os.path.join(src, "**", "*.db"), recursive=True), key=os.path.getmtime,
+             reverse=True)
+csvs = sorted(glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True),
+              key=os.path.getmtime, reverse=True)
 if csvs:
     for r in csv.DictReader(open(csvs[0])):
         rows.append((r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]) / 1e3,

@@ -7,7 +7,8 @@ import sys
 
 src = sys.argv[1]
 tail_ms = float(sys.argv[2]) if len(sys.argv) > 2 else 3.0
-f = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)[0]
+f = sorted(glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True),
+           key=os.path.getmtime)[-1]
 rows = list(csv.DictReader(open(f)))
 ks = []
 for r in rows:
