@@ -83,25 +83,42 @@ void OrbTables::init(int nf, float scaleFactorF, int nl, int ini, int mn) {
 // ======================================================================== kernels
 
 // ---- pyramid level l from level l-1 (cv::resize INTER_LINEAR 8U, scalar fixed point) ----
+constexpr int kResizeRows = 8;  // output rows per workgroup (the x coefficients load once)
+
 __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride,
-                                                int src_off, int sw, int dst_off, int dw,
+                                                int src_off, int sw, int dst_off, int dw, int dh,
                                                 const ResizeX* __restrict__ xt,
                                                 const ResizeY* __restrict__ yt) {
   const int dx = blockIdx.x * 256 + threadIdx.x;
-  const int dy = blockIdx.y;
   if (dx >= dw) return;
   uint8_t* base = pyr + (size_t)blockIdx.z * pyr_stride;
   const uint8_t* src = base + src_off;
   const ResizeX cx = xt[dx];
-  const ResizeY cy = yt[dy];
-  const uint8_t* s0 = src + (size_t)cy.sy0 * sw + cx.sx;
-  const uint8_t* s1 = src + (size_t)cy.sy1 * sw + cx.sx;
-  // a1 == 0 marks the clamped right edge (dx >= xmax): only S[sx]*2048 contributes.
-  const int h0 = cx.a1 ? s0[0] * cx.a0 + s0[1] * cx.a1 : s0[0] * cx.a0;
-  const int h1 = cx.a1 ? s1[0] * cx.a0 + s1[1] * cx.a1 : s1[0] * cx.a0;
-  int v = (cy.b0 * h0 + cy.b1 * h1 + (1 << 21)) >> 22;
-  v = v < 0 ? 0 : (v > 255 ? 255 : v);
-  base[dst_off + (size_t)dy * dw + dx] = (uint8_t)v;
+  const int y0 = blockIdx.y * kResizeRows, y1 = min(y0 + kResizeRows, dh);
+  // all source loads of the band first (independent), then the arithmetic
+  int p00[kResizeRows], p01[kResizeRows], p10[kResizeRows], p11[kResizeRows];
+  ResizeY cy[kResizeRows];
+#pragma unroll
+  for (int k = 0; k < kResizeRows; k++) {
+    const int dy = min(y0 + k, dh - 1);
+    cy[k] = yt[dy];
+    const uint8_t* s0 = src + (size_t)cy[k].sy0 * sw + cx.sx;
+    const uint8_t* s1 = src + (size_t)cy[k].sy1 * sw + cx.sx;
+    p00[k] = s0[0];
+    p10[k] = s1[0];
+    // a1 == 0 marks the clamped right edge (dx >= xmax): only S[sx]*2048 contributes
+    p01[k] = cx.a1 ? s0[1] : 0;
+    p11[k] = cx.a1 ? s1[1] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kResizeRows; k++) {
+    if (y0 + k >= y1) break;
+    const int h0 = cx.a1 ? p00[k] * cx.a0 + p01[k] * cx.a1 : p00[k] * cx.a0;
+    const int h1 = cx.a1 ? p10[k] * cx.a0 + p11[k] * cx.a1 : p10[k] * cx.a0;
+    int v = (cy[k].b0 * h0 + cy[k].b1 * h1 + (1 << 21)) >> 22;
+    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+    base[dst_off + (size_t)(y0 + k) * dw + dx] = (uint8_t)v;
+  }
 }
 
 // ---- FAST arc strength: max over 9-arcs of min(v - p) (dark) and min(p - v) (bright). ----
@@ -670,59 +687,103 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 
 // GaussianBlur(7x7, sigma 2, REFLECT_101) of every level (ORBextractor.cc:1089-1090), bit-exact
 // 8U fixed point: horizontal Q8 taps -> 16-bit sums, vertical Q8 taps, (v + 2^15) >> 16.
-// One workgroup per (stripe of 256 columns, band of kBlurBand rows): the band is walked row by
-// row; each source row is staged once in LDS (double-buffered: one barrier per row), each thread
-// keeps the last seven horizontal sums of its column in registers and emits the vertical tap
-// sum.  Source rows are read once per band (+6 halo rows), outputs written once.
-constexpr int kBlurBand = 64;
+// One wave per (stripe of 256 columns, band of kBlurBand rows); each lane owns four adjacent
+// columns and walks the band: per row it loads the twelve source bytes around its columns as
+// three (unaligned) dwords, forms the four 7-tap horizontal sums with byte-aligned extracts and
+// two v_dot4_u32_u8 each, keeps the last seven rows of sums in a register ring (rows unrolled by
+// seven, so the ring never moves), and stores its four outputs as one dword.  No LDS, no
+// barriers.  Lanes whose columns touch the level edge gather their bytes with REFLECT_101.
+constexpr int kBlurBand = 32;
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
 
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur, size_t pyr_stride,
                                               const LevelInfo* __restrict__ lv,
-                                              const BlurTile* __restrict__ tiles) {
+                                              const BlurTile* __restrict__ tiles, int ntiles) {
   const uint32_t T0 = 18, T1 = 34, T2 = 48, T3 = 56;
-  __shared__ uint8_t row[2][256 + 8];
-  const BlurTile t = tiles[blockIdx.x];
+  const uint32_t W1 = T0 | (T1 << 8) | (T2 << 16) | (T3 << 24);  // bytes x-3+j .. x+j
+  const uint32_t W2 = T2 | (T1 << 8) | (T0 << 16);               // bytes x+1+j .. x+3+j, 0
+  const int tile_id = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile_id >= ntiles) return;
+  const int lane = threadIdx.x & 63;
+  const BlurTile t = tiles[tile_id];
   const LevelInfo L = lv[t.level];
   const size_t fo = (size_t)blockIdx.y * pyr_stride + L.off;
   const uint8_t* img = pyr + fo;
   uint8_t* dst = blur + fo;
-  const int tid = threadIdx.x;
-  const int x = t.x0 + tid;
+  const int x = t.x0 + 4 * lane;  // first of this lane's four columns
+  if (x >= L.w) return;
   const int y_end = min(t.y0 + kBlurBand, L.h);
-  // source columns of this stripe: x0-3 .. x0+258 (reflected at the level edges)
-  const bool edge = t.x0 == 0 || t.x0 + 259 > L.w;
-  int sx0 = 0, sx1 = 0;
-  {
-    const int c0 = t.x0 - 3 + tid;
-    sx0 = edge ? reflect101(min(c0, L.w + 2), L.w) : c0;
-    const int c1 = t.x0 - 3 + 256 + tid;
-    sx1 = tid < 6 ? (edge ? reflect101(min(c1, L.w + 2), L.w) : c1) : 0;
-  }
-  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0, h6 = 0;
-  int buf = 0;
-  for (int r = t.y0 - 3; r < y_end + 3; r++) {
+  const int ncols = min(4, L.w - x);
+  const bool edge = x < 4 || x + 8 > L.w;  // the 12 loaded bytes x-4 .. x+7 leave the row
+  int cx[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) cx[k] = reflect101(min(max(x - 4 + k, -4), L.w + 3), L.w);
+  auto load_row = [&](int r, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
     const int sy = reflect101(min(r, L.h + 2), L.h);
     const uint8_t* srow = img + (size_t)sy * L.w;
-    row[buf][tid] = srow[sx0];
-    if (tid < 6) row[buf][256 + tid] = srow[sx1];
-    __syncthreads();
-    const uint8_t* s = &row[buf][tid];
-    const uint32_t hs = T0 * ((uint32_t)s[0] + s[6]) + T1 * ((uint32_t)s[1] + s[5]) +
-                        T2 * ((uint32_t)s[2] + s[4]) + T3 * (uint32_t)s[3];
-    h0 = h1;
-    h1 = h2;
-    h2 = h3;
-    h3 = h4;
-    h4 = h5;
-    h5 = h6;
-    h6 = hs;
-    const int yo = r - 3;
-    if (yo >= t.y0 && x < L.w) {
-      const uint32_t v = T0 * (h0 + h6) + T1 * (h1 + h5) + T2 * (h2 + h4) + T3 * h3;
-      dst[(size_t)yo * L.w + x] = (uint8_t)min((v + 32768u) >> 16, 255u);
+    if (!edge) {
+      d0 = ld32(srow + x - 4);
+      d1 = ld32(srow + x);
+      d2 = ld32(srow + x + 4);
+    } else {
+      uint32_t b[12];
+#pragma unroll
+      for (int k = 0; k < 12; k++) b[k] = srow[cx[k]];
+      d0 = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+      d1 = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+      d2 = b[8] | (b[9] << 8) | (b[10] << 16) | (b[11] << 24);
     }
-    buf ^= 1;
+  };
+  uint32_t w[7][4];
+#pragma unroll
+  for (int i = 0; i < 7; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) w[i][j] = 0;
+  const int r_end = y_end + 3;
+  int r0 = t.y0 - 3;
+  for (; r0 < r_end; r0 += 7) {
+    uint32_t d[7][3];
+#pragma unroll
+    for (int g = 0; g < 7; g++) load_row(min(r0 + g, r_end - 1), d[g][0], d[g][1], d[g][2]);
+#pragma unroll
+    for (int g = 0; g < 7; g++) {
+      const int r = r0 + g;
+      if (r >= r_end) break;
+      // horizontal sums of the four columns -> ring slot g (rows of this group: slots 0..6)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t a = j < 3 ? __builtin_amdgcn_alignbyte(d[g][1], d[g][0], 1 + j) : d[g][1];
+        const uint32_t bb = j < 3 ? __builtin_amdgcn_alignbyte(d[g][2], d[g][1], 1 + j) : d[g][2];
+        w[g][j] = __builtin_amdgcn_udot4(bb, W2, __builtin_amdgcn_udot4(a, W1, 0u, false), false);
+      }
+      const int yo = r - 3;
+      if (yo >= t.y0) {
+        // rows yo-3 .. yo+3 live in ring slots g+1 .. g+7 (mod 7)
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t v = T0 * (w[(g + 1) % 7][j] + w[g][j]) +
+                             T1 * (w[(g + 2) % 7][j] + w[(g + 6) % 7][j]) +
+                             T2 * (w[(g + 3) % 7][j] + w[(g + 5) % 7][j]) + T3 * w[(g + 4) % 7][j];
+          o[j] = min((v + 32768u) >> 16, 255u);
+        }
+        uint8_t* dp = dst + (size_t)yo * L.w + x;
+        if (ncols == 4) {
+          const uint32_t packed = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+          __builtin_memcpy(dp, &packed, 4);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (j < ncols) dp[j] = (uint8_t)o[j];
+        }
+      }
+    }
   }
 }
 
@@ -1033,9 +1094,9 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
   for (int l = 1; l < nlevels_; l++) {
     const LevelInfo& S = lv_[l - 1];
     const LevelInfo& L = lv_[l];
-    dim3 grid((L.w + 255) / 256, L.h, nframes);
+    dim3 grid((L.w + 255) / 256, (L.h + kResizeRows - 1) / kResizeRows, nframes);
     hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, d_pyr_, pyr_stride_, S.off, S.w,
-                       L.off, L.w, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l]);
+                       L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l]);
   }
   const int fast_per_wave = (fast_tile_max_ + 4 * fast_win_max_ + 31) & ~15;
   hipLaunchKernelGGL(k_fast, dim3((ncells_ + 3) / 4, nframes), dim3(256), 4 * fast_per_wave, stream,
@@ -1045,8 +1106,8 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
   hipLaunchKernelGGL(k_octree, dim3(nlevels_, nframes), dim3(1024), lds, stream, d_lv_, d_cells_,
                      ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,
                      out_slots_, d_ocount_, nlevels_, node_cap_, d_err_);
-  hipLaunchKernelGGL(k_blur, dim3(ntiles_, nframes), dim3(256), 0, stream, d_pyr_, d_blur_,
-                     pyr_stride_, d_lv_, d_tiles_);
+  hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, stream, d_pyr_,
+                     d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
   const int waves = nframes * out_slots_;
   hipLaunchKernelGGL(k_orient_desc, dim3((waves + 3) / 4), dim3(256), 0, stream, d_pyr_, d_blur_,
                      pyr_stride_, d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_,
