@@ -26,9 +26,23 @@ namespace mmt {
 static const int kEdge = 19;       // EDGE_THRESHOLD
 static const int kMinBorder = 16;  // EDGE_THRESHOLD - 3
 
-__constant__ int c_pattern[1024] = {
+// bit_pattern_31_ (ORBextractor.cc:150-407), one int8 quadruple (x0, y0, x1, y1) per test
+constexpr int kPatternRaw[1024] = {
 #include "orb_pattern.inc"
 };
+struct PackedPattern {
+  uint32_t t[256];
+};
+constexpr PackedPattern pack_pattern() {
+  PackedPattern p{};
+  for (int i = 0; i < 256; i++)
+    p.t[i] = (uint32_t)(uint8_t)(int8_t)kPatternRaw[4 * i] |
+             (uint32_t)(uint8_t)(int8_t)kPatternRaw[4 * i + 1] << 8 |
+             (uint32_t)(uint8_t)(int8_t)kPatternRaw[4 * i + 2] << 16 |
+             (uint32_t)(uint8_t)(int8_t)kPatternRaw[4 * i + 3] << 24;
+  return p;
+}
+__constant__ PackedPattern c_pattern = pack_pattern();
 
 static inline int host_round(float v) { return (int)lrintf(v); }
 static inline int host_floor(float v) {
@@ -809,8 +823,16 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {
   return a;
 }
 
-// One wave per output keypoint slot: IC_Angle on the level (:77-104), rotated BRIEF on the
-// blurred level (:108-147), level-major assembly with coordinate scaling (:1079-1108).
+// Four output keypoint slots per wave, 16 lanes each: IC_Angle on the level (:77-104),
+// rotated BRIEF on the blurred level (:108-147), level-major assembly with coordinate scaling
+// (:1079-1108). Every load of a slot is independent of the others (no dependent chains), so a
+// wave keeps four keypoints' disc and pattern gathers in flight.
+__device__ __forceinline__ uint32_t ld16(const uint8_t* p) {
+  uint16_t v;
+  __builtin_memcpy(&v, p, 2);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k_orient_desc(
     const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur, size_t pyr_stride,
     const LevelInfo* __restrict__ lv, int nlevels, const int* __restrict__ umax,
@@ -818,51 +840,77 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     mmt_kp* __restrict__ kps, uint8_t* __restrict__ desc, int cap_frame, int* __restrict__ nkp,
     int nframes) {
   const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int frame = g / out_slots;
-  if (frame >= nframes) return;
-  const int local = g - frame * out_slots;
-  const int* oc = ocount + frame * nlevels;
-  if (local == 0 && lane == 0) {
-    int tot = 0;
-    for (int l = 0; l < nlevels; l++) tot += oc[l];
-    nkp[frame] = min(tot, cap_frame);
-  }
-  int level = 0, before = 0;
-  while (level + 1 < nlevels && local >= lv[level + 1].out_off) {
-    before += oc[level];
-    level++;
-  }
-  const LevelInfo L = lv[level];
-  const int s = local - L.out_off;
-  if (s >= oc[level]) return;
-  const int outi = before + s;
-  if (outi >= cap_frame) return;
+  const int gl = lane & 15, grp = lane >> 4;
+  const int slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + grp;
+  const int frame = slot / out_slots;
+  if (frame >= nframes) return;  // whole 16-lane groups leave together
+  const int local = slot - frame * out_slots;
+  // level lookup: lane gl of the group holds level gl's slot offset and count (nlevels <= 16);
+  // the level is a ballot count within the group and the keys before it a group sum
   const uint32_t k = okeys[(size_t)frame * out_slots + local];
+  int my_off = 0x7fffffff, my_cnt = 0, my_w = 0, my_loff = 0;
+  float my_scale = 0.f, my_size = 0.f;
+  if (gl < nlevels) {
+    my_off = lv[gl].out_off;
+    my_cnt = ocount[frame * nlevels + gl];
+    my_w = lv[gl].w;
+    my_loff = lv[gl].off;
+    my_scale = lv[gl].scale;
+    my_size = lv[gl].size;
+  }
+  const unsigned long long lb = __ballot(gl >= 1 && gl < nlevels && local >= my_off);
+  const int level = __popcll((lb >> (16 * grp)) & 0xFFFFull);
+  int before = gl < level ? my_cnt : 0, tot = my_cnt;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    before += __shfl_xor(before, o, 64);
+    tot += __shfl_xor(tot, o, 64);
+  }
+  const int src = 16 * grp + level;
+  const int lvl_off = __shfl(my_off, src, 64), lvl_cnt = __shfl(my_cnt, src, 64);
+  const int Lw = __shfl(my_w, src, 64);
+  const float Lscale = __shfl(my_scale, src, 64), Lsize = __shfl(my_size, src, 64);
+  const size_t fo = (size_t)frame * pyr_stride + __shfl(my_loff, src, 64);
+  if (local == 0 && gl == 0) nkp[frame] = min(tot, cap_frame);
+  const int sidx = local - lvl_off;
+  const int outi = before + sidx;
+  if (sidx >= lvl_cnt || outi >= cap_frame) return;
   const int kx = (int)((k >> 8) & 0xFFFu), ky = (int)(k >> 20);
   const float response = (float)(k & 0xFFu);
-  const size_t fo = (size_t)frame * pyr_stride + L.off;
-  // --- IC_Angle: lane u+15 owns column u of the radius-15 disc
-  const uint8_t* img = pyr + fo;
-  int m10 = 0, m01 = 0;
-  if (lane < 31) {
-    const int u = lane - 15;
-    const int au = u < 0 ? -u : u;
-    const uint8_t* col = img + (size_t)ky * L.w + kx + u;
-    int colsum = col[0];
-    int vs = 0;
-    for (int v = 1; v <= 15; v++) {
-      if (au <= umax[v]) {
-        const int vp = col[(size_t)v * L.w], vm = col[-(ptrdiff_t)v * L.w];
-        colsum += vp + vm;
-        vs += v * (vp - vm);
-      }
-    }
-    m10 = u * colsum;
-    m01 = vs;
-  }
+  // BRIEF tests 16r + gl of this lane (r = 0..15), fetched while the disc loads are in flight
+  uint32_t pat[16];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
+  for (int r = 0; r < 16; r++) pat[r] = c_pattern.t[16 * r + gl];
+  // --- IC_Angle: lane gl owns disc columns c0 = 2gl-15 and c0+1 (column 16 does not exist; the
+  // keypoint border, >= 19 px, keeps its byte inside the level)
+  const int c0 = 2 * gl - 15, c1 = c0 + 1;
+  const int a0 = c0 < 0 ? -c0 : c0, a1 = c1 < 0 ? -c1 : c1;
+  int vmax0 = 0, vmax1 = 0;
+#pragma unroll
+  for (int v = 1; v <= 15; v++) {
+    const int um = umax[v];
+    vmax0 += a0 <= um ? 1 : 0;
+    vmax1 += a1 <= um ? 1 : 0;
+  }
+  if (c1 > 15) vmax1 = -1;
+  // the whole 31 x 32 square is inside the level: load it unconditionally, mask afterwards
+  const uint8_t* col = pyr + fo + (size_t)ky * Lw + kx + c0;
+  uint32_t rows[31];
+#pragma unroll
+  for (int v = -15; v <= 15; v++) rows[v + 15] = ld16(col + (ptrdiff_t)v * Lw);
+  int cs0 = 0, cs1 = 0, vs = 0;
+#pragma unroll
+  for (int v = -15; v <= 15; v++) {
+    const int av = v < 0 ? -v : v;
+    const int p0 = av <= vmax0 ? (int)(rows[v + 15] & 0xFFu) : 0;
+    const int p1 = av <= vmax1 ? (int)(rows[v + 15] >> 8) : 0;
+    cs0 += p0;
+    cs1 += p1;
+    vs += v * (p0 + p1);
+  }
+  int m10 = c0 * cs0 + c1 * cs1, m01 = vs;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
     m10 += __shfl_xor(m10, o, 64);
     m01 += __shfl_xor(m01, o, 64);
   }
@@ -871,25 +919,33 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   const float factorPI = (float)(3.14159265358979323846 / 180.0);
   const float ang = angle * factorPI;
   const float a = (float)cos((double)ang), b = (float)sin((double)ang);
-  const uint8_t* center = blur + fo + (size_t)ky * L.w + kx;
-  const int step = L.w;
-  uint8_t* dout = desc + ((size_t)frame * cap_frame + outi) * 32;
-  for (int j = 0; j < 4; j++) {
-    const int t = j * 64 + lane;
-    const float x0 = (float)c_pattern[4 * t], y0 = (float)c_pattern[4 * t + 1];
-    const float x1 = (float)c_pattern[4 * t + 2], y1 = (float)c_pattern[4 * t + 3];
+  const uint8_t* center = blur + fo + (size_t)ky * Lw + kx;
+  int bits[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const float x0 = (float)(int8_t)(pat[r] & 0xFFu), y0 = (float)(int8_t)((pat[r] >> 8) & 0xFFu);
+    const float x1 = (float)(int8_t)((pat[r] >> 16) & 0xFFu), y1 = (float)(int8_t)(pat[r] >> 24);
     const float ry0 = x0 * b + y0 * a, rx0 = x0 * a - y0 * b;
     const float ry1 = x1 * b + y1 * a, rx1 = x1 * a - y1 * b;
-    const int v0 = center[__float2int_rn(ry0) * step + __float2int_rn(rx0)];
-    const int v1 = center[__float2int_rn(ry1) * step + __float2int_rn(rx1)];
-    const unsigned long long bal = __ballot(v0 < v1);
-    if (lane == j) *(unsigned long long*)(dout + 8 * j) = bal;
+    const int v0 = center[__float2int_rn(ry0) * Lw + __float2int_rn(rx0)];
+    const int v1 = center[__float2int_rn(ry1) * Lw + __float2int_rn(rx1)];
+    bits[r] = v0 < v1;
   }
-  if (lane == 0) {
+  // round r gives descriptor bytes 2r, 2r+1 (test 16r + gl -> byte 2r + gl/8, bit gl%8);
+  // lane gl < 8 stores bytes 4gl..4gl+3
+  uint32_t word = 0;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const uint32_t seg = (uint32_t)((__ballot(bits[r]) >> (16 * grp)) & 0xFFFFull);
+    if ((r >> 1) == gl) word |= seg << (16 * (r & 1));
+  }
+  uint8_t* dout = desc + ((size_t)frame * cap_frame + outi) * 32;
+  if (gl < 8) *(uint32_t*)(dout + 4 * gl) = word;
+  if (gl == 0) {
     mmt_kp kp;
-    kp.x = level == 0 ? (float)kx : (float)kx * L.scale;
-    kp.y = level == 0 ? (float)ky : (float)ky * L.scale;
-    kp.size = L.size;
+    kp.x = level == 0 ? (float)kx : (float)kx * Lscale;
+    kp.y = level == 0 ? (float)ky : (float)ky * Lscale;
+    kp.size = Lsize;
     kp.angle = angle;
     kp.response = response;
     kp.octave = level;
@@ -1108,7 +1164,7 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
                      out_slots_, d_ocount_, nlevels_, node_cap_, d_err_);
   hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, stream, d_pyr_,
                      d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
-  const int waves = nframes * out_slots_;
+  const int waves = (nframes * out_slots_ + 3) / 4;
   hipLaunchKernelGGL(k_orient_desc, dim3((waves + 3) / 4), dim3(256), 0, stream, d_pyr_, d_blur_,
                      pyr_stride_, d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_,
                      d_kps, d_desc, cap_per_frame, d_n, nframes);
