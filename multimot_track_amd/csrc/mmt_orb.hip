@@ -138,46 +138,57 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
 // ---- FAST arc strength: max over 9-arcs of min(v - p) (dark) and min(p - v) (bright). ----
 // A pixel is a FAST-9 corner at threshold t iff M > t, and OpenCV's cornerScore<16> returns
 // M - 1 for every corner (derivation in DESIGN.md), so one M per pixel serves both thresholds.
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+// (d, -d) per circle point as a packed int16 pair: the dark test (min of v - p over a 9-arc) and
+// the bright test (min of p - v) run in the two halves of one v_pk_min_i16 / v_pk_max_i16 chain.
 __device__ __forceinline__ int arc_strength(const uint8_t* t, int stride, int r, int c) {
   const int v = t[r * stride + c];
-  int d[16];
-  d[0] = v - t[(r + 3) * stride + c];
-  d[1] = v - t[(r + 3) * stride + c + 1];
-  d[2] = v - t[(r + 2) * stride + c + 2];
-  d[3] = v - t[(r + 1) * stride + c + 3];
-  d[4] = v - t[r * stride + c + 3];
-  d[5] = v - t[(r - 1) * stride + c + 3];
-  d[6] = v - t[(r - 2) * stride + c + 2];
-  d[7] = v - t[(r - 3) * stride + c + 1];
-  d[8] = v - t[(r - 3) * stride + c];
-  d[9] = v - t[(r - 3) * stride + c - 1];
-  d[10] = v - t[(r - 2) * stride + c - 2];
-  d[11] = v - t[(r - 1) * stride + c - 3];
-  d[12] = v - t[r * stride + c - 3];
-  d[13] = v - t[(r + 1) * stride + c - 3];
-  d[14] = v - t[(r + 2) * stride + c - 2];
-  d[15] = v - t[(r + 3) * stride + c - 1];
-  int mn2[16], mx2[16];
+  int q[16];
+  q[0] = t[(r + 3) * stride + c];
+  q[1] = t[(r + 3) * stride + c + 1];
+  q[2] = t[(r + 2) * stride + c + 2];
+  q[3] = t[(r + 1) * stride + c + 3];
+  q[4] = t[r * stride + c + 3];
+  q[5] = t[(r - 1) * stride + c + 3];
+  q[6] = t[(r - 2) * stride + c + 2];
+  q[7] = t[(r - 3) * stride + c + 1];
+  q[8] = t[(r - 3) * stride + c];
+  q[9] = t[(r - 3) * stride + c - 1];
+  q[10] = t[(r - 2) * stride + c - 2];
+  q[11] = t[(r - 1) * stride + c - 3];
+  q[12] = t[r * stride + c - 3];
+  q[13] = t[(r + 1) * stride + c - 3];
+  q[14] = t[(r + 2) * stride + c - 2];
+  q[15] = t[(r + 3) * stride + c - 1];
+  short2v d[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) d[k] = short2v{(short)(v - q[k]), (short)(q[k] - v)};
+  short2v mn2[16], mn4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) mn2[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
+#pragma unroll
+  for (int k = 0; k < 16; k++) mn4[k] = __builtin_elementwise_min(mn2[k], mn2[(k + 2) & 15]);
+  short2v best = short2v{-1000, -1000};
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const int a = d[k], b = d[(k + 1) & 15];
-    mn2[k] = min(a, b);
-    mx2[k] = max(a, b);
+    const short2v mn9 = __builtin_elementwise_min(
+        __builtin_elementwise_min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+    best = __builtin_elementwise_max(best, mn9);
   }
-  int mn4[16], mx4[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-  }
-  int best = -1000;
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-    const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-    best = max(best, max(mn9, -mx9));
-  }
-  return best;
+  return max((int)best.x, (int)best.y);
+}
+
+// p -> (p / C, p % C) for p < 2^13, C <= 72: (p + 0.5) / C sits at least 0.5 / C away from an
+// integer, far beyond the float error, so the truncation is exact
+__device__ __forceinline__ int div_small(int p, float invC) {
+  return (int)(((float)p + 0.5f) * invC);
+}
+
+__device__ __forceinline__ uint32_t ldg32(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
 }
 
 #define FAST_TILE_MAX 5184  // 72 x 72 tile
@@ -215,14 +226,21 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
   const int frame = blockIdx.y;
   const LevelInfo L = lv[ci.level];
   const uint8_t* img = pyr + (size_t)frame * pyr_stride + L.off;
-  const int rows = ci.rows, cols = ci.cols;
-  for (int i = lane; i < rows * cols; i += 64) {
-    const int r = i / cols, c = i - r * cols;
-    tile[i] = img[(size_t)(ci.r0 + r) * L.w + ci.c0 + c];
+  const int rows = ci.rows, cols = (ci.cols + 3) & ~3;  // LDS row stride: whole dwords
+  {
+    // dword copy (the pyramid allocation has slack for the <= 3 bytes past the last row)
+    const int nq = cols >> 2;
+    const float inv_nq = 1.0f / (float)nq;
+    const uint8_t* src = img + (size_t)ci.r0 * L.w + ci.c0;
+    for (int i = lane; i < rows * nq; i += 64) {
+      const int r = div_small(i, inv_nq), q = i - r * nq;
+      *(uint32_t*)(tile + 4 * i) = ldg32(src + (size_t)r * L.w + 4 * q);
+    }
   }
   wave_sync();
-  const int R = rows - 6, C = cols - 6;  // detection window: tile rows 3..rows-4, cols 3..cols-4
+  const int R = rows - 6, C = ci.cols - 6;  // detection window: tile rows 3..rows-4, cols 3..-4
   const int npx = R * C;
+  const float invC = 1.0f / (float)C;
   // Arc strength only where it can exceed the lower threshold: a 9-arc covers two adjacent
   // compass points (0/4/8/12), so a pixel whose compass pairs all fail at t_lo has M <= t_lo and
   // is no corner at either threshold (its arcm may then be stored as 0).  Candidates are
@@ -233,7 +251,8 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
     const int p = p0 + lane;
     bool cand = false;
     if (p < npx) {
-      const int r = p / C + 3, c = p - (p / C) * C + 3;
+      const int rq = div_small(p, invC);
+      const int r = rq + 3, c = p - rq * C + 3;
       const int v = tile[r * cols + c];
       const int d0 = v - tile[(r + 3) * cols + c], d4 = v - tile[r * cols + c + 3];
       const int d8 = v - tile[(r - 3) * cols + c], d12 = v - tile[r * cols + c - 3];
@@ -250,7 +269,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
   wave_sync();
   for (int k = lane; k < ncand; k += 64) {
     const int p = cand_list[k];
-    const int r = p / C, c = p - r * C;
+    const int r = div_small(p, invC), c = p - r * C;
     const int m = arc_strength(tile, cols, r + 3, c + 3);
     arcm[p] = (uint8_t)(m < 0 ? 0 : m);
   }
@@ -271,7 +290,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
       bool keep = false;
       int sc = 0;
       if (p < npx && arcm[p] > th) {
-        const int r = p / C, c = p - r * C;
+        const int r = div_small(p, invC), c = p - r * C;
         sc = score[p];
         keep = true;
 #pragma unroll
@@ -286,7 +305,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
       }
       const unsigned long long bal = __ballot(keep);
       if (keep) {
-        const int r = p / C, c = p - r * C;
+        const int r = div_small(p, invC), c = p - r * C;
         const uint32_t x = (uint32_t)(ci.c0 - kMinBorder + c + 3);
         const uint32_t y = (uint32_t)(ci.r0 - kMinBorder + r + 3);
         const int slot = base + __popcll(bal & lt);
@@ -1037,9 +1056,9 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
         c.c0 = (int)iniX;
         c.rows = (int)maxY - (int)iniY;
         c.cols = (int)maxX - (int)iniX;
-        if (c.rows * c.cols > FAST_TILE_MAX || (c.rows - 6) * (c.cols - 6) > FAST_WIN_MAX)
+        if (c.rows * ((c.cols + 3) & ~3) > FAST_TILE_MAX || (c.rows - 6) * (c.cols - 6) > FAST_WIN_MAX)
           throw ArgError("FAST cell larger than the LDS tile");
-        fast_tile_max_ = std::max(fast_tile_max_, c.rows * c.cols);
+        fast_tile_max_ = std::max(fast_tile_max_, c.rows * ((c.cols + 3) & ~3));
         fast_win_max_ = std::max(fast_win_max_, std::max(c.rows - 6, 0) * std::max(c.cols - 6, 0));
         const int R = std::max(c.rows - 6, 0), C = std::max(c.cols - 6, 0);
         c.slot_cap = ((R + 1) / 2) * ((C + 1) / 2);  // max strict-NMS survivors
@@ -1126,7 +1145,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   upload(&d_tiles_, tiles);
   upload(&d_umax_, t.umax);
   const size_t B = (size_t)max_batch_;
-  MMT_HIP(hipMalloc((void**)&d_pyr_, B * pyr_stride_));
+  MMT_HIP(hipMalloc((void**)&d_pyr_, B * pyr_stride_ + 64));  // + dword over-read slack
   MMT_HIP(hipMalloc((void**)&d_blur_, B * pyr_stride_));
   MMT_HIP(hipMalloc((void**)&d_keys_, B * total_slots_ * sizeof(uint32_t)));
   MMT_HIP(hipMalloc((void**)&d_lkeys_, B * total_slots_ * sizeof(uint32_t)));

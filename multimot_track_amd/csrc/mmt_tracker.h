@@ -69,7 +69,7 @@ class Tracker {
     int cur = 0, last = 0, par = 0, nobj = 0;
     FrameOut* out = nullptr;
     std::vector<int> labels, LabId, PreObjID, members;
-    std::vector<PnPObject> po;
+    PnPObject* po = nullptr;  // oh_[par]->po
   };
   struct FrameArgs {
     const float* depth;
@@ -129,6 +129,34 @@ class Tracker {
   float ego_Tinit_[16];
   EgoHost* eh_ = nullptr;
   ObjFrame qa_, fa_, fb_;  // queued (ego done), stage A done, stage B (D3) in flight
+  // Pinned host side of the object path, one per frame parity (frames f and f-1 are in flight
+  // at once): every host<->device transfer of stages A/B and the finish is a single asynchronous
+  // copy into or out of this block (pageable copies are staged synchronously by the runtime).
+  struct ObjHost {
+    LabelStats stats[kMaxLabel];
+    int hist[kMaxLabel * kMaxLabel];
+    int err;
+    PnPObject po[kMaxObj];
+    int subsets[kMaxObj][5 * kRansacIters];
+    int res[8 * kMaxObj];
+    double Rt[12 * kMaxObj];
+    FlowSolveDesc descs[kMaxObj];
+    float X[16 * kMaxObj];
+    int lst[3 * kMaxObj];
+    int nsub[kMaxObj];
+  };
+  ObjHost* oh_[2] = {nullptr, nullptr};
+  int* d_res_[2] = {nullptr, nullptr};     // PnP results of all objects, contiguous
+  double* d_Rt_[2] = {nullptr, nullptr};
+  int* d_nsub_[2] = {nullptr, nullptr};
+  // subset draws depend only on the point count: cache the last few counts
+  struct SubsetCache {
+    int count = -1;
+    std::vector<int> idx;
+  };
+  SubsetCache subset_cache_[16];
+  int subset_cache_next_ = 0;
+  const std::vector<int>& cached_subsets(int count);
   hipStream_t oa_ = nullptr, ob_ = nullptr;
   std::vector<void*> allocs_;
   uint8_t* d_gray_ = nullptr;
@@ -147,7 +175,6 @@ class Tracker {
   int* d_lmstats_ = nullptr;
   PnPObject* d_pnp_[2] = {nullptr, nullptr};
   PnPBuf pnp_[2][kMaxObj];
-  std::vector<int> h_subsets_[2][kMaxObj];
   int frame_par_ = 0;
   bool prof_ = false;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};

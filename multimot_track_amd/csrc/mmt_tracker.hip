@@ -122,6 +122,16 @@ void ransac_subsets(int count, int iters, std::vector<int>& idx) {
   }
 }
 
+const std::vector<int>& Tracker::cached_subsets(int count) {
+  for (SubsetCache& c : subset_cache_)
+    if (c.count == count) return c.idx;
+  SubsetCache& c = subset_cache_[subset_cache_next_];
+  subset_cache_next_ = (subset_cache_next_ + 1) % 16;
+  c.count = count;
+  ransac_subsets(count, kRansacIters, c.idx);
+  return c.idx;
+}
+
 template <typename T>
 static T* dalloc(size_t n) {
   T* p = nullptr;
@@ -137,6 +147,8 @@ Tracker::~Tracker() {
     }
   for (void* p : allocs_) (void)hipFree(p);
   if (eh_) (void)hipHostFree(eh_);
+  for (ObjHost* h : oh_)
+    if (h) (void)hipHostFree(h);
   for (hipEvent_t& e : ev_orb_)
     if (e) (void)hipEventDestroy(e);
 }
@@ -227,6 +239,11 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   mask_words_ = (ocap_ + 63) / 64;
   for (int q = 0; q < 2; q++) {
   d_pnp_[q] = alloc<PnPObject>(kMaxObj);
+  d_res_[q] = alloc<int>(8 * kMaxObj);
+  d_Rt_[q] = alloc<double>(12 * kMaxObj);
+  d_nsub_[q] = alloc<int>(kMaxObj);
+  if (!oh_[q]) MMT_HIP(hipHostMalloc((void**)&oh_[q], sizeof(ObjHost), hipHostMallocDefault));
+  memset(oh_[q], 0, sizeof(ObjHost));
   for (int o = 0; o < kMaxObj; o++) {
     PnPBuf& b = pnp_[q][o];
     b.pts3 = alloc<float>(3 * (size_t)ocap_);
@@ -240,10 +257,9 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     b.inliers = alloc<int>(ocap_);
     b.mm_inliers = alloc<int>(ocap_);
     b.subset = alloc<int>(ocap_);
-    b.n_subset = alloc<int>(1);
-    b.result = alloc<int>(8);
-    b.Rt = alloc<double>(12);
-    h_subsets_[q][o].resize(5 * kRansacIters);
+    b.n_subset = d_nsub_[q] + o;
+    b.result = d_res_[q] + 8 * o;
+    b.Rt = d_Rt_[q] + 12 * o;
   }
   }
   // The two object stages need hardware queues of their own (streams beyond the runtime's
@@ -486,14 +502,14 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   g.hist = d_hist_[q];
   g.err = d_err_;
   launch_obj_group(g, st);
-  LabelStats stats[kMaxLabel];
-  int hist[kMaxLabel * kMaxLabel];
-  int err = 0;
-  MMT_HIP(hipMemcpyAsync(stats, d_stats_[q], sizeof(stats), hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(hist, d_hist_[q], sizeof(hist), hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(&err, d_err_, sizeof(int), hipMemcpyDeviceToHost, st));
+  ObjHost& H = *oh_[q];
+  MMT_HIP(hipMemcpyAsync(H.stats, d_stats_[q], sizeof(H.stats), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(H.hist, d_hist_[q], sizeof(H.hist), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(&H.err, d_err_, sizeof(int), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
-  if (err) throw ArgError("semantic label outside [0, 15] on the object path");
+  if (H.err) throw ArgError("semantic label outside [0, 15] on the object path");
+  const LabelStats* stats = H.stats;
+  const int* hist = H.hist;
   // ---- B7 decisions (Tracking.cc:1424-1536); labels ascending = UniLab order
   std::vector<int> objLabelsNew;  // semantic label of each kept object
   for (int l = 1; l < kMaxLabel; l++) {
@@ -548,7 +564,7 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   F.LabId = LabId;
   F.PreObjID.assign(nobj, -1);
   F.members.assign(nobj, 0);
-  F.po.assign(nobj, PnPObject());
+  F.po = H.po;
   if (nobj == 0) return;
   // ---- D5: PnP-RANSAC per object (GetInitModelObj), motion-model check deferred to stage B
   for (int i = 0; i < nobj; i++) {
@@ -566,9 +582,10 @@ void Tracker::obj_stage_a(ObjFrame& F) {
     o.reproj = 0.3;
     o.confidence = 0.98;
     F.members[i] = stats[l].members;
-    ransac_subsets(std::max(stats[l].members, 1), kRansacIters, h_subsets_[q][i]);
-    MMT_HIP(hipMemcpyAsync(b.subsets, h_subsets_[q][i].data(), sizeof(int) * 5 * kRansacIters,
-                           hipMemcpyHostToDevice, st));
+    const std::vector<int>& sub = cached_subsets(std::max(stats[l].members, 1));
+    memcpy(H.subsets[i], sub.data(), sizeof(H.subsets[i]));
+    MMT_HIP(hipMemcpyAsync(b.subsets, H.subsets[i], sizeof(H.subsets[i]), hipMemcpyHostToDevice,
+                           st));
     o.subsets = b.subsets;
     for (size_t k = 0; k < Ls.nModLabel.size(); k++)
       if (Ls.nModLabel[k] == LabId[i]) {
@@ -591,8 +608,7 @@ void Tracker::obj_stage_a(ObjFrame& F) {
     o.result = b.result;
     o.Rt = b.Rt;
   }
-  MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice,
-                         st));
+  MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po, sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
   launch_pnp(d_pnp_[q], nobj, kRansacIters, st);
 }
 
@@ -615,19 +631,17 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     }
   }
   if (any_mm) {
-    MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po.data(), sizeof(PnPObject) * nobj,
-                           hipMemcpyHostToDevice, st));
+    MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po, sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
     launch_pnp_mm(d_pnp_[q], nobj, st);
   }
-  std::vector<int> res(8 * nobj);
-  std::vector<double> Rt(12 * nobj);
-  for (int i = 0; i < nobj; i++) {
-    MMT_HIP(hipMemcpyAsync(&res[8 * i], pnp_[q][i].result, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
-    MMT_HIP(hipMemcpyAsync(&Rt[12 * i], pnp_[q][i].Rt, sizeof(double) * 12, hipMemcpyDeviceToHost, st));
-  }
+  ObjHost& H = *oh_[q];
+  int* res = H.res;
+  double* Rt = H.Rt;
+  MMT_HIP(hipMemcpyAsync(res, d_res_[q], sizeof(int) * 8 * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(Rt, d_Rt_[q], sizeof(double) * 12 * nobj, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
   // ---- choose RANSAC model or motion model; D3 descriptors
-  std::vector<FlowSolveDesc> descs(nobj);
+  FlowSolveDesc* descs = H.descs;
   std::vector<std::vector<float>> inits(nobj, std::vector<float>(16));
   for (int i = 0; i < nobj; i++) {
     PnPObject& o = F.po[i];
@@ -678,10 +692,10 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     d.pose_out = d_poses_ + 16 * (1 + i);
     d.stats = d_lmstats_ + 3 * (1 + i);
   }
-  MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po.data(), sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
+  MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po, sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
   launch_pnp_subset(d_pnp_[q], nobj, st);
-  MMT_HIP(hipMemcpyAsync(d_descs_ + 1, descs.data(), sizeof(FlowSolveDesc) * nobj,
-                         hipMemcpyHostToDevice, st));
+  MMT_HIP(hipMemcpyAsync(d_descs_ + 1, descs, sizeof(FlowSolveDesc) * nobj, hipMemcpyHostToDevice,
+                         st));
   int n_hint = 0;
   for (int i = 0; i < nobj; i++)
     n_hint = std::max(n_hint, F.po[i].use_mm_choice ? res[8 * i + 4] : res[8 * i + 3]);
@@ -695,12 +709,13 @@ void Tracker::obj_finish(ObjFrame& F) {
   F.active = false;
   if (nobj <= 0) return;
   hipStream_t st = ob_;
-  std::vector<float> X(16 * nobj);
-  std::vector<int> lst(3 * nobj), nsub(nobj);
-  MMT_HIP(hipMemcpyAsync(X.data(), d_poses_ + 16, sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(lst.data(), d_lmstats_ + 3, sizeof(int) * 3 * nobj, hipMemcpyDeviceToHost, st));
-  for (int i = 0; i < nobj; i++)
-    MMT_HIP(hipMemcpyAsync(&nsub[i], pnp_[q][i].n_subset, sizeof(int), hipMemcpyDeviceToHost, st));
+  ObjHost& H = *oh_[q];
+  float* X = H.X;
+  int* lst = H.lst;
+  int* nsub = H.nsub;
+  MMT_HIP(hipMemcpyAsync(X, d_poses_ + 16, sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(lst, d_lmstats_ + 3, sizeof(int) * 3 * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(nsub, d_nsub_[q], sizeof(int) * nobj, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
   float TcwInv[16];
   inv_mat(C.Tcw, TcwInv);
