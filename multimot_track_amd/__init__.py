@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmmt.so")
+LIB_PATH = os.environ.get("MMT_LIB_PATH") or os.path.join(_HERE, "libmmt.so")  # override: tools/ (profiling builds)
 _LIB = None
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),

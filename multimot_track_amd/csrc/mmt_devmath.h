@@ -314,7 +314,14 @@ __device__ inline void block_sum_t(const double (&v)[K], double* tile, double* p
   double* t = tile + (size_t)wave * 64 * 33;
 #pragma unroll
   for (int k = 0; k < K; k++) t[lane * 33 + k] = v[k];
+  // the tile is the wave's own: a wave-level LDS fence replaces the workgroup barrier
+#ifdef MMT_DBG_BARRIER
   __syncthreads();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
   if (lane < K) {
     double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 #pragma unroll 4
@@ -339,6 +346,52 @@ __device__ inline void block_sum_t(const double (&v)[K], double* tile, double* p
     }
     __syncthreads();
   }
+}
+
+// Workgroup sum of K <= 64 values per thread that the threads have written into their rows of a
+// [64][65] per-wave LDS tile (tile_row()) while computing them, so the sums never occupy
+// registers.  Lane k of each wave sums column k, the wave partials meet in `part` (nw * K).
+// out[0..K) is visible to every thread on return.
+constexpr int kTileStride = 65;
+__device__ __forceinline__ double* tile_row(double* tile) {
+  return tile + (size_t)(threadIdx.x >> 6) * 64 * kTileStride + (threadIdx.x & 63) * kTileStride;
+}
+
+template <int K>
+__device__ inline void block_sum_tile(double* tile, double* part, double* out) {
+  static_assert(K <= 64, "block_sum_tile: at most 64 values");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const double* t = tile + (size_t)wave * 64 * kTileStride;
+  // the rows are the wave's own: a wave-level LDS fence orders them before the column reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // column sum in batches of 16 independent loads, so the LDS latency is paid 4 times, not 64
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (lane < K) {
+#pragma unroll
+    for (int r0 = 0; r0 < 64; r0 += 16) {
+      double x[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) x[j] = t[(r0 + j) * kTileStride + lane];
+#pragma unroll
+      for (int j = 0; j < 16; j++) acc[j & 7] += x[j];
+    }
+  }
+  const double mine = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  if (nw == 1) {
+    if (lane < K) out[lane] = mine;
+    __syncthreads();
+    return;
+  }
+  if (lane < K) part[wave * K + lane] = mine;
+  __syncthreads();
+  if (threadIdx.x < K) {
+    double s = 0;
+    for (int w = 0; w < nw; w++) s += part[w * K + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
 }
 
 // Workgroup sum of K doubles held per thread; result broadcast in `out` (LDS, K entries).

@@ -69,15 +69,115 @@ __device__ __forceinline__ void item_store(double* S, int cap, int i, const LMIt
 
 static_assert(sizeof(LMItem) == G_COUNT * sizeof(double), "LMItem layout");
 
+// 1/x and 1/sqrt(x) from the hardware estimates plus two Newton steps (within an ulp of the
+// correctly rounded result; the LM path is compared to the checker within 1e-4, not bitwise).
+// They replace fp64 division/sqrt sequences on the per-trial dependency chains.
+__device__ __forceinline__ double drcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+__device__ __forceinline__ double drsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double h = 0.5 * x * y;
+  double e = fma(-h, y, 0.5);
+  y = fma(y, e, y);
+  h = 0.5 * x * y;
+  e = fma(-h, y, 0.5);
+  return fma(y, e, y);
+}
+
 __device__ __forceinline__ void huber(double e, double dsqr, double delta, double& r0, double& r1) {
   if (e <= dsqr) {
     r0 = e;
     r1 = 1.;
   } else {
-    const double s = sqrt(e);
+    const double rs = drsq(e);
+    const double s = e * rs;
     r0 = 2 * s * delta - dsqr;
-    r1 = delta / s;
+    r1 = delta * rs;
   }
+}
+
+__device__ __forceinline__ void normalize_rot(DQuat& q) {
+  if (q.w < 0) {
+    q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w;
+  }
+  const double in = drsq(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  q.x *= in; q.y *= in; q.z *= in; q.w *= in;
+}
+
+// SE3Quat::exp (g2o, as mmt_devmath.h dse3_exp) on the solve's critical path: the same three
+// regimes (g2o's theta < 1e-5 quirk R = I + O + O^2 kept), with sin(t)/t, (1-cos t)/t^2 and
+// (t - sin t)/t^3 as truncated series below t = 0.05 (remainder < 1e-20), the trace branch of
+// the matrix->quaternion conversion with a refined reciprocal, and the product with P.
+__device__ __forceinline__ DSE3 exp_mul(const double (&u)[6], const DSE3& P) {
+  const double o0 = u[0], o1 = u[1], o2 = u[2];
+  const double th2 = o0 * o0 + o1 * o1 + o2 * o2;
+  const double O[3][3] = {{0, -o2, o1}, {o2, 0, -o0}, {-o1, o0, 0}};
+  double O2[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) O2[r][c] = O[r][0] * O[0][c] + O[r][1] * O[1][c] + O[r][2] * O[2][c];
+  double a, b, c2;
+  if (th2 < 1e-10) {
+    a = 1.0;
+    b = 1.0;
+    c2 = 1.0;
+  } else if (th2 < 0.0025) {
+    const double x = th2;
+    constexpr double k6 = 1.0 / 6, k20 = 1.0 / 20, k42 = 1.0 / 42, k72 = 1.0 / 72;
+    constexpr double k24 = 1.0 / 24, k30 = 1.0 / 30, k56 = 1.0 / 56, k90 = 1.0 / 90;
+    constexpr double k120 = 1.0 / 120, k110 = 1.0 / 110;
+    a = 1.0 - x * k6 * (1.0 - x * k20 * (1.0 - x * k42 * (1.0 - x * k72)));
+    b = 0.5 - x * k24 * (1.0 - x * k30 * (1.0 - x * k56 * (1.0 - x * k90)));
+    c2 = k6 - x * k120 * (1.0 - x * k42 * (1.0 - x * k72 * (1.0 - x * k110)));
+  } else {
+    const double th = sqrt(th2);
+    double st, ct;
+    sincos(th, &st, &ct);
+    const double it = drcp(th), it2 = it * it;
+    a = st * it;
+    b = (1 - ct) * it2;
+    c2 = (th - st) * it2 * it;
+  }
+  double R[3][3], V[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      R[r][c] = (r == c ? 1.0 : 0.0) + a * O[r][c] + b * O2[r][c];
+      V[r][c] = th2 < 1e-10 ? R[r][c] : (r == c ? 1.0 : 0.0) + b * O[r][c] + c2 * O2[r][c];
+    }
+  DSE3 s;
+  const double tr = R[0][0] + R[1][1] + R[2][2];
+  if (tr > 0) {
+    const double rs = drsq(tr + 1.0);
+    s.q.w = 0.5 * (tr + 1.0) * rs;
+    const double h = 0.5 * rs;
+    s.q.x = (R[2][1] - R[1][2]) * h;
+    s.q.y = (R[0][2] - R[2][0]) * h;
+    s.q.z = (R[1][0] - R[0][1]) * h;
+  } else {
+    s.q = dq_from_R(R);
+  }
+#pragma unroll
+  for (int r = 0; r < 3; r++) s.t[r] = V[r][0] * u[3] + V[r][1] * u[4] + V[r][2] * u[5];
+  normalize_rot(s.q);
+  // dse3_mul(s, P)
+  DSE3 out;
+  double x, y, z;
+  dq_rotate(s.q, P.t[0], P.t[1], P.t[2], x, y, z);
+  out.t[0] = s.t[0] + x;
+  out.t[1] = s.t[1] + y;
+  out.t[2] = s.t[2] + z;
+  out.q = dq_mul(s.q, P.q);
+  normalize_rot(out.q);
+  return out;
 }
 
 // projection Jacobian of EdgeFlowCamera / EdgeFlowObj (g2o's EdgeSE3ProjectXYZ form) at the
@@ -112,15 +212,31 @@ struct Cam {
   double fx, fy, cx, cy, pinfo, dsqr, delta;
 };
 
-// linearise at (P, flow fl): errors, chi2 term, robust weight, H/b contributions (acc[0..20] the
-// lower triangle of J^T W J, acc[21..26] J^T W (-e)), landmark gradient
+// sums of one linearisation: [0] chi2, [1] scale term (trial only), [2..22] lower triangle of
+// J^T W J, [23..28] J^T W (-e), [29] Huber-active edge count, [30..50] sum B0a (B0b + B1b),
+// [51..56] sum B0a (bl0 + bl1), [57..62] sum (B1a - B0a) bl1 (B = w J)
+constexpr int kSums = 63;
+
+// linearise at (P, flow fl): errors, robust weight and landmark gradient of the edge; its sums
+// (layout at kSums) go straight into `row`, this thread's row of the LDS reduction tile
+// (block_sum_tile): stored by the thread's first edge (FIRST), accumulated by the others.  No sum
+// lives in registers, which keeps the kernel clear of spills.
+template <bool FIRST>
+__device__ __forceinline__ void put(double* row, int q, double v) {
+  if (FIRST)
+    row[q] = v;
+  else
+    row[q] += v;
+}
+
+template <bool FIRST>
 __device__ __forceinline__ void linearise(const Cam& c, const DSE3& P, const LMItem& it,
-                                          const double f0, const double f1, double* acc,
-                                          double& chi, double& e0, double& e1, double& w,
+                                          const double f0, const double f1, double* row,
+                                          double scale_term, double& e0, double& e1, double& w,
                                           double& bl0, double& bl1, double& mh) {
   double x, y, z;
   map(P, it.X, x, y, z);
-  const double iz = 1.0 / z;
+  const double iz = drcp(z);
   const double pu = x * iz * c.fx + c.cx, pv = y * iz * c.fy + c.cy;
   e0 = (it.ob[0] + f0) - pu;
   e1 = (it.ob[1] + f1) - pv;
@@ -128,21 +244,38 @@ __device__ __forceinline__ void linearise(const Cam& c, const DSE3& P, const LMI
   const double e2 = kInfo * (e0 * e0 + e1 * e1);
   double r0, r1;
   huber(e2, c.dsqr, c.delta, r0, r1);
-  chi += r0 + c.pinfo * (p0 * p0 + p1 * p1);
+  put<FIRST>(row, 0, r0 + c.pinfo * (p0 * p0 + p1 * p1));
+  put<FIRST>(row, 1, scale_term);
   w = kInfo * r1;
+  put<FIRST>(row, 29, w < kInfo ? 1.0 : 0.0);  // Huber-active
   double J[2][6];
   jac(x, y, iz, c.fx, c.fy, J);
-  int k = 0;
-#pragma unroll
-  for (int a = 0; a < 6; a++)
-#pragma unroll
-    for (int b = 0; b <= a; b++) acc[k++] += J[0][a] * w * J[0][b] + J[1][a] * w * J[1][b];
   const double o0 = -w * e0, o1 = -w * e1;
-#pragma unroll
-  for (int a = 0; a < 6; a++) acc[21 + a] += J[0][a] * o0 + J[1][a] * o1;
   bl0 = o0 - c.pinfo * p0;
   bl1 = o1 - c.pinfo * p1;
   mh = fmax(mh, w + c.pinfo);
+  double B0[6], B1[6];
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+    B0[a] = w * J[0][a];
+    B1[a] = w * J[1][a];
+  }
+  // [2..22] J^T W J, [23..28] J^T W (-e); closed-form Schur sums (valid when every edge has the
+  // same weight, see flow_lm_body), B = w J: [30..50] B0a (B0b + B1b), [51..56] B0a (bl0 + bl1),
+  // [57..62] (B1a - B0a) bl1
+  int k = 0;
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+#pragma unroll
+    for (int b = 0; b <= a; b++) {
+      put<FIRST>(row, 2 + k, J[0][a] * w * J[0][b] + J[1][a] * w * J[1][b]);
+      put<FIRST>(row, 30 + k, B0[a] * (B0[b] + B1[b]));
+      k++;
+    }
+    put<FIRST>(row, 23 + a, J[0][a] * o0 + J[1][a] * o1);
+    put<FIRST>(row, 51 + a, B0[a] * (bl0 + bl1));
+    put<FIRST>(row, 57 + a, (B1[a] - B0[a]) * bl1);
+  }
 }
 
 // Schur complement contributions of one correspondence at pose P with damping lam
@@ -151,9 +284,9 @@ __device__ __forceinline__ void schur_terms(const Cam& c, const DSE3& P, const L
   double x, y, z;
   map(P, it.X, x, y, z);
   double J[2][6];
-  jac(x, y, 1.0 / z, c.fx, c.fy, J);
+  jac(x, y, drcp(z), c.fx, c.fy, J);
   const double w = it.w, h = w + c.pinfo;
-  const double d00 = 1.0 / (h + lam), d01 = -h * d00 * ilam, d11 = ilam;
+  const double d00 = drcp(h + lam), d01 = -h * d00 * ilam, d11 = ilam;
   const double bl0 = it.bl[0], bl1 = it.bl[1];
   const double db0 = d00 * bl0 + d01 * bl1, db1 = d11 * bl1;
   int k = 0;
@@ -168,16 +301,17 @@ __device__ __forceinline__ void schur_terms(const Cam& c, const DSE3& P, const L
 }
 
 // back-substitution of the flow increment (when the 6x6 solve succeeded), trial errors and
-// speculative linearisation at (PN, f + xl); v[0] trial chi2, v[1] the scale term, v[2..28] H/b
+// speculative linearisation at (PN, f + xl) into `row` ([0] trial chi2, [1] the scale term)
+template <bool FIRST>
 __device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const DSE3& PN,
                                              LMItem& it, int i, bool ok2, double lam,
-                                             double ilam, const double* xb, double* v) {
+                                             double ilam, const double* xb, double* row) {
   const double bl0 = it.bl[0], bl1 = it.bl[1];
   if (ok2) {
     double x, y, z;
     map(P, it.X, x, y, z);
     double J[2][6];
-    jac(x, y, 1.0 / z, c.fx, c.fy, J);
+    jac(x, y, drcp(z), c.fx, c.fy, J);
     const double w = it.w, h = w + c.pinfo;
     double c0 = bl0, c1 = bl1;
 #pragma unroll
@@ -185,7 +319,7 @@ __device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const 
       c0 -= w * J[0][a] * xb[a];
       c1 -= w * J[1][a] * xb[a];
     }
-    const double ihl = 1.0 / (h + lam);
+    const double ihl = drcp(h + lam);
     double xl0 = c0 * ihl - h * c1 * ihl * ilam;
     if (i > 0) xl0 += c0 * ilam;  // stride-2 spill of landmark i-1's third Dinv row
     it.xl[0] = xl0;
@@ -194,8 +328,8 @@ __device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const 
   const double xl0 = it.xl[0], xl1 = it.xl[1];
   const double f0 = it.f[0] + xl0, f1 = it.f[1] + xl1;
   double mh = 0;
-  linearise(c, PN, it, f0, f1, v + 2, v[0], it.e[0], it.e[1], it.wn, it.bln[0], it.bln[1], mh);
-  v[1] += xl0 * (lam * xl0 + bl0) + xl1 * (lam * xl1 + bl1);
+  linearise<FIRST>(c, PN, it, f0, f1, row, xl0 * (lam * xl0 + bl0) + xl1 * (lam * xl1 + bl1),
+                   it.e[0], it.e[1], it.wn, it.bln[0], it.bln[1], mh);
 }
 
 #ifdef MMT_LM_PROFILE
@@ -213,65 +347,58 @@ __device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const 
   } while (0)
 #endif
 
-// 6x6 LDL^T of the (symmetric positive definite) Schur complement, unpivoted, straight-line
-// code; false when a pivot is negative.  The reduced camera system H_pp + lambda I - B D^-1 B^T
-// is SPD whenever lambda > 0, so the pivoting of Eigen's LDLT only moves rounding.
-__device__ __forceinline__ bool ldlt6(const double (&H)[36], const double (&b)[6], double (&x)[6]) {
-  double L[6][6], D[6], ID[6];
+// 6x6 LDL^T of the (symmetric positive definite) Schur complement, unpivoted, in place on the
+// packed lower triangle A[i(i+1)/2 + j] (L below the diagonal, D on it); false when a pivot is
+// negative.  The reduced camera system H_pp + lambda I - B D^-1 B^T is SPD whenever lambda > 0,
+// so the pivoting of Eigen's LDLT only moves rounding.  b is overwritten by the solution.
+__device__ __forceinline__ bool ldlt6_packed(double (&A)[21], double (&b)[6]) {
+#define PK(i, j) A[(i) * ((i) + 1) / 2 + (j)]
   bool positive = true;
+  double ID[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) {
-    double d = H[6 * k + k];
+    double LD[6];  // L(k, c) D(c)
 #pragma unroll
-    for (int c = 0; c < k; c++) d -= L[k][c] * L[k][c] * D[c];
-    D[k] = d;
+    for (int c = 0; c < k; c++) LD[c] = PK(k, c) * PK(c, c);
+    double d = PK(k, k);
+#pragma unroll
+    for (int c = 0; c < k; c++) d -= PK(k, c) * LD[c];
+    PK(k, k) = d;
     positive = positive && !(d < 0);
-    const double id = d != 0 ? 1.0 / d : 0.0;
+    const double id = d != 0 ? drcp(d) : 0.0;
     ID[k] = id;
 #pragma unroll
     for (int i = k + 1; i < 6; i++) {
-      double s = H[6 * i + k];
+      double s = PK(i, k);
 #pragma unroll
-      for (int c = 0; c < k; c++) s -= L[i][c] * L[k][c] * D[c];
-      L[i][k] = s * id;
+      for (int c = 0; c < k; c++) s -= PK(i, c) * LD[c];
+      PK(i, k) = s * id;
     }
   }
-  double y[6];
 #pragma unroll
   for (int i = 0; i < 6; i++) {
-    double v = b[i];
 #pragma unroll
-    for (int c = 0; c < i; c++) v -= L[i][c] * y[c];
-    y[i] = v;
+    for (int c = 0; c < i; c++) b[i] -= PK(i, c) * b[c];
   }
 #pragma unroll
-  for (int i = 0; i < 6; i++) y[i] *= ID[i];
+  for (int i = 0; i < 6; i++) b[i] *= ID[i];
 #pragma unroll
   for (int i = 5; i >= 0; i--) {
-    double v = y[i];
 #pragma unroll
-    for (int r = i + 1; r < 6; r++) v -= L[r][i] * y[r];
-    y[i] = v;
+    for (int r = i + 1; r < 6; r++) b[i] -= PK(r, i) * b[r];
   }
-#pragma unroll
-  for (int i = 0; i < 6; i++) x[i] = y[i];
+#undef PK
   return positive;
 }
-
-// sums of one linearisation: [0] chi2, [1] scale term (trial only), [2..22] lower triangle of
-// J^T W J, [23..28] J^T W (-e)
-constexpr int kSums = 29;
 
 struct LMSmem {
   long long prof[8];
   double red[16 * 32];
-  double tile[4 * 64 * 33];  // block_sum_t transpose tiles (blockDim <= 256)
+  double tile[4 * 64 * kTileStride];  // block_sum_rows / block_sum_t tiles (blockDim <= 256)
+  double part[4 * kSums];
   double S27[32];
-  double H[2][32];  // current / trial linearisation sums (kSums)
+  double H[2][kSums];  // current / trial linearisation sums
   double mh[16];
-  double xbuf[6];
-  DSE3 pose_new;
-  int ok2;
 };
 
 }  // namespace
@@ -333,33 +460,40 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
   // The LM bookkeeping below is computed redundantly by every thread from the block sums in LDS
   // (identical inputs, identical results), so only the 6x6 solve needs a lane-0 section.
   DSE3 P = dse3_from_float(D.init);
+  const double hin = kInfo + c.pinfo;  // h of every edge when none is Huber-active
   int hs = 0;  // sm.H[hs] holds the linearisation at P
   // ---- initial linearisation (computeActiveErrors + buildSystem at the initial estimate)
+  double* row = tile_row(sm.tile);  // this thread's row of the reduction tile
+  // every thread with an edge has one in register slot 0 (N > nt implies all do), so slot 0
+  // stores the row and everything after accumulates; threads without edges zero it
   {
-    double v[kSums];
-#pragma unroll
-    for (int k = 0; k < kSums; k++) v[k] = 0;
     double mh = 0;
 #pragma unroll
     for (int k = 0; k < IR; k++) {
       const int i = tid + k * nt;
       if (i < N) {
         init_item(i, R[k]);
-        linearise(c, P, R[k], R[k].f[0], R[k].f[1], v + 2, v[0], R[k].e[0], R[k].e[1], R[k].w,
-                  R[k].bl[0], R[k].bl[1], mh);
+        if (k == 0)
+          linearise<true>(c, P, R[k], R[k].f[0], R[k].f[1], row, 0.0, R[k].e[0], R[k].e[1],
+                          R[k].w, R[k].bl[0], R[k].bl[1], mh);
+        else
+          linearise<false>(c, P, R[k], R[k].f[0], R[k].f[1], row, 0.0, R[k].e[0], R[k].e[1],
+                           R[k].w, R[k].bl[0], R[k].bl[1], mh);
       }
     }
     for (int i = n_reg + tid; i < N; i += nt) {
       LMItem it;
       init_item(i, it);
-      linearise(c, P, it, it.f[0], it.f[1], v + 2, v[0], it.e[0], it.e[1], it.w, it.bl[0],
-                it.bl[1], mh);
+      linearise<false>(c, P, it, it.f[0], it.f[1], row, 0.0, it.e[0], it.e[1], it.w, it.bl[0],
+                       it.bl[1], mh);
       item_store(G, cap, i, it);
     }
+    if (tid >= N)
+      for (int q = 0; q < kSums; q++) row[q] = 0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mh = fmax(mh, __shfl_xor(mh, o, 64));
     if ((tid & 63) == 0) sm.mh[tid >> 6] = mh;
-    block_sum_t<kSums>(v, sm.tile, sm.red, sm.H[0]);
+    block_sum_tile<kSums>(sm.tile, sm.part, sm.H[0]);
   }
   double cur = sm.H[0][0], lam, ni = 2, chk = 0;
   {
@@ -371,8 +505,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
     lam = 1e-5 * md;
   }
   int nbad = 0, iters = 0;
-  if (tid == 0)
-    for (int k = 0; k < 6; k++) sm.xbuf[k] = 0;
+  double xb[6] = {0, 0, 0, 0, 0, 0};  // the last increment (reused when the LDLT fails)
   for (int iter = 0; iter < D.max_iters; iter++) {
     const double ini = cur;
     int qmax = 0;
@@ -381,9 +514,17 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
 #ifdef MMT_LM_PROFILE
       if (tid == 0) prof_t = clock64();
 #endif
-      const double ilam = 1.0 / lam;
-      // ---- Schur complement over the flow vertices
-      {
+      const double ilam = drcp(lam);
+      // ---- Schur complement over the flow vertices.  Edge i contributes
+      //   d00 B0 B0^T + d01 B0 B1^T + d11 B1 B1^T,  d00 = 1/(h_i + lam), d11 = 1/lam, d01 = d00 - d11
+      // (h_i = w_i + prior).  With no Huber-active edge every w_i is the same, so the sum is
+      // d00 SA + d11 SB with lam-independent sums the linearisation already reduced: no pass.
+#ifdef MMT_LM_NO_CLOSED
+      const bool clean = false;
+#else
+      const bool clean = sm.H[hs][29] == 0;
+#endif
+      if (!clean) {
         double v[27];
 #pragma unroll
         for (int k = 0; k < 27; k++) v[k] = 0;
@@ -399,57 +540,77 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
         block_sum_t<27>(v, sm.tile, sm.red, sm.S27);
       }
       MMT_LMPROF(0);
-      if (tid == 0) {
+      // the 6x6 solve, computed redundantly by every thread from the LDS sums (identical inputs,
+      // identical results): no lane-0 section, no barrier, no broadcast
+      bool ok2;
+      DSE3 PN;
+      {
         const double* Hc = sm.H[hs];
-        double Hs[36], bs[6], xp[6];
-        int k = 0;
+        double A[21], bs[6];
 #pragma unroll
-        for (int a = 0; a < 6; a++)
+        for (int k = 0; k < 21; k++) A[k] = Hc[2 + k];
 #pragma unroll
-          for (int b = 0; b <= a; b++) {
-            Hs[6 * a + b] = Hc[2 + k] + (a == b ? lam : 0.0) - sm.S27[k];
-            Hs[6 * b + a] = Hs[6 * a + b];
-            k++;
+        for (int a = 0; a < 6; a++) bs[a] = Hc[23 + a];
+        // one branch around straight-line code, so each side's LDS loads issue back to back
+        if (clean) {
+          // SB = sum B1a B1b - B0a B1b = w H - SA (w = kInfo on every edge)
+          const double d00 = drcp(hin + lam);
+#pragma unroll
+          for (int k = 0; k < 21; k++) {
+            const double sa = Hc[30 + k];
+            A[k] -= d00 * sa + ilam * (kInfo * A[k] - sa);
           }
 #pragma unroll
-        for (int a = 0; a < 6; a++) bs[a] = Hc[23 + a] - sm.S27[21 + a];
-        const bool ok2 = ldlt6(Hs, bs, xp);
-        double xu[6];
+          for (int a = 0; a < 6; a++) bs[a] -= d00 * Hc[51 + a] + ilam * Hc[57 + a];
+        } else {
 #pragma unroll
-        for (int a = 0; a < 6; a++) {
-          xu[a] = ok2 ? xp[a] : sm.xbuf[a];  // a failed solve reuses the last increment
-          sm.xbuf[a] = xu[a];
+          for (int k = 0; k < 21; k++) A[k] -= sm.S27[k];
+#pragma unroll
+          for (int a = 0; a < 6; a++) bs[a] -= sm.S27[21 + a];
         }
-        sm.ok2 = ok2;
-        sm.pose_new = dse3_mul(dse3_exp(xu), P);
-      }
-      __syncthreads();
-      MMT_LMPROF(1);
-      const bool ok2 = sm.ok2;
-      const DSE3 PN = sm.pose_new;
-      double xb[6];
 #pragma unroll
-      for (int a = 0; a < 6; a++) xb[a] = sm.xbuf[a];
+        for (int a = 0; a < 6; a++) A[a * (a + 3) / 2] += lam;  // diagonal (a, a)
+        ok2 = ldlt6_packed(A, bs);
+#pragma unroll
+        for (int a = 0; a < 6; a++) xb[a] = ok2 ? bs[a] : xb[a];  // failed solve: last increment
+        PN = exp_mul(xb, P);
+      }
+      MMT_LMPROF(1);
       // ---- flow back-substitution, trial errors, speculative linearisation
       {
-        double v[kSums];
-#pragma unroll
-        for (int k = 0; k < kSums; k++) v[k] = 0;
 #pragma unroll
         for (int k = 0; k < IR; k++) {
           const int i = tid + k * nt;
-          if (i < N) update_terms(c, P, PN, R[k], i, ok2, lam, ilam, xb, v);
+          if (i < N) {
+            if (k == 0)
+              update_terms<true>(c, P, PN, R[k], i, ok2, lam, ilam, xb, row);
+            else
+              update_terms<false>(c, P, PN, R[k], i, ok2, lam, ilam, xb, row);
+          }
         }
         for (int i = n_reg + tid; i < N; i += nt) {
           LMItem it;
           item_load(G, cap, i, it);
-          update_terms(c, P, PN, it, i, ok2, lam, ilam, xb, v);
+          update_terms<false>(c, P, PN, it, i, ok2, lam, ilam, xb, row);
           item_store(G, cap, i, it);
         }
+        if (tid >= N)
+          for (int q = 0; q < kSums; q++) row[q] = 0;
         MMT_LMPROF(5);
-        block_sum_t<kSums>(v, sm.tile, sm.red, sm.H[hs ^ 1]);
+        block_sum_tile<kSums>(sm.tile, sm.part, sm.H[hs ^ 1]);
       }
       MMT_LMPROF(2);
+#ifdef MMT_DBG_TRACE
+      if (tid == 0 && iter < 3) {
+        const double* Hx = sm.H[hs ^ 1];
+        double sh = 0, sb = 0, ss = 0;
+        for (int q = 2; q < 23; q++) sh += Hx[q];
+        for (int q = 23; q < 29; q++) sb += Hx[q];
+        for (int q = 30; q < kSums; q++) ss += Hx[q];
+        printf("trace N=%d nt=%d iter=%d lam=%.9e ok2=%d xb0=%.9e chi=%.9e scale=%.9e H=%.9e b=%.9e "
+               "nout=%g ss=%.9e\n", N, nt, iter, lam, (int)ok2, xb[0], Hx[0], Hx[1], sh, sb, Hx[29], ss);
+      }
+#endif
       // ---- g2o LM step acceptance and termination (every thread, same values)
       const double* Ht = sm.H[hs ^ 1];
       const double* Hc = sm.H[hs];
@@ -515,7 +676,10 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
       }
       MMT_LMPROF(3);
 #ifdef MMT_LM_PROFILE
-      if (tid == 0) sm.prof[6]++;
+      if (tid == 0) {
+        sm.prof[6]++;
+        if (sm.H[hs][29] == 0) sm.prof[7]++;
+      }
 #endif
       if (!again) break;
     }
@@ -542,9 +706,9 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
     D.stats[1] = N - (int)sm.S27[0];
     D.stats[2] = 0;
 #ifdef MMT_LM_PROFILE
-    printf("lmprof N=%d T=%d iters=%d trials=%lld schur_pass=%lld schur_red=%lld solve=%lld "
-           "upd_pass=%lld upd_red=%lld decide=%lld\n", N, nt, iters, sm.prof[6], sm.prof[4],
-           sm.prof[0], sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3]);
+    printf("lmprof N=%d T=%d iters=%d trials=%lld clean=%lld schur_pass=%lld schur_red=%lld "
+           "solve=%lld upd_pass=%lld upd_red=%lld decide=%lld\n", N, nt, iters, sm.prof[6],
+           sm.prof[7], sm.prof[4], sm.prof[0], sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3]);
 #endif
   }
 }
@@ -567,30 +731,23 @@ __global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict
   const int nt = blockDim.x;
   if (N <= nt || MAXIR == 1)
     flow_lm_body<1>(D, N, sm);
-  else if (N <= 2 * nt || MAXIR == 2)
-    flow_lm_body<2>(D, N, sm);
-  else if (N <= 4 * nt || MAXIR == 4)
-    flow_lm_body<4>(D, N, sm);
   else
-    flow_lm_body<8>(D, N, sm);
+    flow_lm_body<2>(D, N, sm);
 }
 
 void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st) {
   // Latency-bound: about one correspondence per thread where the block allows it (a trial's
-  // passes cost about one correspondence's dependency chain), 64..256 threads, up to 8 register
-  // items each; items beyond spill to the scratch arrays.  Each workgroup picks its own item
-  // count (k_flow_lm); n_hint (the largest edge count) only sizes the block.
+  // passes cost about one correspondence's dependency chain), 64..256 threads, up to 2 register
+  // items each (more register items spill: the 6x6 solve and the sums need the room); items
+  // beyond go through the global item arrays.  Each workgroup picks its own item count
+  // (k_flow_lm); n_hint (the largest edge count) only sizes the block.
   static const int force = [] {  // MMT_LM_THREADS=<threads>: tuning knob for tools/
     const char* e = getenv("MMT_LM_THREADS");
     return e ? atoi(e) : 0;
   }();
-  static const bool force8 = getenv("MMT_LM_MAXIR8") != nullptr;
   int threads = std::min(256, std::max(64, (n_hint + 63) / 64 * 64));
   if (force) threads = force;
-  if (n_hint <= 2 * threads && !force8)
-    hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs);
-  else
-    hipLaunchKernelGGL(k_flow_lm<8>, dim3(nsolves), dim3(threads), 0, st, d_descs);
+  hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs);
 }
 
 size_t flow_scratch_doubles(int cap) { return (size_t)G_COUNT * cap; }
