@@ -267,9 +267,11 @@ __device__ inline bool ldlt_solve6(const double (&Hl)[36], const double (&b)[6],
 // waves.  `red` holds 32 doubles per wave; the sums land in out[0..K) (LDS), visible to every
 // thread on return.
 template <int K>
-__device__ inline void block_sum(const double (&v)[K], double* red, double* out) {
+__device__ inline void block_sum(const double (&v)[K], double* red, double* out,
+                                 int nw_active = 0) {
   static_assert(K <= 32, "block_sum: at most 32 values");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nw = nw_active > 0 ? nw_active : (int)(blockDim.x >> 6);
   double a[16];
   {
     const bool hi = lane & 32;
@@ -308,9 +310,11 @@ __device__ inline void block_sum(const double (&v)[K], double* red, double* out)
 // than a shuffle tree when K is large.  `tile` holds 64 * 33 doubles per wave, `part` 32 per wave;
 // out[0..K) is visible to every thread on return.  blockDim <= 256.
 template <int K>
-__device__ inline void block_sum_t(const double (&v)[K], double* tile, double* part, double* out) {
+__device__ inline void block_sum_t(const double (&v)[K], double* tile, double* part, double* out,
+                                   int nw_active = 0) {
   static_assert(K <= 32, "block_sum_t: at most 32 values");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nw = nw_active > 0 ? nw_active : (int)(blockDim.x >> 6);
   double* t = tile + (size_t)wave * 64 * 33;
 #pragma unroll
   for (int k = 0; k < K; k++) t[lane * 33 + k] = v[k];
@@ -358,9 +362,10 @@ __device__ __forceinline__ double* tile_row(double* tile) {
 }
 
 template <int K>
-__device__ inline void block_sum_tile(double* tile, double* part, double* out) {
+__device__ inline void block_sum_tile(double* tile, double* part, double* out, int nw_active = 0) {
   static_assert(K <= 64, "block_sum_tile: at most 64 values");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nw = nw_active > 0 ? nw_active : (int)(blockDim.x >> 6);
   const double* t = tile + (size_t)wave * 64 * kTileStride;
   // the rows are the wave's own: a wave-level LDS fence orders them before the column reads
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

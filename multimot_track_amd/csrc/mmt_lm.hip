@@ -69,6 +69,27 @@ __device__ __forceinline__ void item_store(double* S, int cap, int i, const LMIt
 
 static_assert(sizeof(LMItem) == G_COUNT * sizeof(double), "LMItem layout");
 
+// the fields the update pass changes (xl, e, wn, bln) and the accept step changes (f, w, bl)
+__device__ __forceinline__ void item_store_upd(double* S, int cap, int i, const LMItem& it) {
+  double* dst = S + i;
+  dst[(size_t)G_XL0 * cap] = it.xl[0];
+  dst[(size_t)G_XL1 * cap] = it.xl[1];
+  dst[(size_t)G_WN * cap] = it.wn;
+  dst[(size_t)G_BLN0 * cap] = it.bln[0];
+  dst[(size_t)G_BLN1 * cap] = it.bln[1];
+  dst[(size_t)G_E0 * cap] = it.e[0];
+  dst[(size_t)G_E1 * cap] = it.e[1];
+}
+
+__device__ __forceinline__ void item_accept(double* S, int cap, int i) {
+  double* d = S + i;
+  d[(size_t)G_F0 * cap] += d[(size_t)G_XL0 * cap];
+  d[(size_t)G_F1 * cap] += d[(size_t)G_XL1 * cap];
+  d[(size_t)G_W * cap] = d[(size_t)G_WN * cap];
+  d[(size_t)G_BL0 * cap] = d[(size_t)G_BLN0 * cap];
+  d[(size_t)G_BL1 * cap] = d[(size_t)G_BLN1 * cap];
+}
+
 // 1/x and 1/sqrt(x) from the hardware estimates plus two Newton steps (within an ulp of the
 // correctly rounded result; the LM path is compared to the checker within 1e-4, not bitwise).
 // They replace fp64 division/sqrt sequences on the per-trial dependency chains.
@@ -392,7 +413,7 @@ __device__ __forceinline__ bool ldlt6_packed(double (&A)[21], double (&b)[6]) {
 }
 
 struct LMSmem {
-  long long prof[8];
+  long long prof[12];
   double red[16 * 32];
   double tile[4 * 64 * kTileStride];  // block_sum_rows / block_sum_t tiles (blockDim <= 256)
   double part[4 * kSums];
@@ -404,12 +425,12 @@ struct LMSmem {
 }  // namespace
 
 template <int IR>
-__device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSmem& sm) {
-  const int tid = threadIdx.x, nt = blockDim.x;
+__device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int nt, LMSmem& sm) {
+  const int tid = threadIdx.x, nw = nt >> 6;
 #ifdef MMT_LM_PROFILE
   long long prof_t = 0;
   if (tid == 0)
-    for (int k = 0; k < 8; k++) sm.prof[k] = 0;
+    for (int k = 0; k < 12; k++) sm.prof[k] = 0;
 #endif
   double* G = D.scratch;  // items beyond IR * blockDim
   const int cap = D.cap;
@@ -493,7 +514,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mh = fmax(mh, __shfl_xor(mh, o, 64));
     if ((tid & 63) == 0) sm.mh[tid >> 6] = mh;
-    block_sum_tile<kSums>(sm.tile, sm.part, sm.H[0]);
+    block_sum_tile<kSums>(sm.tile, sm.part, sm.H[0], nw);
   }
   double cur = sm.H[0][0], lam, ni = 2, chk = 0;
   {
@@ -501,7 +522,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
 #pragma unroll
     for (int a = 0; a < 6; a++)
       md = fmax(md, fabs(sm.H[0][2 + a * (a + 3) / 2]));  // diagonal (a, a) of the lower triangle
-    for (int w = 0; w < (nt >> 6); w++) md = fmax(md, sm.mh[w]);
+    for (int w = 0; w < nw; w++) md = fmax(md, sm.mh[w]);
     lam = 1e-5 * md;
   }
   int nbad = 0, iters = 0;
@@ -537,7 +558,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
           schur_terms(c, P, it, lam, ilam, v);
         }
         MMT_LMPROF(4);
-        block_sum_t<27>(v, sm.tile, sm.red, sm.S27);
+        block_sum_t<27>(v, sm.tile, sm.red, sm.S27, nw);
       }
       MMT_LMPROF(0);
       // the 6x6 solve, computed redundantly by every thread from the LDS sums (identical inputs,
@@ -570,7 +591,19 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
         }
 #pragma unroll
         for (int a = 0; a < 6; a++) A[a * (a + 3) / 2] += lam;  // diagonal (a, a)
+#ifdef MMT_LM_PROFILE
+        if (tid == 0) {  // force the loads to complete before the split point
+          double chk = 0;
+          for (int q = 0; q < 21; q++) chk += A[q];
+          if (chk == 12345.678) sm.prof[11]++;
+        }
+#endif
+        MMT_LMPROF(8);
         ok2 = ldlt6_packed(A, bs);
+#ifdef MMT_LM_PROFILE
+        if (tid == 0 && bs[0] == 12345.678) sm.prof[11]++;
+#endif
+        MMT_LMPROF(9);
 #pragma unroll
         for (int a = 0; a < 6; a++) xb[a] = ok2 ? bs[a] : xb[a];  // failed solve: last increment
         PN = exp_mul(xb, P);
@@ -588,16 +621,21 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
               update_terms<false>(c, P, PN, R[k], i, ok2, lam, ilam, xb, row);
           }
         }
-        for (int i = n_reg + tid; i < N; i += nt) {
-          LMItem it;
-          item_load(G, cap, i, it);
-          update_terms<false>(c, P, PN, it, i, ok2, lam, ilam, xb, row);
-          item_store(G, cap, i, it);
+        {  // global items: the next item's loads are in flight while this one computes
+          int i = n_reg + tid;
+          LMItem it, nx;
+          if (i < N) item_load(G, cap, i, it);
+          for (; i < N; i += nt) {
+            if (i + nt < N) item_load(G, cap, i + nt, nx);
+            update_terms<false>(c, P, PN, it, i, ok2, lam, ilam, xb, row);
+            item_store_upd(G, cap, i, it);
+            it = nx;
+          }
         }
         if (tid >= N)
           for (int q = 0; q < kSums; q++) row[q] = 0;
         MMT_LMPROF(5);
-        block_sum_tile<kSums>(sm.tile, sm.part, sm.H[hs ^ 1]);
+        block_sum_tile<kSums>(sm.tile, sm.part, sm.H[hs ^ 1], nw);
       }
       MMT_LMPROF(2);
 #ifdef MMT_DBG_TRACE
@@ -663,16 +701,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
             it.bl[0] = it.bln[0];
             it.bl[1] = it.bln[1];
           }
-        for (int i = n_reg + tid; i < N; i += nt) {
-          LMItem it;
-          item_load(G, cap, i, it);
-          it.f[0] += it.xl[0];
-          it.f[1] += it.xl[1];
-          it.w = it.wn;
-          it.bl[0] = it.bln[0];
-          it.bl[1] = it.bln[1];
-          item_store(G, cap, i, it);
-        }
+        for (int i = n_reg + tid; i < N; i += nt) item_accept(G, cap, i);
       }
       MMT_LMPROF(3);
 #ifdef MMT_LM_PROFILE
@@ -699,7 +728,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
     item_load(G, cap, i, it);
     v[0] += outlier(it);
   }
-  block_sum<1>(v, sm.red, sm.S27);
+  block_sum<1>(v, sm.red, sm.S27, nw);
   if (tid == 0) {
     dse3_to_float(P, D.pose_out);
     D.stats[0] = iters;
@@ -707,8 +736,9 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, LMSm
     D.stats[2] = 0;
 #ifdef MMT_LM_PROFILE
     printf("lmprof N=%d T=%d iters=%d trials=%lld clean=%lld schur_pass=%lld schur_red=%lld "
-           "solve=%lld upd_pass=%lld upd_red=%lld decide=%lld\n", N, nt, iters, sm.prof[6],
-           sm.prof[7], sm.prof[4], sm.prof[0], sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3]);
+           "solve_ld=%lld solve_ldlt=%lld solve_exp=%lld upd_pass=%lld upd_red=%lld decide=%lld\n",
+           N, nt, iters, sm.prof[6], sm.prof[7], sm.prof[4], sm.prof[0], sm.prof[8], sm.prof[9],
+           sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3]);
 #endif
   }
 }
@@ -728,11 +758,16 @@ __global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict
     }
     return;
   }
-  const int nt = blockDim.x;
+  // Threads per solve: one edge per thread up to the block size (the passes are issue-bound:
+  // a second register edge per thread doubles them, measured); a solve smaller than the block
+  // uses only the waves it needs and the others leave at once (a finished wave no longer counts
+  // at the barriers), which keeps the reductions' LDS traffic to the rows in use.
+  const int nt = min((int)blockDim.x, max(64, (N + 63) / 64 * 64));
+  if ((int)threadIdx.x >= nt) return;
   if (N <= nt || MAXIR == 1)
-    flow_lm_body<1>(D, N, sm);
+    flow_lm_body<1>(D, N, nt, sm);
   else
-    flow_lm_body<2>(D, N, sm);
+    flow_lm_body<2>(D, N, nt, sm);
 }
 
 void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st) {

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <deque>
 #include <vector>
 
 #include "mmt_internal.h"
@@ -28,6 +29,19 @@ struct FrameOut {
 };
 
 float rng_first_gaussian(uint64_t seed);
+
+// device side of object stage B (mmt_tracker.hip)
+struct MMPrepArgs {
+  PnPObject* objs;
+  int nobj;
+  int pre[kMaxObj];        // PreObjID per object (-1: no motion model)
+  const float* prevX;      // previous frame's D3 poses (16 per object)
+  const int* prevStats;    // previous frame's D3 stats (3 per object)
+  float TcwPrev[16], TcwCur[16];
+};
+void launch_obj_mm_prep(const MMPrepArgs& a, hipStream_t st);
+void launch_obj_model_choice(PnPObject* objs, int nobj, FlowSolveDesc* descs, float* init,
+                             hipStream_t st);
 // RANSACPointSetRegistrator::getSubset draws (5-point subsets) for a point count.
 void ransac_subsets(int count, int iters, std::vector<int>& idx);
 
@@ -57,19 +71,21 @@ class Tracker {
     HandoffSet ho;
     float Tcw[16];
     bool bSecond = false;  // bSecondFrame as of this frame (label association, B8)
+    int obj_slot = -1;     // object-pipeline slot of this frame's D3 output (-1: none)
     std::vector<int> nModLabel, nSemPosition;
     std::vector<std::vector<float>> vObjMod;
   };
-  // Object work of one frame in flight.  Stage A (grouping, B7/B8, PnP-RANSAC) needs only the
-  // frame's pose and the previous frame's labels; stage B (motion-model check, D3) needs the
-  // previous frame's object motions, i.e. the previous frame's D3.  So stage A of frame f runs
-  // while D3 of frame f-1 is in flight, and both overlap the ego solve of frame f+1.
+  // Object work of one frame.  Stage A (grouping, B7/B8 on the host, PnP-RANSAC on oa_) needs
+  // the frame's pose and the previous frame's labels; stage B (motion-model matrix from the
+  // previous frame's D3 output, MM check, model choice, D3 on ob_) runs entirely on the device,
+  // ordered behind the RANSAC by an event and behind the previous frame's D3 by the stream, so the
+  // host enqueues both stages at once and only reads the results kObjLag frames later (finish).
   struct ObjFrame {
     bool active = false;
-    int cur = 0, last = 0, par = 0, nobj = 0;
+    int cur = 0, last = 0, slot = 0, nobj = 0;
     FrameOut* out = nullptr;
     std::vector<int> labels, LabId, PreObjID, members;
-    PnPObject* po = nullptr;  // oh_[par]->po
+    PnPObject* po = nullptr;  // oh_[slot]->po
   };
   struct FrameArgs {
     const float* depth;
@@ -102,9 +118,9 @@ class Tracker {
   // waits for the ego solve, updates the motion model, queues the frame's object path
   void ego_finish(FrameOut& out, hipStream_t st);
   void obj_stage_a(ObjFrame& F);    // grouping + B7/B8 + PnP-RANSAC launch (stream oa_)
-  void obj_stage_b(ObjFrame& F);    // MM check, model choice, D3 launch (stream ob_)
-  void obj_finish(ObjFrame& F);     // waits for D3, object motions, results
-  void obj_advance();               // one pipeline step after a frame's ego pose is known
+  void obj_stage_b(ObjFrame& F);    // MM matrix, MM check, model choice, D3 (stream ob_, no wait)
+  void obj_finish(ObjFrame& F);     // waits for the frame's D3, object motions, results
+  void obj_advance();               // enqueue the queued frame's object path, finish old frames
   void obj_flush();
 
   mmt_config cfg_{};
@@ -114,7 +130,11 @@ class Tracker {
   int state_ = 0, cur_ = 0, last_ = 2;
   bool bFirstFrame_ = false, bSecondFrame_ = false, hasVelocity_ = false;
   float V_[16] = {0};
-  static constexpr int kSlots = 4;  // frames f (ego), f-1 (stage A), f-2 (D3), f-3 (D3's last)
+  // frame slots: the ego frame, the frames whose object path is in flight (up to kObjLag + 1) and
+  // their last frames; 8 leaves room to spare
+  static constexpr int kSlots = 8;
+  static constexpr int kObjSlots = 4;  // object-pipeline buffers (frames in flight + 1)
+  static constexpr int kObjLag = 2;    // frames between enqueueing a frame's D3 and reading it
   FrameSlot slot_[kSlots];
   // ego in flight; its device->host results land in pinned memory so the copies stay
   // asynchronous while the host drives the previous frame's object path
@@ -128,27 +148,34 @@ class Tracker {
   bool ego_pending_ = false;
   float ego_Tinit_[16];
   EgoHost* eh_ = nullptr;
-  ObjFrame qa_, fa_, fb_;  // queued (ego done), stage A done, stage B (D3) in flight
-  // Pinned host side of the object path, one per frame parity (frames f and f-1 are in flight
-  // at once): every host<->device transfer of stages A/B and the finish is a single asynchronous
-  // copy into or out of this block (pageable copies are staged synchronously by the runtime).
+  ObjFrame qa_;                  // ego done, object path not yet enqueued
+  std::deque<ObjFrame> inflight_;  // object path enqueued, results not yet read
+  int obj_slot_next_ = 0;
+  // Pinned host side of the object path, one per object slot: every host<->device transfer of the
+  // stages and the finish is a single asynchronous copy into or out of this block.
   struct ObjHost {
     LabelStats stats[kMaxLabel];
     int hist[kMaxLabel * kMaxLabel];
     int err;
     PnPObject po[kMaxObj];
     int subsets[kMaxObj][5 * kRansacIters];
-    int res[8 * kMaxObj];
-    double Rt[12 * kMaxObj];
     FlowSolveDesc descs[kMaxObj];
+    int res[8 * kMaxObj];
+    float init[16 * kMaxObj];
     float X[16 * kMaxObj];
     int lst[3 * kMaxObj];
     int nsub[kMaxObj];
   };
-  ObjHost* oh_[2] = {nullptr, nullptr};
-  int* d_res_[2] = {nullptr, nullptr};     // PnP results of all objects, contiguous
-  double* d_Rt_[2] = {nullptr, nullptr};
-  int* d_nsub_[2] = {nullptr, nullptr};
+  ObjHost* oh_[kObjSlots] = {};
+  int* d_res_[kObjSlots] = {};     // PnP results of all objects, contiguous
+  double* d_Rt_[kObjSlots] = {};
+  int* d_nsub_[kObjSlots] = {};
+  FlowSolveDesc* d_descs3_[kObjSlots] = {};  // D3 solves of the slot's frame
+  float* d_poses3_[kObjSlots] = {};
+  int* d_lmstats3_[kObjSlots] = {};
+  float* d_init_[kObjSlots] = {};  // chosen D3 initial motion per object
+  hipEvent_t ev_ransac_[kObjSlots] = {};
+  hipEvent_t ev_d3_[kObjSlots] = {};
   // subset draws depend only on the point count: cache the last few counts
   struct SubsetCache {
     int count = -1;
@@ -164,18 +191,17 @@ class Tracker {
   mmt_kp* d_kps_ = nullptr;
   uint8_t* d_desc_ = nullptr;
   int* d_nkp_ = nullptr;
-  int32_t* d_obj_label_[2] = {nullptr, nullptr};
-  int* d_members_[2] = {nullptr, nullptr};
-  LabelStats* d_stats_[2] = {nullptr, nullptr};
-  int* d_hist_[2] = {nullptr, nullptr};
+  int32_t* d_obj_label_[kObjSlots] = {};
+  int* d_members_[kObjSlots] = {};
+  LabelStats* d_stats_[kObjSlots] = {};
+  int* d_hist_[kObjSlots] = {};
   int* d_err_ = nullptr;
   double* d_lm_scratch_ = nullptr;
   FlowSolveDesc* d_descs_ = nullptr;
   float* d_poses_ = nullptr;
   int* d_lmstats_ = nullptr;
-  PnPObject* d_pnp_[2] = {nullptr, nullptr};
-  PnPBuf pnp_[2][kMaxObj];
-  int frame_par_ = 0;
+  PnPObject* d_pnp_[kObjSlots] = {};
+  PnPBuf pnp_[kObjSlots][kMaxObj];
   bool prof_ = false;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
   double orb_ms_ = 0;

@@ -18,37 +18,12 @@
 #include <vector>
 
 #include "mmt_internal.h"
+#include "mmt_mat4.h"
 #include "mmt_pnp.h"
 #include "mmt_track.h"
 #include "mmt_tracker.h"
 
 namespace mmt {
-
-// ------------------------------------------------------------------ float cv::Mat helpers
-static void mat4_mul(const float* A, const float* B, float* C) {  // cv::gemm, CV_32F
-  float R[16];
-  for (int r = 0; r < 4; r++)
-    for (int c = 0; c < 4; c++) {
-      double s = 0;
-      for (int k = 0; k < 4; k++) s += (double)A[4 * r + k] * (double)B[4 * k + c];
-      R[4 * r + c] = (float)s;
-    }
-  memcpy(C, R, sizeof(R));
-}
-static void inv_mat(const float* T, float* Ti) {  // Tracking::InvMatrix
-  float R[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 3; c++) R[4 * r + c] = T[4 * c + r];
-  for (int r = 0; r < 3; r++) {
-    double s = 0;
-    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)T[4 * k + 3];
-    R[4 * r + 3] = (float)(-s);
-  }
-  memcpy(Ti, R, sizeof(R));
-}
-static void mat4_eye(float* T) {
-  for (int i = 0; i < 16; i++) T[i] = (i % 5 == 0) ? 1.f : 0.f;
-}
 
 // cv::RNG(seed).gaussian(1.0) first draw (randn_0_1_32f ziggurat; Frame.cc:1246-1251)
 static inline uint64_t rng_next(uint64_t x) { return (uint64_t)(unsigned)x * 4164903690ULL + (x >> 32); }
@@ -149,6 +124,10 @@ Tracker::~Tracker() {
   if (eh_) (void)hipHostFree(eh_);
   for (ObjHost* h : oh_)
     if (h) (void)hipHostFree(h);
+  for (int q = 0; q < kObjSlots; q++) {
+    if (ev_ransac_[q]) (void)hipEventDestroy(ev_ransac_[q]);
+    if (ev_d3_[q]) (void)hipEventDestroy(ev_d3_[q]);
+  }
   for (hipEvent_t& e : ev_orb_)
     if (e) (void)hipEventDestroy(e);
 }
@@ -220,7 +199,7 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     MMT_HIP(hipMemset(F.st.count, 0, sizeof(int)));
     MMT_HIP(hipMemset(F.ob.count, 0, sizeof(int)));
   }
-  for (int q = 0; q < 2; q++) {
+  for (int q = 0; q < kObjSlots; q++) {
     d_obj_label_[q] = alloc<int32_t>(ocap_);
     d_members_[q] = alloc<int>((size_t)kMaxLabel * ocap_);
     d_stats_[q] = alloc<LabelStats>(kMaxLabel);
@@ -231,19 +210,26 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // solves: 1 ego + up to kMaxObj objects
   const int lmcap = std::max(kcap_, ocap_);
   lm_cap_ = lmcap;
+  // scratch: the ego solve (caller stream) and the object solves (ob_, one D3 launch at a time)
   d_lm_scratch_ = alloc<double>(flow_scratch_doubles(lmcap) * (1 + kMaxObj));
-  d_descs_ = alloc<FlowSolveDesc>(1 + kMaxObj);
-  d_poses_ = alloc<float>(16 * (1 + kMaxObj));
-  d_lmstats_ = alloc<int>(3 * (1 + kMaxObj));
+  d_descs_ = alloc<FlowSolveDesc>(1);
+  d_poses_ = alloc<float>(16);
+  d_lmstats_ = alloc<int>(3);
   // PnP
   mask_words_ = (ocap_ + 63) / 64;
-  for (int q = 0; q < 2; q++) {
+  for (int q = 0; q < kObjSlots; q++) {
   d_pnp_[q] = alloc<PnPObject>(kMaxObj);
   d_res_[q] = alloc<int>(8 * kMaxObj);
   d_Rt_[q] = alloc<double>(12 * kMaxObj);
   d_nsub_[q] = alloc<int>(kMaxObj);
+  d_descs3_[q] = alloc<FlowSolveDesc>(kMaxObj);
+  d_poses3_[q] = alloc<float>(16 * kMaxObj);
+  d_lmstats3_[q] = alloc<int>(3 * kMaxObj);
+  d_init_[q] = alloc<float>(16 * kMaxObj);
   if (!oh_[q]) MMT_HIP(hipHostMalloc((void**)&oh_[q], sizeof(ObjHost), hipHostMallocDefault));
   memset(oh_[q], 0, sizeof(ObjHost));
+  if (!ev_ransac_[q]) MMT_HIP(hipEventCreateWithFlags(&ev_ransac_[q], hipEventDisableTiming));
+  if (!ev_d3_[q]) MMT_HIP(hipEventCreateWithFlags(&ev_d3_[q], hipEventDisableTiming));
   for (int o = 0; o < kMaxObj; o++) {
     PnPBuf& b = pnp_[q][o];
     b.pts3 = alloc<float>(3 * (size_t)ocap_);
@@ -285,14 +271,14 @@ void Tracker::reset() {
   last_ = kSlots - 1;
   ego_pending_ = false;
   qa_ = ObjFrame();
-  fa_ = ObjFrame();
-  fb_ = ObjFrame();
-  frame_par_ = 0;
+  inflight_.clear();
+  obj_slot_next_ = 0;
   for (FrameSlot& F : slot_) {
     F.nModLabel.clear();
     F.nSemPosition.clear();
     F.vObjMod.clear();
     F.bSecond = false;
+    F.obj_slot = -1;
     mat4_eye(F.Tcw);
   }
 }
@@ -338,24 +324,33 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   obj_flush();  // the chunk's results are complete on return
 }
 
-// One step of the object pipeline: finish D3 of the oldest frame, launch D3 of the next, run
-// stage A of the newest (whose ego pose is known).  Called while the next ego solve runs.
+// Enqueue the queued frame's whole object path (stage A's host decisions need one wait for the
+// grouping statistics; stage B is device-ordered), then read the results of frames older than
+// kObjLag.  Called while the next ego solve runs.
 void Tracker::obj_advance() {
-  if (fb_.active) obj_finish(fb_);  // D3 of frame f-2 done -> its object motions
-  if (fa_.active) {
-    obj_stage_b(fa_);  // MM check + D3 launch for frame f-1 (its RANSAC ran during the last step)
-    fb_ = fa_;
-    fa_ = ObjFrame();
-  }
   if (qa_.active) {
-    obj_stage_a(qa_);  // grouping + RANSAC of frame f, overlapping D3 of frame f-1
-    fa_ = qa_;
+    obj_stage_a(qa_);
+    obj_stage_b(qa_);
+    inflight_.push_back(qa_);
     qa_ = ObjFrame();
+  }
+  while ((int)inflight_.size() > kObjLag) {
+    obj_finish(inflight_.front());
+    inflight_.pop_front();
   }
 }
 
 void Tracker::obj_flush() {
-  for (int k = 0; k < 3 && (qa_.active || fa_.active || fb_.active); k++) obj_advance();
+  if (qa_.active) {
+    obj_stage_a(qa_);
+    obj_stage_b(qa_);
+    inflight_.push_back(qa_);
+    qa_ = ObjFrame();
+  }
+  while (!inflight_.empty()) {
+    obj_finish(inflight_.front());
+    inflight_.pop_front();
+  }
 }
 
 void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
@@ -456,10 +451,8 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
     qa_.active = true;
     qa_.cur = cur_;
     qa_.last = last_;
-    qa_.par = frame_par_;
     qa_.nobj = eh_->nlast_obj > 0 ? -1 : 0;  // -1: grouping decides
     qa_.out = &out;
-    frame_par_ ^= 1;
   }
   ego_pending_ = false;
   if (advance) {
@@ -475,10 +468,13 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   FrameSlot& C = slot_[F.cur];
   FrameSlot& Ls = slot_[F.last];
   hipStream_t st = oa_;
-  const int q = F.par;
+  F.slot = obj_slot_next_;
+  obj_slot_next_ = (obj_slot_next_ + 1) % kObjSlots;
+  const int q = F.slot;
   C.nModLabel.clear();
   C.nSemPosition.clear();
   C.vObjMod.clear();
+  C.obj_slot = -1;
   if (F.nobj == 0) return;  // no object samples carried into this frame
   // ---- B6 + B7 statistics
   GroupArgs g;
@@ -566,6 +562,7 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   F.members.assign(nobj, 0);
   F.po = H.po;
   if (nobj == 0) return;
+  C.obj_slot = q;
   // ---- D5: PnP-RANSAC per object (GetInitModelObj), motion-model check deferred to stage B
   for (int i = 0; i < nobj; i++) {
     const int l = objLabelsNew[i];
@@ -610,70 +607,22 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   }
   MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po, sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
   launch_pnp(d_pnp_[q], nobj, kRansacIters, st);
+  MMT_HIP(hipEventRecord(ev_ransac_[q], st));
 }
 
 void Tracker::obj_stage_b(ObjFrame& F) {
   FrameSlot& C = slot_[F.cur];
   FrameSlot& Ls = slot_[F.last];
-  const int nobj = F.nobj, q = F.par;
-  FrameOut& out = *F.out;
+  const int nobj = F.nobj, q = F.slot;
   if (nobj <= 0) return;
   hipStream_t st = ob_;
-  // RANSAC results (stage A's stream), then the motion-model check with the previous frame's
-  // object motions, now final (Tracking.cc:4375-4405)
-  MMT_HIP(hipStreamSynchronize(oa_));
-  bool any_mm = false;
-  for (int i = 0; i < nobj; i++) {
-    PnPObject& o = F.po[i];
-    if (o.use_mm) {
-      mat4_mul(C.Tcw, Ls.vObjMod[F.PreObjID[i]].data(), o.MM);
-      any_mm = true;
-    }
-  }
-  if (any_mm) {
-    MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po, sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
-    launch_pnp_mm(d_pnp_[q], nobj, st);
-  }
   ObjHost& H = *oh_[q];
-  int* res = H.res;
-  double* Rt = H.Rt;
-  MMT_HIP(hipMemcpyAsync(res, d_res_[q], sizeof(int) * 8 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(Rt, d_Rt_[q], sizeof(double) * 12 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipStreamSynchronize(st));
-  // ---- choose RANSAC model or motion model; D3 descriptors
-  FlowSolveDesc* descs = H.descs;
-  std::vector<std::vector<float>> inits(nobj, std::vector<float>(16));
+  // behind this frame's RANSAC (oa_) by an event, behind the previous frame's D3 (whose motions
+  // the motion model needs) by the stream
+  MMT_HIP(hipStreamWaitEvent(st, ev_ransac_[q], 0));
+  // D3 descriptors; the initial motion is the device's model choice (k_obj_model_choice)
   for (int i = 0; i < nobj; i++) {
-    PnPObject& o = F.po[i];
-    const int n_ransac = res[8 * i + 0] >= 0 ? res[8 * i + 3] : 0;
-    const int n_mm = o.use_mm ? res[8 * i + 4] : -1;
-    float Mod[16];
-    mat4_eye(Mod);
-    for (int r = 0; r < 3; r++) {
-      for (int c = 0; c < 3; c++) Mod[4 * r + c] = (float)Rt[12 * i + 3 * r + c];
-      Mod[4 * r + 3] = (float)Rt[12 * i + 9 + r];
-    }
-    if (o.use_mm && !(n_ransac > n_mm)) {
-      o.use_mm_choice = 1;
-      memcpy(inits[i].data(), o.MM, 64);
-    } else {
-      o.use_mm_choice = 0;
-      memcpy(inits[i].data(), Mod, 64);
-    }
-    if (res[8 * i + 0] < 0 && !o.use_mm_choice) {
-      // RANSAC found no model: empty inlier set (D3 then returns identity)
-      res[8 * i + 3] = 0;
-    }
-    ObjOut oo;
-    oo.label = F.LabId[i];
-    oo.sem_label = F.labels[i];
-    oo.n_points = F.members[i];
-    oo.n_ransac_inliers = n_ransac;
-    oo.n_mm_inliers = n_mm;
-    oo.ransac_iterations = res[8 * i + 2];
-    memcpy(oo.init, inits[i].data(), 64);
-    out.objects.push_back(oo);
-    FlowSolveDesc& d = descs[i];
+    FlowSolveDesc& d = H.descs[i];
     memset(&d, 0, sizeof(d));
     d.d_n = pnp_[q][i].n_subset;
     d.idx = pnp_[q][i].subset;
@@ -681,7 +630,6 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     d.flow = Ls.ob.flow;
     d.depth = Ls.ob.depth;
     memcpy(d.Tcw_last, Ls.Tcw, sizeof(d.Tcw_last));
-    memcpy(d.init, inits[i].data(), 64);
     d.rp_thres = 0.01f;
     d.use_noise = 0;
     d.max_iters = 200;
@@ -689,50 +637,124 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     d.fx = cfg_.fx; d.fy = cfg_.fy; d.cx = cfg_.cx; d.cy = cfg_.cy;
     d.scratch = d_lm_scratch_ + flow_scratch_doubles(lm_cap_) * (1 + i);
     d.cap = lm_cap_;
-    d.pose_out = d_poses_ + 16 * (1 + i);
-    d.stats = d_lmstats_ + 3 * (1 + i);
+    d.pose_out = d_poses3_[q] + 16 * i;
+    d.stats = d_lmstats3_[q] + 3 * i;
   }
-  MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po, sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
+  MMT_HIP(hipMemcpyAsync(d_descs3_[q], H.descs, sizeof(FlowSolveDesc) * nobj,
+                         hipMemcpyHostToDevice, st));
+  // motion model (Tracking.cc:4375-4405): MM = Tcw * vObjMod[PreObjID] of the previous frame,
+  // whose D3 output is still in its slot's buffers
+  bool any_mm = false;
+  MMPrepArgs mp;
+  memset(&mp, 0, sizeof(mp));
+  mp.objs = d_pnp_[q];
+  mp.nobj = nobj;
+  for (int i = 0; i < nobj; i++) {
+    mp.pre[i] = F.po[i].use_mm ? F.PreObjID[i] : -1;
+    any_mm = any_mm || F.po[i].use_mm;
+  }
+  if (any_mm) {
+    if (Ls.obj_slot < 0) throw ArgError("motion model without a previous object solve");
+    mp.prevX = d_poses3_[Ls.obj_slot];
+    mp.prevStats = d_lmstats3_[Ls.obj_slot];
+    memcpy(mp.TcwPrev, Ls.Tcw, sizeof(mp.TcwPrev));
+    memcpy(mp.TcwCur, C.Tcw, sizeof(mp.TcwCur));
+    launch_obj_mm_prep(mp, st);
+    launch_pnp_mm(d_pnp_[q], nobj, st);
+  }
+  launch_obj_model_choice(d_pnp_[q], nobj, d_descs3_[q], d_init_[q], st);
   launch_pnp_subset(d_pnp_[q], nobj, st);
-  MMT_HIP(hipMemcpyAsync(d_descs_ + 1, descs, sizeof(FlowSolveDesc) * nobj, hipMemcpyHostToDevice,
-                         st));
-  int n_hint = 0;
-  for (int i = 0; i < nobj; i++)
-    n_hint = std::max(n_hint, F.po[i].use_mm_choice ? res[8 * i + 4] : res[8 * i + 3]);
-  launch_flow_lm(d_descs_ + 1, nobj, n_hint, st);
+  launch_flow_lm(d_descs3_[q], nobj, 256, st);
+  // everything the finish reads, in one pinned block
+  MMT_HIP(hipMemcpyAsync(H.res, d_res_[q], sizeof(int) * 8 * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(H.init, d_init_[q], sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(H.X, d_poses3_[q], sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(H.lst, d_lmstats3_[q], sizeof(int) * 3 * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(H.nsub, d_nsub_[q], sizeof(int) * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipEventRecord(ev_d3_[q], st));
 }
 
 void Tracker::obj_finish(ObjFrame& F) {
   FrameSlot& C = slot_[F.cur];
-  const int nobj = F.nobj, q = F.par;
+  const int nobj = F.nobj, q = F.slot;
   FrameOut& out = *F.out;
   F.active = false;
   if (nobj <= 0) return;
-  hipStream_t st = ob_;
-  ObjHost& H = *oh_[q];
-  float* X = H.X;
-  int* lst = H.lst;
-  int* nsub = H.nsub;
-  MMT_HIP(hipMemcpyAsync(X, d_poses_ + 16, sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(lst, d_lmstats_ + 3, sizeof(int) * 3 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(nsub, d_nsub_[q], sizeof(int) * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipStreamSynchronize(st));
+  MMT_HIP(hipEventSynchronize(ev_d3_[q]));
+  const ObjHost& H = *oh_[q];
   float TcwInv[16];
   inv_mat(C.Tcw, TcwInv);
   for (int i = 0; i < nobj; i++) {
+    const int* res = H.res + 8 * i;
+    ObjOut oo;
+    oo.label = F.LabId[i];
+    oo.sem_label = F.labels[i];
+    oo.n_points = F.members[i];
+    oo.n_ransac_inliers = res[0] >= 0 ? res[3] : 0;
+    oo.n_mm_inliers = F.po[i].use_mm ? res[4] : -1;
+    oo.ransac_iterations = res[2];
+    memcpy(oo.init, H.init + 16 * i, 64);
     float Xi[16];
-    if (lst[3 * i + 2] != 0)
+    if (H.lst[3 * i + 2] != 0)
       mat4_eye(Xi);  // fewer than 3 correspondences: PoseOptimizationFlow2 returns identity
     else
-      memcpy(Xi, &X[16 * i], 64);
+      memcpy(Xi, H.X + 16 * i, 64);
     mat4_mul(TcwInv, Xi, C.vObjMod[i].data());
-    ObjOut& oo = out.objects[i];
-    oo.n_solve = nsub[i];
-    oo.n_inliers = lst[3 * i + 2] ? 0 : lst[3 * i + 1];
-    oo.iterations = lst[3 * i];
+    oo.n_solve = H.nsub[i];
+    oo.n_inliers = H.lst[3 * i + 2] ? 0 : H.lst[3 * i + 1];
+    oo.iterations = H.lst[3 * i];
     memcpy(oo.X, Xi, 64);
     memcpy(oo.motion, C.vObjMod[i].data(), 64);
+    out.objects.push_back(oo);
   }
+}
+
+// ---------------------------------------------------------------- device side of stage B
+__global__ void k_obj_mm_prep(MMPrepArgs a) {
+  const int i = threadIdx.x;
+  if (i >= a.nobj || a.pre[i] < 0) return;
+  const int p = a.pre[i];
+  float X[16], Ti[16], vobj[16], MM[16];
+  if (a.prevStats[3 * p + 2] != 0)
+    mat4_eye(X);
+  else
+    for (int k = 0; k < 16; k++) X[k] = a.prevX[16 * p + k];
+  inv_mat(a.TcwPrev, Ti);
+  mat4_mul(Ti, X, vobj);  // the previous frame's vObjMod[p] (its finish computes the same)
+  mat4_mul(a.TcwCur, vobj, MM);
+  for (int k = 0; k < 16; k++) a.objs[i].MM[k] = MM[k];
+}
+
+// GetInitModelObj's choice (Tracking.cc:4400-4420): the RANSAC model unless the motion model has
+// at least as many inliers; the chosen motion seeds D3
+__global__ void k_obj_model_choice(PnPObject* objs, int nobj, FlowSolveDesc* descs, float* init) {
+  const int i = threadIdx.x;
+  if (i >= nobj) return;
+  PnPObject& o = objs[i];
+  const int n_ransac = o.result[0] >= 0 ? o.result[3] : 0;
+  const int n_mm = o.use_mm ? o.result[4] : -1;
+  float Mod[16];
+  mat4_eye(Mod);
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) Mod[4 * r + c] = (float)o.Rt[3 * r + c];
+    Mod[4 * r + 3] = (float)o.Rt[9 + r];
+  }
+  const bool choice = o.use_mm && !(n_ransac > n_mm);
+  o.use_mm_choice = choice ? 1 : 0;
+  for (int k = 0; k < 16; k++) {
+    const float v = choice ? o.MM[k] : Mod[k];
+    descs[i].init[k] = v;
+    init[16 * i + k] = v;
+  }
+}
+
+void launch_obj_mm_prep(const MMPrepArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_obj_mm_prep, dim3(1), dim3(64), 0, st, a);
+}
+
+void launch_obj_model_choice(PnPObject* objs, int nobj, FlowSolveDesc* descs, float* init,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_obj_model_choice, dim3(1), dim3(64), 0, st, objs, nobj, descs, init);
 }
 
 }  // namespace mmt
