@@ -463,42 +463,45 @@ __device__ __forceinline__ void rr_partner(int r, int j, int& p, int& q) {
   q = max(j, k);
 }
 
-__device__ __forceinline__ void eig12_group(double (&a)[12], double (&v)[12], int gb, int j,
-                                            bool active, int& rank) {
+__device__ __forceinline__ int eig12_group(double (&a)[12], double (&v)[12], int gb, int j,
+                                           bool active, int& rank) {
   const int lane = threadIdx.x & 63;
   const unsigned long long gmask = active ? (0xFFFull << gb) : 0ull;
-  for (int sweep = 0; sweep < 100; sweep++) {
+  int sweep = 0;
+  for (; sweep < 100; sweep++) {
     bool rotated = false;
     for (int r = 0; r < 11; r++) {
       int p, q;
       rr_partner(r, j, p, q);
       const int src = gb + (j == p ? q : p);
-      double b[12], w[12];
-#pragma unroll
-      for (int k = 0; k < 12; k++) {
-        b[k] = __shfl(a[k], src, 64);
-        w[k] = __shfl(v[k], src, 64);
-      }
       const bool mine_p = (j == p);
-      double al = 0, be = 0, ga = 0;
+      // the partner's column; both lanes of a pair form the same sums bit for bit (same terms,
+      // same order; x*y == y*x), so they take the same decision and rotation
+      double b[12];
+#pragma unroll
+      for (int k = 0; k < 12; k++) b[k] = __shfl(a[k], src, 64);
+      double nm = 0, no = 0, ga = 0;
 #pragma unroll
       for (int k = 0; k < 12; k++) {
-        const double xp = mine_p ? a[k] : b[k], xq = mine_p ? b[k] : a[k];
-        al += xp * xp;
-        be += xq * xq;
-        ga += xp * xq;
+        nm += a[k] * a[k];
+        no += b[k] * b[k];
+        ga += a[k] * b[k];
       }
+      const double al = mine_p ? nm : no, be = mine_p ? no : nm;
       if (active && !(fabs(ga) <= 1e-15 * sqrt(al * be) || ga == 0)) {
         rotated = true;
         const double zeta = (be - al) / (2 * ga);
         const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1 + zeta * zeta));
         const double c = 1 / sqrt(1 + t * t), s = c * t;
+        // p: c x - s y, q: s x + c y (x, y the p and q columns) == c mine + (-/+ s) other
+        const double sg = mine_p ? -s : s;
+        double w[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) w[k] = __shfl(v[k], src, 64);
 #pragma unroll
         for (int k = 0; k < 12; k++) {
-          const double xp = mine_p ? a[k] : b[k], xq = mine_p ? b[k] : a[k];
-          const double vp = mine_p ? v[k] : w[k], vq = mine_p ? w[k] : v[k];
-          a[k] = mine_p ? c * xp - s * xq : s * xp + c * xq;
-          v[k] = mine_p ? c * vp - s * vq : s * vp + c * vq;
+          a[k] = c * a[k] + sg * b[k];
+          v[k] = c * v[k] + sg * w[k];
         }
       }
     }
@@ -518,6 +521,7 @@ __device__ __forceinline__ void eig12_group(double (&a)[12], double (&v)[12], in
     rank += (si > sig) || (i < j && si == sig);
   }
   (void)lane;
+  return sweep;
 }
 
 // ---------------------------------------------------------------- kernels
@@ -930,6 +934,14 @@ __global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
   __shared__ RefitSmem S;
   PnPObject& o = objs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef MMT_PNP_PROFILE
+  long long tp[8];
+  int np = 0;
+  if (tid == 0) tp[np++] = clock64();
+#define PNPPROF() do { if (tid == 0) tp[np++] = clock64(); } while (0)
+#else
+#define PNPPROF() do { } while (0)
+#endif
   const int best = o.result[0];
   if (best < 0) {
     if (tid == 0) o.result[3] = 0;
@@ -958,6 +970,7 @@ __global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
     o.result[3] = base;
   }
   __syncthreads();
+  PNPPROF();
   const int ni = S.n;
   const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
   // control points: centroid, then PCA of the centred points
@@ -1010,6 +1023,7 @@ __global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
     }
     __syncthreads();
   }
+  PNPPROF();
   // M^T M (upper triangle, 78 entries)
   {
     double v[78];
@@ -1043,6 +1057,7 @@ __global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
     }
     __syncthreads();
   }
+  PNPPROF();
   if (wave == 0) {  // the eigen-solve runs on lanes 0..11 of wave 0
     const bool act = lane < 12;
     const int j = act ? lane : 0;
@@ -1053,12 +1068,18 @@ __global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
       v[k] = (act && k == j) ? 1.0 : 0.0;
     }
     int rank;
-    eig12_group(a, v, 0, act ? lane : 12 + (lane % 12), act, rank);
+    const int nsw = eig12_group(a, v, 0, act ? lane : 12 + (lane % 12), act, rank);
+#ifdef MMT_PNP_PROFILE
+    if (lane == 0) S.n = nsw;
+#else
+    (void)nsw;
+#endif
     if (act && rank >= 8)
 #pragma unroll
       for (int k = 0; k < 12; k++) S.ut8[(rank - 8) * 12 + k] = v[k];
   }
   __syncthreads();
+  PNPPROF();
   double* rec = o.hrec;
   for (int e = tid; e < 48; e += blockDim.x) rec[R_UT + e] = S.ut8[e];
   if (tid < 12) rec[R_AL + tid] = S.cws[tid];
@@ -1076,6 +1097,12 @@ __global__ __launch_bounds__(256) void k_refit_null(PnPObject* objs) {
     rec[R_RHO + 4] = d_dist2(cws + 3, cws + 9);
     rec[R_RHO + 5] = d_dist2(cws + 6, cws + 9);
   }
+#ifdef MMT_PNP_PROFILE
+  if (tid == 0)
+    printf("refitprof ni=%d compact=%lld ctrl=%lld mtm=%lld eig=%lld sweeps=%d\n", ni,
+           tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], S.n);
+#endif
+#undef PNPPROF
 }
 
 template <int V>
