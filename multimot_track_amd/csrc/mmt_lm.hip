@@ -131,64 +131,102 @@ __device__ __forceinline__ void normalize_rot(DQuat& q) {
   q.x *= in; q.y *= in; q.z *= in; q.w *= in;
 }
 
-// SE3Quat::exp (g2o, as mmt_devmath.h dse3_exp) on the solve's critical path: the same three
-// regimes (g2o's theta < 1e-5 quirk R = I + O + O^2 kept), with sin(t)/t, (1-cos t)/t^2 and
-// (t - sin t)/t^3 as truncated series below t = 0.05 (remainder < 1e-20), the trace branch of
-// the matrix->quaternion conversion with a refined reciprocal, and the product with P.
+// SE3Quat::exp (g2o, as mmt_devmath.h dse3_exp) times P, on the solve's critical path.  g2o
+// builds R by Rodrigues and converts it to a quaternion; below the sincos regime this computes the
+// same rotation directly as (cos(t/2), w sin(t/2)/t) and V u through two cross products, with the
+// half-angle and V coefficients as truncated series for t < 0.05 (remainder < 1e-20): equal to the
+// matrix route up to rounding.  g2o's t < 1e-5 quirk (R = I + O + O^2, V = R) and the sincos
+// regime keep the matrix route.
 __device__ __forceinline__ DSE3 exp_mul(const double (&u)[6], const DSE3& P) {
   const double o0 = u[0], o1 = u[1], o2 = u[2];
   const double th2 = o0 * o0 + o1 * o1 + o2 * o2;
-  const double O[3][3] = {{0, -o2, o1}, {o2, 0, -o0}, {-o1, o0, 0}};
-  double O2[3][3];
-#pragma unroll
-  for (int r = 0; r < 3; r++)
-#pragma unroll
-    for (int c = 0; c < 3; c++) O2[r][c] = O[r][0] * O[0][c] + O[r][1] * O[1][c] + O[r][2] * O[2][c];
-  double a, b, c2;
-  if (th2 < 1e-10) {
-    a = 1.0;
-    b = 1.0;
-    c2 = 1.0;
-  } else if (th2 < 0.0025) {
-    const double x = th2;
-    constexpr double k6 = 1.0 / 6, k20 = 1.0 / 20, k42 = 1.0 / 42, k72 = 1.0 / 72;
-    constexpr double k24 = 1.0 / 24, k30 = 1.0 / 30, k56 = 1.0 / 56, k90 = 1.0 / 90;
-    constexpr double k120 = 1.0 / 120, k110 = 1.0 / 110;
-    a = 1.0 - x * k6 * (1.0 - x * k20 * (1.0 - x * k42 * (1.0 - x * k72)));
-    b = 0.5 - x * k24 * (1.0 - x * k30 * (1.0 - x * k56 * (1.0 - x * k90)));
-    c2 = k6 - x * k120 * (1.0 - x * k42 * (1.0 - x * k72 * (1.0 - x * k110)));
-  } else {
-    const double th = sqrt(th2);
-    double st, ct;
-    sincos(th, &st, &ct);
-    const double it = drcp(th), it2 = it * it;
-    a = st * it;
-    b = (1 - ct) * it2;
-    c2 = (th - st) * it2 * it;
-  }
-  double R[3][3], V[3][3];
-#pragma unroll
-  for (int r = 0; r < 3; r++)
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-      R[r][c] = (r == c ? 1.0 : 0.0) + a * O[r][c] + b * O2[r][c];
-      V[r][c] = th2 < 1e-10 ? R[r][c] : (r == c ? 1.0 : 0.0) + b * O[r][c] + c2 * O2[r][c];
-    }
   DSE3 s;
-  const double tr = R[0][0] + R[1][1] + R[2][2];
-  if (tr > 0) {
+  if (th2 >= 1e-10 && th2 < 0.0025) {
+    const double x = th2;
+    constexpr double c8 = 1.0 / 8, c48 = 1.0 / 48, c6 = 1.0 / 6, c24 = 1.0 / 24;
+    constexpr double k20 = 1.0 / 20, k42 = 1.0 / 42, k72 = 1.0 / 72, k30 = 1.0 / 30;
+    constexpr double k56 = 1.0 / 56, k90 = 1.0 / 90, k120 = 1.0 / 120, k110 = 1.0 / 110;
+    // cos(t/2) = 1 - x/8 (1 - x/48 (1 - x/120 (1 - x/224)))
+    const double cw = 1.0 - x * c8 * (1.0 - x * c48 * (1.0 - x * k120 * (1.0 - x * (1.0 / 224))));
+    // sin(t/2)/t = 1/2 (1 - x/24 (1 - x/80 (1 - x/168 (1 - x/288))))
+    const double sh = 0.5 * (1.0 - x * c24 * (1.0 - x * (1.0 / 80) * (1.0 - x * (1.0 / 168) *
+                                                                       (1.0 - x * (1.0 / 288)))));
+    const double b = 0.5 - x * c24 * (1.0 - x * k30 * (1.0 - x * k56 * (1.0 - x * k90)));
+    const double c2 = c6 - x * k120 * (1.0 - x * k42 * (1.0 - x * k72 * (1.0 - x * k110)));
+    (void)k20;
+    s.q.w = cw;
+    s.q.x = o0 * sh;
+    s.q.y = o1 * sh;
+    s.q.z = o2 * sh;
+    // V u = u + b (w x u) + c2 (w x (w x u))
+    const double v0 = u[3], v1 = u[4], v2 = u[5];
+    const double a0 = o1 * v2 - o2 * v1, a1 = o2 * v0 - o0 * v2, a2 = o0 * v1 - o1 * v0;
+    const double e0 = o1 * a2 - o2 * a1, e1 = o2 * a0 - o0 * a2, e2 = o0 * a1 - o1 * a0;
+    s.t[0] = v0 + b * a0 + c2 * e0;
+    s.t[1] = v1 + b * a1 + c2 * e1;
+    s.t[2] = v2 + b * a2 + c2 * e2;
+  } else if (th2 < 1e-10) {
+    // g2o's quirk: R = I + O + O^2 (O^2 = w w^T - t^2 I), V = R; Quaternion(R) on the trace
+    // branch (tr = 3 - 2 t^2 > 0): w = sqrt(1 + tr) / 2, v = (R21 - R12, ...) / (4 w) = w_vec / (2 w)
+    const double tr = 3.0 - 2.0 * th2;
     const double rs = drsq(tr + 1.0);
     s.q.w = 0.5 * (tr + 1.0) * rs;
-    const double h = 0.5 * rs;
-    s.q.x = (R[2][1] - R[1][2]) * h;
-    s.q.y = (R[0][2] - R[2][0]) * h;
-    s.q.z = (R[1][0] - R[0][1]) * h;
+    const double h = rs;  // 1 / (2 w) = 1 / sqrt(1 + tr)
+    s.q.x = o0 * h;
+    s.q.y = o1 * h;
+    s.q.z = o2 * h;
+    const double v0 = u[3], v1 = u[4], v2 = u[5];
+    const double a0 = o1 * v2 - o2 * v1, a1 = o2 * v0 - o0 * v2, a2 = o0 * v1 - o1 * v0;
+    const double e0 = o1 * a2 - o2 * a1, e1 = o2 * a0 - o0 * a2, e2 = o0 * a1 - o1 * a0;
+    s.t[0] = v0 + a0 + e0;
+    s.t[1] = v1 + a1 + e1;
+    s.t[2] = v2 + a2 + e2;
+    normalize_rot(s.q);
   } else {
-    s.q = dq_from_R(R);
-  }
+    const double O[3][3] = {{0, -o2, o1}, {o2, 0, -o0}, {-o1, o0, 0}};
+    double O2[3][3];
 #pragma unroll
-  for (int r = 0; r < 3; r++) s.t[r] = V[r][0] * u[3] + V[r][1] * u[4] + V[r][2] * u[5];
-  normalize_rot(s.q);
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int c = 0; c < 3; c++)
+        O2[r][c] = O[r][0] * O[0][c] + O[r][1] * O[1][c] + O[r][2] * O[2][c];
+    double a, b, c2;
+    if (th2 < 1e-10) {
+      a = 1.0;
+      b = 1.0;
+      c2 = 1.0;
+    } else {
+      const double th = sqrt(th2);
+      double st, ct;
+      sincos(th, &st, &ct);
+      const double it = drcp(th), it2 = it * it;
+      a = st * it;
+      b = (1 - ct) * it2;
+      c2 = (th - st) * it2 * it;
+    }
+    double R[3][3], V[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        R[r][c] = (r == c ? 1.0 : 0.0) + a * O[r][c] + b * O2[r][c];
+        V[r][c] = th2 < 1e-10 ? R[r][c] : (r == c ? 1.0 : 0.0) + b * O[r][c] + c2 * O2[r][c];
+      }
+    const double tr = R[0][0] + R[1][1] + R[2][2];
+    if (tr > 0) {
+      const double rs = drsq(tr + 1.0);
+      s.q.w = 0.5 * (tr + 1.0) * rs;
+      const double h = 0.5 * rs;
+      s.q.x = (R[2][1] - R[1][2]) * h;
+      s.q.y = (R[0][2] - R[2][0]) * h;
+      s.q.z = (R[1][0] - R[0][1]) * h;
+    } else {
+      s.q = dq_from_R(R);
+    }
+#pragma unroll
+    for (int r = 0; r < 3; r++) s.t[r] = V[r][0] * u[3] + V[r][1] * u[4] + V[r][2] * u[5];
+    normalize_rot(s.q);
+  }
   // dse3_mul(s, P)
   DSE3 out;
   double x, y, z;
