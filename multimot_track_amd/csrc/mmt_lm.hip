@@ -292,7 +292,8 @@ template <bool FIRST>
 __device__ __forceinline__ void linearise(const Cam& c, const DSE3& P, const LMItem& it,
                                           const double f0, const double f1, double* row,
                                           double scale_term, double& e0, double& e1, double& w,
-                                          double& bl0, double& bl1, double& mh) {
+                                          double& bl0, double& bl1, double& mh,
+                                          double* Bout = nullptr) {
   double x, y, z;
   map(P, it.X, x, y, z);
   const double iz = drcp(z);
@@ -318,6 +319,13 @@ __device__ __forceinline__ void linearise(const Cam& c, const DSE3& P, const LMI
   for (int a = 0; a < 6; a++) {
     B0[a] = w * J[0][a];
     B1[a] = w * J[1][a];
+  }
+  if (Bout) {
+#pragma unroll
+    for (int a = 0; a < 6; a++) {
+      Bout[a] = B0[a];
+      Bout[6 + a] = B1[a];
+    }
   }
   // [2..22] J^T W J, [23..28] J^T W (-e); closed-form Schur sums (valid when every edge has the
   // same weight, see flow_lm_body), B = w J: [30..50] B0a (B0b + B1b), [51..56] B0a (bl0 + bl1),
@@ -364,19 +372,29 @@ __device__ __forceinline__ void schur_terms(const Cam& c, const DSE3& P, const L
 template <bool FIRST>
 __device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const DSE3& PN,
                                              LMItem& it, int i, bool ok2, double lam,
-                                             double ilam, const double* xb, double* row) {
+                                             double ilam, const double* xb, double* row,
+                                             const double* Bcur = nullptr,
+                                             double* Bnext = nullptr) {
   const double bl0 = it.bl[0], bl1 = it.bl[1];
   if (ok2) {
-    double x, y, z;
-    map(P, it.X, x, y, z);
-    double J[2][6];
-    jac(x, y, drcp(z), c.fx, c.fy, J);
     const double w = it.w, h = w + c.pinfo;
     double c0 = bl0, c1 = bl1;
+    if (Bcur) {  // w J at P, kept from the linearisation that built the current system
 #pragma unroll
-    for (int a = 0; a < 6; a++) {
-      c0 -= w * J[0][a] * xb[a];
-      c1 -= w * J[1][a] * xb[a];
+      for (int a = 0; a < 6; a++) {
+        c0 -= Bcur[a] * xb[a];
+        c1 -= Bcur[6 + a] * xb[a];
+      }
+    } else {
+      double x, y, z;
+      map(P, it.X, x, y, z);
+      double J[2][6];
+      jac(x, y, drcp(z), c.fx, c.fy, J);
+#pragma unroll
+      for (int a = 0; a < 6; a++) {
+        c0 -= w * J[0][a] * xb[a];
+        c1 -= w * J[1][a] * xb[a];
+      }
     }
     const double ihl = drcp(h + lam);
     double xl0 = c0 * ihl - h * c1 * ihl * ilam;
@@ -388,7 +406,7 @@ __device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const 
   const double f0 = it.f[0] + xl0, f1 = it.f[1] + xl1;
   double mh = 0;
   linearise<FIRST>(c, PN, it, f0, f1, row, xl0 * (lam * xl0 + bl0) + xl1 * (lam * xl1 + bl1),
-                   it.e[0], it.e[1], it.wn, it.bln[0], it.bln[1], mh);
+                   it.e[0], it.e[1], it.wn, it.bln[0], it.bln[1], mh, Bnext);
 }
 
 #ifdef MMT_LM_PROFILE
@@ -516,6 +534,10 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   };
   LMItem R[IR];
   const int n_reg = IR * nt;
+  // one edge per thread: keep w J of the current and of the trial linearisation in registers,
+  // so the back-substitution needs no projection (two edges per thread would spill)
+  constexpr bool kCacheB = IR == 1;
+  double RB[12], RBn[12];
   // The LM bookkeeping below is computed redundantly by every thread from the block sums in LDS
   // (identical inputs, identical results), so only the 6x6 solve needs a lane-0 section.
   DSE3 P = dse3_from_float(D.init);
@@ -534,7 +556,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         init_item(i, R[k]);
         if (k == 0)
           linearise<true>(c, P, R[k], R[k].f[0], R[k].f[1], row, 0.0, R[k].e[0], R[k].e[1],
-                          R[k].w, R[k].bl[0], R[k].bl[1], mh);
+                          R[k].w, R[k].bl[0], R[k].bl[1], mh, kCacheB ? RB : nullptr);
         else
           linearise<false>(c, P, R[k], R[k].f[0], R[k].f[1], row, 0.0, R[k].e[0], R[k].e[1],
                            R[k].w, R[k].bl[0], R[k].bl[1], mh);
@@ -654,7 +676,8 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
           const int i = tid + k * nt;
           if (i < N) {
             if (k == 0)
-              update_terms<true>(c, P, PN, R[k], i, ok2, lam, ilam, xb, row);
+              update_terms<true>(c, P, PN, R[k], i, ok2, lam, ilam, xb, row,
+                                 kCacheB ? RB : nullptr, kCacheB ? RBn : nullptr);
             else
               update_terms<false>(c, P, PN, R[k], i, ok2, lam, ilam, xb, row);
           }
@@ -738,6 +761,9 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
             it.w = it.wn;
             it.bl[0] = it.bln[0];
             it.bl[1] = it.bln[1];
+            if (kCacheB && k == 0)
+#pragma unroll
+              for (int q = 0; q < 12; q++) RB[q] = RBn[q];
           }
         for (int i = n_reg + tid; i < N; i += nt) item_accept(G, cap, i);
       }
