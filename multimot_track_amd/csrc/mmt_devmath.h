@@ -399,6 +399,48 @@ __device__ inline void block_sum_tile(double* tile, double* part, double* out, i
   __syncthreads();
 }
 
+// block_sum_tile whose result stays in registers: every wave adds the wave partials itself (same
+// order everywhere, so every wave holds the same bits) and returns sum k in lane k.  One barrier,
+// no broadcast through LDS; read single sums with lane_value().
+template <int K>
+__device__ inline double block_sum_tile_lanes(double* tile, double* part, int nw) {
+  static_assert(K <= 64, "block_sum_tile_lanes: at most 64 values");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double* t = tile + (size_t)wave * 64 * kTileStride;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (lane < K) {
+#pragma unroll
+    for (int r0 = 0; r0 < 64; r0 += 16) {
+      double x[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) x[j] = t[(r0 + j) * kTileStride + lane];
+#pragma unroll
+      for (int j = 0; j < 16; j++) acc[j & 7] += x[j];
+    }
+  }
+  const double mine = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  if (nw == 1) return lane < K ? mine : 0.0;
+  if (lane < K) part[wave * K + lane] = mine;
+  __syncthreads();
+  double s = 0;
+  if (lane < K)
+    for (int w = 0; w < nw; w++) s += part[w * K + lane];
+  // the partials are read before anyone rewrites `part` (the next reduction is a full pass away,
+  // with a barrier in between)
+  return s;
+}
+
+// value held by lane `l` (a compile-time constant in unrolled code), as a wave-uniform scalar
+__device__ __forceinline__ double lane_value(double v, int l) {
+  const unsigned long long b = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
 // Workgroup sum of K doubles held per thread; result broadcast in `out` (LDS, K entries).
 // `scratch` holds (blockDim/64) * K doubles.
 template <int K>

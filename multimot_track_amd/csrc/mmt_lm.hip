@@ -472,9 +472,8 @@ struct LMSmem {
   long long prof[12];
   double red[16 * 32];
   double tile[4 * 64 * kTileStride];  // block_sum_rows / block_sum_t tiles (blockDim <= 256)
-  double part[4 * kSums];
+  double part[2][4 * kSums];  // double-buffered: waves read one while a fast wave fills the other
   double S27[32];
-  double H[2][kSums];  // current / trial linearisation sums
   double mh[16];
 };
 
@@ -542,7 +541,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   // (identical inputs, identical results), so only the 6x6 solve needs a lane-0 section.
   DSE3 P = dse3_from_float(D.init);
   const double hin = kInfo + c.pinfo;  // h of every edge when none is Huber-active
-  int hs = 0;  // sm.H[hs] holds the linearisation at P
+  // the sums of the current system (vc) and of the last trial (vt): sum k in lane k of every wave
   // ---- initial linearisation (computeActiveErrors + buildSystem at the initial estimate)
   double* row = tile_row(sm.tile);  // this thread's row of the reduction tile
   // every thread with an edge has one in register slot 0 (N > nt implies all do), so slot 0
@@ -574,14 +573,16 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mh = fmax(mh, __shfl_xor(mh, o, 64));
     if ((tid & 63) == 0) sm.mh[tid >> 6] = mh;
-    block_sum_tile<kSums>(sm.tile, sm.part, sm.H[0], nw);
   }
-  double cur = sm.H[0][0], lam, ni = 2, chk = 0;
+  int pb = 0;  // part buffer of the next reduction
+  double vc = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw), vt = 0;
+  pb ^= 1;
+  double cur = lane_value(vc, 0), lam, ni = 2, chk = 0;
   {
     double md = 0;
 #pragma unroll
     for (int a = 0; a < 6; a++)
-      md = fmax(md, fabs(sm.H[0][2 + a * (a + 3) / 2]));  // diagonal (a, a) of the lower triangle
+      md = fmax(md, fabs(lane_value(vc, 2 + a * (a + 3) / 2)));  // diagonal (a, a) of the lower triangle
     for (int w = 0; w < nw; w++) md = fmax(md, sm.mh[w]);
     lam = 1e-5 * md;
   }
@@ -603,7 +604,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
 #ifdef MMT_LM_NO_CLOSED
       const bool clean = false;
 #else
-      const bool clean = sm.H[hs][29] == 0;
+      const bool clean = lane_value(vc, 29) == 0;
 #endif
       if (!clean) {
         double v[27];
@@ -626,23 +627,22 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
       bool ok2;
       DSE3 PN;
       {
-        const double* Hc = sm.H[hs];
         double A[21], bs[6];
 #pragma unroll
-        for (int k = 0; k < 21; k++) A[k] = Hc[2 + k];
+        for (int k = 0; k < 21; k++) A[k] = lane_value(vc, 2 + k);
 #pragma unroll
-        for (int a = 0; a < 6; a++) bs[a] = Hc[23 + a];
-        // one branch around straight-line code, so each side's LDS loads issue back to back
+        for (int a = 0; a < 6; a++) bs[a] = lane_value(vc, 23 + a);
         if (clean) {
           // SB = sum B1a B1b - B0a B1b = w H - SA (w = kInfo on every edge)
           const double d00 = drcp(hin + lam);
 #pragma unroll
           for (int k = 0; k < 21; k++) {
-            const double sa = Hc[30 + k];
+            const double sa = lane_value(vc, 30 + k);
             A[k] -= d00 * sa + ilam * (kInfo * A[k] - sa);
           }
 #pragma unroll
-          for (int a = 0; a < 6; a++) bs[a] -= d00 * Hc[51 + a] + ilam * Hc[57 + a];
+          for (int a = 0; a < 6; a++)
+            bs[a] -= d00 * lane_value(vc, 51 + a) + ilam * lane_value(vc, 57 + a);
         } else {
 #pragma unroll
           for (int k = 0; k < 21; k++) A[k] -= sm.S27[k];
@@ -696,28 +696,16 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         if (tid >= N)
           for (int q = 0; q < kSums; q++) row[q] = 0;
         MMT_LMPROF(5);
-        block_sum_tile<kSums>(sm.tile, sm.part, sm.H[hs ^ 1], nw);
+        vt = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
+        pb ^= 1;
       }
       MMT_LMPROF(2);
-#ifdef MMT_DBG_TRACE
-      if (tid == 0 && iter < 3) {
-        const double* Hx = sm.H[hs ^ 1];
-        double sh = 0, sb = 0, ss = 0;
-        for (int q = 2; q < 23; q++) sh += Hx[q];
-        for (int q = 23; q < 29; q++) sb += Hx[q];
-        for (int q = 30; q < kSums; q++) ss += Hx[q];
-        printf("trace N=%d nt=%d iter=%d lam=%.9e ok2=%d xb0=%.9e chi=%.9e scale=%.9e H=%.9e b=%.9e "
-               "nout=%g ss=%.9e\n", N, nt, iter, lam, (int)ok2, xb[0], Hx[0], Hx[1], sh, sb, Hx[29], ss);
-      }
-#endif
       // ---- g2o LM step acceptance and termination (every thread, same values)
-      const double* Ht = sm.H[hs ^ 1];
-      const double* Hc = sm.H[hs];
-      const double lastTrialChi = Ht[0];
-      const double tempChi = ok2 ? Ht[0] : DBL_MAX;
-      double scale = Ht[1];
+      const double lastTrialChi = lane_value(vt, 0);
+      const double tempChi = ok2 ? lastTrialChi : DBL_MAX;
+      double scale = lane_value(vt, 1);
 #pragma unroll
-      for (int a = 0; a < 6; a++) scale += xb[a] * (lam * xb[a] + Hc[23 + a]);
+      for (int a = 0; a < 6; a++) scale += xb[a] * (lam * xb[a] + lane_value(vc, 23 + a));
       scale += 1e-3;
       const double rho = (cur - tempChi) / scale;
       const bool accept = rho > 0 && isfinite(tempChi);
@@ -729,7 +717,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         ni = 2;
         cur = tempChi;
         P = PN;
-        hs ^= 1;  // the trial's linearisation becomes the current system
+        vc = vt;  // the trial's linearisation becomes the current system
       } else {
         lam = lam * ni;
         ni = ni * 2;
@@ -771,7 +759,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
 #ifdef MMT_LM_PROFILE
       if (tid == 0) {
         sm.prof[6]++;
-        if (sm.H[hs][29] == 0) sm.prof[7]++;
+        if (lane_value(vc, 29) == 0) sm.prof[7]++;
       }
 #endif
       if (!again) break;
