@@ -158,6 +158,23 @@ typedef struct mmt_flow_problem {
 int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* problem, float* pose_out,
                         int* stats_out /* iterations, inliers, status */);
 
+/* Optimizer::PoseOptimization(Frame*) (reference include/Optimizer.h:43, src/Optimizer.cc:3121-3339)
+ * on the frame's MapPoint observations (the edges of the frame's non-null mvpMapPoints, in index
+ * order): Xw n x 3 world positions, obs n x (u, v, uR) with uR = mvuRight (< 0: mono edge),
+ * inv_sigma2 n = mvInvLevelSigma2[octave].  Tcw = pFrame->mTcw (row-major).  Writes the optimised
+ * pose and mvbOutlier (outlier_out, n bytes); *n_inliers = the function's return value
+ * (nInitialCorrespondences - nBad; 0 with the pose unchanged below 3 edges).  n <= 2048. */
+typedef struct mmt_pose_opt_problem {
+  int n;
+  const float* Xw;
+  const float* obs;
+  const float* inv_sigma2;
+  float Tcw[16];
+  float fx, fy, cx, cy, bf;
+} mmt_pose_opt_problem;
+int mmt_pose_optimization(mmt_ctx* ctx, const mmt_pose_opt_problem* problem, float* pose_out,
+                          uint8_t* outlier_out, int* n_inliers);
+
 /* cv::solvePnPRansac(..., SOLVEPNP_AP3P) probe as called by GetInitModelObj: pts3 n x 3,
  * pts2 n x 2 floats.  R_out row-major 3x3 (after the Rodrigues round trip), t_out 3;
  * inliers_out (optional, n ints) receives the RANSAC inlier indices. */

@@ -58,6 +58,13 @@ class MmtFlowProblem(ctypes.Structure):
                 ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float)]
 
 
+class MmtPoseOptProblem(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("Xw", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+                ("inv_sigma2", ctypes.c_void_p), ("Tcw", ctypes.c_float * 16),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float),
+                ("cy", ctypes.c_float), ("bf", ctypes.c_float)]
+
+
 class MmtProfile(ctypes.Structure):
     _fields_ = [("orb_ms", ctypes.c_double), ("orb_launches", ctypes.c_int64),
                 ("orb_frames", ctypes.c_int64)]
@@ -122,6 +129,7 @@ def lib():
         L.mmt_track_rgbd_chunk_device.argtypes = [vp, i32, vp, sz, vp, sz, vp, sz, vp, sz, vp, vp,
                                                   i32, vp]
         L.mmt_pose_flow_solve.argtypes = [vp, ctypes.POINTER(MmtFlowProblem), vp, vp]
+        L.mmt_pose_optimization.argtypes = [vp, ctypes.POINTER(MmtPoseOptProblem), vp, vp, vp]
         L.mmt_pnp_ransac.argtypes = [vp, vp, vp, i32] + [ctypes.c_float] * 4 + \
             [i32, ctypes.c_double, ctypes.c_double] + [vp] * 5
         L.mmt_profile_enable.argtypes = [vp, i32]
@@ -279,6 +287,25 @@ class Context:
         st = np.zeros(3, np.int32)
         self._check(lib().mmt_pose_flow_solve(self._h, ctypes.byref(pr), _p(pose), _p(st)))
         return int(st[2]), pose.reshape(4, 4), dict(iterations=int(st[0]), inliers=int(st[1]))
+
+    def pose_optimization(self, Xw, obs, inv_sigma2, tcw, K, bf):
+        """Optimizer::PoseOptimization (D1): (n_inliers, pose 4x4, mvbOutlier flags)."""
+        Xw = np.ascontiguousarray(Xw, np.float32)
+        obs = np.ascontiguousarray(obs, np.float32)
+        s2 = np.ascontiguousarray(inv_sigma2, np.float32)
+        n = len(Xw)
+        pr = MmtPoseOptProblem()
+        pr.n = n
+        pr.Xw, pr.obs, pr.inv_sigma2 = Xw.ctypes.data, obs.ctypes.data, s2.ctypes.data
+        pr.Tcw[:] = np.asarray(tcw, np.float32).reshape(16).tolist()
+        pr.fx, pr.fy, pr.cx, pr.cy = K
+        pr.bf = bf
+        pose = np.zeros(16, np.float32)
+        out = np.zeros(max(n, 1), np.uint8)
+        ninl = ctypes.c_int(0)
+        self._check(lib().mmt_pose_optimization(self._h, ctypes.byref(pr), _p(pose), _p(out),
+                                                ctypes.byref(ninl)))
+        return ninl.value, pose.reshape(4, 4), out[:n].astype(bool)
 
     def pnp_ransac(self, pts3, pts2, K, max_iters=500, reproj=0.3, conf=0.98):
         pts3 = np.ascontiguousarray(pts3, np.float32)

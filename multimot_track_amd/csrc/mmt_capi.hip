@@ -366,6 +366,44 @@ int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* pr, float* pose_ou
   });
 }
 
+int mmt_pose_optimization(mmt_ctx* ctx, const mmt_pose_opt_problem* pr, float* pose_out,
+                          uint8_t* outlier_out, int* n_inliers) {
+  if (!ctx || !pr || !pose_out || !n_inliers || pr->n < 0 || pr->n > mmt::kPoseOptMaxEdges ||
+      (pr->n > 0 && (!pr->Xw || !pr->obs || !pr->inv_sigma2 || !outlier_out)))
+    return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    hipStream_t s = ctx->stream;
+    const int n = pr->n, cap = std::max(n, 1);
+    DevBuf<float> X(3 * (size_t)cap), ob(3 * (size_t)cap), s2(cap), pose(16);
+    DevBuf<uint8_t> outl(cap);
+    DevBuf<int> ninl(1);
+    DevBuf<mmt::PoseOptDesc> dd(1);
+    if (n > 0) {
+      MMT_HIP(hipMemcpyAsync(X.p, pr->Xw, 12 * (size_t)n, hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(ob.p, pr->obs, 12 * (size_t)n, hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(s2.p, pr->inv_sigma2, 4 * (size_t)n, hipMemcpyHostToDevice, s));
+    }
+    mmt::PoseOptDesc d;
+    memset(&d, 0, sizeof(d));
+    d.n = n;
+    d.Xw = X.p;
+    d.obs = ob.p;
+    d.inv_sigma2 = s2.p;
+    memcpy(d.Tcw, pr->Tcw, 64);
+    d.fx = pr->fx; d.fy = pr->fy; d.cx = pr->cx; d.cy = pr->cy; d.bf = pr->bf;
+    d.pose_out = pose.p;
+    d.outlier = outl.p;
+    d.n_inliers = ninl.p;
+    MMT_HIP(hipMemcpyAsync(dd.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
+    mmt::launch_pose_opt(dd.p, 1, s);
+    MMT_HIP(hipMemcpyAsync(pose_out, pose.p, 64, hipMemcpyDeviceToHost, s));
+    if (n > 0) MMT_HIP(hipMemcpyAsync(outlier_out, outl.p, n, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(n_inliers, ninl.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+  });
+}
+
 int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, float fx,
                    float fy, float cx, float cy, int max_iters, double reproj, double confidence,
                    double* R_out, double* t_out, int* inliers_out, int* n_inliers,

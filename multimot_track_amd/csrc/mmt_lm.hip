@@ -839,4 +839,285 @@ void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipSt
 
 size_t flow_scratch_doubles(int cap) { return (size_t)G_COUNT * cap; }
 
+// ============================================================================ D1
+// Optimizer::PoseOptimization (reference src/Optimizer.cc:3121-3339; CPU checker:
+// oracle/solve_ref.cpp pose_optimization): pose-only g2o LM over the frame's MapPoint
+// observations.  Mono edges (uR < 0) EdgeSE3ProjectXYZOnlyPose, stereo edges
+// EdgeStereoSE3ProjectXYZOnlyPose (types_six_dof_expmap.cpp:266-364, the stereo projection with a
+// float 1/z), Huber delta^2 5.991 / 7.815, information 1/sigma^2 of the keypoint's octave.  Four
+// rounds of at most 10 LM iterations, each restarting from the input pose on the edges classified
+// inliers by the previous round; the robust kernel is dropped after round 2; fewer than 10 edges
+// stop after one round.  One workgroup, up to 8 edges per thread in registers; per LM trial one
+// pass over the edges (trial errors, robust chi2 and the speculative linearisation at the trial
+// pose) and one block reduction of 28 sums.
+namespace {
+
+constexpr int kPoSums = 28;  // [0] robust chi2, [1..21] lower triangle of H, [22..27] b
+
+struct PoEdgeR {  // constant inputs in registers; the last computed error lives in LDS
+  float X[3], obs[3], s;
+  int flags;  // bit 0 stereo, bit 1 outlier (level 1), bit 2 robust kernel
+};
+constexpr int kPoStereo = 1, kPoOutlier = 2, kPoRobust = 4;
+
+struct PoSmem {
+  double tile[4 * 64 * 33];
+  double red[16 * 32];
+  double H[2][32];  // current / trial sums
+  double e[3][kPoseOptMaxEdges];
+  int flags[kPoseOptMaxEdges];
+};
+
+__device__ __forceinline__ void po_err(const PoEdgeR& E, const DSE3& T, const PoseOptDesc& D,
+                                       double e[3], double& x, double& y, double& z) {
+  const double X[3] = {(double)E.X[0], (double)E.X[1], (double)E.X[2]};
+  map(T, X, x, y, z);
+  if (!(E.flags & kPoStereo)) {
+    const double px = x / z, py = y / z;  // project2d
+    e[0] = (double)E.obs[0] - (px * D.fx + D.cx);
+    e[1] = (double)E.obs[1] - (py * D.fy + D.cy);
+    e[2] = 0;
+  } else {
+    const float invz = 1.0 / z;  // const float invz = 1.0f/trans_xyz[2]
+    const double u = x * invz * D.fx + D.cx, v = y * invz * D.fy + D.cy;
+    e[0] = (double)E.obs[0] - u;
+    e[1] = (double)E.obs[1] - v;
+    e[2] = (double)E.obs[2] - (u - D.bf * invz);
+  }
+}
+
+__device__ __forceinline__ double po_chi2(const PoEdgeR& E, const double e[3]) {
+  return (E.flags & kPoStereo) ? E.s * (e[0] * e[0] + e[1] * e[1] + e[2] * e[2])
+                               : E.s * (e[0] * e[0] + e[1] * e[1]);
+}
+
+// errors at T for an active edge (stored to LDS), robust chi2 and the rho'-weighted
+// J^T Omega J / b terms
+__device__ __forceinline__ void po_linearise(const PoEdgeR& E, const DSE3& T, const PoseOptDesc& D,
+                                             double dM, double dS, double* eo, int stride,
+                                             double* v) {
+  double x, y, z, e[3];
+  po_err(E, T, D, e, x, y, z);
+  eo[0] = e[0];
+  eo[stride] = e[1];
+  eo[2 * stride] = e[2];
+  const bool stereo = E.flags & kPoStereo;
+  const double c = po_chi2(E, e);
+  double r0 = c, r1 = 1.0;
+  if (E.flags & kPoRobust) {
+    const double d = stereo ? dS : dM;
+    huber(c, d * d, d, r0, r1);
+  }
+  v[0] += r0;
+  const double invz = 1.0 / z, invz_2 = invz * invz;
+  double J[3][6];
+  J[0][0] = x * y * invz_2 * D.fx;
+  J[0][1] = -(1 + (x * x * invz_2)) * D.fx;
+  J[0][2] = y * invz * D.fx;
+  J[0][3] = -invz * D.fx;
+  J[0][4] = 0;
+  J[0][5] = x * invz_2 * D.fx;
+  J[1][0] = (1 + y * y * invz_2) * D.fy;
+  J[1][1] = -x * y * invz_2 * D.fy;
+  J[1][2] = -x * invz * D.fy;
+  J[1][3] = 0;
+  J[1][4] = -invz * D.fy;
+  J[1][5] = y * invz_2 * D.fy;
+  J[2][0] = J[0][0] - D.bf * y * invz_2;
+  J[2][1] = J[0][1] + D.bf * x * invz_2;
+  J[2][2] = J[0][2];
+  J[2][3] = J[0][3];
+  J[2][4] = 0;
+  J[2][5] = J[0][5] - D.bf * invz_2;
+  const double w = r1 * (double)E.s;
+  const double se0 = (double)E.s * e[0], se1 = (double)E.s * e[1], se2 = (double)E.s * e[2];
+  int k = 1;
+#pragma unroll
+  for (int a = 0; a < 6; a++)
+#pragma unroll
+    for (int b = 0; b <= a; b++) {
+      double acc = J[0][a] * w * J[0][b] + J[1][a] * w * J[1][b];
+      if (stereo) acc += J[2][a] * w * J[2][b];
+      v[k++] += acc;
+    }
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+    double g = J[0][a] * se0 + J[1][a] * se1;
+    if (stereo) g += J[2][a] * se2;
+    v[22 + a] -= r1 * g;
+  }
+}
+
+__device__ __forceinline__ PoEdgeR po_load(const PoseOptDesc& D, const int* flags, int i) {
+  PoEdgeR E;
+  E.X[0] = D.Xw[3 * i];
+  E.X[1] = D.Xw[3 * i + 1];
+  E.X[2] = D.Xw[3 * i + 2];
+  E.obs[0] = D.obs[3 * i];
+  E.obs[1] = D.obs[3 * i + 1];
+  E.obs[2] = D.obs[3 * i + 2];
+  E.s = D.inv_sigma2[i];
+  E.flags = flags[i];
+  return E;
+}
+
+// Edges are re-read from global memory (L2-resident, a few KB) on every pass and their flags and
+// last errors live in LDS: no per-thread edge arrays, so the kernel stays clear of spills.
+__device__ void pose_opt_body(const PoseOptDesc& D, int N, PoSmem& sm) {
+  const int tid = threadIdx.x, nt = blockDim.x, nw = nt >> 6;
+  // const float deltaMono = sqrt(5.991): double sqrt rounded to float, then setDelta(double)
+  const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
+  int* flags = sm.flags;
+  for (int i = tid; i < N; i += nt) {
+    flags[i] = (D.obs[3 * i + 2] < 0 ? 0 : kPoStereo) | kPoRobust;
+    sm.e[0][i] = sm.e[1][i] = sm.e[2][i] = 0;
+  }
+  __syncthreads();
+  const DSE3 P0 = dse3_from_float(D.Tcw);
+  DSE3 P = P0;
+  int nBad = 0;
+  auto pass = [&](const DSE3& T, double* out) {
+    double v[kPoSums];
+#pragma unroll
+    for (int q = 0; q < kPoSums; q++) v[q] = 0;
+    for (int i = tid; i < N; i += nt) {
+      const PoEdgeR E = po_load(D, flags, i);
+      if (!(E.flags & kPoOutlier)) po_linearise(E, T, D, dM, dS, &sm.e[0][i], kPoseOptMaxEdges, v);
+    }
+    block_sum_t<kPoSums>(v, sm.tile, sm.red, out, nw);
+  };
+  for (int it = 0; it < 4; it++) {
+    P = P0;
+    int hs = 0;
+    pass(P, sm.H[0]);  // computeActiveErrors + buildSystem at the round's start
+    double cur = sm.H[0][0], lam, ni = 2, chk = 0;
+    {
+      double md = 0;
+#pragma unroll
+      for (int a = 0; a < 6; a++) md = fmax(md, fabs(sm.H[0][1 + a * (a + 3) / 2]));
+      lam = 1e-5 * md;
+    }
+    int nRaul = 0;
+    double xb[6] = {0, 0, 0, 0, 0, 0};
+    for (int iter = 0; iter < 10; iter++) {
+      const double ini = cur;
+      int qmax = 0;
+      bool bad = false;
+      for (;;) {
+        // ---- solve (H + lambda I) x = b (every thread, identical inputs)
+        const double* Hc = sm.H[hs];
+        double A[21], bs[6];
+#pragma unroll
+        for (int q = 0; q < 21; q++) A[q] = Hc[1 + q];
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+          A[a * (a + 3) / 2] += lam;
+          bs[a] = Hc[22 + a];
+        }
+        const bool ok2 = ldlt6_packed(A, bs);
+#pragma unroll
+        for (int a = 0; a < 6; a++) xb[a] = ok2 ? bs[a] : xb[a];
+        const DSE3 PN = exp_mul(xb, P);
+        pass(PN, sm.H[hs ^ 1]);  // trial errors, robust chi2, speculative linearisation
+        const double* Ht = sm.H[hs ^ 1];
+        const double lastTrialChi = Ht[0];
+        const double tempChi = ok2 ? Ht[0] : DBL_MAX;
+        double scale = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++) scale += xb[a] * (lam * xb[a] + Hc[22 + a]);
+        scale += 1e-3;
+        const double rho = (cur - tempChi) / scale;
+        const bool accept = rho > 0 && isfinite(tempChi);
+        if (accept) {
+          const double t = 2 * rho - 1;
+          double alpha = 1. - t * t * t;
+          alpha = fmin(alpha, 2. / 3.);
+          lam = lam * fmax(1. / 3., alpha);
+          ni = 2;
+          cur = tempChi;
+          P = PN;
+          hs ^= 1;
+        } else {
+          lam = lam * ni;
+          ni = ni * 2;
+        }
+        qmax++;
+        const bool again = (rho < 0 && qmax < 10);
+        if (!again) {
+          bool ok = true;
+          if (qmax == 10 || rho == 0) ok = false;
+          if (ok) {
+            if ((ini - cur) * 1e3 < ini)
+              nRaul++;
+            else
+              nRaul = 0;
+            if (nRaul >= 3) ok = false;
+          }
+          if (chk < lastTrialChi && iter > 0) ok = false;
+          chk = lastTrialChi;
+          bad = !ok;
+          break;
+        }
+      }
+      if (bad) break;
+    }
+    // ---- re-classification (Optimizer.cc:3266-3322): edges that sat the round out get their
+    // error at the optimised pose, the others keep the last computed one
+    double nb[1] = {0};
+    for (int i = tid; i < N; i += nt) {
+      PoEdgeR E = po_load(D, flags, i);
+      double e[3];
+      if (E.flags & kPoOutlier) {
+        double x, y, z;
+        po_err(E, P, D, e, x, y, z);
+        sm.e[0][i] = e[0];
+        sm.e[1][i] = e[1];
+        sm.e[2][i] = e[2];
+      } else {
+        e[0] = sm.e[0][i];
+        e[1] = sm.e[1][i];
+        e[2] = sm.e[2][i];
+      }
+      const double c = po_chi2(E, e);
+      const float thr = (E.flags & kPoStereo) ? 7.815f : 5.991f;
+      int f = c > (double)thr ? (E.flags | kPoOutlier) : (E.flags & ~kPoOutlier);
+      nb[0] += (f & kPoOutlier) ? 1.0 : 0.0;
+      if (it == 2) f &= ~kPoRobust;
+      flags[i] = f;
+    }
+    block_sum<1>(nb, sm.red, sm.H[0], nw);  // ends with a barrier: flags visible to all
+    nBad = (int)sm.H[0][0];
+    __syncthreads();  // sm.H[0] is rewritten by the next round's first reduction
+    if (N < 10) break;  // optimizer.edges().size() < 10
+  }
+  for (int i = tid; i < N; i += nt) D.outlier[i] = (flags[i] & kPoOutlier) ? 1 : 0;
+  if (tid == 0) {
+    dse3_to_float(P, D.pose_out);
+    *D.n_inliers = N - nBad;
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_pose_opt(const PoseOptDesc* __restrict__ descs) {
+  __shared__ PoSmem sm;
+  const PoseOptDesc& D = descs[blockIdx.x];
+  const int N = D.n;
+  const int nt = blockDim.x;
+  if (N < 3) {
+    if (threadIdx.x == 0) {
+      for (int k = 0; k < 16; k++) D.pose_out[k] = D.Tcw[k];
+      *D.n_inliers = 0;
+    }
+    for (int i = threadIdx.x; i < N; i += nt) D.outlier[i] = 0;
+    return;
+  }
+  pose_opt_body(D, N, sm);
+}
+
+void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, hipStream_t st) {
+  hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs);
+}
+
+
 }  // namespace mmt

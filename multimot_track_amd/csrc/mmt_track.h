@@ -105,4 +105,19 @@ void launch_obj_group(const GroupArgs& a, hipStream_t st);
 void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st);
 size_t flow_scratch_doubles(int cap);
 
+// D1: Optimizer::PoseOptimization on one frame's MapPoint observations (at most 2048 edges).
+struct PoseOptDesc {
+  int n;
+  const float* Xw;          // n x 3
+  const float* obs;         // n x (u, v, uR); uR < 0: mono edge
+  const float* inv_sigma2;  // n
+  float Tcw[16];
+  double fx, fy, cx, cy, bf;
+  float* pose_out;
+  uint8_t* outlier;         // n: mvbOutlier
+  int* n_inliers;
+};
+constexpr int kPoseOptMaxEdges = 2048;
+void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, hipStream_t st);
+
 }  // namespace mmt

@@ -141,6 +141,23 @@ def flow_solve(obs, flow, depth, tcw_last, init, rp_thres, prior_info, max_iters
     return rc, pose.reshape(4, 4), dict(iterations=int(st[0]), inliers=int(st[1]))
 
 
+def pose_optimization(Xw, obs, inv_sigma2, tcw, K, bf):
+    """Optimizer::PoseOptimization (D1): returns (n_inliers, pose 4x4, outlier flags)."""
+    L = lib()
+    L.oracle_pose_optimization.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + \
+        [ctypes.c_float] * 5 + [ctypes.c_void_p] * 2
+    Xw = np.ascontiguousarray(Xw, np.float32)
+    obs = np.ascontiguousarray(obs, np.float32)
+    s2 = np.ascontiguousarray(inv_sigma2, np.float32)
+    t = np.ascontiguousarray(tcw, np.float32).reshape(16)
+    n = len(Xw)
+    pose = np.zeros(16, np.float32)
+    out = np.zeros(max(n, 1), np.uint8)
+    rc = L.oracle_pose_optimization(n, _p(Xw), _p(obs), _p(s2), _p(t), K[0], K[1], K[2], K[3], bf,
+                                    _p(pose), _p(out))
+    return rc, pose.reshape(4, 4), out[:n].astype(bool)
+
+
 def pnp_ransac(pts3, pts2, K, max_iters=500, reproj=0.3, conf=0.98):
     L = lib()
     L.oracle_pnp_ransac.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + \

@@ -155,6 +155,20 @@ int oracle_flow_solve(int n, const float* obs, const float* flow, const float* d
   return rc;
 }
 
+// Optimizer::PoseOptimization probe (D1).
+int oracle_pose_optimization(int n, const float* Xw, const float* obs, const float* inv_sigma2,
+                             const float* tcw, float fx, float fy, float cx, float cy, float bf,
+                             float* pose_out, unsigned char* outlier) {
+  PoseOptProblem p;
+  p.n = n;
+  p.Xw = Xw;
+  p.obs = obs;
+  p.inv_sigma2 = inv_sigma2;
+  memcpy(p.Tcw, tcw, sizeof(p.Tcw));
+  p.fx = fx; p.fy = fy; p.cx = cx; p.cy = cy; p.bf = bf;
+  return pose_optimization(p, pose_out, outlier);
+}
+
 int oracle_pnp_ransac(const float* pts3, const float* pts2, int n, double fx, double fy,
                       double cx, double cy, int max_iters, double reproj, double conf,
                       double* R9, double* t3, int* inliers, int* n_inliers, int* iters) {

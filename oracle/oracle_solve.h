@@ -25,6 +25,19 @@ struct FlowSolveStats {
 };
 int flow_pose_solve(const FlowProblem& p, float pose_out[16], FlowSolveStats* st);
 
+// Optimizer::PoseOptimization (Optimizer.cc:3121-3339): pose-only LM over the frame's MapPoint
+// observations, mono (uR < 0) and stereo edges, 4 rounds x 10 iterations with re-classification.
+struct PoseOptProblem {
+  int n = 0;
+  const float* Xw = nullptr;      // n x 3 MapPoint world positions
+  const float* obs = nullptr;     // n x (u, v, uR): undistorted keypoint, right u (< 0: mono)
+  const float* inv_sigma2 = nullptr;  // n: mvInvLevelSigma2[octave]
+  float Tcw[16];                  // row-major initial pose (pFrame->mTcw)
+  float fx = 0, fy = 0, cx = 0, cy = 0, bf = 0;
+};
+// returns nInitialCorrespondences - nBad (0 and pose untouched below 3 edges); outlier[i] = mvbOutlier
+int pose_optimization(const PoseOptProblem& p, float pose_out[16], uint8_t* outlier);
+
 float cv_rng_first_gaussian(uint64_t seed);
 float noisy_depth(float z, float g0);
 

@@ -509,4 +509,211 @@ int flow_pose_solve(const FlowProblem& P, float pose_out[16], FlowSolveStats* st
   return 0;
 }
 
+// ------------------------------------------------------------------ D1: PoseOptimization
+// Optimizer::PoseOptimization (Optimizer.cc:3121-3339) with the g2o machinery it runs:
+//   EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose (types_six_dof_expmap.cpp:266-364;
+//   the stereo cam_project takes invz as a float, .cpp:296-303), RobustKernelHuber, the
+//   rho'-weighted quadratic form (base_unary_edge.hpp:56-63), OptimizationAlgorithmLevenberg::solve
+//   and the modified SparseOptimizer::optimize (chi2-increase stop) as in flow_pose_solve above.
+// Every round restarts from pFrame->mTcw (Optimizer.cc:3263), optimises the level-0 edges for 10
+// iterations, then re-classifies every edge by its (non-robust) chi2 (3266-3322); the robust kernel
+// is dropped after round 2's classification; fewer than 10 edges stop after one round (3324).
+namespace {
+struct PoEdge {
+  double X[3], obs[3], s;  // world point, measurement, information scale
+  bool stereo, outlier, robust;
+  double e[3];             // last computed error
+};
+
+void po_error(const PoEdge& E, const SE3& T, double fx, double fy, double cx, double cy, double bf,
+              double e[3]) {
+  double pc[3];
+  se3_map(T, E.X, pc);
+  if (!E.stereo) {  // obs - cam_project(project2d(Xc))
+    const double px = pc[0] / pc[2], py = pc[1] / pc[2];
+    e[0] = E.obs[0] - (px * fx + cx);
+    e[1] = E.obs[1] - (py * fy + cy);
+    e[2] = 0;
+  } else {
+    const float invz = 1.0 / pc[2];  // const float invz = 1.0f/trans_xyz[2]
+    const double u = pc[0] * invz * fx + cx, v = pc[1] * invz * fy + cy;
+    e[0] = E.obs[0] - u;
+    e[1] = E.obs[1] - v;
+    e[2] = E.obs[2] - (u - bf * invz);
+  }
+}
+
+double po_chi2(const PoEdge& E, const double e[3]) {
+  return E.stereo ? E.s * (e[0] * e[0] + e[1] * e[1] + e[2] * e[2]) : E.s * (e[0] * e[0] + e[1] * e[1]);
+}
+}  // namespace
+
+int pose_optimization(const PoseOptProblem& P, float pose_out[16], uint8_t* outlier) {
+  const int N = P.n;
+  const double fx = P.fx, fy = P.fy, cx = P.cx, cy = P.cy, bf = P.bf;
+  const float deltaMono = std::sqrt(5.991), deltaStereo = std::sqrt(7.815);
+  const double dM = deltaMono, dS = deltaStereo;
+  std::vector<PoEdge> E(N);
+  for (int i = 0; i < N; i++) {
+    for (int k = 0; k < 3; k++) E[i].X[k] = P.Xw[3 * i + k];
+    E[i].obs[0] = P.obs[3 * i];
+    E[i].obs[1] = P.obs[3 * i + 1];
+    E[i].obs[2] = P.obs[3 * i + 2];
+    E[i].stereo = !(P.obs[3 * i + 2] < 0);
+    E[i].s = P.inv_sigma2[i];
+    E[i].outlier = false;
+    E[i].robust = true;
+    E[i].e[0] = E[i].e[1] = E[i].e[2] = 0;
+  }
+  if (N < 3) {
+    for (int i = 0; i < N; i++) outlier[i] = 0;
+    memcpy(pose_out, P.Tcw, 64);
+    return 0;
+  }
+  const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
+  auto robust_chi2 = [&]() {  // activeRobustChi2 over the level-0 edges, in edge order
+    double chi = 0;
+    for (int i = 0; i < N; i++) {
+      if (E[i].outlier) continue;
+      const double c = po_chi2(E[i], E[i].e);
+      if (E[i].robust) {
+        const double d = E[i].stereo ? dS : dM;
+        double r0, r1;
+        huber(c, d * d, d, r0, r1);
+        chi += r0;
+      } else {
+        chi += c;
+      }
+    }
+    return chi;
+  };
+  SE3 pose = se3_from_float(P.Tcw);
+  int nBad = 0;
+  for (int it = 0; it < 4; it++) {
+    pose = se3_from_float(P.Tcw);  // vSE3->setEstimate(toSE3Quat(pFrame->mTcw))
+    double lambda = 0, ni = 2, chk = 0;
+    int nRaul = 0;
+    double xbuf[6] = {0, 0, 0, 0, 0, 0};
+    for (int iter = 0; iter < 10; iter++) {
+      for (int i = 0; i < N; i++)
+        if (!E[i].outlier) po_error(E[i], pose, fx, fy, cx, cy, bf, E[i].e);
+      double currentChi = robust_chi2();
+      const double iniChi = currentChi;
+      double H[6][6] = {{0}}, b[6] = {0};
+      for (int i = 0; i < N; i++) {
+        if (E[i].outlier) continue;
+        double pc[3];
+        se3_map(pose, E[i].X, pc);
+        const double x = pc[0], y = pc[1], invz = 1.0 / pc[2], invz_2 = invz * invz;
+        double J[3][6] = {{x * y * invz_2 * fx, -(1 + (x * x * invz_2)) * fx, y * invz * fx,
+                           -invz * fx, 0, x * invz_2 * fx},
+                          {(1 + y * y * invz_2) * fy, -x * y * invz_2 * fy, -x * invz * fy, 0,
+                           -invz * fy, y * invz_2 * fy},
+                          {0, 0, 0, 0, 0, 0}};
+        if (E[i].stereo) {
+          J[2][0] = J[0][0] - bf * y * invz_2;
+          J[2][1] = J[0][1] + bf * x * invz_2;
+          J[2][2] = J[0][2];
+          J[2][3] = J[0][3];
+          J[2][4] = 0;
+          J[2][5] = J[0][5] - bf * invz_2;
+        }
+        const int rows = E[i].stereo ? 3 : 2;
+        double r1 = 1.0;
+        if (E[i].robust) {
+          const double d = E[i].stereo ? dS : dM;
+          double r0;
+          huber(po_chi2(E[i], E[i].e), d * d, d, r0, r1);
+        }
+        const double w = r1 * E[i].s;  // rho' Omega (Omega = s I)
+        for (int a = 0; a < 6; a++) {
+          for (int c = 0; c < 6; c++) {
+            double acc = 0;
+            for (int r = 0; r < rows; r++) acc += J[r][a] * w * J[r][c];
+            H[a][c] += acc;
+          }
+          double g = 0;
+          for (int r = 0; r < rows; r++) g += J[r][a] * (E[i].s * E[i].e[r]);
+          b[a] -= r1 * g;  // b -= rho' A^T Omega e
+        }
+      }
+      if (iter == 0) {
+        double maxd = 0;
+        for (int a = 0; a < 6; a++) maxd = std::max(maxd, std::fabs(H[a][a]));
+        lambda = 1e-5 * maxd;
+        ni = 2;
+        nRaul = 0;
+      }
+      // g2o accumulates b -= rho' J^T Omega e and solves (H + lambda I) dx = b
+      double rhs[6];
+      for (int a = 0; a < 6; a++) rhs[a] = b[a];
+      double rho = 0, lastTrialChi = 0;
+      int qmax = 0;
+      do {
+        const SE3 pose_b = pose;
+        double Hs[6][6];
+        for (int a = 0; a < 6; a++)
+          for (int c = 0; c < 6; c++) Hs[a][c] = H[a][c] + (a == c ? lambda : 0.0);
+        double xp[6];
+        const bool ok2 = ldlt_solve6(Hs, rhs, xp);
+        if (ok2) memcpy(xbuf, xp, sizeof(xp));
+        pose = se3_mul(se3_exp(xbuf), pose);
+        for (int i = 0; i < N; i++)
+          if (!E[i].outlier) po_error(E[i], pose, fx, fy, cx, cy, bf, E[i].e);
+        double tempChi = robust_chi2();
+        lastTrialChi = tempChi;
+        if (!ok2) tempChi = DBL_MAX;
+        rho = currentChi - tempChi;
+        double scale = 0;
+        for (int a = 0; a < 6; a++) scale += xbuf[a] * (lambda * xbuf[a] + rhs[a]);
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && std::isfinite(tempChi)) {
+          double alpha = 1. - std::pow((2 * rho - 1), 3);
+          alpha = std::min(alpha, 2. / 3.);
+          lambda *= std::max(1. / 3., alpha);
+          ni = 2;
+          currentChi = tempChi;
+        } else {
+          lambda *= ni;
+          ni *= 2;
+          pose = pose_b;
+        }
+        qmax++;
+      } while (rho < 0 && qmax < 10);
+      bool ok = true;
+      if (qmax == 10 || rho == 0) ok = false;
+      if (ok) {
+        if ((iniChi - currentChi) * 1e3 < iniChi)
+          nRaul++;
+        else
+          nRaul = 0;
+        if (nRaul >= 3) ok = false;
+      }
+      if (chk < lastTrialChi && iter > 0) ok = false;
+      chk = lastTrialChi;
+      if (!ok) break;
+    }
+    // re-classification (Optimizer.cc:3266-3322): edges that sat this round out get their error
+    // at the optimised pose; the others keep the last computed one
+    nBad = 0;
+    for (int i = 0; i < N; i++) {
+      if (E[i].outlier) po_error(E[i], pose, fx, fy, cx, cy, bf, E[i].e);
+      const double c = po_chi2(E[i], E[i].e);
+      const float thr = E[i].stereo ? chi2Stereo : chi2Mono;
+      if (c > thr) {
+        E[i].outlier = true;
+        nBad++;
+      } else {
+        E[i].outlier = false;
+      }
+      if (it == 2) E[i].robust = false;
+    }
+    if (N < 10) break;  // optimizer.edges().size() < 10
+  }
+  se3_to_float(pose, pose_out);
+  for (int i = 0; i < N; i++) outlier[i] = E[i].outlier ? 1 : 0;
+  return N - nBad;
+}
+
 }  // namespace oracle

@@ -63,3 +63,35 @@ def pnp_problem(seed, n, outlier_frac=0.3, pix_noise=0.1, K=K_KITTI):
     if nout:
         uv[-nout:] += rng.uniform(-40, 40, size=(nout, 2))
     return p.astype(np.float32), uv.astype(np.float32), T
+
+
+def pose_opt_problem(seed, n, outlier_frac=0.1, pix_noise=0.8, mono_frac=0.2, K=K_KITTI,
+                     bf=387.5744):
+    """Frame observations of n MapPoints for Optimizer::PoseOptimization: world points, undistorted
+    keypoints with octave-scaled noise, right coordinates (uR = u - bf/z, or -1 for mono), the
+    per-octave information 1/sigma^2 (ORB scale 1.2) and a perturbed initial pose."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = K
+    T = se3(rot(rng.normal(size=3), 0.05 * rng.normal()), rng.normal(size=3))
+    u = rng.uniform(20, 1222, n)
+    v = rng.uniform(20, 355, n)
+    z = rng.uniform(4.0, 40.0, n)
+    pc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    Tinv = np.linalg.inv(T.astype(np.float64))
+    Xw = ((Tinv[:3, :3] @ pc.T).T + Tinv[:3, 3]).astype(np.float32)
+    octave = rng.integers(0, 8, n)
+    scale = 1.2 ** octave
+    inv_sigma2 = (1.0 / (scale * scale)).astype(np.float32)
+    uo = u + rng.normal(scale=pix_noise, size=n) * scale
+    vo = v + rng.normal(scale=pix_noise, size=n) * scale
+    ur = uo - bf / z
+    mono = rng.uniform(size=n) < mono_frac
+    ur[mono] = -1.0
+    nout = int(outlier_frac * n)
+    if nout:
+        uo[:nout] += rng.uniform(-40, 40, nout)
+        vo[:nout] += rng.uniform(-40, 40, nout)
+    obs = np.stack([uo, vo, ur], 1).astype(np.float32)
+    dT = se3(rot(rng.normal(size=3), 0.02 * rng.normal()), rng.normal(size=3) * 0.1)
+    init = (dT.astype(np.float64) @ T.astype(np.float64)).astype(np.float32)
+    return Xw, obs, inv_sigma2, init, T

@@ -149,3 +149,26 @@ def test_track_synthetic_c2_ego_only_matches_oracle(oracle_mod):
 def test_track_synthetic_c5_1080p_matches_oracle(oracle_mod):
     """BASELINE C5 geometry: 1920x1080, 8000 features, 8 moving boxes."""
     assert _synthetic_parity(1920, 1080, 8000, 8, 4, 2000) >= 4
+
+
+@pytest.mark.parametrize("seed,n,out,mono", [(0, 400, 0.15, 0.2), (1, 1500, 0.2, 0.1),
+                                             (2, 60, 0.3, 0.5), (3, 8, 0.0, 0.3),
+                                             (4, 2048, 0.1, 0.0), (5, 300, 0.0, 1.0)])
+def test_pose_optimization_matches_oracle(ctx, oracle_mod, seed, n, out, mono):
+    """D1 (Optimizer::PoseOptimization): pose within 1e-4, mvbOutlier and the inlier count
+    exact, for mixed mono/stereo edges, outliers, the one-round (< 10 edges) case and the 2048
+    edge maximum."""
+    from synth_problems import pose_opt_problem
+    Xw, obs, s2, init, _ = pose_opt_problem(seed, n, outlier_frac=out, mono_frac=mono)
+    n_o, pose_o, outl_o = oracle_mod.pose_optimization(Xw, obs, s2, init, K_KITTI, 387.5744)
+    n_g, pose_g, outl_g = ctx.pose_optimization(Xw, obs, s2, init, K_KITTI, 387.5744)
+    assert np.abs(pose_g - pose_o).max() < POSE_TOL
+    assert n_g == n_o
+    assert np.array_equal(outl_g, outl_o)
+
+
+def test_pose_optimization_too_few_edges(ctx):
+    from synth_problems import pose_opt_problem
+    Xw, obs, s2, init, _ = pose_opt_problem(9, 2)
+    n_g, pose_g, outl_g = ctx.pose_optimization(Xw, obs, s2, init, K_KITTI, 387.5744)
+    assert n_g == 0 and np.array_equal(pose_g, init) and not outl_g.any()

@@ -100,3 +100,22 @@ def test_tracker_oracle_on_kitti_sample(oracle_mod, kitti_frames):
     rel = np.linalg.norm(traj[2][:3, 3] - traj[0][:3, 3])
     rel_gt = np.linalg.norm(gt[2][:3, 3] - gt[0][:3, 3])
     assert abs(rel - rel_gt) < 0.15 * rel_gt
+
+
+def test_pose_optimization_oracle_recovers_pose(oracle_mod):
+    """D1 checker sanity: from a perturbed start the pose-only LM lands near the true pose and
+    flags the gross outliers (Optimizer.cc:3121-3339)."""
+    from synth_problems import K_KITTI, pose_opt_problem
+    Xw, obs, s2, init, T = pose_opt_problem(0, 400, outlier_frac=0.15, pix_noise=0.3)
+    n_in, pose, outl = oracle_mod.pose_optimization(Xw, obs, s2, init, K_KITTI, 387.5744)
+    assert np.abs(pose - T).max() < 5e-3 < np.abs(init - T).max()
+    # the first 60 observations carry +-40 px displacements (synth_problems.pose_opt_problem)
+    assert outl[:60].mean() > 0.7 and outl[60:].mean() < 0.1
+    assert n_in == len(Xw) - int(outl.sum())
+
+
+def test_pose_optimization_oracle_few_edges(oracle_mod):
+    from synth_problems import K_KITTI, pose_opt_problem
+    Xw, obs, s2, init, _ = pose_opt_problem(1, 2)
+    n_in, pose, outl = oracle_mod.pose_optimization(Xw, obs, s2, init, K_KITTI, 387.5744)
+    assert n_in == 0 and np.array_equal(pose, init) and not outl.any()
