@@ -19,6 +19,14 @@
  *                          System.cc:169-220 -> Tracking::GrabImageRGBD Tracking.cc:438-919
  *   mmt_pose_flow_solve <- Optimizer::PoseOptimizationFlow2Cam / PoseOptimizationFlow2
  *                          Optimizer.h:43-56, Optimizer.cc:396-601 / 2170-2377
+ *   mmt_pose_optimization <- Optimizer::PoseOptimization(Frame*) Optimizer.cc:3121-3339
+ *   mmt_frame_grid      <- Frame::ComputeStereoFromRGBD + AssignFeaturesToGrid Frame.cc:1041, 601
+ *   mmt_search_by_projection_frame
+ *                       <- ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
+ *                          ORBmatcher.h / ORBmatcher.cc:1958-2102
+ *   mmt_search_local_points
+ *                       <- Tracking::SearchLocalPoints Tracking.cc:3416-3466 ->
+ *                          ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) :418-502
  *   mmt_destroy         <- System::Shutdown / delete
  */
 #ifndef MMT_H
@@ -182,6 +190,69 @@ int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, fl
                    float fy, float cx, float cy, int max_iters, double reproj, double confidence,
                    double* R_out, double* t_out, int* inliers_out, int* n_inliers,
                    int* iters_out /* iterations run, best hypothesis */);
+
+/* ---- Frame grid and projection matching (rows B3, C1-C3 of the hot path) ----------------------
+ * The current Frame as the matchers read it: its ORB keys (mvKeysUn == mvKeys, no distortion),
+ * descriptors (n x 32) and the metric depth map (w x h floats, the Tcw-independent part of
+ * Frame::ComputeStereoFromRGBD).  Camera intrinsics, bf and the scale pyramid come from the
+ * context's configuration; image bounds are [0, width] x [0, height] (Frame::ComputeImageBounds). */
+typedef struct mmt_match_frame {
+  int n;
+  const mmt_kp* kps;
+  const uint8_t* desc;
+  const float* depth;
+  float Tcw[16];        /* row-major mTcw used for the projections                         */
+} mmt_match_frame;
+
+/* Frame::ComputeStereoFromRGBD + AssignFeaturesToGrid (Frame.cc:1041-1062, 601-616, PosInGrid
+ * 765-775): uR_out/depth_out (n) = mvuRight/mvDepth (-1 without depth); the 64 x 48 grid mGrid as
+ * CSR: cell (ix, iy) holds cell_idx[cell_start[ix*48+iy] .. cell_start[ix*48+iy+1]) in ascending
+ * key order; cell_start has 3073 entries, cell_idx n.  n <= 16384. */
+int mmt_frame_grid(mmt_ctx* ctx, const mmt_match_frame* cur, float* uR_out, float* depth_out,
+                   int* cell_start, int* cell_idx);
+
+/* The last Frame as ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) reads it:
+ * per last-frame key i, its keypoint (octave, angle), the world position and descriptor of
+ * mvpMapPoints[i], and active[i] = (mvpMapPoints[i] != NULL && !mvbOutlier[i]). */
+typedef struct mmt_last_frame {
+  int n;
+  const mmt_kp* kps;
+  const float* Xw;          /* n x 3 */
+  const uint8_t* mp_desc;   /* n x 32 */
+  const uint8_t* active;    /* n */
+  float Tcw[16];            /* row-major LastFrame.mTcw */
+} mmt_last_frame;
+
+/* ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) with mbCheckOrientation
+ * (ORBmatcher.cc:1958-2102, called by Tracking::TrackWithMotionModel Tracking.cc:2962-3010; C1
+ * DescriptorDistance ORBmatcher.cc:2279-2295).  The current frame starts with no MapPoints (as
+ * after the fill(NULL) of Tracking.cc:2975); match_out[i2] (cur->n) = the last-frame index bound
+ * to current key i2, or -1; *nmatches = the function's return value. */
+int mmt_search_by_projection_frame(mmt_ctx* ctx, const mmt_match_frame* cur,
+                                   const mmt_last_frame* last, float th, int mono,
+                                   int check_orientation, int32_t* match_out, int* nmatches);
+
+/* Local MapPoints as Tracking::SearchLocalPoints sees them (Tracking.cc:3416-3466): position,
+ * mNormalVector, mfMinDistance / mfMaxDistance, mDescriptor, and skip = already matched in this
+ * frame (mnLastFrameSeen == mCurrentFrame.mnId) or isBad(). */
+typedef struct mmt_local_points {
+  int m;
+  const float* Xw;        /* m x 3  */
+  const float* normal;    /* m x 3  */
+  const float* min_dist;  /* m      */
+  const float* max_dist;  /* m      */
+  const uint8_t* desc;    /* m x 32 */
+  const uint8_t* skip;    /* m      */
+} mmt_local_points;
+
+/* SearchLocalPoints' projection pass (Frame::isInFrustum(pMP, 0.5), Frame.cc:652-708, with
+ * MapPoint::PredictScale MapPoint.cc:402-417) + ORBmatcher(0.8)::SearchByProjection(Frame&,
+ * vector<MapPoint*>, th) (ORBmatcher.cc:418-502).  taken (cur->n bytes, optional) marks keys
+ * that already hold a MapPoint; match_out[i] (cur->n) = the local point newly bound to key i, or
+ * -1; frustum_out (m x 6 floats, optional) = in_view, predicted level, u, v, uR, view cos. */
+int mmt_search_local_points(mmt_ctx* ctx, const mmt_match_frame* cur,
+                            const mmt_local_points* pts, float th, const uint8_t* taken,
+                            int32_t* match_out, float* frustum_out, int* nmatches);
 
 /* Stage timing with HIP events on the launch stream (no reference counterpart: measurement
  * hook for bench.py).  orb_ms sums the batched ORB launch sequences of the tracked chunks. */

@@ -65,6 +65,23 @@ class MmtPoseOptProblem(ctypes.Structure):
                 ("cy", ctypes.c_float), ("bf", ctypes.c_float)]
 
 
+class MmtMatchFrame(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("kps", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("depth", ctypes.c_void_p), ("Tcw", ctypes.c_float * 16)]
+
+
+class MmtLastFrame(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("kps", ctypes.c_void_p), ("Xw", ctypes.c_void_p),
+                ("mp_desc", ctypes.c_void_p), ("active", ctypes.c_void_p),
+                ("Tcw", ctypes.c_float * 16)]
+
+
+class MmtLocalPoints(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_int), ("Xw", ctypes.c_void_p), ("normal", ctypes.c_void_p),
+                ("min_dist", ctypes.c_void_p), ("max_dist", ctypes.c_void_p),
+                ("desc", ctypes.c_void_p), ("skip", ctypes.c_void_p)]
+
+
 class MmtProfile(ctypes.Structure):
     _fields_ = [("orb_ms", ctypes.c_double), ("orb_launches", ctypes.c_int64),
                 ("orb_frames", ctypes.c_int64)]
@@ -132,6 +149,13 @@ def lib():
         L.mmt_pose_optimization.argtypes = [vp, ctypes.POINTER(MmtPoseOptProblem), vp, vp, vp]
         L.mmt_pnp_ransac.argtypes = [vp, vp, vp, i32] + [ctypes.c_float] * 4 + \
             [i32, ctypes.c_double, ctypes.c_double] + [vp] * 5
+        L.mmt_frame_grid.argtypes = [vp, ctypes.POINTER(MmtMatchFrame), vp, vp, vp, vp]
+        L.mmt_search_by_projection_frame.argtypes = [vp, ctypes.POINTER(MmtMatchFrame),
+                                                     ctypes.POINTER(MmtLastFrame),
+                                                     ctypes.c_float, i32, i32, vp, vp]
+        L.mmt_search_local_points.argtypes = [vp, ctypes.POINTER(MmtMatchFrame),
+                                              ctypes.POINTER(MmtLocalPoints), ctypes.c_float,
+                                              vp, vp, vp, vp]
         L.mmt_profile_enable.argtypes = [vp, i32]
         L.mmt_profile_read.argtypes = [vp, ctypes.POINTER(MmtProfile), i32]
         _LIB = L
@@ -306,6 +330,79 @@ class Context:
         self._check(lib().mmt_pose_optimization(self._h, ctypes.byref(pr), _p(pose), _p(out),
                                                 ctypes.byref(ninl)))
         return ninl.value, pose.reshape(4, 4), out[:n].astype(bool)
+
+    # ---- B3 / C1-C3 probes (Frame grid, ORBmatcher::SearchByProjection) -------------------
+    @staticmethod
+    def _match_frame(kps, desc, depth, tcw, keep):
+        kps = np.ascontiguousarray(kps)
+        desc = np.ascontiguousarray(desc, np.uint8) if desc is not None else None
+        depth = np.ascontiguousarray(depth, np.float32)
+        keep += [kps, desc, depth]
+        fr = MmtMatchFrame()
+        fr.n = len(kps)
+        fr.kps = kps.ctypes.data
+        fr.desc = desc.ctypes.data if desc is not None else None
+        fr.depth = depth.ctypes.data
+        fr.Tcw[:] = np.asarray(tcw, np.float32).reshape(16).tolist()
+        return fr
+
+    def frame_grid(self, kps, depth):
+        """Frame::ComputeStereoFromRGBD + AssignFeaturesToGrid (B3): (uR, depth, cell_start,
+        cell_idx) with the 64x48 grid as CSR over cells ix*48+iy."""
+        keep = []
+        fr = self._match_frame(kps, None, depth, np.eye(4), keep)
+        n = fr.n
+        uR = np.zeros(max(n, 1), np.float32)
+        dep = np.zeros(max(n, 1), np.float32)
+        cs = np.zeros(64 * 48 + 1, np.int32)
+        ci = np.zeros(max(n, 1), np.int32)
+        self._check(lib().mmt_frame_grid(self._h, ctypes.byref(fr), _p(uR), _p(dep), _p(cs),
+                                         _p(ci)))
+        return uR[:n], dep[:n], cs, ci[:cs[-1]]
+
+    def search_by_projection_frame(self, kps, desc, depth, tcw, last_kps, Xw, mp_desc, active,
+                                   tlw, th, mono=False, check_orientation=True):
+        """ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) (C2):
+        (nmatches, match[cur key] = last-frame index or -1)."""
+        keep = []
+        fr = self._match_frame(kps, desc, depth, tcw, keep)
+        lk = np.ascontiguousarray(last_kps)
+        X = np.ascontiguousarray(Xw, np.float32)
+        md = np.ascontiguousarray(mp_desc, np.uint8)
+        act = np.ascontiguousarray(active, np.uint8)
+        L = MmtLastFrame()
+        L.n = len(lk)
+        L.kps, L.Xw, L.mp_desc, L.active = (lk.ctypes.data, X.ctypes.data, md.ctypes.data,
+                                            act.ctypes.data)
+        L.Tcw[:] = np.asarray(tlw, np.float32).reshape(16).tolist()
+        match = np.zeros(max(fr.n, 1), np.int32)
+        nm = ctypes.c_int(0)
+        self._check(lib().mmt_search_by_projection_frame(
+            self._h, ctypes.byref(fr), ctypes.byref(L), th, int(mono), int(check_orientation),
+            _p(match), ctypes.byref(nm)))
+        return nm.value, match[:fr.n]
+
+    def search_local_points(self, kps, desc, depth, tcw, Xw, normal, min_dist, max_dist, pdesc,
+                            skip, th, taken=None):
+        """Tracking::SearchLocalPoints' isInFrustum pass + ORBmatcher::SearchByProjection(Frame&,
+        vector<MapPoint*>, th) (C3): (nmatches, match[cur key], frustum m x 6)."""
+        keep = []
+        fr = self._match_frame(kps, desc, depth, tcw, keep)
+        arrs = [np.ascontiguousarray(a, np.float32) for a in (Xw, normal, min_dist, max_dist)]
+        pd = np.ascontiguousarray(pdesc, np.uint8)
+        sk = np.ascontiguousarray(skip, np.uint8)
+        P = MmtLocalPoints()
+        P.m = len(sk)
+        P.Xw, P.normal, P.min_dist, P.max_dist = [a.ctypes.data for a in arrs]
+        P.desc, P.skip = pd.ctypes.data, sk.ctypes.data
+        tk = None if taken is None else np.ascontiguousarray(taken, np.uint8)
+        match = np.zeros(max(fr.n, 1), np.int32)
+        frus = np.zeros((max(P.m, 1), 6), np.float32)
+        nm = ctypes.c_int(0)
+        self._check(lib().mmt_search_local_points(
+            self._h, ctypes.byref(fr), ctypes.byref(P), th,
+            tk.ctypes.data if tk is not None else None, _p(match), _p(frus), ctypes.byref(nm)))
+        return nm.value, match[:fr.n], frus[:P.m]
 
     def pnp_ransac(self, pts3, pts2, K, max_iters=500, reproj=0.3, conf=0.98):
         pts3 = np.ascontiguousarray(pts3, np.float32)

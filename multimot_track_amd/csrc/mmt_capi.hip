@@ -4,11 +4,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 #include <new>
 
 #include "mmt_ctx.h"
+#include "mmt_match.h"
 #include "mmt_pnp.h"
 #include "mmt_track.h"
 
@@ -38,6 +40,75 @@ struct DevBuf {
   T* p = nullptr;
   explicit DevBuf(size_t n) { MMT_HIP(hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T))); }
   ~DevBuf() { (void)hipFree(p); }
+};
+
+// The current frame of a matcher probe on the device: keys, descriptors, depth map, and the B3
+// outputs (uR, depth, grid) built by k_stereo_grid.
+struct DevMatchFrame {
+  int n;
+  DevBuf<mmt_kp> kps;
+  DevBuf<uint8_t> desc;
+  DevBuf<float> depth, uR, kdepth;
+  DevBuf<int> nk, cell_start, cell_idx;
+  mmt::GridFrame G;
+  DevMatchFrame(mmt_ctx* ctx, const mmt_match_frame* cur, bool need_desc)
+      : n(cur->n), kps(cur->n), desc(32 * (size_t)cur->n),
+        depth((size_t)ctx->cfg.width * ctx->cfg.height), uR(cur->n), kdepth(cur->n), nk(1),
+        cell_start(mmt::kGridCells + 1), cell_idx(cur->n) {
+    const mmt_config& c = ctx->cfg;
+    hipStream_t s = ctx->stream;
+    if (n > 0) {
+      MMT_HIP(hipMemcpyAsync(kps.p, cur->kps, sizeof(mmt_kp) * (size_t)n, hipMemcpyHostToDevice, s));
+      if (need_desc)
+        MMT_HIP(hipMemcpyAsync(desc.p, cur->desc, 32 * (size_t)n, hipMemcpyHostToDevice, s));
+    }
+    MMT_HIP(hipMemcpyAsync(depth.p, cur->depth, sizeof(float) * (size_t)c.width * c.height,
+                           hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(nk.p, &n, sizeof(int), hipMemcpyHostToDevice, s));
+    memset(&G, 0, sizeof(G));
+    G.keys = kps.p;
+    G.desc = desc.p;
+    G.uR = uR.p;
+    G.cell_start = cell_start.p;
+    G.cell_idx = cell_idx.p;
+    G.n = n;
+    G.fx = c.fx; G.fy = c.fy; G.cx = c.cx; G.cy = c.cy; G.bf = c.bf;
+    // Frame::ComputeImageBounds without distortion + grid element sizes (Frame.cc:581-584, 841-846)
+    G.minX = 0.0f; G.maxX = (float)c.width; G.minY = 0.0f; G.maxY = (float)c.height;
+    G.invW = static_cast<float>(mmt::kGridCols) / static_cast<float>(G.maxX - G.minX);
+    G.invH = static_cast<float>(mmt::kGridRows) / static_cast<float>(G.maxY - G.minY);
+    G.nlevels = ctx->orb.nlevels;
+    for (int l = 0; l < G.nlevels && l < mmt::kMaxLevels; l++) G.scale[l] = ctx->orb.scale[l];
+    // mfLogScaleFactor = log(mfScaleFactor), pinned as log in double rounded to float
+    G.logScale = (float)std::log((double)ctx->orb.scale[G.nlevels > 1 ? 1 : 0]);
+    mmt::launch_stereo_grid(kps.p, nk.p, std::max(n, 1), depth.p, (size_t)c.width * c.height,
+                            c.width, c.height, c.bf, G.invW, G.invH, uR.p, kdepth.p,
+                            cell_start.p, cell_idx.p, 1, s);
+  }
+};
+
+static void check_match_frame(mmt_ctx* ctx, const mmt_match_frame* cur, bool need_desc) {
+  if (!cur || cur->n < 0 || cur->n > mmt::kMaxMatchKeys) throw ArgError("bad current frame");
+  if (cur->n > 0 && (!cur->kps || (need_desc && !cur->desc))) throw ArgError("null frame arrays");
+  if (!cur->depth) throw ArgError("null depth map");
+  if (ctx->orb.nlevels > mmt::kMaxLevels) throw ArgError("too many pyramid levels");
+  const int W = ctx->cfg.width, H = ctx->cfg.height;
+  for (int i = 0; i < cur->n; i++) {
+    const mmt_kp& k = cur->kps[i];
+    if (!(k.x >= 0 && k.y >= 0 && (int)k.x < W && (int)k.y < H))
+      throw ArgError("keypoint outside the image");
+    if (k.octave < 0 || k.octave >= ctx->orb.nlevels) throw ArgError("keypoint octave out of range");
+  }
+}
+
+struct DevCands {
+  DevBuf<uint32_t> key;
+  DevBuf<int> idx, n;
+  DevBuf<mmt::PointWin> win;
+  explicit DevCands(int m)
+      : key((size_t)std::max(m, 1) * mmt::kCandK), idx((size_t)std::max(m, 1) * mmt::kCandK),
+        n(std::max(m, 1)), win(std::max(m, 1)) {}
+  mmt::CandSet set() { return mmt::CandSet{key.p, idx.p, n.p, win.p}; }
 };
 
 static thread_local std::string g_create_error;
@@ -401,6 +472,131 @@ int mmt_pose_optimization(mmt_ctx* ctx, const mmt_pose_opt_problem* pr, float* p
     if (n > 0) MMT_HIP(hipMemcpyAsync(outlier_out, outl.p, n, hipMemcpyDeviceToHost, s));
     MMT_HIP(hipMemcpyAsync(n_inliers, ninl.p, sizeof(int), hipMemcpyDeviceToHost, s));
     MMT_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int mmt_frame_grid(mmt_ctx* ctx, const mmt_match_frame* cur, float* uR_out, float* depth_out,
+                   int* cell_start, int* cell_idx) {
+  if (!ctx || !cur || !cell_start || (cur->n > 0 && (!uR_out || !depth_out || !cell_idx)))
+    return MMT_EINVAL;
+  return guard(ctx, [&] {
+    check_match_frame(ctx, cur, false);
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    hipStream_t s = ctx->stream;
+    DevMatchFrame F(ctx, cur, false);
+    const size_t n = (size_t)cur->n;
+    if (n) {
+      MMT_HIP(hipMemcpyAsync(uR_out, F.uR.p, 4 * n, hipMemcpyDeviceToHost, s));
+      MMT_HIP(hipMemcpyAsync(depth_out, F.kdepth.p, 4 * n, hipMemcpyDeviceToHost, s));
+    }
+    MMT_HIP(hipMemcpyAsync(cell_start, F.cell_start.p, 4 * (mmt::kGridCells + 1),
+                           hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+    const int total = cell_start[mmt::kGridCells];
+    if (total > 0) {
+      MMT_HIP(hipMemcpyAsync(cell_idx, F.cell_idx.p, 4 * (size_t)total, hipMemcpyDeviceToHost, s));
+      MMT_HIP(hipStreamSynchronize(s));
+    }
+  });
+}
+
+int mmt_search_by_projection_frame(mmt_ctx* ctx, const mmt_match_frame* cur,
+                                   const mmt_last_frame* last, float th, int mono,
+                                   int check_orientation, int32_t* match_out, int* nmatches) {
+  if (!ctx || !cur || !last || !nmatches || last->n < 0 || (cur->n > 0 && !match_out) ||
+      (last->n > 0 && (!last->kps || !last->Xw || !last->mp_desc || !last->active)))
+    return MMT_EINVAL;
+  return guard(ctx, [&] {
+    check_match_frame(ctx, cur, true);
+    for (int i = 0; i < last->n; i++)
+      if (last->active[i] && (last->kps[i].octave < 0 || last->kps[i].octave >= ctx->orb.nlevels))
+        throw ArgError("last-frame octave out of range");
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    hipStream_t s = ctx->stream;
+    DevMatchFrame F(ctx, cur, true);
+    const int n1 = last->n;
+    DevBuf<mmt_kp> lk(n1);
+    DevBuf<float> X(3 * (size_t)std::max(n1, 1));
+    DevBuf<uint8_t> md(32 * (size_t)std::max(n1, 1)), act(n1);
+    DevBuf<int> match(std::max(cur->n, 1)), nm(1);
+    DevCands cands(n1);
+    if (n1 > 0) {
+      MMT_HIP(hipMemcpyAsync(lk.p, last->kps, sizeof(mmt_kp) * (size_t)n1, hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(X.p, last->Xw, 12 * (size_t)n1, hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(md.p, last->mp_desc, 32 * (size_t)n1, hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(act.p, last->active, (size_t)n1, hipMemcpyHostToDevice, s));
+    }
+    mmt::LastFrameDev L;
+    L.keys = lk.p;
+    L.Xw = X.p;
+    L.mp_desc = md.p;
+    L.active = act.p;
+    L.n = n1;
+    memcpy(L.Tcw, last->Tcw, 64);
+    mmt::launch_sbp_frame(F.G, cur->Tcw, L, th, mono, check_orientation, cands.set(), match.p,
+                          nm.p, s);
+    if (cur->n > 0)
+      MMT_HIP(hipMemcpyAsync(match_out, match.p, 4 * (size_t)cur->n, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(nmatches, nm.p, 4, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int mmt_search_local_points(mmt_ctx* ctx, const mmt_match_frame* cur,
+                            const mmt_local_points* pts, float th, const uint8_t* taken,
+                            int32_t* match_out, float* frustum_out, int* nmatches) {
+  if (!ctx || !cur || !pts || !nmatches || pts->m < 0 || (cur->n > 0 && !match_out) ||
+      (pts->m > 0 && (!pts->Xw || !pts->normal || !pts->min_dist || !pts->max_dist ||
+                      !pts->desc || !pts->skip)))
+    return MMT_EINVAL;
+  return guard(ctx, [&] {
+    check_match_frame(ctx, cur, true);
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    hipStream_t s = ctx->stream;
+    DevMatchFrame F(ctx, cur, true);
+    const int m = pts->m;
+    std::vector<mmt::LocalPointDev> hp(std::max(m, 1));
+    for (int j = 0; j < m; j++) {
+      mmt::LocalPointDev& p = hp[j];
+      memset(&p, 0, sizeof(p));
+      memcpy(p.Xw, pts->Xw + 3 * (size_t)j, 12);
+      memcpy(p.normal, pts->normal + 3 * (size_t)j, 12);
+      p.min_dist = pts->min_dist[j];
+      p.max_dist = pts->max_dist[j];
+      p.skip = pts->skip[j] != 0;
+    }
+    DevBuf<mmt::LocalPointDev> dp(m);
+    DevBuf<uint8_t> pd(32 * (size_t)std::max(m, 1)), tk(std::max(cur->n, 1));
+    DevBuf<mmt::FrustumRec> fr(m);
+    DevBuf<int> match(std::max(cur->n, 1)), nm(1);
+    DevCands cands(m);
+    if (m > 0) {
+      MMT_HIP(hipMemcpyAsync(dp.p, hp.data(), sizeof(mmt::LocalPointDev) * (size_t)m,
+                             hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(pd.p, pts->desc, 32 * (size_t)m, hipMemcpyHostToDevice, s));
+    }
+    if (taken && cur->n > 0)
+      MMT_HIP(hipMemcpyAsync(tk.p, taken, (size_t)cur->n, hipMemcpyHostToDevice, s));
+    mmt::launch_search_local(F.G, cur->Tcw, dp.p, pd.p, m, th, taken ? tk.p : nullptr, fr.p,
+                             cands.set(), match.p, nm.p, s);
+    std::vector<mmt::FrustumRec> hfr(std::max(m, 1));
+    if (cur->n > 0)
+      MMT_HIP(hipMemcpyAsync(match_out, match.p, 4 * (size_t)cur->n, hipMemcpyDeviceToHost, s));
+    if (m > 0)
+      MMT_HIP(hipMemcpyAsync(hfr.data(), fr.p, sizeof(mmt::FrustumRec) * (size_t)m,
+                             hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(nmatches, nm.p, 4, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+    if (frustum_out)
+      for (int j = 0; j < m; j++) {
+        float* o = frustum_out + 6 * (size_t)j;
+        o[0] = (float)hfr[j].in_view;
+        o[1] = (float)hfr[j].level;
+        o[2] = hfr[j].u;
+        o[3] = hfr[j].v;
+        o[4] = hfr[j].uR;
+        o[5] = hfr[j].view_cos;
+      }
   });
 }
 

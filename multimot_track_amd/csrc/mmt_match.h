@@ -1,0 +1,89 @@
+// multimot_track_amd/csrc/mmt_match.h -- device records of the frame grid (B3) and the projection
+// matchers (C1-C3): Frame::ComputeStereoFromRGBD / AssignFeaturesToGrid / GetFeaturesInArea /
+// isInFrustum, ORBmatcher::DescriptorDistance / SearchByProjection (reference Frame.cc,
+// ORBmatcher.cc).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/mmt.h"
+
+namespace mmt {
+
+constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:37-38)
+constexpr int kGridCells = kGridCols * kGridRows;
+constexpr int kCandK = 8;              // candidates kept per point (sorted by distance, order)
+constexpr int kMaxMatchKeys = 16384;   // current-frame keys a matcher accepts (LDS bitmap)
+constexpr int kMaxLevels = 16;  // mmt_create accepts orb_nlevels <= 16
+
+// One frame as the matchers read it (Frame's mvKeysUn, mDescriptors, mvuRight, mGrid).
+struct GridFrame {
+  const mmt_kp* keys;
+  const uint8_t* desc;   // n x 32
+  const float* uR;       // mvuRight (B3)
+  const int* cell_start; // kGridCells + 1, cells ix * kGridRows + iy (CSR)
+  const int* cell_idx;   // n, ascending key order inside a cell
+  int n;
+  float fx, fy, cx, cy, bf;
+  float minX, maxX, minY, maxY, invW, invH;
+  float scale[kMaxLevels];
+  float logScale;
+  int nlevels;
+};
+
+// A point's search window (GetFeaturesInArea arguments + the stereo check) for rescans.
+struct PointWin {
+  float x, y, r, ur, er;
+  int minLevel, maxLevel, pad;
+};
+
+struct FrustumRec {  // isInFrustum outputs (MapPoint::mTrack* fields)
+  int in_view, level;
+  float u, v, uR, view_cos;
+};
+
+struct LocalPointDev {  // a local MapPoint: position, normal, distance invariance, state
+  float Xw[3];
+  float normal[3];
+  float min_dist, max_dist;
+  int skip;  // mnLastFrameSeen == frame (already matched) or isBad()
+  int pad[3];
+};
+
+// Candidates of one matcher call: per point kCandK (dist << 20 | order) keys + key indices,
+// the number of candidates that passed the filters (-1: point inactive) and its window.
+struct CandSet {
+  uint32_t* key;
+  int* idx;
+  int* n;
+  PointWin* win;
+};
+
+// B3 for nframes frames: keys/uR/kdepth/cell_idx at frame stride `cap`, cell_start at
+// kGridCells + 1, depth map at depth_pitch floats.
+void launch_stereo_grid(const mmt_kp* keys, const int* nkp, int cap, const float* depth,
+                        size_t depth_pitch, int W, int H, float bf, float invW, float invH,
+                        float* uR, float* kdepth, int* cell_start, int* cell_idx, int nframes,
+                        hipStream_t st);
+
+// C2: SearchByProjection(Frame&, const Frame&, th, bMono) candidates + greedy replay.
+struct LastFrameDev {
+  const mmt_kp* keys;
+  const float* Xw;          // n x 3
+  const uint8_t* mp_desc;   // n x 32
+  const uint8_t* active;    // MapPoint present and not an outlier
+  int n;
+  float Tcw[16];
+};
+void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& L, float th,
+                      int mono, int check_orientation, const CandSet& cs, int* match,
+                      int* nmatches, hipStream_t st);
+
+// C3: SearchLocalPoints' isInFrustum pass + SearchByProjection(Frame&, vector<MapPoint*>, th).
+void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointDev* pts,
+                         const uint8_t* pdesc, int m, float th, const uint8_t* taken,
+                         FrustumRec* fr, const CandSet& cs, int* match, int* nmatches,
+                         hipStream_t st);
+
+}  // namespace mmt

@@ -220,3 +220,85 @@ class Tracker:
         return dict(initialized=bool(info[0]), Tcw=tcw.reshape(4, 4), n_keys=int(info[1]),
                     n_static=int(info[2]), n_obj_samples=int(info[3]), ego_iterations=int(info[4]),
                     ego_inliers=int(info[5]), objects=objs)
+
+
+# ---------------------------------------------------------------- B3 / C1-C3 (match_ref.cpp)
+def _cam(K, bf):
+    return np.array([K[0], K[1], K[2], K[3], bf], np.float32)
+
+
+def frame_stereo_grid(kps, depth, K, bf):
+    """Frame::ComputeStereoFromRGBD + AssignFeaturesToGrid: (uR, depth, cell_start, cell_idx)."""
+    L = lib()
+    L.oracle_frame_stereo_grid.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 5
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    depth = np.ascontiguousarray(depth, np.float32)
+    H, W = depth.shape
+    n = len(kps)
+    uR = np.zeros(max(n, 1), np.float32)
+    dep = np.zeros(max(n, 1), np.float32)
+    cs = np.zeros(64 * 48 + 1, np.int32)
+    ci = np.zeros(max(n, 1), np.int32)
+    cam = _cam(K, bf)
+    tot = L.oracle_frame_stereo_grid(n, _p(kps), _p(depth), W, H, _p(cam), _p(uR), _p(dep),
+                                     _p(cs), _p(ci))
+    return uR[:n], dep[:n], cs, ci[:tot]
+
+
+def search_by_projection_frame(kps, desc, depth, tcw, last_kps, Xw, mp_desc, active, tlw, th,
+                               K, bf, scale, mono=False, check_orientation=True):
+    L = lib()
+    vp = ctypes.c_void_p
+    L.oracle_search_by_projection_frame.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int,
+                                                    ctypes.c_int, vp, vp, ctypes.c_int, vp,
+                                                    ctypes.c_int, vp, vp, vp, vp, vp,
+                                                    ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                                    vp]
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    depth = np.ascontiguousarray(depth, np.float32)
+    H, W = depth.shape
+    lk = np.ascontiguousarray(last_kps, KP_DTYPE)
+    X = np.ascontiguousarray(Xw, np.float32)
+    md = np.ascontiguousarray(mp_desc, np.uint8)
+    act = np.ascontiguousarray(active, np.uint8)
+    sc = np.ascontiguousarray(scale, np.float32)
+    t = np.ascontiguousarray(tcw, np.float32).reshape(16)
+    tl = np.ascontiguousarray(tlw, np.float32).reshape(16)
+    cam = _cam(K, bf)
+    match = np.zeros(max(len(kps), 1), np.int32)
+    nm = L.oracle_search_by_projection_frame(len(kps), _p(kps), _p(desc), _p(depth), W, H,
+                                             _p(cam), _p(sc), len(sc), _p(t), len(lk), _p(lk),
+                                             _p(X), _p(md), _p(act), _p(tl), th, int(mono),
+                                             int(check_orientation), _p(match))
+    return nm, match[:len(kps)]
+
+
+def search_local_points(kps, desc, depth, tcw, Xw, normal, min_dist, max_dist, pdesc, skip, th,
+                        K, bf, scale, taken=None):
+    L = lib()
+    vp = ctypes.c_void_p
+    L.oracle_search_local_points.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int,
+                                             ctypes.c_int, vp, vp, ctypes.c_int, vp,
+                                             ctypes.c_int, vp, vp, vp, vp, vp, vp,
+                                             ctypes.c_float, vp, vp, vp]
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    depth = np.ascontiguousarray(depth, np.float32)
+    H, W = depth.shape
+    arrs = [np.ascontiguousarray(a, np.float32) for a in (Xw, normal, min_dist, max_dist)]
+    pd = np.ascontiguousarray(pdesc, np.uint8)
+    sk = np.ascontiguousarray(skip, np.uint8)
+    m = len(sk)
+    tk = np.zeros(max(len(kps), 1), np.uint8) if taken is None else \
+        np.ascontiguousarray(taken, np.uint8)
+    sc = np.ascontiguousarray(scale, np.float32)
+    t = np.ascontiguousarray(tcw, np.float32).reshape(16)
+    cam = _cam(K, bf)
+    match = np.zeros(max(len(kps), 1), np.int32)
+    frus = np.zeros((max(m, 1), 6), np.float32)
+    nm = L.oracle_search_local_points(len(kps), _p(kps), _p(desc), _p(depth), W, H, _p(cam),
+                                      _p(sc), len(sc), _p(t), m, *[_p(a) for a in arrs], _p(pd),
+                                      _p(sk), th, _p(tk), _p(match), _p(frus))
+    return nm, match[:len(kps)], frus[:m]

@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "oracle_common.h"
+#include "oracle_match.h"
 
 using namespace oracle;
 
@@ -233,6 +234,92 @@ int oracle_tracker_track(void* tp, const uint8_t* bgr, const uint16_t* disp, con
     memcpy(of + 32, o.motion, 64);
   }
   return 0;
+}
+
+// ---------------------------------------------------------------- B3 / C1-C3 (oracle_match.h)
+// cam = fx, fy, cx, cy, bf; scale = mvScaleFactors (nlevels).
+static void match_frame(MatchFrame& F, int n, const Key* keys, const uint8_t* desc,
+                        const float* depth, int W, int H, const float* cam, const float* scale,
+                        int nlevels) {
+  F.n = n;
+  F.keys = keys;
+  F.desc = desc;
+  F.fx = cam[0]; F.fy = cam[1]; F.cx = cam[2]; F.cy = cam[3]; F.bf = cam[4];
+  F.scale.assign(scale, scale + nlevels);
+  F.nlevels = nlevels;
+  F.logScale = (float)std::log((double)scale[1]);  // mfLogScaleFactor = log(mfScaleFactor)
+  frame_stereo_grid(F, depth, W, H);
+}
+
+// B3: uR, depth (n each); cell_start (64*48+1) and cell_idx (n) as CSR over cells ix*48+iy.
+int oracle_frame_stereo_grid(int n, const Key* keys, const float* depth, int W, int H,
+                             const float* cam, float* uR, float* dep, int* cell_start,
+                             int* cell_idx) {
+  MatchFrame F;
+  const float scale[2] = {1.f, 1.2f};
+  match_frame(F, n, keys, nullptr, depth, W, H, cam, scale, 2);
+  int pos = 0;
+  for (int c = 0; c < kGridCols * kGridRows; c++) {
+    cell_start[c] = pos;
+    for (int k : F.grid[c]) cell_idx[pos++] = k;
+  }
+  cell_start[kGridCols * kGridRows] = pos;
+  for (int i = 0; i < n; i++) {
+    uR[i] = F.uR[i];
+    dep[i] = F.depth[i];
+  }
+  return pos;
+}
+
+int oracle_search_by_projection_frame(int n2, const Key* keys2, const uint8_t* desc2,
+                                      const float* depth, int W, int H, const float* cam,
+                                      const float* scale, int nlevels, const float* Tcw, int n1,
+                                      const Key* keys1, const float* Xw, const uint8_t* mp_desc,
+                                      const uint8_t* active, const float* Tlw, float th, int mono,
+                                      int check_orientation, int* match) {
+  MatchFrame C;
+  match_frame(C, n2, keys2, desc2, depth, W, H, cam, scale, nlevels);
+  LastFrameView L;
+  L.n = n1;
+  L.keys = keys1;
+  L.Xw = Xw;
+  L.mp_desc = mp_desc;
+  L.active = active;
+  memcpy(L.Tcw, Tlw, sizeof(L.Tcw));
+  return search_by_projection_frame(C, Tcw, L, th, mono != 0, check_orientation != 0, match);
+}
+
+// frustum_out: m x 6 floats (in_view, level, u, v, uR, view_cos).
+int oracle_search_local_points(int n, const Key* keys, const uint8_t* desc, const float* depth,
+                               int W, int H, const float* cam, const float* scale, int nlevels,
+                               const float* Tcw, int m, const float* Xw, const float* normal,
+                               const float* min_dist, const float* max_dist,
+                               const uint8_t* pdesc, const uint8_t* skip, float th,
+                               const uint8_t* taken, int* match, float* frustum_out) {
+  MatchFrame C;
+  match_frame(C, n, keys, desc, depth, W, H, cam, scale, nlevels);
+  std::vector<LocalPoint> pts(m);
+  for (int j = 0; j < m; j++) {
+    LocalPoint& p = pts[j];
+    memcpy(p.Xw, Xw + 3 * j, 12);
+    memcpy(p.normal, normal + 3 * j, 12);
+    p.min_dist = min_dist[j];
+    p.max_dist = max_dist[j];
+    p.desc = pdesc + 32 * (size_t)j;
+    p.skip = skip[j];
+  }
+  std::vector<FrustumOut> fr(m);
+  const int nm = search_local_points(C, Tcw, pts.data(), m, th, taken, match, fr.data());
+  for (int j = 0; j < m; j++) {
+    float* o = frustum_out + 6 * j;
+    o[0] = (float)fr[j].in_view;
+    o[1] = (float)fr[j].level;
+    o[2] = fr[j].u;
+    o[3] = fr[j].v;
+    o[4] = fr[j].uR;
+    o[5] = fr[j].view_cos;
+  }
+  return nm;
 }
 
 }  // extern "C"
