@@ -30,8 +30,34 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+CLI = os.path.join(HERE, "cli")
+IO_LIB = os.path.join(HERE, "libmmt_io.so")
+CLI_BIN = os.path.join(HERE, "rgbd_mmt")
+CXX = os.environ.get("CXX", "g++")
+
+
+def build_cli(force=False, verbose=True):
+    """Host-only pieces above the C-ABI: libmmt_io.so (sequence decoding) and the rgbd_mmt
+    drop-in executable (links libmmt.so through an $ORIGIN rpath)."""
+    srcs = [os.path.join(CLI, f) for f in ("mmt_io.cpp", "mmt_io.h", "rgbd_mmt.cpp")]
+    newest = max(os.path.getmtime(s) for s in srcs + [OUT])
+    cmds = []
+    if force or not os.path.exists(IO_LIB) or os.path.getmtime(IO_LIB) < newest:
+        cmds.append([CXX, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+                     os.path.join(CLI, "mmt_io.cpp"), "-lz", "-o", IO_LIB])
+    if force or not os.path.exists(CLI_BIN) or os.path.getmtime(CLI_BIN) < newest:
+        cmds.append([CXX, "-O2", "-std=c++17", "-Wall", os.path.join(CLI, "rgbd_mmt.cpp"),
+                     os.path.join(CLI, "mmt_io.cpp"), "-L" + HERE, "-l:libmmt.so", "-lz",
+                     "-Wl,-rpath,$ORIGIN", "-o", CLI_BIN])
+    for c in cmds:
+        if verbose:
+            print(" ".join(c), flush=True)
+        subprocess.check_call(c)
+
+
 def build(force=False, verbose=True):
     if not force and not needs_build():
+        build_cli(force, verbose)
         return OUT
     objs = []
     procs = []
@@ -50,6 +76,7 @@ def build(force=False, verbose=True):
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
+    build_cli(True, verbose)
     return OUT
 
 

@@ -1,0 +1,281 @@
+// multimot_track_amd/cli/mmt_io.cpp -- sequence input decoding (see mmt_io.h).
+#include "mmt_io.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+namespace {
+
+bool read_file(const char* path, std::vector<uint8_t>& out) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return false;
+  if (fseek(f, 0, SEEK_END) != 0) {
+    fclose(f);
+    return false;
+  }
+  const long n = ftell(f);
+  if (n < 0) {
+    fclose(f);
+    return false;
+  }
+  rewind(f);
+  out.resize((size_t)n);
+  const bool ok = n == 0 || fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+  fclose(f);
+  return ok;
+}
+
+uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+int paeth(int a, int b, int c) {
+  const int p = a + b - c;
+  const int pa = abs(p - a), pb = abs(p - b), pc = abs(p - c);
+  if (pa <= pb && pa <= pc) return a;
+  return pb <= pc ? b : c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mmt_io_read_png(const char* path, int* w_out, int* h_out, int* ch_out, int* db_out,
+                    void** data) {
+  if (!path || !w_out || !h_out || !ch_out || !db_out || !data) return -22;
+  std::vector<uint8_t> f;
+  if (!read_file(path, f)) return -2;
+  static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+  if (f.size() < 8 || memcmp(f.data(), sig, 8) != 0) return -3;
+  size_t pos = 8;
+  uint32_t W = 0, H = 0;
+  int bitdepth = 0, ctype = -1, interlace = 0;
+  std::vector<uint8_t> idat;
+  bool have_hdr = false, end = false;
+  while (!end) {
+    if (pos + 12 > f.size()) return -3;
+    const uint32_t len = be32(&f[pos]);
+    const uint8_t* type = &f[pos + 4];
+    const uint8_t* body = &f[pos + 8];
+    if (pos + 12 + (size_t)len > f.size()) return -3;
+    if (!memcmp(type, "IHDR", 4)) {
+      if (len < 13) return -3;
+      W = be32(body);
+      H = be32(body + 4);
+      bitdepth = body[8];
+      ctype = body[9];
+      interlace = body[12];
+      if (body[10] != 0 || body[11] != 0) return -4;
+      have_hdr = true;
+    } else if (!memcmp(type, "IDAT", 4)) {
+      idat.insert(idat.end(), body, body + len);
+    } else if (!memcmp(type, "IEND", 4)) {
+      end = true;
+    } else if (!memcmp(type, "PLTE", 4)) {
+      return -4;  // palette images: not produced by the dataset
+    }
+    pos += 12 + (size_t)len;
+  }
+  if (!have_hdr || W == 0 || H == 0 || W > 65535 || H > 65535 || interlace != 0) return -4;
+  int channels;
+  switch (ctype) {
+    case 0: channels = 1; break;
+    case 2: channels = 3; break;
+    case 4: channels = 2; break;
+    case 6: channels = 4; break;
+    default: return -4;
+  }
+  if (bitdepth != 8 && bitdepth != 16) return -4;
+  const int db = bitdepth / 8;
+  const size_t bpp = (size_t)channels * db;
+  const size_t stride = (size_t)W * bpp;
+  std::vector<uint8_t> raw((stride + 1) * H);
+  uLongf rawlen = (uLongf)raw.size();
+  if (uncompress(raw.data(), &rawlen, idat.data(), (uLong)idat.size()) != Z_OK ||
+      rawlen != raw.size())
+    return -5;
+  // PNG filter types 0..4, byte-wise with the left neighbour `bpp` bytes back
+  std::vector<uint8_t> img(stride * H);
+  for (uint32_t y = 0; y < H; y++) {
+    const uint8_t ft = raw[y * (stride + 1)];
+    const uint8_t* s = &raw[y * (stride + 1) + 1];
+    uint8_t* d = &img[y * stride];
+    const uint8_t* up = y ? &img[(y - 1) * stride] : nullptr;
+    for (size_t x = 0; x < stride; x++) {
+      const int a = x >= bpp ? d[x - bpp] : 0;
+      const int b = up ? up[x] : 0;
+      const int c = (up && x >= bpp) ? up[x - bpp] : 0;
+      int v;
+      switch (ft) {
+        case 0: v = s[x]; break;
+        case 1: v = s[x] + a; break;
+        case 2: v = s[x] + b; break;
+        case 3: v = s[x] + ((a + b) >> 1); break;
+        case 4: v = s[x] + paeth(a, b, c); break;
+        default: return -5;
+      }
+      d[x] = (uint8_t)v;
+    }
+  }
+  // imread: big-endian 16-bit samples to host order, RGB(A) to BGR(A)
+  void* out = malloc(img.size());
+  if (!out) return -12;
+  if (db == 2) {
+    uint16_t* o = (uint16_t*)out;
+    for (size_t i = 0; i < img.size() / 2; i++) o[i] = (uint16_t)((img[2 * i] << 8) | img[2 * i + 1]);
+  } else {
+    memcpy(out, img.data(), img.size());
+  }
+  if (channels >= 3) {
+    const size_t npx = (size_t)W * H;
+    if (db == 1) {
+      uint8_t* o = (uint8_t*)out;
+      for (size_t i = 0; i < npx; i++) std::swap(o[i * channels], o[i * channels + 2]);
+    } else {
+      uint16_t* o = (uint16_t*)out;
+      for (size_t i = 0; i < npx; i++) std::swap(o[i * channels], o[i * channels + 2]);
+    }
+  }
+  *w_out = (int)W;
+  *h_out = (int)H;
+  *ch_out = channels;
+  *db_out = db;
+  *data = out;
+  return 0;
+}
+
+int mmt_io_read_flo(const char* path, int* w, int* h, float** data) {
+  if (!path || !w || !h || !data) return -22;
+  std::vector<uint8_t> f;
+  if (!read_file(path, f)) return -2;
+  if (f.size() < 12) return -3;
+  float tag;
+  int32_t ww, hh;
+  memcpy(&tag, f.data(), 4);
+  memcpy(&ww, f.data() + 4, 4);
+  memcpy(&hh, f.data() + 8, 4);
+  if (tag != 202021.25f || ww <= 0 || hh <= 0 || ww > 100000 || hh > 100000) return -3;
+  const size_t n = (size_t)ww * hh * 2;
+  if (f.size() < 12 + n * 4) return -3;
+  float* out = (float*)malloc(n * 4);
+  if (!out) return -12;
+  memcpy(out, f.data() + 12, n * 4);
+  *w = ww;
+  *h = hh;
+  *data = out;
+  return 0;
+}
+
+int mmt_io_read_mask(const char* path, int rows, int cols, int32_t* out) {
+  if (!path || !out || rows <= 0 || cols <= 0) return -22;
+  std::ifstream file(path);
+  if (!file) return -2;
+  int count = 0;
+  std::string s;
+  while (count < rows && std::getline(file, s)) {
+    if (s.empty()) continue;
+    std::stringstream ss(s);
+    int32_t* row = out + (size_t)count * cols;
+    for (int i = 0; i < cols; i++) {
+      int tmp = 0;
+      if (!(ss >> tmp)) tmp = 0;
+      row[i] = (tmp != 0 && tmp < 4) ? tmp : 0;
+    }
+    count++;
+  }
+  return count;
+}
+
+static int read_rows(const char* path, int skip_first, int nvals, float** out, int* n) {
+  if (!path || !out || !n) return -22;
+  std::ifstream file(path);
+  if (!file) return -2;
+  std::vector<float> v;
+  std::string s;
+  int rows = 0;
+  while (std::getline(file, s)) {
+    if (s.empty()) continue;
+    std::stringstream ss(s);
+    if (skip_first) {
+      int id;
+      ss >> id;
+    }
+    for (int k = 0; k < nvals; k++) {
+      float x = 0;
+      ss >> x;
+      v.push_back(x);
+    }
+    rows++;
+  }
+  float* o = (float*)malloc(std::max<size_t>(v.size(), 1) * sizeof(float));
+  if (!o) return -12;
+  if (!v.empty()) memcpy(o, v.data(), v.size() * sizeof(float));
+  *out = o;
+  *n = rows;
+  return 0;
+}
+
+int mmt_io_read_times(const char* path, double** out, int* n) {
+  if (!path || !out || !n) return -22;
+  std::ifstream file(path);
+  if (!file) return -2;
+  std::vector<double> v;
+  std::string s;
+  while (std::getline(file, s)) {
+    if (s.empty()) continue;
+    std::stringstream ss(s);
+    double t = 0;
+    ss >> t;
+    v.push_back(t);
+  }
+  double* o = (double*)malloc(std::max<size_t>(v.size(), 1) * sizeof(double));
+  if (!o) return -12;
+  if (!v.empty()) memcpy(o, v.data(), v.size() * sizeof(double));
+  *out = o;
+  *n = (int)v.size();
+  return 0;
+}
+
+int mmt_io_read_poses(const char* path, float** out, int* n) {
+  return read_rows(path, 1, 16, out, n);
+}
+
+int mmt_io_read_object_poses(const char* path, float** out, int* n) {
+  return read_rows(path, 0, 10, out, n);
+}
+
+int mmt_io_yaml_float(const char* path, const char* key, double* value) {
+  if (!path || !key || !value) return -22;
+  std::ifstream file(path);
+  if (!file) return -2;
+  std::string s;
+  const std::string k(key);
+  while (std::getline(file, s)) {
+    const size_t hash = s.find('#');
+    if (hash != std::string::npos) s = s.substr(0, hash);
+    const size_t colon = s.find(':');
+    if (colon == std::string::npos) continue;
+    std::string name = s.substr(0, colon);
+    name.erase(0, name.find_first_not_of(" \t"));
+    name.erase(name.find_last_not_of(" \t") + 1);
+    if (name != k) continue;
+    std::stringstream ss(s.substr(colon + 1));
+    double v;
+    if (!(ss >> v)) return -3;
+    *value = v;
+    return 0;
+  }
+  return -1;
+}
+
+void mmt_io_free(void* p) { free(p); }
+
+}  // extern "C"

@@ -1,0 +1,282 @@
+// multimot_track_amd/cli/rgbd_mmt.cpp -- drop-in for the reference's RGB-D example
+// (Examples/RGB-D/rgbd_tum.cc, built as `rgbd_mmt`): same arguments, same sequence layout
+// (image/ depth/ semantic/ flow/ times.txt pose_gt.txt object_pose.txt, LoadData :213-312), the
+// same per-frame camera relative-pose-error lines (Tracking.cc:1321-1341) and tracking-time
+// statistics (rgbd_tum.cc:196-203), with System::TrackRGBD replaced by mmt_track_rgbd.
+//
+//   rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence [--realtime] [--nfeatures N]
+//            [--device D] [--noise-seed S] [--poses out.txt]
+//
+// Differences from the reference binary: the vocabulary is not read (this path
+// never uses BoW); no viewer, no imshow/waitKey; the usleep pacing to the timestamps is off
+// unless --realtime; a sequence whose times.txt lists more frames than exist on disk stops
+// cleanly after the last frame (the reference fails at the first missing image).
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+#include <algorithm>
+
+#include "../../include/mmt.h"
+#include "mmt_io.h"
+
+namespace {
+
+// cv::Mat float products (double accumulation, rounded to float), row-major 4x4
+void mul4(const float* A, const float* B, float* C) {
+  float R[16];
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) {
+      double s = 0;
+      for (int k = 0; k < 4; k++) s += (double)A[4 * r + k] * (double)B[4 * k + c];
+      R[4 * r + c] = (float)s;
+    }
+  memcpy(C, R, sizeof(R));
+}
+
+// Tracking::InvMatrix (Tracking.cc:5106-5121)
+void inv4(const float* T, float* Ti) {
+  float R[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) R[4 * r + c] = T[4 * c + r];
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)T[4 * k + 3];
+    R[4 * r + 3] = (float)(-s);
+  }
+  memcpy(Ti, R, sizeof(R));
+}
+
+// The camera RPE block of Tracking::Track (Tracking.cc:1321-1341).
+void print_camera_rpe(const float* Tcw, const float* Tlw, const float* Tcw_gt, const float* Tlw_gt) {
+  float a[16], b[16], T_lc_inv[16], T_lc_gt[16], E[16];
+  inv4(Tlw, a);
+  mul4(Tcw, a, T_lc_inv);
+  inv4(Tcw_gt, b);
+  mul4(Tlw_gt, b, T_lc_gt);
+  mul4(T_lc_inv, T_lc_gt, E);
+  const float t_rpe = std::sqrt(E[3] * E[3] + E[7] * E[7] + E[11] * E[11]);
+  float trace = 0;
+  for (int i = 0; i < 3; i++) {
+    const float d = E[5 * i];
+    trace = d > 1.0 ? (float)(trace + 1.0 - (d - 1.0)) : trace + d;
+  }
+  const float r_rpe = (float)(std::acos((trace - 1.0) / 2.0) * 180.0 / 3.1415926);
+  const float t_gt = std::sqrt(T_lc_gt[3] * T_lc_gt[3] + T_lc_gt[7] * T_lc_gt[7] +
+                               T_lc_gt[11] * T_lc_gt[11]);
+  printf("\nthe relative pose error of estimated camera pose, t: %.4f%% R: %.4fdeg/m\n",
+         (t_rpe / t_gt) * 100, r_rpe / t_gt);
+  printf("the relative pose error of estimated camera pose, t: %.4f R: %.4f\n", t_rpe, r_rpe);
+}
+
+std::string frame_name(const std::string& dir, const char* sub, int i, const char* ext) {
+  char buf[32];
+  snprintf(buf, sizeof(buf), "%06d", i);
+  return dir + "/" + sub + "/" + buf + ext;
+}
+
+bool exists(const std::string& p) {
+  FILE* f = fopen(p.c_str(), "rb");
+  if (f) fclose(f);
+  return f != nullptr;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::vector<std::string> pos;
+  bool realtime = false;
+  int nfeat = -1, device = 0;
+  unsigned seed = 0;
+  std::string poses_out;
+  for (int i = 1; i < argc; i++) {
+    const std::string a = argv[i];
+    if (a == "--realtime") realtime = true;
+    else if (a == "--nfeatures" && i + 1 < argc) nfeat = atoi(argv[++i]);
+    else if (a == "--device" && i + 1 < argc) device = atoi(argv[++i]);
+    else if (a == "--noise-seed" && i + 1 < argc) seed = (unsigned)strtoul(argv[++i], nullptr, 10);
+    else if (a == "--poses" && i + 1 < argc) poses_out = argv[++i];
+    else pos.push_back(a);
+  }
+  if (pos.size() != 3) {
+    fprintf(stderr, "\nUsage: ./rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence "
+                    "[--realtime] [--nfeatures N] [--device D] [--noise-seed S] [--poses file]\n");
+    return 1;
+  }
+  const std::string settings = pos[1], seq = pos[2];
+  // ---- settings (Tracking::Tracking, Tracking.cc:135-238)
+  auto get = [&](const char* k, double def) {
+    double v = def;
+    if (mmt_io_yaml_float(settings.c_str(), k, &v) != 0) v = def;
+    return v;
+  };
+  double probe;
+  if (mmt_io_yaml_float(settings.c_str(), "Camera.fx", &probe) != 0) {
+    fprintf(stderr, "Failed to open settings file at: %s\n", settings.c_str());
+    return 1;
+  }
+  // ---- sequence (LoadData, rgbd_tum.cc:213-312)
+  double* times = nullptr;
+  int ntimes = 0;
+  if (mmt_io_read_times((seq + "/times.txt").c_str(), &times, &ntimes) != 0 || ntimes == 0) {
+    fprintf(stderr, "\nNo images found in provided path.\n");
+    return 1;
+  }
+  float* gt = nullptr;
+  int ngt = 0;
+  mmt_io_read_poses((seq + "/pose_gt.txt").c_str(), &gt, &ngt);
+  int nImages = 0;
+  while (nImages < ntimes && exists(frame_name(seq, "image", nImages, ".png"))) nImages++;
+  if (nImages == 0) {
+    fprintf(stderr, "\nNo images found in provided path.\n");
+    return 1;
+  }
+  mmt_config cfg;
+  memset(&cfg, 0, sizeof(cfg));
+  cfg.width = (int)get("Camera.width", 0);
+  cfg.height = (int)get("Camera.height", 0);
+  cfg.fx = (float)get("Camera.fx", 0);
+  cfg.fy = (float)get("Camera.fy", 0);
+  cfg.cx = (float)get("Camera.cx", 0);
+  cfg.cy = (float)get("Camera.cy", 0);
+  cfg.k1 = (float)get("Camera.k1", 0);
+  cfg.k2 = (float)get("Camera.k2", 0);
+  cfg.p1 = (float)get("Camera.p1", 0);
+  cfg.p2 = (float)get("Camera.p2", 0);
+  cfg.k3 = (float)get("Camera.k3", 0);
+  cfg.bf = (float)get("Camera.bf", 0);
+  cfg.th_depth = (float)get("ThDepth", 0);
+  cfg.rgb = (int)get("Camera.RGB", 1);
+  cfg.orb_nfeatures = nfeat > 0 ? nfeat : (int)get("ORBextractor.nFeatures", 2000);
+  cfg.orb_scale_factor = (float)get("ORBextractor.scaleFactor", 1.2);
+  cfg.orb_nlevels = (int)get("ORBextractor.nLevels", 8);
+  cfg.orb_ini_th_fast = (int)get("ORBextractor.iniThFAST", 20);
+  cfg.orb_min_th_fast = (int)get("ORBextractor.minThFAST", 7);
+  cfg.noise_seed = seed;
+  cfg.device_id = device;
+  cfg.max_batch = 1;
+  // image size from the first frame when the settings omit it
+  int w0 = 0, h0 = 0, ch0 = 0, db0 = 0;
+  void* probe_img = nullptr;
+  if (mmt_io_read_png(frame_name(seq, "image", 0, ".png").c_str(), &w0, &h0, &ch0, &db0,
+                      &probe_img) != 0) {
+    fprintf(stderr, "\nFailed to load image at: %s\n", frame_name(seq, "image", 0, ".png").c_str());
+    return 1;
+  }
+  mmt_io_free(probe_img);
+  if (cfg.width <= 0 || cfg.height <= 0) {
+    cfg.width = w0;
+    cfg.height = h0;
+  }
+  mmt_ctx* ctx = mmt_create(&cfg);
+  if (!ctx) {
+    fprintf(stderr, "mmt_create failed: %s\n", mmt_last_error(nullptr));
+    return 1;
+  }
+  const int W = cfg.width, H = cfg.height;
+  const size_t npix = (size_t)W * H;
+  std::vector<int32_t> mask(npix);
+  std::vector<uint16_t> disp(npix);
+  std::vector<mmt_motion> objs(64);
+  std::vector<float> track_times(nImages);
+  FILE* fp = poses_out.empty() ? nullptr : fopen(poses_out.c_str(), "w");
+  float lastTcw[16], lastGt[16];
+  bool haveLast = false;
+
+  printf("\n-------\nStart processing sequence ...\nImages in the sequence: %d\n\n", nImages);
+  int rc_all = 0;
+  for (int ni = 0; ni < nImages; ni++) {
+    printf("\n=======================================================\n");
+    printf("Processing Frame: %d\n", ni);
+    int w, h, ch, db;
+    void* img = nullptr;
+    void* dimg = nullptr;
+    float* flow = nullptr;
+    int fw = 0, fh = 0;
+    if (mmt_io_read_png(frame_name(seq, "image", ni, ".png").c_str(), &w, &h, &ch, &db, &img) != 0 ||
+        w != W || h != H || ch != 3 || db != 1) {
+      fprintf(stderr, "\nFailed to load image at: %s\n", frame_name(seq, "image", ni, ".png").c_str());
+      rc_all = 1;
+      mmt_io_free(img);
+      break;
+    }
+    int dw, dh, dch, ddb;
+    if (mmt_io_read_png(frame_name(seq, "depth", ni, ".png").c_str(), &dw, &dh, &dch, &ddb, &dimg) != 0 ||
+        dw != W || dh != H || dch != 1) {
+      fprintf(stderr, "\nFailed to load depth at: %s\n", frame_name(seq, "depth", ni, ".png").c_str());
+      rc_all = 1;
+      mmt_io_free(img);
+      mmt_io_free(dimg);
+      break;
+    }
+    for (size_t p = 0; p < npix; p++)
+      disp[p] = ddb == 2 ? ((uint16_t*)dimg)[p] : ((uint8_t*)dimg)[p];  // imD.convertTo(CV_32F)
+    if (mmt_io_read_flo(frame_name(seq, "flow", ni, ".flo").c_str(), &fw, &fh, &flow) != 0 ||
+        fw != W || fh != H) {
+      fprintf(stderr, "\nFailed to load flow at: %s\n", frame_name(seq, "flow", ni, ".flo").c_str());
+      rc_all = 1;
+      mmt_io_free(img);
+      mmt_io_free(dimg);
+      mmt_io_free(flow);
+      break;
+    }
+    std::fill(mask.begin(), mask.end(), 0);
+    mmt_io_read_mask(frame_name(seq, "semantic", ni, ".txt").c_str(), H, W, mask.data());
+    const auto t1 = std::chrono::steady_clock::now();
+    mmt_frame_result res;
+    const int rc = mmt_track_rgbd(ctx, (const uint8_t*)img, disp.data(), flow, mask.data(),
+                                  times[ni], &res, objs.data(), (int)objs.size());
+    const auto t2 = std::chrono::steady_clock::now();
+    mmt_io_free(img);
+    mmt_io_free(dimg);
+    mmt_io_free(flow);
+    if (rc != 0) {
+      fprintf(stderr, "mmt_track_rgbd failed (%d): %s\n", rc, mmt_last_error(ctx));
+      rc_all = 1;
+      break;
+    }
+    const double ttrack = std::chrono::duration<double>(t2 - t1).count();
+    track_times[ni] = (float)ttrack;
+    const float* Tgt = (ni < ngt) ? gt + 16 * ni : nullptr;
+    if (haveLast && res.initialized && Tgt) print_camera_rpe(res.Tcw, lastTcw, Tgt, lastGt);
+    for (int k = 0; k < res.n_objects && k < (int)objs.size(); k++) {
+      const mmt_motion& m = objs[k];
+      printf("object %d (semantic label %d): %d points, %d RANSAC inliers, %d inliers; motion t = "
+             "[%.4f %.4f %.4f]\n", m.label, m.sem_label, m.n_points, m.n_ransac_inliers,
+             m.n_inliers, m.world_motion[3], m.world_motion[7], m.world_motion[11]);
+    }
+    if (fp) {
+      fprintf(fp, "%d", ni);
+      for (int k = 0; k < 16; k++) fprintf(fp, " %.9f", res.Tcw[k]);
+      fprintf(fp, "\n");
+    }
+    if (res.initialized && Tgt) {
+      memcpy(lastTcw, res.Tcw, sizeof(lastTcw));
+      memcpy(lastGt, Tgt, sizeof(lastGt));
+      haveLast = true;
+    }
+    if (realtime) {  // rgbd_tum.cc:180-188
+      double T = 0;
+      if (ni < nImages - 1) T = times[ni + 1] - times[ni];
+      else if (ni > 0) T = times[ni] - times[ni - 1];
+      if (ttrack < T) std::this_thread::sleep_for(std::chrono::duration<double>(T - ttrack));
+    }
+  }
+  if (fp) fclose(fp);
+  mmt_destroy(ctx);
+  mmt_io_free(times);
+  mmt_io_free(gt);
+  if (rc_all) return rc_all;
+  std::vector<float> sorted = track_times;
+  std::sort(sorted.begin(), sorted.end());
+  float total = 0;
+  for (float t : sorted) total += t;
+  printf("-------------------------------------------------------------------\n");
+  printf("median tracking time: %g\n", sorted[nImages / 2]);
+  printf("mean tracking time: %g\n", total / nImages);
+  return 0;
+}
