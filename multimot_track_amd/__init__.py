@@ -126,7 +126,7 @@ def lib():
             import torch  # noqa: F401
         except ImportError:
             pass
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(os.environ.get("MMT_LIB_PATH", LIB_PATH))  # override: A/B builds
         vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         L.mmt_version.restype = i32
         L.mmt_last_error.restype = ctypes.c_char_p

@@ -84,19 +84,25 @@ class OrbEngine {
   const std::vector<LevelInfo>& levels() const { return lv_; }
   // Device pyramid of the last run (frame-major, pyr_stride_ bytes per frame).
   const uint8_t* pyramid() const { return d_pyr_; }
+  // Level 0 of frame f is written here by a producer that skips the staging copy: run() with
+  // d_gray == level0() and frame_pitch == pyramid_stride() reads the pyramid in place.
+  uint8_t* level0() { return d_pyr_; }
   size_t pyramid_stride() const { return pyr_stride_; }
   long debug_fetch(int what, int frame, void* out, size_t cap, hipStream_t stream);
 
  private:
   void release();
   int w_ = 0, h_ = 0, nlevels_ = 0, max_batch_ = 0, ncells_ = 0, ntiles_ = 0;
-  int fast_tile_max_ = 0, fast_win_max_ = 0;  // largest FAST cell tile / window (bytes)
+  int fast_rows_max_ = 0, fast_cols_max_ = 0, fast_win_max_ = 0;  // largest FAST tile / window
   int total_slots_ = 0, out_slots_ = 0, cap_frame_ = 0, node_cap_ = 0;
+  int key_cap_ = 0;          // k_octree: keys per (level, frame) held in LDS
+  size_t octree_lds_ = 0;    // k_octree dynamic LDS bytes
   int iniTh_ = 20, minTh_ = 7;
   size_t pyr_stride_ = 0;
   std::vector<LevelInfo> lv_;
   std::vector<CellInfo> cells_;
   std::vector<int> xtab_off_, ytab_off_;
+  std::vector<int> rs_pitch_, rs_lds_;  // k_resize LDS row pitch and bytes per level
   LevelInfo* d_lv_ = nullptr;
   CellInfo* d_cells_ = nullptr;
   ResizeX* d_xtab_ = nullptr;

@@ -97,41 +97,92 @@ void OrbTables::init(int nf, float scaleFactorF, int nl, int ini, int mn) {
 // ======================================================================== kernels
 
 // ---- pyramid level l from level l-1 (cv::resize INTER_LINEAR 8U, scalar fixed point) ----
-constexpr int kResizeRows = 8;  // output rows per workgroup (the x coefficients load once)
+// One workgroup per (band of kResizeRows output rows, 1024 output columns, frame).  The source
+// rows and columns the band reads are staged once in LDS with coalesced dword loads; each thread
+// then forms four adjacent outputs per row from LDS and stores them as one dword.
+constexpr int kResizeRows = 8;
+constexpr int kResizeCols = 1024;  // 256 threads x 4 columns
+constexpr int kResizeStage = 16;   // staging dwords per thread issued together
 
 __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                 int src_off, int sw, int dst_off, int dw, int dh,
                                                 const ResizeX* __restrict__ xt,
-                                                const ResizeY* __restrict__ yt) {
-  const int dx = blockIdx.x * 256 + threadIdx.x;
-  if (dx >= dw) return;
+                                                const ResizeY* __restrict__ yt, int lds_pitch) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t rs_lds[];
+  const int tid = threadIdx.x;
   uint8_t* base = pyr + (size_t)blockIdx.z * pyr_stride;
   const uint8_t* src = base + src_off;
-  const ResizeX cx = xt[dx];
+  const int dx0 = blockIdx.x * kResizeCols, dx1 = min(dx0 + kResizeCols, dw);
   const int y0 = blockIdx.y * kResizeRows, y1 = min(y0 + kResizeRows, dh);
-  // all source loads of the band first (independent), then the arithmetic
-  int p00[kResizeRows], p01[kResizeRows], p10[kResizeRows], p11[kResizeRows];
+  // source window (sx and sy are non-decreasing in dx and dy)
+  const int sx_lo = xt[dx0].sx, sx_hi = min(xt[dx1 - 1].sx + 1, sw - 1);
+  const int sy_lo = yt[y0].sy0, sy_hi = yt[y1 - 1].sy1;
+  const int nq = (sx_hi - sx_lo + 4) >> 2;  // dwords per staged row
+  const int items = (sy_hi - sy_lo + 1) * nq;
+  const float inv_nq = 1.0f / (float)nq;
+  const uint8_t* s0 = src + (size_t)sy_lo * sw + sx_lo;
+  // every staging load is issued before the first LDS store (one memory round trip per
+  // workgroup; the source may be 3 bytes past a row end: next row, next level or slack)
+  auto item_addr = [&](int i, int& lds_off) {
+    int r = (int)((float)i * inv_nq);
+    r -= r * nq > i ? 1 : 0;
+    r += (r + 1) * nq <= i ? 1 : 0;
+    const int q = i - r * nq;
+    lds_off = r * lds_pitch + 4 * q;
+    return s0 + (size_t)r * sw + 4 * q;
+  };
+  uint32_t v[kResizeStage];
+  int off[kResizeStage];
+#pragma unroll
+  for (int k = 0; k < kResizeStage; k++) {
+    const int i = tid + 256 * k;
+    if (i < items) __builtin_memcpy(&v[k], item_addr(i, off[k]), 4);
+  }
+  const int dx = dx0 + 4 * tid;
+  ResizeX cx[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) cx[j] = xt[min(dx + j, dw - 1)];
   ResizeY cy[kResizeRows];
 #pragma unroll
-  for (int k = 0; k < kResizeRows; k++) {
-    const int dy = min(y0 + k, dh - 1);
-    cy[k] = yt[dy];
-    const uint8_t* s0 = src + (size_t)cy[k].sy0 * sw + cx.sx;
-    const uint8_t* s1 = src + (size_t)cy[k].sy1 * sw + cx.sx;
-    p00[k] = s0[0];
-    p10[k] = s1[0];
-    // a1 == 0 marks the clamped right edge (dx >= xmax): only S[sx]*2048 contributes
-    p01[k] = cx.a1 ? s0[1] : 0;
-    p11[k] = cx.a1 ? s1[1] : 0;
+  for (int k = 0; k < kResizeRows; k++) cy[k] = yt[min(y0 + k, dh - 1)];
+#pragma unroll
+  for (int k = 0; k < kResizeStage; k++)
+    if (tid + 256 * k < items) *(uint32_t*)(rs_lds + off[k]) = v[k];
+  for (int i = tid + 256 * kResizeStage; i < items; i += 256) {  // wide windows only
+    int o;
+    uint32_t w;
+    __builtin_memcpy(&w, item_addr(i, o), 4);
+    *(uint32_t*)(rs_lds + o) = w;
   }
+  __syncthreads();
+  if (dx >= dx1) return;
+  const int ncols = min(4, dx1 - dx);
+  int lx[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) lx[j] = cx[j].sx - sx_lo;
 #pragma unroll
   for (int k = 0; k < kResizeRows; k++) {
-    if (y0 + k >= y1) break;
-    const int h0 = cx.a1 ? p00[k] * cx.a0 + p01[k] * cx.a1 : p00[k] * cx.a0;
-    const int h1 = cx.a1 ? p10[k] * cx.a0 + p11[k] * cx.a1 : p10[k] * cx.a0;
-    int v = (cy[k].b0 * h0 + cy[k].b1 * h1 + (1 << 21)) >> 22;
-    v = v < 0 ? 0 : (v > 255 ? 255 : v);
-    base[dst_off + (size_t)(y0 + k) * dw + dx] = (uint8_t)v;
+    const int y = y0 + k;
+    if (y >= y1) break;
+    const uint8_t* r0 = rs_lds + (cy[k].sy0 - sy_lo) * lds_pitch;
+    const uint8_t* r1 = rs_lds + (cy[k].sy1 - sy_lo) * lds_pitch;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      // a1 == 0 marks the clamped right edge (dx >= xmax): only S[sx]*2048 contributes (the
+      // byte at sx+1 is then multiplied by 0; it lies inside the LDS row pitch)
+      const int h0 = r0[lx[j]] * cx[j].a0 + r0[lx[j] + 1] * cx[j].a1;
+      const int h1 = r1[lx[j]] * cx[j].a0 + r1[lx[j] + 1] * cx[j].a1;
+      int v = (cy[k].b0 * h0 + cy[k].b1 * h1 + (1 << 21)) >> 22;
+      v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      packed |= (uint32_t)v << (8 * j);
+    }
+    uint8_t* dp = base + dst_off + (size_t)y * dw + dx;
+    if (ncols == 4) {
+      __builtin_memcpy(dp, &packed, 4);
+    } else {
+      for (int j = 0; j < ncols; j++) dp[j] = (uint8_t)(packed >> (8 * j));
+    }
   }
 }
 
@@ -140,27 +191,33 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
 // M - 1 for every corner (derivation in DESIGN.md), so one M per pixel serves both thresholds.
 typedef short short2v __attribute__((ext_vector_type(2)));
 
+// LDS row stride of a FAST tile (template parameter FS): a compile-time constant, so every
+// circle / compass / NMS neighbour read is one ds_read with an immediate offset from the pixel's
+// address.  40 covers the ~31-pixel cells of any image (tile = cell + 6); 72 is the general case.
+constexpr int kFSSmall = 40, kFSMax = 72;
+
 // (d, -d) per circle point as a packed int16 pair: the dark test (min of v - p over a 9-arc) and
 // the bright test (min of p - v) run in the two halves of one v_pk_min_i16 / v_pk_max_i16 chain.
-__device__ __forceinline__ int arc_strength(const uint8_t* t, int stride, int r, int c) {
-  const int v = t[r * stride + c];
+template <int kFS>
+__device__ __forceinline__ int arc_strength(const uint8_t* t) {
+  const int v = t[0];
   int q[16];
-  q[0] = t[(r + 3) * stride + c];
-  q[1] = t[(r + 3) * stride + c + 1];
-  q[2] = t[(r + 2) * stride + c + 2];
-  q[3] = t[(r + 1) * stride + c + 3];
-  q[4] = t[r * stride + c + 3];
-  q[5] = t[(r - 1) * stride + c + 3];
-  q[6] = t[(r - 2) * stride + c + 2];
-  q[7] = t[(r - 3) * stride + c + 1];
-  q[8] = t[(r - 3) * stride + c];
-  q[9] = t[(r - 3) * stride + c - 1];
-  q[10] = t[(r - 2) * stride + c - 2];
-  q[11] = t[(r - 1) * stride + c - 3];
-  q[12] = t[r * stride + c - 3];
-  q[13] = t[(r + 1) * stride + c - 3];
-  q[14] = t[(r + 2) * stride + c - 2];
-  q[15] = t[(r + 3) * stride + c - 1];
+  q[0] = t[3 * kFS];
+  q[1] = t[3 * kFS + 1];
+  q[2] = t[2 * kFS + 2];
+  q[3] = t[kFS + 3];
+  q[4] = t[3];
+  q[5] = t[-kFS + 3];
+  q[6] = t[-2 * kFS + 2];
+  q[7] = t[-3 * kFS + 1];
+  q[8] = t[-3 * kFS];
+  q[9] = t[-3 * kFS - 1];
+  q[10] = t[-2 * kFS - 2];
+  q[11] = t[-kFS - 3];
+  q[12] = t[-3];
+  q[13] = t[kFS - 3];
+  q[14] = t[2 * kFS - 2];
+  q[15] = t[3 * kFS - 1];
   short2v d[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) d[k] = short2v{(short)(v - q[k]), (short)(q[k] - v)};
@@ -191,9 +248,6 @@ __device__ __forceinline__ uint32_t ldg32(const uint8_t* p) {
   return v;
 }
 
-#define FAST_TILE_MAX 5184  // 72 x 72 tile
-#define FAST_WIN_MAX 4356   // 66 x 66 window
-
 // Wave-level LDS ordering (no s_barrier): a wave's LDS writes are visible to its other lanes
 // after this point.
 __device__ __forceinline__ void wave_sync() {
@@ -202,112 +256,148 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Compass pre-test: is some pair of adjacent compass points (0/4/8/12) both darker or both
+// brighter than the centre by more than th?
+__device__ __forceinline__ bool compass_pass(int v, int q0, int q4, int q8, int q12, int th) {
+  const int d0 = v - q0, d4 = v - q4, d8 = v - q8, d12 = v - q12;
+  const bool k0 = d0 > th, k4 = d4 > th, k8 = d8 > th, k12 = d12 > th;
+  const bool b0 = d0 < -th, b4 = d4 < -th, b8 = d8 < -th, b12 = d12 < -th;
+  return (k0 && k4) || (k4 && k8) || (k8 && k12) || (k12 && k0) || (b0 && b4) || (b4 && b8) ||
+         (b8 && b12) || (b12 && b0);
+}
+
+// LDS bytes of one wave's FAST workspace: tile and arc-strength map (rows x kFS each) and the
+// u16 candidate list (one entry per window pixel).
+__host__ __device__ constexpr int fast_wave_lds(int kFS, int rows_max, int win_max) {
+  return ((2 * rows_max * kFS + 2 * win_max) + 15) & ~15;
+}
+
 // One wave per (cell, frame); four cells per workgroup.  Cell = the submatrix the reference hands
-// to cv::FAST (ORBextractor.cc:791-816).  The wave stages the cell in its own LDS region, scores
-// every pixel once (arc strength M), then per threshold (iniTh, then minTh if the cell came out
-// empty) runs the cell-local 3x3 strict NMS and an order-preserving ballot compaction -- all
-// wave-synchronous, so cells of different sizes never wait for each other.
+// to cv::FAST (ORBextractor.cc:791-816).  The wave stages the cell in its own LDS tile (row
+// stride kFS) and keeps an arc-strength map of the same shape, zero except at the candidates of
+// the current pass, so out-of-window NMS neighbours read 0 without bounds checks.  Per threshold
+// (iniTh, then minTh if the cell came out empty, ORBextractor.cc:809-816):
+//  1) compass pre-test at th over the window (2 rows x 32 columns or 1 row x 64 columns per
+//     wave step): a 9-arc covers two adjacent compass points (0/4/8/12), so a pixel whose pairs
+//     all fail has M <= th and is no corner; survivors are compacted in row-major order;
+//  2) arc strength M of the candidates;
+//  3) cell-local 3x3 strict NMS on scores s = (M > th ? M - 1 : 0) over the candidate list,
+//     neighbours scored on the fly from the map; ballot compaction keeps row-major order.
+// All wave-synchronous, so cells of different sizes never wait for each other.
+template <int kFS>
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                               const LevelInfo* __restrict__ lv,
                                               const CellInfo* __restrict__ cells, int ncells,
                                               uint32_t* __restrict__ keys, int total_slots,
                                               int* __restrict__ cellcnt, int iniTh, int minTh,
-                                              int tile_max, int win_max) {
-  extern __shared__ uint8_t fast_lds[];
+                                              int rows_max, int win_max) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t fast_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cell = blockIdx.x * 4 + wave;
   if (cell >= ncells) return;
-  const int per_wave = (tile_max + 4 * win_max + 31) & ~15;
-  uint8_t* tile = fast_lds + wave * per_wave;
-  uint8_t* arcm = tile + tile_max;
-  uint8_t* score = arcm + win_max;
-  uint16_t* cand_list = (uint16_t*)(((uintptr_t)(score + win_max) + 1) & ~(uintptr_t)1);
+  uint8_t* tile = fast_lds + wave * fast_wave_lds(kFS, rows_max, win_max);
+  uint8_t* arcm = tile + rows_max * kFS;
+  uint16_t* cand_list = (uint16_t*)(arcm + rows_max * kFS);
   const CellInfo ci = cells[cell];
   const int frame = blockIdx.y;
   const LevelInfo L = lv[ci.level];
   const uint8_t* img = pyr + (size_t)frame * pyr_stride + L.off;
-  const int rows = ci.rows, cols = (ci.cols + 3) & ~3;  // LDS row stride: whole dwords
+  const int rows = ci.rows, nq = (ci.cols + 3) >> 2;  // dwords per tile row
   {
-    // dword copy (the pyramid allocation has slack for the <= 3 bytes past the last row)
-    const int nq = cols >> 2;
+    // dword copy (the pyramid allocation has slack for the <= 3 bytes past the last row); every
+    // load of the first kStage rounds is issued before the first LDS store
     const float inv_nq = 1.0f / (float)nq;
     const uint8_t* src = img + (size_t)ci.r0 * L.w + ci.c0;
-    for (int i = lane; i < rows * nq; i += 64) {
+    const int items = rows * nq;
+    constexpr int kStage = 8;
+    uint32_t v[kStage];
+    int o[kStage];
+#pragma unroll
+    for (int k = 0; k < kStage; k++) {
+      const int i = lane + 64 * k;
+      if (i < items) {
+        const int r = div_small(i, inv_nq), q = i - r * nq;
+        v[k] = ldg32(src + (size_t)r * L.w + 4 * q);
+        o[k] = r * kFS + 4 * q;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kStage; k++)
+      if (lane + 64 * k < items) *(uint32_t*)(tile + o[k]) = v[k];
+    for (int i = lane + 64 * kStage; i < items; i += 64) {
       const int r = div_small(i, inv_nq), q = i - r * nq;
-      *(uint32_t*)(tile + 4 * i) = ldg32(src + (size_t)r * L.w + 4 * q);
+      *(uint32_t*)(tile + r * kFS + 4 * q) = ldg32(src + (size_t)r * L.w + 4 * q);
     }
+    for (int i = lane; i < rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
   }
   wave_sync();
-  const int R = rows - 6, C = ci.cols - 6;  // detection window: tile rows 3..rows-4, cols 3..-4
-  const int npx = R * C;
-  const float invC = 1.0f / (float)C;
-  // Arc strength only where it can exceed the lower threshold: a 9-arc covers two adjacent
-  // compass points (0/4/8/12), so a pixel whose compass pairs all fail at t_lo has M <= t_lo and
-  // is no corner at either threshold (its arcm may then be stored as 0).  Candidates are
-  // compacted so the full 16-point test runs on dense lanes.
-  const int t_lo = min(min(max(iniTh, 0), 255), min(max(minTh, 0), 255));
-  int ncand = 0;
-  for (int p0 = 0; p0 < npx; p0 += 64) {
-    const int p = p0 + lane;
-    bool cand = false;
-    if (p < npx) {
-      const int rq = div_small(p, invC);
-      const int r = rq + 3, c = p - rq * C + 3;
-      const int v = tile[r * cols + c];
-      const int d0 = v - tile[(r + 3) * cols + c], d4 = v - tile[r * cols + c + 3];
-      const int d8 = v - tile[(r - 3) * cols + c], d12 = v - tile[r * cols + c - 3];
-      const bool k0 = d0 > t_lo, k4 = d4 > t_lo, k8 = d8 > t_lo, k12 = d12 > t_lo;
-      const bool b0 = d0 < -t_lo, b4 = d4 < -t_lo, b8 = d8 < -t_lo, b12 = d12 < -t_lo;
-      cand = (k0 && k4) || (k4 && k8) || (k8 && k12) || (k12 && k0) || (b0 && b4) ||
-             (b4 && b8) || (b8 && b12) || (b12 && b0);
-      if (!cand) arcm[p] = 0;
-    }
-    const unsigned long long bal = __ballot(cand);
-    if (cand) cand_list[ncand + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)p;
-    ncand += __popcll(bal);
-  }
-  wave_sync();
-  for (int k = lane; k < ncand; k += 64) {
-    const int p = cand_list[k];
-    const int r = div_small(p, invC), c = p - r * C;
-    const int m = arc_strength(tile, cols, r + 3, c + 3);
-    arcm[p] = (uint8_t)(m < 0 ? 0 : m);
-  }
-  wave_sync();
+  const int R = rows - 6, C = ci.cols - 6;  // detection window: tile rows 3..rows-4, cols 3..C+2
+  // pre-test lane mapping: lg = log2(columns per step), rows per step = 64 >> lg
+  const int lg = C <= 32 ? 5 : 6;
+  const int col = lane & ((1 << lg) - 1), rsub = lane >> lg, rstep = 64 >> lg;
   uint32_t* out = keys + (size_t)frame * total_slots + ci.slot_off;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  int count = 0;
+  int count = 0, ncand = 0;
   for (int pass = 0; pass < 2; pass++) {
     const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
-    for (int p = lane; p < npx; p += 64) {
-      const int m = arcm[p];
-      score[p] = (uint8_t)(m > th ? m - 1 : 0);
+    if (pass) {  // clear pass 0's candidates from the map
+      for (int k = lane; k < ncand; k += 64) arcm[cand_list[k]] = 0;
+      wave_sync();
+    }
+    ncand = 0;
+    // two wave steps per iteration: all ten reads are issued before the first test
+    for (int r0 = 0; r0 < R; r0 += 2 * rstep) {
+      const int ra = r0 + rsub, rb = ra + rstep;
+      const int pa = (ra + 3) * kFS + col + 3, pb = pa + rstep * kFS;  // tile positions
+      const bool ina = ra < R && col < C, inb = rb < R && col < C;
+      int va = 0, a0 = 0, a4 = 0, a8 = 0, a12 = 0, vb = 0, b0 = 0, b4 = 0, b8 = 0, b12 = 0;
+      if (ina) {
+        const uint8_t* t = tile + pa;
+        va = t[0]; a0 = t[3 * kFS]; a4 = t[3]; a8 = t[-3 * kFS]; a12 = t[-3];
+      }
+      if (inb) {
+        const uint8_t* t = tile + pb;
+        vb = t[0]; b0 = t[3 * kFS]; b4 = t[3]; b8 = t[-3 * kFS]; b12 = t[-3];
+      }
+      const bool ca = ina && compass_pass(va, a0, a4, a8, a12, th);
+      const bool cb = inb && compass_pass(vb, b0, b4, b8, b12, th);
+      const unsigned long long bala = __ballot(ca), balb = __ballot(cb);
+      if (ca) cand_list[ncand + __popcll(bala & lt)] = (uint16_t)pa;
+      ncand += __popcll(bala);
+      if (cb) cand_list[ncand + __popcll(balb & lt)] = (uint16_t)pb;
+      ncand += __popcll(balb);
+    }
+    wave_sync();
+    for (int k = lane; k < ncand; k += 64) {
+      const int p = cand_list[k];
+      const int m = arc_strength<kFS>(tile + p);
+      arcm[p] = (uint8_t)(m < 0 ? 0 : m);
     }
     wave_sync();
     int base = 0;
-    for (int p0 = 0; p0 < npx; p0 += 64) {
-      const int p = p0 + lane;
+    for (int k0 = 0; k0 < ncand; k0 += 64) {
+      const int k = k0 + lane;
       bool keep = false;
-      int sc = 0;
-      if (p < npx && arcm[p] > th) {
-        const int r = div_small(p, invC), c = p - r * C;
-        sc = score[p];
-        keep = true;
+      int sc = 0, p = 0;
+      if (k < ncand) {
+        p = cand_list[k];
+        const uint8_t* a = arcm + p;
+        const int m = a[0];
+        if (m > th) {
+          sc = m - 1;
+          const int n[8] = {a[-kFS - 1], a[-kFS], a[-kFS + 1], a[-1],
+                            a[1],        a[kFS - 1], a[kFS], a[kFS + 1]};
+          int nmax = 0;
 #pragma unroll
-        for (int dr = -1; dr <= 1; dr++)
-#pragma unroll
-          for (int dc = -1; dc <= 1; dc++) {
-            if (dr == 0 && dc == 0) continue;
-            const int rr = r + dr, cc = c + dc;
-            const int ns = (rr >= 0 && rr < R && cc >= 0 && cc < C) ? score[rr * C + cc] : 0;
-            keep = keep && (sc > ns);
-          }
+          for (int j = 0; j < 8; j++) nmax = max(nmax, n[j] > th ? n[j] - 1 : 0);
+          keep = sc > nmax;
+        }
       }
       const unsigned long long bal = __ballot(keep);
       if (keep) {
-        const int r = div_small(p, invC), c = p - r * C;
-        const uint32_t x = (uint32_t)(ci.c0 - kMinBorder + c + 3);
-        const uint32_t y = (uint32_t)(ci.r0 - kMinBorder + r + 3);
+        const int tr = p / kFS, tc = p - tr * kFS;
+        const uint32_t x = (uint32_t)(ci.c0 - kMinBorder + tc);
+        const uint32_t y = (uint32_t)(ci.r0 - kMinBorder + tr);
         const int slot = base + __popcll(bal & lt);
         if (slot < ci.slot_cap) out[slot] = (y << 20) | (x << 8) | (uint32_t)sc;
       }
@@ -315,14 +405,23 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
     }
     count = base;
     if (count > 0) break;
-    wave_sync();  // the next pass rewrites `score`
+    wave_sync();
   }
   if (lane == 0) cellcnt[(size_t)frame * ncells + cell] = min(count, ci.slot_cap);
 }
 
 // ---------------------------------------------------------------- octree helpers
+// LDS arrays are typed as address-space-3 pointers so every access is a ds_* instruction, also
+// through the double-buffered node arrays selected at run time.
+#define LDS __attribute__((address_space(3)))
+typedef LDS uint16_t lds_u16;
+typedef LDS uint32_t lds_u32;
+typedef LDS int lds_i32;
+typedef LDS uint8_t lds_u8;
+typedef LDS unsigned long long lds_u64;
+
 // In-place exclusive scan of LDS ints a[0..n) by the whole workgroup; returns the total.
-__device__ int wg_scan_excl(int* a, int n, int* s_tmp /*[17]*/) {
+__device__ int wg_scan_excl(lds_i32* a, int n, lds_i32* s_tmp /*[17]*/) {
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const int per = (n + nt - 1) / nt;
   const int b = min(tid * per, n), e = min(b + per, n);
@@ -363,45 +462,56 @@ __device__ __forceinline__ uint32_t key_y(uint32_t k) { return k >> 20; }
 __device__ __forceinline__ uint32_t key_s(uint32_t k) { return k & 0xFFu; }
 
 struct OctLDS {
-  uint16_t* x0[2];
-  uint16_t* y0[2];
-  uint16_t* x1[2];
-  uint16_t* y1[2];
-  uint32_t* cnt[2];
-  uint32_t* seq[2];
-  int* prank;
-  int* order;
-  int* gst;    // group start of processed rank r, later reused
-  int* cumnc;  // exclusive prefix of child counts
-  int* krank;  // kept-node rank
-  uint32_t* cc;          // 4 per processed rank (aliases sortkey / best)
-  unsigned long long* sortkey;
-  uint32_t* best;
+  lds_u16* x0[2];
+  lds_u16* y0[2];
+  lds_u16* x1[2];
+  lds_u16* y1[2];
+  lds_u32* cnt[2];
+  lds_u32* seq[2];
+  lds_i32* prank;
+  lds_i32* order;
+  lds_i32* gst;    // group start of processed rank r, later reused
+  lds_i32* cumnc;  // exclusive prefix of child counts
+  lds_i32* krank;  // kept-node rank
+  lds_u32* cc;     // 4 per processed rank (aliases sortkey / best / the gather's cell offsets)
+  lds_u64* sortkey;
+  lds_u32* best;
+  lds_i32* s_tmp;  // [17]
+  lds_i32* s_ctl;  // [4]
+};
+
+// Per-key arrays of one (level, frame): gathered keys, key -> node, quadrant scratch.  In LDS
+// when the level's keys fit, otherwise in global memory (KP/NP/QP are the pointer types).
+template <typename KP, typename NP, typename QP>
+struct OctKeys {
+  KP lk;
+  NP knode;
+  QP kq;
 };
 
 // One division pass: nodes order[0..D) (processing order) are divided; every other node is kept.
 // Children of the last processed node go to the front (std::list::push_front semantics).
 // If `limitN` > 0 the pass stops after the first node whose division makes size >= limitN.
-__device__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D, int limitN,
-                         const uint32_t* __restrict__ lk, uint32_t* __restrict__ knode,
-                         uint8_t* __restrict__ kq, int n, int* s_tmp, int* s_ctl) {
+template <typename KA>
+__device__ __forceinline__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D,
+                                         int limitN, const KA& kk, int n) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const int c = cur;
   for (int i = tid; i < 4 * D; i += nt) S.cc[i] = 0;
   __syncthreads();
   // 1) child counts per processed node
   for (int i = tid; i < n; i += nt) {
-    const uint32_t nd = knode[i];
+    const uint32_t nd = kk.knode[i];
     const int r = S.prank[nd];
     if (r >= 0) {
-      const uint32_t k = lk[i];
+      const uint32_t k = kk.lk[i];
       const int hx = (int)ceilf((float)(S.x1[c][nd] - S.x0[c][nd]) / 2.f);
       const int hy = (int)ceilf((float)(S.y1[c][nd] - S.y0[c][nd]) / 2.f);
       const int mx = S.x0[c][nd] + hx, my = S.y0[c][nd] + hy;
       const int q = ((int)key_x(k) < mx) ? (((int)key_y(k) < my) ? 0 : 2)
                                          : (((int)key_y(k) < my) ? 1 : 3);
-      kq[i] = (uint8_t)q;
-      atomicAdd(&S.cc[r * 4 + q], 1u);
+      kk.kq[i] = (uint8_t)q;
+      atomicAdd((uint32_t*)&S.cc[r * 4 + q], 1u);
     }
   }
   __syncthreads();
@@ -411,22 +521,22 @@ __device__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D, 
     for (int k = 0; k < 4; k++) nc += S.cc[r * 4 + k] > 0;
     S.cumnc[r] = nc;
   }
-  if (tid == 0) s_ctl[0] = D;
+  if (tid == 0) S.s_ctl[0] = D;
   __syncthreads();
   if (limitN > 0) {
     for (int r = tid; r < D; r += nt) S.gst[r] = S.cumnc[r] - 1;
     __syncthreads();
-    wg_scan_excl(S.gst, D, s_tmp);
+    wg_scan_excl(S.gst, D, S.s_tmp);
     for (int r = tid; r < D; r += nt) {
       const int incl = S.gst[r] + S.cumnc[r] - 1;
-      if (L + incl >= limitN) atomicMin(&s_ctl[0], r + 1);
+      if (L + incl >= limitN) atomicMin((int*)&S.s_ctl[0], r + 1);
     }
     __syncthreads();
   }
-  const int Dt = s_ctl[0];
+  const int Dt = S.s_ctl[0];
   for (int r = tid + Dt; r < D; r += nt) S.prank[S.order[r]] = -1;  // not divided this pass
   __syncthreads();
-  const int T = wg_scan_excl(S.cumnc, Dt, s_tmp);  // cumnc = sum_{q<r} nc
+  const int T = wg_scan_excl(S.cumnc, Dt, S.s_tmp);  // cumnc = sum_{q<r} nc
   for (int r = tid; r < Dt; r += nt) {
     int nc = 0;
     for (int k = 0; k < 4; k++) nc += S.cc[r * 4 + k] > 0;
@@ -434,7 +544,7 @@ __device__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D, 
   }
   for (int s = tid; s < L; s += nt) S.krank[s] = S.prank[s] < 0 ? 1 : 0;
   __syncthreads();
-  const int K = wg_scan_excl(S.krank, L, s_tmp);
+  const int K = wg_scan_excl(S.krank, L, S.s_tmp);
   const int o = c ^ 1;
   // 3) new node list: processed children (n4..n1 per group, last group first), then kept nodes
   for (int r = tid; r < Dt; r += nt) {
@@ -445,11 +555,14 @@ __device__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D, 
     const int rx0[4] = {X0, mx, X0, mx}, ry0[4] = {Y0, Y0, my, my};
     const int rx1[4] = {mx, X1, mx, X1}, ry1[4] = {my, my, Y1, Y1};
     uint32_t cnts[4];
+#pragma unroll
     for (int k = 0; k < 4; k++) cnts[k] = S.cc[r * 4 + k];
     int before = 0;
+#pragma unroll
     for (int k = 0; k < 4; k++) {
       if (!cnts[k]) continue;
       int after = 0;
+#pragma unroll
       for (int k2 = k + 1; k2 < 4; k2++) after += cnts[k2] > 0;
       const int slot = S.gst[r] + after;
       S.x0[o][slot] = (uint16_t)rx0[k];
@@ -475,15 +588,15 @@ __device__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D, 
   __syncthreads();
   // 4) key -> new node
   for (int i = tid; i < n; i += nt) {
-    const uint32_t nd = knode[i];
+    const uint32_t nd = kk.knode[i];
     const int r = S.prank[nd];
     if (r >= 0) {
-      const int q = kq[i];
+      const int q = kk.kq[i];
       int after = 0;
       for (int k2 = q + 1; k2 < 4; k2++) after += S.cc[r * 4 + k2] > 0;
-      knode[i] = (uint32_t)(S.gst[r] + after);
+      kk.knode[i] = (uint16_t)(S.gst[r] + after);
     } else {
-      knode[i] = (uint32_t)(T + S.krank[nd]);
+      kk.knode[i] = (uint16_t)(T + S.krank[nd]);
     }
   }
   __syncthreads();
@@ -493,11 +606,11 @@ __device__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D, 
 }
 
 // Nodes with cnt > 1, in list order, into S.order; sets prank; returns their count.
-__device__ int oct_expandable_in_order(OctLDS& S, int cur, int L, int* s_tmp) {
+__device__ int oct_expandable_in_order(OctLDS& S, int cur, int L) {
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int s = tid; s < L; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
   __syncthreads();
-  const int D = wg_scan_excl(S.gst, L, s_tmp);
+  const int D = wg_scan_excl(S.gst, L, S.s_tmp);
   for (int s = tid; s < L; s += nt) {
     if (S.cnt[cur][s] > 1) {
       S.order[S.gst[s]] = s;
@@ -513,11 +626,11 @@ __device__ int oct_expandable_in_order(OctLDS& S, int cur, int L, int* s_tmp) {
 // Phase-2 order: expandable nodes sorted by (size, creation seq) descending (ORBextractor.cc:684
 // sorts pair<size, ExtractorNode*> ascending and walks it backwards; pointer order is pinned to
 // creation order).
-__device__ int oct_expandable_sorted(OctLDS& S, int cur, int L, int ncap, int* s_tmp) {
+__device__ int oct_expandable_sorted(OctLDS& S, int cur, int L) {
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int s = tid; s < L; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
   __syncthreads();
-  const int D = wg_scan_excl(S.gst, L, s_tmp);
+  const int D = wg_scan_excl(S.gst, L, S.s_tmp);
   int P = 1;
   while (P < D) P <<= 1;
   for (int i = tid; i < P; i += nt) S.sortkey[i] = 0ull;
@@ -554,77 +667,39 @@ __device__ int oct_expandable_sorted(OctLDS& S, int cur, int L, int ncap, int* s
     S.prank[s] = r;
   }
   __syncthreads();
-  (void)ncap;
   return D;
 }
 
-// One workgroup per (level, frame).  Gathers the level's FAST candidates in cell order and runs
-// DistributeOctTree.  Output: selected keys in list order, level coordinates.
-__global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ lv,
-                                                 const CellInfo* __restrict__ cells, int ncells,
-                                                 const uint32_t* __restrict__ keys,
-                                                 const int* __restrict__ cellcnt, int total_slots,
-                                                 uint32_t* __restrict__ lkeys,
-                                                 uint32_t* __restrict__ knode_g,
-                                                 uint32_t* __restrict__ okeys, int out_slots,
-                                                 int* __restrict__ ocount, int nlevels,
-                                                 int ncap, int* __restrict__ err) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int s_tmp[17];
-  __shared__ int s_ctl[4];
-  const int level = blockIdx.x, frame = blockIdx.y;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const LevelInfo L0 = lv[level];
-  // ---- carve LDS (all offsets multiples of 16)
-  OctLDS S;
-  unsigned char* p = smem;
-  auto carve = [&](size_t bytes) {
-    unsigned char* r = p;
-    p += (bytes + 15) & ~(size_t)15;
-    return r;
-  };
-  for (int b = 0; b < 2; b++) {
-    S.x0[b] = (uint16_t*)carve(2 * ncap);
-    S.y0[b] = (uint16_t*)carve(2 * ncap);
-    S.x1[b] = (uint16_t*)carve(2 * ncap);
-    S.y1[b] = (uint16_t*)carve(2 * ncap);
-    S.cnt[b] = (uint32_t*)carve(4 * ncap);
-    S.seq[b] = (uint32_t*)carve(4 * ncap);
-  }
-  S.prank = (int*)carve(4 * ncap);
-  S.order = (int*)carve(4 * ncap);
-  S.gst = (int*)carve(4 * ncap);
-  S.cumnc = (int*)carve(4 * ncap);
-  S.krank = (int*)carve(4 * ncap);
-  S.cc = (uint32_t*)carve(16 * ncap);
-  S.sortkey = (unsigned long long*)S.cc;
-  S.best = S.cc;
+// LDS layout of k_octree: node arrays (ncap nodes), then the per-key arrays of up to kcap keys.
+static size_t octree_node_lds_bytes(int ncap) {
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  size_t b = 0;
+  for (int i = 0; i < 2; i++) b += 4 * r16(2 * ncap) + 2 * r16(4 * ncap);
+  b += 5 * r16(4 * ncap) + r16(16 * ncap) + r16(4 * 24);
+  return b;
+}
+static size_t octree_key_lds_bytes(int kcap) { return (size_t)kcap * 7 + 16; }
 
-  // ---- gather candidates of this level in cell order
-  const int nc = L0.cell_end - L0.cell_begin;
-  const int* cnt = cellcnt + (size_t)frame * ncells + L0.cell_begin;
-  int* coff = (int*)S.cc;  // reuse as scratch (nc <= 4 * ncap checked on host)
-  for (int i = tid; i < nc; i += nt) coff[i] = cnt[i];
-  __syncthreads();
-  const int n = wg_scan_excl(coff, nc, s_tmp);
-  uint32_t* lk = lkeys + (size_t)frame * total_slots + L0.key_off;
-  uint32_t* knode = knode_g + (size_t)frame * total_slots + L0.key_off;
-  // quadrant scratch lives in the upper bytes of this level's gathered-key region of `lkeys`?
-  // no: use a dedicated byte view after knode's slots (total_slots*4 bytes per frame reserved).
-  uint8_t* kq = (uint8_t*)(knode_g + (size_t)gridDim.y * total_slots) +
-                (size_t)frame * total_slots + L0.key_off;
-  const uint32_t* fk = keys + (size_t)frame * total_slots;
-  // one thread per cell (a cell holds at most a few dozen survivors)
-  for (int ci = tid; ci < nc; ci += nt) {
-    const int m = cnt[ci], o = coff[ci], so = cells[L0.cell_begin + ci].slot_off;
-    for (int j = 0; j < m; j++) lk[o + j] = fk[so + j];
+// Gather of the level's FAST candidates in cell order (cells hold them row-major), then
+// DistributeOctTree (ORBextractor.cc:539-763) and the best key per node.
+template <typename KA>
+__device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo& L0,
+                                        const CellInfo* __restrict__ cells, const int* cnt,
+                                        int nc, const uint32_t* __restrict__ fk, int n,
+                                        uint32_t* __restrict__ outp, int* __restrict__ ocount_p,
+                                        int ncap, int* __restrict__ err) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  // thread per key: its cell is the last one whose offset is <= the key index
+  const lds_i32* coff = (const lds_i32*)S.cc;
+  for (int i = tid; i < n; i += nt) {
+    int lo = 0, hi = nc - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (coff[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    kk.lk[i] = fk[cells[L0.cell_begin + lo].slot_off + (i - coff[lo])];
   }
   __syncthreads();
-  uint32_t* outp = okeys + (size_t)frame * out_slots + L0.out_off;
-  if (n == 0) {
-    if (tid == 0) ocount[frame * nlevels + level] = 0;
-    return;
-  }
   // ---- initial nodes (ORBextractor.cc:552-585)
   const int nIni = L0.nIni;
   const float hX = L0.hX;
@@ -632,14 +707,14 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
   for (int i = tid; i < nIni; i += nt) S.cnt[0][i] = 0;
   __syncthreads();
   for (int i = tid; i < n; i += nt) {
-    const int idx = (int)((float)key_x(lk[i]) / hX);
-    knode[i] = (uint32_t)idx;
-    atomicAdd(&S.cnt[0][idx], 1u);
+    const int idx = (int)((float)key_x(kk.lk[i]) / hX);
+    kk.knode[i] = (uint16_t)idx;
+    atomicAdd((uint32_t*)&S.cnt[0][idx], 1u);
   }
   __syncthreads();
   for (int i = tid; i < nIni; i += nt) S.krank[i] = S.cnt[0][i] > 0 ? 1 : 0;
   __syncthreads();
-  int Lsz = wg_scan_excl(S.krank, nIni, s_tmp);
+  int Lsz = wg_scan_excl(S.krank, nIni, S.s_tmp);
   for (int i = tid; i < nIni; i += nt) {
     if (S.cnt[0][i] > 0) {
       const int s = S.krank[i];
@@ -652,7 +727,7 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
     }
   }
   __syncthreads();
-  for (int i = tid; i < n; i += nt) knode[i] = (uint32_t)S.krank[knode[i]];
+  for (int i = tid; i < n; i += nt) kk.knode[i] = (uint16_t)S.krank[kk.knode[i]];
   __syncthreads();
   int cur = 1;
   uint32_t seqBase = (uint32_t)nIni;
@@ -666,12 +741,12 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
       break;
     }
     const int prevSize = Lsz;
-    const int D = oct_expandable_in_order(S, cur, Lsz, s_tmp);
-    oct_pass(S, cur, Lsz, seqBase, D, 0, lk, knode, kq, n, s_tmp, s_ctl);
+    const int D = oct_expandable_in_order(S, cur, Lsz);
+    oct_pass(S, cur, Lsz, seqBase, D, 0, kk, n);
     // nToExpand = nodes with more than one key
     for (int s = tid; s < Lsz; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
     __syncthreads();
-    const int nToExpand = wg_scan_excl(S.gst, Lsz, s_tmp);
+    const int nToExpand = wg_scan_excl(S.gst, Lsz, S.s_tmp);
     if (Lsz >= N || Lsz == prevSize) {
       finish = true;
     } else if (Lsz + nToExpand * 3 > N) {
@@ -682,8 +757,8 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
           break;
         }
         const int prev2 = Lsz;
-        const int D2 = oct_expandable_sorted(S, cur, Lsz, ncap, s_tmp);
-        oct_pass(S, cur, Lsz, seqBase, D2, N, lk, knode, kq, n, s_tmp, s_ctl);
+        const int D2 = oct_expandable_sorted(S, cur, Lsz);
+        oct_pass(S, cur, Lsz, seqBase, D2, N, kk, n);
         if (Lsz >= N || Lsz == prev2) finish = true;
       }
     }
@@ -696,18 +771,92 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
   for (int s = tid; s < Lsz; s += nt) S.best[s] = 0;
   __syncthreads();
   for (int i = tid; i < n; i += nt)
-    atomicMax(&S.best[knode[i]], (key_s(lk[i]) << 24) | (0xFFFFFFu - (uint32_t)i));
+    atomicMax((uint32_t*)&S.best[kk.knode[i]], (key_s(kk.lk[i]) << 24) | (0xFFFFFFu - (uint32_t)i));
   __syncthreads();
   const int nout = min(Lsz, L0.out_cap);
   for (int s = tid; s < nout; s += nt) {
     const uint32_t i = 0xFFFFFFu - (S.best[s] & 0xFFFFFFu);
-    const uint32_t k = lk[i];
+    const uint32_t k = kk.lk[i];
     const uint32_t x = key_x(k) + kMinBorder, y = key_y(k) + kMinBorder;
     outp[s] = (y << 20) | (x << 8) | key_s(k);
   }
   if (tid == 0) {
-    ocount[frame * nlevels + level] = nout;
+    *ocount_p = nout;
     if (Lsz > L0.out_cap) atomicOr(err, 4);
+  }
+}
+
+// One workgroup per (level, frame).  Keys of the level live in LDS when at most kcap of them
+// survived FAST (the usual case), in global scratch otherwise.
+__global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ lv,
+                                                 const CellInfo* __restrict__ cells, int ncells,
+                                                 const uint32_t* __restrict__ keys,
+                                                 const int* __restrict__ cellcnt, int total_slots,
+                                                 uint32_t* __restrict__ lkeys,
+                                                 uint32_t* __restrict__ knode_g,
+                                                 uint32_t* __restrict__ okeys, int out_slots,
+                                                 int* __restrict__ ocount, int nlevels,
+                                                 int ncap, int kcap, int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_generic[];
+  LDS unsigned char* smem = (LDS unsigned char*)smem_generic;
+  const int level = blockIdx.x, frame = blockIdx.y;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const LevelInfo L0 = lv[level];
+  // ---- carve LDS (all offsets multiples of 16)
+  OctLDS S;
+  LDS unsigned char* p = smem;
+  auto carve = [&](size_t bytes) {
+    LDS unsigned char* r = p;
+    p += (bytes + 15) & ~(size_t)15;
+    return r;
+  };
+  for (int b = 0; b < 2; b++) {
+    S.x0[b] = (lds_u16*)carve(2 * ncap);
+    S.y0[b] = (lds_u16*)carve(2 * ncap);
+    S.x1[b] = (lds_u16*)carve(2 * ncap);
+    S.y1[b] = (lds_u16*)carve(2 * ncap);
+    S.cnt[b] = (lds_u32*)carve(4 * ncap);
+    S.seq[b] = (lds_u32*)carve(4 * ncap);
+  }
+  S.prank = (lds_i32*)carve(4 * ncap);
+  S.order = (lds_i32*)carve(4 * ncap);
+  S.gst = (lds_i32*)carve(4 * ncap);
+  S.cumnc = (lds_i32*)carve(4 * ncap);
+  S.krank = (lds_i32*)carve(4 * ncap);
+  S.cc = (lds_u32*)carve(16 * ncap);
+  S.sortkey = (lds_u64*)S.cc;
+  S.best = S.cc;
+  S.s_tmp = (lds_i32*)carve(4 * 20);
+  S.s_ctl = S.s_tmp + 17;
+  lds_u32* k_lk = (lds_u32*)carve(4 * kcap);
+  lds_u16* k_node = (lds_u16*)carve(2 * kcap);
+  lds_u8* k_q = (lds_u8*)carve(kcap);
+
+  // ---- cell offsets of this level's candidates
+  const int nc = L0.cell_end - L0.cell_begin;
+  const int* cnt = cellcnt + (size_t)frame * ncells + L0.cell_begin;
+  lds_i32* coff = (lds_i32*)S.cc;  // scratch (nc <= 4 * ncap checked on host)
+  for (int i = tid; i < nc; i += nt) coff[i] = cnt[i];
+  __syncthreads();
+  const int n = wg_scan_excl(coff, nc, S.s_tmp);
+  uint32_t* outp = okeys + (size_t)frame * out_slots + L0.out_off;
+  int* ocount_p = ocount + frame * nlevels + level;
+  if (n == 0) {
+    if (tid == 0) *ocount_p = 0;
+    return;
+  }
+  const uint32_t* fk = keys + (size_t)frame * total_slots;
+  if (n <= kcap) {
+    OctKeys<lds_u32*, lds_u16*, lds_u8*> kk{k_lk, k_node, k_q};
+    oct_run(S, kk, L0, cells, cnt, nc, fk, n, outp, ocount_p, ncap, err);
+  } else {
+    // global scratch: knode as u16 in the u32 slots, quadrant bytes after all frames' knode
+    uint32_t* lk = lkeys + (size_t)frame * total_slots + L0.key_off;
+    uint16_t* knode = (uint16_t*)(knode_g + (size_t)frame * total_slots + L0.key_off);
+    uint8_t* kq = (uint8_t*)(knode_g + (size_t)gridDim.y * total_slots) +
+                  (size_t)frame * total_slots + L0.key_off;
+    OctKeys<uint32_t*, uint16_t*, uint8_t*> kk{lk, knode, kq};
+    oct_run(S, kk, L0, cells, cnt, nc, fk, n, outp, ocount_p, ncap, err);
   }
 }
 
@@ -975,13 +1124,6 @@ __global__ __launch_bounds__(256) void k_orient_desc(
 
 // ======================================================================== host engine
 
-static size_t octree_lds_bytes(int ncap) {
-  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-  size_t b = 0;
-  for (int i = 0; i < 2; i++) b += 4 * r16(2 * ncap) + 2 * r16(4 * ncap);
-  b += 5 * r16(4 * ncap) + r16(16 * ncap);
-  return b;
-}
 
 OrbEngine::~OrbEngine() { release(); }
 
@@ -1018,12 +1160,14 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   minTh_ = t.minTh;
   lv_.assign(nlevels_, LevelInfo());
   cells_.clear();
-  fast_tile_max_ = fast_win_max_ = 0;
+  fast_rows_max_ = fast_cols_max_ = fast_win_max_ = 0;
   int off = 0, key_off = 0, out_off = 0, maxN = 0;
   std::vector<ResizeX> xt;
   std::vector<ResizeY> yt;
   xtab_off_.assign(nlevels_, 0);
   ytab_off_.assign(nlevels_, 0);
+  rs_pitch_.assign(nlevels_, 0);
+  rs_lds_.assign(nlevels_, 0);
   std::vector<BlurTile> tiles;
   for (int l = 0; l < nlevels_; l++) {
     LevelInfo& L = lv_[l];
@@ -1056,9 +1200,10 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
         c.c0 = (int)iniX;
         c.rows = (int)maxY - (int)iniY;
         c.cols = (int)maxX - (int)iniX;
-        if (c.rows * ((c.cols + 3) & ~3) > FAST_TILE_MAX || (c.rows - 6) * (c.cols - 6) > FAST_WIN_MAX)
+        if (c.rows > kFSMax || ((c.cols + 3) & ~3) > kFSMax || c.cols - 6 > 64)
           throw ArgError("FAST cell larger than the LDS tile");
-        fast_tile_max_ = std::max(fast_tile_max_, c.rows * ((c.cols + 3) & ~3));
+        fast_rows_max_ = std::max(fast_rows_max_, c.rows);
+        fast_cols_max_ = std::max(fast_cols_max_, (c.cols + 3) & ~3);
         fast_win_max_ = std::max(fast_win_max_, std::max(c.rows - 6, 0) * std::max(c.cols - 6, 0));
         const int R = std::max(c.rows - 6, 0), C = std::max(c.cols - 6, 0);
         c.slot_cap = ((R + 1) / 2) * ((C + 1) / 2);  // max strict-NMS survivors
@@ -1119,6 +1264,22 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
         r.b1 = (short)std::min(std::max(host_round(fy * 2048), -32768), 32767);
         yt.push_back(r);
       }
+      // k_resize staging window: widest column block, tallest row band
+      int pitch = 0, rows = 0;
+      const ResizeX* X = xt.data() + xtab_off_[l];
+      const ResizeY* Y = yt.data() + ytab_off_[l];
+      for (int dx0 = 0; dx0 < dw; dx0 += kResizeCols) {
+        const int dx1 = std::min(dx0 + kResizeCols, dw);
+        const int lo = X[dx0].sx, hi = std::min(X[dx1 - 1].sx + 1, sw - 1);
+        pitch = std::max(pitch, 4 * ((hi - lo + 4) >> 2) + 4);
+      }
+      for (int y0 = 0; y0 < dh; y0 += kResizeRows) {
+        const int y1 = std::min(y0 + kResizeRows, dh);
+        rows = std::max(rows, Y[y1 - 1].sy1 - Y[y0].sy0 + 1);
+      }
+      rs_pitch_[l] = pitch;
+      rs_lds_[l] = pitch * rows;
+      if (rs_lds_[l] > 64 * 1024) throw ArgError("resize staging window exceeds 64 KB of LDS");
     }
     for (int y0 = 0; y0 < L.h; y0 += kBlurBand)
       for (int x0 = 0; x0 < L.w; x0 += 256) tiles.push_back(BlurTile{l, x0, y0, 0});
@@ -1136,8 +1297,20 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
     if (L.nIni > node_cap_) throw ArgError("too many initial octree nodes");
   }
   if (node_cap_ > 2048) throw ArgError("ORB nfeatures too large for the LDS octree (max ~9000)");
+  for (int fs : {kFSSmall, kFSMax}) {
+    const int lds = 4 * fast_wave_lds(fs, fast_rows_max_, fast_win_max_);
+    if (lds > 160 * 1024) throw ArgError("FAST cells too large for LDS");
+    MMT_HIP(hipFuncSetAttribute(fs == kFSSmall ? (const void*)k_fast<kFSSmall> : (const void*)k_fast<kFSMax>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  }
+  // keys in LDS up to what the node arrays leave of the CU's 160 KB (global scratch beyond)
+  const size_t node_lds = octree_node_lds_bytes(node_cap_);
+  const size_t lds_budget = 160 * 1024 - 1024;
+  key_cap_ = node_lds + octree_key_lds_bytes(256) <= lds_budget
+                 ? (int)std::min<size_t>(16384, (lds_budget - node_lds - 16) / 7) : 0;
+  octree_lds_ = node_lds + octree_key_lds_bytes(key_cap_);
   MMT_HIP(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)octree_lds_bytes(node_cap_)));
+                               (int)octree_lds_));
   upload(&d_lv_, lv_);
   upload(&d_cells_, cells_);
   upload(&d_xtab_, xt);
@@ -1164,23 +1337,28 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
   if (cap_per_frame < cap_frame_) throw ArgError("cap_per_frame below mmt_orb_capacity()");
   const size_t lvl0 = (size_t)w_ * h_;
   // level 0: copy the gray frames into the pyramid buffer
-  MMT_HIP(hipMemcpy2DAsync(d_pyr_, pyr_stride_, d_gray, frame_pitch, lvl0, nframes,
-                           hipMemcpyDeviceToDevice, stream));
+  if (d_gray != d_pyr_ || frame_pitch != pyr_stride_)
+    MMT_HIP(hipMemcpy2DAsync(d_pyr_, pyr_stride_, d_gray, frame_pitch, lvl0, nframes,
+                             hipMemcpyDeviceToDevice, stream));
   for (int l = 1; l < nlevels_; l++) {
     const LevelInfo& S = lv_[l - 1];
     const LevelInfo& L = lv_[l];
-    dim3 grid((L.w + 255) / 256, (L.h + kResizeRows - 1) / kResizeRows, nframes);
-    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, d_pyr_, pyr_stride_, S.off, S.w,
-                       L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l]);
+    dim3 grid((L.w + kResizeCols - 1) / kResizeCols, (L.h + kResizeRows - 1) / kResizeRows,
+              nframes);
+    hipLaunchKernelGGL(k_resize, grid, dim3(256), rs_lds_[l], stream, d_pyr_, pyr_stride_, S.off,
+                       S.w, L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l],
+                       rs_pitch_[l]);
   }
-  const int fast_per_wave = (fast_tile_max_ + 4 * fast_win_max_ + 31) & ~15;
-  hipLaunchKernelGGL(k_fast, dim3((ncells_ + 3) / 4, nframes), dim3(256), 4 * fast_per_wave, stream,
-                     d_pyr_, pyr_stride_, d_lv_, d_cells_, ncells_, d_keys_, total_slots_,
-                     d_cellcnt_, iniTh_, minTh_, fast_tile_max_, fast_win_max_);
-  const size_t lds = octree_lds_bytes(node_cap_);
+  const int fs = fast_cols_max_ <= kFSSmall ? kFSSmall : kFSMax;
+  hipLaunchKernelGGL(fs == kFSSmall ? k_fast<kFSSmall> : k_fast<kFSMax>,
+                     dim3((ncells_ + 3) / 4, nframes), dim3(256),
+                     4 * fast_wave_lds(fs, fast_rows_max_, fast_win_max_), stream, d_pyr_,
+                     pyr_stride_, d_lv_, d_cells_, ncells_, d_keys_, total_slots_, d_cellcnt_,
+                     iniTh_, minTh_, fast_rows_max_, fast_win_max_);
+  const size_t lds = octree_lds_;
   hipLaunchKernelGGL(k_octree, dim3(nlevels_, nframes), dim3(1024), lds, stream, d_lv_, d_cells_,
                      ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,
-                     out_slots_, d_ocount_, nlevels_, node_cap_, d_err_);
+                     out_slots_, d_ocount_, nlevels_, node_cap_, key_cap_, d_err_);
   hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, stream, d_pyr_,
                      d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
   const int waves = (nframes * out_slots_ + 3) / 4;

@@ -19,18 +19,40 @@
 namespace mmt {
 
 // ------------------------------------------------------------------ frame preparation
+__device__ __forceinline__ void gray_depth_px(const uint8_t* c, uint16_t d, float bf, uint8_t* g,
+                                              float* z) {
+  *g = (uint8_t)((c[0] * 4899 + c[1] * 9617 + c[2] * 1868 + (1 << 13)) >> 14);
+  const float dp = (float)((float)d / 256.0);
+  *z = bf / dp;
+}
+
+// Four pixels per thread: 12 BGR bytes and four u16 disparities in, one gray dword and four
+// depths out (unaligned vector accesses: frame pitches need not be multiples of 4).
 __global__ __launch_bounds__(256) void k_gray_depth(const uint8_t* __restrict__ bgr, size_t bgr_pitch,
                                                     const uint16_t* __restrict__ disp,
                                                     size_t disp_pitch, uint8_t* __restrict__ gray,
                                                     size_t gray_pitch, float* __restrict__ depth,
                                                     size_t depth_pitch, int npix, float bf) {
   const int f = blockIdx.y;
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < npix; p += gridDim.x * 256) {
-    const uint8_t* c = bgr + f * bgr_pitch + 3 * (size_t)p;
-    gray[f * gray_pitch + p] = (uint8_t)((c[0] * 4899 + c[1] * 9617 + c[2] * 1868 + (1 << 13)) >> 14);
-    const float dp = (float)((float)disp[f * disp_pitch + p] / 256.0);
-    depth[f * depth_pitch + p] = bf / dp;
+  const uint8_t* B = bgr + f * bgr_pitch;
+  const uint16_t* D = disp + f * disp_pitch;
+  uint8_t* G = gray + f * gray_pitch;
+  float* Z = depth + f * depth_pitch;
+  const int nq = npix >> 2;
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
+    uint8_t c[12];
+    __builtin_memcpy(c, B + 12 * (size_t)q, 12);
+    uint16_t d[4];
+    __builtin_memcpy(d, D + 4 * (size_t)q, 8);
+    uint8_t g[4];
+    float z[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) gray_depth_px(c + 3 * k, d[k], bf, g + k, z + k);
+    __builtin_memcpy(G + 4 * (size_t)q, g, 4);
+    __builtin_memcpy(Z + 4 * (size_t)q, z, 16);
   }
+  const int p = 4 * nq + blockIdx.x * 256 + threadIdx.x;
+  if (p < npix) gray_depth_px(B + 3 * (size_t)p, D[p], bf, G + p, Z + p);
 }
 
 // order-preserving workgroup compaction helper: returns this lane's slot (or -1) and advances
@@ -359,7 +381,7 @@ __global__ __launch_bounds__(1024) void k_obj_group(GroupArgs a) {
 void launch_gray_depth(const uint8_t* bgr, size_t bgr_pitch, const uint16_t* disp,
                        size_t disp_pitch, uint8_t* gray, size_t gray_pitch, float* depth,
                        size_t depth_pitch, int npix, int nframes, float bf, hipStream_t st) {
-  const int blocks = std::min((npix + 255) / 256, 2048);
+  const int blocks = std::max(1, std::min((npix / 4 + 255) / 256, 2048));
   hipLaunchKernelGGL(k_gray_depth, dim3(blocks, nframes), dim3(256), 0, st, bgr, bgr_pitch, disp,
                      disp_pitch, gray, gray_pitch, depth, depth_pitch, npix, bf);
 }

@@ -186,7 +186,6 @@ class Tracker {
   const std::vector<int>& cached_subsets(int count);
   hipStream_t oa_ = nullptr, ob_ = nullptr;
   std::vector<void*> allocs_;
-  uint8_t* d_gray_ = nullptr;
   float* d_depth_ = nullptr;
   mmt_kp* d_kps_ = nullptr;
   uint8_t* d_desc_ = nullptr;

@@ -168,7 +168,6 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   kcap_ = engine->capacity();
   ocap_ = ((W_ + 3) / 4) * ((H_ + 3) / 4);
   const size_t npix = (size_t)W_ * H_;
-  d_gray_ = alloc<uint8_t>(npix * max_chunk);
   d_depth_ = alloc<float>(npix * max_chunk);
   d_kps_ = alloc<mmt_kp>((size_t)kcap_ * max_chunk);
   d_desc_ = alloc<uint8_t>((size_t)kcap_ * 32 * max_chunk);
@@ -290,10 +289,13 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   if (nframes < 1 || nframes > max_chunk_) throw ArgError("chunk size outside [1, max_batch]");
   const size_t npix = (size_t)W_ * H_;
   // ---- per-frame preparation and batched ORB extraction for the whole chunk
-  launch_gray_depth(d_bgr, bgr_pitch, d_disp, disp_pitch / sizeof(uint16_t), d_gray_, npix,
+  // gray goes straight into level 0 of the ORB pyramid (no staging copy)
+  uint8_t* gray = engine_->level0();
+  const size_t gpitch = engine_->pyramid_stride();
+  launch_gray_depth(d_bgr, bgr_pitch, d_disp, disp_pitch / sizeof(uint16_t), gray, gpitch,
                     d_depth_, npix, (int)npix, nframes, cfg_.bf, st);
   if (prof_) MMT_HIP(hipEventRecord(ev_orb_[0], st));
-  engine_->run(d_gray_, nframes, npix, d_kps_, d_desc_, kcap_, d_nkp_, st);
+  engine_->run(gray, nframes, gpitch, d_kps_, d_desc_, kcap_, d_nkp_, st);
   if (prof_) MMT_HIP(hipEventRecord(ev_orb_[1], st));
   std::vector<int> nkp(nframes);
   MMT_HIP(hipMemcpyAsync(nkp.data(), d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));

@@ -16,9 +16,15 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 W, H, NF = 1242, 375, 2000
 dev = torch.device("cuda:0")
-seq = scene.kitti_like_sequence(B, W, H, n_objects=3, seed=1003, device=dev)
-gray = (seq["bgr"].to(torch.int32) * torch.tensor([4899, 9617, 1868], device=dev)).sum(-1)
-gray = ((gray + 8192) >> 14).to(torch.uint8).contiguous()
+if os.environ.get("ORB_MB_SCENE") == "synthetic":
+    seq = scene.kitti_like_sequence(B, W, H, n_objects=3, seed=1003, device=dev)
+    bgr = seq["bgr"].cpu().numpy()
+else:  # the reference's kitti_sample frames, cycled (few host-side ops: cheap under --pmc)
+    KITTI = os.path.join(ROOT, "tests", "golden", "kitti_sample")
+    fr = [np.load(os.path.join(KITTI, "frame_%06d.npz" % i))["bgr"] for i in range(5)]
+    bgr = np.stack([fr[i % 5] for i in range(B)])
+g = (bgr.astype(np.int32) * np.array([4899, 9617, 1868], np.int32)).sum(-1)
+gray = torch.from_numpy(((g + 8192) >> 14).astype(np.uint8)).to(dev).contiguous()
 ctx = M.Context(M.kitti03_config(W, H, NF, max_batch=B))
 cap = ctx.capacity()
 kps = torch.empty((B, cap * 28), dtype=torch.uint8, device=dev)
