@@ -97,6 +97,8 @@ class OrbEngine {
   int total_slots_ = 0, out_slots_ = 0, cap_frame_ = 0, node_cap_ = 0;
   int key_cap_ = 0;          // k_octree: keys per (level, frame) held in LDS
   size_t octree_lds_ = 0;    // k_octree dynamic LDS bytes
+  hipStream_t side_ = nullptr;  // k_blur runs here, overlapping FAST + octree
+  hipEvent_t ev_pyr_ = nullptr, ev_blur_ = nullptr, ev_gray_ = nullptr, ev_fast0_ = nullptr;
   int iniTh_ = 20, minTh_ = 7;
   size_t pyr_stride_ = 0;
   std::vector<LevelInfo> lv_;

@@ -290,11 +290,12 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
                                               const CellInfo* __restrict__ cells, int ncells,
                                               uint32_t* __restrict__ keys, int total_slots,
                                               int* __restrict__ cellcnt, int iniTh, int minTh,
-                                              int rows_max, int win_max) {
+                                              int rows_max, int win_max, int cell_begin,
+                                              int cell_end) {
   extern __shared__ __attribute__((aligned(16))) uint8_t fast_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int cell = blockIdx.x * 4 + wave;
-  if (cell >= ncells) return;
+  const int cell = cell_begin + blockIdx.x * 4 + wave;
+  if (cell >= cell_end) return;
   uint8_t* tile = fast_lds + wave * fast_wave_lds(kFS, rows_max, win_max);
   uint8_t* arcm = tile + rows_max * kFS;
   uint16_t* cand_list = (uint16_t*)(arcm + rows_max * kFS);
@@ -903,23 +904,32 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
   const int y_end = min(t.y0 + kBlurBand, L.h);
   const int ncols = min(4, L.w - x);
   const bool edge = x < 4 || x + 8 > L.w;  // the 12 loaded bytes x-4 .. x+7 leave the row
-  int cx[12];
+  // Every lane loads three dwords at `base`; edge lanes then pick their REFLECT_101 bytes out of
+  // those 12 with v_perm (all reflected positions lie inside [base, base + 12)).
+  const int base = min(max(x - 4, 0), max(L.w - 12, 0));
+  uint32_t selA[3] = {0, 0, 0}, selB[3] = {0, 0, 0};
+  if (edge) {
 #pragma unroll
-  for (int k = 0; k < 12; k++) cx[k] = reflect101(min(max(x - 4 + k, -4), L.w + 3), L.w);
+    for (int k = 0; k < 12; k++) {
+      const int sidx = reflect101(min(max(x - 4 + k, -4), L.w + 3), L.w) - base;  // 0..11
+      const uint32_t a = sidx < 8 ? (uint32_t)sidx : 0x0cu;
+      const uint32_t b = sidx >= 8 ? (uint32_t)(sidx - 8) : 0x0cu;
+      selA[k >> 2] |= a << (8 * (k & 3));
+      selB[k >> 2] |= b << (8 * (k & 3));
+    }
+  }
   auto load_row = [&](int r, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
     const int sy = reflect101(min(r, L.h + 2), L.h);
-    const uint8_t* srow = img + (size_t)sy * L.w;
+    const uint8_t* srow = img + (size_t)sy * L.w + base;
+    const uint32_t s0 = ld32(srow), s1 = ld32(srow + 4), s2 = ld32(srow + 8);
     if (!edge) {
-      d0 = ld32(srow + x - 4);
-      d1 = ld32(srow + x);
-      d2 = ld32(srow + x + 4);
+      d0 = s0;
+      d1 = s1;
+      d2 = s2;
     } else {
-      uint32_t b[12];
-#pragma unroll
-      for (int k = 0; k < 12; k++) b[k] = srow[cx[k]];
-      d0 = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-      d1 = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
-      d2 = b[8] | (b[9] << 8) | (b[10] << 16) | (b[11] << 24);
+      d0 = __builtin_amdgcn_perm(s1, s0, selA[0]) | __builtin_amdgcn_perm(s2, s2, selB[0]);
+      d1 = __builtin_amdgcn_perm(s1, s0, selA[1]) | __builtin_amdgcn_perm(s2, s2, selB[1]);
+      d2 = __builtin_amdgcn_perm(s1, s0, selA[2]) | __builtin_amdgcn_perm(s2, s2, selB[2]);
     }
   };
   uint32_t w[7][4];
@@ -1141,6 +1151,14 @@ void OrbEngine::release() {
   d_pyr_ = d_blur_ = nullptr;
   d_keys_ = d_lkeys_ = d_knode_ = d_okeys_ = nullptr;
   d_cellcnt_ = d_ocount_ = d_err_ = nullptr;
+  if (ev_pyr_) (void)hipEventDestroy(ev_pyr_);
+  if (ev_blur_) (void)hipEventDestroy(ev_blur_);
+  if (ev_gray_) (void)hipEventDestroy(ev_gray_);
+  if (ev_fast0_) (void)hipEventDestroy(ev_fast0_);
+  ev_gray_ = ev_fast0_ = nullptr;
+  if (side_) (void)hipStreamDestroy(side_);
+  ev_pyr_ = ev_blur_ = nullptr;
+  side_ = nullptr;
 }
 
 template <typename T>
@@ -1328,6 +1346,11 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   MMT_HIP(hipMalloc((void**)&d_okeys_, B * out_slots_ * sizeof(uint32_t)));
   MMT_HIP(hipMalloc((void**)&d_ocount_, B * nlevels_ * sizeof(int)));
   MMT_HIP(hipMalloc((void**)&d_err_, sizeof(int)));
+  MMT_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  MMT_HIP(hipEventCreateWithFlags(&ev_pyr_, hipEventDisableTiming));
+  MMT_HIP(hipEventCreateWithFlags(&ev_blur_, hipEventDisableTiming));
+  MMT_HIP(hipEventCreateWithFlags(&ev_gray_, hipEventDisableTiming));
+  MMT_HIP(hipEventCreateWithFlags(&ev_fast0_, hipEventDisableTiming));
   MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
 }
 
@@ -1340,6 +1363,21 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
   if (d_gray != d_pyr_ || frame_pitch != pyr_stride_)
     MMT_HIP(hipMemcpy2DAsync(d_pyr_, pyr_stride_, d_gray, frame_pitch, lvl0, nframes,
                              hipMemcpyDeviceToDevice, stream));
+  // FAST on level 0 needs only the gray frames: it runs on the side stream while the main stream
+  // walks the (latency-bound) resize chain; FAST on levels 1.. follows the chain
+  const int fs = fast_cols_max_ <= kFSSmall ? kFSSmall : kFSMax;
+  const int fast_lds = 4 * fast_wave_lds(fs, fast_rows_max_, fast_win_max_);
+  auto fast = [&](int c0, int c1, hipStream_t st) {
+    if (c1 <= c0) return;
+    hipLaunchKernelGGL(fs == kFSSmall ? k_fast<kFSSmall> : k_fast<kFSMax>,
+                       dim3((c1 - c0 + 3) / 4, nframes), dim3(256), fast_lds, st, d_pyr_,
+                       pyr_stride_, d_lv_, d_cells_, ncells_, d_keys_, total_slots_, d_cellcnt_,
+                       iniTh_, minTh_, fast_rows_max_, fast_win_max_, c0, c1);
+  };
+  MMT_HIP(hipEventRecord(ev_gray_, stream));
+  MMT_HIP(hipStreamWaitEvent(side_, ev_gray_, 0));
+  fast(lv_[0].cell_begin, lv_[0].cell_end, side_);
+  MMT_HIP(hipEventRecord(ev_fast0_, side_));
   for (int l = 1; l < nlevels_; l++) {
     const LevelInfo& S = lv_[l - 1];
     const LevelInfo& L = lv_[l];
@@ -1349,18 +1387,21 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
                        S.w, L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l],
                        rs_pitch_[l]);
   }
-  const int fs = fast_cols_max_ <= kFSSmall ? kFSSmall : kFSMax;
-  hipLaunchKernelGGL(fs == kFSSmall ? k_fast<kFSSmall> : k_fast<kFSMax>,
-                     dim3((ncells_ + 3) / 4, nframes), dim3(256),
-                     4 * fast_wave_lds(fs, fast_rows_max_, fast_win_max_), stream, d_pyr_,
-                     pyr_stride_, d_lv_, d_cells_, ncells_, d_keys_, total_slots_, d_cellcnt_,
-                     iniTh_, minTh_, fast_rows_max_, fast_win_max_);
+  // the Gaussian blur needs only the pyramid: it follows level-0 FAST on the side stream,
+  // concurrently with FAST on levels 1.. and the octree (one latency-bound workgroup per CU
+  // leaves most wave slots idle), and joins before orientation
+  MMT_HIP(hipEventRecord(ev_pyr_, stream));
+  MMT_HIP(hipStreamWaitEvent(side_, ev_pyr_, 0));
+  hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, side_, d_pyr_,
+                     d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
+  MMT_HIP(hipEventRecord(ev_blur_, side_));
+  fast(lv_[0].cell_end, ncells_, stream);
+  MMT_HIP(hipStreamWaitEvent(stream, ev_fast0_, 0));
   const size_t lds = octree_lds_;
   hipLaunchKernelGGL(k_octree, dim3(nlevels_, nframes), dim3(1024), lds, stream, d_lv_, d_cells_,
                      ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,
                      out_slots_, d_ocount_, nlevels_, node_cap_, key_cap_, d_err_);
-  hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, stream, d_pyr_,
-                     d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
+  MMT_HIP(hipStreamWaitEvent(stream, ev_blur_, 0));
   const int waves = (nframes * out_slots_ + 3) / 4;
   hipLaunchKernelGGL(k_orient_desc, dim3((waves + 3) / 4), dim3(256), 0, stream, d_pyr_, d_blur_,
                      pyr_stride_, d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_,
