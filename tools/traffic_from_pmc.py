@@ -16,16 +16,26 @@ ORB = ("k_resize", "k_fast", "k_octree", "k_blur", "k_orient_desc")
 
 
 def load(d, counter):
-    f = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True),
-               key=os.path.getmtime)[-1]
+    files = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True),
+                   key=os.path.getmtime)
+    if files:
+        recs = [(r["Kernel_Name"], r["Counter_Name"], float(r["Counter_Value"]), r["Dispatch_Id"])
+                for r in csv.DictReader(open(files[-1]))]
+    else:  # rocprofv3 writing a results database
+        import sqlite3
+        db = sorted(glob.glob(os.path.join(d, "**", "*.db"), recursive=True),
+                    key=os.path.getmtime)[-1]
+        recs = list(sqlite3.connect(db).execute(
+            "select kernel_name, counter_name, value, dispatch_id from counters_collection"))
     tot = collections.defaultdict(float)
     n = collections.defaultdict(set)
-    for r in csv.DictReader(open(f)):
-        if r["Counter_Name"] != counter:
+    for kn, cn, val, did in recs:
+        if cn != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("mmt::", "")
-        tot[name] += float(r["Counter_Value"])
-        n[name].add(r["Dispatch_Id"])
+        # "void mmt::k_fast<40>(...)" -> "k_fast"
+        name = kn.split("(")[0].replace("void ", "").replace("mmt::", "").split("<")[0]
+        tot[name] += float(val)
+        n[name].add(did)
     return tot, n
 
 
