@@ -15,9 +15,10 @@ Multi-GPU: one process per GPU (torchrun), independent sequences, no data-path c
 barrier + device sync bracket the timed region; time = MAX over ranks; value = frames of all
 ranks / that time ("scaling": "weak").
 
-roofline: the batched ORB launch sequence (B_orb = 3WH + 4P + 60N algorithmic bytes
-per frame x frames per launch) / its average duration from HIP events the library records on the
-launch stream around every ORB launch sequence (mmt_profile_*), vs the 8 TB/s HBM peak.
+roofline: the batched ORB window -- k_gray_depth (A1 + A2) and the ORB launch sequence (A3-A9) --
+with SURVEY 8(d)'s B_orb = 3WH + 4P + 60N plus A2's 6WH algorithmic bytes per frame x frames per
+launch, over its average duration from HIP events the library records on the launch stream around
+every window (mmt_profile_*), vs the 8 TB/s HBM peak.
 cpu_baseline: the CPU oracle tracker (oracle/track_ref.cpp, a scalar C++ restatement of the
 reference's per-frame path) on rank 0 over the first frames of the same sequence, 1 core.
 """
@@ -37,8 +38,11 @@ METRIC = "KITTI RGB-D frames/sec (ego+object poses) at 1/2/4/8 GPUs; CPU ref fps
 
 
 def b_orb(w, h, nfeat, lw, lh):
+    """Algorithmic bytes per frame of the profiled ORB window: SURVEY 8(d)'s B_orb = 3WH (BGR
+    read, A1) + 4P (pyramid write + read, blurred write + read) + 60N (keypoints + descriptors),
+    plus 6WH for A2, which the same fused kernel does (u16 disparity in, f32 depth out)."""
     P = int(sum(int(a) * int(b) for a, b in zip(lw, lh)))
-    return 3 * w * h + 4 * P + 60 * nfeat
+    return 3 * w * h + 4 * P + 60 * nfeat + 6 * w * h
 
 
 def load_traffic(path, cfg_key):
@@ -163,8 +167,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
-                         "kernel": "batched ORB launch sequence (k_resize, k_fast, k_octree, "
-                                   "k_blur, k_orient_desc) over %d frames" % C,
+                         "kernel": "batched ORB window (k_gray_depth, k_resize, k_fast, "
+                                   "k_octree, k_blur, k_orient_desc) over %d frames" % C,
                          "launch_ms": round(launch_ms, 4), "bytes_per_launch": bytes_per_launch,
                          "orb_share_of_step": round(prof["orb_ms"] / (elapsed * 1e3), 4)},
             "cpu_baseline": cpu,

@@ -289,12 +289,13 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   if (nframes < 1 || nframes > max_chunk_) throw ArgError("chunk size outside [1, max_batch]");
   const size_t npix = (size_t)W_ * H_;
   // ---- per-frame preparation and batched ORB extraction for the whole chunk
-  // gray goes straight into level 0 of the ORB pyramid (no staging copy)
+  // A1 + A2 (gray straight into level 0 of the ORB pyramid, depth) and A3-A9: the profiled ORB
+  // window (mmt_profile_*) covers both
+  if (prof_) MMT_HIP(hipEventRecord(ev_orb_[0], st));
   uint8_t* gray = engine_->level0();
   const size_t gpitch = engine_->pyramid_stride();
   launch_gray_depth(d_bgr, bgr_pitch, d_disp, disp_pitch / sizeof(uint16_t), gray, gpitch,
                     d_depth_, npix, (int)npix, nframes, cfg_.bf, st);
-  if (prof_) MMT_HIP(hipEventRecord(ev_orb_[0], st));
   engine_->run(gray, nframes, gpitch, d_kps_, d_desc_, kcap_, d_nkp_, st);
   if (prof_) MMT_HIP(hipEventRecord(ev_orb_[1], st));
   std::vector<int> nkp(nframes);

@@ -1,10 +1,13 @@
-"""HBM traffic of one batched ORB launch sequence from two rocprofv3 --pmc passes (FETCH_SIZE and
-WRITE_SIZE cannot share a pass on gfx950), for profiles/traffic.json (bench.py roofline.traffic).
+"""HBM traffic of one batched ORB window (k_gray_depth + the ORB launch sequence) from two
+rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950), for
+profiles/traffic.json (bench.py roofline.traffic).
 
 Usage: traffic_from_pmc.py <fetch_dir> <write_dir> <launches> <key> [json_out]
-Counter values are KB per dispatch (rocprofv3).  The guide's x2 FETCH_SIZE correction is for
-16-byte-per-lane streaming reads; the ORB kernels read 1-4 bytes per lane, so it is not applied
-(the calibration against k_resize's known read bytes is printed instead)."""
+Counter values are KB per dispatch (rocprofv3), KB = 1024 B.  gfx950 correction
+(MI355X_MICROARCH.md, HBM): FETCH_SIZE reports half the bytes of coalesced streaming reads, so it
+is doubled; calibrated here on k_gray_depth, whose reads are known exactly (5 B per pixel: BGR +
+u16 disparity, read once), and printed.  WRITE_SIZE is taken as is (k_gray_depth's known 5 B per
+pixel of writes calibrate it too)."""
 import collections
 import csv
 import glob
@@ -12,7 +15,7 @@ import json
 import os
 import sys
 
-ORB = ("k_resize", "k_fast", "k_octree", "k_blur", "k_orient_desc")
+ORB = ("k_gray_depth", "k_resize", "k_fast", "k_octree", "k_blur", "k_orient_desc")
 
 
 def load(d, counter):
@@ -45,17 +48,30 @@ fetch, nf = load(fd, "FETCH_SIZE")
 write, nw = load(wd, "WRITE_SIZE")
 total = 0.0
 print("kernel            dispatches  FETCH_KB/launch  WRITE_KB/launch")
+raw = 0.0
 for k in ORB:
     fk = fetch.get(k, 0.0) / launches
     wk = write.get(k, 0.0) / launches
-    total += (fk + wk) * 1024
+    raw += (fk + wk) * 1024
+    total += (2 * fk + wk) * 1024
     print("%-16s %10d %16.1f %16.1f" % (k, len(nf.get(k, ())), fk, wk))
-print("ORB launch sequence traffic: %.0f bytes (%.1f MB)" % (total, total / 1e6))
+W, H, B = 1242, 375, 32  # key 1242x375_n2000_b32
+known = 5.0 * W * H * B
+print("calibration k_gray_depth: known reads %.1f MB, FETCH_SIZE %.1f MB (x%.2f); known writes "
+      "%.1f MB, WRITE_SIZE %.1f MB" % (known / 1e6, fetch.get("k_gray_depth", 0) / launches *
+                                       1024 / 1e6, known / max(fetch.get("k_gray_depth", 0) /
+                                                               launches * 1024, 1),
+                                       known / 1e6, write.get("k_gray_depth", 0) / launches *
+                                       1024 / 1e6))
+print("ORB window traffic: raw FETCH+WRITE %.1f MB; corrected 2*FETCH+WRITE %.0f bytes (%.1f MB)"
+      % (raw / 1e6, total, total / 1e6))
 if out:
     d = {}
     if os.path.exists(out):
         d = json.load(open(out))
     d[key] = int(total)
-    d["_note"] = ("HBM-side bytes (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes, KB -> B) "
-                  "summed over the ORB kernels of one batched launch sequence; see DESIGN.md")
+    d["_note"] = ("HBM-side bytes (rocprofv3 2 x FETCH_SIZE + WRITE_SIZE, separate passes, KB -> B, "
+                  "gfx950 FETCH correction calibrated on k_gray_depth) "
+                  "summed over the kernels of one batched ORB window (k_gray_depth + the ORB "
+                  "launch sequence; tools/orb_traffic.sh); see DESIGN.md")
     json.dump(d, open(out, "w"), indent=1, sort_keys=True)
