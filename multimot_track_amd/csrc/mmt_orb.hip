@@ -421,40 +421,50 @@ typedef LDS int lds_i32;
 typedef LDS uint8_t lds_u8;
 typedef LDS unsigned long long lds_u64;
 
-// In-place exclusive scan of LDS ints a[0..n) by the whole workgroup; returns the total.
-__device__ int wg_scan_excl(lds_i32* a, int n, lds_i32* s_tmp /*[17]*/) {
+// Inclusive prefix sum over the 64 lanes of a wave with DPP (row shifts within rows of 16, then
+// the row broadcasts of GFX9): no LDS round trips.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// In-place exclusive scan of LDS ints a[0..n) by the whole workgroup; returns the total.  One
+// barrier: wave totals go to one of two alternating LDS slots, every thread sums the ones before
+// its wave.  Afterwards each thread has rewritten only its own items (the contiguous chunk
+// [tid * per, tid * per + per)); with per == 1 these are the items a loop "for (i = tid; i < n;
+// i += blockDim.x)" visits, so such a loop may read them without a barrier.  sync_after adds
+// the barrier for callers that read other threads' items.
+__device__ int wg_scan_excl(lds_i32* a, int n, lds_i32* s_tmp /*[2 * 16]*/, int& pp,
+                            bool sync_after) {
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
+  const int nw = nt >> 6;
   const int per = (n + nt - 1) / nt;
   const int b = min(tid * per, n), e = min(b + per, n);
   int local = 0;
   for (int i = b; i < e; i++) local += a[i];
-  int incl = local;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) s_tmp[wave] = incl;
+  const int incl = wave_incl_scan(local);
+  lds_i32* slot = s_tmp + 16 * pp;
+  pp ^= 1;
+  if (lane == 63) slot[wave] = incl;
   __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    const int nw = nt >> 6;
-    for (int w = 0; w < nw; w++) {
-      const int t = s_tmp[w];
-      s_tmp[w] = acc;
-      acc += t;
-    }
-    s_tmp[16] = acc;
+  int before = 0, total = 0;
+  for (int w = 0; w < nw; w++) {
+    const int t = slot[w];
+    before += w < wave ? t : 0;
+    total += t;
   }
-  __syncthreads();
-  int run = s_tmp[wave] + incl - local;
+  int run = before + incl - local;
   for (int i = b; i < e; i++) {
     const int t = a[i];
     a[i] = run;
     run += t;
   }
-  const int total = s_tmp[16];
-  __syncthreads();
+  if (sync_after || per > 1) __syncthreads();
   return total;
 }
 
@@ -477,8 +487,9 @@ struct OctLDS {
   lds_u32* cc;     // 4 per processed rank (aliases sortkey / best / the gather's cell offsets)
   lds_u64* sortkey;
   lds_u32* best;
-  lds_i32* s_tmp;  // [17]
+  lds_i32* s_tmp;  // [2 * 16] alternating wave-total slots of wg_scan_excl
   lds_i32* s_ctl;  // [4]
+  int pp;          // next s_tmp slot (uniform across the workgroup)
 };
 
 // Per-key arrays of one (level, frame): gathered keys, key -> node, quadrant scratch.  In LDS
@@ -490,18 +501,109 @@ struct OctKeys {
   QP kq;
 };
 
-// One division pass: nodes order[0..D) (processing order) are divided; every other node is kept.
-// Children of the last processed node go to the front (std::list::push_front semantics).
-// If `limitN` > 0 the pass stops after the first node whose division makes size >= limitN.
-template <typename KA>
-__device__ __forceinline__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D,
-                                         int limitN, const KA& kk, int n) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int c = cur;
+// ---- division passes.  Node-level work (at most ncap nodes) runs on wave 0 alone, wave-
+// synchronously (DPP scans, no barriers); key-level work (n keys) runs on every wave.  A pass is
+//   [A: wave 0]   the nodes to divide, in processing order: order[r], prank[node] = r or -1
+//   [B: all]      child counts per divided node (key quadrants, LDS atomics)
+//   [C: wave 0]   children and the new node list (push_front order), the pass's results in ctl
+//   [D: all]      key -> node in the new list
+// with one barrier after each step.
+
+// wave 0: in-place exclusive scan of a[0..n), lane-contiguous chunks; returns the total
+__device__ int w0_scan_excl(lds_i32* a, int n) {
+  const int lane = threadIdx.x & 63;
+  const int per = (n + 63) >> 6;
+  const int b = min(lane * per, n), e = min(b + per, n);
+  int local = 0;
+  for (int i = b; i < e; i++) local += a[i];
+  const int incl = wave_incl_scan(local);
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  int run = incl - local;
+  for (int i = b; i < e; i++) {
+    const int t = a[i];
+    a[i] = run;
+    run += t;
+  }
+  wave_sync();
+  return total;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// [A, phase 1, wave 0] nodes with cnt > 1 in list order into order[]; prank; zero their child
+// counters.  Returns D.
+__device__ int w0_expandable_in_order(OctLDS& S, int cur, int L) {
+  const int lane = threadIdx.x & 63;
+  for (int s = lane; s < L; s += 64) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
+  wave_sync();
+  const int D = w0_scan_excl(S.gst, L);
+  for (int s = lane; s < L; s += 64) {
+    if (S.cnt[cur][s] > 1) {
+      S.order[S.gst[s]] = s;
+      S.prank[s] = S.gst[s];
+    } else {
+      S.prank[s] = -1;
+    }
+  }
+  for (int i = lane; i < 4 * D; i += 64) S.cc[i] = 0;
+  return D;
+}
+
+// [A, phase 2] expandable nodes sorted by (size, creation seq) descending (ORBextractor.cc:684
+// sorts pair<size, ExtractorNode*> ascending and walks it backwards; pointer order is pinned to
+// creation order).  Wave 0 compacts the keys, then every wave ranks them.
+__device__ int oct_expandable_sorted(OctLDS& S, int cur, int L) {
+  const int tid = threadIdx.x, nt = blockDim.x, wave = tid >> 6, lane = tid & 63;
+  if (wave == 0) {
+    for (int s = lane; s < L; s += 64) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
+    wave_sync();
+    const int D = w0_scan_excl(S.gst, L);
+    for (int s = lane; s < L; s += 64) {
+      if (S.cnt[cur][s] > 1)
+        S.sortkey[S.gst[s]] = ((unsigned long long)S.cnt[cur][s] << 40) |
+                              ((unsigned long long)(S.seq[cur][s] & 0xFFFFFFu) << 16) |
+                              (unsigned long long)s;
+      S.prank[s] = -1;
+    }
+    if (lane == 0) {
+      S.sortkey[D] = 0ull;  // pad to an even count (0 is below every key)
+      S.s_ctl[3] = D;
+    }
+  }
+  __syncthreads();
+  const int D = S.s_ctl[3];
+  // rank sort, descending: the keys are unique (node index in the low bits), so a key's rank is
+  // the number of keys above it; every thread ranks its keys against all of them (broadcast LDS
+  // reads, two keys per read): one barrier instead of a sorting network's log^2 steps
+  for (int i = tid; i < D; i += nt) {
+    const unsigned long long k = S.sortkey[i];
+    int rank = 0;
+    for (int j = 0; j < D; j += 2) rank += (S.sortkey[j] > k) + (S.sortkey[j + 1] > k);
+    const int s = (int)(k & 0xFFFFull);
+    S.order[rank] = s;
+    S.prank[s] = rank;
+  }
+  __syncthreads();
+  // cc aliases sortkey: zero the child counters only once every rank is done
   for (int i = tid; i < 4 * D; i += nt) S.cc[i] = 0;
   __syncthreads();
-  // 1) child counts per processed node
-  for (int i = tid; i < n; i += nt) {
+  return D;
+}
+
+// [B, all waves] child counts per divided node
+template <typename KA>
+__device__ __forceinline__ void oct_count_children(OctLDS& S, int c, const KA& kk, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const uint32_t nd = kk.knode[i];
     const int r = S.prank[nd];
     if (r >= 0) {
@@ -515,40 +617,47 @@ __device__ __forceinline__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& 
       atomicAdd((uint32_t*)&S.cc[r * 4 + q], 1u);
     }
   }
-  __syncthreads();
-  // 2) children per processed node; optional break at limitN (phase 2, ORBextractor.cc:730)
-  for (int r = tid; r < D; r += nt) {
+}
+
+// [C, wave 0] divide order[0..D) (children of the last processed node go to the front:
+// std::list::push_front); every other node is kept.  With limitN > 0 (phase 2,
+// ORBextractor.cc:730) the pass stops after the first node whose division makes the list size
+// reach limitN.  Writes the new list into buffer c ^ 1 and ctl = {new size, nodes with more than
+// one key, T = children created}.
+__device__ void w0_divide(OctLDS& S, int c, int L, uint32_t seqBase, int D, int limitN) {
+  const int lane = threadIdx.x & 63;
+  for (int r = lane; r < D; r += 64) {
     int nc = 0;
+#pragma unroll
     for (int k = 0; k < 4; k++) nc += S.cc[r * 4 + k] > 0;
     S.cumnc[r] = nc;
   }
-  if (tid == 0) S.s_ctl[0] = D;
-  __syncthreads();
+  wave_sync();
+  int Dt = D;
   if (limitN > 0) {
-    for (int r = tid; r < D; r += nt) S.gst[r] = S.cumnc[r] - 1;
-    __syncthreads();
-    wg_scan_excl(S.gst, D, S.s_tmp);
-    for (int r = tid; r < D; r += nt) {
-      const int incl = S.gst[r] + S.cumnc[r] - 1;
-      if (L + incl >= limitN) atomicMin((int*)&S.s_ctl[0], r + 1);
-    }
-    __syncthreads();
+    for (int r = lane; r < D; r += 64) S.gst[r] = S.cumnc[r] - 1;
+    wave_sync();
+    w0_scan_excl(S.gst, D);
+    int first = D;
+    for (int r = lane; r < D; r += 64)
+      if (L + S.gst[r] + S.cumnc[r] - 1 >= limitN) first = min(first, r + 1);
+    Dt = wave_min(first);
   }
-  const int Dt = S.s_ctl[0];
-  for (int r = tid + Dt; r < D; r += nt) S.prank[S.order[r]] = -1;  // not divided this pass
-  __syncthreads();
-  const int T = wg_scan_excl(S.cumnc, Dt, S.s_tmp);  // cumnc = sum_{q<r} nc
-  for (int r = tid; r < Dt; r += nt) {
+  for (int r = Dt + lane; r < D; r += 64) S.prank[S.order[r]] = -1;  // not divided this pass
+  wave_sync();
+  const int T = w0_scan_excl(S.cumnc, Dt);  // cumnc = sum_{q<r} nc
+  for (int r = lane; r < Dt; r += 64) {
     int nc = 0;
+#pragma unroll
     for (int k = 0; k < 4; k++) nc += S.cc[r * 4 + k] > 0;
     S.gst[r] = T - S.cumnc[r] - nc;  // sum_{q>r} nc
   }
-  for (int s = tid; s < L; s += nt) S.krank[s] = S.prank[s] < 0 ? 1 : 0;
-  __syncthreads();
-  const int K = wg_scan_excl(S.krank, L, S.s_tmp);
+  for (int s = lane; s < L; s += 64) S.krank[s] = S.prank[s] < 0 ? 1 : 0;
+  wave_sync();
+  const int K = w0_scan_excl(S.krank, L);
   const int o = c ^ 1;
-  // 3) new node list: processed children (n4..n1 per group, last group first), then kept nodes
-  for (int r = tid; r < Dt; r += nt) {
+  // new node list: processed children (n4..n1 per group, last group first), then kept nodes
+  for (int r = lane; r < Dt; r += 64) {
     const int nd = S.order[r];
     const int X0 = S.x0[c][nd], Y0 = S.y0[c][nd], X1 = S.x1[c][nd], Y1 = S.y1[c][nd];
     const int mx = X0 + (int)ceilf((float)(X1 - X0) / 2.f);
@@ -575,7 +684,7 @@ __device__ __forceinline__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& 
       before++;
     }
   }
-  for (int s = tid; s < L; s += nt) {
+  for (int s = lane; s < L; s += 64) {
     if (S.prank[s] < 0) {
       const int slot = T + S.krank[s];
       S.x0[o][slot] = S.x0[c][s];
@@ -586,9 +695,22 @@ __device__ __forceinline__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& 
       S.seq[o][slot] = S.seq[c][s];
     }
   }
-  __syncthreads();
-  // 4) key -> new node
-  for (int i = tid; i < n; i += nt) {
+  wave_sync();
+  const int Ln = T + K;
+  int e = 0;
+  for (int s = lane; s < Ln; s += 64) e += S.cnt[o][s] > 1 ? 1 : 0;
+  e = wave_sum(e);
+  if (lane == 0) {
+    S.s_ctl[0] = Ln;
+    S.s_ctl[1] = e;
+    S.s_ctl[2] = T;
+  }
+}
+
+// [D, all waves] key -> node in the new list
+template <typename KA>
+__device__ __forceinline__ void oct_relink_keys(OctLDS& S, const KA& kk, int n, int T) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const uint32_t nd = kk.knode[i];
     const int r = S.prank[nd];
     if (r >= 0) {
@@ -600,75 +722,24 @@ __device__ __forceinline__ void oct_pass(OctLDS& S, int& cur, int& L, uint32_t& 
       kk.knode[i] = (uint16_t)(T + S.krank[nd]);
     }
   }
+}
+
+// One division pass over the D nodes selected by step A (already behind a barrier).  Updates the
+// uniform list state of every thread; returns the number of nodes with more than one key.
+template <typename KA>
+__device__ __forceinline__ int oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D,
+                                        int limitN, const KA& kk, int n) {
+  oct_count_children(S, cur, kk, n);
   __syncthreads();
-  cur = o;
-  L = T + K;
+  if ((threadIdx.x >> 6) == 0) w0_divide(S, cur, L, seqBase, D, limitN);
+  __syncthreads();
+  const int Ln = S.s_ctl[0], nexp = S.s_ctl[1], T = S.s_ctl[2];
+  oct_relink_keys(S, kk, n, T);
+  __syncthreads();
+  cur ^= 1;
+  L = Ln;
   seqBase += (uint32_t)T;
-}
-
-// Nodes with cnt > 1, in list order, into S.order; sets prank; returns their count.
-__device__ int oct_expandable_in_order(OctLDS& S, int cur, int L) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int s = tid; s < L; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
-  __syncthreads();
-  const int D = wg_scan_excl(S.gst, L, S.s_tmp);
-  for (int s = tid; s < L; s += nt) {
-    if (S.cnt[cur][s] > 1) {
-      S.order[S.gst[s]] = s;
-      S.prank[s] = S.gst[s];
-    } else {
-      S.prank[s] = -1;
-    }
-  }
-  __syncthreads();
-  return D;
-}
-
-// Phase-2 order: expandable nodes sorted by (size, creation seq) descending (ORBextractor.cc:684
-// sorts pair<size, ExtractorNode*> ascending and walks it backwards; pointer order is pinned to
-// creation order).
-__device__ int oct_expandable_sorted(OctLDS& S, int cur, int L) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int s = tid; s < L; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
-  __syncthreads();
-  const int D = wg_scan_excl(S.gst, L, S.s_tmp);
-  int P = 1;
-  while (P < D) P <<= 1;
-  for (int i = tid; i < P; i += nt) S.sortkey[i] = 0ull;
-  __syncthreads();
-  for (int s = tid; s < L; s += nt) {
-    if (S.cnt[cur][s] > 1)
-      S.sortkey[S.gst[s]] = ((unsigned long long)S.cnt[cur][s] << 40) |
-                            ((unsigned long long)(S.seq[cur][s] & 0xFFFFFFu) << 16) |
-                            (unsigned long long)s;
-  }
-  __syncthreads();
-  // bitonic sort, descending
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < P; i += nt) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long a = S.sortkey[i], b = S.sortkey[ixj];
-          const bool desc = (i & k) == 0;
-          if (desc ? (a < b) : (a > b)) {
-            S.sortkey[i] = b;
-            S.sortkey[ixj] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int s = tid; s < L; s += nt) S.prank[s] = -1;
-  __syncthreads();
-  for (int r = tid; r < D; r += nt) {
-    const int s = (int)(S.sortkey[r] & 0xFFFFull);
-    S.order[r] = s;
-    S.prank[s] = r;
-  }
-  __syncthreads();
-  return D;
+  return nexp;
 }
 
 // LDS layout of k_octree: node arrays (ncap nodes), then the per-key arrays of up to kcap keys.
@@ -701,6 +772,10 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
     kk.lk[i] = fk[cells[L0.cell_begin + lo].slot_off + (i - coff[lo])];
   }
   __syncthreads();
+#ifdef MMT_OCT_PROFILE
+  long long tp0 = clock64(), tsort = 0, tpass = 0, tmain = 0;
+  int npass1 = 0, npass2 = 0;
+#endif
   // ---- initial nodes (ORBextractor.cc:552-585)
   const int nIni = L0.nIni;
   const float hX = L0.hX;
@@ -715,7 +790,7 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
   __syncthreads();
   for (int i = tid; i < nIni; i += nt) S.krank[i] = S.cnt[0][i] > 0 ? 1 : 0;
   __syncthreads();
-  int Lsz = wg_scan_excl(S.krank, nIni, S.s_tmp);
+  int Lsz = wg_scan_excl(S.krank, nIni, S.s_tmp, S.pp, false);
   for (int i = tid; i < nIni; i += nt) {
     if (S.cnt[0][i] > 0) {
       const int s = S.krank[i];
@@ -742,12 +817,20 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
       break;
     }
     const int prevSize = Lsz;
-    const int D = oct_expandable_in_order(S, cur, Lsz);
-    oct_pass(S, cur, Lsz, seqBase, D, 0, kk, n);
-    // nToExpand = nodes with more than one key
-    for (int s = tid; s < Lsz; s += nt) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
+#ifdef MMT_OCT_PROFILE
+    long long ta = clock64();
+    npass1++;
+#endif
+    if ((tid >> 6) == 0) {
+      const int D = w0_expandable_in_order(S, cur, Lsz);
+      if ((tid & 63) == 0) S.s_ctl[3] = D;
+    }
     __syncthreads();
-    const int nToExpand = wg_scan_excl(S.gst, Lsz, S.s_tmp);
+    const int D = S.s_ctl[3];
+    const int nToExpand = oct_pass(S, cur, Lsz, seqBase, D, 0, kk, n);
+#ifdef MMT_OCT_PROFILE
+    tmain += clock64() - ta;
+#endif
     if (Lsz >= N || Lsz == prevSize) {
       finish = true;
     } else if (Lsz + nToExpand * 3 > N) {
@@ -758,8 +841,19 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
           break;
         }
         const int prev2 = Lsz;
+#ifdef MMT_OCT_PROFILE
+        long long tb = clock64();
+        npass2++;
+#endif
         const int D2 = oct_expandable_sorted(S, cur, Lsz);
+#ifdef MMT_OCT_PROFILE
+        long long tc = clock64();
+        tsort += tc - tb;
+#endif
         oct_pass(S, cur, Lsz, seqBase, D2, N, kk, n);
+#ifdef MMT_OCT_PROFILE
+        tpass += clock64() - tc;
+#endif
         if (Lsz >= N || Lsz == prev2) finish = true;
       }
     }
@@ -781,6 +875,11 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
     const uint32_t x = key_x(k) + kMinBorder, y = key_y(k) + kMinBorder;
     outp[s] = (y << 20) | (x << 8) | key_s(k);
   }
+#ifdef MMT_OCT_PROFILE
+  if (tid == 0 && blockIdx.y == 0)
+    printf("octprof level=%d n=%d N=%d L=%d total=%lld main=%lld (%d passes) sort=%lld pass2=%lld (%d)\n",
+           L0.out_off, n, N, Lsz, clock64() - tp0, tmain, npass1, tsort, tpass, npass2);
+#endif
   if (tid == 0) {
     *ocount_p = nout;
     if (Lsz > L0.out_cap) atomicOr(err, 4);
@@ -797,10 +896,11 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
                                                  uint32_t* __restrict__ knode_g,
                                                  uint32_t* __restrict__ okeys, int out_slots,
                                                  int* __restrict__ ocount, int nlevels,
-                                                 int ncap, int kcap, int* __restrict__ err) {
+                                                 int ncap, int kcap, int level_begin,
+                                                 int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_generic[];
   LDS unsigned char* smem = (LDS unsigned char*)smem_generic;
-  const int level = blockIdx.x, frame = blockIdx.y;
+  const int level = level_begin + blockIdx.x, frame = blockIdx.y;
   const int tid = threadIdx.x, nt = blockDim.x;
   const LevelInfo L0 = lv[level];
   // ---- carve LDS (all offsets multiples of 16)
@@ -827,8 +927,9 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
   S.cc = (lds_u32*)carve(16 * ncap);
   S.sortkey = (lds_u64*)S.cc;
   S.best = S.cc;
-  S.s_tmp = (lds_i32*)carve(4 * 20);
-  S.s_ctl = S.s_tmp + 17;
+  S.s_tmp = (lds_i32*)carve(4 * 36);
+  S.s_ctl = S.s_tmp + 32;
+  S.pp = 0;
   lds_u32* k_lk = (lds_u32*)carve(4 * kcap);
   lds_u16* k_node = (lds_u16*)carve(2 * kcap);
   lds_u8* k_q = (lds_u8*)carve(kcap);
@@ -839,7 +940,7 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
   lds_i32* coff = (lds_i32*)S.cc;  // scratch (nc <= 4 * ncap checked on host)
   for (int i = tid; i < nc; i += nt) coff[i] = cnt[i];
   __syncthreads();
-  const int n = wg_scan_excl(coff, nc, S.s_tmp);
+  const int n = wg_scan_excl(coff, nc, S.s_tmp, S.pp, true);
   uint32_t* outp = okeys + (size_t)frame * out_slots + L0.out_off;
   int* ocount_p = ocount + frame * nlevels + level;
   if (n == 0) {
@@ -1374,10 +1475,19 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
                        pyr_stride_, d_lv_, d_cells_, ncells_, d_keys_, total_slots_, d_cellcnt_,
                        iniTh_, minTh_, fast_rows_max_, fast_win_max_, c0, c1);
   };
+  const size_t lds = octree_lds_;
+  auto octree = [&](int l0, int l1, hipStream_t st) {
+    hipLaunchKernelGGL(k_octree, dim3(l1 - l0, nframes), dim3(1024), lds, st, d_lv_, d_cells_,
+                       ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,
+                       out_slots_, d_ocount_, nlevels_, node_cap_, key_cap_, l0, d_err_);
+  };
+  // Two chains that meet before orientation:
+  //   side:  FAST + octree of level 0 (they need only the gray frames), then the Gaussian blur
+  //   main:  the (latency-bound) resize chain, FAST + octree of levels 1..
   MMT_HIP(hipEventRecord(ev_gray_, stream));
   MMT_HIP(hipStreamWaitEvent(side_, ev_gray_, 0));
   fast(lv_[0].cell_begin, lv_[0].cell_end, side_);
-  MMT_HIP(hipEventRecord(ev_fast0_, side_));
+  octree(0, 1, side_);
   for (int l = 1; l < nlevels_; l++) {
     const LevelInfo& S = lv_[l - 1];
     const LevelInfo& L = lv_[l];
@@ -1387,20 +1497,13 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
                        S.w, L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l],
                        rs_pitch_[l]);
   }
-  // the Gaussian blur needs only the pyramid: it follows level-0 FAST on the side stream,
-  // concurrently with FAST on levels 1.. and the octree (one latency-bound workgroup per CU
-  // leaves most wave slots idle), and joins before orientation
   MMT_HIP(hipEventRecord(ev_pyr_, stream));
   MMT_HIP(hipStreamWaitEvent(side_, ev_pyr_, 0));
   hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, side_, d_pyr_,
                      d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
   MMT_HIP(hipEventRecord(ev_blur_, side_));
   fast(lv_[0].cell_end, ncells_, stream);
-  MMT_HIP(hipStreamWaitEvent(stream, ev_fast0_, 0));
-  const size_t lds = octree_lds_;
-  hipLaunchKernelGGL(k_octree, dim3(nlevels_, nframes), dim3(1024), lds, stream, d_lv_, d_cells_,
-                     ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,
-                     out_slots_, d_ocount_, nlevels_, node_cap_, key_cap_, d_err_);
+  if (nlevels_ > 1) octree(1, nlevels_, stream);
   MMT_HIP(hipStreamWaitEvent(stream, ev_blur_, 0));
   const int waves = (nframes * out_slots_ + 3) / 4;
   hipLaunchKernelGGL(k_orient_desc, dim3((waves + 3) / 4), dim3(256), 0, stream, d_pyr_, d_blur_,

@@ -10,4 +10,5 @@ for v in base "$@"; do
   echo "== $v kitti: $(grep batch= gpurun_out/ab_$v.log)"
   python tools/dispatch_times.py gpurun_out/ab_$v/run_results.db | grep -v "k_resize"
   ORB_MB_SCENE=synthetic timeout -k 10 120 python tools/orb_microbench.py 32 20 2>&1 | tail -1 | sed "s/^/== $v synthetic: /"
+  timeout -k 10 120 python tools/orb_window_bench.py 32 20 2>&1 | grep batch= | sed "s/^/== $v window: /"
 done
