@@ -191,6 +191,49 @@ int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, fl
                    double* R_out, double* t_out, int* inliers_out, int* n_inliers,
                    int* iters_out /* iterations run, best hypothesis */);
 
+/* ---- PnPsolver (row D6): ORB-SLAM2's P4P EPnP-RANSAC of Tracking::Relocalization -------------
+ * PnPsolver(F, vpMapPointMatches) + SetRansacParameters(probability, minInliers, maxIterations,
+ * minSet, epsilon, th2) + iterate(nIterations, bNoMore, vbInliers, nInliers) (reference
+ * src/PnPsolver.cc:67-339, driven by Tracking.cc:3659-3700 with (0.99, 10, 300, 4, 0.5, 5.991)
+ * and nIterations 5).  The n correspondences in mvP2D / mvP3Dw order: pts3 n x 3 world points,
+ * pts2 n x 2 pixels (mvKeysUn), sigma2 n = mvLevelSigma2[octave].  min_set must be 4.
+ *
+ * Random minimal sets: the reference draws them with DUtils::Random::RandomInt (rand()), so the
+ * caller keeps that stream.  randi[4 k + j] = RandomInt(0, n - 1 - j) of draw j in iteration k of
+ * this call; n_draw_iters must cover the call: max(maxIts - state->iterations, n_iterations),
+ * maxIts being the iteration cap SetRansacParameters derives.  The solver's state across calls
+ * (mnIterations, mnBestInliers, mBestTcw, mvbBestInliers) is *state, caller-owned (best_mask: n
+ * bytes); zero it (iterations = best_inliers = 0) for a new solver.
+ *
+ * Outputs: *pose_found = 1 and Tcw_out / inliers_out (n bytes, mvKeyPointIndices order) /
+ * *n_inliers when iterate() returns a pose (refined, or the best hypothesis once the iterations
+ * are exhausted), 0 for the reference's empty cv::Mat; *no_more = bNoMore. */
+typedef struct mmt_pnpsolver_problem {
+  int n;
+  const float* pts3;
+  const float* pts2;
+  const float* sigma2;
+  float fx, fy, cx, cy;
+  double probability;
+  int min_inliers;
+  int max_iterations;
+  int min_set;
+  float epsilon;
+  float th2;
+} mmt_pnpsolver_problem;
+
+typedef struct mmt_pnpsolver_state {
+  int iterations;          /* mnIterations                                                 */
+  int best_inliers;        /* mnBestInliers                                                */
+  float best_Tcw[16];      /* mBestTcw (row-major)                                         */
+  uint8_t* best_mask;      /* mvbBestInliers, n bytes                                      */
+} mmt_pnpsolver_state;
+
+int mmt_pnpsolver_iterate(mmt_ctx* ctx, const mmt_pnpsolver_problem* problem,
+                          const int32_t* randi, int n_draw_iters, int n_iterations,
+                          mmt_pnpsolver_state* state, float* Tcw_out, uint8_t* inliers_out,
+                          int* n_inliers, int* pose_found, int* no_more);
+
 /* ---- Frame grid and projection matching (rows B3, C1-C3 of the hot path) ----------------------
  * The current Frame as the matchers read it: its ORB keys (mvKeysUn == mvKeys, no distortion),
  * descriptors (n x 32) and the metric depth map (w x h floats, the Tcw-independent part of

@@ -82,6 +82,19 @@ class MmtLocalPoints(ctypes.Structure):
                 ("desc", ctypes.c_void_p), ("skip", ctypes.c_void_p)]
 
 
+class MmtPnPsolverProblem(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("pts3", ctypes.c_void_p), ("pts2", ctypes.c_void_p),
+                ("sigma2", ctypes.c_void_p), ("fx", ctypes.c_float), ("fy", ctypes.c_float),
+                ("cx", ctypes.c_float), ("cy", ctypes.c_float), ("probability", ctypes.c_double),
+                ("min_inliers", ctypes.c_int), ("max_iterations", ctypes.c_int),
+                ("min_set", ctypes.c_int), ("epsilon", ctypes.c_float), ("th2", ctypes.c_float)]
+
+
+class MmtPnPsolverState(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int), ("best_inliers", ctypes.c_int),
+                ("best_Tcw", ctypes.c_float * 16), ("best_mask", ctypes.c_void_p)]
+
+
 class MmtProfile(ctypes.Structure):
     _fields_ = [("orb_ms", ctypes.c_double), ("orb_launches", ctypes.c_int64),
                 ("orb_frames", ctypes.c_int64)]
@@ -149,6 +162,9 @@ def lib():
         L.mmt_pose_optimization.argtypes = [vp, ctypes.POINTER(MmtPoseOptProblem), vp, vp, vp]
         L.mmt_pnp_ransac.argtypes = [vp, vp, vp, i32] + [ctypes.c_float] * 4 + \
             [i32, ctypes.c_double, ctypes.c_double] + [vp] * 5
+        L.mmt_pnpsolver_iterate.argtypes = [vp, ctypes.POINTER(MmtPnPsolverProblem), vp, i32,
+                                            i32, ctypes.POINTER(MmtPnPsolverState), vp, vp, vp,
+                                            vp, vp]
         L.mmt_frame_grid.argtypes = [vp, ctypes.POINTER(MmtMatchFrame), vp, vp, vp, vp]
         L.mmt_search_by_projection_frame.argtypes = [vp, ctypes.POINTER(MmtMatchFrame),
                                                      ctypes.POINTER(MmtLastFrame),
@@ -418,6 +434,47 @@ class Context:
                                          ctypes.byref(ninl), _p(its)))
         return R.reshape(3, 3), t, inl[:ninl.value].copy(), dict(iterations=int(its[0]),
                                                                  best_iter=int(its[1]))
+
+    def pnpsolver_iterate(self, pts3, pts2, sigma2, K, randi, n_iterations=5, state=None,
+                          params=(0.99, 10, 300, 4, 0.5, 5.991)):
+        """PnPsolver::SetRansacParameters(*params) + iterate(n_iterations) (row D6) with the
+        caller's RandomInt draws `randi` (iterations x 4).  state: dict(iterations,
+        best_inliers, best_Tcw, best_mask), updated in place (the solver carried across
+        calls).  Returns dict(found, no_more, n_inliers, Tcw, mask) like oracle's."""
+        pts3 = np.ascontiguousarray(pts3, np.float32)
+        pts2 = np.ascontiguousarray(pts2, np.float32)
+        s2 = np.ascontiguousarray(sigma2, np.float32)
+        n = len(pts3)
+        if state is None:
+            state = {}
+        pr = MmtPnPsolverProblem()
+        pr.n = n
+        pr.pts3, pr.pts2, pr.sigma2 = pts3.ctypes.data, pts2.ctypes.data, s2.ctypes.data
+        pr.fx, pr.fy, pr.cx, pr.cy = K
+        (pr.probability, pr.min_inliers, pr.max_iterations, pr.min_set, pr.epsilon,
+         pr.th2) = params
+        mask_state = np.ascontiguousarray(state.get("best_mask", np.zeros(n, bool)), np.uint8)
+        if len(mask_state) < max(n, 1):
+            mask_state = np.zeros(max(n, 1), np.uint8)
+        st = MmtPnPsolverState()
+        st.iterations = state.get("iterations", 0)
+        st.best_inliers = state.get("best_inliers", 0)
+        st.best_Tcw[:] = np.asarray(state.get("best_Tcw", np.zeros((4, 4))),
+                                    np.float32).reshape(16).tolist()
+        st.best_mask = mask_state.ctypes.data
+        ri = np.ascontiguousarray(randi, np.int32).reshape(-1, 4)
+        T = np.zeros(16, np.float32)
+        m = np.zeros(max(n, 1), np.uint8)
+        nin, found, no_more = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        self._check(lib().mmt_pnpsolver_iterate(self._h, ctypes.byref(pr), _p(ri), len(ri),
+                                                n_iterations, ctypes.byref(st), _p(T), _p(m),
+                                                ctypes.byref(nin), ctypes.byref(found),
+                                                ctypes.byref(no_more)))
+        state.update(iterations=st.iterations, best_inliers=st.best_inliers,
+                     best_Tcw=np.array(st.best_Tcw[:], np.float32).reshape(4, 4),
+                     best_mask=mask_state[:n].astype(bool))
+        return dict(found=bool(found.value), no_more=bool(no_more.value),
+                    n_inliers=nin.value, Tcw=T.reshape(4, 4), mask=m[:n].astype(bool))
 
     def debug_fetch(self, what, frame=0, nbytes=1 << 26):
         buf = np.zeros(nbytes, np.uint8)

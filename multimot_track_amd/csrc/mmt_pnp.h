@@ -33,8 +33,14 @@ struct PnPObject {
   int* mm_inliers;
   int* subset;              // D3 edge -> sample index
   int* n_subset;
-  int* result;              // best, maxGood, iterations, n_ransac_inliers, n_mm_inliers
+  int* result;              // best, maxGood, iterations, n_ransac_inliers, n_mm_inliers,
+                            // D6: refined inlier count (6)
   double* Rt;               // R (9), t (3)
+  // D6 (PnPsolver) only
+  int raw_pixels;           // EPnP inputs are the pixels as they are (add_correspondence)
+  int rt_raw;               // refit R without the Rodrigues round trip
+  const float* max_err;     // [n] mvMaxError = sigma2 * th2 (CheckInliers thresholds)
+  double* hrt;              // [max_iters][12] R, t of each hypothesis' chosen estimate
 };
 
 constexpr int kHypRec = 160;  // doubles per hypothesis record
@@ -45,5 +51,11 @@ void launch_pnp(PnPObject* d_objs, int nobj, int max_iters, hipStream_t st, bool
 // motion-model inliers (needs PnPObject::MM, i.e. the previous frame's object motions)
 void launch_pnp_mm(PnPObject* d_objs, int nobj, hipStream_t st);
 void launch_pnp_subset(PnPObject* d_objs, int nobj, hipStream_t st);
+// D6: P4P hypotheses (subsets [K][4]), their chosen estimates (hrt) and CheckInliers (good,
+// masks rows 0..K-1)
+void launch_p4p_hypotheses(PnPObject* d_obj, int K, hipStream_t st);
+// D6: PnPsolver::Refine on the inliers of masks row `row` (EPnP over them, CheckInliers of the
+// refined pose: count in result[6], mask in row `row_out`, pose in Rt)
+void launch_p4p_refine(PnPObject* d_obj, int row, int row_out, hipStream_t st);
 
 }  // namespace mmt

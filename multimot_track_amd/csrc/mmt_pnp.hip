@@ -557,42 +557,52 @@ constexpr int R_UT = 0, R_AL = 48, R_PW = 68, R_US = 83, R_L = 93, R_RHO = 153;
 // column of M^T M and runs its column of the eigen-solve.
 constexpr int kHypPerBlock = 5;
 
+// NP = points per minimal set: 5 for D5 (solvePnPRansac's EPnP sets), 4 for D6 (PnPsolver's
+// P4P sets).  D6 (o.raw_pixels) feeds the pixel coordinates to EPnP as they are
+// (PnPsolver::add_correspondence); D5 round-trips them through undistortPoints.
+template <int NP>
 __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) {
   __shared__ double s_al[kHypPerBlock][20], s_us[kHypPerBlock][10], s_pws[kHypPerBlock][15];
   __shared__ double s_cws[kHypPerBlock][12], s_ut[kHypPerBlock][48];
   const int lane = threadIdx.x, g = lane / 12, j = lane - 12 * g, gb = 12 * g;
   PnPObject& o = objs[blockIdx.y];
   const int n = *o.n;
-  if (n < 5) return;
+  if (n < NP) return;
   const int h = blockIdx.x * kHypPerBlock + g;
   const bool active = g < kHypPerBlock && h < max_iters;
   const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
   if (active && j == 0) {
-    double pws[15], us[10], cws[12];
+    double pws[3 * NP], us[2 * NP], cws[12];
     const double ifx = 1. / fu, ify = 1. / fv;
-    const int* sub = o.subsets + 5 * h;
+    const int* sub = o.subsets + NP * h;
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const int jj = n == 5 ? i : sub[i];  // count == modelPoints: the kernel runs on all points
+    for (int i = 0; i < NP; i++) {
+      // D5 with count == modelPoints: the kernel runs on all points
+      const int jj = (NP == 5 && n == 5) ? i : sub[i];
 #pragma unroll
       for (int k = 0; k < 3; k++) pws[3 * i + k] = o.pts3[3 * jj + k];
       const float2 pt = o.pts2[jj];
-      const float xn = (float)(((double)pt.x - uc) * ifx);
-      const float yn = (float)(((double)pt.y - vc) * ify);
-      us[2 * i] = (double)xn * fu + uc;
-      us[2 * i + 1] = (double)yn * fv + vc;
+      if (o.raw_pixels) {
+        us[2 * i] = pt.x;
+        us[2 * i + 1] = pt.y;
+      } else {
+        const float xn = (float)(((double)pt.x - uc) * ifx);
+        const float yn = (float)(((double)pt.y - vc) * ify);
+        us[2 * i] = (double)xn * fu + uc;
+        us[2 * i + 1] = (double)yn * fv + vc;
+      }
     }
     // choose_control_points
     cws[0] = cws[1] = cws[2] = 0;
 #pragma unroll
-    for (int i = 0; i < 5; i++)
+    for (int i = 0; i < NP; i++)
 #pragma unroll
       for (int k = 0; k < 3; k++) cws[k] += pws[3 * i + k];
 #pragma unroll
-    for (int k = 0; k < 3; k++) cws[k] /= 5;
+    for (int k = 0; k < 3; k++) cws[k] /= NP;
     double m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < NP; i++) {
       double pp[3];
 #pragma unroll
       for (int k = 0; k < 3; k++) pp[k] = pws[3 * i + k] - cws[k];
@@ -605,7 +615,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
     eig_sym_small<3>(m, dc, uct);
 #pragma unroll
     for (int i = 1; i < 4; i++) {
-      const double k = sqrt(fmax(dc[i - 1], 0.0) / 5);
+      const double k = sqrt(fmax(dc[i - 1], 0.0) / NP);
 #pragma unroll
       for (int x = 0; x < 3; x++) cws[3 * i + x] = cws[x] + k * uct[3 * (i - 1) + x];
     }
@@ -617,7 +627,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
       for (int x = 1; x < 4; x++) cc[3 * i + x - 1] = cws[3 * x + i] - cws[i];
     pinv3(cc, ci);
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < NP; i++) {
       const double* pi = &pws[3 * i];
       double al[4];
 #pragma unroll
@@ -629,9 +639,9 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
       for (int x = 0; x < 4; x++) s_al[g][4 * i + x] = al[x];
     }
 #pragma unroll
-    for (int i = 0; i < 15; i++) s_pws[g][i] = pws[i];
+    for (int i = 0; i < 3 * NP; i++) s_pws[g][i] = pws[i];
 #pragma unroll
-    for (int i = 0; i < 10; i++) s_us[g][i] = us[i];
+    for (int i = 0; i < 2 * NP; i++) s_us[g][i] = us[i];
 #pragma unroll
     for (int i = 0; i < 12; i++) s_cws[g][i] = cws[i];
   }
@@ -645,7 +655,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
     for (int k = 0; k < 12; k++) {
       const int qa = k / 3, ca = k - 3 * qa;
       double acc = 0;
-      for (int i = 0; i < 5; i++) {
+      for (int i = 0; i < NP; i++) {
         const double u = s_us[gg][2 * i], vv = s_us[gg][2 * i + 1];
         const double aa = s_al[gg][4 * i + qa], ab = s_al[gg][4 * i + qb];
         const double m1a = ca == 0 ? aa * fu : (ca == 1 ? 0.0 : aa * (uc - u));
@@ -668,9 +678,9 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
   if (!active) return;
   double* rec = o.hrec + (size_t)kHypRec * h;
   for (int e = j; e < 48; e += 12) rec[R_UT + e] = s_ut[g][e];
-  for (int e = j; e < 20; e += 12) rec[R_AL + e] = s_al[g][e];
-  for (int e = j; e < 15; e += 12) rec[R_PW + e] = s_pws[g][e];
-  if (j < 10) rec[R_US + j] = s_us[g][j];
+  for (int e = j; e < 4 * NP; e += 12) rec[R_AL + e] = s_al[g][e];
+  for (int e = j; e < 3 * NP; e += 12) rec[R_PW + e] = s_pws[g][e];
+  if (j < 2 * NP) rec[R_US + j] = s_us[g][j];
   if (j == 0) {
     double L[60];
     compute_L_6x10(s_ut[g], L);
@@ -688,11 +698,11 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(PnPObject* objs, int max_iters) 
 
 // one lane per (hypothesis, object) for beta estimate V (betas_approx_V + gauss_newton +
 // compute_R_and_t); each variant is its own launch so a wave runs one code path
-template <int V>
+template <int V, int NP>
 __device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
   const int h = blockIdx.x * 64 + threadIdx.x;
   const int n = *o.n;
-  if (h >= max_iters || n < 5) return;
+  if (h >= max_iters || n < NP) return;
   const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
   const double* rec = o.hrec + (size_t)kHypRec * h;
   double L[60], rho[6], betas[4];
@@ -708,7 +718,7 @@ __device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
     betas_approx_3(L, rho, betas);
   gauss_newton(L, rho, betas);
   // compute_R_and_t: ccs, pcs, solve_for_sign, estimate_R_and_t, reprojection_error
-  double ccs[12], pcs[15], pws[15], R[9], t[3];
+  double ccs[12], pcs[3 * NP], pws[3 * NP], R[9], t[3];
 #pragma unroll
   for (int i = 0; i < 12; i++) ccs[i] = 0.0f;
 #pragma unroll
@@ -718,7 +728,7 @@ __device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
     for (int j = 0; j < 12; j++) ccs[j] += betas[i] * v[j];
   }
 #pragma unroll
-  for (int i = 0; i < 5; i++) {
+  for (int i = 0; i < NP; i++) {
     const double* a = rec + R_AL + 4 * i;
 #pragma unroll
     for (int j = 0; j < 3; j++)
@@ -726,13 +736,13 @@ __device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
   }
   if (pcs[2] < 0.0) {
 #pragma unroll
-    for (int i = 0; i < 15; i++) pcs[i] = -pcs[i];
+    for (int i = 0; i < 3 * NP; i++) pcs[i] = -pcs[i];
   }
 #pragma unroll
-  for (int i = 0; i < 15; i++) pws[i] = rec[R_PW + i];
+  for (int i = 0; i < 3 * NP; i++) pws[i] = rec[R_PW + i];
   double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
 #pragma unroll
-  for (int i = 0; i < 5; i++)
+  for (int i = 0; i < NP; i++)
 #pragma unroll
     for (int j = 0; j < 3; j++) {
       pc0[j] += pcs[3 * i + j];
@@ -740,12 +750,12 @@ __device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
     }
 #pragma unroll
   for (int j = 0; j < 3; j++) {
-    pc0[j] /= 5;
-    pw0[j] /= 5;
+    pc0[j] /= NP;
+    pw0[j] /= NP;
   }
   double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int i = 0; i < 5; i++) {
+  for (int i = 0; i < NP; i++) {
     const double* pc = &pcs[3 * i];
     const double* pw = &pws[3 * i];
 #pragma unroll
@@ -760,7 +770,7 @@ __device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
   for (int r = 0; r < 3; r++) t[r] = pc0[r] - d_dot3(R + 3 * r, pw0);
   double sum2 = 0.0;
 #pragma unroll
-  for (int i = 0; i < 5; i++) {
+  for (int i = 0; i < NP; i++) {
     const double* pw = &pws[3 * i];
     const double Xc = d_dot3(R, pw) + t[0], Yc = d_dot3(R + 3, pw) + t[1];
     const double inv_Zc = 1.0 / (d_dot3(R + 6, pw) + t[2]);
@@ -769,7 +779,7 @@ __device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
     sum2 += sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
   }
   double* out = o.hout + (size_t)kHypOut * (3 * h + V - 1);
-  out[0] = sum2 / 5;
+  out[0] = sum2 / NP;
 #pragma unroll
   for (int i = 0; i < 9; i++) out[1 + i] = R[i];
 #pragma unroll
@@ -778,14 +788,15 @@ __device__ __forceinline__ void pnp_beta(PnPObject& o, int max_iters) {
 
 // the three estimates of every hypothesis run concurrently (blockIdx.z = estimate), each block on
 // one code path
+template <int NP>
 __global__ __launch_bounds__(64) void k_pnp_beta(PnPObject* objs, int max_iters) {
   PnPObject& o = objs[blockIdx.y];
   if (blockIdx.z == 0)
-    pnp_beta<1>(o, max_iters);
+    pnp_beta<1, NP>(o, max_iters);
   else if (blockIdx.z == 1)
-    pnp_beta<2>(o, max_iters);
+    pnp_beta<2, NP>(o, max_iters);
   else
-    pnp_beta<3>(o, max_iters);
+    pnp_beta<3, NP>(o, max_iters);
 }
 
 // one workgroup per (hypothesis, object): inlier count + mask (PnPRansacCallback::computeError,
@@ -915,6 +926,11 @@ __device__ __forceinline__ void refit_pw(const PnPObject& o, int k, double* p) {
 // normalised coordinates in double here (the hypotheses round them to float)
 __device__ __forceinline__ void refit_us(const PnPObject& o, int k, double& u, double& v) {
   const float2 q = o.pts2[o.inliers[k]];
+  if (o.raw_pixels) {  // D6: PnPsolver::Refine adds the pixels as they are
+    u = q.x;
+    v = q.y;
+    return;
+  }
   const double fu = o.fx, fv = o.fy, uc = o.cx, vc = o.cy;
   u = (((double)q.x - uc) * (1. / fu)) * fu + uc;
   v = (((double)q.y - vc) * (1. / fv)) * fv + vc;
@@ -1251,8 +1267,12 @@ __global__ __launch_bounds__(256) void k_refit_rt(PnPObject* objs) {
       if (S.sum[1] / ni < S.sum[0] / ni) best = 1;
       if (S.sum[2] / ni < S.sum[best] / ni) best = 2;
       double rv[3], R[9];
-      d_rodrigues_r2v(S.R + 9 * best, rv);
-      d_rodrigues_v2r(rv, R);
+      if (o.rt_raw) {  // D6: compute_pose's R as it is (no Rodrigues round trip)
+        for (int i = 0; i < 9; i++) R[i] = S.R[9 * best + i];
+      } else {
+        d_rodrigues_r2v(S.R + 9 * best, rv);
+        d_rodrigues_v2r(rv, R);
+      }
       for (int i = 0; i < 9; i++) o.Rt[i] = R[i];
       for (int i = 0; i < 3; i++) o.Rt[9 + i] = S.t[3 * best + i];
     }
@@ -1308,11 +1328,101 @@ __global__ __launch_bounds__(256) void k_pnp_subset(PnPObject* objs) {
   if (threadIdx.x == 0) *o.n_subset = n;
 }
 
+// ---------------------------------------------------------------- D6: PnPsolver (P4P RANSAC)
+// PnPsolver::CheckInliers (PnPsolver.cc:310-337) for the pose R, t (double): camera coordinates
+// and 1/Zc rounded to float, the projection in double, the squared error in float against
+// mvMaxError (strict)
+__device__ __forceinline__ bool p4p_inlier(const PnPObject& o, const double* R, const double* t,
+                                           int i) {
+  const double X = o.pts3[3 * i], Y = o.pts3[3 * i + 1], Z = o.pts3[3 * i + 2];
+  const float Xc = (float)(R[0] * X + R[1] * Y + R[2] * Z + t[0]);
+  const float Yc = (float)(R[3] * X + R[4] * Y + R[5] * Z + t[1]);
+  const float invZc = (float)(1 / (R[6] * X + R[7] * Y + R[8] * Z + t[2]));
+  const double ue = (double)o.cx + (double)o.fx * (double)Xc * (double)invZc;
+  const double ve = (double)o.cy + (double)o.fy * (double)Yc * (double)invZc;
+  const float2 q = o.pts2[i];
+  const float distX = (float)((double)q.x - ue), distY = (float)((double)q.y - ve);
+  const float error2 = distX * distX + distY * distY;
+  return error2 < o.max_err[i];
+}
+
+// inlier count + mask of pose (R, t) into masks row `row`; block-wide, 256 threads
+__device__ int p4p_check(PnPObject& o, const double* R, const double* t, int row, int* s_w) {
+  const int n = *o.n;
+  int good = 0;
+  for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+    const int i = i0 + threadIdx.x;
+    const bool in = i < n && p4p_inlier(o, R, t, i);
+    const unsigned long long bal = __ballot(in);
+    if ((threadIdx.x & 63) == 0 && i0 + (threadIdx.x & ~63) < n)
+      o.masks[(size_t)row * o.mask_words + (i0 + (threadIdx.x & ~63)) / 64] = bal;
+    good += in ? 1 : 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) good += __shfl_xor(good, off, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = good;
+  __syncthreads();
+  return s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// one workgroup per hypothesis: compute_pose's choice among the three beta estimates
+// (rep_errors[2] < [1]; [3] < [N]), then CheckInliers
+__global__ __launch_bounds__(256) void k_p4p_check(PnPObject* objs, int K) {
+  __shared__ double sRt[12];
+  __shared__ int s_w[4];
+  PnPObject& o = objs[0];
+  const int h = blockIdx.x;
+  if (h >= K || *o.n < 4) return;
+  if (threadIdx.x == 0) {
+    const double* out = o.hout + (size_t)kHypOut * 3 * h;
+    int best = 0;
+    if (out[kHypOut] < out[0]) best = 1;
+    if (out[2 * kHypOut] < out[best * kHypOut]) best = 2;
+    const double* bo = out + best * kHypOut;
+    for (int i = 0; i < 12; i++) {
+      sRt[i] = bo[1 + i];
+      o.hrt[12 * h + i] = bo[1 + i];
+    }
+  }
+  __syncthreads();
+  const int good = p4p_check(o, sRt, sRt + 9, h, s_w);
+  if (threadIdx.x == 0) o.good[h] = good;
+}
+
+// CheckInliers of the refined pose o.Rt
+__global__ __launch_bounds__(256) void k_p4p_check_rt(PnPObject* objs, int row_out) {
+  __shared__ double sRt[12];
+  __shared__ int s_w[4];
+  PnPObject& o = objs[0];
+  if (threadIdx.x < 12) sRt[threadIdx.x] = o.Rt[threadIdx.x];
+  __syncthreads();
+  const int good = p4p_check(o, sRt, sRt + 9, row_out, s_w);
+  if (threadIdx.x == 0) o.result[6] = good;
+}
+
+__global__ void k_p4p_set_row(PnPObject* objs, int row) {
+  if (threadIdx.x == 0) objs[0].result[0] = row;
+}
+
+void launch_p4p_hypotheses(PnPObject* d_obj, int K, hipStream_t st) {
+  hipLaunchKernelGGL(k_pnp_hyp<4>, dim3((K + kHypPerBlock - 1) / kHypPerBlock, 1), dim3(64), 0,
+                     st, d_obj, K);
+  hipLaunchKernelGGL(k_pnp_beta<4>, dim3((K + 63) / 64, 1, 3), dim3(64), 0, st, d_obj, K);
+  hipLaunchKernelGGL(k_p4p_check, dim3(K), dim3(256), 0, st, d_obj, K);
+}
+
+void launch_p4p_refine(PnPObject* d_obj, int row, int row_out, hipStream_t st) {
+  hipLaunchKernelGGL(k_p4p_set_row, dim3(1), dim3(64), 0, st, d_obj, row);
+  hipLaunchKernelGGL(k_refit_null, dim3(1), dim3(256), 0, st, d_obj);
+  hipLaunchKernelGGL(k_refit_beta, dim3(1, 3), dim3(64), 0, st, d_obj);
+  hipLaunchKernelGGL(k_refit_rt, dim3(1), dim3(256), 0, st, d_obj);
+  hipLaunchKernelGGL(k_p4p_check_rt, dim3(1), dim3(256), 0, st, d_obj, row_out);
+}
+
 void launch_pnp(PnPObject* d_objs, int nobj, int max_iters, hipStream_t st, bool gather) {
   if (gather) hipLaunchKernelGGL(k_pnp_gather, dim3(nobj), dim3(256), 0, st, d_objs);
-  hipLaunchKernelGGL(k_pnp_hyp, dim3((max_iters + kHypPerBlock - 1) / kHypPerBlock, nobj), dim3(64),
-                     0, st, d_objs, max_iters);
-  hipLaunchKernelGGL(k_pnp_beta, dim3((max_iters + 63) / 64, nobj, 3), dim3(64), 0, st, d_objs,
+  hipLaunchKernelGGL(k_pnp_hyp<5>, dim3((max_iters + kHypPerBlock - 1) / kHypPerBlock, nobj),
+                     dim3(64), 0, st, d_objs, max_iters);
+  hipLaunchKernelGGL(k_pnp_beta<5>, dim3((max_iters + 63) / 64, nobj, 3), dim3(64), 0, st, d_objs,
                      max_iters);
   hipLaunchKernelGGL(k_pnp_score, dim3(max_iters, nobj), dim3(256), 0, st, d_objs, max_iters);
   hipLaunchKernelGGL(k_pnp_select, dim3(nobj), dim3(64), 0, st, d_objs, max_iters);

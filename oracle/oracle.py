@@ -176,6 +176,51 @@ def pnp_ransac(pts3, pts2, K, max_iters=500, reproj=0.3, conf=0.98):
                                                                  best_iter=int(its[1]))
 
 
+def p4p_randi(n, iters, seed=1):
+    """RandomInt(0, n-1-j) draws of a P4P RANSAC from glibc rand() seeded with `seed`."""
+    out = np.zeros(max(iters, 1) * 4, np.int32)
+    lib().oracle_p4p_randi(n, iters, ctypes.c_uint(seed), _p(out))
+    return out[:iters * 4].reshape(iters, 4)
+
+
+def glibc_rand(seed, count):
+    out = np.zeros(count, np.int32)
+    lib().oracle_glibc_rand(ctypes.c_uint(seed), count, _p(out))
+    return out
+
+
+def pnpsolver_iterate(pts3, pts2, sigma2, K, randi, n_iterations=5, state=None,
+                      params=(0.99, 10, 300, 4, 0.5, 5.991)):
+    """PnPsolver::SetRansacParameters(*params) + iterate(n_iterations) (oracle/pnp_ref.cpp).
+    state: dict(iterations, best_inliers, best_Tcw (4x4), best_mask (n bool)), updated in place.
+    Returns dict(found, no_more, n_inliers, Tcw, mask)."""
+    L = lib()
+    L.oracle_pnpsolver_iterate.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] + \
+        [ctypes.c_double] * 5 + [ctypes.c_int] * 3 + [ctypes.c_float] * 2 + \
+        [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6
+    pts3 = np.ascontiguousarray(pts3, np.float32)
+    pts2 = np.ascontiguousarray(pts2, np.float32)
+    s2 = np.ascontiguousarray(sigma2, np.float32)
+    n = len(pts3)
+    if state is None:
+        state = {}
+    its = np.array([state.get("iterations", 0), state.get("best_inliers", 0)], np.int32)
+    sT = np.ascontiguousarray(state.get("best_Tcw", np.zeros((4, 4))), np.float32).reshape(16)
+    sm = np.ascontiguousarray(state.get("best_mask", np.zeros(n, bool)), np.uint8)
+    ri = np.ascontiguousarray(randi, np.int32).reshape(-1)
+    T = np.zeros(16, np.float32)
+    m = np.zeros(max(n, 1), np.uint8)
+    o3 = np.zeros(3, np.int32)
+    L.oracle_pnpsolver_iterate(_p(pts3), _p(pts2), _p(s2), n, K[0], K[1], K[2], K[3],
+                               params[0], params[1], params[2], params[3], params[4], params[5],
+                               _p(ri), n_iterations, _p(its), _p(sT), _p(sm), _p(T), _p(m),
+                               _p(o3))
+    state.update(iterations=int(its[0]), best_inliers=int(its[1]), best_Tcw=sT.reshape(4, 4),
+                 best_mask=sm[:n].astype(bool))
+    return dict(found=bool(o3[0]), no_more=bool(o3[1]), n_inliers=int(o3[2]),
+                Tcw=T.reshape(4, 4), mask=m[:n].astype(bool))
+
+
 def ransac_subsets(count, iters):
     out = np.zeros(iters * 5, np.int32)
     lib().oracle_ransac_subsets(count, iters, _p(out))

@@ -183,6 +183,47 @@ int oracle_pnp_ransac(const float* pts3, const float* pts2, int n, double fx, do
   return r.ok ? 0 : 1;
 }
 
+// D6 probe: one iterate() call; state in/out (iterations, best_inliers, best_Tcw, best_mask)
+int oracle_pnpsolver_iterate(const float* pts3, const float* pts2, const float* sigma2, int n,
+                             double fx, double fy, double cx, double cy, double prob, int min_inl,
+                             int max_it, int min_set, float eps, float th2, const int* randi,
+                             int n_iterations, int* st_its, float* st_T, uint8_t* st_mask,
+                             float* T_out, uint8_t* mask_out, int* out3) {
+  P4PState st;
+  st.iterations = st_its[0];
+  st.best_inliers = st_its[1];
+  memcpy(st.best_Tcw, st_T, sizeof(st.best_Tcw));
+  st.best_mask.assign(st_mask, st_mask + n);
+  P4PResult r = pnpsolver_iterate(pts3, pts2, sigma2, n, fx, fy, cx, cy, prob, min_inl, max_it,
+                                  min_set, eps, th2, randi, n_iterations, &st);
+  st_its[0] = st.iterations;
+  st_its[1] = st.best_inliers;
+  memcpy(st_T, st.best_Tcw, sizeof(st.best_Tcw));
+  if (!st.best_mask.empty()) memcpy(st_mask, st.best_mask.data(), n);
+  memcpy(T_out, r.Tcw, sizeof(r.Tcw));
+  memset(mask_out, 0, n);
+  if (!r.mask.empty()) memcpy(mask_out, r.mask.data(), n);
+  out3[0] = r.found;
+  out3[1] = r.no_more;
+  out3[2] = r.n_inliers;
+  return 0;
+}
+
+// DUtils::Random::RandomInt draws of a P4P RANSAC (4 per iteration: RandomInt(0, n-1-j)) from
+// glibc's rand() stream seeded with `seed` (1 = an unseeded process)
+int oracle_p4p_randi(int n, int iters, unsigned seed, int* out) {
+  GlibcRand g(seed);
+  for (int k = 0; k < iters; k++)
+    for (int j = 0; j < 4; j++) out[4 * k + j] = g.random_int(0, n - 1 - j);
+  return 0;
+}
+
+int oracle_glibc_rand(unsigned seed, int count, int* out) {
+  GlibcRand g(seed);
+  for (int i = 0; i < count; i++) out[i] = g.next();
+  return 0;
+}
+
 int oracle_ransac_subsets(int count, int iters, int* out) {
   std::vector<int> idx;
   ransac_subsets(count, 5, iters, idx);

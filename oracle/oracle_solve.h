@@ -58,7 +58,34 @@ void ransac_subsets(int count, int model_points, int iters, std::vector<int>& id
 // EPnP on n >= 4 correspondences (epnp.cpp / PnPsolver.cc:342-1022), pixel inputs.
 void epnp_pose(const float* pts3, const float* pts2, const int* sel, int n, double fx, double fy,
                double cx, double cy, double R[9], double t[3], bool f64_points);
+void epnp_pose_raw(const float* pts3, const float* pts2, const int* sel, int n, double fx,
+                   double fy, double cx, double cy, double R[9], double t[3]);
 void rodrigues_r2v(const double R[9], double r[3]);
+
+// D6: glibc rand() (the stream DUtils::Random::RandomInt draws from) and PnPsolver.
+struct GlibcRand {
+  std::vector<int32_t> r;
+  explicit GlibcRand(unsigned seed = 1);
+  int next();
+  int random_int(int min, int max);
+};
+struct P4PState {
+  int iterations = 0, best_inliers = 0;
+  float best_Tcw[16] = {0};
+  std::vector<uint8_t> best_mask;
+};
+struct P4PResult {
+  bool found = false, no_more = false;
+  int n_inliers = 0;
+  float Tcw[16] = {0};
+  std::vector<uint8_t> mask;
+};
+// PnPsolver::SetRansacParameters + iterate(nIterations) on a solver in state *st; randi[4 k + j]
+// = RandomInt(0, N - 1 - j) of draw j in iteration k of this call.
+P4PResult pnpsolver_iterate(const float* pts3, const float* pts2, const float* sigma2, int N,
+                            double fu, double fv, double uc, double vc, double probability,
+                            int minInliers, int maxIterations, int minSet, float epsilon,
+                            float th2, const int* randi, int nIterations, P4PState* st);
 void rodrigues_v2r(const double r[3], double R[9]);
 
 }  // namespace oracle

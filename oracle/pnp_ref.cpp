@@ -577,6 +577,31 @@ void epnp_pose(const float* pts3, const float* pts2, const int* sel, int n, doub
     for (int c = 0; c < 3; c++) R[3 * r + c] = Rm[r][c];
 }
 
+// EPnP as PnPsolver uses it (add_correspondence with the pixel coordinates as they are).
+void epnp_pose_raw(const float* pts3, const float* pts2, const int* sel, int n, double fx,
+                   double fy, double cx, double cy, double R[9], double t[3]) {
+  EPnP e;
+  e.n = n;
+  e.fu = fx;
+  e.fv = fy;
+  e.uc = cx;
+  e.vc = cy;
+  e.pws.resize(3 * n);
+  e.us.resize(2 * n);
+  e.alphas.resize(4 * n);
+  e.pcs.resize(3 * n);
+  for (int i = 0; i < n; i++) {
+    const int j = sel ? sel[i] : i;
+    for (int k = 0; k < 3; k++) e.pws[3 * i + k] = pts3[3 * j + k];
+    e.us[2 * i] = pts2[2 * j];
+    e.us[2 * i + 1] = pts2[2 * j + 1];
+  }
+  double Rm[3][3];
+  e.compute_pose(Rm, t);
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) R[3 * r + c] = Rm[r][c];
+}
+
 // cv::Rodrigues matrix -> vector (orthonormalisation by SVD omitted: EPnP's R is orthonormal to
 // rounding, the effect is below 1e-15).
 void rodrigues_r2v(const double R[9], double r[3]) {
@@ -737,6 +762,147 @@ PnPResult pnp_ransac(const float* pts3, const float* pts2, int n, double fx, dou
   memcpy(res.t, t, sizeof(t));
   res.inliers = sel;
   res.ok = true;
+  return res;
+}
+
+// ---------------------------------------------------------------- D6: PnPsolver (P4P RANSAC)
+// glibc rand() (random_r TYPE_3: additive feedback r[i] = r[i-3] + r[i-31], seeded by srand) --
+// the stream DUtils::Random::RandomInt draws from (Thirdparty/DBoW2/DUtils/Random.cpp:47-50).
+GlibcRand::GlibcRand(unsigned seed) {
+  if (seed == 0) seed = 1;
+  r.resize(34);
+  r[0] = (int32_t)seed;
+  for (int i = 1; i < 31; i++) {
+    const int64_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+    int64_t word = 16807 * lo - 2836 * hi;
+    if (word < 0) word += 2147483647;
+    r[i] = (int32_t)word;
+  }
+  for (int i = 31; i < 34; i++) r[i] = r[i - 31];
+  for (int i = 0; i < 310; i++) next();
+}
+
+int GlibcRand::next() {
+  const size_t i = r.size();
+  const uint32_t v = (uint32_t)r[i - 31] + (uint32_t)r[i - 3];
+  r.push_back((int32_t)v);
+  if (r.size() > 4096) r.erase(r.begin(), r.end() - 34);
+  return (int)(v >> 1);
+}
+
+int GlibcRand::random_int(int min, int max) {  // DUtils::Random::RandomInt
+  const int d = max - min + 1;
+  return int(((double)next() / ((double)2147483647 + 1.0)) * d) + min;
+}
+
+// PnPsolver::CheckInliers (PnPsolver.cc:310-337)
+static int p4p_check(const float* pts3, const float* pts2, const std::vector<float>& maxErr, int n,
+                     const double R[9], const double t[3], double fu, double fv, double uc,
+                     double vc, std::vector<uint8_t>& mask) {
+  int good = 0;
+  mask.assign(n, 0);
+  for (int i = 0; i < n; i++) {
+    const double X = pts3[3 * i], Y = pts3[3 * i + 1], Z = pts3[3 * i + 2];
+    const float Xc = (float)(R[0] * X + R[1] * Y + R[2] * Z + t[0]);
+    const float Yc = (float)(R[3] * X + R[4] * Y + R[5] * Z + t[1]);
+    const float invZc = (float)(1 / (R[6] * X + R[7] * Y + R[8] * Z + t[2]));
+    const double ue = uc + fu * Xc * invZc;
+    const double ve = vc + fv * Yc * invZc;
+    const float distX = (float)(pts2[2 * i] - ue), distY = (float)(pts2[2 * i + 1] - ve);
+    const float error2 = distX * distX + distY * distY;
+    if (error2 < maxErr[i]) {
+      mask[i] = 1;
+      good++;
+    }
+  }
+  return good;
+}
+
+static void to_Tcw(const double R[9], const double t[3], float T[16]) {
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) T[4 * r + c] = r == c ? 1.f : 0.f;
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) T[4 * r + c] = (float)R[3 * r + c];
+    T[4 * r + 3] = (float)t[r];
+  }
+}
+
+// SetRansacParameters (PnPsolver.cc:119-152) + iterate (PnPsolver.cc:160-264) + Refine
+// (PnPsolver.cc:266-308), state carried in *st.
+P4PResult pnpsolver_iterate(const float* pts3, const float* pts2, const float* sigma2, int N,
+                            double fu, double fv, double uc, double vc, double probability,
+                            int minInliers, int maxIterations, int minSet, float epsilon,
+                            float th2, const int* randi, int nIterations, P4PState* st) {
+  P4PResult res;
+  float eps = epsilon;
+  int nMinInliers = (int)(N * eps);
+  if (nMinInliers < minInliers) nMinInliers = minInliers;
+  if (nMinInliers < minSet) nMinInliers = minSet;
+  const int minInl = nMinInliers;
+  if (N > 0 && eps < (float)minInl / N) eps = (float)minInl / N;
+  int nIt;
+  if (minInl == N)
+    nIt = 1;
+  else
+    nIt = (int)std::ceil(std::log(1 - probability) / std::log(1 - std::pow(eps, 3)));
+  const int maxIts = std::max(1, std::min(nIt, maxIterations));
+  std::vector<float> maxErr(N);
+  for (int i = 0; i < N; i++) maxErr[i] = sigma2[i] * th2;
+  if (N < minInl) {
+    res.no_more = true;
+    return res;
+  }
+  if ((int)st->best_mask.size() != N) st->best_mask.assign(N, 0);
+  int cur = 0, k = 0;
+  std::vector<uint8_t> mask;
+  while (st->iterations < maxIts || cur < nIterations) {
+    cur++;
+    st->iterations++;
+    std::vector<int> avail(N);
+    for (int i = 0; i < N; i++) avail[i] = i;
+    int sel[4];
+    for (int j = 0; j < 4; j++) {
+      const int r = randi[4 * k + j];
+      sel[j] = avail[r];
+      avail[r] = avail.back();
+      avail.pop_back();
+    }
+    k++;
+    double R[9], t[3];
+    epnp_pose_raw(pts3, pts2, sel, 4, fu, fv, uc, vc, R, t);
+    const int good = p4p_check(pts3, pts2, maxErr, N, R, t, fu, fv, uc, vc, mask);
+    if (good >= minInl) {
+      if (good > st->best_inliers) {
+        st->best_mask = mask;
+        st->best_inliers = good;
+        to_Tcw(R, t, st->best_Tcw);
+      }
+      // Refine: EPnP over the best inliers, CheckInliers
+      std::vector<int> idx;
+      for (int i = 0; i < N; i++)
+        if (st->best_mask[i]) idx.push_back(i);
+      double Rr[9], tr[3];
+      epnp_pose_raw(pts3, pts2, idx.data(), (int)idx.size(), fu, fv, uc, vc, Rr, tr);
+      std::vector<uint8_t> rmask;
+      const int rgood = p4p_check(pts3, pts2, maxErr, N, Rr, tr, fu, fv, uc, vc, rmask);
+      if (rgood > minInl) {
+        res.found = true;
+        res.n_inliers = rgood;
+        res.mask = rmask;
+        to_Tcw(Rr, tr, res.Tcw);
+        return res;
+      }
+    }
+  }
+  if (st->iterations >= maxIts) {
+    res.no_more = true;
+    if (st->best_inliers >= minInl) {
+      res.found = true;
+      res.n_inliers = st->best_inliers;
+      res.mask = st->best_mask;
+      memcpy(res.Tcw, st->best_Tcw, sizeof(res.Tcw));
+    }
+  }
   return res;
 }
 

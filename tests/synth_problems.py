@@ -95,3 +95,27 @@ def pose_opt_problem(seed, n, outlier_frac=0.1, pix_noise=0.8, mono_frac=0.2, K=
     dT = se3(rot(rng.normal(size=3), 0.02 * rng.normal()), rng.normal(size=3) * 0.1)
     init = (dT.astype(np.float64) @ T.astype(np.float64)).astype(np.float32)
     return Xw, obs, inv_sigma2, init, T
+
+
+def p4p_problem(seed, n, outlier_frac=0.3, pix_noise=0.5, K=K_KITTI):
+    """Relocalization-style PnPsolver input (row D6): n MapPoint world positions, their keypoint
+    pixels in the current frame (octave-scaled noise; an outlier fraction moved by up to 60 px)
+    and mvLevelSigma2[octave] (ORB scale 1.2); returns (pts3, pts2, sigma2, Tcw_true)."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = K
+    T = se3(rot(rng.normal(size=3), 0.2 * rng.normal()), rng.normal(size=3) * [1.0, 0.2, 2.0])
+    u = rng.uniform(20, 1222, n)
+    v = rng.uniform(20, 355, n)
+    z = rng.uniform(4.0, 40.0, n)
+    pc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    Tinv = np.linalg.inv(T.astype(np.float64))
+    Xw = ((Tinv[:3, :3] @ pc.T).T + Tinv[:3, 3]).astype(np.float32)
+    octave = rng.integers(0, 8, n)
+    scale = 1.2 ** octave
+    sigma2 = (scale * scale).astype(np.float32)
+    uv = np.stack([u, v], 1) + rng.normal(scale=pix_noise, size=(n, 2)) * scale[:, None]
+    nout = int(outlier_frac * n)
+    if nout:
+        idx = rng.choice(n, nout, replace=False)
+        uv[idx] += rng.uniform(-60, 60, size=(nout, 2))
+    return Xw, uv.astype(np.float32), sigma2, T
