@@ -211,7 +211,9 @@ def pnpsolver_iterate(pts3, pts2, sigma2, K, randi, n_iterations=5, state=None,
     T = np.zeros(16, np.float32)
     m = np.zeros(max(n, 1), np.uint8)
     o3 = np.zeros(3, np.int32)
-    L.oracle_pnpsolver_iterate(_p(pts3), _p(pts2), _p(s2), n, K[0], K[1], K[2], K[3],
+    # PnPsolver's fu, fv, uc, vc are doubles holding Frame's float fx, fy, cx, cy
+    Kf = [float(np.float32(k)) for k in K]
+    L.oracle_pnpsolver_iterate(_p(pts3), _p(pts2), _p(s2), n, Kf[0], Kf[1], Kf[2], Kf[3],
                                params[0], params[1], params[2], params[3], params[4], params[5],
                                _p(ri), n_iterations, _p(its), _p(sT), _p(sm), _p(T), _p(m),
                                _p(o3))

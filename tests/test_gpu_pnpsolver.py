@@ -4,8 +4,9 @@ and the same RandomInt draws (glibc rand() stream, restatement pinned in
 tests/test_oracle_pnpsolver.py).
 
 Tolerance: iterations, found / no_more, inlier counts and masks, the solver state exact; poses
-within 1e-4 (the hypotheses' EPnP is operation-for-operation the checker's; the refine sums over
-the inliers are reduced in a different order)."""
+within 1e-4 (the 4-point hypotheses' EPnP is operation for operation the checker's; Refine()'s
+sums over the inliers are reduced in a different order).  The camera intrinsics are float, as
+Frame's fx..cy that PnPsolver copies into its doubles."""
 import numpy as np
 import pytest
 
@@ -30,7 +31,7 @@ def _compare(g, o, gs, os_):
     assert np.array_equal(g["mask"], o["mask"])
     assert gs["iterations"] == os_["iterations"] and gs["best_inliers"] == os_["best_inliers"]
     assert np.array_equal(gs["best_mask"], os_["best_mask"])
-    if g["found"]:
+    if g["found"]:  # refined pose, or mBestTcw once the iterations are exhausted
         assert np.abs(g["Tcw"] - o["Tcw"]).max() < POSE_TOL
     if gs["best_inliers"]:
         assert np.abs(gs["best_Tcw"] - os_["best_Tcw"]).max() < POSE_TOL

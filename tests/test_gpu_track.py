@@ -172,3 +172,10 @@ def test_pose_optimization_too_few_edges(ctx):
     Xw, obs, s2, init, _ = pose_opt_problem(9, 2)
     n_g, pose_g, outl_g = ctx.pose_optimization(Xw, obs, s2, init, K_KITTI, 387.5744)
     assert n_g == 0 and np.array_equal(pose_g, init) and not outl_g.any()
+
+
+@pytest.mark.parametrize("w,h,seed", [(1241, 376, 1000), (1226, 370, 1005)])
+def test_track_synthetic_c4_sizes_matches_oracle(oracle_mod, w, h, seed):
+    """BASELINE C4 geometries (KITTI 00 at 1241x376, 05/07 at 1226x370), 4000 features,
+    ego + 3 moving boxes."""
+    assert _synthetic_parity(w, h, 4000, 3, 5, seed) >= 1
