@@ -472,17 +472,21 @@ __device__ __forceinline__ uint32_t key_x(uint32_t k) { return (k >> 8) & 0xFFFu
 __device__ __forceinline__ uint32_t key_y(uint32_t k) { return k >> 20; }
 __device__ __forceinline__ uint32_t key_s(uint32_t k) { return k & 0xFFu; }
 
+// Node arrays are double-buffered as two halves of one array (buffer c at offset c * nb): a
+// run-time buffer index is then address arithmetic, not a pointer array in scratch memory.
 struct OctLDS {
-  lds_u16* x0[2];
-  lds_u16* y0[2];
-  lds_u16* x1[2];
-  lds_u16* y1[2];
-  lds_u32* cnt[2];
-  lds_u32* seq[2];
+  lds_u16* x0;
+  lds_u16* y0;
+  lds_u16* x1;
+  lds_u16* y1;
+  lds_u32* cnt;
+  lds_u32* seq;
+  int nb;
   lds_i32* prank;
   lds_i32* order;
   lds_i32* gst;    // group start of processed rank r, later reused
   lds_i32* cumnc;  // exclusive prefix of child counts
+  lds_u32* mid;    // aliases cumnc between steps A and B: split point (mx | my << 16) per rank
   lds_i32* krank;  // kept-node rank
   lds_u32* cc;     // 4 per processed rank (aliases sortkey / best / the gather's cell offsets)
   lds_u64* sortkey;
@@ -540,17 +544,41 @@ __device__ __forceinline__ int wave_min(int v) {
   return v;
 }
 
+// atomicAdd(&a[key], 1) for every active lane with key != ~0u, one LDS atomic per distinct key
+// of the wave: keys arrive in cell order, so a wave holds a few distinct nodes/quadrants, and
+// same-address LDS atomics would serialise lane by lane.
+__device__ __forceinline__ void wave_agg_inc(lds_u32* a, uint32_t key) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long act = __ballot(key != ~0u);
+  while (act) {
+    const int leader = __builtin_ctzll(act);
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)key, leader);
+    const unsigned long long m = __ballot(key == v);
+    if (lane == leader) atomicAdd((uint32_t*)&a[v], (uint32_t)__popcll(m));
+    act &= ~m;
+  }
+}
+
+// split point of node nd of buffer c (ExtractorNode::DivideNode, ORBextractor.cc:481-486)
+__device__ __forceinline__ uint32_t node_mid(const OctLDS& S, int c, int nd) {
+  const int X0 = S.x0[(c) * S.nb + nd], Y0 = S.y0[(c) * S.nb + nd];
+  const int mx = X0 + (int)ceilf((float)(S.x1[(c) * S.nb + nd] - X0) / 2.f);
+  const int my = Y0 + (int)ceilf((float)(S.y1[(c) * S.nb + nd] - Y0) / 2.f);
+  return (uint32_t)mx | ((uint32_t)my << 16);
+}
+
 // [A, phase 1, wave 0] nodes with cnt > 1 in list order into order[]; prank; zero their child
 // counters.  Returns D.
 __device__ int w0_expandable_in_order(OctLDS& S, int cur, int L) {
   const int lane = threadIdx.x & 63;
-  for (int s = lane; s < L; s += 64) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
+  for (int s = lane; s < L; s += 64) S.gst[s] = S.cnt[(cur) * S.nb + s] > 1 ? 1 : 0;
   wave_sync();
   const int D = w0_scan_excl(S.gst, L);
   for (int s = lane; s < L; s += 64) {
-    if (S.cnt[cur][s] > 1) {
+    if (S.cnt[(cur) * S.nb + s] > 1) {
       S.order[S.gst[s]] = s;
       S.prank[s] = S.gst[s];
+      S.mid[S.gst[s]] = node_mid(S, cur, s);
     } else {
       S.prank[s] = -1;
     }
@@ -565,13 +593,13 @@ __device__ int w0_expandable_in_order(OctLDS& S, int cur, int L) {
 __device__ int oct_expandable_sorted(OctLDS& S, int cur, int L) {
   const int tid = threadIdx.x, nt = blockDim.x, wave = tid >> 6, lane = tid & 63;
   if (wave == 0) {
-    for (int s = lane; s < L; s += 64) S.gst[s] = S.cnt[cur][s] > 1 ? 1 : 0;
+    for (int s = lane; s < L; s += 64) S.gst[s] = S.cnt[(cur) * S.nb + s] > 1 ? 1 : 0;
     wave_sync();
     const int D = w0_scan_excl(S.gst, L);
     for (int s = lane; s < L; s += 64) {
-      if (S.cnt[cur][s] > 1)
-        S.sortkey[S.gst[s]] = ((unsigned long long)S.cnt[cur][s] << 40) |
-                              ((unsigned long long)(S.seq[cur][s] & 0xFFFFFFu) << 16) |
+      if (S.cnt[(cur) * S.nb + s] > 1)
+        S.sortkey[S.gst[s]] = ((unsigned long long)S.cnt[(cur) * S.nb + s] << 40) |
+                              ((unsigned long long)(S.seq[(cur) * S.nb + s] & 0xFFFFFFu) << 16) |
                               (unsigned long long)s;
       S.prank[s] = -1;
     }
@@ -592,6 +620,7 @@ __device__ int oct_expandable_sorted(OctLDS& S, int cur, int L) {
     const int s = (int)(k & 0xFFFFull);
     S.order[rank] = s;
     S.prank[s] = rank;
+    S.mid[rank] = node_mid(S, cur, s);
   }
   __syncthreads();
   // cc aliases sortkey: zero the child counters only once every rank is done
@@ -606,16 +635,15 @@ __device__ __forceinline__ void oct_count_children(OctLDS& S, int c, const KA& k
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const uint32_t nd = kk.knode[i];
     const int r = S.prank[nd];
+    uint32_t key = ~0u;
     if (r >= 0) {
-      const uint32_t k = kk.lk[i];
-      const int hx = (int)ceilf((float)(S.x1[c][nd] - S.x0[c][nd]) / 2.f);
-      const int hy = (int)ceilf((float)(S.y1[c][nd] - S.y0[c][nd]) / 2.f);
-      const int mx = S.x0[c][nd] + hx, my = S.y0[c][nd] + hy;
-      const int q = ((int)key_x(k) < mx) ? (((int)key_y(k) < my) ? 0 : 2)
-                                         : (((int)key_y(k) < my) ? 1 : 3);
+      const uint32_t k = kk.lk[i], m = S.mid[r];
+      const uint32_t mx = m & 0xFFFFu, my = m >> 16;
+      const int q = (key_x(k) < mx) ? ((key_y(k) < my) ? 0 : 2) : ((key_y(k) < my) ? 1 : 3);
       kk.kq[i] = (uint8_t)q;
-      atomicAdd((uint32_t*)&S.cc[r * 4 + q], 1u);
+      key = (uint32_t)(r * 4 + q);
     }
+    wave_agg_inc(S.cc, key);
   }
 }
 
@@ -659,7 +687,7 @@ __device__ void w0_divide(OctLDS& S, int c, int L, uint32_t seqBase, int D, int 
   // new node list: processed children (n4..n1 per group, last group first), then kept nodes
   for (int r = lane; r < Dt; r += 64) {
     const int nd = S.order[r];
-    const int X0 = S.x0[c][nd], Y0 = S.y0[c][nd], X1 = S.x1[c][nd], Y1 = S.y1[c][nd];
+    const int X0 = S.x0[(c) * S.nb + nd], Y0 = S.y0[(c) * S.nb + nd], X1 = S.x1[(c) * S.nb + nd], Y1 = S.y1[(c) * S.nb + nd];
     const int mx = X0 + (int)ceilf((float)(X1 - X0) / 2.f);
     const int my = Y0 + (int)ceilf((float)(Y1 - Y0) / 2.f);
     const int rx0[4] = {X0, mx, X0, mx}, ry0[4] = {Y0, Y0, my, my};
@@ -675,30 +703,31 @@ __device__ void w0_divide(OctLDS& S, int c, int L, uint32_t seqBase, int D, int 
 #pragma unroll
       for (int k2 = k + 1; k2 < 4; k2++) after += cnts[k2] > 0;
       const int slot = S.gst[r] + after;
-      S.x0[o][slot] = (uint16_t)rx0[k];
-      S.y0[o][slot] = (uint16_t)ry0[k];
-      S.x1[o][slot] = (uint16_t)rx1[k];
-      S.y1[o][slot] = (uint16_t)ry1[k];
-      S.cnt[o][slot] = cnts[k];
-      S.seq[o][slot] = seqBase + (uint32_t)(S.cumnc[r] + before);
+      S.cc[r * 4 + k] = (uint32_t)slot;  // child slot for step D (the counts are in cnts)
+      S.x0[(o) * S.nb + slot] = (uint16_t)rx0[k];
+      S.y0[(o) * S.nb + slot] = (uint16_t)ry0[k];
+      S.x1[(o) * S.nb + slot] = (uint16_t)rx1[k];
+      S.y1[(o) * S.nb + slot] = (uint16_t)ry1[k];
+      S.cnt[(o) * S.nb + slot] = cnts[k];
+      S.seq[(o) * S.nb + slot] = seqBase + (uint32_t)(S.cumnc[r] + before);
       before++;
     }
   }
   for (int s = lane; s < L; s += 64) {
     if (S.prank[s] < 0) {
       const int slot = T + S.krank[s];
-      S.x0[o][slot] = S.x0[c][s];
-      S.y0[o][slot] = S.y0[c][s];
-      S.x1[o][slot] = S.x1[c][s];
-      S.y1[o][slot] = S.y1[c][s];
-      S.cnt[o][slot] = S.cnt[c][s];
-      S.seq[o][slot] = S.seq[c][s];
+      S.x0[(o) * S.nb + slot] = S.x0[(c) * S.nb + s];
+      S.y0[(o) * S.nb + slot] = S.y0[(c) * S.nb + s];
+      S.x1[(o) * S.nb + slot] = S.x1[(c) * S.nb + s];
+      S.y1[(o) * S.nb + slot] = S.y1[(c) * S.nb + s];
+      S.cnt[(o) * S.nb + slot] = S.cnt[(c) * S.nb + s];
+      S.seq[(o) * S.nb + slot] = S.seq[(c) * S.nb + s];
     }
   }
   wave_sync();
   const int Ln = T + K;
   int e = 0;
-  for (int s = lane; s < Ln; s += 64) e += S.cnt[o][s] > 1 ? 1 : 0;
+  for (int s = lane; s < Ln; s += 64) e += S.cnt[(o) * S.nb + s] > 1 ? 1 : 0;
   e = wave_sum(e);
   if (lane == 0) {
     S.s_ctl[0] = Ln;
@@ -714,10 +743,7 @@ __device__ __forceinline__ void oct_relink_keys(OctLDS& S, const KA& kk, int n, 
     const uint32_t nd = kk.knode[i];
     const int r = S.prank[nd];
     if (r >= 0) {
-      const int q = kk.kq[i];
-      int after = 0;
-      for (int k2 = q + 1; k2 < 4; k2++) after += S.cc[r * 4 + k2] > 0;
-      kk.knode[i] = (uint16_t)(S.gst[r] + after);
+      kk.knode[i] = (uint16_t)S.cc[r * 4 + kk.kq[i]];
     } else {
       kk.knode[i] = (uint16_t)(T + S.krank[nd]);
     }
@@ -726,16 +752,36 @@ __device__ __forceinline__ void oct_relink_keys(OctLDS& S, const KA& kk, int n, 
 
 // One division pass over the D nodes selected by step A (already behind a barrier).  Updates the
 // uniform list state of every thread; returns the number of nodes with more than one key.
+#ifdef MMT_OCT_PROFILE
+#define OP_T(k, t) do { long long _n = clock64(); g_op[k] += _n - t; t = _n; } while (0)
+#define OP_PARAM , long long* g_op
+#define OP_ARG , g_op
+#else
+#define OP_T(k, t) do {} while (0)
+#define OP_PARAM
+#define OP_ARG
+#endif
+#ifdef MMT_OCT_PROFILE
+#define OP_DECL(t) long long t = clock64()
+#define OP_SET(t) t = clock64()
+#else
+#define OP_DECL(t) do {} while (0)
+#define OP_SET(t) do {} while (0)
+#endif
 template <typename KA>
 __device__ __forceinline__ int oct_pass(OctLDS& S, int& cur, int& L, uint32_t& seqBase, int D,
-                                        int limitN, const KA& kk, int n) {
+                                        int limitN, const KA& kk, int n OP_PARAM) {
+  OP_DECL(t);
   oct_count_children(S, cur, kk, n);
   __syncthreads();
+  OP_T(0, t);
   if ((threadIdx.x >> 6) == 0) w0_divide(S, cur, L, seqBase, D, limitN);
   __syncthreads();
+  OP_T(1, t);
   const int Ln = S.s_ctl[0], nexp = S.s_ctl[1], T = S.s_ctl[2];
   oct_relink_keys(S, kk, n, T);
   __syncthreads();
+  OP_T(2, t);
   cur ^= 1;
   L = Ln;
   seqBase += (uint32_t)T;
@@ -762,16 +808,37 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
                                         int ncap, int* __restrict__ err) {
   const int tid = threadIdx.x, nt = blockDim.x;
   // thread per key: its cell is the last one whose offset is <= the key index
-  const lds_i32* coff = (const lds_i32*)S.cc;
-  for (int i = tid; i < n; i += nt) {
-    int lo = 0, hi = nc - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (coff[mid] <= i) lo = mid; else hi = mid - 1;
-    }
-    kk.lk[i] = fk[cells[L0.cell_begin + lo].slot_off + (i - coff[lo])];
+#ifdef MMT_OCT_PROFILE
+  long long g_op[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  OP_DECL(tq);
+  // cell of every key: one thread per cell marks its key range (knode as scratch), and the
+  // cell's slot base minus its key offset goes next to the offsets when it fits
+  lds_i32* coff = (lds_i32*)S.cc;
+  const bool lds_base = 2 * nc <= 4 * ncap;
+  for (int c = tid; c < nc; c += nt) {
+    const int b = coff[c], e = c + 1 < nc ? coff[c + 1] : n;
+    for (int i = b; i < e; i++) kk.knode[i] = (uint16_t)c;
+    if (lds_base) coff[nc + c] = cells[L0.cell_begin + c].slot_off - b;
   }
   __syncthreads();
+  for (int i0 = tid; i0 < n; i0 += 4 * nt) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + u * nt;
+      if (i < n) {
+        const int c = kk.knode[i];
+        const int base = lds_base ? coff[nc + c] : cells[L0.cell_begin + c].slot_off - coff[c];
+        v[u] = fk[base + i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (i0 + u * nt < n) kk.lk[i0 + u * nt] = v[u];
+  }
+  __syncthreads();
+  OP_T(3, tq);
 #ifdef MMT_OCT_PROFILE
   long long tp0 = clock64(), tsort = 0, tpass = 0, tmain = 0;
   int npass1 = 0, npass2 = 0;
@@ -780,31 +847,32 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
   const int nIni = L0.nIni;
   const float hX = L0.hX;
   const int H = (L0.h - kEdge + 3) - kMinBorder;  // maxBorderY - minBorderY
-  for (int i = tid; i < nIni; i += nt) S.cnt[0][i] = 0;
+  for (int i = tid; i < nIni; i += nt) S.cnt[(0) * S.nb + i] = 0;
   __syncthreads();
   for (int i = tid; i < n; i += nt) {
     const int idx = (int)((float)key_x(kk.lk[i]) / hX);
     kk.knode[i] = (uint16_t)idx;
-    atomicAdd((uint32_t*)&S.cnt[0][idx], 1u);
+    wave_agg_inc(S.cnt, (uint32_t)idx);
   }
   __syncthreads();
-  for (int i = tid; i < nIni; i += nt) S.krank[i] = S.cnt[0][i] > 0 ? 1 : 0;
+  for (int i = tid; i < nIni; i += nt) S.krank[i] = S.cnt[(0) * S.nb + i] > 0 ? 1 : 0;
   __syncthreads();
   int Lsz = wg_scan_excl(S.krank, nIni, S.s_tmp, S.pp, false);
   for (int i = tid; i < nIni; i += nt) {
-    if (S.cnt[0][i] > 0) {
+    if (S.cnt[(0) * S.nb + i] > 0) {
       const int s = S.krank[i];
-      S.x0[1][s] = (uint16_t)(int)(hX * (float)i);
-      S.x1[1][s] = (uint16_t)(int)(hX * (float)(i + 1));
-      S.y0[1][s] = 0;
-      S.y1[1][s] = (uint16_t)H;
-      S.cnt[1][s] = S.cnt[0][i];
-      S.seq[1][s] = (uint32_t)i;
+      S.x0[(1) * S.nb + s] = (uint16_t)(int)(hX * (float)i);
+      S.x1[(1) * S.nb + s] = (uint16_t)(int)(hX * (float)(i + 1));
+      S.y0[(1) * S.nb + s] = 0;
+      S.y1[(1) * S.nb + s] = (uint16_t)H;
+      S.cnt[(1) * S.nb + s] = S.cnt[(0) * S.nb + i];
+      S.seq[(1) * S.nb + s] = (uint32_t)i;
     }
   }
   __syncthreads();
   for (int i = tid; i < n; i += nt) kk.knode[i] = (uint16_t)S.krank[kk.knode[i]];
   __syncthreads();
+  OP_T(4, tq);
   int cur = 1;
   uint32_t seqBase = (uint32_t)nIni;
   const int N = L0.N;
@@ -827,7 +895,7 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
     }
     __syncthreads();
     const int D = S.s_ctl[3];
-    const int nToExpand = oct_pass(S, cur, Lsz, seqBase, D, 0, kk, n);
+    const int nToExpand = oct_pass(S, cur, Lsz, seqBase, D, 0, kk, n OP_ARG);
 #ifdef MMT_OCT_PROFILE
     tmain += clock64() - ta;
 #endif
@@ -850,7 +918,7 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
         long long tc = clock64();
         tsort += tc - tb;
 #endif
-        oct_pass(S, cur, Lsz, seqBase, D2, N, kk, n);
+        oct_pass(S, cur, Lsz, seqBase, D2, N, kk, n OP_ARG);
 #ifdef MMT_OCT_PROFILE
         tpass += clock64() - tc;
 #endif
@@ -863,6 +931,7 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
     }
   }
   // ---- retain the best key per node: max response, first in key order (:744-760)
+  OP_SET(tq);
   for (int s = tid; s < Lsz; s += nt) S.best[s] = 0;
   __syncthreads();
   for (int i = tid; i < n; i += nt)
@@ -875,7 +944,10 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
     const uint32_t x = key_x(k) + kMinBorder, y = key_y(k) + kMinBorder;
     outp[s] = (y << 20) | (x << 8) | key_s(k);
   }
+  OP_T(5, tq);
 #ifdef MMT_OCT_PROFILE
+  if (tid == 0 && blockIdx.y == 0 && blockIdx.x == 0)
+    printf("steps count=%lld divide=%lld relink=%lld gather=%lld init=%lld best=%lld\n", g_op[0], g_op[1], g_op[2], g_op[3], g_op[4], g_op[5]);
   if (tid == 0 && blockIdx.y == 0)
     printf("octprof level=%d n=%d N=%d L=%d total=%lld main=%lld (%d passes) sort=%lld pass2=%lld (%d)\n",
            L0.out_off, n, N, Lsz, clock64() - tp0, tmain, npass1, tsort, tpass, npass2);
@@ -911,18 +983,18 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
     p += (bytes + 15) & ~(size_t)15;
     return r;
   };
-  for (int b = 0; b < 2; b++) {
-    S.x0[b] = (lds_u16*)carve(2 * ncap);
-    S.y0[b] = (lds_u16*)carve(2 * ncap);
-    S.x1[b] = (lds_u16*)carve(2 * ncap);
-    S.y1[b] = (lds_u16*)carve(2 * ncap);
-    S.cnt[b] = (lds_u32*)carve(4 * ncap);
-    S.seq[b] = (lds_u32*)carve(4 * ncap);
-  }
+  S.nb = ncap;
+  S.x0 = (lds_u16*)carve(2 * 2 * ncap);
+  S.y0 = (lds_u16*)carve(2 * 2 * ncap);
+  S.x1 = (lds_u16*)carve(2 * 2 * ncap);
+  S.y1 = (lds_u16*)carve(2 * 2 * ncap);
+  S.cnt = (lds_u32*)carve(2 * 4 * ncap);
+  S.seq = (lds_u32*)carve(2 * 4 * ncap);
   S.prank = (lds_i32*)carve(4 * ncap);
   S.order = (lds_i32*)carve(4 * ncap);
   S.gst = (lds_i32*)carve(4 * ncap);
   S.cumnc = (lds_i32*)carve(4 * ncap);
+  S.mid = (lds_u32*)S.cumnc;
   S.krank = (lds_i32*)carve(4 * ncap);
   S.cc = (lds_u32*)carve(16 * ncap);
   S.sortkey = (lds_u64*)S.cc;
