@@ -3,7 +3,9 @@
 Workload (BASELINE.json configs[2]): KITTI-03 geometry 1242x375, 2000 ORB
 features, ego + 3 object motions.  Synthetic seeded street sequence (multimot_track_amd/scene.py:
 ray-cast ground, facades and three moving boxes with exact depth, flow and semantic labels),
-rendered straight into HBM before the timed region.  One sequence per GPU (seed 1003 + rank).
+rendered straight into HBM before the timed region.  One sequence per GPU (seed 1003 + rank) by
+default; --seqs-per-gpu K tracks K independent sequences per GPU (one context, stream set and
+host thread each; SURVEY 8(e) allows several sequences per device), seeds 1003 + rank * K + k.
 
 A "step" = System::TrackRGBD over one chunk of `--chunk` consecutive frames of the sequence:
 batched ORB extraction for the chunk, then per frame the association (B1-B9), the ego flow solve
@@ -64,6 +66,8 @@ def main():
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--objects", type=int, default=3)
+    ap.add_argument("--seqs-per-gpu", type=int, default=1,
+                    help="independent sequences tracked concurrently on each GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -80,26 +84,40 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    W, H, NF, C = args.width, args.height, args.nfeatures, args.chunk
+    W, H, NF, C, K = args.width, args.height, args.nfeatures, args.chunk, args.seqs_per_gpu
     nframes = (args.warmup + args.steps) * C
-    seed = shard.sequence_seed(1003, rank)
     t_gen = time.perf_counter()
-    seq = scene.kitti_like_sequence(nframes, W, H, n_objects=args.objects, seed=seed, device=dev)
+    seqs = [scene.kitti_like_sequence(nframes, W, H, n_objects=args.objects,
+                                      seed=shard.sequence_seed(1003, rank * K + k), device=dev)
+            for k in range(K)]
+    seq = seqs[0]
     torch.cuda.synchronize(dev)
     t_gen = time.perf_counter() - t_gen
 
     cfg = M.kitti03_config(W, H, NF, max_batch=C, device_id=local)
-    ctx = M.Context(cfg)
+    ctxs = [M.Context(cfg) for _ in range(K)]
+    ctx = ctxs[0]
     lv = ctx.levels()
-    # a dedicated (non-default) stream: the library launches on it and records its HIP events on
-    # it, and torch's sync below waits for it
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
+    # dedicated (non-default) streams: the library launches on them and records its HIP events
+    # on them; torch.cuda.synchronize below waits for all of them
+    streams = [torch.cuda.Stream(dev) for _ in range(K)]
+    torch.cuda.set_stream(streams[0])
+
+    def step_k(k, i):
+        sl = slice(i * C, (i + 1) * C)
+        s = seqs[k]
+        return ctxs[k].track_chunk_device(s["bgr"][sl], s["disp"][sl], s["flow"][sl],
+                                          s["mask"][sl], streams[k].cuda_stream, parse=False)
+
+    pool = None
+    if K > 1:  # one host thread per sequence (the C-ABI calls release the GIL)
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=K)
 
     def step(i):
-        sl = slice(i * C, (i + 1) * C)
-        return ctx.track_chunk_device(seq["bgr"][sl], seq["disp"][sl], seq["flow"][sl],
-                                      seq["mask"][sl], stream.cuda_stream, parse=False)
+        if pool is None:
+            return step_k(0, i)
+        return [f.result() for f in [pool.submit(step_k, k, i) for k in range(K)]][0]
 
     for i in range(args.warmup):
         step(i)
@@ -114,7 +132,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = ctx.profile_read()
     elapsed = shard.max_over_ranks(elapsed, world, dev)
-    frames_all = shard.sum_over_ranks(args.steps * C, world, dev)
+    frames_all = shard.sum_over_ranks(args.steps * C * K, world, dev)
 
     # per-frame outputs of the timed region (sanity: every frame tracked, objects found)
     res, objs = results[-1]
@@ -160,7 +178,7 @@ def main():
             "config": {"workload": "C3: KITTI-03-like RGB-D, end-to-end TrackRGBD (ORB + "
                                    "association + ego + %d object motions)" % args.objects,
                        "width": W, "height": H, "orb_features": NF, "chunk_frames": C,
-                       "sequences_per_gpu": 1, "parallelism": "dp%d" % world,
+                       "sequences_per_gpu": K, "parallelism": "dp%d" % world,
                        "frames_tracked": tracked, "objects_last_frame": n_obj_last,
                        "ego_abs_err_last_frame": round(ego_err, 5),
                        "scene_render_s": round(t_gen, 2)},
@@ -174,7 +192,10 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
+    if pool is not None:
+        pool.shutdown()
     if world > 1:
         dist.destroy_process_group()
 
