@@ -152,8 +152,8 @@ def main():
         if not args.no_cpu:
             from oracle import oracle as O
             O.build()
-            K = (cfg.fx, cfg.fy, cfg.cx, cfg.cy)
-            tr = O.Tracker(W, H, K, cfg.bf, 0, NF)
+            kcam = (cfg.fx, cfg.fy, cfg.cx, cfg.cy)
+            tr = O.Tracker(W, H, kcam, cfg.bf, 0, NF)
             n_done, tcpu = 0, 0.0
             while tcpu < args.cpu_seconds and n_done < nframes:
                 f = scene.to_numpy_frames({k: seq[k][n_done:n_done + 1]

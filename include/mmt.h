@@ -120,10 +120,21 @@ int mmt_orb_extract_batch(mmt_ctx* ctx, const uint8_t* const* grays, int nframes
 
 /* Device-resident variant: d_gray holds nframes gray frames (pitch frame_pitch bytes, rows of
  * `width` bytes, tightly packed); all outputs are device pointers; runs on `stream`
- * (hipStream_t, may be NULL for the context stream).  No host synchronisation. */
+ * (hipStream_t, may be NULL for the context stream).  No host synchronisation, so the device-side
+ * error flags of these launches are reported by mmt_orb_device_status. */
 int mmt_orb_extract_device(mmt_ctx* ctx, const uint8_t* d_gray, int nframes, size_t frame_pitch,
                            mmt_kp* d_kps, uint8_t* d_desc, int cap_per_frame, int* d_n,
                            void* stream);
+
+/* Synchronises `stream` (NULL: the context stream) and reports the device-side error flags that
+ * ORB launches set since the last check (octree pass guard, node capacity, output truncation):
+ * MMT_OK, or MMT_EDEVICE with mmt_last_error naming the flags.  The flags are cleared.  The
+ * synchronous entry points (mmt_orb_extract*, mmt_track_rgbd*) run this check themselves, so a
+ * tripped guard is never returned as MMT_OK with truncated keypoints. */
+int mmt_orb_device_status(mmt_ctx* ctx, void* stream);
+
+/* Test hook: OR `flags` into the ORB device error word (as a tripped kernel guard would). */
+int mmt_debug_orb_raise(mmt_ctx* ctx, int flags);
 
 /* Debug: copy an intermediate device buffer of the last ORB run (frame 0..max_batch-1) to the
  * host.  what: 0 pyramid, 1 blurred pyramid (both level-major, unpadded), 2 FAST per-cell

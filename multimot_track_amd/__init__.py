@@ -152,6 +152,8 @@ def lib():
         L.mmt_orb_extract.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, vp]
         L.mmt_orb_extract_batch.argtypes = [vp, vp, i32, i32, vp, vp, i32, vp]
         L.mmt_orb_extract_device.argtypes = [vp, vp, i32, sz, vp, vp, i32, vp, vp]
+        L.mmt_orb_device_status.argtypes = [vp, vp]
+        L.mmt_debug_orb_raise.argtypes = [vp, i32]
         L.mmt_debug_fetch.restype = ctypes.c_long
         L.mmt_debug_fetch.argtypes = [vp, i32, i32, vp, sz]
         L.mmt_reset.argtypes = [vp]
@@ -475,6 +477,13 @@ class Context:
                      best_mask=mask_state[:n].astype(bool))
         return dict(found=bool(found.value), no_more=bool(no_more.value),
                     n_inliers=nin.value, Tcw=T.reshape(4, 4), mask=m[:n].astype(bool))
+
+    def orb_device_status(self, stream=0):
+        """mmt_orb_device_status: raises MmtError if an ORB launch tripped a device guard."""
+        self._check(lib().mmt_orb_device_status(self._h, stream))
+
+    def debug_orb_raise(self, flags):
+        self._check(lib().mmt_debug_orb_raise(self._h, flags))
 
     def debug_fetch(self, what, frame=0, nbytes=1 << 26):
         buf = np.zeros(nbytes, np.uint8)

@@ -225,7 +225,7 @@ int mmt_orb_extract_batch(mmt_ctx* ctx, const uint8_t* const* grays, int nframes
       ctx->engine.run(ctx->d_in, nb, fb, ctx->d_kps, ctx->d_desc, cap, ctx->d_n, ctx->stream);
       MMT_HIP(hipMemcpyAsync(counts.data() + done, ctx->d_n, sizeof(int) * nb,
                              hipMemcpyDeviceToHost, ctx->stream));
-      MMT_HIP(hipStreamSynchronize(ctx->stream));
+      ctx->engine.check_flags(ctx->stream);  // synchronises the stream
       for (int f = 0; f < nb; f++) {
         const int n = counts[done + f];
         n_per_frame[done + f] = n;
@@ -280,6 +280,22 @@ int mmt_orb_extract_device(mmt_ctx* ctx, const uint8_t* d_gray, int nframes, siz
   return guard(ctx, [&] {
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     ctx->engine.run(d_gray, nframes, frame_pitch, d_kps, d_desc, cap_per_frame, d_n, s);
+  });
+}
+
+int mmt_orb_device_status(mmt_ctx* ctx, void* stream) {
+  if (!ctx) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ctx->engine.check_flags(stream ? (hipStream_t)stream : ctx->stream);
+  });
+}
+
+int mmt_debug_orb_raise(mmt_ctx* ctx, int flags) {
+  if (!ctx) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ctx->engine.raise_flags(flags, ctx->stream);
   });
 }
 

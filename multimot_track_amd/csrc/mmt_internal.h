@@ -89,6 +89,11 @@ class OrbEngine {
   uint8_t* level0() { return d_pyr_; }
   size_t pyramid_stride() const { return pyr_stride_; }
   long debug_fetch(int what, int frame, void* out, size_t cap, hipStream_t stream);
+  // Device-side error flags of the launches so far (k_octree: 1 pass guard, 2 node capacity,
+  // 4 output truncated).  Reads them on `stream` (synchronising it); throws DeviceError and
+  // clears them when any is set.
+  void check_flags(hipStream_t stream);
+  void raise_flags(int flags, hipStream_t stream);
 
  private:
   void release();

@@ -17,7 +17,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
+#include <string>
 
 #include "mmt_internal.h"
 
@@ -788,15 +790,39 @@ __device__ __forceinline__ int oct_pass(OctLDS& S, int& cur, int& L, uint32_t& s
   return nexp;
 }
 
-// LDS layout of k_octree: node arrays (ncap nodes), then the per-key arrays of up to kcap keys.
-static size_t octree_node_lds_bytes(int ncap) {
-  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-  size_t b = 0;
-  for (int i = 0; i < 2; i++) b += 4 * r16(2 * ncap) + 2 * r16(4 * ncap);
-  b += 5 * r16(4 * ncap) + r16(16 * ncap) + r16(4 * 24);
-  return b;
+// LDS layout of k_octree: node arrays (ncap nodes, double-buffered where the passes alternate),
+// then the per-key arrays of up to kcap keys.  The kernel carves exactly these offsets and the
+// host sizes the launch from `end`, so the two cannot drift apart.
+struct OctLayout {
+  uint32_t x0, y0, x1, y1, cnt, seq, prank, order, gst, cumnc, krank, cc, tmp, lk, knode, kq, end;
+};
+__host__ __device__ inline OctLayout oct_layout(int ncap, int kcap) {
+  OctLayout o{};
+  uint32_t p = 0;
+  auto take = [&](uint32_t bytes) {
+    const uint32_t r = p;
+    p += (bytes + 15u) & ~15u;
+    return r;
+  };
+  o.x0 = take(2 * 2 * ncap);
+  o.y0 = take(2 * 2 * ncap);
+  o.x1 = take(2 * 2 * ncap);
+  o.y1 = take(2 * 2 * ncap);
+  o.cnt = take(2 * 4 * ncap);
+  o.seq = take(2 * 4 * ncap);
+  o.prank = take(4 * ncap);
+  o.order = take(4 * ncap);
+  o.gst = take(4 * ncap);
+  o.cumnc = take(4 * ncap);
+  o.krank = take(4 * ncap);
+  o.cc = take(16 * ncap);
+  o.tmp = take(4 * 36);  // s_tmp [2 * 16] + s_ctl [4]
+  o.lk = take(4 * kcap);
+  o.knode = take(2 * kcap);
+  o.kq = take(kcap);
+  o.end = p;
+  return o;
 }
-static size_t octree_key_lds_bytes(int kcap) { return (size_t)kcap * 7 + 16; }
 
 // Gather of the level's FAST candidates in cell order (cells hold them row-major), then
 // DistributeOctTree (ORBextractor.cc:539-763) and the best key per node.
@@ -975,36 +1001,31 @@ __global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ l
   const int level = level_begin + blockIdx.x, frame = blockIdx.y;
   const int tid = threadIdx.x, nt = blockDim.x;
   const LevelInfo L0 = lv[level];
-  // ---- carve LDS (all offsets multiples of 16)
+  // ---- carve LDS (oct_layout: the same offsets the host sized the launch with)
+  const OctLayout ly = oct_layout(ncap, kcap);
   OctLDS S;
-  LDS unsigned char* p = smem;
-  auto carve = [&](size_t bytes) {
-    LDS unsigned char* r = p;
-    p += (bytes + 15) & ~(size_t)15;
-    return r;
-  };
   S.nb = ncap;
-  S.x0 = (lds_u16*)carve(2 * 2 * ncap);
-  S.y0 = (lds_u16*)carve(2 * 2 * ncap);
-  S.x1 = (lds_u16*)carve(2 * 2 * ncap);
-  S.y1 = (lds_u16*)carve(2 * 2 * ncap);
-  S.cnt = (lds_u32*)carve(2 * 4 * ncap);
-  S.seq = (lds_u32*)carve(2 * 4 * ncap);
-  S.prank = (lds_i32*)carve(4 * ncap);
-  S.order = (lds_i32*)carve(4 * ncap);
-  S.gst = (lds_i32*)carve(4 * ncap);
-  S.cumnc = (lds_i32*)carve(4 * ncap);
+  S.x0 = (lds_u16*)(smem + ly.x0);
+  S.y0 = (lds_u16*)(smem + ly.y0);
+  S.x1 = (lds_u16*)(smem + ly.x1);
+  S.y1 = (lds_u16*)(smem + ly.y1);
+  S.cnt = (lds_u32*)(smem + ly.cnt);
+  S.seq = (lds_u32*)(smem + ly.seq);
+  S.prank = (lds_i32*)(smem + ly.prank);
+  S.order = (lds_i32*)(smem + ly.order);
+  S.gst = (lds_i32*)(smem + ly.gst);
+  S.cumnc = (lds_i32*)(smem + ly.cumnc);
   S.mid = (lds_u32*)S.cumnc;
-  S.krank = (lds_i32*)carve(4 * ncap);
-  S.cc = (lds_u32*)carve(16 * ncap);
+  S.krank = (lds_i32*)(smem + ly.krank);
+  S.cc = (lds_u32*)(smem + ly.cc);
   S.sortkey = (lds_u64*)S.cc;
   S.best = S.cc;
-  S.s_tmp = (lds_i32*)carve(4 * 36);
+  S.s_tmp = (lds_i32*)(smem + ly.tmp);
   S.s_ctl = S.s_tmp + 32;
   S.pp = 0;
-  lds_u32* k_lk = (lds_u32*)carve(4 * kcap);
-  lds_u16* k_node = (lds_u16*)carve(2 * kcap);
-  lds_u8* k_q = (lds_u8*)carve(kcap);
+  lds_u32* k_lk = (lds_u32*)(smem + ly.lk);
+  lds_u16* k_node = (lds_u16*)(smem + ly.knode);
+  lds_u8* k_q = (lds_u8*)(smem + ly.kq);
 
   // ---- cell offsets of this level's candidates
   const int nc = L0.cell_end - L0.cell_begin;
@@ -1495,11 +1516,15 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   }
   // keys in LDS up to what the node arrays leave of the CU's 160 KB (global scratch beyond)
-  const size_t node_lds = octree_node_lds_bytes(node_cap_);
-  const size_t lds_budget = 160 * 1024 - 1024;
-  key_cap_ = node_lds + octree_key_lds_bytes(256) <= lds_budget
-                 ? (int)std::min<size_t>(16384, (lds_budget - node_lds - 16) / 7) : 0;
-  octree_lds_ = node_lds + octree_key_lds_bytes(key_cap_);
+  const uint32_t lds_budget = 160 * 1024 - 1024;
+  key_cap_ = 0;  // largest multiple of 16 keys (<= 16384) whose carved layout fits the budget
+  for (int k = 16384; k >= 256; k -= 16)
+    if (oct_layout(node_cap_, k).end <= lds_budget) {
+      key_cap_ = k;
+      break;
+    }
+  octree_lds_ = oct_layout(node_cap_, key_cap_).end;
+  if (octree_lds_ > lds_budget) throw ArgError("octree node arrays exceed the LDS budget");
   MMT_HIP(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)octree_lds_));
   upload(&d_lv_, lv_);
@@ -1582,6 +1607,31 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
                      pyr_stride_, d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_,
                      d_kps, d_desc, cap_per_frame, d_n, nframes);
   MMT_HIP(hipGetLastError());
+}
+
+void OrbEngine::check_flags(hipStream_t stream) {
+  int flags = 0;
+  MMT_HIP(hipMemcpyAsync(&flags, d_err_, sizeof(int), hipMemcpyDeviceToHost, stream));
+  MMT_HIP(hipStreamSynchronize(stream));
+  if (flags == 0) return;
+  MMT_HIP(hipMemsetAsync(d_err_, 0, sizeof(int), stream));
+  MMT_HIP(hipStreamSynchronize(stream));
+  std::string what;
+  if (flags & 1) what += " octree-pass-guard";
+  if (flags & 2) what += " octree-node-capacity";
+  if (flags & 4) what += " octree-output-truncated";
+  char hex[16];
+  snprintf(hex, sizeof(hex), "0x%x", flags);
+  throw DeviceError(std::string("ORB device error flags ") + hex + ":" + what);
+}
+
+void OrbEngine::raise_flags(int flags, hipStream_t stream) {
+  int cur = 0;
+  MMT_HIP(hipMemcpyAsync(&cur, d_err_, sizeof(int), hipMemcpyDeviceToHost, stream));
+  MMT_HIP(hipStreamSynchronize(stream));
+  cur |= flags;
+  MMT_HIP(hipMemcpyAsync(d_err_, &cur, sizeof(int), hipMemcpyHostToDevice, stream));
+  MMT_HIP(hipStreamSynchronize(stream));
 }
 
 long OrbEngine::debug_fetch(int what, int frame, void* out, size_t cap, hipStream_t stream) {

@@ -300,7 +300,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   if (prof_) MMT_HIP(hipEventRecord(ev_orb_[1], st));
   std::vector<int> nkp(nframes);
   MMT_HIP(hipMemcpyAsync(nkp.data(), d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipStreamSynchronize(st));
+  engine_->check_flags(st);  // synchronises st; throws on a tripped octree guard
   if (prof_) {
     float ms = 0;
     MMT_HIP(hipEventElapsedTime(&ms, ev_orb_[0], ev_orb_[1]));

@@ -117,3 +117,23 @@ def test_orbextractor_mirror_api(kitti_frames, oracle_mod):
     _compare(k, d, kr, dr, "mirror")
     assert ex.GetLevels() == 8
     assert np.allclose(ex.GetScaleFactors(), oracle_mod.orb_config(2000)["scale"])
+
+
+def test_device_error_flags_are_reported(kitti_frames, oracle_mod):
+    """A tripped octree guard (pass limit, node capacity, output truncation) surfaces as
+    MMT_EDEVICE from the next synchronous call and from mmt_orb_device_status, then clears."""
+    ctx = _ctx(1242, 375, 2000)
+    gray = oracle_mod.gray_from_bgr(kitti_frames[0]["bgr"])
+    ctx.orb_extract(gray)
+    ctx.orb_device_status()  # clean
+    ctx.debug_orb_raise(4)
+    with pytest.raises(M.MmtError, match="octree-output-truncated"):
+        ctx.orb_extract(gray)
+    k, d = ctx.orb_extract(gray)  # cleared by the report
+    kr, dr = oracle_mod.orb_extract(gray, 2000)
+    _compare(k, d, kr, dr, "after flag reset")
+    ctx.debug_orb_raise(1 | 2)
+    with pytest.raises(M.MmtError, match="octree-pass-guard octree-node-capacity"):
+        ctx.orb_device_status()
+    ctx.orb_device_status()
+    ctx.close()

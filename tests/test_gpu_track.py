@@ -179,3 +179,18 @@ def test_track_synthetic_c4_sizes_matches_oracle(oracle_mod, w, h, seed):
     """BASELINE C4 geometries (KITTI 00 at 1241x376, 05/07 at 1226x370), 4000 features,
     ego + 3 moving boxes."""
     assert _synthetic_parity(w, h, 4000, 3, 5, seed) >= 1
+
+
+def test_track_reports_orb_device_flags(kitti_frames):
+    """TrackRGBD checks the ORB device error word at its host sync: a tripped octree guard is an
+    error return, not a frame tracked on truncated keypoints."""
+    import multimot_track_amd as M
+    c = M.Context(M.kitti03_config(nfeatures=2000))
+    f = kitti_frames[0]
+    c.debug_orb_raise(2)
+    with pytest.raises(M.MmtError, match="octree-node-capacity"):
+        c.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+    c.reset()
+    r = c.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+    assert r["n_keys"] > 500
+    c.close()
