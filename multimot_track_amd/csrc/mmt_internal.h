@@ -102,14 +102,17 @@ class OrbEngine {
   int total_slots_ = 0, out_slots_ = 0, cap_frame_ = 0, node_cap_ = 0;
   int key_cap_ = 0;          // k_octree: keys per (level, frame) held in LDS
   size_t octree_lds_ = 0;    // k_octree dynamic LDS bytes
-  hipStream_t side_ = nullptr;  // k_blur runs here, overlapping FAST + octree
-  hipEvent_t ev_pyr_ = nullptr, ev_blur_ = nullptr, ev_gray_ = nullptr, ev_fast0_ = nullptr;
+  // One side stream beside the caller's (run()): a process has 4 hardware queues
+  // (GPU_MAX_HW_QUEUES), and streams beyond them end up sharing the caller's queue.
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_pyr_ = nullptr, ev_blur_ = nullptr, ev_gray_ = nullptr;
   int iniTh_ = 20, minTh_ = 7;
   size_t pyr_stride_ = 0;
   std::vector<LevelInfo> lv_;
   std::vector<CellInfo> cells_;
   std::vector<int> xtab_off_, ytab_off_;
   std::vector<int> rs_pitch_, rs_lds_;  // k_resize LDS row pitch and bytes per level
+  int sched_ = 0;  // MMT_ORB_SCHED=2: one stream (standalone kernel times for profiling)
   LevelInfo* d_lv_ = nullptr;
   CellInfo* d_cells_ = nullptr;
   ResizeX* d_xtab_ = nullptr;

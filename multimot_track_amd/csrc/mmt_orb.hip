@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -258,14 +259,51 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Compass pre-test: is some pair of adjacent compass points (0/4/8/12) both darker or both
-// brighter than the centre by more than th?
-__device__ __forceinline__ bool compass_pass(int v, int q0, int q4, int q8, int q12, int th) {
-  const int d0 = v - q0, d4 = v - q4, d8 = v - q8, d12 = v - q12;
-  const bool k0 = d0 > th, k4 = d4 > th, k8 = d8 > th, k12 = d12 > th;
-  const bool b0 = d0 < -th, b4 = d4 < -th, b8 = d8 < -th, b12 = d12 < -th;
-  return (k0 && k4) || (k4 && k8) || (k8 && k12) || (k12 && k0) || (b0 && b4) || (b4 && b8) ||
-         (b8 && b12) || (b12 && b0);
+// Inclusive prefix sum over the 64 lanes of a wave with DPP (row shifts within rows of 16, then
+// the row broadcasts of GFX9): no LDS round trips.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Compass pre-test of four adjacent pixels at once (packed u16 halves, saturating arithmetic):
+// is some pair of adjacent compass points (0/4/8/12) both darker or both brighter than the
+// centre by more than th?  Adjacent pairs: (b0 && b4) || (b4 && b8) || (b8 && b12) || (b12 && b0)
+// == (b0 || b8) && (b4 || b12).  sat(q - (v + th)) is nonzero iff q > v + th, sat((v - th) - q)
+// nonzero iff q < v - th, so OR is bitwise or and AND is min of the saturated differences.
+// c/dn/rt/up/lf hold the centre and the compass points 0 (down 3), 4 (right 3), 8 (up 3),
+// 12 (left 3) of pixels 0..3 in bytes 0..3; returns the 4-bit mask of passing pixels.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+
+__device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t dn, uint32_t rt, uint32_t up,
+                                             uint32_t lf, uint32_t th2) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;  // bytes (1, 3) or (0, 2) -> u16 halves
+    const u16x2 v = as_u16x2(__builtin_amdgcn_perm(0u, c, sel));
+    const u16x2 q0 = as_u16x2(__builtin_amdgcn_perm(0u, dn, sel));
+    const u16x2 q4 = as_u16x2(__builtin_amdgcn_perm(0u, rt, sel));
+    const u16x2 q8 = as_u16x2(__builtin_amdgcn_perm(0u, up, sel));
+    const u16x2 q12 = as_u16x2(__builtin_amdgcn_perm(0u, lf, sel));
+    const u16x2 t = as_u16x2(th2);
+    const u16x2 hi = v + t, lo = __builtin_elementwise_sub_sat(v, t);
+    const u16x2 br = __builtin_elementwise_min(
+        __builtin_elementwise_sub_sat(q0, hi) | __builtin_elementwise_sub_sat(q8, hi),
+        __builtin_elementwise_sub_sat(q4, hi) | __builtin_elementwise_sub_sat(q12, hi));
+    const u16x2 dk = __builtin_elementwise_min(
+        __builtin_elementwise_sub_sat(lo, q0) | __builtin_elementwise_sub_sat(lo, q8),
+        __builtin_elementwise_sub_sat(lo, q4) | __builtin_elementwise_sub_sat(lo, q12));
+    const u16x2 one = {1, 1};
+    m |= __builtin_bit_cast(uint32_t, __builtin_elementwise_min(br | dk, one)) << h;
+  }
+  return (m & 3u) | ((m >> 14) & 0xCu);  // bits 0/1 (pixels 0, 1), 16/17 (pixels 2, 3)
 }
 
 // LDS bytes of one wave's FAST workspace: tile and arc-strength map (rows x kFS each) and the
@@ -276,12 +314,14 @@ __host__ __device__ constexpr int fast_wave_lds(int kFS, int rows_max, int win_m
 
 // One wave per (cell, frame); four cells per workgroup.  Cell = the submatrix the reference hands
 // to cv::FAST (ORBextractor.cc:791-816).  The wave stages the cell in its own LDS tile (row
-// stride kFS) and keeps an arc-strength map of the same shape, zero except at the candidates of
-// the current pass, so out-of-window NMS neighbours read 0 without bounds checks.  Per threshold
-// (iniTh, then minTh if the cell came out empty, ORBextractor.cc:809-816):
-//  1) compass pre-test at th over the window (2 rows x 32 columns or 1 row x 64 columns per
-//     wave step): a 9-arc covers two adjacent compass points (0/4/8/12), so a pixel whose pairs
-//     all fail has M <= th and is no corner; survivors are compacted in row-major order;
+// stride kFS, tile column c at LDS column c + 1 so the detection window starts on a dword) and
+// keeps an arc-strength map of the same shape, zero except at the candidates of the current
+// pass, so out-of-window NMS neighbours read 0 without bounds checks.  Per threshold (iniTh,
+// then minTh if the cell came out empty, ORBextractor.cc:809-816):
+//  1) compass pre-test at th over the window, four pixels per lane (one aligned dword of the
+//     window row, packed u16 arithmetic): a 9-arc covers two adjacent compass points (0/4/8/12),
+//     so a pixel whose pairs all fail has M <= th and is no corner; survivors are compacted in
+//     row-major order (lanes are row-major groups of four pixels);
 //  2) arc strength M of the candidates;
 //  3) cell-local 3x3 strict NMS on scores s = (M > th ? M - 1 : 0) over the candidate list,
 //     neighbours scored on the fly from the map; ballot compaction keeps row-major order.
@@ -305,12 +345,13 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
   const int frame = blockIdx.y;
   const LevelInfo L = lv[ci.level];
   const uint8_t* img = pyr + (size_t)frame * pyr_stride + L.off;
-  const int rows = ci.rows, nq = (ci.cols + 3) >> 2;  // dwords per tile row
+  const int rows = ci.rows, nq = (ci.cols + 4) >> 2;  // dwords per LDS row (tile shifted by 1)
   {
-    // dword copy (the pyramid allocation has slack for the <= 3 bytes past the last row); every
-    // load of the first kStage rounds is issued before the first LDS store
+    // dword copy from one byte before the tile (c0 >= 16; the pyramid allocation has slack for
+    // the <= 3 bytes read past the last row); every load of the first kStage rounds is issued
+    // before the first LDS store
     const float inv_nq = 1.0f / (float)nq;
-    const uint8_t* src = img + (size_t)ci.r0 * L.w + ci.c0;
+    const uint8_t* src = img + (size_t)ci.r0 * L.w + ci.c0 - 1;
     const int items = rows * nq;
     constexpr int kStage = 8;
     uint32_t v[kStage];
@@ -334,47 +375,51 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
     for (int i = lane; i < rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
   }
   wave_sync();
-  const int R = rows - 6, C = ci.cols - 6;  // detection window: tile rows 3..rows-4, cols 3..C+2
-  // pre-test lane mapping: lg = log2(columns per step), rows per step = 64 >> lg
-  const int lg = C <= 32 ? 5 : 6;
-  const int col = lane & ((1 << lg) - 1), rsub = lane >> lg, rstep = 64 >> lg;
+  const int R = rows - 6, C = ci.cols - 6;  // detection window: tile rows 3..R+2, cols 3..C+2
+  // pre-test lane mapping: gs groups of four pixels per row (power of two), 64 / gs rows per step
+  const int G = (C + 3) >> 2, lgg = G <= 8 ? 3 : 4;
+  const int grp = lane & ((1 << lgg) - 1), rsub = lane >> lgg, rstep = 64 >> lgg;
+  const int nvalid = C - 4 * grp;  // window pixels of this lane's group
+  const uint32_t colmask = grp < G ? (nvalid >= 4 ? 0xFu : (1u << nvalid) - 1u) : 0u;
+  const uint32_t* t32 = (const uint32_t*)tile;
+  constexpr int kRow32 = kFS / 4;  // dwords per LDS row
   uint32_t* out = keys + (size_t)frame * total_slots + ci.slot_off;
   const unsigned long long lt = (1ull << lane) - 1ull;
   int count = 0, ncand = 0;
   for (int pass = 0; pass < 2; pass++) {
     const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
+    const uint32_t th2 = (uint32_t)th | ((uint32_t)th << 16);
     if (pass) {  // clear pass 0's candidates from the map
       for (int k = lane; k < ncand; k += 64) arcm[cand_list[k]] = 0;
       wave_sync();
     }
     ncand = 0;
-    // two wave steps per iteration: all ten reads are issued before the first test
-    for (int r0 = 0; r0 < R; r0 += 2 * rstep) {
-      const int ra = r0 + rsub, rb = ra + rstep;
-      const int pa = (ra + 3) * kFS + col + 3, pb = pa + rstep * kFS;  // tile positions
-      const bool ina = ra < R && col < C, inb = rb < R && col < C;
-      int va = 0, a0 = 0, a4 = 0, a8 = 0, a12 = 0, vb = 0, b0 = 0, b4 = 0, b8 = 0, b12 = 0;
-      if (ina) {
-        const uint8_t* t = tile + pa;
-        va = t[0]; a0 = t[3 * kFS]; a4 = t[3]; a8 = t[-3 * kFS]; a12 = t[-3];
+    for (int r0 = 0; r0 < R; r0 += rstep) {
+      const int wr = r0 + rsub;
+      uint32_t m = 0;
+      const int base = (wr + 3) * kRow32 + 1 + grp;  // dword of window pixels 4 grp .. 4 grp + 3
+      if (wr < R && colmask) {
+        const uint32_t c = t32[base], cp = t32[base - 1], cn = t32[base + 1];
+        const uint32_t up = t32[base - 3 * kRow32], dn = t32[base + 3 * kRow32];
+        m = compass4(c, dn, __builtin_amdgcn_alignbyte(cn, c, 3), up,
+                     __builtin_amdgcn_alignbyte(c, cp, 1), th2) & colmask;
       }
-      if (inb) {
-        const uint8_t* t = tile + pb;
-        vb = t[0]; b0 = t[3 * kFS]; b4 = t[3]; b8 = t[-3 * kFS]; b12 = t[-3];
+      const int n = __popc(m);
+      const int incl = wave_incl_scan(n);
+      int slot = ncand + incl - n;
+      ncand += __builtin_amdgcn_readlane(incl, 63);
+      const int p0 = 4 * base;  // LDS byte position of pixel 0 of the group
+      while (m) {
+        const int j = __builtin_ctz(m);
+        cand_list[slot++] = (uint16_t)(p0 + j);
+        m &= m - 1;
       }
-      const bool ca = ina && compass_pass(va, a0, a4, a8, a12, th);
-      const bool cb = inb && compass_pass(vb, b0, b4, b8, b12, th);
-      const unsigned long long bala = __ballot(ca), balb = __ballot(cb);
-      if (ca) cand_list[ncand + __popcll(bala & lt)] = (uint16_t)pa;
-      ncand += __popcll(bala);
-      if (cb) cand_list[ncand + __popcll(balb & lt)] = (uint16_t)pb;
-      ncand += __popcll(balb);
     }
     wave_sync();
     for (int k = lane; k < ncand; k += 64) {
       const int p = cand_list[k];
-      const int m = arc_strength<kFS>(tile + p);
-      arcm[p] = (uint8_t)(m < 0 ? 0 : m);
+      const int mm = arc_strength<kFS>(tile + p);
+      arcm[p] = (uint8_t)(mm < 0 ? 0 : mm);
     }
     wave_sync();
     int base = 0;
@@ -385,20 +430,20 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
       if (k < ncand) {
         p = cand_list[k];
         const uint8_t* a = arcm + p;
-        const int m = a[0];
-        if (m > th) {
-          sc = m - 1;
-          const int n[8] = {a[-kFS - 1], a[-kFS], a[-kFS + 1], a[-1],
-                            a[1],        a[kFS - 1], a[kFS], a[kFS + 1]};
+        const int mm = a[0];
+        if (mm > th) {
+          sc = mm - 1;
+          const int n8[8] = {a[-kFS - 1], a[-kFS], a[-kFS + 1], a[-1],
+                             a[1],        a[kFS - 1], a[kFS], a[kFS + 1]};
           int nmax = 0;
 #pragma unroll
-          for (int j = 0; j < 8; j++) nmax = max(nmax, n[j] > th ? n[j] - 1 : 0);
+          for (int j = 0; j < 8; j++) nmax = max(nmax, n8[j] > th ? n8[j] - 1 : 0);
           keep = sc > nmax;
         }
       }
       const unsigned long long bal = __ballot(keep);
       if (keep) {
-        const int tr = p / kFS, tc = p - tr * kFS;
+        const int tr = p / kFS, tc = p - tr * kFS - 1;  // LDS column = tile column + 1
         const uint32_t x = (uint32_t)(ci.c0 - kMinBorder + tc);
         const uint32_t y = (uint32_t)(ci.r0 - kMinBorder + tr);
         const int slot = base + __popcll(bal & lt);
@@ -423,17 +468,6 @@ typedef LDS int lds_i32;
 typedef LDS uint8_t lds_u8;
 typedef LDS unsigned long long lds_u64;
 
-// Inclusive prefix sum over the 64 lanes of a wave with DPP (row shifts within rows of 16, then
-// the row broadcasts of GFX9): no LDS round trips.
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
-  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
-  return v;
-}
 
 // In-place exclusive scan of LDS ints a[0..n) by the whole workgroup; returns the total.  One
 // barrier: wave totals go to one of two alternating LDS slots, every thread sums the ones before
@@ -1195,6 +1229,38 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {
   return a;
 }
 
+// sin and cos of x in [0, 2pi] in double precision: Cody-Waite reduction by pi/2 (k <= 4, so
+// k * PIO2_HI is exact) and the fdlibm kernels __kernel_sin / __kernel_cos (|r| <= pi/4, error
+// < 1 ulp), evaluated without contraction like the C they come from.  Rounded to float this
+// equals (float)cos((double)x) / (float)sin((double)x) of the host libm unless the double lies
+// within an ulp of a float rounding boundary; it replaces OCML's general sin/cos (about 200
+// FP64 instructions with the large-argument path) on the descriptor's critical chain.
+__device__ __forceinline__ void sincos_small(double x, double* s_out, double* c_out) {
+  const double PIO2_HI = 1.57079632673412561417e+00, PIO2_LO = 6.07710050650619224932e-11;
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double kd = __builtin_rint(x * 6.36619772367581382433e-01);  // x * 2/pi
+  const int k = (int)kd;
+  const double r = (x - kd * PIO2_HI) - kd * PIO2_LO;
+  const double z = r * r;
+  const double v = z * r;
+  const double ps = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  const double sn = r + v * (S1 + z * ps);
+  const double pc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double cs = w + (((1.0 - w) - hz) + z * pc);
+  switch (k & 3) {
+    case 0: *s_out = sn; *c_out = cs; break;
+    case 1: *s_out = cs; *c_out = -sn; break;
+    case 2: *s_out = -sn; *c_out = -cs; break;
+    default: *s_out = -cs; *c_out = sn; break;
+  }
+}
+
 // Four output keypoint slots per wave, 16 lanes each: IC_Angle on the level (:77-104),
 // rotated BRIEF on the blurred level (:108-147), level-major assembly with coordinate scaling
 // (:1079-1108). Every load of a slot is independent of the others (no dependent chains), so a
@@ -1213,10 +1279,19 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     int nframes) {
   const int lane = threadIdx.x & 63;
   const int gl = lane & 15, grp = lane >> 4;
-  const int slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + grp;
-  const int frame = slot / out_slots;
+  __shared__ uint32_t od_pat[256];  // the packed test pattern, once per workgroup
+  od_pat[threadIdx.x] = c_pattern.t[threadIdx.x];
+  __syncthreads();
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b % 8 share one; speed
+  // only, never correctness), so workgroup b serves frame (b % 8) + 8 * (b / 8 / wgf): the
+  // slots of a frame run on one XCD, whose L2 then holds that frame's level and blurred level
+  // rows across the overlapping patches of its keypoints
+  const int wgf = (out_slots + 15) / 16;  // workgroups per frame (16 slots each)
+  const int jx = blockIdx.x >> 3;
+  const int frame = (blockIdx.x & 7) + 8 * (jx / wgf);
   if (frame >= nframes) return;  // whole 16-lane groups leave together
-  const int local = slot - frame * out_slots;
+  const int local = (jx % wgf) * 16 + (threadIdx.x >> 6) * 4 + grp;
+  if (local >= out_slots) return;
   // level lookup: lane gl of the group holds level gl's slot offset and count (nlevels <= 16);
   // the level is a ballot count within the group and the keys before it a group sum
   const uint32_t k = okeys[(size_t)frame * out_slots + local];
@@ -1252,7 +1327,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   // BRIEF tests 16r + gl of this lane (r = 0..15), fetched while the disc loads are in flight
   uint32_t pat[16];
 #pragma unroll
-  for (int r = 0; r < 16; r++) pat[r] = c_pattern.t[16 * r + gl];
+  for (int r = 0; r < 16; r++) pat[r] = od_pat[16 * r + gl];
   // --- IC_Angle: lane gl owns disc columns c0 = 2gl-15 and c0+1 (column 16 does not exist; the
   // keypoint border, >= 19 px, keeps its byte inside the level)
   const int c0 = 2 * gl - 15, c1 = c0 + 1;
@@ -1290,7 +1365,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   // --- rotated BRIEF; cos/sin pinned to (float)cos((double)angle) (parity hazards)
   const float factorPI = (float)(3.14159265358979323846 / 180.0);
   const float ang = angle * factorPI;
-  const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+  double sd, cd;
+  sincos_small((double)ang, &sd, &cd);
+  const float a = (float)cd, b = (float)sd;
   const uint8_t* center = blur + fo + (size_t)ky * Lw + kx;
   int bits[16];
 #pragma unroll
@@ -1345,13 +1422,11 @@ void OrbEngine::release() {
   d_pyr_ = d_blur_ = nullptr;
   d_keys_ = d_lkeys_ = d_knode_ = d_okeys_ = nullptr;
   d_cellcnt_ = d_ocount_ = d_err_ = nullptr;
-  if (ev_pyr_) (void)hipEventDestroy(ev_pyr_);
-  if (ev_blur_) (void)hipEventDestroy(ev_blur_);
-  if (ev_gray_) (void)hipEventDestroy(ev_gray_);
-  if (ev_fast0_) (void)hipEventDestroy(ev_fast0_);
-  ev_gray_ = ev_fast0_ = nullptr;
+  for (hipEvent_t* e : {&ev_pyr_, &ev_blur_, &ev_gray_}) {
+    if (*e) (void)hipEventDestroy(*e);
+    *e = nullptr;
+  }
   if (side_) (void)hipStreamDestroy(side_);
-  ev_pyr_ = ev_blur_ = nullptr;
   side_ = nullptr;
 }
 
@@ -1412,10 +1487,10 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
         c.c0 = (int)iniX;
         c.rows = (int)maxY - (int)iniY;
         c.cols = (int)maxX - (int)iniX;
-        if (c.rows > kFSMax || ((c.cols + 3) & ~3) > kFSMax || c.cols - 6 > 64)
+        if (c.rows > kFSMax || ((c.cols + 4) & ~3) > kFSMax || c.cols - 6 > 64)
           throw ArgError("FAST cell larger than the LDS tile");
         fast_rows_max_ = std::max(fast_rows_max_, c.rows);
-        fast_cols_max_ = std::max(fast_cols_max_, (c.cols + 3) & ~3);
+        fast_cols_max_ = std::max(fast_cols_max_, (c.cols + 4) & ~3);  // tile at LDS column 1
         fast_win_max_ = std::max(fast_win_max_, std::max(c.rows - 6, 0) * std::max(c.cols - 6, 0));
         const int R = std::max(c.rows - 6, 0), C = std::max(c.cols - 6, 0);
         c.slot_cap = ((R + 1) / 2) * ((C + 1) / 2);  // max strict-NMS survivors
@@ -1498,6 +1573,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   }
   ncells_ = (int)cells_.size();
   ntiles_ = (int)tiles.size();
+  if (const char* e = getenv("MMT_ORB_SCHED")) sched_ = atoi(e);
   total_slots_ = key_off;
   out_slots_ = out_off;
   cap_frame_ = out_off;
@@ -1535,7 +1611,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   upload(&d_umax_, t.umax);
   const size_t B = (size_t)max_batch_;
   MMT_HIP(hipMalloc((void**)&d_pyr_, B * pyr_stride_ + 64));  // + dword over-read slack
-  MMT_HIP(hipMalloc((void**)&d_blur_, B * pyr_stride_));
+  MMT_HIP(hipMalloc((void**)&d_blur_, B * pyr_stride_ + 64));  // + aligned over-read slack
   MMT_HIP(hipMalloc((void**)&d_keys_, B * total_slots_ * sizeof(uint32_t)));
   MMT_HIP(hipMalloc((void**)&d_lkeys_, B * total_slots_ * sizeof(uint32_t)));
   // knode (u32 per slot) followed by the per-key quadrant bytes (u8 per slot)
@@ -1545,10 +1621,8 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   MMT_HIP(hipMalloc((void**)&d_ocount_, B * nlevels_ * sizeof(int)));
   MMT_HIP(hipMalloc((void**)&d_err_, sizeof(int)));
   MMT_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-  MMT_HIP(hipEventCreateWithFlags(&ev_pyr_, hipEventDisableTiming));
-  MMT_HIP(hipEventCreateWithFlags(&ev_blur_, hipEventDisableTiming));
-  MMT_HIP(hipEventCreateWithFlags(&ev_gray_, hipEventDisableTiming));
-  MMT_HIP(hipEventCreateWithFlags(&ev_fast0_, hipEventDisableTiming));
+  for (hipEvent_t* e : {&ev_pyr_, &ev_blur_, &ev_gray_})
+    MMT_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
 }
 
@@ -1578,32 +1652,51 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
                        ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,
                        out_slots_, d_ocount_, nlevels_, node_cap_, key_cap_, l0, d_err_);
   };
-  // Two chains that meet before orientation:
-  //   side:  FAST + octree of level 0 (they need only the gray frames), then the Gaussian blur
-  //   main:  the (latency-bound) resize chain, FAST + octree of levels 1..
-  MMT_HIP(hipEventRecord(ev_gray_, stream));
-  MMT_HIP(hipStreamWaitEvent(side_, ev_gray_, 0));
-  fast(lv_[0].cell_begin, lv_[0].cell_end, side_);
-  octree(0, 1, side_);
-  for (int l = 1; l < nlevels_; l++) {
+  auto resize = [&](int l, hipStream_t st) {
     const LevelInfo& S = lv_[l - 1];
     const LevelInfo& L = lv_[l];
     dim3 grid((L.w + kResizeCols - 1) / kResizeCols, (L.h + kResizeRows - 1) / kResizeRows,
               nframes);
-    hipLaunchKernelGGL(k_resize, grid, dim3(256), rs_lds_[l], stream, d_pyr_, pyr_stride_, S.off,
+    hipLaunchKernelGGL(k_resize, grid, dim3(256), rs_lds_[l], st, d_pyr_, pyr_stride_, S.off,
                        S.w, L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l],
                        rs_pitch_[l]);
+  };
+  auto blur = [&](hipStream_t st) {
+    hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, st, d_pyr_,
+                       d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
+  };
+  auto cells = [&](int l) { return std::make_pair(lv_[l].cell_begin, lv_[l].cell_end); };
+  const int NL = nlevels_;
+  if (sched_ & 2) {  // one stream: standalone kernel times (profiling)
+    fast(cells(0).first, cells(0).second, stream);
+    octree(0, 1, stream);
+    for (int l = 1; l < NL; l++) resize(l, stream);
+    blur(stream);
+    fast(cells(0).second, ncells_, stream);
+    if (NL > 1) octree(1, NL, stream);
+  } else {
+    // Two chains that meet before orientation:
+    //   side:  FAST + octree of level 0 (they need only the gray frames), then the blur of
+    //          every level once the pyramid is complete
+    //   main:  the (latency-bound) chain of k_resize launches, FAST + octree of levels 1..
+    // Tried and measured equal or slower (the window is throughput-bound once FAST overlaps
+    // the chain): FAST per level as each level lands, FAST of levels 1-3 beside the chain, one
+    // octree launch for every level, the chain on a high-priority stream.
+    MMT_HIP(hipEventRecord(ev_gray_, stream));
+    MMT_HIP(hipStreamWaitEvent(side_, ev_gray_, 0));
+    fast(cells(0).first, cells(0).second, side_);
+    octree(0, 1, side_);
+    for (int l = 1; l < NL; l++) resize(l, stream);
+    MMT_HIP(hipEventRecord(ev_pyr_, stream));
+    MMT_HIP(hipStreamWaitEvent(side_, ev_pyr_, 0));
+    blur(side_);
+    MMT_HIP(hipEventRecord(ev_blur_, side_));
+    fast(cells(0).second, ncells_, stream);
+    if (NL > 1) octree(1, NL, stream);
+    MMT_HIP(hipStreamWaitEvent(stream, ev_blur_, 0));
   }
-  MMT_HIP(hipEventRecord(ev_pyr_, stream));
-  MMT_HIP(hipStreamWaitEvent(side_, ev_pyr_, 0));
-  hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, side_, d_pyr_,
-                     d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
-  MMT_HIP(hipEventRecord(ev_blur_, side_));
-  fast(lv_[0].cell_end, ncells_, stream);
-  if (nlevels_ > 1) octree(1, nlevels_, stream);
-  MMT_HIP(hipStreamWaitEvent(stream, ev_blur_, 0));
-  const int waves = (nframes * out_slots_ + 3) / 4;
-  hipLaunchKernelGGL(k_orient_desc, dim3((waves + 3) / 4), dim3(256), 0, stream, d_pyr_, d_blur_,
+  const int od_grid = 8 * ((nframes + 7) / 8) * ((out_slots_ + 15) / 16);  // see k_orient_desc
+  hipLaunchKernelGGL(k_orient_desc, dim3(od_grid), dim3(256), 0, stream, d_pyr_, d_blur_,
                      pyr_stride_, d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_,
                      d_kps, d_desc, cap_per_frame, d_n, nframes);
   MMT_HIP(hipGetLastError());
