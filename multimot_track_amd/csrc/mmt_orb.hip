@@ -199,44 +199,45 @@ typedef short short2v __attribute__((ext_vector_type(2)));
 // address.  40 covers the ~31-pixel cells of any image (tile = cell + 6); 72 is the general case.
 constexpr int kFSSmall = 40, kFSMax = 72;
 
-// (d, -d) per circle point as a packed int16 pair: the dark test (min of v - p over a 9-arc) and
-// the bright test (min of p - v) run in the two halves of one v_pk_min_i16 / v_pk_max_i16 chain.
+// Circle differences as packed f16 pairs (v - q, q - v): every value is an integer of
+// magnitude <= 255, exact in f16, and min / max are exact, so the result equals the integer
+// formulation.  The pair comes from one v_pk_add_f16 (op_sel / neg modifiers on the scalar
+// halves), the 9-arc minima from two rounds of 3-input v_pk_minimum3_f16 (arc k = d[k..k+2],
+// d[k+3..k+5], d[k+6..k+8]) and the maximum over arcs from v_pk_maximum3_f16: about half the
+// instructions of the 2-input integer min/max chain.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
 template <int kFS>
 __device__ __forceinline__ int arc_strength(const uint8_t* t) {
-  const int v = t[0];
-  int q[16];
-  q[0] = t[3 * kFS];
-  q[1] = t[3 * kFS + 1];
-  q[2] = t[2 * kFS + 2];
-  q[3] = t[kFS + 3];
-  q[4] = t[3];
-  q[5] = t[-kFS + 3];
-  q[6] = t[-2 * kFS + 2];
-  q[7] = t[-3 * kFS + 1];
-  q[8] = t[-3 * kFS];
-  q[9] = t[-3 * kFS - 1];
-  q[10] = t[-2 * kFS - 2];
-  q[11] = t[-kFS - 3];
-  q[12] = t[-3];
-  q[13] = t[kFS - 3];
-  q[14] = t[2 * kFS - 2];
-  q[15] = t[3 * kFS - 1];
-  short2v d[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) d[k] = short2v{(short)(v - q[k]), (short)(q[k] - v)};
-  short2v mn2[16], mn4[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) mn2[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
-#pragma unroll
-  for (int k = 0; k < 16; k++) mn4[k] = __builtin_elementwise_min(mn2[k], mn2[(k + 2) & 15]);
-  short2v best = short2v{-1000, -1000};
+  const int off[16] = {3 * kFS,     3 * kFS + 1,  2 * kFS + 2,  kFS + 3,
+                       3,           -kFS + 3,     -2 * kFS + 2, -3 * kFS + 1,
+                       -3 * kFS,    -3 * kFS - 1, -2 * kFS - 2, -kFS - 3,
+                       -3,          kFS - 3,      2 * kFS - 2,  3 * kFS - 1};
+  const _Float16 v = (_Float16)(unsigned)t[0];
+  h2v d[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const short2v mn9 = __builtin_elementwise_min(
-        __builtin_elementwise_min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-    best = __builtin_elementwise_max(best, mn9);
+    const _Float16 q = (_Float16)(unsigned)t[off[k]];
+    d[k] = (h2v){v, -v} + (h2v){-q, q};
   }
-  return max((int)best.x, (int)best.y);
+  h2v m3[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    m3[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[k], d[(k + 1) & 15]),
+                                          d[(k + 2) & 15]);
+  h2v mx[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) mx[j] = (h2v){(_Float16)-1000.f, (_Float16)-1000.f};
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const h2v mn9 = __builtin_elementwise_minimum(
+        __builtin_elementwise_minimum(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]);
+    mx[k % 6] = __builtin_elementwise_maximum(mx[k % 6], mn9);
+  }
+  const h2v b = __builtin_elementwise_maximum(
+      __builtin_elementwise_maximum(__builtin_elementwise_maximum(mx[0], mx[1]), mx[2]),
+      __builtin_elementwise_maximum(__builtin_elementwise_maximum(mx[3], mx[4]), mx[5]));
+  return (int)(float)__builtin_elementwise_maximum(b.x, b.y);
 }
 
 // p -> (p / C, p % C) for p < 2^13, C <= 72: (p + 0.5) / C sits at least 0.5 / C away from an
@@ -335,6 +336,12 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
                                               int rows_max, int win_max, int cell_begin,
                                               int cell_end) {
   extern __shared__ __attribute__((aligned(16))) uint8_t fast_lds[];
+#ifdef MMT_FAST_PROFILE
+  long long fp_t = clock64(), fp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define FP_T(k) do { long long _n = clock64(); fp[k] += _n - fp_t; fp_t = _n; } while (0)
+#else
+#define FP_T(k) do {} while (0)
+#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cell = cell_begin + blockIdx.x * 4 + wave;
   if (cell >= cell_end) return;
@@ -375,6 +382,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
     for (int i = lane; i < rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
   }
   wave_sync();
+  FP_T(0);
   const int R = rows - 6, C = ci.cols - 6;  // detection window: tile rows 3..R+2, cols 3..C+2
   // pre-test lane mapping: gs groups of four pixels per row (power of two), 64 / gs rows per step
   const int G = (C + 3) >> 2, lgg = G <= 8 ? 3 : 4;
@@ -389,57 +397,82 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
   for (int pass = 0; pass < 2; pass++) {
     const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
     const uint32_t th2 = (uint32_t)th | ((uint32_t)th << 16);
-    if (pass) {  // clear pass 0's candidates from the map
-      for (int k = lane; k < ncand; k += 64) arcm[cand_list[k]] = 0;
+    if (pass && minTh > iniTh) {  // pass 0's candidates are then no subset of pass 1's
+      for (int i = lane; i < rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
       wave_sync();
     }
+    // (with minTh <= iniTh, pass 0's candidates are pass 1's too and their arc strengths, which
+    // do not depend on the threshold, stay valid in the map)
     ncand = 0;
-    for (int r0 = 0; r0 < R; r0 += rstep) {
-      const int wr = r0 + rsub;
-      uint32_t m = 0;
-      const int base = (wr + 3) * kRow32 + 1 + grp;  // dword of window pixels 4 grp .. 4 grp + 3
-      if (wr < R && colmask) {
-        const uint32_t c = t32[base], cp = t32[base - 1], cn = t32[base + 1];
-        const uint32_t up = t32[base - 3 * kRow32], dn = t32[base + 3 * kRow32];
-        m = compass4(c, dn, __builtin_amdgcn_alignbyte(cn, c, 3), up,
-                     __builtin_amdgcn_alignbyte(c, cp, 1), th2) & colmask;
+    // two wave steps per iteration: the ten dword reads of both are in flight together
+    for (int r0 = 0; r0 < R; r0 += 2 * rstep) {
+      uint32_t m[2];
+      int base[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int wr = r0 + u * rstep + rsub;
+        base[u] = (wr + 3) * kRow32 + 1 + grp;  // dword of window pixels 4 grp .. 4 grp + 3
+        m[u] = 0;
+        if (wr < R && colmask) {
+          const int bb = base[u];
+          const uint32_t c = t32[bb], cp = t32[bb - 1], cn = t32[bb + 1];
+          const uint32_t up = t32[bb - 3 * kRow32], dn = t32[bb + 3 * kRow32];
+          m[u] = compass4(c, dn, __builtin_amdgcn_alignbyte(cn, c, 3), up,
+                          __builtin_amdgcn_alignbyte(c, cp, 1), th2) & colmask;
+        }
       }
-      const int n = __popc(m);
-      const int incl = wave_incl_scan(n);
-      int slot = ncand + incl - n;
-      ncand += __builtin_amdgcn_readlane(incl, 63);
-      const int p0 = 4 * base;  // LDS byte position of pixel 0 of the group
-      while (m) {
-        const int j = __builtin_ctz(m);
-        cand_list[slot++] = (uint16_t)(p0 + j);
-        m &= m - 1;
+      // candidates of step 0 precede those of step 1 (row-major): one scan of n0 + (n1 << 16)
+      const int n0 = __popc(m[0]), n1 = __popc(m[1]);
+      const int incl = wave_incl_scan(n0 | (n1 << 16));
+      const int tot = __builtin_amdgcn_readlane(incl, 63);
+      int slot0 = ncand + (incl & 0xFFFF) - n0;
+      int slot1 = ncand + (tot & 0xFFFF) + (incl >> 16) - n1;
+      ncand += (tot & 0xFFFF) + (tot >> 16);
+      uint32_t ma = m[0], mb = m[1];
+      while (ma) {
+        cand_list[slot0++] = (uint16_t)(4 * base[0] + __builtin_ctz(ma));
+        ma &= ma - 1;
+      }
+      while (mb) {
+        cand_list[slot1++] = (uint16_t)(4 * base[1] + __builtin_ctz(mb));
+        mb &= mb - 1;
       }
     }
     wave_sync();
-    for (int k = lane; k < ncand; k += 64) {
-      const int p = cand_list[k];
-      const int mm = arc_strength<kFS>(tile + p);
-      arcm[p] = (uint8_t)(mm < 0 ? 0 : mm);
-    }
-    wave_sync();
-    int base = 0;
+    FP_T(1 + 3 * pass);
+    // arc strengths into the map; corners (M > th) are compacted in place at the front of the
+    // candidate list (a write never passes the iteration's reads), keeping row-major order
+    int ncorner = 0;
     for (int k0 = 0; k0 < ncand; k0 += 64) {
+      const int k = k0 + lane;
+      int p = 0, mm = 0;
+      if (k < ncand) {
+        p = cand_list[k];
+        mm = arc_strength<kFS>(tile + p);
+        arcm[p] = (uint8_t)(mm < 0 ? 0 : mm);
+      }
+      const bool corner = k < ncand && mm > th;
+      const unsigned long long bc = __ballot(corner);
+      if (corner) cand_list[ncorner + __popcll(bc & lt)] = (uint16_t)p;
+      ncorner += __popcll(bc);
+    }
+    wave_sync();
+    FP_T(2 + 3 * pass);
+    int base = 0;
+    for (int k0 = 0; k0 < ncorner; k0 += 64) {  // cell-local 3x3 NMS over the corners
       const int k = k0 + lane;
       bool keep = false;
       int sc = 0, p = 0;
-      if (k < ncand) {
+      if (k < ncorner) {
         p = cand_list[k];
         const uint8_t* a = arcm + p;
-        const int mm = a[0];
-        if (mm > th) {
-          sc = mm - 1;
-          const int n8[8] = {a[-kFS - 1], a[-kFS], a[-kFS + 1], a[-1],
-                             a[1],        a[kFS - 1], a[kFS], a[kFS + 1]};
-          int nmax = 0;
+        sc = a[0] - 1;
+        const int n8[8] = {a[-kFS - 1], a[-kFS], a[-kFS + 1], a[-1],
+                           a[1],        a[kFS - 1], a[kFS], a[kFS + 1]};
+        int nmax = 0;
 #pragma unroll
-          for (int j = 0; j < 8; j++) nmax = max(nmax, n8[j] > th ? n8[j] - 1 : 0);
-          keep = sc > nmax;
-        }
+        for (int j = 0; j < 8; j++) nmax = max(nmax, n8[j] > th ? n8[j] - 1 : 0);
+        keep = sc > nmax;
       }
       const unsigned long long bal = __ballot(keep);
       if (keep) {
@@ -452,9 +485,18 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
       base += __popcll(bal);
     }
     count = base;
+    FP_T(3 + 3 * pass);
+#ifdef MMT_FAST_PROFILE
+    fp[7] = ncand;
+#endif
     if (count > 0) break;
     wave_sync();
   }
+#ifdef MMT_FAST_PROFILE
+  if (lane == 0 && frame == 0 && cell % 37 == 0)
+    printf("fastprof cell %d lvl %d: copy %lld pre %lld arc %lld nms %lld | pass2 pre %lld arc %lld nms %lld | ncand %lld cnt %d\n",
+           cell, ci.level, fp[0], fp[1], fp[2], fp[3], fp[4], fp[5], fp[6], fp[7], count);
+#endif
   if (lane == 0) cellcnt[(size_t)frame * ncells + cell] = min(count, ci.slot_cap);
 }
 
