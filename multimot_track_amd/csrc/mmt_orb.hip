@@ -1318,7 +1318,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     const LevelInfo* __restrict__ lv, int nlevels, const int* __restrict__ umax,
     const uint32_t* __restrict__ okeys, int out_slots, const int* __restrict__ ocount,
     mmt_kp* __restrict__ kps, uint8_t* __restrict__ desc, int cap_frame, int* __restrict__ nkp,
-    int nframes) {
+    int nframes, int slot_begin, int slot_end, int write_total) {
+  // slots [slot_begin, slot_end) of every frame (a level range: level 0 runs as soon as its
+  // octree and the blur are done); write_total: this launch stores the frame's keypoint count
   const int lane = threadIdx.x & 63;
   const int gl = lane & 15, grp = lane >> 4;
   __shared__ uint32_t od_pat[256];  // the packed test pattern, once per workgroup
@@ -1328,12 +1330,12 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   // only, never correctness), so workgroup b serves frame (b % 8) + 8 * (b / 8 / wgf): the
   // slots of a frame run on one XCD, whose L2 then holds that frame's level and blurred level
   // rows across the overlapping patches of its keypoints
-  const int wgf = (out_slots + 15) / 16;  // workgroups per frame (16 slots each)
+  const int wgf = (slot_end - slot_begin + 15) / 16;  // workgroups per frame (16 slots each)
   const int jx = blockIdx.x >> 3;
   const int frame = (blockIdx.x & 7) + 8 * (jx / wgf);
   if (frame >= nframes) return;  // whole 16-lane groups leave together
-  const int local = (jx % wgf) * 16 + (threadIdx.x >> 6) * 4 + grp;
-  if (local >= out_slots) return;
+  const int local = slot_begin + (jx % wgf) * 16 + (threadIdx.x >> 6) * 4 + grp;
+  if (local >= slot_end) return;
   // level lookup: lane gl of the group holds level gl's slot offset and count (nlevels <= 16);
   // the level is a ballot count within the group and the keys before it a group sum
   const uint32_t k = okeys[(size_t)frame * out_slots + local];
@@ -1360,7 +1362,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   const int Lw = __shfl(my_w, src, 64);
   const float Lscale = __shfl(my_scale, src, 64), Lsize = __shfl(my_size, src, 64);
   const size_t fo = (size_t)frame * pyr_stride + __shfl(my_loff, src, 64);
-  if (local == 0 && gl == 0) nkp[frame] = min(tot, cap_frame);
+  if (write_total && local == slot_begin && gl == 0) nkp[frame] = min(tot, cap_frame);
   const int sidx = local - lvl_off;
   const int outi = before + sidx;
   if (sidx >= lvl_cnt || outi >= cap_frame) return;
@@ -1737,10 +1739,23 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
     if (NL > 1) octree(1, NL, stream);
     MMT_HIP(hipStreamWaitEvent(stream, ev_blur_, 0));
   }
-  const int od_grid = 8 * ((nframes + 7) / 8) * ((out_slots_ + 15) / 16);  // see k_orient_desc
-  hipLaunchKernelGGL(k_orient_desc, dim3(od_grid), dim3(256), 0, stream, d_pyr_, d_blur_,
-                     pyr_stride_, d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_,
-                     d_kps, d_desc, cap_per_frame, d_n, nframes);
+  auto orient = [&](int s0, int s1, int write_total, hipStream_t st) {
+    const int grid = 8 * ((nframes + 7) / 8) * ((s1 - s0 + 15) / 16);  // see k_orient_desc
+    hipLaunchKernelGGL(k_orient_desc, dim3(grid), dim3(256), 0, st, d_pyr_, d_blur_, pyr_stride_,
+                       d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_, d_kps, d_desc,
+                       cap_per_frame, d_n, nframes, s0, s1, write_total);
+  };
+  if (NL > 1 && !(sched_ & 2)) {
+    // level 0's orientation on the side stream (its octree and the blur are done there) while
+    // the main stream runs the octree of levels 1..; the main stream's own orientation of levels
+    // 1.. writes the totals, then waits for the side stream
+    orient(0, lv_[1].out_off, 0, side_);
+    MMT_HIP(hipEventRecord(ev_pyr_, side_));
+    orient(lv_[1].out_off, out_slots_, 1, stream);
+    MMT_HIP(hipStreamWaitEvent(stream, ev_pyr_, 0));
+  } else {
+    orient(0, out_slots_, 1, stream);
+  }
   MMT_HIP(hipGetLastError());
 }
 
