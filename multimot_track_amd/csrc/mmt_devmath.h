@@ -441,6 +441,53 @@ __device__ __forceinline__ double lane_value(double v, int l) {
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
+// v + (v of the lane selected by the DPP control CTRL), both 32-bit halves moved by DPP
+template <int CTRL>
+__device__ __forceinline__ double dpp_add(double v) {
+  const unsigned long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+  return v + __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// wave sum of a double, wave-uniform result: quad swaps (xor 1, xor 2), half-row and row mirrors
+// give every lane its 16-lane row sum, then the four row sums are added from lanes 0/16/32/48 in
+// a fixed order.  Inactive lanes must hold 0.
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v = dpp_add<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = dpp_add<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = dpp_add<0x141>(v);  // row_half_mirror
+  v = dpp_add<0x140>(v);  // row_mirror
+  return (lane_value(v, 0) + lane_value(v, 16)) + (lane_value(v, 32) + lane_value(v, 48));
+}
+
+// Workgroup sums of two doubles per thread, identical in every wave: DPP wave sums, one LDS
+// exchange of the wave totals (`part`: 2 * nw doubles), one barrier.  For the light pass of an
+// LM trial, whose two sums would otherwise pay a whole tile reduction's latency.
+__device__ __forceinline__ void block_sum2(double a, double b, double* part, int nw, double& sa,
+                                           double& sb) {
+  a = wave_sum_dpp(a);
+  b = wave_sum_dpp(b);
+  if (nw == 1) {
+    sa = a;
+    sb = b;
+    return;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    part[2 * wave] = a;
+    part[2 * wave + 1] = b;
+  }
+  __syncthreads();
+  double s0 = 0, s1 = 0;
+  for (int w = 0; w < nw; w++) {
+    s0 += part[2 * w];
+    s1 += part[2 * w + 1];
+  }
+  sa = s0;
+  sb = s1;
+}
+
 // Workgroup sum of K doubles held per thread; result broadcast in `out` (LDS, K entries).
 // `scratch` holds (blockDim/64) * K doubles.
 template <int K>

@@ -12,14 +12,17 @@
 //
 // One workgroup per solve (ego + every object of a frame in one launch), fp64.  Per-correspondence
 // state lives in registers (IR items per thread; items beyond IR * blockDim spill to the global
-// scratch arrays).  Each LM trial is two passes over the correspondences:
-//   Schur pass   J^T W J terms of the Schur complement (27 sums)
-//   update pass  flow back-substitution, the trial's errors and chi2, and -- speculatively -- the
-//                linearisation at the trial state (H, b: 29 sums); accepted trials hand it to the
-//                next iteration, so no separate linearisation pass is needed
-// and one lane solves the 6x6 system in between.  Reductions are butterfly reduce-scatters
-// (mmt_devmath.h: block_sum).  Sums are reduced in a different order than the CPU checker's
-// sequential loops, so poses agree to rounding (1e-4 bar), not bit for bit.
+// scratch arrays).  An LM trial is
+//   Schur pass   J^T W J terms of the Schur complement (27 sums; only when some edge is
+//                Huber-active, otherwise closed form from the current system's sums)
+//   6x6 solve    computed redundantly by every thread from the sums
+//   pass 1       flow back-substitution and the trial's errors: chi2 and the scale term (2 sums)
+//   pass 2       accepted trials only: the flow step and the linearisation at the new state
+//                (H, b and the closed-form Schur sums: 63 sums), the next trial's system
+// so a rejected trial costs one light pass and a DPP reduction of two sums.  The 63-sum reductions
+// go through an LDS transpose tile (mmt_devmath.h: block_sum_tile_lanes).  Sums are reduced in a
+// different order than the CPU checker's sequential loops, so poses agree to rounding (1e-4 bar),
+// not bit for bit.
 
 #include <hip/hip_runtime.h>
 
@@ -46,12 +49,11 @@ struct LMItem {
   double f[2];      // flow vertex estimate
   double xl[2];     // last flow increment (reused when the 6x6 solve fails)
   double w, bl[2];  // robust weight, landmark gradient at the current state
-  double wn, bln[2];  // the same at the trial state
   double e[2];      // errors of the last evaluated state
 };
 
 enum { G_X0 = 0, G_X1, G_X2, G_OB0, G_OB1, G_PR0, G_PR1, G_F0, G_F1, G_XL0, G_XL1, G_W, G_BL0,
-       G_BL1, G_WN, G_BLN0, G_BLN1, G_E0, G_E1, G_COUNT };
+       G_BL1, G_E0, G_E1, G_COUNT };
 
 __device__ __forceinline__ void item_load(const double* S, int cap, int i, LMItem& it) {
   double* d = &it.X[0];
@@ -69,25 +71,23 @@ __device__ __forceinline__ void item_store(double* S, int cap, int i, const LMIt
 
 static_assert(sizeof(LMItem) == G_COUNT * sizeof(double), "LMItem layout");
 
-// the fields the update pass changes (xl, e, wn, bln) and the accept step changes (f, w, bl)
-__device__ __forceinline__ void item_store_upd(double* S, int cap, int i, const LMItem& it) {
+// the fields a trial changes (xl, e)
+__device__ __forceinline__ void item_store_trial(double* S, int cap, int i, const LMItem& it) {
   double* dst = S + i;
   dst[(size_t)G_XL0 * cap] = it.xl[0];
   dst[(size_t)G_XL1 * cap] = it.xl[1];
-  dst[(size_t)G_WN * cap] = it.wn;
-  dst[(size_t)G_BLN0 * cap] = it.bln[0];
-  dst[(size_t)G_BLN1 * cap] = it.bln[1];
   dst[(size_t)G_E0 * cap] = it.e[0];
   dst[(size_t)G_E1 * cap] = it.e[1];
 }
 
-__device__ __forceinline__ void item_accept(double* S, int cap, int i) {
-  double* d = S + i;
-  d[(size_t)G_F0 * cap] += d[(size_t)G_XL0 * cap];
-  d[(size_t)G_F1 * cap] += d[(size_t)G_XL1 * cap];
-  d[(size_t)G_W * cap] = d[(size_t)G_WN * cap];
-  d[(size_t)G_BL0 * cap] = d[(size_t)G_BLN0 * cap];
-  d[(size_t)G_BL1 * cap] = d[(size_t)G_BLN1 * cap];
+// the fields an accepted trial changes (f, w, bl)
+__device__ __forceinline__ void item_store_accept(double* S, int cap, int i, const LMItem& it) {
+  double* dst = S + i;
+  dst[(size_t)G_F0 * cap] = it.f[0];
+  dst[(size_t)G_F1 * cap] = it.f[1];
+  dst[(size_t)G_W * cap] = it.w;
+  dst[(size_t)G_BL0 * cap] = it.bl[0];
+  dst[(size_t)G_BL1 * cap] = it.bl[1];
 }
 
 // 1/x and 1/sqrt(x) from the hardware estimates plus two Newton steps (within an ulp of the
@@ -275,6 +275,7 @@ struct Cam {
 // J^T W J, [23..28] J^T W (-e), [29] Huber-active edge count, [30..50] sum B0a (B0b + B1b),
 // [51..56] sum B0a (bl0 + bl1), [57..62] sum (B1a - B0a) bl1 (B = w J)
 constexpr int kSums = 63;
+constexpr int kCandStride = 16;  // doubles per candidate solve in LMSmem::cand
 
 // linearise at (P, flow fl): errors, robust weight and landmark gradient of the edge; its sums
 // (layout at kSums) go straight into `row`, this thread's row of the LDS reduction tile
@@ -367,14 +368,13 @@ __device__ __forceinline__ void schur_terms(const Cam& c, const DSE3& P, const L
   }
 }
 
-// back-substitution of the flow increment (when the 6x6 solve succeeded), trial errors and
-// speculative linearisation at (PN, f + xl) into `row` ([0] trial chi2, [1] the scale term)
-template <bool FIRST>
-__device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const DSE3& PN,
-                                             LMItem& it, int i, bool ok2, double lam,
-                                             double ilam, const double* xb, double* row,
-                                             const double* Bcur = nullptr,
-                                             double* Bnext = nullptr) {
+// pass 1 of a trial: back-substitution of the flow increment (when the 6x6 solve succeeded) and
+// the errors at the trial state (PN, f + xl), accumulated into s_chi (the trial chi2 term) and
+// s_sc (the scale term)
+__device__ __forceinline__ void trial_terms(const Cam& c, const DSE3& P, const DSE3& PN,
+                                            LMItem& it, int i, bool ok2, double lam, double ilam,
+                                            const double* xb, double& s_chi, double& s_sc,
+                                            const double* Bcur = nullptr) {
   const double bl0 = it.bl[0], bl1 = it.bl[1];
   if (ok2) {
     const double w = it.w, h = w + c.pinfo;
@@ -404,9 +404,32 @@ __device__ __forceinline__ void update_terms(const Cam& c, const DSE3& P, const 
   }
   const double xl0 = it.xl[0], xl1 = it.xl[1];
   const double f0 = it.f[0] + xl0, f1 = it.f[1] + xl1;
+  double x, y, z;
+  map(PN, it.X, x, y, z);
+  const double iz = drcp(z);
+  const double pu = x * iz * c.fx + c.cx, pv = y * iz * c.fy + c.cy;
+  const double e0 = (it.ob[0] + f0) - pu;
+  const double e1 = (it.ob[1] + f1) - pv;
+  it.e[0] = e0;
+  it.e[1] = e1;
+  const double p0 = f0 - it.pr[0], p1 = f1 - it.pr[1];
+  const double e2 = kInfo * (e0 * e0 + e1 * e1);
+  double r0, r1;
+  huber(e2, c.dsqr, c.delta, r0, r1);
+  s_chi += r0 + c.pinfo * (p0 * p0 + p1 * p1);
+  s_sc += xl0 * (lam * xl0 + bl0) + xl1 * (lam * xl1 + bl1);
+}
+
+// pass 2 (accepted trials only): the flow step is taken and the edge linearised at the new state
+// (PN, f + xl), which builds the next iteration's system
+template <bool FIRST>
+__device__ __forceinline__ void accept_terms(const Cam& c, const DSE3& PN, LMItem& it, double* row,
+                                             double* Bnext = nullptr) {
+  it.f[0] += it.xl[0];
+  it.f[1] += it.xl[1];
   double mh = 0;
-  linearise<FIRST>(c, PN, it, f0, f1, row, xl0 * (lam * xl0 + bl0) + xl1 * (lam * xl1 + bl1),
-                   it.e[0], it.e[1], it.wn, it.bln[0], it.bln[1], mh, Bnext);
+  linearise<FIRST>(c, PN, it, it.f[0], it.f[1], row, 0.0, it.e[0], it.e[1], it.w, it.bl[0],
+                   it.bl[1], mh, Bnext);
 }
 
 #ifdef MMT_LM_PROFILE
@@ -475,6 +498,7 @@ struct LMSmem {
   double part[2][4 * kSums];  // double-buffered: waves read one while a fast wave fills the other
   double S27[32];
   double mh[16];
+  double cand[4 * 4 * 16];  // per wave: 4 candidate solves (ok, x[6], pose[7])
 };
 
 }  // namespace
@@ -533,15 +557,15 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   };
   LMItem R[IR];
   const int n_reg = IR * nt;
-  // one edge per thread: keep w J of the current and of the trial linearisation in registers,
-  // so the back-substitution needs no projection (two edges per thread would spill)
+  // one edge per thread: keep w J of the current linearisation in registers, so the
+  // back-substitution needs no projection
   constexpr bool kCacheB = IR == 1;
-  double RB[12], RBn[12];
+  double RB[12];
   // The LM bookkeeping below is computed redundantly by every thread from the block sums in LDS
   // (identical inputs, identical results), so only the 6x6 solve needs a lane-0 section.
   DSE3 P = dse3_from_float(D.init);
   const double hin = kInfo + c.pinfo;  // h of every edge when none is Huber-active
-  // the sums of the current system (vc) and of the last trial (vt): sum k in lane k of every wave
+  // the sums of the current system (vc): sum k in lane k of every wave
   // ---- initial linearisation (computeActiveErrors + buildSystem at the initial estimate)
   double* row = tile_row(sm.tile);  // this thread's row of the reduction tile
   // every thread with an edge has one in register slot 0 (N > nt implies all do), so slot 0
@@ -575,7 +599,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
     if ((tid & 63) == 0) sm.mh[tid >> 6] = mh;
   }
   int pb = 0;  // part buffer of the next reduction
-  double vc = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw), vt = 0;
+  double vc = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
   pb ^= 1;
   double cur = lane_value(vc, 0), lam, ni = 2, chk = 0;
   {
@@ -588,6 +612,9 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   }
   int nbad = 0, iters = 0;
   double xb[6] = {0, 0, 0, 0, 0, 0};  // the last increment (reused when the LDLT fails)
+  // candidate solves of the rejection chain (this wave's copy): [16 lanes][kCandStride]
+  double* cand = sm.cand + (tid >> 6) * 4 * kCandStride;
+  int ncand = 0, kc = 0;
   for (int iter = 0; iter < D.max_iters; iter++) {
     const double ini = cur;
     int qmax = 0;
@@ -622,11 +649,21 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         block_sum_t<27>(v, sm.tile, sm.red, sm.S27, nw);
       }
       MMT_LMPROF(0);
-      // the 6x6 solve, computed redundantly by every thread from the LDS sums (identical inputs,
-      // identical results): no lane-0 section, no barrier, no broadcast
-      bool ok2;
-      DSE3 PN;
-      {
+      // the 6x6 solve, computed redundantly by every wave from the sums (no lane-0 section, no
+      // barrier).  A rejected trial changes only lambda (lam *= ni, ni *= 2), so on the
+      // closed-form path the four 16-lane groups of a wave solve for the next four lambdas of the
+      // rejection chain at once (the same instructions, a different lambda per lane): a trial
+      // after a rejection takes its increment and pose from the wave's candidate table instead of
+      // paying the solve's dependency chain again.  Each candidate is computed exactly as the
+      // sequential solve for its lambda would be.
+      if (!(clean && kc < ncand)) {
+        double lg = lam, ilg = ilam;
+        if (clean) {
+          const double l1 = lam * ni, n1 = ni * 2, l2 = l1 * n1, n2 = n1 * 2, l3 = l2 * n2;
+          const int g = (tid & 63) >> 4;
+          lg = g == 0 ? lam : g == 1 ? l1 : g == 2 ? l2 : l3;
+          ilg = drcp(lg);
+        }
         double A[21], bs[6];
 #pragma unroll
         for (int k = 0; k < 21; k++) A[k] = lane_value(vc, 2 + k);
@@ -634,15 +671,15 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         for (int a = 0; a < 6; a++) bs[a] = lane_value(vc, 23 + a);
         if (clean) {
           // SB = sum B1a B1b - B0a B1b = w H - SA (w = kInfo on every edge)
-          const double d00 = drcp(hin + lam);
+          const double d00 = drcp(hin + lg);
 #pragma unroll
           for (int k = 0; k < 21; k++) {
             const double sa = lane_value(vc, 30 + k);
-            A[k] -= d00 * sa + ilam * (kInfo * A[k] - sa);
+            A[k] -= d00 * sa + ilg * (kInfo * A[k] - sa);
           }
 #pragma unroll
           for (int a = 0; a < 6; a++)
-            bs[a] -= d00 * lane_value(vc, 51 + a) + ilam * lane_value(vc, 57 + a);
+            bs[a] -= d00 * lane_value(vc, 51 + a) + ilg * lane_value(vc, 57 + a);
         } else {
 #pragma unroll
           for (int k = 0; k < 21; k++) A[k] -= sm.S27[k];
@@ -650,7 +687,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
           for (int a = 0; a < 6; a++) bs[a] -= sm.S27[21 + a];
         }
 #pragma unroll
-        for (int a = 0; a < 6; a++) A[a * (a + 3) / 2] += lam;  // diagonal (a, a)
+        for (int a = 0; a < 6; a++) A[a * (a + 3) / 2] += lg;  // diagonal (a, a)
 #ifdef MMT_LM_PROFILE
         if (tid == 0) {  // force the loads to complete before the split point
           double chk = 0;
@@ -659,28 +696,65 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         }
 #endif
         MMT_LMPROF(8);
-        ok2 = ldlt6_packed(A, bs);
+        const bool okg = ldlt6_packed(A, bs);
 #ifdef MMT_LM_PROFILE
         if (tid == 0 && bs[0] == 12345.678) sm.prof[11]++;
 #endif
         MMT_LMPROF(9);
+        double xg[6];
 #pragma unroll
-        for (int a = 0; a < 6; a++) xb[a] = ok2 ? bs[a] : xb[a];  // failed solve: last increment
-        PN = exp_mul(xb, P);
+        for (int a = 0; a < 6; a++) xg[a] = okg ? bs[a] : xb[a];
+        const DSE3 PG = exp_mul(xg, P);
+        if ((tid & 15) == 0) {
+          double* cw = cand + ((tid & 63) >> 4) * kCandStride;
+          cw[0] = okg ? 1.0 : 0.0;
+#pragma unroll
+          for (int a = 0; a < 6; a++) cw[1 + a] = xg[a];
+          cw[7] = PG.q.w;
+          cw[8] = PG.q.x;
+          cw[9] = PG.q.y;
+          cw[10] = PG.q.z;
+          cw[11] = PG.t[0];
+          cw[12] = PG.t[1];
+          cw[13] = PG.t[2];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        ncand = clean ? 4 : 1;
+        kc = 0;
+      }
+      bool ok2;
+      DSE3 PN;
+      {
+        const double* cw = cand + kc * kCandStride;
+        ok2 = cw[0] != 0.0;
+        if (ok2) {
+#pragma unroll
+          for (int a = 0; a < 6; a++) xb[a] = cw[1 + a];
+          PN.q.w = cw[7];
+          PN.q.x = cw[8];
+          PN.q.y = cw[9];
+          PN.q.z = cw[10];
+          PN.t[0] = cw[11];
+          PN.t[1] = cw[12];
+          PN.t[2] = cw[13];
+        } else {
+          PN = exp_mul(xb, P);  // failed solve: the last increment (g2o's stale x)
+        }
+        kc++;
       }
       MMT_LMPROF(1);
-      // ---- flow back-substitution, trial errors, speculative linearisation
+      // ---- pass 1: flow back-substitution and the trial's errors (chi2 and scale sums only)
+      double lastTrialChi, scale;
       {
+        double s_chi = 0, s_sc = 0;
 #pragma unroll
         for (int k = 0; k < IR; k++) {
           const int i = tid + k * nt;
-          if (i < N) {
-            if (k == 0)
-              update_terms<true>(c, P, PN, R[k], i, ok2, lam, ilam, xb, row,
-                                 kCacheB ? RB : nullptr, kCacheB ? RBn : nullptr);
-            else
-              update_terms<false>(c, P, PN, R[k], i, ok2, lam, ilam, xb, row);
-          }
+          if (i < N)
+            trial_terms(c, P, PN, R[k], i, ok2, lam, ilam, xb, s_chi, s_sc,
+                        (kCacheB && k == 0) ? RB : nullptr);
         }
         {  // global items: the next item's loads are in flight while this one computes
           int i = n_reg + tid;
@@ -688,22 +762,18 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
           if (i < N) item_load(G, cap, i, it);
           for (; i < N; i += nt) {
             if (i + nt < N) item_load(G, cap, i + nt, nx);
-            update_terms<false>(c, P, PN, it, i, ok2, lam, ilam, xb, row);
-            item_store_upd(G, cap, i, it);
+            trial_terms(c, P, PN, it, i, ok2, lam, ilam, xb, s_chi, s_sc);
+            item_store_trial(G, cap, i, it);
             it = nx;
           }
         }
-        if (tid >= N)
-          for (int q = 0; q < kSums; q++) row[q] = 0;
         MMT_LMPROF(5);
-        vt = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
+        block_sum2(s_chi, s_sc, sm.part[pb], nw, lastTrialChi, scale);
         pb ^= 1;
       }
       MMT_LMPROF(2);
       // ---- g2o LM step acceptance and termination (every thread, same values)
-      const double lastTrialChi = lane_value(vt, 0);
       const double tempChi = ok2 ? lastTrialChi : DBL_MAX;
-      double scale = lane_value(vt, 1);
 #pragma unroll
       for (int a = 0; a < 6; a++) scale += xb[a] * (lam * xb[a] + lane_value(vc, 23 + a));
       scale += 1e-3;
@@ -717,7 +787,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         ni = 2;
         cur = tempChi;
         P = PN;
-        vc = vt;  // the trial's linearisation becomes the current system
+        ncand = 0;  // the candidates belong to the old system
       } else {
         lam = lam * ni;
         ni = ni * 2;
@@ -740,20 +810,31 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         bad = !ok;
       }
       if (accept) {
+        // ---- pass 2: take the flow step and linearise at the accepted state (the system of the
+        // next trial); rejected trials skip it, so they cost the errors and two sums only
 #pragma unroll
         for (int k = 0; k < IR; k++)
           if (tid + k * nt < N) {
-            LMItem& it = R[k];
-            it.f[0] += it.xl[0];
-            it.f[1] += it.xl[1];
-            it.w = it.wn;
-            it.bl[0] = it.bln[0];
-            it.bl[1] = it.bln[1];
-            if (kCacheB && k == 0)
-#pragma unroll
-              for (int q = 0; q < 12; q++) RB[q] = RBn[q];
+            if (k == 0)
+              accept_terms<true>(c, P, R[k], row, kCacheB ? RB : nullptr);
+            else
+              accept_terms<false>(c, P, R[k], row);
           }
-        for (int i = n_reg + tid; i < N; i += nt) item_accept(G, cap, i);
+        {
+          int i = n_reg + tid;
+          LMItem it, nx;
+          if (i < N) item_load(G, cap, i, it);
+          for (; i < N; i += nt) {
+            if (i + nt < N) item_load(G, cap, i + nt, nx);
+            accept_terms<false>(c, P, it, row);
+            item_store_accept(G, cap, i, it);
+            it = nx;
+          }
+        }
+        if (tid >= N)
+          for (int q = 0; q < kSums; q++) row[q] = 0;
+        vc = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
+        pb ^= 1;
       }
       MMT_LMPROF(3);
 #ifdef MMT_LM_PROFILE
