@@ -622,18 +622,23 @@ __device__ __forceinline__ int wave_min(int v) {
   return v;
 }
 
-// atomicAdd(&a[key], 1) for every active lane with key != ~0u, one LDS atomic per distinct key
-// of the wave: keys arrive in cell order, so a wave holds a few distinct nodes/quadrants, and
-// same-address LDS atomics would serialise lane by lane.
-__device__ __forceinline__ void wave_agg_inc(lds_u32* a, uint32_t key) {
+// atomicAdd(&a[key], 1) for every active lane with key != ~0u, one LDS atomic per run of equal
+// keys in adjacent lanes: keys arrive in cell order, so equal nodes/quadrants sit next to each
+// other, and the instruction count does not grow with the number of distinct keys (repeats of a
+// key in separate runs just add separately).  Lanes outside the loop's exec mask count as ~0u.
+__device__ __forceinline__ void wave_run_inc(lds_u32* a, uint32_t key) {
   const int lane = threadIdx.x & 63;
-  unsigned long long act = __ballot(key != ~0u);
-  while (act) {
-    const int leader = __builtin_ctzll(act);
-    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)key, leader);
-    const unsigned long long m = __ballot(key == v);
-    if (lane == leader) atomicAdd((uint32_t*)&a[v], (uint32_t)__popcll(m));
-    act &= ~m;
+  // key of lane - 1 (wave_shr:1; lane 0 and lanes whose left neighbour is inactive read ~0u)
+  const uint32_t prev =
+      (uint32_t)__builtin_amdgcn_update_dpp((int)~0u, (int)key, 0x138, 0xF, 0xF, false);
+  const bool valid = key != ~0u;
+  const bool head = valid && (lane == 0 || prev != key);
+  // run boundaries: heads and invalid lanes (inactive lanes read as set, ending every run)
+  const unsigned long long bnd = __ballot(head || !valid) | ~__ballot(1);
+  if (head) {
+    const unsigned long long rest = lane < 63 ? bnd >> (lane + 1) : 0ull;
+    const int len = rest ? __builtin_ctzll(rest) + 1 : 64 - lane;
+    atomicAdd((uint32_t*)&a[key], (uint32_t)len);
   }
 }
 
@@ -721,7 +726,7 @@ __device__ __forceinline__ void oct_count_children(OctLDS& S, int c, const KA& k
       kk.kq[i] = (uint8_t)q;
       key = (uint32_t)(r * 4 + q);
     }
-    wave_agg_inc(S.cc, key);
+    wave_run_inc(S.cc, key);
   }
 }
 
@@ -954,7 +959,7 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
   for (int i = tid; i < n; i += nt) {
     const int idx = (int)((float)key_x(kk.lk[i]) / hX);
     kk.knode[i] = (uint16_t)idx;
-    wave_agg_inc(S.cnt, (uint32_t)idx);
+    wave_run_inc(S.cnt, (uint32_t)idx);
   }
   __syncthreads();
   for (int i = tid; i < nIni; i += nt) S.krank[i] = S.cnt[(0) * S.nb + i] > 0 ? 1 : 0;
