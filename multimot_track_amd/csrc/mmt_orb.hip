@@ -694,16 +694,26 @@ __device__ int oct_expandable_sorted(OctLDS& S, int cur, int L) {
   __syncthreads();
   const int D = S.s_ctl[3];
   // rank sort, descending: the keys are unique (node index in the low bits), so a key's rank is
-  // the number of keys above it; every thread ranks its keys against all of them (broadcast LDS
-  // reads, two keys per read): one barrier instead of a sorting network's log^2 steps
-  for (int i = tid; i < D; i += nt) {
+  // the number of keys above it.  T adjacent lanes rank one key, each against an even-sized
+  // slice of the keys (broadcast LDS reads, two keys per read), and add their counts with
+  // shuffles: one barrier instead of a sorting network's log^2 steps, about D^2 / nt compares per
+  // thread instead of D.
+  int T = 1;
+  while (T < 64 && D * (2 * T) <= nt) T *= 2;
+  const int slice = (((D + 1) >> 1) + T - 1) / T * 2;  // keys per lane, even (sortkey[D] is 0)
+  for (int base = tid; base < D * T; base += nt) {
+    const int i = base / T, part = base & (T - 1);
     const unsigned long long k = S.sortkey[i];
+    const int j0 = part * slice, j1 = min(j0 + slice, D + (D & 1));
     int rank = 0;
-    for (int j = 0; j < D; j += 2) rank += (S.sortkey[j] > k) + (S.sortkey[j + 1] > k);
-    const int s = (int)(k & 0xFFFFull);
-    S.order[rank] = s;
-    S.prank[s] = rank;
-    S.mid[rank] = node_mid(S, cur, s);
+    for (int j = j0; j < j1; j += 2) rank += (S.sortkey[j] > k) + (S.sortkey[j + 1] > k);
+    for (int o = T >> 1; o > 0; o >>= 1) rank += __shfl_xor(rank, o, 64);
+    if (part == 0) {
+      const int s = (int)(k & 0xFFFFull);
+      S.order[rank] = s;
+      S.prank[s] = rank;
+      S.mid[rank] = node_mid(S, cur, s);
+    }
   }
   __syncthreads();
   // cc aliases sortkey: zero the child counters only once every rank is done
