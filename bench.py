@@ -61,7 +61,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--chunk", type=int, default=32, help="frames per step (ORB batch)")
+    ap.add_argument("--chunk", type=int, default=64,
+                    help="frames per step (ORB batch; SURVEY 8(d): >= 64 frames in flight)")
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--nfeatures", type=int, default=2000)

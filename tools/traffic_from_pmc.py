@@ -55,7 +55,8 @@ for k in ORB:
     raw += (fk + wk) * 1024
     total += (2 * fk + wk) * 1024
     print("%-16s %10d %16.1f %16.1f" % (k, len(nf.get(k, ())), fk, wk))
-W, H, B = 1242, 375, 32  # key 1242x375_n2000_b32
+W, H = 1242, 375
+B = int(key.rsplit('_b', 1)[1])  # key 1242x375_n2000_b<batch>
 known = 5.0 * W * H * B
 print("calibration k_gray_depth: known reads %.1f MB, FETCH_SIZE %.1f MB (x%.2f); known writes "
       "%.1f MB, WRITE_SIZE %.1f MB" % (known / 1e6, fetch.get("k_gray_depth", 0) / launches *
