@@ -102,6 +102,9 @@ class OrbEngine {
   int total_slots_ = 0, out_slots_ = 0, cap_frame_ = 0, node_cap_ = 0;
   int key_cap_ = 0;          // k_octree: keys per (level, frame) held in LDS
   size_t octree_lds_ = 0;    // k_octree dynamic LDS bytes
+  int key_cap1_ = 0;         // the same for the launch of levels 1.. (two workgroups per CU)
+  size_t octree_lds1_ = 0;
+  bool oct_two_per_cu_ = false;
   // One side stream beside the caller's (run()): a process has 4 hardware queues
   // (GPU_MAX_HW_QUEUES), and streams beyond them end up sharing the caller's queue.
   hipStream_t side_ = nullptr;

@@ -1077,7 +1077,12 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
 
 // One workgroup per (level, frame).  Keys of the level live in LDS when at most kcap of them
 // survived FAST (the usual case), in global scratch otherwise.
-__global__ __launch_bounds__(1024) void k_octree(const LevelInfo* __restrict__ lv,
+// kWaves: minimum waves per SIMD the register allocation must allow.  8 (at most 64 VGPRs) lets
+// two 1024-thread workgroups share a CU when their LDS fits in half of it (the launch of levels
+// 1.., whose key counts are small); 1 leaves the allocation unconstrained (level 0).
+template <int kWaves>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kWaves))) void k_octree(
+                                                 const LevelInfo* __restrict__ lv,
                                                  const CellInfo* __restrict__ cells, int ncells,
                                                  const uint32_t* __restrict__ keys,
                                                  const int* __restrict__ cellcnt, int total_slots,
@@ -1161,7 +1166,10 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 // two v_dot4_u32_u8 each, keeps the last seven rows of sums in a register ring (rows unrolled by
 // seven, so the ring never moves), and stores its four outputs as one dword.  No LDS, no
 // barriers.  Lanes whose columns touch the level edge gather their bytes with REFLECT_101.
-constexpr int kBlurBand = 32;
+#ifndef MMT_BLUR_BAND
+#define MMT_BLUR_BAND 32
+#endif
+constexpr int kBlurBand = MMT_BLUR_BAND;
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
   uint32_t v;
@@ -1660,8 +1668,31 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
     }
   octree_lds_ = oct_layout(node_cap_, key_cap_).end;
   if (octree_lds_ > lds_budget) throw ArgError("octree node arrays exceed the LDS budget");
-  MMT_HIP(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+  MMT_HIP(hipFuncSetAttribute((const void*)k_octree<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)octree_lds_));
+  // levels 1..: keys in LDS up to half a CU's LDS, so two workgroups share a CU and a batch's
+  // (levels x frames) workgroups run in one round; the few (level, frame) pairs with more keys
+  // take the global-scratch path
+  const uint32_t half_budget = 80 * 1024 - 512;
+  key_cap1_ = 0;
+  for (int k = std::min(key_cap_, 16384); k >= 256; k -= 16)
+    if (oct_layout(node_cap_, k).end <= half_budget) {
+      key_cap1_ = k;
+      break;
+    }
+  int max_key_cap1 = 0;  // keys any level 1.. can hold at most (its FAST slot capacity)
+  for (int l = 1; l < nlevels_; l++) max_key_cap1 = std::max(max_key_cap1, lv_[l].key_cap);
+  if (key_cap1_ < 256 || getenv("MMT_OCT_ONE_PER_CU")) {
+    key_cap1_ = key_cap_;  // the node arrays alone fill half the LDS: one workgroup per CU
+    octree_lds1_ = octree_lds_;
+    oct_two_per_cu_ = false;
+  } else {
+    key_cap1_ = std::min(key_cap1_, (max_key_cap1 + 15) & ~15);
+    octree_lds1_ = oct_layout(node_cap_, key_cap1_).end;
+    oct_two_per_cu_ = true;
+    MMT_HIP(hipFuncSetAttribute((const void*)k_octree<8>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds1_));
+  }
   upload(&d_lv_, lv_);
   upload(&d_cells_, cells_);
   upload(&d_xtab_, xt);
@@ -1705,11 +1736,13 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
                        pyr_stride_, d_lv_, d_cells_, ncells_, d_keys_, total_slots_, d_cellcnt_,
                        iniTh_, minTh_, fast_rows_max_, fast_win_max_, c0, c1);
   };
-  const size_t lds = octree_lds_;
   auto octree = [&](int l0, int l1, hipStream_t st) {
-    hipLaunchKernelGGL(k_octree, dim3(l1 - l0, nframes), dim3(1024), lds, st, d_lv_, d_cells_,
-                       ncells_, d_keys_, d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_,
-                       out_slots_, d_ocount_, nlevels_, node_cap_, key_cap_, l0, d_err_);
+    // level 0 alone: the full-LDS variant; levels 1..: two workgroups per CU when they fit
+    const bool two = l0 > 0 && oct_two_per_cu_;
+    hipLaunchKernelGGL(two ? k_octree<8> : k_octree<1>, dim3(l1 - l0, nframes), dim3(1024),
+                       two ? octree_lds1_ : octree_lds_, st, d_lv_, d_cells_, ncells_, d_keys_,
+                       d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_, out_slots_,
+                       d_ocount_, nlevels_, node_cap_, two ? key_cap1_ : key_cap_, l0, d_err_);
   };
   auto resize = [&](int l, hipStream_t st) {
     const LevelInfo& S = lv_[l - 1];
