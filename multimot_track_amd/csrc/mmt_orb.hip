@@ -1336,6 +1336,13 @@ __device__ __forceinline__ uint32_t ld16(const uint8_t* p) {
   return v;
 }
 
+// k_orient_desc LDS slot of one keypoint: the blurred window, kOdBRows rows of kOdBw bytes
+// around the keypoint (radius kOdR)
+constexpr int kOdR = 18, kOdBRows = 2 * kOdR + 1, kOdBw = 40;
+constexpr int kOdSlot = kOdBRows * kOdBw;                      // 1480 (a multiple of 4)
+constexpr int kOdBLoads = (kOdBRows * (kOdBw / 4) + 15) / 16;  // dwords per lane (24)
+static_assert(kOdSlot % 4 == 0, "dword-aligned slots");
+
 __global__ __launch_bounds__(256) void k_orient_desc(
     const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur, size_t pyr_stride,
     const LevelInfo* __restrict__ lv, int nlevels, const int* __restrict__ umax,
@@ -1347,6 +1354,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   const int lane = threadIdx.x & 63;
   const int gl = lane & 15, grp = lane >> 4;
   __shared__ uint32_t od_pat[256];  // the packed test pattern, once per workgroup
+  __shared__ __attribute__((aligned(16))) uint8_t od_lds[16 * kOdSlot];  // 16 keypoint slots
   od_pat[threadIdx.x] = c_pattern.t[threadIdx.x];
   __syncthreads();
   // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b % 8 share one; speed
@@ -1391,13 +1399,38 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   if (sidx >= lvl_cnt || outi >= cap_frame) return;
   const int kx = (int)((k >> 8) & 0xFFFu), ky = (int)(k >> 20);
   const float response = (float)(k & 0xFFu);
-  // BRIEF tests 16r + gl of this lane (r = 0..15), fetched while the disc loads are in flight
+  // The blurred 37 x 37 window the rotated tests can reach (|rotated offset| <= 13 sqrt 2 < 18.5;
+  // rows of kOdBw bytes) goes to this group's LDS slot with coalesced dword loads, issued
+  // together with the IC_Angle disc loads (two bytes per lane and row, into registers): one memory
+  // round trip per keypoint.  Keypoints sit >= 19 px inside the level, so the windows stay inside
+  // it (row tails may read a few bytes of the next row).
+  uint8_t* slot_lds = od_lds + ((threadIdx.x >> 6) * 4 + grp) * kOdSlot;
+  const int c0 = 2 * gl - 15, c1 = c0 + 1;
+  uint32_t rows[31];
+  {
+    const uint8_t* bsrc = blur + fo + (size_t)(ky - kOdR) * Lw + (kx - kOdR);
+    uint32_t vb[kOdBLoads];
+#pragma unroll
+    for (int k = 0; k < kOdBLoads; k++) {
+      const int i = gl + 16 * k, r = i / (kOdBw / 4), q = i - r * (kOdBw / 4);
+      if (i < kOdBRows * (kOdBw / 4)) vb[k] = ld32(bsrc + (size_t)r * Lw + 4 * q);
+    }
+    // the whole 31 x 32 disc square is inside the level: load it unconditionally, mask later
+    const uint8_t* col = pyr + fo + (size_t)ky * Lw + kx + c0;
+#pragma unroll
+    for (int v = -15; v <= 15; v++) rows[v + 15] = ld16(col + (ptrdiff_t)v * Lw);
+#pragma unroll
+    for (int k = 0; k < kOdBLoads; k++) {
+      const int i = gl + 16 * k;
+      if (i < kOdBRows * (kOdBw / 4)) *(uint32_t*)(slot_lds + 4 * i) = vb[k];
+    }
+  }
+  // BRIEF tests 16r + gl of this lane (r = 0..15)
   uint32_t pat[16];
 #pragma unroll
   for (int r = 0; r < 16; r++) pat[r] = od_pat[16 * r + gl];
   // --- IC_Angle: lane gl owns disc columns c0 = 2gl-15 and c0+1 (column 16 does not exist; the
   // keypoint border, >= 19 px, keeps its byte inside the level)
-  const int c0 = 2 * gl - 15, c1 = c0 + 1;
   const int a0 = c0 < 0 ? -c0 : c0, a1 = c1 < 0 ? -c1 : c1;
   int vmax0 = 0, vmax1 = 0;
 #pragma unroll
@@ -1407,11 +1440,6 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     vmax1 += a1 <= um ? 1 : 0;
   }
   if (c1 > 15) vmax1 = -1;
-  // the whole 31 x 32 square is inside the level: load it unconditionally, mask afterwards
-  const uint8_t* col = pyr + fo + (size_t)ky * Lw + kx + c0;
-  uint32_t rows[31];
-#pragma unroll
-  for (int v = -15; v <= 15; v++) rows[v + 15] = ld16(col + (ptrdiff_t)v * Lw);
   int cs0 = 0, cs1 = 0, vs = 0;
 #pragma unroll
   for (int v = -15; v <= 15; v++) {
@@ -1435,7 +1463,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   double sd, cd;
   sincos_small((double)ang, &sd, &cd);
   const float a = (float)cd, b = (float)sd;
-  const uint8_t* center = blur + fo + (size_t)ky * Lw + kx;
+  wave_sync();  // the staged window of every group of the wave
+  const uint8_t* center = slot_lds + kOdR * kOdBw + kOdR;
   int bits[16];
 #pragma unroll
   for (int r = 0; r < 16; r++) {
@@ -1443,8 +1472,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     const float x1 = (float)(int8_t)((pat[r] >> 16) & 0xFFu), y1 = (float)(int8_t)(pat[r] >> 24);
     const float ry0 = x0 * b + y0 * a, rx0 = x0 * a - y0 * b;
     const float ry1 = x1 * b + y1 * a, rx1 = x1 * a - y1 * b;
-    const int v0 = center[__float2int_rn(ry0) * Lw + __float2int_rn(rx0)];
-    const int v1 = center[__float2int_rn(ry1) * Lw + __float2int_rn(rx1)];
+    const int v0 = center[__float2int_rn(ry0) * kOdBw + __float2int_rn(rx0)];
+    const int v1 = center[__float2int_rn(ry1) * kOdBw + __float2int_rn(rx1)];
     bits[r] = v0 < v1;
   }
   // round r gives descriptor bytes 2r, 2r+1 (test 16r + gl -> byte 2r + gl/8, bit gl%8);
