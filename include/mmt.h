@@ -83,6 +83,10 @@ typedef struct mmt_motion {
   float world_motion[16];   /* row-major 4x4 vObjMod = Tcw^-1 * X                      */
   float cam_pose[16];       /* row-major 4x4 X (PoseOptimizationFlow2 output)          */
   float init_pose[16];      /* row-major 4x4 mInitModel (PnP or motion model)          */
+  float centre_pre[3];      /* ObjCentre3D_pre (Tracking.cc:2032-2049): mean world point of
+                               the solve's last-frame samples, noisy depth (UnprojectStereoObject
+                               (j, 1)); the object-speed estimate of Tracking.cc:2186 uses it.
+                               0 when the solve had fewer than 3 correspondences          */
 } mmt_motion;
 
 /* Per-frame tracking result (the Tcw cv::Mat returned by System::TrackRGBD + counters). */

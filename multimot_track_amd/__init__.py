@@ -39,7 +39,7 @@ class MmtMotion(ctypes.Structure):
                 ("n_ransac_inliers", ctypes.c_int32), ("n_mm_inliers", ctypes.c_int32),
                 ("n_solve", ctypes.c_int32), ("iterations", ctypes.c_int32),
                 ("world_motion", ctypes.c_float * 16), ("cam_pose", ctypes.c_float * 16),
-                ("init_pose", ctypes.c_float * 16)]
+                ("init_pose", ctypes.c_float * 16), ("centre_pre", ctypes.c_float * 3)]
 
 
 class MmtFrameResult(ctypes.Structure):
@@ -114,7 +114,8 @@ def _frame_dict(r, objs):
         out.append(dict(label=o.label, sem_label=o.sem_label, n_points=o.n_points,
                         ransac_inliers=o.n_ransac_inliers, mm_inliers=o.n_mm_inliers,
                         n_solve=o.n_solve, n_inliers=o.n_inliers, iterations=o.iterations,
-                        init=_mat(o.init_pose), X=_mat(o.cam_pose), motion=_mat(o.world_motion)))
+                        init=_mat(o.init_pose), X=_mat(o.cam_pose), motion=_mat(o.world_motion),
+                        centre_pre=np.array(o.centre_pre[:], np.float32)))
     return dict(initialized=bool(r.initialized), Tcw=_mat(r.Tcw), n_keys=r.n_keypoints,
                 n_obj_samples=r.n_obj_samples, ego_iterations=r.ego_iterations,
                 ego_inliers=r.ego_inliers, objects=out)

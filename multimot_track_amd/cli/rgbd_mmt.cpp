@@ -1,8 +1,10 @@
 // multimot_track_amd/cli/rgbd_mmt.cpp -- drop-in for the reference's RGB-D example
 // (Examples/RGB-D/rgbd_tum.cc, built as `rgbd_mmt`): same arguments, same sequence layout
 // (image/ depth/ semantic/ flow/ times.txt pose_gt.txt object_pose.txt, LoadData :213-312), the
-// same per-frame camera relative-pose-error lines (Tracking.cc:1321-1341) and tracking-time
-// statistics (rgbd_tum.cc:196-203), with System::TrackRGBD replaced by mmt_track_rgbd.
+// same per-frame camera relative-pose-error lines (Tracking.cc:1321-1341), per-object speed and
+// relative-pose-error lines (Tracking.cc:2178-2243, ground truth from object_pose.txt) and
+// tracking-time statistics (rgbd_tum.cc:196-203), with System::TrackRGBD replaced by
+// mmt_track_rgbd.
 //
 //   rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence [--realtime] [--nfeatures N]
 //            [--device D] [--noise-seed S] [--poses out.txt]
@@ -73,6 +75,83 @@ void print_camera_rpe(const float* Tcw, const float* Tlw, const float* Tcw_gt, c
   printf("the relative pose error of estimated camera pose, t: %.4f R: %.4f\n", t_rpe, r_rpe);
 }
 
+// Tracking::ObjPoseParsing (Tracking.cc:4997-5104): object_pose.txt row (frame, id, bbox[4],
+// t[3], ry) -> 4x4 pose, R = Ry Rx Rz with x = z = 0 and y = ry + pi/2, float arithmetic
+void obj_pose_parsing(const float* row, float* P) {
+  const float y = (float)(row[9] + (3.1415926 / 2)), x = 0.0f, z = 0.0f;
+  const float cy = std::cos(y), sy = std::sin(y), cx = std::cos(x), sx = std::sin(x);
+  const float cz = std::cos(z), sz = std::sin(z);
+  const float R[9] = {cy * cz + sy * sx * sz, -cy * sz + sy * sx * cz, sy * cx,
+                      cx * sz,                cx * cz,                 -sx,
+                      -sy * cz + cy * sx * sz, sy * sz + cy * sx * cz, cy * cx};
+  const float E[16] = {R[0], R[1], R[2], row[6], R[3], R[4], R[5], row[7],
+                       R[6], R[7], R[8], row[8], 0,    0,    0,    1};
+  memcpy(P, E, sizeof(E));
+}
+
+// The per-object evaluation block of Tracking::Track (Tracking.cc:1655-1681 ground-truth motion,
+// 2178-2243 speed and relative pose error): ground-truth poses of the object's semantic label
+// in the last and current frames (object_pose.txt), H_p_c = L_w_c L_w_p^-1 with L_w = Twc_gt L,
+// the estimated speed from vObjMod and ObjCentre3D_pre.  Printed like the reference's cout
+// (fixed, 4 decimals: Tracking.cc:1335 leaves cout so).  Objects whose label has no
+// ground-truth row in either frame get the separator line only (the reference would read an
+// empty cv::Mat there).
+void print_object_eval(const mmt_motion& m, const float* Tlw_gt, const float* Tcw_gt,
+                       const std::vector<const float*>& last_rows,
+                       const std::vector<const float*>& cur_rows) {
+  printf("~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~~\n");
+  const float* rp = nullptr;
+  const float* rc = nullptr;
+  for (const float* r : last_rows)
+    if ((int)r[1] == m.sem_label) { rp = r; break; }
+  for (const float* r : cur_rows)
+    if ((int)r[1] == m.sem_label) { rc = r; break; }
+  if (!rp || !rc || !Tlw_gt || !Tcw_gt) return;
+  float Lp[16], Lc[16], Twl[16], Twc[16], Lwp[16], Lwc[16], Lwp_inv[16], H[16];
+  obj_pose_parsing(rp, Lp);
+  obj_pose_parsing(rc, Lc);
+  inv4(Tlw_gt, Twl);
+  inv4(Tcw_gt, Twc);
+  mul4(Twl, Lp, Lwp);
+  mul4(Twc, Lc, Lwc);
+  inv4(Lwp, Lwp_inv);
+  mul4(Lwc, Lwp_inv, H);
+  // ground-truth speed: L_w_p.t - L_w_c.t
+  const float g[3] = {Lwp[3] - Lwc[3], Lwp[7] - Lwc[7], Lwp[11] - Lwc[11]};
+  const float sp_gt = std::sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+  // estimated speed: vObjMod.t - (I - vObjMod.R) ObjCentre3D_pre (cv::Mat float products)
+  const float* M = m.world_motion;
+  float e[3];
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) {
+      const float IR = (float)((r == k ? 1.0f : 0.0f) - M[4 * r + k]);
+      s += (double)IR * (double)m.centre_pre[k];
+    }
+    e[r] = M[4 * r + 3] - (float)s;
+  }
+  const float sp_est = std::sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+  printf("estimated and ground truth object speed: %.4fkm/h %.4fkm/h %.4fkm/h\n", sp_est * 36,
+         sp_gt * 36, std::abs(sp_est - sp_gt) * 36);
+  const float sp_dis = std::abs(sp_est - sp_gt);
+  // relative pose error (Tracking.cc:2200-2243, metric (1)): RePoEr = vObjMod^-1 H_p_c
+  float Minv[16], E[16];
+  inv4(M, Minv);
+  mul4(Minv, H, E);
+  const float t_rpe = std::sqrt(E[3] * E[3] + E[7] * E[7] + E[11] * E[11]);
+  float trace = 0;
+  for (int i = 0; i < 3; i++) {
+    const float d = E[5 * i];
+    trace = d > 1.0 ? (float)(trace + 1.0 - (d - 1.0)) : trace + d;
+  }
+  const float r_rpe = (float)(std::acos((trace - 1.0) / 2.0) * 180.0 / 3.1415926);
+  const float t_gt = std::sqrt(H[3] * H[3] + H[7] * H[7] + H[11] * H[11]);
+  printf("the relative pose error of the object, t: %.4f%% R: %.4fdeg/m\n", (t_rpe / t_gt) * 100,
+         r_rpe / t_gt);
+  printf("the relative pose error of the object, t: %.4f R: %.4f\n", t_rpe, r_rpe);
+  printf("the object speed error, s: %.4f%%\n", sp_dis / sp_gt * 100);
+}
+
 std::string frame_name(const std::string& dir, const char* sub, int i, const char* ext) {
   char buf[32];
   snprintf(buf, sizeof(buf), "%06d", i);
@@ -129,6 +208,15 @@ int main(int argc, char** argv) {
   float* gt = nullptr;
   int ngt = 0;
   mmt_io_read_poses((seq + "/pose_gt.txt").c_str(), &gt, &ngt);
+  // object_pose.txt rows grouped by frame (rgbd_tum.cc:68-75, 139-150)
+  float* objgt = nullptr;
+  int nobjgt = 0;
+  mmt_io_read_object_poses((seq + "/object_pose.txt").c_str(), &objgt, &nobjgt);
+  std::vector<std::vector<const float*>> obj_rows(ntimes);
+  for (int i = 0; i < nobjgt; i++) {
+    const int f = (int)objgt[10 * i];
+    if (f >= 0 && f < ntimes) obj_rows[f].push_back(objgt + 10 * i);
+  }
   int nImages = 0;
   while (nImages < ntimes && exists(frame_name(seq, "image", nImages, ".png"))) nImages++;
   if (nImages == 0) {
@@ -243,11 +331,14 @@ int main(int argc, char** argv) {
     track_times[ni] = (float)ttrack;
     const float* Tgt = (ni < ngt) ? gt + 16 * ni : nullptr;
     if (haveLast && res.initialized && Tgt) print_camera_rpe(res.Tcw, lastTcw, Tgt, lastGt);
+    const float* Tlw_gt = (ni > 0 && ni - 1 < ngt) ? gt + 16 * (ni - 1) : nullptr;
     for (int k = 0; k < res.n_objects && k < (int)objs.size(); k++) {
       const mmt_motion& m = objs[k];
       printf("object %d (semantic label %d): %d points, %d RANSAC inliers, %d inliers; motion t = "
              "[%.4f %.4f %.4f]\n", m.label, m.sem_label, m.n_points, m.n_ransac_inliers,
              m.n_inliers, m.world_motion[3], m.world_motion[7], m.world_motion[11]);
+      if (ni > 0)
+        print_object_eval(m, Tlw_gt, Tgt, obj_rows[ni - 1], obj_rows[ni]);
     }
     if (fp) {
       fprintf(fp, "%d", ni);
@@ -270,6 +361,7 @@ int main(int argc, char** argv) {
   mmt_destroy(ctx);
   mmt_io_free(times);
   mmt_io_free(gt);
+  mmt_io_free(objgt);
   if (rc_all) return rc_all;
   std::vector<float> sorted = track_times;
   std::sort(sorted.begin(), sorted.end());

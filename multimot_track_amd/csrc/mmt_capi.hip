@@ -333,6 +333,7 @@ static void fill_results(const std::vector<mmt::FrameOut>& outs, mmt_frame_resul
       memcpy(m.world_motion, s.motion, 64);
       memcpy(m.cam_pose, s.X, 64);
       memcpy(m.init_pose, s.init, 64);
+      memcpy(m.centre_pre, s.centre_pre, 12);
     }
   }
 }

@@ -862,10 +862,48 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
     v[0] += outlier(it);
   }
   block_sum<1>(v, sm.red, sm.S27, nw);
+  const int n_out = N - (int)sm.S27[0];
+  if (D.centre_out) {
+    // ObjCentre3D_pre: float world points of the last frame (noisy depth, as the reference's
+    // UnprojectStereoObject(j, 1)), summed in double (the reference adds floats in order; the
+    // two agree to the reference's own rounding) and scaled by 1 / n as cv::Mat / int does
+    double cv3[3] = {0, 0, 0};
+    const float ifx = 1.0f / D.fx, ify = 1.0f / D.fy;
+    float Rlw[9], tlw[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+#pragma unroll
+      for (int cc = 0; cc < 3; cc++) Rlw[3 * r + cc] = D.Tcw_last[4 * r + cc];
+      tlw[r] = D.Tcw_last[4 * r + 3];
+    }
+    float twl[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {  // -Rlw^T tlw (cv::Mat float product)
+      double s = 0;
+#pragma unroll
+      for (int k = 0; k < 3; k++) s += (double)Rlw[3 * k + r] * (double)tlw[k];
+      twl[r] = -(float)s;
+    }
+    for (int i = tid; i < N; i += nt) {
+      const int s = D.idx ? D.idx[i] : i;
+      float z = D.depth[s];
+      const float noise = (float)((double)D.g0 * ((double)(z * z) / (725 * 0.5) * 0.15));
+      z = z + noise;
+      const float2 ob = D.obs[s];
+      const float x = (ob.x - D.cx) * z * ifx, y = (ob.y - D.cy) * z * ify;
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const double s3 = (double)Rlw[r] * x + (double)Rlw[3 + r] * y + (double)Rlw[6 + r] * z;
+        cv3[r] += (double)((float)s3 + twl[r]);
+      }
+    }
+    block_sum<3>(cv3, sm.red, sm.S27, nw);
+    if (tid < 3) D.centre_out[tid] = (float)((double)(float)sm.S27[tid] * (1.0 / N));
+  }
   if (tid == 0) {
     dse3_to_float(P, D.pose_out);
     D.stats[0] = iters;
-    D.stats[1] = N - (int)sm.S27[0];
+    D.stats[1] = n_out;
     D.stats[2] = 0;
 #ifdef MMT_LM_PROFILE
     printf("lmprof N=%d T=%d iters=%d trials=%lld clean=%lld schur_pass=%lld schur_red=%lld "

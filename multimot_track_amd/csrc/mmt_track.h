@@ -88,6 +88,10 @@ struct FlowSolveDesc {
   int cap;
   float* pose_out;
   int* stats;  // iterations, inliers, status (1: fewer than 3 edges, pose not written)
+  // optional: ObjCentre3D_pre (Tracking.cc:2032-2049), the mean world position of the solve's
+  // last-frame points unprojected with the frame's depth noise (UnprojectStereoObject(i, 1),
+  // Frame.cc:1118-1152: noise = gaussian(z^2 / 362.5 * 0.15) with the first draw g0)
+  float* centre_out;
 };
 
 void launch_gray_depth(const uint8_t* bgr, size_t bgr_pitch, const uint16_t* disp,

@@ -19,6 +19,7 @@ struct ObjOut {
   int label = 0, sem_label = 0, n_points = 0, n_ransac_inliers = 0, n_mm_inliers = -1;
   int ransac_iterations = 0, n_solve = 0, n_inliers = 0, iterations = 0;
   float init[16], X[16], motion[16];
+  float centre_pre[3] = {0, 0, 0};  // ObjCentre3D_pre (Tracking.cc:2032-2049)
 };
 
 struct FrameOut {
@@ -165,11 +166,13 @@ class Tracker {
     float X[16 * kMaxObj];
     int lst[3 * kMaxObj];
     int nsub[kMaxObj];
+    float centre[3 * kMaxObj];
   };
   ObjHost* oh_[kObjSlots] = {};
   int* d_res_[kObjSlots] = {};     // PnP results of all objects, contiguous
   double* d_Rt_[kObjSlots] = {};
   int* d_nsub_[kObjSlots] = {};
+  float* d_centre_[kObjSlots] = {};  // ObjCentre3D_pre per object (D3 kernel output)
   FlowSolveDesc* d_descs3_[kObjSlots] = {};  // D3 solves of the slot's frame
   float* d_poses3_[kObjSlots] = {};
   int* d_lmstats3_[kObjSlots] = {};

@@ -221,6 +221,7 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   d_res_[q] = alloc<int>(8 * kMaxObj);
   d_Rt_[q] = alloc<double>(12 * kMaxObj);
   d_nsub_[q] = alloc<int>(kMaxObj);
+  d_centre_[q] = alloc<float>(3 * kMaxObj);
   d_descs3_[q] = alloc<FlowSolveDesc>(kMaxObj);
   d_poses3_[q] = alloc<float>(16 * kMaxObj);
   d_lmstats3_[q] = alloc<int>(3 * kMaxObj);
@@ -642,6 +643,8 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     d.cap = lm_cap_;
     d.pose_out = d_poses3_[q] + 16 * i;
     d.stats = d_lmstats3_[q] + 3 * i;
+    d.g0 = g0_;  // the centroid's depth noise (the solve itself runs without noise)
+    d.centre_out = d_centre_[q] + 3 * i;
   }
   MMT_HIP(hipMemcpyAsync(d_descs3_[q], H.descs, sizeof(FlowSolveDesc) * nobj,
                          hipMemcpyHostToDevice, st));
@@ -674,6 +677,8 @@ void Tracker::obj_stage_b(ObjFrame& F) {
   MMT_HIP(hipMemcpyAsync(H.X, d_poses3_[q], sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(H.lst, d_lmstats3_[q], sizeof(int) * 3 * nobj, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(H.nsub, d_nsub_[q], sizeof(int) * nobj, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(H.centre, d_centre_[q], sizeof(float) * 3 * nobj,
+                         hipMemcpyDeviceToHost, st));
   MMT_HIP(hipEventRecord(ev_d3_[q], st));
 }
 
@@ -708,6 +713,7 @@ void Tracker::obj_finish(ObjFrame& F) {
     oo.iterations = H.lst[3 * i];
     memcpy(oo.X, Xi, 64);
     memcpy(oo.motion, C.vObjMod[i].data(), 64);
+    if (H.lst[3 * i + 2] == 0) memcpy(oo.centre_pre, H.centre + 3 * i, 12);
     out.objects.push_back(oo);
   }
 }

@@ -254,7 +254,7 @@ class Tracker:
         tcw = np.zeros(16, np.float32)
         info = np.zeros(7, np.int32)
         oi = np.zeros((16, 8), np.int32)
-        of = np.zeros((16, 48), np.float32)
+        of = np.zeros((16, 51), np.float32)
         lib().oracle_tracker_track(self._h, _p(bgr), _p(disp), _p(flow), _p(mask), _p(tcw),
                                    _p(info), _p(oi), _p(of), 16)
         objs = []
@@ -263,7 +263,8 @@ class Tracker:
                              ransac_inliers=int(oi[i, 3]), mm_inliers=int(oi[i, 4]),
                              n_solve=int(oi[i, 5]), n_inliers=int(oi[i, 6]),
                              iterations=int(oi[i, 7]), init=of[i, :16].reshape(4, 4),
-                             X=of[i, 16:32].reshape(4, 4), motion=of[i, 32:].reshape(4, 4)))
+                             X=of[i, 16:32].reshape(4, 4), motion=of[i, 32:48].reshape(4, 4),
+                             centre_pre=of[i, 48:51].copy()))
         return dict(initialized=bool(info[0]), Tcw=tcw.reshape(4, 4), n_keys=int(info[1]),
                     n_static=int(info[2]), n_obj_samples=int(info[3]), ego_iterations=int(info[4]),
                     ego_inliers=int(info[5]), objects=objs)

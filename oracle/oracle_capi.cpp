@@ -249,7 +249,7 @@ void oracle_tracker_destroy(void* t) { delete (OTracker*)t; }
 
 // Tracks one frame.  info: [initialized, n_keys, n_static, n_obj_samples, ego_iters,
 // ego_inliers, n_objects].  objs: per object 8 ints (label, sem, n_points, ransac_inliers,
-// mm_inliers, n_solve, n_inliers, iterations) + 48 floats (init, X, motion).
+// mm_inliers, n_solve, n_inliers, iterations) + 51 floats (init, X, motion, centre_pre).
 int oracle_tracker_track(void* tp, const uint8_t* bgr, const uint16_t* disp, const float* flow,
                          const int32_t* mask, float* tcw, int* info, int* obj_i, float* obj_f,
                          int obj_cap) {
@@ -269,10 +269,11 @@ int oracle_tracker_track(void* tp, const uint8_t* bgr, const uint16_t* disp, con
     int* oi = obj_i + 8 * i;
     oi[0] = o.label; oi[1] = o.sem_label; oi[2] = o.n_points; oi[3] = o.n_ransac_inliers;
     oi[4] = o.n_mm_inliers; oi[5] = o.n_solve; oi[6] = o.n_inliers; oi[7] = o.iterations;
-    float* of = obj_f + 48 * i;
+    float* of = obj_f + 51 * i;
     memcpy(of, o.init, 64);
     memcpy(of + 16, o.X, 64);
     memcpy(of + 32, o.motion, 64);
+    memcpy(of + 48, o.centre_pre, 12);
   }
   return 0;
 }

@@ -41,6 +41,7 @@ struct ObjectResult {
   int label = 0, sem_label = 0, n_points = 0, n_ransac_inliers = 0, n_mm_inliers = -1;
   int n_solve = 0, n_inliers = 0, iterations = 0;
   float init[16], X[16], motion[16];
+  float centre_pre[3] = {0, 0, 0};  // ObjCentre3D_pre (Tracking.cc:2032-2049)
   std::vector<int> ids, sub;
 };
 

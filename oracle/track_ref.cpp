@@ -442,7 +442,23 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
     fp.fx = P.fx; fp.fy = P.fy; fp.cx = P.cx; fp.cy = P.cy;
     float X[16];
     FlowSolveStats st;
-    if (flow_pose_solve(fp, X, &st) != 0) mat4_eye(X);
+    const bool solved = flow_pose_solve(fp, X, &st) == 0;
+    if (!solved) mat4_eye(X);
+    // ObjCentre3D_pre (Tracking.cc:2032-2049): float sum, in order, of the last frame's
+    // UnprojectStereoObject(j, 1) (Frame.cc:1118-1152: z + (float)gaussian(z^2 / 362.5 * 0.15),
+    // the RNG's first draw g0), then cv::Mat / size: * (1.0 / n) in double, rounded to float
+    float centre[3] = {0, 0, 0};
+    if (solved) {
+      for (int i = 0; i < NS; i++) {
+        float z = dep[i];
+        const float noise = (float)((double)g0 * ((double)(z * z) / (725 * 0.5) * 0.15));
+        z = z + noise;
+        float xw[3];
+        unproject_world(P, L.Tcw, obs[2 * i], obs[2 * i + 1], z, xw);
+        for (int r = 0; r < 3; r++) centre[r] = centre[r] + xw[r];
+      }
+      for (int r = 0; r < 3; r++) centre[r] = (float)((double)centre[r] * (1.0 / NS));
+    }
     mat4_mul(TcwInv, X, C.vObjMod[oi].data());
     ObjectResult r;
     r.label = C.nModLabel[oi];
@@ -456,6 +472,7 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
     memcpy(r.init, Init, sizeof(r.init));
     memcpy(r.X, X, sizeof(r.X));
     memcpy(r.motion, C.vObjMod[oi].data(), sizeof(r.motion));
+    memcpy(r.centre_pre, centre, sizeof(r.centre_pre));
     r.ids = ids;
     r.sub = sub;
     out.objects.push_back(r);

@@ -1,7 +1,9 @@
 """GPU test of the rgbd_mmt drop-in: the reference's sequence layout is written
 from the kitti_sample fixture (PNG image + u16 disparity, .flo, semantic text, times.txt,
-pose_gt.txt, settings yaml), rgbd_mmt tracks it through libmmt, and its poses equal the
-C-ABI's mmt_track_rgbd on the same decoded frames bit for bit and the CPU oracle within 1e-4."""
+pose_gt.txt, object_pose.txt, settings yaml), rgbd_mmt tracks it through libmmt, and its poses
+equal the C-ABI's mmt_track_rgbd on the same decoded frames bit for bit and the CPU oracle within
+1e-4; its per-object speed and relative-pose-error lines equal a float64 restatement over the
+C-ABI's object motions and centroids to the printed precision."""
 import json
 import os
 import subprocess
@@ -34,6 +36,10 @@ def write_sequence(d):
     with open(os.path.join(d, "pose_gt.txt"), "w") as f:
         for row in meta["pose_gt"]:
             f.write("%d " % int(row[0]) + " ".join("%.9f" % v for v in row[1:]) + "\n")
+    with open(os.path.join(d, "object_pose.txt"), "w") as f:
+        for row in meta["object_pose"]:
+            f.write("%d %d " % (int(row[0]), int(row[1])) +
+                    " ".join("%.9g" % v for v in row[2:]) + "\n")
     with open(os.path.join(d, "settings.yaml"), "w") as f:
         f.write("%YAML:1.0\n")
         for k, v in meta["settings"].items():
@@ -58,10 +64,55 @@ def test_cli_tracks_sequence_like_the_c_abi(tmp_path, oracle_mod):
     ctx = M.Context(M.kitti03_config(nfeatures=2000))
     tr = oracle_mod.Tracker(1242, 375, (ctx.cfg.fx, ctx.cfg.fy, ctx.cfg.cx, ctx.cfg.cy),
                             ctx.cfg.bf, 0, 2000)
+    expected = []
+    meta = kitti_meta()
+    gt = {int(r[0]): np.array(r[1:], np.float64).reshape(4, 4) for r in meta["pose_gt"]}
     for i in range(n):
         f = load_kitti_frame(i)
         g = ctx.track(f["bgr"], f["disp"], f["flow"], f["sem"])
         o = tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
         assert np.abs(cli[i] - g["Tcw"]).max() <= 1e-6  # printed with 9 decimals
         assert np.abs(cli[i] - o["Tcw"]).max() < 1e-4
+        if i > 0:
+            for ob in g["objects"]:
+                e = object_eval(ob, gt[i - 1], gt[i], meta["object_pose"], i)
+                if e is not None:
+                    expected.append(e)
     ctx.close()
+    # the per-object evaluation lines (Tracking.cc:2178-2243) against a float64 restatement
+    # over the C-ABI's vObjMod and ObjCentre3D_pre (printed with 4 decimals)
+    speeds = [l for l in r.stdout.splitlines() if l.startswith("estimated and ground truth")]
+    rpes = [l for l in r.stdout.splitlines() if l.startswith("the relative pose error of the "
+                                                             "object, t:") and "%" in l]
+    assert len(expected) > 0 and len(speeds) == len(expected) == len(rpes)
+    for line, rpe, e in zip(speeds, rpes, expected):
+        got = [float(v) for v in line.split(":")[1].replace("km/h", " ").split()]
+        assert np.allclose(got, e[:3], rtol=1e-3, atol=2e-3), (line, e)
+        t_pct = float(rpe.split("t:")[1].split("%")[0])
+        assert abs(t_pct - e[3]) <= 1e-3 * max(1.0, abs(e[3])) + 2e-3, (rpe, e)
+
+
+def _obj_pose(row):
+    """Tracking::ObjPoseParsing: R = Ry(ry + pi/2), t = row[6:9]."""
+    y = row[9] + 3.1415926 / 2
+    P = np.eye(4)
+    P[:3, :3] = [[np.cos(y), 0, np.sin(y)], [0, 1, 0], [-np.sin(y), 0, np.cos(y)]]
+    P[:3, 3] = row[6:9]
+    return P
+
+
+def object_eval(ob, Tlw_gt, Tcw_gt, rows, i):
+    """Speeds (est, gt, |diff|) in km/h and t_rpe/t_gt in % for one object of frame i."""
+    rp = [r for r in rows if int(r[0]) == i - 1 and int(r[1]) == ob["sem_label"]]
+    rc = [r for r in rows if int(r[0]) == i and int(r[1]) == ob["sem_label"]]
+    if not rp or not rc:
+        return None
+    Lwp = np.linalg.inv(Tlw_gt) @ _obj_pose(np.array(rp[0], np.float64))
+    Lwc = np.linalg.inv(Tcw_gt) @ _obj_pose(np.array(rc[0], np.float64))
+    H = Lwc @ np.linalg.inv(Lwp)
+    sp_gt = np.linalg.norm(Lwp[:3, 3] - Lwc[:3, 3])
+    M = ob["motion"].astype(np.float64)
+    sp_est = np.linalg.norm(M[:3, 3] - (np.eye(3) - M[:3, :3]) @ ob["centre_pre"])
+    E = np.linalg.inv(M) @ H
+    t_rpe, t_gt = np.linalg.norm(E[:3, 3]), np.linalg.norm(H[:3, 3])
+    return (sp_est * 36, sp_gt * 36, abs(sp_est - sp_gt) * 36, t_rpe / t_gt * 100)

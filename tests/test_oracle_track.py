@@ -119,3 +119,36 @@ def test_pose_optimization_oracle_few_edges(oracle_mod):
     Xw, obs, s2, init, _ = pose_opt_problem(1, 2)
     n_in, pose, outl = oracle_mod.pose_optimization(Xw, obs, s2, init, K_KITTI, 387.5744)
     assert n_in == 0 and np.array_equal(pose, init) and not outl.any()
+
+
+def test_tracker_oracle_object_centroid_and_speed(oracle_mod, kitti_frames):
+    """ObjCentre3D_pre (Tracking.cc:2032-2049) is the mean world point of the object's solve
+    samples (the RANSAC inliers): it lies within 2 m of the mean of all the object's sampled pixels
+    (B1's grid: every 4th row and column, 0 < depth < 25), unprojected with the tracker's
+    last-frame pose; the speed estimate of Tracking.cc:2186 built from it is finite and bounded."""
+    tr = oracle_mod.Tracker(1242, 375, K_KITTI, 387.5744, 0, 2000)
+    fx, fy, cx, cy = K_KITTI
+    checked, prev_T = 0, None
+    for i, f in enumerate(kitti_frames):
+        r = tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+        if i > 0:
+            pf = kitti_frames[i - 1]
+            d = pf["disp"].astype(np.float64)
+            z = np.where(d > 0, 387.5744 / np.maximum(d / 256.0, 1e-9), 0.0)
+            Twc = np.linalg.inv(prev_T.astype(np.float64))
+            for ob in r["objects"]:
+                sel = np.zeros_like(z, bool)
+                sel[::4, ::4] = True
+                sel &= (pf["sem"] == ob["sem_label"]) & (z > 0) & (z < 25)
+                v, u = np.nonzero(sel)
+                zz = z[v, u]
+                Xc = np.stack([(u - cx) * zz / fx, (v - cy) * zz / fy, zz, np.ones_like(zz)])
+                mean_w = (Twc @ Xc)[:3].mean(1)
+                c = ob["centre_pre"].astype(np.float64)
+                assert np.linalg.norm(c - mean_w) < 2.0, (i, ob["sem_label"], c, mean_w)
+                M = ob["motion"].astype(np.float64)
+                vel = M[:3, 3] - (np.eye(3) - M[:3, :3]) @ c
+                assert np.isfinite(vel).all() and np.linalg.norm(vel) * 36 < 200.0
+                checked += 1
+        prev_T = r["Tcw"]
+    assert checked >= 2
