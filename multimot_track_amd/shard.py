@@ -20,7 +20,10 @@ def sequence_seed(base, rank):
 
 def barrier(world, device=None):
     if world > 1:
-        dist.barrier()
+        if device is not None and device.type == "cuda" and dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[device.index])  # RCCL: the rank's own GPU, no guessing
+        else:
+            dist.barrier()
     if device is not None and device.type == "cuda":
         torch.cuda.synchronize(device)
 
