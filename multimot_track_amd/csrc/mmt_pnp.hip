@@ -1279,53 +1279,14 @@ __global__ __launch_bounds__(256) void k_refit_rt(PnPObject* objs) {
   }
 }
 
-// motion-model inliers, ascending (GetInitModelObj, Tracking.cc:4380-4399); MM row-major float
+// motion-model inliers (pnp_mm_inliers_block, mmt_pnp.h), one workgroup per object
 __global__ __launch_bounds__(256) void k_mm_inliers(PnPObject* objs) {
-  __shared__ int s_w[4];
-  PnPObject& o = objs[blockIdx.x];
-  if (!o.use_mm) return;
-  const int n = *o.n;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int base = 0;
-  for (int i0 = 0; i0 < n; i0 += blockDim.x) {
-    const int i = i0 + threadIdx.x;
-    bool in = false;
-    if (i < n) {
-      float xc[3];
-      for (int r = 0; r < 3; r++) {
-        double s = 0;
-        for (int k = 0; k < 3; k++) s += (double)o.MM[4 * r + k] * (double)o.pts3[3 * i + k];
-        xc[r] = (float)s + o.MM[4 * r + 3];
-      }
-      const float invzc = (float)(1.0 / (double)xc[2]);
-      const float u = o.fx * xc[0] * invzc + o.cx, v = o.fy * xc[1] * invzc + o.cy;
-      const float2 q = o.pts2[i];
-      const float u_ = q.x - u, v_ = q.y - v;
-      const float Rpe = sqrtf(u_ * u_ + v_ * v_);
-      in = (double)Rpe < o.reproj;
-    }
-    const unsigned long long bal = __ballot(in);
-    if (lane == 0) s_w[wave] = __popcll(bal);
-    __syncthreads();
-    int off = 0, tot = 0;
-    for (int w = 0; w < 4; w++) {
-      if (w < wave) off += s_w[w];
-      tot += s_w[w];
-    }
-    if (in) o.mm_inliers[base + off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-    base += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) o.result[4] = base;
+  pnp_mm_inliers_block(objs[blockIdx.x]);
 }
 
-// D3 edge index list: ObjId_sub[i] = ObjId[inliers[i]] (sample indices)
+// D3 edge index list (pnp_subset_block, mmt_pnp.h), one workgroup per object
 __global__ __launch_bounds__(256) void k_pnp_subset(PnPObject* objs) {
-  PnPObject& o = objs[blockIdx.x];
-  const int n = o.use_mm_choice ? o.result[4] : o.result[3];
-  const int* src = o.use_mm_choice ? o.mm_inliers : o.inliers;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) o.subset[i] = o.members[src[i]];
-  if (threadIdx.x == 0) *o.n_subset = n;
+  pnp_subset_block(objs[blockIdx.x]);
 }
 
 // ---------------------------------------------------------------- D6: PnPsolver (P4P RANSAC)

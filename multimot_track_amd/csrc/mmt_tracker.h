@@ -41,6 +41,9 @@ struct MMPrepArgs {
   float TcwPrev[16], TcwCur[16];
 };
 void launch_obj_mm_prep(const MMPrepArgs& a, hipStream_t st);
+// the four kernels of stage B (motion-model matrix and inliers, model choice, D3 edge list) as
+// one launch, one workgroup per object
+void launch_obj_stage_b(const MMPrepArgs& a, FlowSolveDesc* descs, float* init, hipStream_t st);
 void launch_obj_model_choice(PnPObject* objs, int nobj, FlowSolveDesc* descs, float* init,
                              hipStream_t st);
 // RANSACPointSetRegistrator::getSubset draws (5-point subsets) for a point count.

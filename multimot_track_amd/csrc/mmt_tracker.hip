@@ -665,11 +665,8 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     mp.prevStats = d_lmstats3_[Ls.obj_slot];
     memcpy(mp.TcwPrev, Ls.Tcw, sizeof(mp.TcwPrev));
     memcpy(mp.TcwCur, C.Tcw, sizeof(mp.TcwCur));
-    launch_obj_mm_prep(mp, st);
-    launch_pnp_mm(d_pnp_[q], nobj, st);
   }
-  launch_obj_model_choice(d_pnp_[q], nobj, d_descs3_[q], d_init_[q], st);
-  launch_pnp_subset(d_pnp_[q], nobj, st);
+  launch_obj_stage_b(mp, d_descs3_[q], d_init_[q], st);
   launch_flow_lm(d_descs3_[q], nobj, 256, st);
   // everything the finish reads, in one pinned block
   MMT_HIP(hipMemcpyAsync(H.res, d_res_[q], sizeof(int) * 8 * nobj, hipMemcpyDeviceToHost, st));
@@ -755,6 +752,55 @@ __global__ void k_obj_model_choice(PnPObject* objs, int nobj, FlowSolveDesc* des
     descs[i].init[k] = v;
     init[16 * i + k] = v;
   }
+}
+
+// Stage B of one frame's objects in one launch (one workgroup per object; the objects are
+// independent): the motion-model matrix (k_obj_mm_prep), its inliers (pnp_mm_inliers_block), the
+// model choice that seeds D3 (k_obj_model_choice) and D3's edge list (pnp_subset_block) -- the
+// same code as the four separate kernels, without three dependent launches on the critical
+// chain.
+__global__ __launch_bounds__(256) void k_obj_stage_b(MMPrepArgs a, FlowSolveDesc* descs,
+                                                     float* init) {
+  const int i = blockIdx.x;
+  PnPObject& o = a.objs[i];
+  if (threadIdx.x == 0 && a.pre[i] >= 0) {
+    const int p = a.pre[i];
+    float X[16], Ti[16], vobj[16], MM[16];
+    if (a.prevStats[3 * p + 2] != 0)
+      mat4_eye(X);
+    else
+      for (int k = 0; k < 16; k++) X[k] = a.prevX[16 * p + k];
+    inv_mat(a.TcwPrev, Ti);
+    mat4_mul(Ti, X, vobj);
+    mat4_mul(a.TcwCur, vobj, MM);
+    for (int k = 0; k < 16; k++) o.MM[k] = MM[k];
+  }
+  __syncthreads();
+  pnp_mm_inliers_block(o);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int n_ransac = o.result[0] >= 0 ? o.result[3] : 0;
+    const int n_mm = o.use_mm ? o.result[4] : -1;
+    float Mod[16];
+    mat4_eye(Mod);
+    for (int r = 0; r < 3; r++) {
+      for (int c = 0; c < 3; c++) Mod[4 * r + c] = (float)o.Rt[3 * r + c];
+      Mod[4 * r + 3] = (float)o.Rt[9 + r];
+    }
+    const bool choice = o.use_mm && !(n_ransac > n_mm);
+    o.use_mm_choice = choice ? 1 : 0;
+    for (int k = 0; k < 16; k++) {
+      const float v = choice ? o.MM[k] : Mod[k];
+      descs[i].init[k] = v;
+      init[16 * i + k] = v;
+    }
+  }
+  __syncthreads();
+  pnp_subset_block(o);
+}
+
+void launch_obj_stage_b(const MMPrepArgs& a, FlowSolveDesc* descs, float* init, hipStream_t st) {
+  hipLaunchKernelGGL(k_obj_stage_b, dim3(a.nobj), dim3(256), 0, st, a, descs, init);
 }
 
 void launch_obj_mm_prep(const MMPrepArgs& a, hipStream_t st) {
