@@ -43,3 +43,10 @@ print("D3 queue %s: k_flow_lm mean %.1f us; end-to-start gap to the next D3 mean
       "(median %.1f)" % (d3q, np.mean(lm) / 1e3, np.mean(gaps) / 1e3, np.median(gaps) / 1e3))
 for k, v in sorted(between.items(), key=lambda kv: -np.mean(kv[1])):
     print("   %-22s %6.1f us per gap" % (k, np.mean(v) / 1e3))
+g = np.array(gaps) / 1e3
+print("gap percentiles (us): p50 %.0f p75 %.0f p90 %.0f p95 %.0f p99 %.0f max %.0f; gaps > 300 us: "
+      "%d of %d, their share of the total gap time %.0f%%" % (
+          np.percentile(g, 50), np.percentile(g, 75), np.percentile(g, 90), np.percentile(g, 95),
+          np.percentile(g, 99), g.max(), (g > 300).sum(), len(g), 100 * g[g > 300].sum() / g.sum()))
+big = [i for i, v in enumerate(g) if v > 300]
+print("indices of gaps > 300 us:", big[:40])
