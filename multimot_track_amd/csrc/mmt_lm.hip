@@ -559,7 +559,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   const int n_reg = IR * nt;
   // one edge per thread: keep w J of the current linearisation in registers, so the
   // back-substitution needs no projection
-  constexpr bool kCacheB = IR == 1;
+  constexpr bool kCacheB = true;  // register item 0 of every thread
   double RB[12];
   // The LM bookkeeping below is computed redundantly by every thread from the block sums in LDS
   // (identical inputs, identical results), so only the 6x6 solve needs a lane-0 section.
