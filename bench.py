@@ -47,6 +47,17 @@ def b_orb(w, h, nfeat, lw, lh):
     return 3 * w * h + 4 * P + 60 * nfeat + 6 * w * h
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), for the CPU baseline record."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def load_traffic(path, cfg_key):
     """HBM bytes per ORB launch sequence from a committed rocprofv3 --pmc summary (or None)."""
     try:
@@ -156,18 +167,27 @@ def main():
             kcam = (cfg.fx, cfg.fy, cfg.cx, cfg.cy)
             tr = O.Tracker(W, H, kcam, cfg.bf, 0, NF)
             n_done, tcpu = 0, 0.0
-            while tcpu < args.cpu_seconds and n_done < nframes:
-                f = scene.to_numpy_frames({k: seq[k][n_done:n_done + 1]
-                                           for k in ("bgr", "disp", "flow", "mask")})[0]
-                tc = time.perf_counter()
-                tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
-                tcpu += time.perf_counter() - tc
-                n_done += 1
+            # one pinned core (the process's first allowed CPU), restored afterwards
+            affinity = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+            if affinity:
+                os.sched_setaffinity(0, {min(affinity)})
+            try:
+                while tcpu < args.cpu_seconds and n_done < nframes:
+                    f = scene.to_numpy_frames({k: seq[k][n_done:n_done + 1]
+                                               for k in ("bgr", "disp", "flow", "mask")})[0]
+                    tc = time.perf_counter()
+                    tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+                    tcpu += time.perf_counter() - tc
+                    n_done += 1
+            finally:
+                if affinity:
+                    os.sched_setaffinity(0, affinity)
             cpu = {"value": round(n_done / tcpu, 3), "unit": "frames/s", "cores": 1,
-                   "kind": "port",
+                   "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
                    "sample": "first %d frames of the same C3 sequence, full per-frame tracking "
                              "(oracle/track_ref.cpp: ORB, association, ego + object solves), "
-                             "single thread, %.1f s of CPU time" % (n_done, tcpu)}
+                             "single thread pinned to one core, %.1f s of CPU time"
+                             % (n_done, tcpu)}
         out = {
             "metric": METRIC,
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
