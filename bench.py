@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--chunk", type=int, default=64,
+    ap.add_argument("--chunk", type=int, default=128,
                     help="frames per step (ORB batch; SURVEY 8(d): >= 64 frames in flight)")
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--height", type=int, default=375)
@@ -99,9 +99,21 @@ def main():
     W, H, NF, C, K = args.width, args.height, args.nfeatures, args.chunk, args.seqs_per_gpu
     nframes = (args.warmup + args.steps) * C
     t_gen = time.perf_counter()
-    seqs = [scene.kitti_like_sequence(nframes, W, H, n_objects=args.objects,
-                                      seed=shard.sequence_seed(1003, rank * K + k), device=dev)
-            for k in range(K)]
+    def render(seed):
+        # in pieces of 400 frames (each frame is rendered on its own, so the sequence is the
+        # same), with a progress line on stderr for long runs under a profiler
+        parts = []
+        for s0 in range(0, nframes, 400):
+            parts.append(scene.kitti_like_sequence(min(400, nframes - s0), W, H,
+                                                   n_objects=args.objects, seed=seed,
+                                                   device=dev, start=s0))
+            print("rank %d: rendered %d / %d frames" % (rank, s0 + len(parts[-1]["Tcw"]),
+                                                         nframes), file=sys.stderr, flush=True)
+        out = {k: torch.cat([p[k] for p in parts]) for k in ("bgr", "disp", "flow", "mask")}
+        out["Tcw"] = np.concatenate([p["Tcw"] for p in parts])
+        return out
+
+    seqs = [render(shard.sequence_seed(1003, rank * K + k)) for k in range(K)]
     seq = seqs[0]
     torch.cuda.synchronize(dev)
     t_gen = time.perf_counter() - t_gen
