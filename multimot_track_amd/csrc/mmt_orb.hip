@@ -1075,7 +1075,7 @@ __device__ __forceinline__ void oct_run(OctLDS& S, const KA& kk, const LevelInfo
   }
 }
 
-// One workgroup per (level, frame).  Keys of the level live in LDS when at most kcap of them
+// One workgroup per (frame, level), dispatched level-major.  Keys of the level live in LDS when at most kcap of them
 // survived FAST (the usual case), in global scratch otherwise.
 // kWaves: minimum waves per SIMD the register allocation must allow.  8 (at most 64 VGPRs) lets
 // two 1024-thread workgroups share a CU when their LDS fits in half of it (the launch of levels
@@ -1094,7 +1094,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kWaves))) 
                                                  int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_generic[];
   LDS unsigned char* smem = (LDS unsigned char*)smem_generic;
-  const int level = level_begin + blockIdx.x, frame = blockIdx.y;
+  // frames along x: workgroups are dispatched level-major, the heavy low levels first, so the
+  // light levels fill in behind them instead of heavy workgroups trailing at the end
+  const int level = level_begin + blockIdx.y, frame = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
   const LevelInfo L0 = lv[level];
   // ---- carve LDS (oct_layout: the same offsets the host sized the launch with)
@@ -1144,7 +1146,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kWaves))) 
     // global scratch: knode as u16 in the u32 slots, quadrant bytes after all frames' knode
     uint32_t* lk = lkeys + (size_t)frame * total_slots + L0.key_off;
     uint16_t* knode = (uint16_t*)(knode_g + (size_t)frame * total_slots + L0.key_off);
-    uint8_t* kq = (uint8_t*)(knode_g + (size_t)gridDim.y * total_slots) +
+    uint8_t* kq = (uint8_t*)(knode_g + (size_t)gridDim.x * total_slots) +
                   (size_t)frame * total_slots + L0.key_off;
     OctKeys<uint32_t*, uint16_t*, uint8_t*> kk{lk, knode, kq};
     oct_run(S, kk, L0, cells, cnt, nc, fk, n, outp, ocount_p, ncap, err);
@@ -1768,7 +1770,7 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
   auto octree = [&](int l0, int l1, hipStream_t st) {
     // level 0 alone: the full-LDS variant; levels 1..: two workgroups per CU when they fit
     const bool two = l0 > 0 && oct_two_per_cu_;
-    hipLaunchKernelGGL(two ? k_octree<8> : k_octree<1>, dim3(l1 - l0, nframes), dim3(1024),
+    hipLaunchKernelGGL(two ? k_octree<8> : k_octree<1>, dim3(nframes, l1 - l0), dim3(1024),
                        two ? octree_lds1_ : octree_lds_, st, d_lv_, d_cells_, ncells_, d_keys_,
                        d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_, out_slots_,
                        d_ocount_, nlevels_, node_cap_, two ? key_cap1_ : key_cap_, l0, d_err_);
