@@ -157,6 +157,17 @@ class Tracker {
   int obj_slot_next_ = 0;
   // Pinned host side of the object path, one per object slot: every host<->device transfer of the
   // stages and the finish is a single asynchronous copy into or out of this block.
+  // Everything the finish reads from the device: one block per object slot, written by the
+  // RANSAC, stage B and D3 kernels and brought back with a single copy behind the D3 launch
+  // (small copies cost a queue round trip each on the critical D3 stream).
+  struct ObjResults {
+    int res[8 * kMaxObj];      // PnP results of all objects
+    float init[16 * kMaxObj];  // chosen D3 initial motion per object
+    float X[16 * kMaxObj];     // D3 poses
+    int lst[3 * kMaxObj];      // D3 stats
+    int nsub[kMaxObj];
+    float centre[3 * kMaxObj];  // ObjCentre3D_pre per object (D3 kernel output)
+  };
   struct ObjHost {
     LabelStats stats[kMaxLabel];
     int hist[kMaxLabel * kMaxLabel];
@@ -164,22 +175,12 @@ class Tracker {
     PnPObject po[kMaxObj];
     int subsets[kMaxObj][5 * kRansacIters];
     FlowSolveDesc descs[kMaxObj];
-    int res[8 * kMaxObj];
-    float init[16 * kMaxObj];
-    float X[16 * kMaxObj];
-    int lst[3 * kMaxObj];
-    int nsub[kMaxObj];
-    float centre[3 * kMaxObj];
+    ObjResults r;
   };
   ObjHost* oh_[kObjSlots] = {};
-  int* d_res_[kObjSlots] = {};     // PnP results of all objects, contiguous
+  ObjResults* d_r_[kObjSlots] = {};
   double* d_Rt_[kObjSlots] = {};
-  int* d_nsub_[kObjSlots] = {};
-  float* d_centre_[kObjSlots] = {};  // ObjCentre3D_pre per object (D3 kernel output)
   FlowSolveDesc* d_descs3_[kObjSlots] = {};  // D3 solves of the slot's frame
-  float* d_poses3_[kObjSlots] = {};
-  int* d_lmstats3_[kObjSlots] = {};
-  float* d_init_[kObjSlots] = {};  // chosen D3 initial motion per object
   hipEvent_t ev_ransac_[kObjSlots] = {};
   hipEvent_t ev_d3_[kObjSlots] = {};
   // subset draws depend only on the point count: cache the last few counts

@@ -218,14 +218,9 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   mask_words_ = (ocap_ + 63) / 64;
   for (int q = 0; q < kObjSlots; q++) {
   d_pnp_[q] = alloc<PnPObject>(kMaxObj);
-  d_res_[q] = alloc<int>(8 * kMaxObj);
+  d_r_[q] = alloc<ObjResults>(1);
   d_Rt_[q] = alloc<double>(12 * kMaxObj);
-  d_nsub_[q] = alloc<int>(kMaxObj);
-  d_centre_[q] = alloc<float>(3 * kMaxObj);
   d_descs3_[q] = alloc<FlowSolveDesc>(kMaxObj);
-  d_poses3_[q] = alloc<float>(16 * kMaxObj);
-  d_lmstats3_[q] = alloc<int>(3 * kMaxObj);
-  d_init_[q] = alloc<float>(16 * kMaxObj);
   if (!oh_[q]) MMT_HIP(hipHostMalloc((void**)&oh_[q], sizeof(ObjHost), hipHostMallocDefault));
   memset(oh_[q], 0, sizeof(ObjHost));
   if (!ev_ransac_[q]) MMT_HIP(hipEventCreateWithFlags(&ev_ransac_[q], hipEventDisableTiming));
@@ -243,8 +238,8 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     b.inliers = alloc<int>(ocap_);
     b.mm_inliers = alloc<int>(ocap_);
     b.subset = alloc<int>(ocap_);
-    b.n_subset = d_nsub_[q] + o;
-    b.result = d_res_[q] + 8 * o;
+    b.n_subset = d_r_[q]->nsub + o;
+    b.result = d_r_[q]->res + 8 * o;
     b.Rt = d_Rt_[q] + 12 * o;
   }
   }
@@ -611,7 +606,7 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   }
   MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po, sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
   launch_pnp(d_pnp_[q], nobj, kRansacIters, st);
-  MMT_HIP(hipEventRecord(ev_ransac_[q], st));
+  // ev_ransac_[q] is recorded by stage B, behind the D3 descriptors' copy on this stream
 }
 
 void Tracker::obj_stage_b(ObjFrame& F) {
@@ -623,7 +618,6 @@ void Tracker::obj_stage_b(ObjFrame& F) {
   ObjHost& H = *oh_[q];
   // behind this frame's RANSAC (oa_) by an event, behind the previous frame's D3 (whose motions
   // the motion model needs) by the stream
-  MMT_HIP(hipStreamWaitEvent(st, ev_ransac_[q], 0));
   // D3 descriptors; the initial motion is the device's model choice (k_obj_model_choice)
   for (int i = 0; i < nobj; i++) {
     FlowSolveDesc& d = H.descs[i];
@@ -641,13 +635,16 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     d.fx = cfg_.fx; d.fy = cfg_.fy; d.cx = cfg_.cx; d.cy = cfg_.cy;
     d.scratch = d_lm_scratch_ + flow_scratch_doubles(lm_cap_) * (1 + i);
     d.cap = lm_cap_;
-    d.pose_out = d_poses3_[q] + 16 * i;
-    d.stats = d_lmstats3_[q] + 3 * i;
+    d.pose_out = d_r_[q]->X + 16 * i;
+    d.stats = d_r_[q]->lst + 3 * i;
     d.g0 = g0_;  // the centroid's depth noise (the solve itself runs without noise)
-    d.centre_out = d_centre_[q] + 3 * i;
+    d.centre_out = d_r_[q]->centre + 3 * i;
   }
+  // the descriptors go up on the RANSAC stream, off the D3 chain
   MMT_HIP(hipMemcpyAsync(d_descs3_[q], H.descs, sizeof(FlowSolveDesc) * nobj,
-                         hipMemcpyHostToDevice, st));
+                         hipMemcpyHostToDevice, oa_));
+  MMT_HIP(hipEventRecord(ev_ransac_[q], oa_));
+  MMT_HIP(hipStreamWaitEvent(st, ev_ransac_[q], 0));
   // motion model (Tracking.cc:4375-4405): MM = Tcw * vObjMod[PreObjID] of the previous frame,
   // whose D3 output is still in its slot's buffers
   bool any_mm = false;
@@ -661,21 +658,15 @@ void Tracker::obj_stage_b(ObjFrame& F) {
   }
   if (any_mm) {
     if (Ls.obj_slot < 0) throw ArgError("motion model without a previous object solve");
-    mp.prevX = d_poses3_[Ls.obj_slot];
-    mp.prevStats = d_lmstats3_[Ls.obj_slot];
+    mp.prevX = d_r_[Ls.obj_slot]->X;
+    mp.prevStats = d_r_[Ls.obj_slot]->lst;
     memcpy(mp.TcwPrev, Ls.Tcw, sizeof(mp.TcwPrev));
     memcpy(mp.TcwCur, C.Tcw, sizeof(mp.TcwCur));
   }
-  launch_obj_stage_b(mp, d_descs3_[q], d_init_[q], st);
+  launch_obj_stage_b(mp, d_descs3_[q], d_r_[q]->init, st);
   launch_flow_lm(d_descs3_[q], nobj, 256, st);
   // everything the finish reads, in one pinned block
-  MMT_HIP(hipMemcpyAsync(H.res, d_res_[q], sizeof(int) * 8 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(H.init, d_init_[q], sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(H.X, d_poses3_[q], sizeof(float) * 16 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(H.lst, d_lmstats3_[q], sizeof(int) * 3 * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(H.nsub, d_nsub_[q], sizeof(int) * nobj, hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(H.centre, d_centre_[q], sizeof(float) * 3 * nobj,
-                         hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(&H.r, d_r_[q], sizeof(ObjResults), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipEventRecord(ev_d3_[q], st));
 }
 
@@ -690,7 +681,7 @@ void Tracker::obj_finish(ObjFrame& F) {
   float TcwInv[16];
   inv_mat(C.Tcw, TcwInv);
   for (int i = 0; i < nobj; i++) {
-    const int* res = H.res + 8 * i;
+    const int* res = H.r.res + 8 * i;
     ObjOut oo;
     oo.label = F.LabId[i];
     oo.sem_label = F.labels[i];
@@ -698,19 +689,19 @@ void Tracker::obj_finish(ObjFrame& F) {
     oo.n_ransac_inliers = res[0] >= 0 ? res[3] : 0;
     oo.n_mm_inliers = F.po[i].use_mm ? res[4] : -1;
     oo.ransac_iterations = res[2];
-    memcpy(oo.init, H.init + 16 * i, 64);
+    memcpy(oo.init, H.r.init + 16 * i, 64);
     float Xi[16];
-    if (H.lst[3 * i + 2] != 0)
+    if (H.r.lst[3 * i + 2] != 0)
       mat4_eye(Xi);  // fewer than 3 correspondences: PoseOptimizationFlow2 returns identity
     else
-      memcpy(Xi, H.X + 16 * i, 64);
+      memcpy(Xi, H.r.X + 16 * i, 64);
     mat4_mul(TcwInv, Xi, C.vObjMod[i].data());
-    oo.n_solve = H.nsub[i];
-    oo.n_inliers = H.lst[3 * i + 2] ? 0 : H.lst[3 * i + 1];
-    oo.iterations = H.lst[3 * i];
+    oo.n_solve = H.r.nsub[i];
+    oo.n_inliers = H.r.lst[3 * i + 2] ? 0 : H.r.lst[3 * i + 1];
+    oo.iterations = H.r.lst[3 * i];
     memcpy(oo.X, Xi, 64);
     memcpy(oo.motion, C.vObjMod[i].data(), 64);
-    if (H.lst[3 * i + 2] == 0) memcpy(oo.centre_pre, H.centre + 3 * i, 12);
+    if (H.r.lst[3 * i + 2] == 0) memcpy(oo.centre_pre, H.r.centre + 3 * i, 12);
     out.objects.push_back(oo);
   }
 }
