@@ -748,46 +748,109 @@ __global__ void k_obj_model_choice(PnPObject* objs, int nobj, FlowSolveDesc* des
 // Stage B of one frame's objects in one launch (one workgroup per object; the objects are
 // independent): the motion-model matrix (k_obj_mm_prep), its inliers (pnp_mm_inliers_block), the
 // model choice that seeds D3 (k_obj_model_choice) and D3's edge list (pnp_subset_block) -- the
-// same code as the four separate kernels, without three dependent launches on the critical
+// same results as the four separate kernels, without three dependent launches on the critical
 // chain.
 __global__ __launch_bounds__(256) void k_obj_stage_b(MMPrepArgs a, FlowSolveDesc* descs,
                                                      float* init) {
-  const int i = blockIdx.x;
+  __shared__ float s_MM[16];
+  __shared__ int s_w[4];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
   PnPObject& o = a.objs[i];
-  if (threadIdx.x == 0 && a.pre[i] >= 0) {
+  // Everything this launch reads but does not write is loaded up front, so the dependent global
+  // round trips on the critical D3 chain are the motion-model matrix and the inlier lists only.
+  const int use_mm = o.use_mm;
+  const int n = use_mm ? *o.n : 0;
+  const float* pts3 = o.pts3;
+  const float2* pts2 = o.pts2;
+  const int* members = o.members;
+  const int* rs_inliers = o.inliers;
+  int* mm_inliers = o.mm_inliers;
+  const float fx = o.fx, fy = o.fy, cx = o.cx, cy = o.cy;
+  const double reproj = o.reproj;
+  const int* res = o.result;
+  const int res3 = res[3];
+  const int n_ransac = res[0] >= 0 ? res3 : 0;
+  if (tid == 0 && a.pre[i] >= 0) {  // MM = Tcw * vObjMod[PreObjID] (k_obj_mm_prep)
     const int p = a.pre[i];
     float X[16], Ti[16], vobj[16], MM[16];
-    if (a.prevStats[3 * p + 2] != 0)
-      mat4_eye(X);
-    else
-      for (int k = 0; k < 16; k++) X[k] = a.prevX[16 * p + k];
+    const int fail = a.prevStats[3 * p + 2];
+    for (int k = 0; k < 16; k++) X[k] = a.prevX[16 * p + k];
+    if (fail != 0) mat4_eye(X);
     inv_mat(a.TcwPrev, Ti);
     mat4_mul(Ti, X, vobj);
     mat4_mul(a.TcwCur, vobj, MM);
-    for (int k = 0; k < 16; k++) o.MM[k] = MM[k];
-  }
-  __syncthreads();
-  pnp_mm_inliers_block(o);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int n_ransac = o.result[0] >= 0 ? o.result[3] : 0;
-    const int n_mm = o.use_mm ? o.result[4] : -1;
-    float Mod[16];
-    mat4_eye(Mod);
-    for (int r = 0; r < 3; r++) {
-      for (int c = 0; c < 3; c++) Mod[4 * r + c] = (float)o.Rt[3 * r + c];
-      Mod[4 * r + 3] = (float)o.Rt[9 + r];
-    }
-    const bool choice = o.use_mm && !(n_ransac > n_mm);
-    o.use_mm_choice = choice ? 1 : 0;
     for (int k = 0; k < 16; k++) {
-      const float v = choice ? o.MM[k] : Mod[k];
-      descs[i].init[k] = v;
-      init[16 * i + k] = v;
+      o.MM[k] = MM[k];
+      s_MM[k] = MM[k];
     }
   }
   __syncthreads();
-  pnp_subset_block(o);
+  // motion-model inliers, ascending (pnp_mm_inliers_block with the matrix from LDS)
+  int n_mm = -1;
+  if (use_mm) {
+    float MM[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) MM[k] = s_MM[k];
+    int base = 0;
+    for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+      const int j = i0 + tid;
+      bool in = false;
+      if (j < n) {
+        float xc[3];
+        for (int r = 0; r < 3; r++) {
+          double sum = 0;
+          for (int k = 0; k < 3; k++) sum += (double)MM[4 * r + k] * (double)pts3[3 * j + k];
+          xc[r] = (float)sum + MM[4 * r + 3];
+        }
+        const float invzc = (float)(1.0 / (double)xc[2]);
+        const float u = fx * xc[0] * invzc + cx, v = fy * xc[1] * invzc + cy;
+        const float2 q = pts2[j];
+        const float u_ = q.x - u, v_ = q.y - v;
+        const float Rpe = sqrtf(u_ * u_ + v_ * v_);
+        in = (double)Rpe < reproj;
+      }
+      const unsigned long long bal = __ballot(in);
+      if (lane == 0) s_w[wave] = __popcll(bal);
+      __syncthreads();
+      int off = 0, tot = 0;
+      for (int w = 0; w < 4; w++) {
+        if (w < wave) off += s_w[w];
+        tot += s_w[w];
+      }
+      if (in) mm_inliers[base + off + __popcll(bal & ((1ull << lane) - 1ull))] = j;
+      base += tot;
+      __syncthreads();
+    }
+    n_mm = base;
+  }
+  // model choice (k_obj_model_choice), the same in every thread
+  const bool choice = use_mm && !(n_ransac > n_mm);
+  if (tid == 0) {
+    if (use_mm) o.result[4] = n_mm;
+    o.use_mm_choice = choice ? 1 : 0;
+    float Mod[16];
+    if (choice) {
+      for (int k = 0; k < 16; k++) Mod[k] = s_MM[k];
+    } else {
+      mat4_eye(Mod);
+      for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Mod[4 * r + c] = (float)o.Rt[3 * r + c];
+        Mod[4 * r + 3] = (float)o.Rt[9 + r];
+      }
+    }
+    for (int k = 0; k < 16; k++) {
+      descs[i].init[k] = Mod[k];
+      init[16 * i + k] = Mod[k];
+    }
+  }
+  // D3 edge list (pnp_subset_block): the chosen model's inliers as sample indices; the motion-model
+  // list was completed before the inlier loop's last barrier
+  const int n_sub = choice ? n_mm : res3;
+  const int* src = choice ? mm_inliers : rs_inliers;
+  int* sub = o.subset;
+  for (int j = tid; j < n_sub; j += blockDim.x) sub[j] = members[src[j]];
+  if (tid == 0) *o.n_subset = n_sub;
 }
 
 void launch_obj_stage_b(const MMPrepArgs& a, FlowSolveDesc* descs, float* init, hipStream_t st) {
