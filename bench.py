@@ -8,26 +8,38 @@ default; --seqs-per-gpu K tracks K independent sequences per GPU (one context, s
 host thread each; SURVEY 8(e) allows several sequences per device), seeds 1003 + rank * K + k.
 
 A "step" = System::TrackRGBD over one chunk of `--chunk` consecutive frames of the sequence:
-batched ORB extraction for the chunk, then per frame the association (B1-B9), the ego flow solve
-(PoseOptimizationFlow2Cam), object grouping, per-object PnP-RANSAC + PoseOptimizationFlow2 --
-everything the reference does per frame on this path (mmt_track_rgbd_chunk_device).  Frames are
-processed in order, so the tracker state carries across steps exactly as in rgbd_mmt.
+batched ORB extraction for the chunk, then per frame everything the reference does on this path
+(mmt_track_rgbd_chunk_device).  Frames are processed in order, so the tracker state carries
+across steps exactly as in rgbd_mmt.
 
-Multi-GPU: one process per GPU (torchrun), independent sequences, no data-path collective;
-barrier + device sync bracket the timed region; time = MAX over ranks; value = frames of all
-ranks / that time ("scaling": "weak").
+Multi-GPU: one process per GPU, independent sequences, no data-path collective; barrier + device
+sync bracket the timed region; time = MAX over ranks; value = frames of all ranks / that time
+("scaling": "weak").  `--gpus N` without a torchrun environment launches the N ranks itself
+(torch.distributed.run as a child process; this parent never touches the GPU); n_gpus is the
+world size the process group was initialised with.
 
 roofline: the batched ORB window -- k_gray_depth (A1 + A2) and the ORB launch sequence (A3-A9) --
 with SURVEY 8(d)'s B_orb = 3WH + 4P + 60N plus A2's 6WH algorithmic bytes per frame x frames per
 launch, over its average duration from HIP events the library records on the launch stream around
 every window (mmt_profile_*), vs the 8 TB/s HBM peak.
-cpu_baseline: the CPU oracle tracker (oracle/track_ref.cpp, a scalar C++ restatement of the
-reference's per-frame path) on rank 0 over the first frames of the same sequence, 1 core.
+
+cpu_baseline (rank 0, N = 1 only): the CPU oracle tracker (oracle/track_ref.cpp, a scalar C++
+restatement of the reference's per-frame path) on one pinned core.  It tracks the same sequence
+from frame 0 (the chain has to be replayed), is timed on the frame range the GPU timed region
+starts with, and every frame it tracks is compared with the GPU's result for that frame (the
+"parity" record).  --cpu-seqs K adds K independent sequences on K pinned cores (BASELINE C4/C5
+style), and the C2 (ego-only) workload is timed beside C3 on both sides.
+
+--dry: CPU-only rehearsal of the rank logic (gloo, no libmmt, a fixed sleep per step); used by
+tests/test_dist.py.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -67,7 +79,7 @@ def load_traffic(path, cfg_key):
         return None
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -80,40 +92,215 @@ def main():
     ap.add_argument("--objects", type=int, default=3)
     ap.add_argument("--seqs-per-gpu", type=int, default=1,
                     help="independent sequences tracked concurrently on each GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="CPU time of the timed oracle leg (after the run-up to the GPU's "
+                         "first timed frame)")
+    ap.add_argument("--cpu-seqs", type=int, default=4,
+                    help="independent sequences on as many pinned cores (0: skip)")
+    ap.add_argument("--cpu-seqs-seconds", type=float, default=8.0)
+    ap.add_argument("--c2-steps", type=int, default=3,
+                    help="timed steps of the C2 (ego-only) leg (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dry", action="store_true", help="CPU rehearsal of the rank logic")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(args):
+    """--gpus N outside a torchrun environment: start N ranks (one per GPU) with
+    torch.distributed.run as a child process and return its exit code.  Nothing here touches the
+    GPU, so the ranks own their devices from the start."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------ per-frame result plumbing
+def frames_from_raw(raw, C):
+    """(MmtFrameResult[C], MmtMotion[C * MAX_OBJECTS]) -> the per-frame dicts of Context.track."""
+    import multimot_track_amd as M
+    res, objs = raw
+    mo = M.MAX_OBJECTS
+    return [M._frame_dict(res[i], objs[i * mo:(i + 1) * mo]) for i in range(C)]
+
+
+def seq_frame_numpy(seq, i):
+    """Host copy of frame i of a device-resident sequence (oracle input layout)."""
+    from multimot_track_amd import scene
+    return scene.to_numpy_frames({k: seq[k][i:i + 1] for k in ("bgr", "disp", "flow", "mask")})[0]
+
+
+# ------------------------------------------------------------------ CPU legs (rank 0, N = 1)
+def cpu_leg(args, seq, gpu_frames, timed_from, W, H, NF):
+    """The oracle on one pinned core: untimed run-up over frames [0, timed_from), then timed
+    frames from `timed_from` for --cpu-seconds; every tracked frame is compared with the GPU."""
+    from oracle import compare, oracle as O
+    O.build()
+    K = (721.5377, 721.5377, 609.5593, 172.8540)
+    tr = O.Tracker(W, H, K, 387.5744, 0, NF)
+    affinity = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    if affinity:
+        os.sched_setaffinity(0, {min(affinity)})
+    ofr = []
+    n_timed, t_timed = 0, 0.0
+    t_run = time.perf_counter()
+    try:
+        i = 0
+        nmax = len(gpu_frames)
+        while i < nmax:
+            f = seq_frame_numpy(seq, i)
+            t0 = time.perf_counter()
+            ofr.append(tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]))
+            dt = time.perf_counter() - t0
+            if i >= timed_from:
+                n_timed += 1
+                t_timed += dt
+                if t_timed >= args.cpu_seconds:
+                    break
+            if i % 100 == 0:
+                print("cpu leg: frame %d (%.0f s)" % (i, time.perf_counter() - t_run),
+                      file=sys.stderr, flush=True)
+            i += 1
+    finally:
+        if affinity:
+            os.sched_setaffinity(0, affinity)
+    par = compare.parity_record(gpu_frames[:len(ofr)], ofr)
+    return n_timed, t_timed, par
+
+
+def cpu_multi_leg(args, render, W, H, NF, fps1):
+    """--cpu-seqs K independent sequences, one oracle process pinned to each of K cores, started
+    together (BASELINE.md C4/C5 "k sequences on k cores")."""
+    K = args.cpu_seqs
+    affinity = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    cores = affinity[:K] if len(affinity) >= K else [-1] * K
+    need = int(max(fps1, 1.0) * args.cpu_seqs_seconds * 1.5) + 8
+    tmp = tempfile.mkdtemp(prefix="mmt_cpuseq_")
+    procs = []
+    try:
+        for k in range(K):
+            seq = render(2003 + k, need)
+            d = os.path.join(tmp, "s%d" % k)
+            os.makedirs(d)
+            np.save(os.path.join(d, "bgr.npy"), seq["bgr"].cpu().numpy())
+            np.save(os.path.join(d, "disp.npy"), seq["disp"].cpu().numpy().view(np.uint16))
+            np.save(os.path.join(d, "flow.npy"), seq["flow"].cpu().numpy())
+            np.save(os.path.join(d, "mask.npy"), seq["mask"].cpu().numpy())
+            del seq
+        t0 = time.perf_counter()
+        for k in range(K):
+            procs.append(subprocess.Popen(
+                [sys.executable, "-m", "oracle.cpu_worker", os.path.join(tmp, "s%d" % k),
+                 str(cores[k]), str(args.cpu_seqs_seconds), str(W), str(H), str(NF)],
+                cwd=ROOT, stdout=subprocess.PIPE, text=True))
+        outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
+        wall = time.perf_counter() - t0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        import shutil
+        shutil.rmtree(tmp, ignore_errors=True)
+    rate = sum(o["frames"] / o["seconds"] for o in outs if o["seconds"] > 0)
+    return {"sequences": K, "cores": K, "value": round(rate, 3), "unit": "frames/s",
+            "frames": [o["frames"] for o in outs], "wall_s": round(wall, 2),
+            "pinned_cores": cores,
+            "sample": "%d independent C3 sequences (seeds 2003..%d), one oracle process pinned to "
+                      "each core, started together, %.0f s of CPU time each; value = sum of the "
+                      "per-core rates" % (K, 2002 + K, args.cpu_seqs_seconds)}
+
+
+# ------------------------------------------------------------------ dry rehearsal
+def run_dry(args, rank, world):
+    """The rank logic of the real run on CPU (gloo): per-rank seed, barrier-bracketed timed
+    region, MAX-over-ranks time, SUM of frames, world-size-based n_gpus."""
+    import torch
+    import torch.distributed as dist
+    from multimot_track_amd import shard
+    dev = torch.device("cpu")
+    C, K = args.chunk, args.seqs_per_gpu
+    seeds = [shard.sequence_seed(1003, rank * K + k) for k in range(K)]
+    step_s = 0.01 * (rank + 1)  # rank r's stand-in step cost
+    for _ in range(args.warmup):
+        time.sleep(step_s)
+    shard.barrier(world, dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(step_s)
+    shard.barrier(world, dev)
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, world, dev)
+    frames_all = shard.sum_over_ranks(args.steps * C * K, world, dev)
+    all_seeds = [None] * world
+    if world > 1:
+        dist.all_gather_object(all_seeds, seeds)
+    else:
+        all_seeds = [seeds]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(frames_all / elapsed, 2),
+                          "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                          "dtype": "u8", "data": "dry run (no GPU work)",
+                          "config": {"workload": "dry", "chunk_frames": C, "sequences_per_gpu": K,
+                                     "parallelism": "dp%d" % world, "seeds": all_seeds,
+                                     "frames_all": frames_all}}), flush=True)
+
+
+# ------------------------------------------------------------------ main
+def main(argv=None):
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args)
 
     import torch
     import torch.distributed as dist
-    import multimot_track_amd as M
-    from multimot_track_amd import scene, shard
+    from multimot_track_amd import shard
 
     rank, world, local = shard.rank_env()
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo" if args.dry else "nccl", init_method="env://")
+        world = dist.get_world_size()
+    if args.dry:
+        run_dry(args, rank, world)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
+
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     W, H, NF, C, K = args.width, args.height, args.nfeatures, args.chunk, args.seqs_per_gpu
     nframes = (args.warmup + args.steps) * C
     t_gen = time.perf_counter()
-    def render(seed):
+
+    def render(seed, n, objects=args.objects):
         # in pieces of 400 frames (each frame is rendered on its own, so the sequence is the
         # same), with a progress line on stderr for long runs under a profiler
         parts = []
-        for s0 in range(0, nframes, 400):
-            parts.append(scene.kitti_like_sequence(min(400, nframes - s0), W, H,
-                                                   n_objects=args.objects, seed=seed,
-                                                   device=dev, start=s0))
-            print("rank %d: rendered %d / %d frames" % (rank, s0 + len(parts[-1]["Tcw"]),
-                                                         nframes), file=sys.stderr, flush=True)
+        for s0 in range(0, n, 400):
+            parts.append(scene.kitti_like_sequence(min(400, n - s0), W, H, n_objects=objects,
+                                                   seed=seed, device=dev, start=s0))
+            print("rank %d: rendered %d / %d frames" % (rank, s0 + len(parts[-1]["Tcw"]), n),
+                  file=sys.stderr, flush=True)
         out = {k: torch.cat([p[k] for p in parts]) for k in ("bgr", "disp", "flow", "mask")}
         out["Tcw"] = np.concatenate([p["Tcw"] for p in parts])
         return out
 
-    seqs = [render(shard.sequence_seed(1003, rank * K + k)) for k in range(K)]
+    seqs = [render(shard.sequence_seed(1003, rank * K + k), nframes) for k in range(K)]
     seq = seqs[0]
     torch.cuda.synchronize(dev)
     t_gen = time.perf_counter() - t_gen
@@ -127,11 +314,12 @@ def main():
     streams = [torch.cuda.Stream(dev) for _ in range(K)]
     torch.cuda.set_stream(streams[0])
 
-    def step_k(k, i):
+    def step_k(k, i, s=None, c=None):
         sl = slice(i * C, (i + 1) * C)
-        s = seqs[k]
-        return ctxs[k].track_chunk_device(s["bgr"][sl], s["disp"][sl], s["flow"][sl],
-                                          s["mask"][sl], streams[k].cuda_stream, parse=False)
+        s = s if s is not None else seqs[k]
+        c = c if c is not None else ctxs[k]
+        return c.track_chunk_device(s["bgr"][sl], s["disp"][sl], s["flow"][sl], s["mask"][sl],
+                                    streams[k].cuda_stream, parse=False)
 
     pool = None
     if K > 1:  # one host thread per sequence (the C-ABI calls release the GIL)
@@ -143,8 +331,7 @@ def main():
             return step_k(0, i)
         return [f.result() for f in [pool.submit(step_k, k, i) for k in range(K)]][0]
 
-    for i in range(args.warmup):
-        step(i)
+    warm = [step(i) for i in range(args.warmup)]
     torch.cuda.synchronize(dev)
     ctx.profile_enable(True)
     ctx.profile_read(reset=True)
@@ -161,7 +348,7 @@ def main():
     # per-frame outputs of the timed region (sanity: every frame tracked, objects found)
     res, objs = results[-1]
     n_obj_last = int(res[C - 1].n_objects)
-    tracked = sum(int(r.initialized) for rr, _ in results for r in rr)
+    tracked = sum(int(res_[f].initialized) for res_, _ in results for f in range(C))
     gt = seq["Tcw"][-1]
     ego_err = float(np.abs(np.array(res[C - 1].Tcw[:]).reshape(4, 4) - gt).max())
 
@@ -172,34 +359,51 @@ def main():
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         key = "%dx%d_n%d_b%d" % (W, H, NF, C)
         traffic = load_traffic(args.traffic_file, key)
-        cpu = None
-        if not args.no_cpu:
-            from oracle import oracle as O
-            O.build()
-            kcam = (cfg.fx, cfg.fy, cfg.cx, cfg.cy)
-            tr = O.Tracker(W, H, kcam, cfg.bf, 0, NF)
-            n_done, tcpu = 0, 0.0
-            # one pinned core (the process's first allowed CPU), restored afterwards
-            affinity = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
-            if affinity:
-                os.sched_setaffinity(0, {min(affinity)})
-            try:
-                while tcpu < args.cpu_seconds and n_done < nframes:
-                    f = scene.to_numpy_frames({k: seq[k][n_done:n_done + 1]
-                                               for k in ("bgr", "disp", "flow", "mask")})[0]
-                    tc = time.perf_counter()
-                    tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
-                    tcpu += time.perf_counter() - tc
-                    n_done += 1
-            finally:
-                if affinity:
-                    os.sched_setaffinity(0, affinity)
-            cpu = {"value": round(n_done / tcpu, 3), "unit": "frames/s", "cores": 1,
+        cpu, parity, c2 = None, None, None
+        if world == 1 and args.c2_steps > 0:
+            # C2 (ego only): same camera and sequence seed, mask == 0
+            nc2 = (1 + args.c2_steps) * C
+            s2 = render(shard.sequence_seed(1003, 0), nc2, objects=0)
+            c2ctx = M.Context(cfg)
+            step_k(0, 0, s2, c2ctx)
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            for i in range(args.c2_steps):
+                step_k(0, 1 + i, s2, c2ctx)
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter() - t2
+            c2 = {"value": round(args.c2_steps * C / t2, 2), "unit": "frames/s",
+                  "frames": args.c2_steps * C, "timed_from": C}
+            c2ctx.close()
+        if world == 1 and not args.no_cpu:
+            gpu_frames = []
+            for raw in warm + results:
+                gpu_frames.extend(frames_from_raw(raw, C))
+            timed_from = args.warmup * C
+            n_t, t_t, parity = cpu_leg(args, seq, gpu_frames, timed_from, W, H, NF)
+            fps1 = n_t / t_t if t_t > 0 else 0.0
+            cpu = {"value": round(fps1, 3), "unit": "frames/s", "cores": 1,
                    "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-                   "sample": "first %d frames of the same C3 sequence, full per-frame tracking "
-                             "(oracle/track_ref.cpp: ORB, association, ego + object solves), "
-                             "single thread pinned to one core, %.1f s of CPU time"
-                             % (n_done, tcpu)}
+                   "sample": "frames %d-%d of the same C3 sequence (the GPU timed region starts "
+                             "at frame %d), full per-frame tracking (oracle/track_ref.cpp), one "
+                             "thread pinned to one core, %.1f s of CPU time, after an untimed "
+                             "run-up over frames 0-%d" % (timed_from, timed_from + n_t - 1,
+                                                          timed_from, t_t, timed_from - 1)}
+            if c2 is not None:
+                from oracle import oracle as O
+                tr2 = O.Tracker(W, H, (721.5377, 721.5377, 609.5593, 172.8540), 387.5744, 0, NF)
+                n2, tt2 = 0, 0.0
+                while tt2 < 5.0 and n2 < nc2:
+                    f = seq_frame_numpy(s2, n2)
+                    ta = time.perf_counter()
+                    tr2.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+                    tt2 += time.perf_counter() - ta
+                    n2 += 1
+                cpu["c2_value"] = round(n2 / tt2, 3)
+                cpu["c2_sample"] = "frames 0-%d of the C2 sequence, one core, %.1f s" % (n2 - 1,
+                                                                                         tt2)
+            if args.cpu_seqs > 0:
+                cpu["multi"] = cpu_multi_leg(args, lambda sd, n: render(sd, n), W, H, NF, fps1)
         out = {
             "metric": METRIC,
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
@@ -214,7 +418,7 @@ def main():
                        "sequences_per_gpu": K, "parallelism": "dp%d" % world,
                        "frames_tracked": tracked, "objects_last_frame": n_obj_last,
                        "ego_abs_err_last_frame": round(ego_err, 5),
-                       "scene_render_s": round(t_gen, 2)},
+                       "scene_render_s": round(t_gen, 2), "c2": c2},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
@@ -223,6 +427,7 @@ def main():
                          "launch_ms": round(launch_ms, 4), "bytes_per_launch": bytes_per_launch,
                          "orb_share_of_step": round(prof["orb_ms"] / (elapsed * 1e3), 4)},
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(out), flush=True)
     for c in ctxs:
@@ -231,7 +436,8 @@ def main():
         pool.shutdown()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

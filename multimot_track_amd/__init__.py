@@ -100,7 +100,7 @@ class MmtProfile(ctypes.Structure):
                 ("orb_frames", ctypes.c_int64)]
 
 
-MAX_OBJECTS = 8  # objects reported per frame (kMaxObj in csrc/mmt_tracker.h)
+MAX_OBJECTS = 15  # objects reported per frame (kMaxObj in csrc/mmt_tracker.h: labels 1..15)
 
 
 def _mat(a):

@@ -503,6 +503,57 @@ struct LMSmem {
 
 }  // namespace
 
+// One last-frame sample of ObjCentre3D_pre (Tracking.cc:2032-2049): the world point of
+// Frame::UnprojectStereoObject(j, 1) (Frame.cc:1118-1152) with the depth noise of the frame's
+// first gaussian draw, as cv::Mat float products (double accumulation rounded to float).
+__device__ __forceinline__ void centre_point(const FlowSolveDesc& D, int i, float p[3]) {
+  const float ifx = 1.0f / D.fx, ify = 1.0f / D.fy;
+  float twl[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {  // -Rlw^T tlw (cv::Mat float product)
+    double s = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) s += (double)D.Tcw_last[4 * k + r] * (double)D.Tcw_last[4 * k + 3];
+    twl[r] = -(float)s;
+  }
+  const int s = D.idx ? D.idx[i] : i;
+  float z = D.depth[s];
+  const float noise = (float)((double)D.g0 * ((double)(z * z) / (725 * 0.5) * 0.15));
+  z = z + noise;
+  const float2 ob = D.obs[s];
+  const float x = (ob.x - D.cx) * z * ifx, y = (ob.y - D.cy) * z * ify;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const double s3 = (double)D.Tcw_last[r] * x + (double)D.Tcw_last[4 + r] * y +
+                      (double)D.Tcw_last[8 + r] * z;
+    p[r] = (float)s3 + twl[r];
+  }
+}
+
+// ObjCentre3D_pre = (sum of the points, added in float in sample order, as the reference's
+// cv::Mat accumulation) / n, the division as cv::Mat / size_t: * (1.0 / n) in double.  No points
+// give 0 * (1 / 0) = NaN.  One wave: the lanes compute 64 points at a time, the sum walks them in
+// order (three independent float chains).  Called by the lanes of wave 0 only.
+__device__ __forceinline__ void centre_sum_wave(const FlowSolveDesc& D, int N) {
+  const int lane = threadIdx.x & 63;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int b = 0; b < N; b += 64) {
+    float p[3] = {0.f, 0.f, 0.f};
+    if (b + lane < N) centre_point(D, b + lane, p);
+    const int m = min(64, N - b);
+    for (int k = 0; k < m; k++) {
+      a0 += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[0]), k));
+      a1 += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[1]), k));
+      a2 += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[2]), k));
+    }
+  }
+  if (lane == 0) {
+    D.centre_out[0] = (float)((double)a0 * (1.0 / N));
+    D.centre_out[1] = (float)((double)a1 * (1.0 / N));
+    D.centre_out[2] = (float)((double)a2 * (1.0 / N));
+  }
+}
+
 template <int IR>
 __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int nt, LMSmem& sm) {
   const int tid = threadIdx.x, nw = nt >> 6;
@@ -863,43 +914,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   }
   block_sum<1>(v, sm.red, sm.S27, nw);
   const int n_out = N - (int)sm.S27[0];
-  if (D.centre_out) {
-    // ObjCentre3D_pre: float world points of the last frame (noisy depth, as the reference's
-    // UnprojectStereoObject(j, 1)), summed in double (the reference adds floats in order; the
-    // two agree to the reference's own rounding) and scaled by 1 / n as cv::Mat / int does
-    double cv3[3] = {0, 0, 0};
-    const float ifx = 1.0f / D.fx, ify = 1.0f / D.fy;
-    float Rlw[9], tlw[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-#pragma unroll
-      for (int cc = 0; cc < 3; cc++) Rlw[3 * r + cc] = D.Tcw_last[4 * r + cc];
-      tlw[r] = D.Tcw_last[4 * r + 3];
-    }
-    float twl[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) {  // -Rlw^T tlw (cv::Mat float product)
-      double s = 0;
-#pragma unroll
-      for (int k = 0; k < 3; k++) s += (double)Rlw[3 * k + r] * (double)tlw[k];
-      twl[r] = -(float)s;
-    }
-    for (int i = tid; i < N; i += nt) {
-      const int s = D.idx ? D.idx[i] : i;
-      float z = D.depth[s];
-      const float noise = (float)((double)D.g0 * ((double)(z * z) / (725 * 0.5) * 0.15));
-      z = z + noise;
-      const float2 ob = D.obs[s];
-      const float x = (ob.x - D.cx) * z * ifx, y = (ob.y - D.cy) * z * ify;
-#pragma unroll
-      for (int r = 0; r < 3; r++) {
-        const double s3 = (double)Rlw[r] * x + (double)Rlw[3 + r] * y + (double)Rlw[6 + r] * z;
-        cv3[r] += (double)((float)s3 + twl[r]);
-      }
-    }
-    block_sum<3>(cv3, sm.red, sm.S27, nw);
-    if (tid < 3) D.centre_out[tid] = (float)((double)(float)sm.S27[tid] * (1.0 / N));
-  }
+  if (D.centre_out && tid < 64) centre_sum_wave(D, N);  // ObjCentre3D_pre, wave 0
   if (tid == 0) {
     dse3_to_float(P, D.pose_out);
     D.stats[0] = iters;
@@ -927,6 +942,9 @@ __global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict
       D.stats[1] = 0;
       D.stats[2] = 1;
     }
+    // the reference computes ObjCentre3D_pre before the solve whatever the count: 1-2 points
+    // give their mean, none gives 0 * (1 / 0) = NaN (Tracking.cc:2032-2049)
+    if (D.centre_out && threadIdx.x < 64) centre_sum_wave(D, N);
     return;
   }
   // Threads per solve: one edge per thread up to the block size (the passes are issue-bound:

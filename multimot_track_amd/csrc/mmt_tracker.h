@@ -12,7 +12,9 @@
 
 namespace mmt {
 
-constexpr int kMaxObj = 8;         // objects solved per frame
+// objects solved per frame: one per semantic label 1..15 (label 0 is the static background), so
+// every object the grouping keeps is solved (the reference has no cap)
+constexpr int kMaxObj = kMaxLabel - 1;
 constexpr int kRansacIters = 500;  // solvePnPRansac iterationsCount (Tracking.cc:4361)
 
 struct ObjOut {

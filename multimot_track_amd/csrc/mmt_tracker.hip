@@ -206,7 +206,8 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   }
   d_err_ = alloc<int>(1);
   MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
-  // solves: 1 ego + up to kMaxObj objects
+  // solves: 1 ego + up to kMaxObj objects.  An object solve has at most ocap_ edges (its
+  // samples), the ego solve at most kcap_, so no solve is ever truncated to the scratch capacity
   const int lmcap = std::max(kcap_, ocap_);
   lm_cap_ = lmcap;
   // scratch: the ego solve (caller stream) and the object solves (ob_, one D3 launch at a time)
@@ -526,7 +527,8 @@ void Tracker::obj_stage_a(ObjFrame& F) {
     mx = *std::max_element(Ls.nModLabel.begin(), Ls.nModLabel.end()) + 1;
   else
     mx = 1;  // uninitialised in the reference (Tracking.cc:1557): pinned 1
-  const int nobj = std::min((int)objLabelsNew.size(), kMaxObj);
+  const int nobj = (int)objLabelsNew.size();
+  if (nobj > kMaxObj) throw ArgError("more dynamic objects than semantic labels 1..15");
   std::vector<int> LabId(nobj);
   for (int i = 0; i < nobj; i++) {
     const int l = objLabelsNew[i];
@@ -701,7 +703,7 @@ void Tracker::obj_finish(ObjFrame& F) {
     oo.iterations = H.r.lst[3 * i];
     memcpy(oo.X, Xi, 64);
     memcpy(oo.motion, C.vObjMod[i].data(), 64);
-    if (H.r.lst[3 * i + 2] == 0) memcpy(oo.centre_pre, H.r.centre + 3 * i, 12);
+    memcpy(oo.centre_pre, H.r.centre + 3 * i, 12);  // computed whatever the solve's size
     out.objects.push_back(oo);
   }
 }

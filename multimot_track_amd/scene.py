@@ -42,14 +42,14 @@ def _se3(R, t):
 class StreetScene:
     """Trajectories of the camera and the objects (closed form in the frame index)."""
 
-    def __init__(self, n_objects=3, seed=1003, speed=1.0):
+    def __init__(self, n_objects=3, seed=1003, speed=1.0, lanes=None):
         rng = np.random.default_rng(seed)
         self.seed = int(seed)
         self.speed = speed
         self.sway = (0.25 + 0.1 * rng.random(), 0.04 + 0.02 * rng.random())
         self.yaw = (0.02 + 0.01 * rng.random(), 0.03 + 0.01 * rng.random())
-        lanes = [(-3.0, 12.0), (3.2, 16.0), (-0.3, 21.0), (3.4, 9.0), (-3.4, 19.0),
-                 (0.0, 11.0), (-5.0, 14.0), (5.2, 20.0)]
+        lanes = lanes or [(-3.0, 12.0), (3.2, 16.0), (-0.3, 21.0), (3.4, 9.0), (-3.4, 19.0),
+                          (0.0, 11.0), (-5.0, 14.0), (5.2, 20.0)]
         self.objs = []
         for k in range(n_objects):
             x0, d0 = lanes[k % len(lanes)]
@@ -238,10 +238,11 @@ class SequenceRenderer:
 
 
 def kitti_like_sequence(nframes, width=1242, height=375, n_objects=3, seed=1003, device="cpu",
-                        start=0):
-    """C2 (n_objects=0) / C3 (n_objects=3) / C5 (1920x1080, n_objects=8) sequences."""
-    return SequenceRenderer(StreetScene(n_objects, seed), width, height, device=device).sequence(
-        nframes, start)
+                        start=0, lanes=None):
+    """C2 (n_objects=0) / C3 (n_objects=3) / C5 (1920x1080, n_objects=8) sequences; `lanes`
+    (x, distance ahead) per object overrides the default street layout."""
+    return SequenceRenderer(StreetScene(n_objects, seed, lanes=lanes), width, height,
+                            device=device).sequence(nframes, start)
 
 
 def to_numpy_frames(seq):

@@ -1,0 +1,66 @@
+"""Frame-by-frame parity of GPU tracking results against the CPU oracle -- TEST INFRASTRUCTURE.
+
+Both sides are the per-frame dicts of multimot_track_amd.Context.track / track_chunk_device and
+oracle.Tracker.track (same keys).  The bar (BASELINE.json north_star): SE(3) poses within 1e-4
+(max abs over the 4x4 entries), every integer output exact; the object centroid of the speed
+evaluation (ObjCentre3D_pre, metres) within 1e-3.  Used by tests/ and by bench.py's CPU leg
+(the parity record of the bench's own frames)."""
+import numpy as np
+
+POSE_TOL = 1e-4
+CENTRE_TOL = 1e-3
+FRAME_INT = ("initialized", "n_keys", "n_obj_samples", "ego_iterations", "ego_inliers")
+OBJ_INT = ("label", "sem_label", "n_points", "ransac_inliers", "mm_inliers", "n_solve",
+           "n_inliers", "iterations")
+OBJ_POSE = ("init", "X", "motion")
+MAP_INT = ("map_state", "map_matches_mm", "map_inliers_local", "n_keyframes", "n_mappoints")
+
+
+def compare_frame(g, o):
+    """(max pose diff, max centre diff, [integer mismatch descriptions]) of one frame."""
+    bad = []
+    for k in FRAME_INT + MAP_INT:
+        if k in g and k in o and int(g[k]) != int(o[k]):
+            bad.append("%s %r != %r" % (k, g[k], o[k]))
+    pose = float(np.abs(np.asarray(g["Tcw"]) - np.asarray(o["Tcw"])).max())
+    if "Tcw_map" in g and "Tcw_map" in o:
+        pose = max(pose, float(np.abs(np.asarray(g["Tcw_map"]) - np.asarray(o["Tcw_map"])).max()))
+    centre = 0.0
+    if len(g["objects"]) != len(o["objects"]):
+        bad.append("objects %d != %d" % (len(g["objects"]), len(o["objects"])))
+    for j, (a, b) in enumerate(zip(g["objects"], o["objects"])):
+        for k in OBJ_INT:
+            if int(a[k]) != int(b[k]):
+                bad.append("object %d %s %r != %r" % (j, k, a[k], b[k]))
+        for k in OBJ_POSE:
+            pose = max(pose, float(np.abs(np.asarray(a[k]) - np.asarray(b[k])).max()))
+        ca, cb = np.asarray(a["centre_pre"], np.float64), np.asarray(b["centre_pre"], np.float64)
+        if not np.array_equal(np.isnan(ca), np.isnan(cb)):  # NaN: a solve without points
+            bad.append("object %d centre_pre %s != %s" % (j, ca, cb))
+        elif not np.isnan(ca).all():
+            centre = max(centre, float(np.nanmax(np.abs(ca - cb))))
+    return pose, centre, bad
+
+
+def parity_record(gpu_frames, oracle_frames, first_frame=0):
+    """Summary over aligned frame lists: frames compared, max pose / centre diff, number of
+    frames with an integer mismatch, the first frame that breaks the bar and why."""
+    n = min(len(gpu_frames), len(oracle_frames))
+    max_pose = max_centre = 0.0
+    nbad = 0
+    first = None
+    why = None
+    for i in range(n):
+        p, c, bad = compare_frame(gpu_frames[i], oracle_frames[i])
+        max_pose = max(max_pose, p)
+        max_centre = max(max_centre, c)
+        if bad:
+            nbad += 1
+        if first is None and (bad or p >= POSE_TOL or c >= CENTRE_TOL):
+            first = first_frame + i
+            why = "; ".join(bad[:4]) if bad else ("pose diff %.3g" % p if p >= POSE_TOL
+                                                  else "centre diff %.3g" % c)
+    return {"frames": n, "first_frame": first_frame, "max_pose_diff": max_pose,
+            "max_centre_diff": max_centre, "int_mismatch_frames": nbad,
+            "first_divergent_frame": first, "first_divergence": why,
+            "pose_tol": POSE_TOL, "centre_tol": CENTRE_TOL}

@@ -446,9 +446,10 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
     if (!solved) mat4_eye(X);
     // ObjCentre3D_pre (Tracking.cc:2032-2049): float sum, in order, of the last frame's
     // UnprojectStereoObject(j, 1) (Frame.cc:1118-1152: z + (float)gaussian(z^2 / 362.5 * 0.15),
-    // the RNG's first draw g0), then cv::Mat / size: * (1.0 / n) in double, rounded to float
+    // the RNG's first draw g0), then cv::Mat / size: * (1.0 / n) in double, rounded to float.
+    // Computed before the solve whatever its size: no points give 0 * (1 / 0) = NaN.
     float centre[3] = {0, 0, 0};
-    if (solved) {
+    {
       for (int i = 0; i < NS; i++) {
         float z = dep[i];
         const float noise = (float)((double)g0 * ((double)(z * z) / (725 * 0.5) * 0.15));

@@ -50,3 +50,28 @@ def test_two_rank_sharding():
     assert res[0][3] != res[1][3]                       # independent sequences
     assert all(res[r][4] == pytest.approx(2.5) for r in range(2))   # max over ranks
     assert all(res[r][5] == pytest.approx(96.0) for r in range(2))  # all frames
+
+
+def test_bench_self_launches_ranks_dry():
+    """bench.py --gpus 2 outside torchrun starts its own two ranks (torch.distributed.run child,
+    gloo in --dry mode) and reports the world size the process group was initialised with, the
+    per-rank sequence seeds, MAX-over-ranks time and the frames of all ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry",
+                        "--steps", "3", "--warmup", "1", "--chunk", "8"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["seeds"] == [[1003], [1004]]
+    assert d["config"]["frames_all"] == 2 * 3 * 8
+    # the slower rank (2 x 10 ms per step) sets the time: 3 steps >= 60 ms
+    assert d["ms_per_step"] >= 20.0
+    assert d["value"] == pytest.approx(48 / (d["ms_per_step"] * 3 / 1000.0), rel=0.02)
