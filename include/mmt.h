@@ -62,6 +62,8 @@ typedef struct mmt_config {
   uint32_t noise_seed;            /* replaces cv::RNG(time(NULL)), Frame.cc:1246         */
   int device_id;                  /* HIP device ordinal                                  */
   int max_batch;                  /* frames in flight for batched ORB extraction         */
+  float fps;                      /* Camera.fps: mMaxFrames of the keyframe policy
+                                     (Tracking.cc:170-176; 0 -> 30 as the reference)     */
 } mmt_config;
 
 /* cv::KeyPoint, same field order and size (28 bytes). */
@@ -98,6 +100,15 @@ typedef struct mmt_frame_result {
   int32_t ego_iterations;   /* LM iterations of PoseOptimizationFlow2Cam               */
   int32_t ego_inliers;      /* its inliers (chi2 <= 0.04)                              */
   int32_t n_objects;        /* dynamic objects solved this frame                       */
+  /* ORB-SLAM2 map tracking (Tracking.cc:985-1176), which sets the flow solve's initial pose */
+  int32_t map_state;        /* mState after the frame: 0 not initialised, 1 OK, 2 LOST     */
+  int32_t map_matches_mm;   /* TrackWithMotionModel's SearchByProjection matches (-1: none) */
+  int32_t map_inliers_local;/* mnMatchesInliers of TrackLocalMap (-1: not run)             */
+  int32_t n_keyframes;      /* keyframes in the map                                      */
+  int32_t n_mappoints;      /* map points in the map                                     */
+  int32_t new_keyframe;     /* this frame became a keyframe                              */
+  float Tcw_map[16];        /* row-major pose of the map branch (PoseOptimization's output,
+                               the initial estimate of PoseOptimizationFlow2Cam)        */
 } mmt_frame_result;
 
 typedef struct mmt_ctx mmt_ctx;
@@ -186,7 +197,7 @@ int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* problem, float* po
  * order): Xw n x 3 world positions, obs n x (u, v, uR) with uR = mvuRight (< 0: mono edge),
  * inv_sigma2 n = mvInvLevelSigma2[octave].  Tcw = pFrame->mTcw (row-major).  Writes the optimised
  * pose and mvbOutlier (outlier_out, n bytes); *n_inliers = the function's return value
- * (nInitialCorrespondences - nBad; 0 with the pose unchanged below 3 edges).  n <= 2048. */
+ * (nInitialCorrespondences - nBad; 0 with the pose unchanged below 3 edges). */
 typedef struct mmt_pose_opt_problem {
   int n;
   const float* Xw;
@@ -279,6 +290,10 @@ typedef struct mmt_last_frame {
   const uint8_t* mp_desc;   /* n x 32 */
   const uint8_t* active;    /* n */
   float Tcw[16];            /* row-major LastFrame.mTcw */
+  const uint8_t* obs;       /* n, optional: mvpMapPoints[i]->Observations() > 0.  A current key
+                               bound to a point without observations (a temporal visual-odometry
+                               point of UpdateLastFrame) stays open to later points (NULL: every
+                               point has observations) */
 } mmt_last_frame;
 
 /* ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) with mbCheckOrientation

@@ -30,7 +30,8 @@ class MmtConfig(ctypes.Structure):
                 ("orb_nfeatures", ctypes.c_int), ("orb_scale_factor", ctypes.c_float),
                 ("orb_nlevels", ctypes.c_int), ("orb_ini_th_fast", ctypes.c_int),
                 ("orb_min_th_fast", ctypes.c_int), ("noise_seed", ctypes.c_uint32),
-                ("device_id", ctypes.c_int), ("max_batch", ctypes.c_int)]
+                ("device_id", ctypes.c_int), ("max_batch", ctypes.c_int),
+                ("fps", ctypes.c_float)]
 
 
 class MmtMotion(ctypes.Structure):
@@ -46,7 +47,10 @@ class MmtFrameResult(ctypes.Structure):
     _fields_ = [("Tcw", ctypes.c_float * 16), ("initialized", ctypes.c_int32),
                 ("n_keypoints", ctypes.c_int32), ("n_obj_samples", ctypes.c_int32),
                 ("ego_iterations", ctypes.c_int32), ("ego_inliers", ctypes.c_int32),
-                ("n_objects", ctypes.c_int32)]
+                ("n_objects", ctypes.c_int32), ("map_state", ctypes.c_int32),
+                ("map_matches_mm", ctypes.c_int32), ("map_inliers_local", ctypes.c_int32),
+                ("n_keyframes", ctypes.c_int32), ("n_mappoints", ctypes.c_int32),
+                ("new_keyframe", ctypes.c_int32), ("Tcw_map", ctypes.c_float * 16)]
 
 
 class MmtFlowProblem(ctypes.Structure):
@@ -73,7 +77,7 @@ class MmtMatchFrame(ctypes.Structure):
 class MmtLastFrame(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("kps", ctypes.c_void_p), ("Xw", ctypes.c_void_p),
                 ("mp_desc", ctypes.c_void_p), ("active", ctypes.c_void_p),
-                ("Tcw", ctypes.c_float * 16)]
+                ("Tcw", ctypes.c_float * 16), ("obs", ctypes.c_void_p)]
 
 
 class MmtLocalPoints(ctypes.Structure):
@@ -118,7 +122,10 @@ def _frame_dict(r, objs):
                         centre_pre=np.array(o.centre_pre[:], np.float32)))
     return dict(initialized=bool(r.initialized), Tcw=_mat(r.Tcw), n_keys=r.n_keypoints,
                 n_obj_samples=r.n_obj_samples, ego_iterations=r.ego_iterations,
-                ego_inliers=r.ego_inliers, objects=out)
+                ego_inliers=r.ego_inliers, objects=out, map_state=r.map_state,
+                map_matches_mm=r.map_matches_mm, map_inliers_local=r.map_inliers_local,
+                n_keyframes=r.n_keyframes, n_mappoints=r.n_mappoints,
+                new_keyframe=r.new_keyframe, Tcw_map=_mat(r.Tcw_map))
 
 
 class MmtError(RuntimeError):
@@ -191,7 +198,7 @@ def kitti03_config(width=1242, height=375, nfeatures=2000, max_batch=1, device_i
     c = MmtConfig()
     c.width, c.height = width, height
     c.fx, c.fy, c.cx, c.cy = 721.5377, 721.5377, 609.5593, 172.8540
-    c.bf, c.th_depth, c.rgb = 387.5744, 65.2, 1
+    c.bf, c.th_depth, c.rgb, c.fps = 387.5744, 65.2, 1, 10.0
     c.orb_nfeatures, c.orb_scale_factor, c.orb_nlevels = nfeatures, 1.2, 8
     c.orb_ini_th_fast, c.orb_min_th_fast = 20, 7
     c.noise_seed, c.device_id, c.max_batch = noise_seed, device_id, max_batch
@@ -380,9 +387,11 @@ class Context:
         return uR[:n], dep[:n], cs, ci[:cs[-1]]
 
     def search_by_projection_frame(self, kps, desc, depth, tcw, last_kps, Xw, mp_desc, active,
-                                   tlw, th, mono=False, check_orientation=True):
+                                   tlw, th, mono=False, check_orientation=True, obs=None):
         """ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) (C2):
-        (nmatches, match[cur key] = last-frame index or -1)."""
+        (nmatches, match[cur key] = last-frame index or -1).  obs (optional, per last-frame
+        point): the point has observations (False: a temporal VO point, whose binding a later
+        point may replace)."""
         keep = []
         fr = self._match_frame(kps, desc, depth, tcw, keep)
         lk = np.ascontiguousarray(last_kps)
@@ -394,6 +403,10 @@ class Context:
         L.kps, L.Xw, L.mp_desc, L.active = (lk.ctypes.data, X.ctypes.data, md.ctypes.data,
                                             act.ctypes.data)
         L.Tcw[:] = np.asarray(tlw, np.float32).reshape(16).tolist()
+        if obs is not None:
+            ob = np.ascontiguousarray(obs, np.uint8)
+            keep.append(ob)
+            L.obs = ob.ctypes.data
         match = np.zeros(max(fr.n, 1), np.int32)
         nm = ctypes.c_int(0)
         self._check(lib().mmt_search_by_projection_frame(

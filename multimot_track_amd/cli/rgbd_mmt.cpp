@@ -247,6 +247,7 @@ int main(int argc, char** argv) {
   cfg.noise_seed = seed;
   cfg.device_id = device;
   cfg.max_batch = 1;
+  cfg.fps = (float)get("Camera.fps", 0);
   // image size from the first frame when the settings omit it
   int w0 = 0, h0 = 0, ch0 = 0, db0 = 0;
   void* probe_img = nullptr;

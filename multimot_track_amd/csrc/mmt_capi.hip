@@ -318,6 +318,13 @@ static void fill_results(const std::vector<mmt::FrameOut>& outs, mmt_frame_resul
     r.ego_iterations = o.ego_iterations;
     r.ego_inliers = o.ego_inliers;
     r.n_objects = (int)o.objects.size();
+    r.map_state = o.map.state;
+    r.map_matches_mm = o.map.matches_mm;
+    r.map_inliers_local = o.map.inliers_local;
+    r.n_keyframes = o.map.n_keyframes;
+    r.n_mappoints = o.map.n_mappoints;
+    r.new_keyframe = o.map.new_keyframe;
+    memcpy(r.Tcw_map, o.map.Tcw_map, sizeof(r.Tcw_map));
     if (!objs) continue;
     for (int i = 0; i < (int)o.objects.size() && i < objs_cap; i++) {
       const mmt::ObjOut& s = o.objects[i];
@@ -456,7 +463,7 @@ int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* pr, float* pose_ou
 
 int mmt_pose_optimization(mmt_ctx* ctx, const mmt_pose_opt_problem* pr, float* pose_out,
                           uint8_t* outlier_out, int* n_inliers) {
-  if (!ctx || !pr || !pose_out || !n_inliers || pr->n < 0 || pr->n > mmt::kPoseOptMaxEdges ||
+  if (!ctx || !pr || !pose_out || !n_inliers || pr->n < 0 ||
       (pr->n > 0 && (!pr->Xw || !pr->obs || !pr->inv_sigma2 || !outlier_out)))
     return MMT_EINVAL;
   return guard(ctx, [&] {
@@ -465,7 +472,8 @@ int mmt_pose_optimization(mmt_ctx* ctx, const mmt_pose_opt_problem* pr, float* p
     const int n = pr->n, cap = std::max(n, 1);
     DevBuf<float> X(3 * (size_t)cap), ob(3 * (size_t)cap), s2(cap), pose(16);
     DevBuf<uint8_t> outl(cap);
-    DevBuf<int> ninl(1);
+    DevBuf<int> ninl(1), fsc(n > mmt::kPoseOptMaxEdges ? cap : 1);
+    DevBuf<double> esc(n > mmt::kPoseOptMaxEdges ? 3 * (size_t)cap : 1);
     DevBuf<mmt::PoseOptDesc> dd(1);
     if (n > 0) {
       MMT_HIP(hipMemcpyAsync(X.p, pr->Xw, 12 * (size_t)n, hipMemcpyHostToDevice, s));
@@ -483,6 +491,8 @@ int mmt_pose_optimization(mmt_ctx* ctx, const mmt_pose_opt_problem* pr, float* p
     d.pose_out = pose.p;
     d.outlier = outl.p;
     d.n_inliers = ninl.p;
+    d.e_scratch = esc.p;
+    d.f_scratch = fsc.p;
     MMT_HIP(hipMemcpyAsync(dd.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
     mmt::launch_pose_opt(dd.p, 1, s);
     MMT_HIP(hipMemcpyAsync(pose_out, pose.p, 64, hipMemcpyDeviceToHost, s));
@@ -534,7 +544,7 @@ int mmt_search_by_projection_frame(mmt_ctx* ctx, const mmt_match_frame* cur,
     const int n1 = last->n;
     DevBuf<mmt_kp> lk(n1);
     DevBuf<float> X(3 * (size_t)std::max(n1, 1));
-    DevBuf<uint8_t> md(32 * (size_t)std::max(n1, 1)), act(n1);
+    DevBuf<uint8_t> md(32 * (size_t)std::max(n1, 1)), act(n1), obs(n1);
     DevBuf<int> match(std::max(cur->n, 1)), nm(1);
     DevCands cands(n1);
     if (n1 > 0) {
@@ -542,12 +552,15 @@ int mmt_search_by_projection_frame(mmt_ctx* ctx, const mmt_match_frame* cur,
       MMT_HIP(hipMemcpyAsync(X.p, last->Xw, 12 * (size_t)n1, hipMemcpyHostToDevice, s));
       MMT_HIP(hipMemcpyAsync(md.p, last->mp_desc, 32 * (size_t)n1, hipMemcpyHostToDevice, s));
       MMT_HIP(hipMemcpyAsync(act.p, last->active, (size_t)n1, hipMemcpyHostToDevice, s));
+      if (last->obs)
+        MMT_HIP(hipMemcpyAsync(obs.p, last->obs, (size_t)n1, hipMemcpyHostToDevice, s));
     }
     mmt::LastFrameDev L;
     L.keys = lk.p;
     L.Xw = X.p;
     L.mp_desc = md.p;
     L.active = act.p;
+    L.obs = last->obs ? obs.p : nullptr;
     L.n = n1;
     memcpy(L.Tcw, last->Tcw, 64);
     mmt::launch_sbp_frame(F.G, cur->Tcw, L, th, mono, check_orientation, cands.set(), match.p,

@@ -1100,14 +1100,19 @@ __device__ __forceinline__ PoEdgeR po_load(const PoseOptDesc& D, const int* flag
 
 // Edges are re-read from global memory (L2-resident, a few KB) on every pass and their flags and
 // last errors live in LDS: no per-thread edge arrays, so the kernel stays clear of spills.
+// GLOBAL: more edges than the LDS arrays hold (kPoseOptMaxEdges): the per-edge errors and flags
+// live in the caller's scratch (D.e_scratch: 3 x N doubles, D.f_scratch: N ints) instead.
+template <bool GLOBAL>
 __device__ void pose_opt_body(const PoseOptDesc& D, int N, PoSmem& sm) {
   const int tid = threadIdx.x, nt = blockDim.x, nw = nt >> 6;
   // const float deltaMono = sqrt(5.991): double sqrt rounded to float, then setDelta(double)
   const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
-  int* flags = sm.flags;
+  int* flags = GLOBAL ? D.f_scratch : sm.flags;
+  double* const E = GLOBAL ? D.e_scratch : &sm.e[0][0];
+  const int ES = GLOBAL ? N : kPoseOptMaxEdges;  // row stride of the three error rows
   for (int i = tid; i < N; i += nt) {
     flags[i] = (D.obs[3 * i + 2] < 0 ? 0 : kPoStereo) | kPoRobust;
-    sm.e[0][i] = sm.e[1][i] = sm.e[2][i] = 0;
+    E[i] = E[ES + i] = E[2 * ES + i] = 0;
   }
   __syncthreads();
   const DSE3 P0 = dse3_from_float(D.Tcw);
@@ -1118,8 +1123,8 @@ __device__ void pose_opt_body(const PoseOptDesc& D, int N, PoSmem& sm) {
 #pragma unroll
     for (int q = 0; q < kPoSums; q++) v[q] = 0;
     for (int i = tid; i < N; i += nt) {
-      const PoEdgeR E = po_load(D, flags, i);
-      if (!(E.flags & kPoOutlier)) po_linearise(E, T, D, dM, dS, &sm.e[0][i], kPoseOptMaxEdges, v);
+      const PoEdgeR Ed = po_load(D, flags, i);
+      if (!(Ed.flags & kPoOutlier)) po_linearise(Ed, T, D, dM, dS, E + i, ES, v);
     }
     block_sum_t<kPoSums>(v, sm.tile, sm.red, out, nw);
   };
@@ -1202,22 +1207,22 @@ __device__ void pose_opt_body(const PoseOptDesc& D, int N, PoSmem& sm) {
     // error at the optimised pose, the others keep the last computed one
     double nb[1] = {0};
     for (int i = tid; i < N; i += nt) {
-      PoEdgeR E = po_load(D, flags, i);
+      PoEdgeR Ed = po_load(D, flags, i);
       double e[3];
-      if (E.flags & kPoOutlier) {
+      if (Ed.flags & kPoOutlier) {
         double x, y, z;
-        po_err(E, P, D, e, x, y, z);
-        sm.e[0][i] = e[0];
-        sm.e[1][i] = e[1];
-        sm.e[2][i] = e[2];
+        po_err(Ed, P, D, e, x, y, z);
+        E[i] = e[0];
+        E[ES + i] = e[1];
+        E[2 * ES + i] = e[2];
       } else {
-        e[0] = sm.e[0][i];
-        e[1] = sm.e[1][i];
-        e[2] = sm.e[2][i];
+        e[0] = E[i];
+        e[1] = E[ES + i];
+        e[2] = E[2 * ES + i];
       }
-      const double c = po_chi2(E, e);
-      const float thr = (E.flags & kPoStereo) ? 7.815f : 5.991f;
-      int f = c > (double)thr ? (E.flags | kPoOutlier) : (E.flags & ~kPoOutlier);
+      const double c = po_chi2(Ed, e);
+      const float thr = (Ed.flags & kPoStereo) ? 7.815f : 5.991f;
+      int f = c > (double)thr ? (Ed.flags | kPoOutlier) : (Ed.flags & ~kPoOutlier);
       nb[0] += (f & kPoOutlier) ? 1.0 : 0.0;
       if (it == 2) f &= ~kPoRobust;
       flags[i] = f;
@@ -1249,7 +1254,10 @@ __global__ __launch_bounds__(256) void k_pose_opt(const PoseOptDesc* __restrict_
     for (int i = threadIdx.x; i < N; i += nt) D.outlier[i] = 0;
     return;
   }
-  pose_opt_body(D, N, sm);
+  if (N <= kPoseOptMaxEdges)
+    pose_opt_body<false>(D, N, sm);
+  else
+    pose_opt_body<true>(D, N, sm);
 }
 
 void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, hipStream_t st) {

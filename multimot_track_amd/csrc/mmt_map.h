@@ -1,0 +1,226 @@
+// multimot_track_amd/csrc/mmt_map.h -- ORB-SLAM2 map tracking for RGB-D: the
+// MapPoint / KeyFrame state and Tracking's map branch that produce the ego pose the flow solve
+// (PoseOptimizationFlow2Cam, D2) starts from.
+//
+// Reference: MapPoint.cc, KeyFrame.cc, Map.cc; Tracking.cc:985-1176 (Track's map branch),
+// 2531-2575 (StereoInitialization), 2766-3612 (CheckReplacedInLastFrame, UpdateLastFrame,
+// TrackWithMotionModel, TrackReferenceKeyFrame, TrackLocalMap, NeedNewKeyFrame, CreateNewKeyFrame,
+// SearchLocalPoints, UpdateLocalMap); LocalMapping.cc:131-208 (ProcessNewKeyFrame,
+// MapPointCulling, run synchronously after each new keyframe).
+//
+// The bookkeeping (observations, covisibility graph, spanning tree, local map, keyframe policy)
+// is host C++ where the reference keeps it; the data-parallel parts run on the GPU through the
+// C1-C3 / D1 kernels: SearchByProjection frame-to-frame (k_sbp_frame + k_match_greedy),
+// SearchLocalPoints (k_local_cand + k_match_greedy over a device-resident pool of the map points,
+// updated by scatter as points are created or refined) and PoseOptimization (k_pose_opt).
+// Pinned choices and deviations (the same in oracle/oracle_map.h):
+//  * maps and sets keyed by KeyFrame* iterate in keyframe creation order;
+//  * LocalMapping runs synchronously (always idle for NeedNewKeyFrame) and does
+//    ProcessNewKeyFrame without the BoW conversion, then MapPointCulling; CreateNewMapPoints needs
+//    the missing vocabulary, SearchInNeighbors / LocalBundleAdjustment / KeyFrameCulling are
+//    SURVEY 8(f)-3;
+//  * TrackReferenceKeyFrame's SearchByBoW and Relocalization (BoW database) become
+//    SearchByProjection against the last frame at the last frame's pose (th 15) + the reference's
+//    PoseOptimization and acceptance tests.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <set>
+#include <utility>
+#include <vector>
+
+#include "mmt_internal.h"
+#include "mmt_match.h"
+#include "mmt_track.h"
+
+namespace mmt {
+
+struct MapCamH {
+  int W = 0, H = 0;
+  float fx = 0, fy = 0, cx = 0, cy = 0, invfx = 0, invfy = 0, bf = 0;
+  float thDepth = 0;  // mThDepth = mbf * ThDepth / fx (Tracking.cc:225)
+  int maxFrames = 0;  // mMaxFrames = fps (Tracking.cc:176)
+  int nlevels = 0;
+  float logScale = 0;
+  std::vector<float> scale, invSigma2;
+};
+
+struct MPoint {
+  float pos[3] = {0, 0, 0};
+  float normal[3] = {0, 0, 0};
+  float minDist = 0, maxDist = 0;
+  uint8_t desc[32] = {0};
+  std::vector<std::pair<int, int>> obs;  // mObservations (keyframe id, key index), id-ascending
+  int nObs = 0;
+  int refKF = -1;
+  int firstKFid = -1;
+  int visible = 1, found = 1;
+  bool bad = false;
+  bool trackInView = false;
+  bool dirty = false;  // pool record out of date
+  long trackRef = 0, lastSeen = 0;
+  int obs_index(int kf) const {
+    for (const auto& o : obs)
+      if (o.first == kf) return o.second;
+    return -1;
+  }
+};
+
+struct KFrame {
+  int id = 0;
+  long frameId = 0;
+  float Tcw[16], Twc[16], Ow[3];
+  std::vector<mmt_kp> keys;
+  std::vector<float> uR, depth;
+  std::vector<uint8_t> desc;
+  std::vector<int> mps;
+  std::map<int, int> conn;  // mConnectedKeyFrameWeights
+  std::vector<int> ordered;
+  bool firstConnection = true;
+  int parent = -1;
+  std::set<int> children;
+  long trackRef = 0;
+  bool bad = false;
+};
+
+// The map-path view of one Frame: its ORB output and B3 arrays (host copies of the device ones)
+// and its map state.
+struct MapFrameH {
+  long id = 0;
+  int n = 0;
+  const mmt_kp* kps = nullptr;
+  const uint8_t* desc = nullptr;
+  const float* uR = nullptr;     // mvuRight
+  const float* depth = nullptr;  // mvDepth
+  std::vector<int> mps;          // mvpMapPoints (point handle or -1)
+  std::vector<uint8_t> outlier;  // mvbOutlier
+  int refKF = -1;                // mpReferenceKF
+};
+
+struct MapStatsH {
+  int state = 0;           // 0 not initialised, 1 OK, 2 LOST
+  int matches_mm = -1;     // TrackWithMotionModel's nmatches before PoseOptimization (-1: not run)
+  int inliers_local = -1;  // mnMatchesInliers after TrackLocalMap (-1: not run)
+  int n_keyframes = 0, n_mappoints = 0;
+  int new_keyframe = 0;
+  float Tcw_map[16];       // the map branch's pose: PoseOptimizationFlow2Cam's initial estimate
+};
+
+class MapEngine {
+ public:
+  ~MapEngine();
+  void setup(const MapCamH& cam, int kcap);
+  void reset();  // Tracking::Reset (map part)
+  long next_frame_id() { return frameNextId_++; }
+  void prepare(MapFrameH& F) const;  // mvpMapPoints / mvbOutlier of a new frame
+  // StereoInitialization's map part (Tracking.cc:2531-2575)
+  void initialize(MapFrameH& C, const float* Tcw);
+  // Track()'s map branch (Tracking.cc:985-1176); G: the current frame on the device.  Returns 1
+  // when the reference resets the system (LOST with <= 5 keyframes, Tracking.cc:1165-1172).
+  int track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L, float* Tlast, float* vel,
+            bool& has_vel, bool& bSecondFrame, MapStatsH& st, hipStream_t s);
+  // end of Track: mlRelativeFramePoses.push_back(Tcw * Tref^-1) (Tracking.cc:2481-2489)
+  void frame_done(const MapFrameH& C, const float* Tcw);
+  int state() const { return state_; }
+  int n_keyframes() const;
+  int n_mappoints() const { return n_good_; }
+
+ private:
+  static constexpr int kTemp = 1 << 29;
+  MPoint& mp(int h) { return h >= kTemp ? temps_[h - kTemp] : pts_[h]; }
+  bool track_with_motion_model(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
+                               float* Tlast, const float* vel, MapStatsH& st);
+  bool track_reference_subst(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
+                             const float* Tlast);
+  bool track_local_map(MapFrameH& C, const GridFrame& G, float* Tcw);
+  int discard_outliers(MapFrameH& C, int nmatches, int* nmatchesMap);
+  void update_last_frame(MapFrameH& L, float* Tlast);
+  void update_local_keyframes(MapFrameH& C);
+  void update_local_points();
+  void search_local_points(MapFrameH& C, const GridFrame& G, const float* Tcw);
+  bool need_new_keyframe(const MapFrameH& C);
+  void create_new_keyframe(MapFrameH& C, const float* Tcw);
+  int new_keyframe(const MapFrameH& C, const float* Tcw);
+  int new_point_kf(const float* pos, int kf);
+  void add_observation(int h, int kf, int idx);
+  void set_bad(int h);
+  void compute_distinctive(int h);
+  void update_normal_depth(int h);
+  void update_connections(int kf);
+  void add_connection(int kf, int other, int w);
+  void update_best_covisibles(int kf);
+  int tracked_map_points(int kf, int minObs);
+  void process_new_keyframe(int kf);
+  void map_point_culling(int kf);
+  void mark_dirty(int h);
+  // GPU stages (synchronous on s_)
+  int gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* Tcw, const MapFrameH& L,
+                       const float* Tlast, float th);
+  int gpu_pose_opt(MapFrameH& C, float* Tcw);
+  void gpu_flush_pool();
+  template <typename T>
+  T* dev(size_t n);
+  template <typename T>
+  T* pinned(size_t n);
+  void grow_local(int m);
+
+  MapCamH cam_;
+  int kcap_ = 0;
+  std::vector<MPoint> pts_, temps_;
+  std::vector<KFrame> kfs_;
+  int state_ = 0;
+  long frameNextId_ = 0;
+  int kfNextId_ = 0;
+  long lastKFFrameId_ = 0;
+  int refKF_ = -1;
+  std::vector<int> localKFs_, localPts_, recent_, dirty_;
+  float Tlr_[16];
+  bool hasTlr_ = false;
+  int matchesInliers_ = 0;
+  bool mbVO_ = false;
+  long lastRelocFrameId_ = 0;
+  long curId_ = 0;
+  int n_good_ = 0;  // non-bad map points
+  hipStream_t s_ = nullptr;
+
+  // device / pinned buffers
+  std::vector<void*> dallocs_, hallocs_;
+  // C2: the last frame, packed [kps][Xw][desc][active][obs]
+  uint8_t* d_last_ = nullptr;
+  uint8_t* h_last_ = nullptr;
+  CandSet c2_{};
+  int* d_match_ = nullptr;
+  int* d_nm_ = nullptr;
+  int* h_match_ = nullptr;
+  int* h_nm_ = nullptr;
+  // D1
+  float* d_edges_ = nullptr;
+  float* h_edges_ = nullptr;
+  PoseOptDesc* d_pod_ = nullptr;
+  PoseOptDesc* h_pod_ = nullptr;
+  float* d_pose_ = nullptr;
+  uint8_t* d_outl_ = nullptr;
+  int* d_ninl_ = nullptr;
+  double* d_esc_ = nullptr;
+  int* d_fsc_ = nullptr;
+  float* h_pose_ = nullptr;
+  uint8_t* h_outl_ = nullptr;
+  int* h_ninl_ = nullptr;
+  // C3: point pool, local selection, candidates
+  LocalPointDev* d_pool_ = nullptr;
+  uint8_t* d_pool_desc_ = nullptr;
+  int pool_cap_ = 0;
+  PoolUpdate* d_up_ = nullptr;
+  PoolUpdate* h_up_ = nullptr;
+  int up_cap_ = 0;
+  uint8_t* d_sel_ = nullptr;  // [ids m][skip m][taken kcap]
+  uint8_t* h_sel_ = nullptr;
+  uint8_t* d_inview_ = nullptr;
+  uint8_t* h_inview_ = nullptr;
+  CandSet c3_{};
+  int local_cap_ = 0;
+};
+
+}  // namespace mmt

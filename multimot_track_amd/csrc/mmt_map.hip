@@ -1,0 +1,910 @@
+// multimot_track_amd/csrc/mmt_map.hip -- ORB-SLAM2 map tracking for RGB-D (see mmt_map.h).
+//
+// cv::Mat float arithmetic as elsewhere on the host side of this path: products accumulate in
+// double and round to float, the translation is added in float; Mat / scalar is * (1.0 / s) in
+// double; cv::norm is the double square root of the double sum of squares.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+
+#include "mmt_map.h"
+#include "mmt_mat4.h"
+
+namespace mmt {
+
+// ------------------------------------------------------------------ pose helpers
+// Frame::UpdatePoseMatrices / KeyFrame::SetPose: Ow = -Rcw^T tcw
+static void cam_centre(const float* T, float* Ow) {
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)T[4 * k + 3];
+    Ow[r] = -(float)s;
+  }
+}
+
+// Frame::UnprojectStereo (Frame.cc:1064-1079): Rwc * ((u - cx) z / fx, (v - cy) z / fy, z) + Ow
+static void unproject(const MapCamH& c, const float* T, float u, float v, float z, float* out) {
+  const float x = (u - c.cx) * z * c.invfx;
+  const float y = (v - c.cy) * z * c.invfy;
+  const float xc[3] = {x, y, z};
+  float Ow[3];
+  cam_centre(T, Ow);
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)xc[k];
+    out[r] = (float)s + Ow[r];
+  }
+}
+
+static float norm3(const float* v) {
+  double s = 0;
+  for (int k = 0; k < 3; k++) s += (double)v[k] * (double)v[k];
+  return (float)std::sqrt(s);
+}
+
+// ------------------------------------------------------------------ buffers
+template <typename T>
+T* MapEngine::dev(size_t n) {
+  T* p = nullptr;
+  MMT_HIP(hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T)));
+  dallocs_.push_back(p);
+  return p;
+}
+
+template <typename T>
+T* MapEngine::pinned(size_t n) {
+  T* p = nullptr;
+  MMT_HIP(hipHostMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault));
+  hallocs_.push_back(p);
+  return p;
+}
+
+MapEngine::~MapEngine() {
+  if (s_) (void)hipStreamSynchronize(s_);
+  for (void* p : dallocs_) (void)hipFree(p);
+  for (void* p : hallocs_) (void)hipHostFree(p);
+}
+
+static size_t last_bytes(int n) { return (size_t)n * (sizeof(mmt_kp) + 12 + 32 + 2); }
+
+void MapEngine::setup(const MapCamH& cam, int kcap) {
+  cam_ = cam;
+  kcap_ = kcap;
+  d_last_ = dev<uint8_t>(last_bytes(kcap));
+  h_last_ = pinned<uint8_t>(last_bytes(kcap));
+  c2_ = CandSet{dev<uint32_t>((size_t)kcap * kCandK), dev<int>((size_t)kcap * kCandK),
+                dev<int>(kcap), dev<PointWin>(kcap)};
+  d_match_ = dev<int>(kcap);
+  d_nm_ = dev<int>(1);
+  h_match_ = pinned<int>(kcap);
+  h_nm_ = pinned<int>(1);
+  d_edges_ = dev<float>(7 * (size_t)kcap);
+  h_edges_ = pinned<float>(7 * (size_t)kcap);
+  d_pod_ = dev<PoseOptDesc>(1);
+  h_pod_ = pinned<PoseOptDesc>(1);
+  d_pose_ = dev<float>(16);
+  d_outl_ = dev<uint8_t>(kcap);
+  d_ninl_ = dev<int>(1);
+  d_esc_ = dev<double>(3 * (size_t)kcap);
+  d_fsc_ = dev<int>(kcap);
+  h_pose_ = pinned<float>(16);
+  h_outl_ = pinned<uint8_t>(kcap);
+  h_ninl_ = pinned<int>(1);
+  frameNextId_ = 0;
+  mbVO_ = false;
+  matchesInliers_ = 0;
+  lastRelocFrameId_ = 0;
+  reset();
+}
+
+// the local-map buffers grow with the local map; the point pool with the map
+void MapEngine::grow_local(int m) {
+  if (m <= local_cap_) return;
+  const int cap = std::max(m + 4096, 2 * local_cap_);
+  void* old[] = {d_sel_, h_sel_, d_inview_, h_inview_, c3_.key, c3_.idx, c3_.n, c3_.win};
+  if (s_) MMT_HIP(hipStreamSynchronize(s_));
+  for (int i = 0; i < 8; i++) {
+    if (!old[i]) continue;
+    auto it = std::find(i == 1 || i == 3 ? hallocs_.begin() : dallocs_.begin(),
+                        i == 1 || i == 3 ? hallocs_.end() : dallocs_.end(), old[i]);
+    if (i == 1 || i == 3) {
+      (void)hipHostFree(old[i]);
+      hallocs_.erase(it);
+    } else {
+      (void)hipFree(old[i]);
+      dallocs_.erase(it);
+    }
+  }
+  d_sel_ = dev<uint8_t>((size_t)5 * cap + kcap_);
+  h_sel_ = pinned<uint8_t>((size_t)5 * cap + kcap_);
+  d_inview_ = dev<uint8_t>(cap);
+  h_inview_ = pinned<uint8_t>(cap);
+  c3_ = CandSet{dev<uint32_t>((size_t)cap * kCandK), dev<int>((size_t)cap * kCandK), dev<int>(cap),
+                dev<PointWin>(cap)};
+  local_cap_ = cap;
+}
+
+void MapEngine::reset() {
+  pts_.clear();
+  temps_.clear();
+  kfs_.clear();
+  state_ = 0;
+  frameNextId_ = 0;  // Frame::nNextId = 0 (Tracking.cc:3808)
+  kfNextId_ = 0;
+  lastKFFrameId_ = 0;
+  refKF_ = -1;
+  localKFs_.clear();
+  localPts_.clear();
+  recent_.clear();
+  dirty_.clear();
+  hasTlr_ = false;
+  n_good_ = 0;
+}
+
+int MapEngine::n_keyframes() const {
+  int n = 0;
+  for (const KFrame& k : kfs_) n += !k.bad;
+  return n;
+}
+
+void MapEngine::prepare(MapFrameH& F) const {
+  F.mps.assign(F.n, -1);
+  F.outlier.assign(F.n, 0);
+  F.refKF = -1;
+}
+
+// ------------------------------------------------------------------ MapPoint
+void MapEngine::mark_dirty(int h) {
+  if (h >= kTemp) return;  // temporal points never enter the local map
+  MPoint& p = pts_[h];
+  if (!p.dirty) {
+    p.dirty = true;
+    dirty_.push_back(h);
+  }
+}
+
+int MapEngine::new_point_kf(const float* pos, int kf) {  // MapPoint(Pos, pRefKF, pMap)
+  MPoint p;
+  memcpy(p.pos, pos, 12);
+  p.firstKFid = kfs_[kf].id;
+  p.refKF = kf;
+  pts_.push_back(p);
+  n_good_++;
+  const int h = (int)pts_.size() - 1;
+  mark_dirty(h);
+  return h;
+}
+
+void MapEngine::add_observation(int h, int kf, int idx) {  // MapPoint::AddObservation
+  MPoint& p = mp(h);
+  if (p.obs_index(kf) >= 0) return;
+  auto it = std::lower_bound(p.obs.begin(), p.obs.end(), std::make_pair(kf, INT_MIN));
+  p.obs.insert(it, {kf, idx});
+  if (kfs_[kf].uR[idx] >= 0)
+    p.nObs += 2;
+  else
+    p.nObs++;
+}
+
+void MapEngine::set_bad(int h) {  // MapPoint::SetBadFlag
+  MPoint& p = mp(h);
+  if (!p.bad && h < kTemp) n_good_--;
+  p.bad = true;
+  const std::vector<std::pair<int, int>> o = p.obs;
+  p.obs.clear();
+  for (const auto& kv : o) kfs_[kv.first].mps[kv.second] = -1;
+  mark_dirty(h);
+}
+
+void MapEngine::compute_distinctive(int h) {  // MapPoint::ComputeDistinctiveDescriptors
+  MPoint& p = mp(h);
+  if (p.bad || p.obs.empty()) return;
+  std::vector<const uint8_t*> Dv;
+  size_t N = 0;
+  for (const auto& kv : p.obs)
+    if (!kfs_[kv.first].bad) Dv.push_back(kfs_[kv.first].desc.data() + 32 * (size_t)kv.second);
+  N = Dv.size();
+  if (N == 0) return;
+  std::vector<int> dist(N * N, 0);
+  for (size_t i = 0; i < N; i++)
+    for (size_t j = i + 1; j < N; j++) {
+      int d = 0;
+      for (int w = 0; w < 8; w++) {
+        uint32_t a, b;
+        memcpy(&a, Dv[i] + 4 * w, 4);
+        memcpy(&b, Dv[j] + 4 * w, 4);
+        d += __builtin_popcount(a ^ b);
+      }
+      dist[i * N + j] = dist[j * N + i] = d;
+    }
+  int best = INT_MAX;
+  size_t bi = 0;
+  std::vector<int> v(N);
+  for (size_t i = 0; i < N; i++) {
+    std::copy(dist.begin() + i * N, dist.begin() + (i + 1) * N, v.begin());
+    std::sort(v.begin(), v.end());
+    const int median = v[(size_t)(0.5 * (N - 1))];
+    if (median < best) {
+      best = median;
+      bi = i;
+    }
+  }
+  memcpy(p.desc, Dv[bi], 32);
+  mark_dirty(h);
+}
+
+void MapEngine::update_normal_depth(int h) {  // MapPoint::UpdateNormalAndDepth
+  MPoint& p = mp(h);
+  if (p.bad || p.obs.empty()) return;
+  float normal[3] = {0, 0, 0};
+  int n = 0;
+  for (const auto& kv : p.obs) {
+    const float* Ow = kfs_[kv.first].Ow;
+    const float ni[3] = {p.pos[0] - Ow[0], p.pos[1] - Ow[1], p.pos[2] - Ow[2]};
+    const double inv = 1.0 / (double)norm3(ni);
+    for (int k = 0; k < 3; k++) normal[k] = normal[k] + (float)((double)ni[k] * inv);
+    n++;
+  }
+  const KFrame& R = kfs_[p.refKF];
+  const float PC[3] = {p.pos[0] - R.Ow[0], p.pos[1] - R.Ow[1], p.pos[2] - R.Ow[2]};
+  const float dist = norm3(PC);
+  const int level = R.keys[p.obs_index(p.refKF)].octave;
+  p.maxDist = dist * cam_.scale[level];
+  p.minDist = p.maxDist / cam_.scale[cam_.nlevels - 1];
+  for (int k = 0; k < 3; k++) p.normal[k] = (float)((double)normal[k] * (1.0 / n));
+  mark_dirty(h);
+}
+
+// ------------------------------------------------------------------ KeyFrame
+int MapEngine::new_keyframe(const MapFrameH& C, const float* Tcw) {  // KeyFrame(F, ...)
+  kfs_.emplace_back();
+  KFrame& k = kfs_.back();
+  k.id = kfNextId_++;
+  k.frameId = C.id;
+  memcpy(k.Tcw, Tcw, 64);
+  cam_centre(Tcw, k.Ow);
+  mat4_eye(k.Twc);
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) k.Twc[4 * r + c] = Tcw[4 * c + r];
+    k.Twc[4 * r + 3] = k.Ow[r];
+  }
+  k.keys.assign(C.kps, C.kps + C.n);
+  k.uR.assign(C.uR, C.uR + C.n);
+  k.depth.assign(C.depth, C.depth + C.n);
+  k.desc.assign(C.desc, C.desc + 32 * (size_t)C.n);
+  k.mps = C.mps;
+  return (int)kfs_.size() - 1;
+}
+
+void MapEngine::update_best_covisibles(int kf) {  // KeyFrame::UpdateBestCovisibles
+  KFrame& K = kfs_[kf];
+  std::vector<std::pair<int, int>> v;
+  for (const auto& kv : K.conn) v.push_back({kv.second, kv.first});
+  std::sort(v.begin(), v.end());
+  K.ordered.clear();
+  for (auto it = v.rbegin(); it != v.rend(); ++it) K.ordered.push_back(it->second);
+}
+
+void MapEngine::add_connection(int kf, int other, int w) {  // KeyFrame::AddConnection
+  KFrame& K = kfs_[kf];
+  auto it = K.conn.find(other);
+  if (it == K.conn.end())
+    K.conn[other] = w;
+  else if (it->second != w)
+    it->second = w;
+  else
+    return;
+  update_best_covisibles(kf);
+}
+
+void MapEngine::update_connections(int kf) {  // KeyFrame::UpdateConnections
+  std::map<int, int> counter;
+  for (int h : kfs_[kf].mps) {
+    if (h < 0) continue;
+    const MPoint& p = mp(h);
+    if (p.bad) continue;
+    for (const auto& kv : p.obs)
+      if (kv.first != kf) counter[kv.first]++;
+  }
+  if (counter.empty()) return;
+  int nmax = 0, kmax = -1;
+  std::vector<std::pair<int, int>> v;
+  for (const auto& kv : counter) {
+    if (kv.second > nmax) {
+      nmax = kv.second;
+      kmax = kv.first;
+    }
+    if (kv.second >= 15) {
+      v.push_back({kv.second, kv.first});
+      add_connection(kv.first, kf, kv.second);
+    }
+  }
+  if (v.empty()) {
+    v.push_back({nmax, kmax});
+    add_connection(kmax, kf, nmax);
+  }
+  std::sort(v.begin(), v.end());
+  KFrame& K = kfs_[kf];
+  K.conn = counter;
+  K.ordered.clear();
+  for (auto it = v.rbegin(); it != v.rend(); ++it) K.ordered.push_back(it->second);
+  if (K.firstConnection && K.id != 0) {
+    K.parent = K.ordered.front();
+    kfs_[K.parent].children.insert(kf);
+    K.firstConnection = false;
+  }
+}
+
+int MapEngine::tracked_map_points(int kf, int minObs) {  // KeyFrame::TrackedMapPoints
+  int n = 0;
+  for (int h : kfs_[kf].mps) {
+    if (h < 0) continue;
+    const MPoint& p = mp(h);
+    if (p.bad) continue;
+    if (minObs > 0) {
+      if (p.nObs >= minObs) n++;
+    } else {
+      n++;
+    }
+  }
+  return n;
+}
+
+void MapEngine::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFrame, no BoW
+  const std::vector<int> mps = kfs_[kf].mps;
+  for (size_t i = 0; i < mps.size(); i++) {
+    const int h = mps[i];
+    if (h < 0 || mp(h).bad) continue;
+    if (mp(h).obs_index(kf) < 0) {
+      add_observation(h, kf, (int)i);
+      update_normal_depth(h);
+      compute_distinctive(h);
+    } else {
+      recent_.push_back(h);
+    }
+  }
+  update_connections(kf);
+}
+
+void MapEngine::map_point_culling(int kf) {  // LocalMapping::MapPointCulling (RGB-D: 3 obs)
+  const int cur = kfs_[kf].id;
+  std::vector<int> keep;
+  keep.reserve(recent_.size());
+  for (int h : recent_) {
+    MPoint& p = mp(h);
+    if (p.bad) continue;
+    if ((float)p.found / p.visible < 0.25f) {
+      set_bad(h);
+    } else if (cur - p.firstKFid >= 2 && p.nObs <= 3) {
+      set_bad(h);
+    } else if (cur - p.firstKFid < 3) {
+      keep.push_back(h);
+    }
+  }
+  recent_.swap(keep);
+}
+
+// ------------------------------------------------------------------ GPU stages
+int MapEngine::gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* Tcw,
+                                const MapFrameH& L, const float* Tlast, float th) {
+  // SearchByProjection(CurrentFrame, LastFrame, th, bMono=false) with mbCheckOrientation
+  const int n1 = L.n;
+  uint8_t* hk = h_last_;
+  float* hX = (float*)(h_last_ + (size_t)n1 * sizeof(mmt_kp));
+  uint8_t* hD = (uint8_t*)(hX + 3 * (size_t)n1);
+  uint8_t* hA = hD + 32 * (size_t)n1;
+  uint8_t* hO = hA + n1;
+  memcpy(hk, L.kps, sizeof(mmt_kp) * (size_t)n1);
+  for (int i = 0; i < n1; i++) {
+    const int h = L.mps[i];
+    hA[i] = h >= 0 && !L.outlier[i];
+    hO[i] = 0;
+    if (h >= 0) {
+      const MPoint& p = mp(h);
+      memcpy(hX + 3 * (size_t)i, p.pos, 12);
+      memcpy(hD + 32 * (size_t)i, p.desc, 32);
+      hO[i] = p.nObs > 0;
+    }
+  }
+  MMT_HIP(hipMemcpyAsync(d_last_, h_last_, last_bytes(n1), hipMemcpyHostToDevice, s_));
+  LastFrameDev LD;
+  LD.keys = (const mmt_kp*)d_last_;
+  LD.Xw = (const float*)(d_last_ + (size_t)n1 * sizeof(mmt_kp));
+  LD.mp_desc = (const uint8_t*)(LD.Xw + 3 * (size_t)n1);
+  LD.active = LD.mp_desc + 32 * (size_t)n1;
+  LD.obs = LD.active + n1;
+  LD.n = n1;
+  memcpy(LD.Tcw, Tlast, 64);
+  launch_sbp_frame(G, Tcw, LD, th, 0, 1, c2_, d_match_, d_nm_, s_);
+  MMT_HIP(hipMemcpyAsync(h_match_, d_match_, sizeof(int) * (size_t)C.n, hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipMemcpyAsync(h_nm_, d_nm_, sizeof(int), hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipStreamSynchronize(s_));
+  for (int i2 = 0; i2 < C.n; i2++)
+    if (h_match_[i2] >= 0) C.mps[i2] = L.mps[h_match_[i2]];
+  return *h_nm_;
+}
+
+int MapEngine::gpu_pose_opt(MapFrameH& C, float* Tcw) {
+  // Optimizer::PoseOptimization(&mCurrentFrame): the frame's MapPoints in key order
+  std::vector<int> idx;
+  idx.reserve(C.n);
+  for (int i = 0; i < C.n; i++)
+    if (C.mps[i] >= 0) idx.push_back(i);
+  const int n = (int)idx.size();
+  float* X = h_edges_;
+  float* ob = X + 3 * (size_t)n;
+  float* s2 = ob + 3 * (size_t)n;
+  for (int e = 0; e < n; e++) {
+    const int i = idx[e];
+    const MPoint& p = mp(C.mps[i]);
+    memcpy(X + 3 * (size_t)e, p.pos, 12);
+    ob[3 * e] = C.kps[i].x;
+    ob[3 * e + 1] = C.kps[i].y;
+    ob[3 * e + 2] = C.uR[i];
+    s2[e] = cam_.invSigma2[C.kps[i].octave];
+    C.outlier[i] = 0;
+  }
+  PoseOptDesc& d = *h_pod_;
+  memset(&d, 0, sizeof(d));
+  d.n = n;
+  d.Xw = d_edges_;
+  d.obs = d_edges_ + 3 * (size_t)n;
+  d.inv_sigma2 = d_edges_ + 6 * (size_t)n;
+  memcpy(d.Tcw, Tcw, 64);
+  d.fx = cam_.fx; d.fy = cam_.fy; d.cx = cam_.cx; d.cy = cam_.cy; d.bf = cam_.bf;
+  d.pose_out = d_pose_;
+  d.outlier = d_outl_;
+  d.n_inliers = d_ninl_;
+  d.e_scratch = d_esc_;
+  d.f_scratch = d_fsc_;
+  if (n > 0)
+    MMT_HIP(hipMemcpyAsync(d_edges_, h_edges_, sizeof(float) * 7 * (size_t)n,
+                           hipMemcpyHostToDevice, s_));
+  MMT_HIP(hipMemcpyAsync(d_pod_, h_pod_, sizeof(PoseOptDesc), hipMemcpyHostToDevice, s_));
+  launch_pose_opt(d_pod_, 1, s_);
+  MMT_HIP(hipMemcpyAsync(h_pose_, d_pose_, 64, hipMemcpyDeviceToHost, s_));
+  if (n > 0) MMT_HIP(hipMemcpyAsync(h_outl_, d_outl_, (size_t)n, hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipMemcpyAsync(h_ninl_, d_ninl_, sizeof(int), hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipStreamSynchronize(s_));
+  if (n >= 3) {
+    memcpy(Tcw, h_pose_, 64);
+    for (int e = 0; e < n; e++) C.outlier[idx[e]] = h_outl_[e];
+  }
+  return *h_ninl_;
+}
+
+void MapEngine::gpu_flush_pool() {
+  // grow the pool with the map, then scatter the changed records
+  if ((int)pts_.size() > pool_cap_) {
+    const int cap = std::max((int)pts_.size() + 8192, 2 * pool_cap_);
+    LocalPointDev* np = nullptr;
+    uint8_t* nd = nullptr;
+    MMT_HIP(hipMalloc((void**)&np, sizeof(LocalPointDev) * (size_t)cap));
+    MMT_HIP(hipMalloc((void**)&nd, 32 * (size_t)cap));
+    if (pool_cap_ > 0) {
+      MMT_HIP(hipMemcpyAsync(np, d_pool_, sizeof(LocalPointDev) * (size_t)pool_cap_,
+                             hipMemcpyDeviceToDevice, s_));
+      MMT_HIP(hipMemcpyAsync(nd, d_pool_desc_, 32 * (size_t)pool_cap_, hipMemcpyDeviceToDevice,
+                             s_));
+      MMT_HIP(hipStreamSynchronize(s_));
+      auto drop = [&](void* p) {
+        dallocs_.erase(std::find(dallocs_.begin(), dallocs_.end(), p));
+        (void)hipFree(p);
+      };
+      drop(d_pool_);
+      drop(d_pool_desc_);
+    }
+    d_pool_ = np;
+    d_pool_desc_ = nd;
+    dallocs_.push_back(np);
+    dallocs_.push_back(nd);
+    pool_cap_ = cap;
+  }
+  const int nd = (int)dirty_.size();
+  if (nd == 0) return;
+  if (nd > up_cap_) {
+    MMT_HIP(hipStreamSynchronize(s_));
+    if (d_up_) {
+      dallocs_.erase(std::find(dallocs_.begin(), dallocs_.end(), (void*)d_up_));
+      hallocs_.erase(std::find(hallocs_.begin(), hallocs_.end(), (void*)h_up_));
+      (void)hipFree(d_up_);
+      (void)hipHostFree(h_up_);
+    }
+    up_cap_ = std::max(nd + 4096, 2 * up_cap_);
+    d_up_ = dev<PoolUpdate>(up_cap_);
+    h_up_ = pinned<PoolUpdate>(up_cap_);
+  }
+  for (int q = 0; q < nd; q++) {
+    const int h = dirty_[q];
+    MPoint& p = pts_[h];
+    PoolUpdate& u = h_up_[q];
+    u.h = h;
+    memcpy(u.p.Xw, p.pos, 12);
+    memcpy(u.p.normal, p.normal, 12);
+    u.p.min_dist = p.minDist;
+    u.p.max_dist = p.maxDist;
+    u.p.skip = 0;
+    memcpy(u.desc, p.desc, 32);
+    p.dirty = false;
+  }
+  MMT_HIP(hipMemcpyAsync(d_up_, h_up_, sizeof(PoolUpdate) * (size_t)nd, hipMemcpyHostToDevice,
+                         s_));
+  launch_pool_scatter(d_up_, nd, d_pool_, d_pool_desc_, s_);
+  dirty_.clear();
+}
+
+// ------------------------------------------------------------------ Tracking
+void MapEngine::initialize(MapFrameH& C, const float* Tcw) {
+  const int kf = new_keyframe(C, Tcw);
+  for (int i = 0; i < C.n; i++) {
+    const float z = C.depth[i];
+    if (z > 0) {
+      float x3D[3];
+      unproject(cam_, Tcw, C.kps[i].x, C.kps[i].y, z, x3D);
+      const int h = new_point_kf(x3D, kf);
+      add_observation(h, kf, i);
+      kfs_[kf].mps[i] = h;
+      compute_distinctive(h);
+      update_normal_depth(h);
+      C.mps[i] = h;
+    }
+  }
+  process_new_keyframe(kf);
+  map_point_culling(kf);
+  lastKFFrameId_ = C.id;
+  localKFs_.assign(1, kf);
+  localPts_.clear();
+  for (size_t h = 0; h < pts_.size(); h++)
+    if (!pts_[h].bad) localPts_.push_back((int)h);  // mpMap->GetAllMapPoints()
+  refKF_ = kf;
+  C.refKF = kf;
+  state_ = 1;
+}
+
+void MapEngine::frame_done(const MapFrameH& C, const float* Tcw) {
+  if (C.refKF < 0) return;
+  mat4_mul(Tcw, kfs_[C.refKF].Twc, Tlr_);  // Tcr = mTcw * mpReferenceKF->GetPoseInverse()
+  hasTlr_ = true;
+}
+
+void MapEngine::update_last_frame(MapFrameH& L, float* Tlast) {  // Tracking.cc:2894-2960
+  if (L.refKF >= 0 && hasTlr_) mat4_mul(Tlr_, kfs_[L.refKF].Tcw, Tlast);
+  if (lastKFFrameId_ == L.id) return;
+  std::vector<std::pair<float, int>> v;
+  v.reserve(L.n);
+  for (int i = 0; i < L.n; i++)
+    if (L.depth[i] > 0) v.push_back({L.depth[i], i});
+  if (v.empty()) return;
+  std::sort(v.begin(), v.end());
+  int nPoints = 0;
+  for (size_t j = 0; j < v.size(); j++) {
+    const int i = v[j].second;
+    if (L.mps[i] < 0 || mp(L.mps[i]).nObs < 1) {
+      MPoint p;  // MapPoint(x3D, mpMap, &mLastFrame, i): C2 reads its position and descriptor
+      unproject(cam_, Tlast, L.kps[i].x, L.kps[i].y, L.depth[i], p.pos);
+      memcpy(p.desc, L.desc + 32 * (size_t)i, 32);
+      temps_.push_back(p);
+      L.mps[i] = kTemp + (int)temps_.size() - 1;
+    }
+    nPoints++;
+    if (v[j].first > cam_.thDepth && nPoints > 200) break;
+  }
+}
+
+// TrackWithMotionModel / TrackReferenceKeyFrame's outlier discard: returns nmatches
+int MapEngine::discard_outliers(MapFrameH& C, int nmatches, int* nmatchesMap) {
+  *nmatchesMap = 0;
+  for (int i = 0; i < C.n; i++) {
+    if (C.mps[i] < 0) continue;
+    if (C.outlier[i]) {
+      MPoint& p = mp(C.mps[i]);
+      C.mps[i] = -1;
+      C.outlier[i] = 0;
+      p.trackInView = false;
+      p.lastSeen = curId_;
+      nmatches--;
+    } else if (mp(C.mps[i]).nObs > 0) {
+      (*nmatchesMap)++;
+    }
+  }
+  return nmatches;
+}
+
+bool MapEngine::track_with_motion_model(MapFrameH& C, const GridFrame& G, float* Tcw,
+                                        MapFrameH& L, float* Tlast, const float* vel,
+                                        MapStatsH& st) {
+  update_last_frame(L, Tlast);
+  mat4_mul(vel, Tlast, Tcw);
+  std::fill(C.mps.begin(), C.mps.end(), -1);
+  const float th = 15;
+  int nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, th);
+  if (nmatches < 20) {
+    std::fill(C.mps.begin(), C.mps.end(), -1);
+    nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, 2 * th);
+  }
+  st.matches_mm = nmatches;
+  if (nmatches < 20) return false;
+  gpu_pose_opt(C, Tcw);
+  int nmatchesMap = 0;
+  discard_outliers(C, nmatches, &nmatchesMap);
+  mbVO_ = nmatchesMap < 20;
+  return nmatchesMap >= 10;
+}
+
+bool MapEngine::track_reference_subst(MapFrameH& C, const GridFrame& G, float* Tcw,
+                                      const MapFrameH& L, const float* Tlast) {
+  std::fill(C.mps.begin(), C.mps.end(), -1);
+  memcpy(Tcw, Tlast, 64);
+  const int nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, 15);
+  if (nmatches < 15) {
+    std::fill(C.mps.begin(), C.mps.end(), -1);
+    return false;
+  }
+  gpu_pose_opt(C, Tcw);
+  int nmatchesMap = 0;
+  discard_outliers(C, nmatches, &nmatchesMap);
+  return nmatchesMap >= 10;
+}
+
+void MapEngine::update_local_keyframes(MapFrameH& C) {  // Tracking::UpdateLocalKeyFrames
+  std::map<int, int> counter;
+  for (int i = 0; i < C.n; i++) {
+    if (C.mps[i] < 0) continue;
+    const MPoint& p = mp(C.mps[i]);
+    if (!p.bad) {
+      for (const auto& kv : p.obs) counter[kv.first]++;
+    } else {
+      C.mps[i] = -1;
+    }
+  }
+  if (counter.empty()) return;
+  int mx = 0, kmax = -1;
+  localKFs_.clear();
+  for (const auto& kv : counter) {
+    KFrame& K = kfs_[kv.first];
+    if (K.bad) continue;
+    if (kv.second > mx) {
+      mx = kv.second;
+      kmax = kv.first;
+    }
+    localKFs_.push_back(kv.first);
+    K.trackRef = curId_;
+  }
+  const size_t n0 = localKFs_.size();
+  for (size_t q = 0; q < n0; q++) {
+    if (localKFs_.size() > 80) break;
+    const KFrame& K = kfs_[localKFs_[q]];
+    const size_t nn = std::min<size_t>(10, K.ordered.size());
+    for (size_t a = 0; a < nn; a++) {
+      KFrame& N = kfs_[K.ordered[a]];
+      if (!N.bad && N.trackRef != curId_) {
+        localKFs_.push_back(K.ordered[a]);
+        N.trackRef = curId_;
+        break;
+      }
+    }
+    for (int ch : K.children) {
+      KFrame& N = kfs_[ch];
+      if (!N.bad && N.trackRef != curId_) {
+        localKFs_.push_back(ch);
+        N.trackRef = curId_;
+        break;
+      }
+    }
+    if (K.parent >= 0) {
+      KFrame& Pa = kfs_[K.parent];
+      if (Pa.trackRef != curId_) {
+        localKFs_.push_back(K.parent);
+        Pa.trackRef = curId_;
+        break;  // leaves the keyframe loop (Tracking.cc:3601)
+      }
+    }
+  }
+  if (kmax >= 0) {
+    refKF_ = kmax;
+    C.refKF = kmax;
+  }
+}
+
+void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
+  localPts_.clear();
+  for (int kf : localKFs_)
+    for (int h : kfs_[kf].mps) {
+      if (h < 0) continue;
+      MPoint& p = mp(h);
+      if (p.trackRef == curId_) continue;
+      if (!p.bad) {
+        localPts_.push_back(h);
+        p.trackRef = curId_;
+      }
+    }
+}
+
+void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const float* Tcw) {
+  // Tracking::SearchLocalPoints (Tracking.cc:3416-3466)
+  for (int i = 0; i < C.n; i++) {
+    if (C.mps[i] < 0) continue;
+    MPoint& p = mp(C.mps[i]);
+    if (p.bad) {
+      C.mps[i] = -1;
+    } else {
+      p.visible++;
+      p.lastSeen = curId_;
+      p.trackInView = false;
+    }
+  }
+  const int m = (int)localPts_.size();
+  grow_local(m);
+  gpu_flush_pool();
+  int* ids = (int*)h_sel_;
+  uint8_t* skip = h_sel_ + 4 * (size_t)m;
+  uint8_t* taken = skip + m;
+  for (int j = 0; j < m; j++) {
+    const MPoint& p = mp(localPts_[j]);
+    ids[j] = localPts_[j];
+    skip[j] = (p.lastSeen == curId_) || p.bad;
+  }
+  for (int i = 0; i < C.n; i++) taken[i] = C.mps[i] >= 0 && mp(C.mps[i]).nObs > 0;
+  MMT_HIP(hipMemcpyAsync(d_sel_, h_sel_, 5 * (size_t)m + C.n, hipMemcpyHostToDevice, s_));
+  // ORBmatcher(0.8)::SearchByProjection's th: 3 for RGB-D, 5 right after a relocalisation
+  const float th = curId_ < lastRelocFrameId_ + 2 ? 5.f : 3.f;
+  LocalSel sel{(const int*)d_sel_, d_sel_ + 4 * (size_t)m, d_inview_};
+  launch_search_local(G, Tcw, d_pool_, d_pool_desc_, m, th, d_sel_ + 5 * (size_t)m, nullptr, c3_,
+                      d_match_, d_nm_, s_, &sel);
+  MMT_HIP(hipMemcpyAsync(h_match_, d_match_, sizeof(int) * (size_t)C.n, hipMemcpyDeviceToHost, s_));
+  if (m > 0) MMT_HIP(hipMemcpyAsync(h_inview_, d_inview_, (size_t)m, hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipStreamSynchronize(s_));
+  for (int j = 0; j < m; j++) {
+    if (skip[j]) continue;
+    MPoint& p = mp(localPts_[j]);
+    p.trackInView = h_inview_[j] != 0;
+    if (p.trackInView) p.visible++;
+  }
+  for (int i = 0; i < C.n; i++)
+    if (h_match_[i] >= 0) C.mps[i] = localPts_[h_match_[i]];
+}
+
+bool MapEngine::track_local_map(MapFrameH& C, const GridFrame& G, float* Tcw) {
+  update_local_keyframes(C);
+  update_local_points();
+  search_local_points(C, G, Tcw);
+  gpu_pose_opt(C, Tcw);
+  matchesInliers_ = 0;
+  for (int i = 0; i < C.n; i++) {
+    if (C.mps[i] < 0 || C.outlier[i]) continue;
+    MPoint& p = mp(C.mps[i]);
+    p.found++;
+    if (p.nObs > 0) matchesInliers_++;
+  }
+  if (curId_ < lastRelocFrameId_ + cam_.maxFrames && matchesInliers_ < 50) return false;
+  return matchesInliers_ >= 30;
+}
+
+bool MapEngine::need_new_keyframe(const MapFrameH& C) {  // Tracking::NeedNewKeyFrame (RGB-D)
+  const int nKFs = n_keyframes();
+  if (curId_ < lastRelocFrameId_ + cam_.maxFrames && nKFs > cam_.maxFrames) return false;
+  const int nMinObs = nKFs <= 2 ? 2 : 3;
+  const int nRefMatches = tracked_map_points(refKF_, nMinObs);
+  const bool bLocalMappingIdle = true;  // synchronous LocalMapping (pinned)
+  int nNonTrackedClose = 0, nTrackedClose = 0;
+  for (int i = 0; i < C.n; i++)
+    if (C.depth[i] > 0 && C.depth[i] < cam_.thDepth) {
+      if (C.mps[i] >= 0 && !C.outlier[i])
+        nTrackedClose++;
+      else
+        nNonTrackedClose++;
+    }
+  const bool bNeedToInsertClose = (nTrackedClose < 100) && (nNonTrackedClose > 70);
+  const float thRefRatio = nKFs < 2 ? 0.4f : 0.75f;
+  const bool c1a = curId_ >= lastKFFrameId_ + cam_.maxFrames;
+  const bool c1b = curId_ >= lastKFFrameId_ && bLocalMappingIdle;
+  const bool c1c = matchesInliers_ < nRefMatches * 0.25 || bNeedToInsertClose;
+  const bool c2 = (matchesInliers_ < nRefMatches * thRefRatio || bNeedToInsertClose) &&
+                  matchesInliers_ > 15;
+  return (c1a || c1b || c1c) && c2;
+}
+
+void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracking.cc:3333-3414
+  const int kf = new_keyframe(C, Tcw);
+  refKF_ = kf;
+  C.refKF = kf;
+  std::vector<std::pair<float, int>> v;
+  v.reserve(C.n);
+  for (int i = 0; i < C.n; i++)
+    if (C.depth[i] > 0) v.push_back({C.depth[i], i});
+  if (!v.empty()) {
+    std::sort(v.begin(), v.end());
+    int nPoints = 0;
+    for (size_t j = 0; j < v.size(); j++) {
+      const int i = v[j].second;
+      bool create = false;
+      if (C.mps[i] < 0) {
+        create = true;
+      } else if (mp(C.mps[i]).nObs < 1) {
+        create = true;
+        C.mps[i] = -1;
+      }
+      if (create) {
+        float x3D[3];
+        unproject(cam_, Tcw, C.kps[i].x, C.kps[i].y, C.depth[i], x3D);
+        const int h = new_point_kf(x3D, kf);
+        add_observation(h, kf, i);
+        kfs_[kf].mps[i] = h;
+        compute_distinctive(h);
+        update_normal_depth(h);
+        C.mps[i] = h;
+      }
+      nPoints++;
+      if (v[j].first > cam_.thDepth && nPoints > 200) break;
+    }
+  }
+  process_new_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKF), processed at once
+  map_point_culling(kf);
+  lastKFFrameId_ = C.id;
+}
+
+int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L, float* Tlast,
+                     float* vel, bool& has_vel, bool& bSecondFrame, MapStatsH& st,
+                     hipStream_t s) {
+  s_ = s;
+  curId_ = C.id;
+  bool bOK;
+  // CheckReplacedInLastFrame: no MapPoint is ever replaced on this path (no Fuse, no loops)
+  if (state_ == 1) {
+    if (!has_vel || C.id < lastRelocFrameId_ + 2) {
+      bSecondFrame = true;
+      bOK = track_reference_subst(C, G, Tcw, L, Tlast);
+    } else {
+      bSecondFrame = false;
+      bOK = track_with_motion_model(C, G, Tcw, L, Tlast, vel, st);
+      if (!bOK) {
+        bSecondFrame = true;
+        bOK = track_reference_subst(C, G, Tcw, L, Tlast);
+      }
+    }
+  } else {
+    bOK = track_reference_subst(C, G, Tcw, L, Tlast);  // Relocalization (substitute)
+    if (bOK) lastRelocFrameId_ = C.id;
+  }
+  C.refKF = refKF_;
+  if (bOK && !mbVO_) {
+    bOK = track_local_map(C, G, Tcw);
+    st.inliers_local = matchesInliers_;
+  }
+  state_ = bOK ? 1 : 2;
+  if (bOK) {
+    // motion model from the map pose (Tracking.cc:1117-1125): LastTwc = [Rwc, Ow] of mLastFrame
+    float LastTwc[16], Ow[3];
+    mat4_eye(LastTwc);
+    cam_centre(Tlast, Ow);
+    for (int r = 0; r < 3; r++) {
+      for (int c = 0; c < 3; c++) LastTwc[4 * r + c] = Tlast[4 * c + r];
+      LastTwc[4 * r + 3] = Ow[r];
+    }
+    mat4_mul(Tcw, LastTwc, vel);
+    has_vel = true;
+    for (int i = 0; i < C.n; i++)  // clean VO matches
+      if (C.mps[i] >= 0 && mp(C.mps[i]).nObs < 1) {
+        C.outlier[i] = 0;
+        C.mps[i] = -1;
+      }
+    for (int i = 0; i < L.n; i++)  // delete temporal MapPoints (mLastFrame's become dangling)
+      if (L.mps[i] >= kTemp) L.mps[i] = -1;
+    temps_.clear();
+    if (need_new_keyframe(C)) {
+      create_new_keyframe(C, Tcw);
+      st.new_keyframe = 1;
+    }
+    for (int i = 0; i < C.n; i++)
+      if (C.mps[i] >= 0 && C.outlier[i]) C.mps[i] = -1;
+  }
+  if (state_ == 2 && n_keyframes() <= 5) return 1;  // mpSystem->Reset(); return
+  if (C.refKF < 0) C.refKF = refKF_;
+  return 0;
+}
+
+}  // namespace mmt

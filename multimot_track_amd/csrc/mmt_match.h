@@ -73,6 +73,9 @@ struct LastFrameDev {
   const float* Xw;          // n x 3
   const uint8_t* mp_desc;   // n x 32
   const uint8_t* active;    // MapPoint present and not an outlier
+  // MapPoint::Observations() > 0 (null: all).  A key bound to a point without observations (a
+  // temporal VO point of UpdateLastFrame) stays open to later points (ORBmatcher.cc:2033-2035).
+  const uint8_t* obs;
   int n;
   float Tcw[16];
 };
@@ -81,9 +84,27 @@ void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& 
                       int* nmatches, hipStream_t st);
 
 // C3: SearchLocalPoints' isInFrustum pass + SearchByProjection(Frame&, vector<MapPoint*>, th).
+// ids (null: point j is pts[j]) selects the local points from a resident pool, skip (null: the
+// pool record's own flag) overrides their skip flag; fr (optional) receives the isInFrustum
+// records, inview (optional) one byte per point.
+struct LocalSel {
+  const int* ids;
+  const uint8_t* skip;
+  uint8_t* inview;
+};
 void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointDev* pts,
                          const uint8_t* pdesc, int m, float th, const uint8_t* taken,
                          FrustumRec* fr, const CandSet& cs, int* match, int* nmatches,
+                         hipStream_t st, const LocalSel* sel = nullptr);
+
+// pool maintenance: scatter n packed (handle, record, descriptor) updates into the pool
+struct alignas(16) PoolUpdate {
+  int h;
+  int pad[3];
+  LocalPointDev p;   // offset 16
+  uint8_t desc[32];  // offset 64 (16-byte aligned: copied as two uint4)
+};
+void launch_pool_scatter(const PoolUpdate* up, int n, LocalPointDev* pool, uint8_t* pool_desc,
                          hipStream_t st);
 
 }  // namespace mmt

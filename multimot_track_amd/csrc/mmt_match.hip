@@ -25,6 +25,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
 
 #include "mmt_internal.h"
@@ -175,6 +176,9 @@ void launch_stereo_grid(const mmt_kp* keys, const int* nkp, int cap, const float
 // GetFeaturesInArea's cell range (Frame.cc:711-729); false when the window is empty.
 __device__ __forceinline__ bool window_cells(const GridFrame& G, float x, float y, float r,
                                              int& cx0, int& cx1, int& cy0, int& cy1) {
+  // a non-finite centre (a map point unprojected from depth +inf) has no cells: the reference's
+  // float -> int conversions are undefined there, x86 gives INT_MIN and an empty range
+  if (!isfinite(x) || !isfinite(y)) return false;
   cx0 = max(0, (int)floorf((x - G.minX - r) * G.invW));
   if (cx0 >= kGridCols) return false;
   cx1 = min(kGridCols - 1, (int)ceilf((x - G.minX + r) * G.invW));
@@ -371,6 +375,7 @@ struct LocalArgs {
   float th;
   FrustumRec* fr;
   CandSet cs;
+  LocalSel sel;
 };
 
 __global__ __launch_bounds__(256) void k_local_cand(LocalArgs a) {
@@ -378,11 +383,13 @@ __global__ __launch_bounds__(256) void k_local_cand(LocalArgs a) {
   if (j >= a.m) return;
   const int lane = threadIdx.x & 63;
   const GridFrame& C = a.C;
-  const LocalPointDev p = a.pts[j];
+  const int pj = a.sel.ids ? a.sel.ids[j] : j;
+  const LocalPointDev p = a.pts[pj];
+  const bool skip = a.sel.skip ? a.sel.skip[j] != 0 : p.skip != 0;
   FrustumRec o = {0, 0, 0.f, 0.f, 0.f, 0.f};
   PointWin w = {};
   bool in = false;
-  if (!p.skip) {
+  if (!skip) {
     // Frame::isInFrustum(pMP, 0.5)
     float Pc[3];
     pose_xform(a.Tcw, p.Xw, Pc);
@@ -406,7 +413,9 @@ __global__ __launch_bounds__(256) void k_local_cand(LocalArgs a) {
           const float viewCos = (float)(dot / (double)dist);
           if (!(viewCos < 0.5f)) {
             const float ratio = p.max_dist / dist;
-            int nScale = (int)ceilf((float)log((double)ratio) / C.logScale);
+            // (int)ceil of a non-finite value (a NaN point): INT_MIN on x86 -> level 0
+            const float ls = (float)log((double)ratio) / C.logScale;
+            int nScale = isfinite(ls) ? (int)ceilf(ls) : INT_MIN;
             if (nScale < 0) nScale = 0;
             else if (nScale >= C.nlevels) nScale = C.nlevels - 1;
             o.in_view = 1;
@@ -421,7 +430,10 @@ __global__ __launch_bounds__(256) void k_local_cand(LocalArgs a) {
       }
     }
   }
-  if (lane == 0) a.fr[j] = o;
+  if (lane == 0) {
+    if (a.fr) a.fr[j] = o;
+    if (a.sel.inview) a.sel.inview[j] = (uint8_t)o.in_view;
+  }
   if (!in) {
     store_cands(a.cs, j, -1, kNoCand, -1, w);
     return;
@@ -436,7 +448,7 @@ __global__ __launch_bounds__(256) void k_local_cand(LocalArgs a) {
   w.minLevel = o.level - 1;
   w.maxLevel = o.level;
   uint32_t dmp[8];
-  load_desc8(a.pdesc + 32 * (size_t)j, dmp);
+  load_desc8(a.pdesc + 32 * (size_t)pj, dmp);
   uint32_t tk;
   int ti;
   const int passed = wave_topk<kCandK>(C, w, dmp, nullptr, tk, ti);
@@ -449,8 +461,10 @@ struct GreedyArgs {
   int mode;  // 0: C2 (best only), 1: C3 (best + second-best ratio test)
   int npts;
   CandSet cs;
-  const uint8_t* pdesc;      // npts x 32 point descriptors (rescans)
+  const uint8_t* pdesc;      // npts x 32 point descriptors (rescans), or the pool with ids
+  const int* ids;            // C3 pool indices (null: point j's descriptor is pdesc[j])
   const uint8_t* taken_in;   // C.n bytes or null
+  const uint8_t* obs;        // C2: per point, its binding takes the key (null: all do)
   int check_orientation;
   const mmt_kp* lkeys;       // C2: last-frame keys (angles)
   int* match;                // C.n
@@ -468,13 +482,30 @@ __device__ __forceinline__ int decide(const GreedyArgs& a, int best, int bestD, 
   return best;
 }
 
+// C2's rotation bin of a binding event (ORBmatcher.cc:2064-2071): round() of the float product,
+// only bins 0..12 are reachable (the reference's 1/30 factor on degrees)
+__device__ __forceinline__ int rot_bin(float a_last, float a_cur) {
+  float rot = a_last - a_cur;
+  if (rot < 0.0f) rot += 360.0f;
+  int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
+  if (bin == HISTO_LENGTH) bin = 0;
+  return bin;
+}
+
+// Points bind in index order.  A binding by a point with observations takes its key for the
+// points after it; one by a point without (a temporal VO point) leaves the key open, and a later
+// point's binding replaces it (the key keeps the last binder; match[] is raised with atomicMax,
+// binders arrive in index order).  Every binding is an event of C2's rotation histogram; an event
+// in a rejected bin clears its key, whoever binds it last (ORBmatcher.cc:2087-2098).
 __global__ __launch_bounds__(64) void k_match_greedy(GreedyArgs a) {
   __shared__ uint32_t s_taken[kMaxMatchKeys / 32];
+  __shared__ short s_evt[kMaxMatchKeys];  // C2: the key of point i's binding event (-1: none)
   __shared__ int s_hist[HISTO_LENGTH];
   __shared__ int s_ind[3];
   const int lane = threadIdx.x;
   const int n = a.C.n;
   const int nwords = (n + 31) >> 5;
+  const bool rot = a.mode == 0 && a.check_orientation;
   for (int wd = lane; wd < nwords; wd += 64) {
     uint32_t bits = 0;
     if (a.taken_in)
@@ -485,6 +516,8 @@ __global__ __launch_bounds__(64) void k_match_greedy(GreedyArgs a) {
     s_taken[wd] = bits;
   }
   for (int k = lane; k < n; k += 64) a.match[k] = -1;
+  if (rot)
+    for (int i = lane; i < a.npts; i += 64) s_evt[i] = -1;
   if (lane < HISTO_LENGTH) s_hist[lane] = 0;
   __syncthreads();
   int nm = 0;
@@ -493,6 +526,7 @@ __global__ __launch_bounds__(64) void k_match_greedy(GreedyArgs a) {
     const int i = b + lane;
     int best = -1, bestD = 256, sec = -1, secD = 256;
     bool act = false, resc = false;
+    const bool tk = i < a.npts && (!a.obs || a.obs[i]);
     if (i < a.npts) {
       const int cn = a.cs.n[i];
       if (cn > 0) {
@@ -519,52 +553,50 @@ __global__ __launch_bounds__(64) void k_match_greedy(GreedyArgs a) {
     bool conf = false;
     for (int l = 0; l < 63; l++) {
       const int t = __shfl(tgt, l, 64);
-      if (l < lane && t >= 0 && (t == best || (a.mode == 1 && t == sec))) conf = true;
+      const bool tl = __shfl((int)tk, l, 64) != 0;
+      if (l < lane && t >= 0 && tl && (t == best || (a.mode == 1 && t == sec))) conf = true;
     }
     const unsigned long long stop = __ballot(act && (conf || resc));
     const int c = stop ? (__ffsll((long long)stop) - 1) : min(64, a.npts - b);
     if (c == 0) {
       // lane 0's point needs its whole window against the current bindings
       uint32_t dmp[8];
-      load_desc8(a.pdesc + 32 * (size_t)b, dmp);
+      load_desc8(a.pdesc + 32 * (size_t)(a.ids ? a.ids[b] : b), dmp);
       const PointWin w = a.cs.win[b];
-      uint32_t tk;
+      uint32_t tkey;
       int ti;
-      wave_topk<2>(a.C, w, dmp, s_taken, tk, ti);
-      const uint32_t k0 = __shfl((int)tk, 0, 64), k1 = __shfl((int)tk, 1, 64);
+      wave_topk<2>(a.C, w, dmp, s_taken, tkey, ti);
+      const uint32_t k0 = __shfl((int)tkey, 0, 64), k1 = __shfl((int)tkey, 1, 64);
       const int i0 = __shfl(ti, 0, 64), i1 = __shfl(ti, 1, 64);
       const int t0 = decide(a, k0 != kNoCand ? i0 : -1, k0 != kNoCand ? (int)(k0 >> 20) : 256,
                             k1 != kNoCand ? i1 : -1, k1 != kNoCand ? (int)(k1 >> 20) : 256);
-      if (t0 >= 0) {
-        if (lane == 0) {
-          s_taken[t0 >> 5] |= 1u << (t0 & 31);
-          a.match[t0] = b;
+      const bool tk0 = __shfl((int)tk, 0, 64) != 0;
+      if (lane == 0) {
+        if (t0 >= 0) {
+          if (tk0) s_taken[t0 >> 5] |= 1u << (t0 & 31);
+          atomicMax(&a.match[t0], b);
         }
-        nm++;
+        if (rot) s_evt[b] = (short)t0;
       }
+      if (t0 >= 0) nm++;
       b += 1;
       __syncthreads();
       continue;
     }
     const bool com = lane < c && tgt >= 0;
     if (com) {
-      atomicOr(&s_taken[tgt >> 5], 1u << (tgt & 31));
-      a.match[tgt] = i;
+      if (tk) atomicOr(&s_taken[tgt >> 5], 1u << (tgt & 31));
+      atomicMax(&a.match[tgt], i);
     }
+    if (rot && lane < c) s_evt[i] = (short)(com ? tgt : -1);
     nm += __popcll(__ballot(com));
     b += c;
     __syncthreads();
   }
-  if (a.mode == 0 && a.check_orientation) {
-    const float factor = 1.0f / HISTO_LENGTH;
-    for (int k = lane; k < n; k += 64) {
-      const int i = a.match[k];
-      if (i < 0) continue;
-      float rot = a.lkeys[i].angle - a.C.keys[k].angle;
-      if (rot < 0.0f) rot += 360.0f;
-      int bin = (int)roundf(rot * factor);
-      if (bin == HISTO_LENGTH) bin = 0;
-      atomicAdd(&s_hist[bin], 1);
+  if (rot) {
+    for (int i = lane; i < a.npts; i += 64) {
+      const int k = s_evt[i];
+      if (k >= 0) atomicAdd(&s_hist[rot_bin(a.lkeys[i].angle, a.C.keys[k].angle)], 1);
     }
     __syncthreads();
     if (lane == 0) {
@@ -592,24 +624,26 @@ __global__ __launch_bounds__(64) void k_match_greedy(GreedyArgs a) {
       s_ind[1] = ind2;
       s_ind[2] = ind3;
     }
+    // s_taken becomes the bitmap of keys an event in a rejected bin clears
+    for (int wd = lane; wd < nwords; wd += 64) s_taken[wd] = 0;
     __syncthreads();
     int removed = 0;
-    for (int k0 = 0; k0 < n; k0 += 64) {
-      const int k = k0 + lane;
+    for (int i0 = 0; i0 < a.npts; i0 += 64) {
+      const int i = i0 + lane;
       bool rm = false;
-      if (k < n) {
-        const int i = a.match[k];
-        if (i >= 0) {
-          float rot = a.lkeys[i].angle - a.C.keys[k].angle;
-          if (rot < 0.0f) rot += 360.0f;
-          int bin = (int)roundf(rot * factor);
-          if (bin == HISTO_LENGTH) bin = 0;
+      if (i < a.npts) {
+        const int k = s_evt[i];
+        if (k >= 0) {
+          const int bin = rot_bin(a.lkeys[i].angle, a.C.keys[k].angle);
           rm = bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2];
-          if (rm) a.match[k] = -1;
+          if (rm) atomicOr(&s_taken[k >> 5], 1u << (k & 31));
         }
       }
       removed += __popcll(__ballot(rm));
     }
+    __syncthreads();
+    for (int k = lane; k < n; k += 64)
+      if (key_taken(s_taken, k)) a.match[k] = -1;
     nm -= removed;
   }
   if (lane == 0) *a.nmatches = nm;
@@ -619,6 +653,8 @@ void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& 
                       int mono, int check_orientation, const CandSet& cs, int* match,
                       int* nmatches, hipStream_t st) {
   if (C.n > kMaxMatchKeys) throw ArgError("SearchByProjection: more than 16384 current keys");
+  if (check_orientation && L.n > kMaxMatchKeys)
+    throw ArgError("SearchByProjection: more than 16384 last-frame keys");
   SbpArgs a;
   a.C = C;
   a.L = L;
@@ -636,7 +672,9 @@ void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& 
   g.npts = L.n;
   g.cs = cs;
   g.pdesc = L.mp_desc;
+  g.ids = nullptr;
   g.taken_in = nullptr;
+  g.obs = L.obs;
   g.check_orientation = check_orientation;
   g.lkeys = L.keys;
   g.match = match;
@@ -648,7 +686,7 @@ void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& 
 void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointDev* pts,
                          const uint8_t* pdesc, int m, float th, const uint8_t* taken,
                          FrustumRec* fr, const CandSet& cs, int* match, int* nmatches,
-                         hipStream_t st) {
+                         hipStream_t st, const LocalSel* sel) {
   if (C.n > kMaxMatchKeys) throw ArgError("SearchByProjection: more than 16384 current keys");
   LocalArgs a;
   a.C = C;
@@ -659,6 +697,7 @@ void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointD
   a.th = th;
   a.fr = fr;
   a.cs = cs;
+  a.sel = sel ? *sel : LocalSel{nullptr, nullptr, nullptr};
   if (m > 0) {
     hipLaunchKernelGGL(k_local_cand, dim3((m + 3) / 4), dim3(256), 0, st, a);
     MMT_HIP(hipGetLastError());
@@ -669,12 +708,35 @@ void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointD
   g.npts = m;
   g.cs = cs;
   g.pdesc = pdesc;
+  g.ids = a.sel.ids;
   g.taken_in = taken;
+  g.obs = nullptr;
   g.check_orientation = 0;
   g.lkeys = nullptr;
   g.match = match;
   g.nmatches = nmatches;
   hipLaunchKernelGGL(k_match_greedy, dim3(1), dim3(64), 0, st, g);
+  MMT_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------ pool
+__global__ void k_pool_scatter(const PoolUpdate* __restrict__ up, int n, LocalPointDev* pool,
+                               uint8_t* pool_desc) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const PoolUpdate u = up[t];
+  pool[u.h] = u.p;
+  uint4* d = reinterpret_cast<uint4*>(pool_desc + 32 * (size_t)u.h);
+  const uint4* s = reinterpret_cast<const uint4*>(u.desc);
+  d[0] = s[0];
+  d[1] = s[1];
+}
+
+void launch_pool_scatter(const PoolUpdate* up, int n, LocalPointDev* pool, uint8_t* pool_desc,
+                         hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pool_scatter, dim3((n + 255) / 256), dim3(256), 0, st, up, n, pool,
+                     pool_desc);
   MMT_HIP(hipGetLastError());
 }
 

@@ -120,8 +120,11 @@ struct PoseOptDesc {
   float* pose_out;
   uint8_t* outlier;         // n: mvbOutlier
   int* n_inliers;
+  // n > kPoseOptMaxEdges: per-edge errors (3 n doubles) and flags (n ints) in global memory
+  double* e_scratch;
+  int* f_scratch;
 };
-constexpr int kPoseOptMaxEdges = 2048;
+constexpr int kPoseOptMaxEdges = 2048;  // edges whose state fits the kernel's LDS
 void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, hipStream_t st);
 
 }  // namespace mmt

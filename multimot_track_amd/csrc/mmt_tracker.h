@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "mmt_internal.h"
+#include "mmt_map.h"
 #include "mmt_pnp.h"
 #include "mmt_track.h"
 
@@ -29,6 +30,7 @@ struct FrameOut {
   float Tcw[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
   int n_keys = 0, n_obj_samples = 0, ego_iterations = 0, ego_inliers = 0;
   std::vector<ObjOut> objects;
+  MapStatsH map;
 };
 
 float rng_first_gaussian(uint64_t seed);
@@ -76,6 +78,11 @@ class Tracker {
     ObjSampleSet ob;
     HandoffSet ho;
     float Tcw[16];
+    // the frame's pose as its successor sees it (mLastFrame.mTcw): UpdateLastFrame resets it to
+    // Tlr * Tref (Tracking.cc:2900); the successor's flow solve, scene flow and object solves read
+    // it, while this frame's own object path keeps Tcw
+    float Tview[16];
+    MapFrameH m;  // Frame's map fields (mnId, mvpMapPoints, mvbOutlier, mpReferenceKF, keys)
     bool bSecond = false;  // bSecondFrame as of this frame (label association, B8)
     int obj_slot = -1;     // object-pipeline slot of this frame's D3 output (-1: none)
     std::vector<int> nModLabel, nSemPosition;
@@ -100,6 +107,8 @@ class Tracker {
     const mmt_kp* kps;
     const int* nkp;
     int n_keys;
+    int f;    // index in the chunk
+    int buf;  // host chunk buffer of the frame's map arrays
   };
   struct PnPBuf {
     float* pts3;
@@ -131,6 +140,24 @@ class Tracker {
 
   mmt_config cfg_{};
   OrbEngine* engine_ = nullptr;
+  // map tracking (ORB-SLAM2's TrackWithMotionModel / TrackLocalMap / keyframes), the frame grid
+  // (B3) of every chunk frame on the device and its host copy (two chunk buffers: the first frame
+  // of a chunk reads the last frame of the previous one)
+  MapEngine map_;
+  GridFrame grid0_{};  // camera, bounds and scales of every frame's GridFrame
+  float* d_uR_ = nullptr;
+  float* d_kdepth_ = nullptr;
+  int* d_cell_start_ = nullptr;
+  int* d_cell_idx_ = nullptr;
+  struct HostChunk {
+    mmt_kp* kps = nullptr;
+    uint8_t* desc = nullptr;
+    float* uR = nullptr;
+    float* kdepth = nullptr;
+  };
+  HostChunk hc_[2];
+  int chunk_buf_ = 0;
+  bool reset_pending_ = false;  // System::Reset requested (LOST with <= 5 keyframes)
   int W_ = 0, H_ = 0, max_chunk_ = 0, kcap_ = 0, ocap_ = 0, lm_cap_ = 0, mask_words_ = 0;
   float g0_ = 0;
   int state_ = 0, cur_ = 0, last_ = 2;

@@ -4,9 +4,8 @@
 // and Tracking::StereoInitialization (:2512-2570): every per-pixel / per-sample / per-edge stage
 // runs as HIP kernels (mmt_orb.hip, mmt_track.hip, mmt_pnp.hip); the host keeps the scalar
 // state machine -- poses, motion model, label bookkeeping (B8), per-object decisions -- exactly
-// where the reference keeps it.  Deviation: the ego *initial* pose comes from the
-// constant-velocity motion model instead of ORB-SLAM2's map tracking (MapPoints/KeyFrames/
-// vocabulary are not on this path yet).
+// where the reference keeps it.  The ego initial pose comes from ORB-SLAM2's map tracking
+// (mmt_map.hip: TrackWithMotionModel / TrackLocalMap / keyframes on GPU matchers and solves).
 
 #include <hip/hip_runtime.h>
 
@@ -18,6 +17,7 @@
 #include <vector>
 
 #include "mmt_internal.h"
+#include "mmt_map.h"
 #include "mmt_mat4.h"
 #include "mmt_pnp.h"
 #include "mmt_track.h"
@@ -124,6 +124,9 @@ Tracker::~Tracker() {
   if (eh_) (void)hipHostFree(eh_);
   for (ObjHost* h : oh_)
     if (h) (void)hipHostFree(h);
+  for (HostChunk& h : hc_)
+    for (void* p : {(void*)h.kps, (void*)h.desc, (void*)h.uR, (void*)h.kdepth})
+      if (p) (void)hipHostFree(p);
   for (int q = 0; q < kObjSlots; q++) {
     if (ev_ransac_[q]) (void)hipEventDestroy(ev_ransac_[q]);
     if (ev_d3_[q]) (void)hipEventDestroy(ev_d3_[q]);
@@ -244,6 +247,53 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     b.Rt = d_Rt_[q] + 12 * o;
   }
   }
+  // ---- map tracking: B3 grids of the chunk on the device, their host copies, the map engine
+  d_uR_ = alloc<float>((size_t)kcap_ * max_chunk);
+  d_kdepth_ = alloc<float>((size_t)kcap_ * max_chunk);
+  d_cell_start_ = alloc<int>((size_t)(kGridCells + 1) * max_chunk);
+  d_cell_idx_ = alloc<int>((size_t)kcap_ * max_chunk);
+  for (HostChunk& h : hc_) {
+    if (!h.kps) {
+      MMT_HIP(hipHostMalloc((void**)&h.kps, sizeof(mmt_kp) * (size_t)kcap_ * max_chunk,
+                            hipHostMallocDefault));
+      MMT_HIP(hipHostMalloc((void**)&h.desc, 32 * (size_t)kcap_ * max_chunk,
+                            hipHostMallocDefault));
+      MMT_HIP(hipHostMalloc((void**)&h.uR, sizeof(float) * (size_t)kcap_ * max_chunk,
+                            hipHostMallocDefault));
+      MMT_HIP(hipHostMalloc((void**)&h.kdepth, sizeof(float) * (size_t)kcap_ * max_chunk,
+                            hipHostMallocDefault));
+    }
+  }
+  {
+    OrbTables t;
+    t.init(cfg.orb_nfeatures, cfg.orb_scale_factor, cfg.orb_nlevels, cfg.orb_ini_th_fast,
+           cfg.orb_min_th_fast);
+    if (t.nlevels > kMaxLevels) throw ArgError("too many pyramid levels for the matchers");
+    MapCamH mc;
+    mc.W = W_;
+    mc.H = H_;
+    mc.fx = cfg.fx; mc.fy = cfg.fy; mc.cx = cfg.cx; mc.cy = cfg.cy; mc.bf = cfg.bf;
+    mc.invfx = 1.0f / cfg.fx;
+    mc.invfy = 1.0f / cfg.fy;
+    mc.thDepth = cfg.bf * cfg.th_depth / cfg.fx;  // mbf * (float)ThDepth / fx (Tracking.cc:225)
+    mc.maxFrames = (int)(cfg.fps == 0.f ? 30.f : cfg.fps);
+    mc.nlevels = t.nlevels;
+    mc.scale = t.scale;
+    mc.invSigma2 = t.invSigma2;
+    // mfLogScaleFactor = log(mfScaleFactor), as log in double rounded to float
+    mc.logScale = (float)std::log((double)t.scale[t.nlevels > 1 ? 1 : 0]);
+    map_.setup(mc, kcap_);
+    GridFrame& G = grid0_;
+    memset(&G, 0, sizeof(G));
+    G.fx = cfg.fx; G.fy = cfg.fy; G.cx = cfg.cx; G.cy = cfg.cy; G.bf = cfg.bf;
+    // Frame::ComputeImageBounds without distortion + grid element sizes (Frame.cc:581-584, 841)
+    G.minX = 0.0f; G.maxX = (float)W_; G.minY = 0.0f; G.maxY = (float)H_;
+    G.invW = static_cast<float>(kGridCols) / static_cast<float>(G.maxX - G.minX);
+    G.invH = static_cast<float>(kGridRows) / static_cast<float>(G.maxY - G.minY);
+    G.nlevels = t.nlevels;
+    for (int l = 0; l < t.nlevels; l++) G.scale[l] = t.scale[l];
+    G.logScale = mc.logScale;
+  }
   // The two object stages need hardware queues of their own (streams beyond the runtime's
   // GPU_MAX_HW_QUEUES share queues and serialise): the D3 stage, the longest chain, gets a
   // high-priority stream, which the runtime maps to a separate queue.
@@ -276,7 +326,11 @@ void Tracker::reset() {
     F.bSecond = false;
     F.obj_slot = -1;
     mat4_eye(F.Tcw);
+    mat4_eye(F.Tview);
+    F.m = MapFrameH();
   }
+  map_.reset();
+  reset_pending_ = false;
 }
 
 void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t* d_disp,
@@ -295,6 +349,20 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
                     d_depth_, npix, (int)npix, nframes, cfg_.bf, st);
   engine_->run(gray, nframes, gpitch, d_kps_, d_desc_, kcap_, d_nkp_, st);
   if (prof_) MMT_HIP(hipEventRecord(ev_orb_[1], st));
+  // B3 (ComputeStereoFromRGBD + AssignFeaturesToGrid) of every frame of the chunk, and the host
+  // copies the map bookkeeping reads (keys, descriptors, mvuRight, mvDepth)
+  launch_stereo_grid(d_kps_, d_nkp_, kcap_, d_depth_, npix, W_, H_, cfg_.bf, grid0_.invW,
+                     grid0_.invH, d_uR_, d_kdepth_, d_cell_start_, d_cell_idx_, nframes, st);
+  chunk_buf_ ^= 1;
+  const HostChunk& hc = hc_[chunk_buf_];
+  MMT_HIP(hipMemcpyAsync(hc.kps, d_kps_, sizeof(mmt_kp) * (size_t)kcap_ * nframes,
+                         hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(hc.desc, d_desc_, 32 * (size_t)kcap_ * nframes, hipMemcpyDeviceToHost,
+                         st));
+  MMT_HIP(hipMemcpyAsync(hc.uR, d_uR_, sizeof(float) * (size_t)kcap_ * nframes,
+                         hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(hc.kdepth, d_kdepth_, sizeof(float) * (size_t)kcap_ * nframes,
+                         hipMemcpyDeviceToHost, st));
   std::vector<int> nkp(nframes);
   MMT_HIP(hipMemcpyAsync(nkp.data(), d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));
   engine_->check_flags(st);  // synchronises st; throws on a tripped octree guard
@@ -317,8 +385,10 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
     a.kps = d_kps_ + (size_t)kcap_ * f;
     a.nkp = d_nkp_ + f;
     a.n_keys = nkp[f];
+    a.f = f;
+    a.buf = chunk_buf_;
+    obj_advance();  // the previous frame's object path, ahead of this frame's map tracking
     ego_launch(a, outs[f], st);
-    obj_advance();
     ego_finish(outs[f], st);
   }
   obj_flush();  // the chunk's results are complete on return
@@ -354,10 +424,27 @@ void Tracker::obj_flush() {
 }
 
 void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
+  if (reset_pending_) {  // System::TrackRGBD -> Tracking::Reset (System.cc:203-211)
+    map_.reset();
+    state_ = 0;
+    reset_pending_ = false;
+  }
   FrameSlot& C = slot_[cur_];
   FrameSlot& Ls = slot_[last_];
   out = FrameOut();
   out.n_keys = a.n_keys;
+  // ---- the Frame's map fields (Frame ctor: mnId, B3 arrays, empty mvpMapPoints)
+  {
+    const HostChunk& hc = hc_[a.buf];
+    MapFrameH& m = C.m;
+    m.id = map_.next_frame_id();
+    m.n = a.n_keys;
+    m.kps = hc.kps + (size_t)kcap_ * a.f;
+    m.desc = hc.desc + 32 * (size_t)kcap_ * a.f;
+    m.uR = hc.uR + (size_t)kcap_ * a.f;
+    m.depth = hc.kdepth + (size_t)kcap_ * a.f;
+    map_.prepare(m);
+  }
   C.nModLabel.clear();
   C.nSemPosition.clear();
   C.vObjMod.clear();
@@ -377,13 +464,28 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
     ego_pending_ = false;
     return;
   }
-  // ---- ego initial pose: motion model (deviation, see header)
-  if (hasVelocity_) {
-    mat4_mul(V_, Ls.Tcw, ego_Tinit_);
-    bSecondFrame_ = false;
-  } else {
-    memcpy(ego_Tinit_, Ls.Tcw, sizeof(ego_Tinit_));
-    bSecondFrame_ = true;
+  // ---- ORB-SLAM2 map tracking (Tracking.cc:985-1176): the initial pose of the flow solve; it
+  // may reset mLastFrame's pose (UpdateLastFrame), which the rest of this frame reads
+  {
+    GridFrame G = grid0_;
+    G.keys = a.kps;
+    G.desc = d_desc_ + 32 * (size_t)kcap_ * a.f;
+    G.uR = d_uR_ + (size_t)kcap_ * a.f;
+    G.cell_start = d_cell_start_ + (size_t)(kGridCells + 1) * a.f;
+    G.cell_idx = d_cell_idx_ + (size_t)kcap_ * a.f;
+    G.n = a.n_keys;
+    MapStatsH& ms = out.map;
+    const int rr = map_.track(C.m, G, ego_Tinit_, Ls.m, Ls.Tview, V_, hasVelocity_,
+                              bSecondFrame_, ms, st);
+    ms.state = map_.state();
+    ms.n_keyframes = map_.n_keyframes();
+    ms.n_mappoints = map_.n_mappoints();
+    memcpy(ms.Tcw_map, ego_Tinit_, sizeof(ego_Tinit_));
+    if (rr == 1) {  // LOST with <= 5 keyframes: mpSystem->Reset(); Track returns (:1165-1172)
+      reset_pending_ = true;
+      ego_pending_ = false;
+      return;
+    }
   }
   C.bSecond = bSecondFrame_;
   // ---- D2 (PoseOptimizationFlow2Cam)
@@ -394,7 +496,7 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   d2.obs = Ls.st.keys;  // mLastFrame.mvSiftKeys (= its own mvSiftKeysTmp)
   d2.flow = Ls.st.flow;
   d2.depth = Ls.st.depth;
-  memcpy(d2.Tcw_last, Ls.Tcw, sizeof(d2.Tcw_last));
+  memcpy(d2.Tcw_last, Ls.Tview, sizeof(d2.Tcw_last));
   memcpy(d2.init, ego_Tinit_, sizeof(d2.init));
   d2.rp_thres = 0.04f;
   d2.use_noise = 1;
@@ -419,15 +521,29 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
   MMT_HIP(hipStreamSynchronize(st));
   out.n_obj_samples = eh_->nlast_obj;
   bool advance = true;
+  if (reset_pending_) {
+    // the reset frame: Track returned after the map branch (no flow solve, no objects, and
+    // mLastFrame stays the previous frame)
+    memcpy(out.Tcw, ego_Tinit_, sizeof(out.Tcw));
+    out.initialized = false;
+    return;
+  }
   if (state_ == 0) {
     // ---- StereoInitialization (needs more than 500 keypoints)
     bFirstFrame_ = true;
     bSecondFrame_ = false;
     if (out.n_keys > 500) {
       mat4_eye(C.Tcw);
+      memcpy(C.Tview, C.Tcw, sizeof(C.Tview));
+      map_.initialize(C.m, C.Tcw);
+      map_.frame_done(C.m, C.Tcw);
       memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
       state_ = 1;
       out.initialized = true;
+      out.map.state = map_.state();
+      out.map.n_keyframes = map_.n_keyframes();
+      out.map.n_mappoints = map_.n_mappoints();
+      memcpy(out.map.Tcw_map, C.Tcw, sizeof(C.Tcw));
     } else {
       mat4_eye(out.Tcw);
       advance = false;  // the reference keeps its last frame until initialisation succeeds
@@ -440,11 +556,13 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
     out.ego_iterations = eh_->st[0];
     out.ego_inliers = eh_->st[1];
     float LastTwc[16];
-    inv_mat(Ls.Tcw, LastTwc);
+    inv_mat(Ls.Tview, LastTwc);  // mLastFrame's pose (Tracking.cc:1311-1317)
     mat4_mul(C.Tcw, LastTwc, V_);
     hasVelocity_ = true;
     memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
-    out.initialized = true;
+    out.initialized = map_.state() == 1;
+    map_.frame_done(C.m, C.Tcw);  // mlRelativeFramePoses (Tracking.cc:2481-2489)
+    memcpy(C.Tview, C.Tcw, sizeof(C.Tview));
     // queue the frame's object work (also when there are no object samples: its labels and
     // motions must be reset for the next frame, in pipeline order)
     qa_ = ObjFrame();
@@ -487,7 +605,7 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   g.last_depth = Ls.ob.depth;
   g.last_label = Ls.ob.label;
   memcpy(g.Tcur, C.Tcw, sizeof(g.Tcur));
-  memcpy(g.Tlast, Ls.Tcw, sizeof(g.Tlast));
+  memcpy(g.Tlast, Ls.Tview, sizeof(g.Tlast));
   g.fx = cfg_.fx; g.fy = cfg_.fy; g.cx = cfg_.cx; g.cy = cfg_.cy;
   g.W = W_;
   g.H = H_;
@@ -575,7 +693,7 @@ void Tracker::obj_stage_a(ObjFrame& F) {
     o.last_keys = Ls.ob.keys;
     o.last_depth = Ls.ob.depth;
     o.cur_keys = C.ho.okeys;
-    memcpy(o.Tlast, Ls.Tcw, sizeof(o.Tlast));
+    memcpy(o.Tlast, Ls.Tview, sizeof(o.Tlast));
     o.fx = cfg_.fx; o.fy = cfg_.fy; o.cx = cfg_.cx; o.cy = cfg_.cy;
     o.reproj = 0.3;
     o.confidence = 0.98;
@@ -629,7 +747,7 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     d.obs = Ls.ob.keys;
     d.flow = Ls.ob.flow;
     d.depth = Ls.ob.depth;
-    memcpy(d.Tcw_last, Ls.Tcw, sizeof(d.Tcw_last));
+    memcpy(d.Tcw_last, Ls.Tview, sizeof(d.Tcw_last));
     d.rp_thres = 0.01f;
     d.use_noise = 0;
     d.max_iters = 200;

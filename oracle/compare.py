@@ -13,7 +13,8 @@ FRAME_INT = ("initialized", "n_keys", "n_obj_samples", "ego_iterations", "ego_in
 OBJ_INT = ("label", "sem_label", "n_points", "ransac_inliers", "mm_inliers", "n_solve",
            "n_inliers", "iterations")
 OBJ_POSE = ("init", "X", "motion")
-MAP_INT = ("map_state", "map_matches_mm", "map_inliers_local", "n_keyframes", "n_mappoints")
+MAP_INT = ("map_state", "map_matches_mm", "map_inliers_local", "n_keyframes", "n_mappoints",
+           "new_keyframe")
 
 
 def compare_frame(g, o):

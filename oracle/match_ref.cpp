@@ -9,6 +9,7 @@
 // logf is within 0.52 ulp of that).
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 
@@ -54,6 +55,9 @@ void frame_stereo_grid(MatchFrame& F, const float* depth, int W, int H) {
 std::vector<int> features_in_area(const MatchFrame& F, float x, float y, float r, int minLevel,
                                   int maxLevel) {
   std::vector<int> out;
+  // a non-finite window centre (a map point unprojected from depth +inf) gives no cell: the
+  // reference's float -> int conversions are undefined there, x86 yields INT_MIN and an empty range
+  if (!std::isfinite(x) || !std::isfinite(y)) return out;
   const int nMinCellX = std::max(0, (int)std::floor((x - F.minX - r) * F.invW));
   if (nMinCellX >= kGridCols) return out;
   const int nMaxCellX = std::min(kGridCols - 1, (int)std::ceil((x - F.minX + r) * F.invW));
@@ -140,6 +144,7 @@ int search_by_projection_frame(const MatchFrame& C, const float* Tcw, const Last
   std::vector<int> rotHist[HISTO_LENGTH];
   const float factor = 1.0f / HISTO_LENGTH;
   for (int i = 0; i < C.n; i++) match[i] = -1;
+  std::vector<uint8_t> taken(C.n, 0);  // bound to a MapPoint with Observations() > 0
   float twc[3], tlc[3];
   centre(Tcw, twc);
   xform(L.Tcw, twc, tlc);
@@ -170,7 +175,7 @@ int search_by_projection_frame(const MatchFrame& C, const float* Tcw, const Last
     const uint8_t* dMP = L.mp_desc + 32 * (size_t)i;
     int bestDist = 256, bestIdx2 = -1;
     for (int i2 : idx2) {
-      if (match[i2] >= 0) continue;  // mvpMapPoints[i2] with Observations() > 0
+      if (taken[i2]) continue;  // mvpMapPoints[i2] with Observations() > 0
       if (C.uR[i2] > 0) {
         const float ur = u - C.bf * invzc;
         const float er = std::fabs(ur - C.uR[i2]);
@@ -184,6 +189,7 @@ int search_by_projection_frame(const MatchFrame& C, const float* Tcw, const Last
     }
     if (bestDist <= TH_HIGH) {
       match[bestIdx2] = i;
+      if (!L.obs || L.obs[i]) taken[bestIdx2] = 1;
       nmatches++;
       if (check_orientation) {
         float rot = L.keys[i].angle - C.keys[bestIdx2].angle;
@@ -235,7 +241,9 @@ bool is_in_frustum(const MatchFrame& F, const float* Tcw, const LocalPoint& p,
   if (viewCos < viewing_cos_limit) return false;
   // MapPoint::PredictScale (MapPoint.cc:402-417)
   const float ratio = p.max_dist / dist;
-  int nScale = (int)std::ceil(logf_pinned(ratio) / F.logScale);
+  // (int)ceil of a non-finite value (a NaN point): INT_MIN on x86, which clamps to level 0
+  const float ls = logf_pinned(ratio) / F.logScale;
+  int nScale = std::isfinite(ls) ? (int)std::ceil(ls) : INT_MIN;
   if (nScale < 0)
     nScale = 0;
   else if (nScale >= F.nlevels)

@@ -251,8 +251,8 @@ class Tracker:
         disp = np.ascontiguousarray(disp, np.uint16)
         flow = np.ascontiguousarray(flow, np.float32)
         mask = np.ascontiguousarray(mask, np.int32)
-        tcw = np.zeros(16, np.float32)
-        info = np.zeros(7, np.int32)
+        tcw = np.zeros(32, np.float32)
+        info = np.zeros(13, np.int32)
         oi = np.zeros((16, 8), np.int32)
         of = np.zeros((16, 51), np.float32)
         lib().oracle_tracker_track(self._h, _p(bgr), _p(disp), _p(flow), _p(mask), _p(tcw),
@@ -265,9 +265,12 @@ class Tracker:
                              iterations=int(oi[i, 7]), init=of[i, :16].reshape(4, 4),
                              X=of[i, 16:32].reshape(4, 4), motion=of[i, 32:48].reshape(4, 4),
                              centre_pre=of[i, 48:51].copy()))
-        return dict(initialized=bool(info[0]), Tcw=tcw.reshape(4, 4), n_keys=int(info[1]),
+        return dict(initialized=bool(info[0]), Tcw=tcw[:16].reshape(4, 4), n_keys=int(info[1]),
                     n_static=int(info[2]), n_obj_samples=int(info[3]), ego_iterations=int(info[4]),
-                    ego_inliers=int(info[5]), objects=objs)
+                    ego_inliers=int(info[5]), objects=objs, map_state=int(info[7]),
+                    map_matches_mm=int(info[8]), map_inliers_local=int(info[9]),
+                    n_keyframes=int(info[10]), n_mappoints=int(info[11]),
+                    new_keyframe=int(info[12]), Tcw_map=tcw[16:].reshape(4, 4).copy())
 
 
 # ---------------------------------------------------------------- B3 / C1-C3 (match_ref.cpp)
@@ -295,14 +298,15 @@ def frame_stereo_grid(kps, depth, K, bf):
 
 
 def search_by_projection_frame(kps, desc, depth, tcw, last_kps, Xw, mp_desc, active, tlw, th,
-                               K, bf, scale, mono=False, check_orientation=True):
+                               K, bf, scale, mono=False, check_orientation=True, obs=None):
     L = lib()
     vp = ctypes.c_void_p
     L.oracle_search_by_projection_frame.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int,
                                                     ctypes.c_int, vp, vp, ctypes.c_int, vp,
                                                     ctypes.c_int, vp, vp, vp, vp, vp,
                                                     ctypes.c_float, ctypes.c_int, ctypes.c_int,
-                                                    vp]
+                                                    vp, vp]
+    ob = None if obs is None else np.ascontiguousarray(obs, np.uint8)
     kps = np.ascontiguousarray(kps, KP_DTYPE)
     desc = np.ascontiguousarray(desc, np.uint8)
     depth = np.ascontiguousarray(depth, np.float32)
@@ -319,7 +323,8 @@ def search_by_projection_frame(kps, desc, depth, tcw, last_kps, Xw, mp_desc, act
     nm = L.oracle_search_by_projection_frame(len(kps), _p(kps), _p(desc), _p(depth), W, H,
                                              _p(cam), _p(sc), len(sc), _p(t), len(lk), _p(lk),
                                              _p(X), _p(md), _p(act), _p(tl), th, int(mono),
-                                             int(check_orientation), _p(match))
+                                             int(check_orientation), _p(match),
+                                             None if ob is None else _p(ob))
     return nm, match[:len(kps)]
 
 

@@ -248,8 +248,10 @@ void* oracle_tracker_create(int w, int h, float fx, float fy, float cx, float cy
 void oracle_tracker_destroy(void* t) { delete (OTracker*)t; }
 
 // Tracks one frame.  info: [initialized, n_keys, n_static, n_obj_samples, ego_iters,
-// ego_inliers, n_objects].  objs: per object 8 ints (label, sem, n_points, ransac_inliers,
-// mm_inliers, n_solve, n_inliers, iterations) + 51 floats (init, X, motion, centre_pre).
+// ego_inliers, n_objects, map_state, map_matches_mm, map_inliers_local, n_keyframes,
+// n_mappoints, new_keyframe].  tcw: 32 floats (the frame's pose, then the map branch's pose).
+// objs: per object 8 ints (label, sem, n_points, ransac_inliers, mm_inliers, n_solve, n_inliers,
+// iterations) + 51 floats (init, X, motion, centre_pre).
 int oracle_tracker_track(void* tp, const uint8_t* bgr, const uint16_t* disp, const float* flow,
                          const int32_t* mask, float* tcw, int* info, int* obj_i, float* obj_f,
                          int obj_cap) {
@@ -257,6 +259,13 @@ int oracle_tracker_track(void* tp, const uint8_t* bgr, const uint16_t* disp, con
   FrameResult r;
   t->track(bgr, disp, flow, mask, r);
   memcpy(tcw, r.Tcw, sizeof(r.Tcw));
+  memcpy(tcw + 16, r.map.Tcw_map, sizeof(r.map.Tcw_map));
+  info[7] = r.map.state;
+  info[8] = r.map.matches_mm;
+  info[9] = r.map.inliers_local;
+  info[10] = r.map.n_keyframes;
+  info[11] = r.map.n_mappoints;
+  info[12] = r.map.new_keyframe;
   info[0] = r.initialized;
   info[1] = r.n_keys;
   info[2] = r.n_static;
@@ -318,7 +327,7 @@ int oracle_search_by_projection_frame(int n2, const Key* keys2, const uint8_t* d
                                       const float* scale, int nlevels, const float* Tcw, int n1,
                                       const Key* keys1, const float* Xw, const uint8_t* mp_desc,
                                       const uint8_t* active, const float* Tlw, float th, int mono,
-                                      int check_orientation, int* match) {
+                                      int check_orientation, int* match, const uint8_t* obs) {
   MatchFrame C;
   match_frame(C, n2, keys2, desc2, depth, W, H, cam, scale, nlevels);
   LastFrameView L;
@@ -327,6 +336,7 @@ int oracle_search_by_projection_frame(int n2, const Key* keys2, const uint8_t* d
   L.Xw = Xw;
   L.mp_desc = mp_desc;
   L.active = active;
+  L.obs = obs;
   memcpy(L.Tcw, Tlw, sizeof(L.Tcw));
   return search_by_projection_frame(C, Tcw, L, th, mono != 0, check_orientation != 0, match);
 }

@@ -1,0 +1,192 @@
+// oracle/oracle_map.h -- TEST INFRASTRUCTURE ONLY (see orb_ref.cpp header).
+//
+// CPU restatement of ORB-SLAM2's map tracking as the reference runs it for RGB-D (the ego initial
+// pose that PoseOptimizationFlow2Cam starts from):
+//   MapPoint / KeyFrame / Map                    src/MapPoint.cc, src/KeyFrame.cc, src/Map.cc
+//   Tracking::StereoInitialization (map part)    src/Tracking.cc:2531-2575
+//   Tracking::Track, map branch                  src/Tracking.cc:985-1176
+//   CheckReplacedInLastFrame / UpdateLastFrame   src/Tracking.cc:2766-2781, 2894-2960
+//   TrackWithMotionModel / TrackReferenceKeyFrame src/Tracking.cc:2962-3187, 2836-2892
+//   TrackLocalMap / SearchLocalPoints / UpdateLocalMap / UpdateLocalKeyFrames / UpdateLocalPoints
+//                                                src/Tracking.cc:3189-3240, 3416-3612
+//   NeedNewKeyFrame / CreateNewKeyFrame          src/Tracking.cc:3243-3414
+//   LocalMapping::ProcessNewKeyFrame / MapPointCulling  src/LocalMapping.cc:131-208 (run
+//                                                synchronously after every new keyframe)
+// Pinned choices:
+//  * std::map / std::set keyed by KeyFrame* iterate in keyframe creation order (the reference's
+//    order is the heap's);
+//  * LocalMapping runs synchronously and is always idle when Tracking asks (AcceptKeyFrames);
+//    of its steps only ProcessNewKeyFrame (without the BoW conversion) and MapPointCulling run:
+//    CreateNewMapPoints needs the BoW vocabulary (missing), SearchInNeighbors / LocalBundleAdjustment
+//    / KeyFrameCulling are SURVEY 8(f)-3 and out of this row;
+//  * TrackReferenceKeyFrame's SearchByBoW (and Relocalization, whose candidates come from the BoW
+//    database) needs the missing vocabulary: both are replaced by SearchByProjection against the
+//    last frame at the last frame's pose (th 15, orientation check), then PoseOptimization and the
+//    reference's own acceptance tests;
+//  * map points whose unprojection is not finite (depth +inf where the disparity is 0) project to
+//    no pixel (the reference would index the grid with an undefined float -> int conversion).
+#pragma once
+#include <cstdint>
+#include <map>
+#include <set>
+#include <vector>
+
+#include "oracle_common.h"
+#include "oracle_match.h"
+
+namespace oracle {
+
+struct MapCam {
+  int W = 0, H = 0;
+  float fx = 0, fy = 0, cx = 0, cy = 0, invfx = 0, invfy = 0, bf = 0;
+  float thDepth = 0;  // mThDepth = mbf * ThDepth / fx (Tracking.cc:225)
+  int maxFrames = 0;  // mMaxFrames = fps (Tracking.cc:176)
+  int nlevels = 0;
+  float logScale = 0;
+  std::vector<float> scale, invSigma2;
+};
+
+struct OMapPoint {
+  float pos[3] = {0, 0, 0};
+  float normal[3] = {0, 0, 0};
+  uint8_t desc[32] = {0};
+  std::map<int, int> obs;  // mObservations: keyframe id -> key index
+  int nObs = 0;
+  int refKF = -1;
+  int firstKFid = -1;
+  long firstFrame = 0;
+  int visible = 1, found = 1;
+  bool bad = false;
+  float minDist = 0, maxDist = 0;
+  long trackRefForFrame = 0, lastFrameSeen = 0;
+  bool trackInView = false;
+};
+
+struct OKeyFrame {
+  int id = 0;
+  long frameId = 0;
+  float Tcw[16], Twc[16], Ow[3];
+  std::vector<Key> keys;
+  std::vector<float> uR, depth;
+  std::vector<uint8_t> desc;
+  std::vector<int> mps;  // mvpMapPoints (point handle or -1)
+  std::map<int, int> conn;  // mConnectedKeyFrameWeights
+  std::vector<int> ordered, orderedW;
+  bool firstConnection = true;
+  int parent = -1;
+  std::set<int> children;
+  long trackRefForFrame = 0;
+  bool bad = false;
+};
+
+// Map-path fields of one Frame (Frame.h): its keys and descriptors live in OFrame.
+struct MapFrame {
+  long id = 0;
+  std::vector<float> uR, depth;  // mvuRight, mvDepth (ComputeStereoFromRGBD)
+  std::vector<int> mps;          // mvpMapPoints
+  std::vector<uint8_t> outlier;  // mvbOutlier
+  int refKF = -1;                // mpReferenceKF
+};
+
+// What the parity tests compare besides the poses.
+struct MapStats {
+  int state = 0;            // 0 not initialised, 1 OK, 2 LOST
+  int matches_mm = -1;      // TrackWithMotionModel's nmatches before PoseOptimization (-1: not run)
+  int inliers_local = -1;   // mnMatchesInliers after TrackLocalMap (-1: not run)
+  int n_keyframes = 0, n_mappoints = 0;
+  int new_keyframe = 0;
+  float Tcw_map[16];        // pose after the map branch (the initial estimate of PoseOptimizationFlow2Cam)
+};
+
+class MapTracker {
+ public:
+  void init(const MapCam& cam);
+  // Tracking::Reset (map part): clears the map, keyframe and frame ids restart
+  void reset();
+  long next_frame_id() { return frameNextId_++; }
+  // mCurrentFrame's ComputeStereoFromRGBD + grid (Frame.cc:1041-1062, 601-616)
+  void prepare_frame(const std::vector<Key>& keys, const float* depth, MapFrame& F);
+  // StereoInitialization, map part (Tracking.cc:2531-2575): C has pose identity
+  void initialize(const std::vector<Key>& keys, const std::vector<uint8_t>& desc, MapFrame& C,
+                  const float* Tcw);
+  // Track()'s map branch (Tracking.cc:985-1176) for current frame C against last frame L.
+  // Tcw (in/out): the current pose; Tlast (in/out): mLastFrame.mTcw (UpdateLastFrame resets it).
+  // vel / has_vel: mVelocity (read; line 1122's update written).  bSecondFrame: the reference's
+  // flag (TrackReferenceKeyFrame sets it, TrackWithMotionModel clears it).  Returns 1 when the
+  // reference resets the system here (LOST with <= 5 keyframes: Track returns at line 1171).
+  int track(const std::vector<Key>& keys, const std::vector<uint8_t>& desc, MapFrame& C,
+            float* Tcw, const std::vector<Key>& lkeys, const std::vector<uint8_t>& ldesc,
+            MapFrame& L, float* Tlast, float* vel, bool& has_vel, bool& bSecondFrame,
+            MapStats& st);
+  // end of Track (Tracking.cc:2481-2489): mlRelativeFramePoses.push_back(Tcw * Tref^-1)
+  void frame_done(const MapFrame& C, const float* Tcw);
+  int state() const { return state_; }
+  int n_keyframes() const;
+  int n_mappoints() const;
+
+  // ---- everything below is the reference's state (public for the product parity probes)
+  MapCam cam;
+  std::vector<OMapPoint> pts;    // map points (handles 0..)
+  std::vector<OMapPoint> temps;  // temporal VO points (handles kTemp + i)
+  std::vector<OKeyFrame> kfs;
+  static constexpr int kTemp = 1 << 29;
+  OMapPoint& mp(int h) { return h >= kTemp ? temps[h - kTemp] : pts[h]; }
+
+ private:
+  bool track_with_motion_model(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                               MapFrame& C, float* Tcw, const std::vector<Key>& lkeys,
+                               const std::vector<uint8_t>& ldesc, MapFrame& L, float* Tlast,
+                               const float* vel, MapStats& st);
+  bool track_reference_subst(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                             MapFrame& C, float* Tcw, const std::vector<Key>& lkeys,
+                             const MapFrame& L, const float* Tlast);
+  bool track_local_map(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                       MapFrame& C, float* Tcw);
+  int search_frame(const std::vector<Key>& keys, const std::vector<uint8_t>& desc, MapFrame& C,
+                   const float* Tcw, const std::vector<Key>& lkeys, const MapFrame& L,
+                   const float* Tlast, float th);
+  int pose_optimization(const std::vector<Key>& keys, MapFrame& C, float* Tcw);
+  void update_local_keyframes(MapFrame& C);
+  void update_local_points(const MapFrame& C);
+  void search_local_points(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                           MapFrame& C, const float* Tcw);
+  bool need_new_keyframe(const MapFrame& C);
+  void create_new_keyframe(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                           MapFrame& C, const float* Tcw);
+  void process_new_keyframe(int kf);
+  void map_point_culling(int kf);
+  void update_last_frame(const std::vector<Key>& lkeys, const std::vector<uint8_t>& ldesc,
+                         MapFrame& L, float* Tlast);
+  int new_keyframe(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                   const MapFrame& C, const float* Tcw);
+  int new_point_kf(const float* pos, int kf);
+  void add_observation(int h, int kf, int idx);
+  void set_bad(int h);
+  void compute_distinctive(int h);
+  void update_normal_depth(int h);
+  void update_connections(int kf);
+  void add_connection(int kf, int other, int w);
+  void update_best_covisibles(int kf);
+  int tracked_map_points(int kf, int minObs);
+  void build_grid(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                  const MapFrame& C, MatchFrame& G);
+
+  int state_ = 0;
+  long frameNextId_ = 0;
+  int kfNextId_ = 0;
+  long lastKFFrameId_ = 0;  // mnLastKeyFrameId
+  int lastKF_ = -1;
+  int refKF_ = -1;          // mpReferenceKF
+  std::vector<int> localKFs_, localPts_;
+  std::vector<int> temporal_;  // mlpTemporalPoints
+  std::vector<int> recent_;    // LocalMapping::mlpRecentAddedMapPoints
+  float Tlr_[16];
+  bool hasTlr_ = false;
+  int matchesInliers_ = 0;     // mnMatchesInliers
+  bool mbVO_ = false;
+  long lastRelocFrameId_ = 0;
+  long curId_ = 0;
+  const float* depth_ = nullptr;
+};
+
+}  // namespace oracle

@@ -42,6 +42,10 @@ struct LastFrameView {
   const float* Xw = nullptr;       // n x 3 world position of mvpMapPoints[i]
   const uint8_t* mp_desc = nullptr;  // n x 32 descriptor of mvpMapPoints[i]
   const uint8_t* active = nullptr;   // mvpMapPoints[i] && !mvbOutlier[i]
+  // mvpMapPoints[i]->Observations() > 0 (null: every point has observations).  A current key
+  // bound to a point without observations (a temporal "visual odometry" point of UpdateLastFrame)
+  // stays open: a later point may bind it again (ORBmatcher.cc:2033-2035, 2058).
+  const uint8_t* obs = nullptr;
   float Tcw[16];
 };
 

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "oracle_common.h"
+#include "oracle_map.h"
 
 namespace oracle {
 
@@ -16,6 +17,8 @@ struct TrackParams {
   int width = 0, height = 0;
   float fx = 0, fy = 0, cx = 0, cy = 0, bf = 0;
   uint64_t noise_seed = 0;
+  float th_depth = 65.2f;  // ThDepth (kitti03.yaml:32)
+  float fps = 10.f;        // Camera.fps (kitti03.yaml:23)
 };
 
 // The parts of ORB_SLAM2::Frame this path reads (Frame.h of the reference).
@@ -35,6 +38,7 @@ struct OFrame {
   bool hasPose = false;
   std::vector<int> nModLabel, nSemPosition;
   std::vector<std::vector<float>> vObjMod;
+  MapFrame m;  // mnId, mvuRight, mvDepth, mvpMapPoints, mvbOutlier, mpReferenceKF
 };
 
 struct ObjectResult {
@@ -50,6 +54,7 @@ struct FrameResult {
   float Tcw[16] = {0};
   int n_keys = 0, n_static = 0, n_obj_samples = 0, ego_iterations = 0, ego_inliers = 0;
   std::vector<ObjectResult> objects;
+  MapStats map;  // the ORB-SLAM2 map branch that sets PoseOptimizationFlow2Cam's initial pose
 };
 
 void build_frame(const TrackParams& P, const OrbConfig& orb, const uint8_t* bgr,
@@ -64,6 +69,8 @@ class OTracker {
   OrbConfig orbc;
   int state = 0;
   bool bFirstFrame = false, bSecondFrame = false, hasVelocity = false;
+  bool reset_pending = false;  // System::Reset requested (LOST with <= 5 keyframes)
+  MapTracker map;
   float V[16] = {0};
   float g0 = 0;
   OFrame L;  // mLastFrame

@@ -9,11 +9,10 @@
 //                                           flow, B7 grouping, B8 labels, D5 + D3 per object,
 //                                           B9 last-frame hand-off)
 //   Tracking::StereoInitialization          src/Tracking.cc:2512-2570
-// Deviation: the ORB-SLAM2 map tracking that produces the ego *initial* pose
-// (TrackReferenceKeyFrame / TrackWithMotionModel + TrackLocalMap, needing MapPoints, KeyFrames,
-// LocalMapping and the missing ORB vocabulary) is replaced by its motion-model prediction
-// Tcw0 = V * Tcw_last (V empty -> Tcw_last), the pose ORB-SLAM2 itself seeds PoseOptimization
-// with.  Everything downstream of that initial pose follows the reference.
+// The ORB-SLAM2 map tracking that produces the ego initial pose (TrackWithMotionModel /
+// TrackReferenceKeyFrame + TrackLocalMap, the keyframe policy and a synchronous LocalMapping) is
+// oracle/map_ref.cpp; its pinned deviations (the BoW matcher of TrackReferenceKeyFrame and
+// Relocalization, LocalMapping's BoW / BA steps) are listed in oracle_map.h.
 
 #include <algorithm>
 #include <cmath>
@@ -135,15 +134,36 @@ void OTracker::init(const TrackParams& p, const OrbConfig& orb) {
   bSecondFrame = false;
   bFirstFrame = false;  // uninitialised in the reference (Tracking.h:180): pinned false
   hasVelocity = false;
+  reset_pending = false;
   g0 = cv_rng_first_gaussian(p.noise_seed);
+  MapCam mc;
+  mc.W = p.width;
+  mc.H = p.height;
+  mc.fx = p.fx; mc.fy = p.fy; mc.cx = p.cx; mc.cy = p.cy; mc.bf = p.bf;
+  mc.invfx = 1.0f / p.fx;
+  mc.invfy = 1.0f / p.fy;
+  mc.thDepth = p.bf * p.th_depth / p.fx;  // mbf * (float)ThDepth / fx (Tracking.cc:225)
+  mc.maxFrames = (int)(p.fps == 0 ? 30.f : p.fps);
+  mc.nlevels = orb.nlevels;
+  mc.scale = orb.scale;
+  mc.invSigma2 = orb.invSigma2;
+  mc.logScale = (float)std::log((double)orb.scale[orb.nlevels > 1 ? 1 : 0]);
+  map.init(mc);
 }
 
 // GrabImageRGBD + Track for one frame.  Returns 0 and fills `out`.
 int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
                     const int32_t* mask, FrameResult& out) {
   const int W = P.width, H = P.height;
+  if (reset_pending) {  // System::TrackRGBD -> Tracking::Reset (System.cc:203-211)
+    map.reset();
+    state = 0;
+    reset_pending = false;
+  }
   OFrame C;
   build_frame(P, orbc, bgr, disp, flow, mask, C);
+  C.m.id = map.next_frame_id();
+  map.prepare_frame(C.keys, C.depth.data(), C.m);
   std::vector<P2> mvTmpObjKeys;
   std::vector<float> mvTmpObjDepth;
   std::vector<int> mvTmpSemObjLabel;
@@ -192,6 +212,8 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
     if ((int)C.keys.size() > 500) {
       mat4_eye(C.Tcw);
       C.hasPose = true;
+      map.initialize(C.keys, C.desc, C.m, C.Tcw);
+      map.frame_done(C.m, C.Tcw);
       L = C;  // Frame copy + the own-sample hand-off of :2545-2549
       L.siftKeys = C.siftTmp;
       L.siftDepth = C.siftDepthTmp;
@@ -199,20 +221,33 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
     }
     memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
     out.initialized = state == 1;
+    out.map.state = map.state();
+    out.map.n_keyframes = map.n_keyframes();
+    out.map.n_mappoints = map.n_mappoints();
+    memcpy(out.map.Tcw_map, C.Tcw, sizeof(C.Tcw));
     return 0;
   }
 
-  // ---- ego initial pose (deviation: motion-model prediction, see header)
+  // ---- ORB-SLAM2 map tracking (Tracking.cc:985-1176): the initial pose of the flow solve.
+  // It may reset mLastFrame's pose (UpdateLastFrame), which everything below then reads.
   float Tinit[16];
-  if (hasVelocity) {
-    mat4_mul(V, L.Tcw, Tinit);
-    bSecondFrame = false;  // TrackWithMotionModel (Tracking.cc:2966-2967)
-  } else {
-    memcpy(Tinit, L.Tcw, sizeof(Tinit));
-    bSecondFrame = true;  // TrackReferenceKeyFrame (Tracking.cc:2839-2840)
+  {
+    MapStats& ms = out.map;
+    const int rr = map.track(C.keys, C.desc, C.m, Tinit, L.keys, L.desc, L.m, L.Tcw, V,
+                             hasVelocity, bSecondFrame, ms);
+    ms.state = map.state();
+    ms.n_keyframes = map.n_keyframes();
+    ms.n_mappoints = map.n_mappoints();
+    memcpy(ms.Tcw_map, Tinit, sizeof(Tinit));
+    memcpy(C.Tcw, Tinit, sizeof(Tinit));
+    C.hasPose = true;
+    if (rr == 1) {  // lost with <= 5 keyframes: mpSystem->Reset(); Track returns (Tracking.cc:1165-1172)
+      reset_pending = true;
+      memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
+      out.initialized = false;
+      return 0;
+    }
   }
-  memcpy(C.Tcw, Tinit, sizeof(Tinit));
-  C.hasPose = true;
 
   // ---- D2: PoseOptimizationFlow2Cam with identity temporal matches (Tracking.cc:1190-1307)
   {
@@ -479,7 +514,8 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
     out.objects.push_back(r);
   }
   memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
-  out.initialized = true;
+  out.initialized = map.state() == 1;
+  map.frame_done(C.m, C.Tcw);  // mlRelativeFramePoses (Tracking.cc:2481-2489)
 
   // ---- B9: last-frame hand-off (Tracking.cc:2463-2477)
   L = C;

@@ -95,6 +95,13 @@ def sbp_case(O, name, seed=0):
     elif name == "duplicates":   # 12 copies of each point: greedy conflicts and rescans
         li, ci, Tl, Tc = 0, 1, T[0], T[1]
         dup = 12
+    elif name == "vo_points":    # 40 % temporal VO points (no observations): keys they bind stay open
+        li, ci, Tl, Tc = 0, 1, T[0], T[1]
+    elif name == "vo_duplicates":  # copies alternating VO / mapped: rebinding events, cleared keys
+        li, ci, Tl, Tc = 0, 1, T[0], T[1]
+        dup = 6
+    elif name == "nan_points":   # points unprojected from depth +inf (NaN / inf coordinates)
+        li, ci, Tl, Tc = 0, 1, T[0], T[1]
     else:
         raise KeyError(name)
     lk, ld, ldep = frame(O, li)
@@ -105,9 +112,23 @@ def sbp_case(O, name, seed=0):
         sel = np.nonzero(active)[0][::7][:60]
         lk, Xw, md = np.repeat(lk[sel], dup), np.repeat(Xw[sel], dup, 0), np.repeat(md[sel], dup, 0)
         active = np.ones(len(lk), bool)
+    obs = None
+    if name == "vo_points":
+        obs = (rng.random(len(lk)) > 0.4).astype(np.uint8)
+    elif name == "vo_duplicates":
+        obs = (np.arange(len(lk)) % 2).astype(np.uint8)
+        # perturb some copies' angles so the rotation histogram rejects some events
+        lk = lk.copy()
+        lk["angle"][::5] = (lk["angle"][::5] + 97.0) % 360.0
+    elif name == "nan_points":
+        Xw = Xw.copy()
+        Xw[::11] = np.nan
+        Xw[5::13, 0] = np.inf
+        Xw[7::17, 2] = np.inf
+        active = active | (np.arange(len(lk)) % 11 == 0)
     return dict(kps=ck, desc=cd, depth=cdep, tcw=Tc, last_kps=lk, Xw=Xw, mp_desc=md,
                 active=active.astype(np.uint8), tlw=Tl, th=th, mono=mono,
-                check_orientation=check)
+                check_orientation=check, obs=obs)
 
 
 def local_case(O, name, seed=0):
@@ -147,5 +168,6 @@ def local_case(O, name, seed=0):
                 max_dist=dmax, pdesc=md, skip=skip, th=th, taken=taken)
 
 
-SBP_CASES = ["forward", "backward", "still", "mono_wide", "no_orientation", "duplicates"]
+SBP_CASES = ["forward", "backward", "still", "mono_wide", "no_orientation", "duplicates",
+             "vo_points", "vo_duplicates", "nan_points"]
 LOCAL_CASES = ["rgbd", "reloc_th5", "th1", "duplicates"]

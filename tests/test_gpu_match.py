@@ -52,10 +52,12 @@ def test_search_by_projection_frame_matches_oracle(ctx, oracle_mod, name):
     args = (c["kps"], c["desc"], c["depth"], c["tcw"], c["last_kps"], c["Xw"], c["mp_desc"],
             c["active"], c["tlw"], c["th"])
     nm, match = ctx.search_by_projection_frame(*args, mono=c["mono"],
-                                               check_orientation=c["check_orientation"])
+                                               check_orientation=c["check_orientation"],
+                                               obs=c["obs"])
     onm, omatch = oracle_mod.search_by_projection_frame(*args, MP.K, MP.BF,
                                                         MP.scale_factors(oracle_mod),
-                                                        c["mono"], c["check_orientation"])
+                                                        c["mono"], c["check_orientation"],
+                                                        obs=c["obs"])
     assert nm == onm
     assert np.array_equal(match, omatch), np.nonzero(match != omatch)[0][:10]
 
