@@ -103,12 +103,12 @@ static void check_match_frame(mmt_ctx* ctx, const mmt_match_frame* cur, bool nee
 
 struct DevCands {
   DevBuf<uint32_t> key;
-  DevBuf<int> idx, n;
+  DevBuf<int> idx, n, choice;
   DevBuf<mmt::PointWin> win;
   explicit DevCands(int m)
       : key((size_t)std::max(m, 1) * mmt::kCandK), idx((size_t)std::max(m, 1) * mmt::kCandK),
-        n(std::max(m, 1)), win(std::max(m, 1)) {}
-  mmt::CandSet set() { return mmt::CandSet{key.p, idx.p, n.p, win.p}; }
+        n(std::max(m, 1)), choice(std::max(m, 1)), win(std::max(m, 1)) {}
+  mmt::CandSet set() { return mmt::CandSet{key.p, idx.p, n.p, win.p, choice.p}; }
 };
 
 static thread_local std::string g_create_error;

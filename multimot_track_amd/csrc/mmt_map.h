@@ -184,6 +184,10 @@ class MapEngine {
   long curId_ = 0;
   int n_good_ = 0;  // non-bad map points
   hipStream_t s_ = nullptr;
+  // MMT_MAP_PROFILE=1: host wall time per stage of track(), printed to stderr at destruction
+  bool prof_on_ = false;
+  double prof_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long prof_n_ = 0;
 
   // device / pinned buffers
   std::vector<void*> dallocs_, hallocs_;

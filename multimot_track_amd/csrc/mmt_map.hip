@@ -7,7 +7,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -63,7 +66,27 @@ T* MapEngine::pinned(size_t n) {
   return p;
 }
 
+#define MAP_PROF(k, stmt)                       \
+  do {                                          \
+    const double _t0 = prof_on_ ? now_us() : 0; \
+    stmt;                                       \
+    if (prof_on_) prof_[k] += now_us() - _t0;   \
+  } while (0)
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 MapEngine::~MapEngine() {
+  if (prof_on_ && prof_n_ > 0) {
+    static const char* names[8] = {"C2 search", "D1 (motion model)", "local map update",
+                                   "C3 search", "D1 (local map)", "keyframe + mapping",
+                                   "other", "total"};
+    fprintf(stderr, "[mmt map profile] %ld frames, host wall us per frame:", prof_n_);
+    for (int k = 0; k < 8; k++) fprintf(stderr, " %s %.1f%s", names[k], prof_[k] / prof_n_,
+                                        k < 7 ? "," : "\n");
+  }
   if (s_) (void)hipStreamSynchronize(s_);
   for (void* p : dallocs_) (void)hipFree(p);
   for (void* p : hallocs_) (void)hipHostFree(p);
@@ -77,7 +100,7 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
   d_last_ = dev<uint8_t>(last_bytes(kcap));
   h_last_ = pinned<uint8_t>(last_bytes(kcap));
   c2_ = CandSet{dev<uint32_t>((size_t)kcap * kCandK), dev<int>((size_t)kcap * kCandK),
-                dev<int>(kcap), dev<PointWin>(kcap)};
+                dev<int>(kcap), dev<PointWin>(kcap), dev<int>(kcap)};
   d_match_ = dev<int>(kcap);
   d_nm_ = dev<int>(1);
   h_match_ = pinned<int>(kcap);
@@ -94,6 +117,7 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
   h_pose_ = pinned<float>(16);
   h_outl_ = pinned<uint8_t>(kcap);
   h_ninl_ = pinned<int>(1);
+  prof_on_ = getenv("MMT_MAP_PROFILE") != nullptr;
   frameNextId_ = 0;
   mbVO_ = false;
   matchesInliers_ = 0;
@@ -105,9 +129,10 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
 void MapEngine::grow_local(int m) {
   if (m <= local_cap_) return;
   const int cap = std::max(m + 4096, 2 * local_cap_);
-  void* old[] = {d_sel_, h_sel_, d_inview_, h_inview_, c3_.key, c3_.idx, c3_.n, c3_.win};
+  void* old[] = {d_sel_, h_sel_, d_inview_, h_inview_, c3_.key, c3_.idx, c3_.n, c3_.win,
+                 c3_.choice};
   if (s_) MMT_HIP(hipStreamSynchronize(s_));
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < 9; i++) {
     if (!old[i]) continue;
     auto it = std::find(i == 1 || i == 3 ? hallocs_.begin() : dallocs_.begin(),
                         i == 1 || i == 3 ? hallocs_.end() : dallocs_.end(), old[i]);
@@ -124,7 +149,7 @@ void MapEngine::grow_local(int m) {
   d_inview_ = dev<uint8_t>(cap);
   h_inview_ = pinned<uint8_t>(cap);
   c3_ = CandSet{dev<uint32_t>((size_t)cap * kCandK), dev<int>((size_t)cap * kCandK), dev<int>(cap),
-                dev<PointWin>(cap)};
+                dev<PointWin>(cap), dev<int>(cap)};
   local_cap_ = cap;
 }
 
@@ -621,14 +646,15 @@ bool MapEngine::track_with_motion_model(MapFrameH& C, const GridFrame& G, float*
   mat4_mul(vel, Tlast, Tcw);
   std::fill(C.mps.begin(), C.mps.end(), -1);
   const float th = 15;
-  int nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, th);
+  int nmatches;
+  MAP_PROF(0, nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, th));
   if (nmatches < 20) {
     std::fill(C.mps.begin(), C.mps.end(), -1);
-    nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, 2 * th);
+    MAP_PROF(0, nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, 2 * th));
   }
   st.matches_mm = nmatches;
   if (nmatches < 20) return false;
-  gpu_pose_opt(C, Tcw);
+  MAP_PROF(1, gpu_pose_opt(C, Tcw));
   int nmatchesMap = 0;
   discard_outliers(C, nmatches, &nmatchesMap);
   mbVO_ = nmatchesMap < 20;
@@ -769,10 +795,9 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
 }
 
 bool MapEngine::track_local_map(MapFrameH& C, const GridFrame& G, float* Tcw) {
-  update_local_keyframes(C);
-  update_local_points();
-  search_local_points(C, G, Tcw);
-  gpu_pose_opt(C, Tcw);
+  MAP_PROF(2, update_local_keyframes(C); update_local_points());
+  MAP_PROF(3, search_local_points(C, G, Tcw));
+  MAP_PROF(4, gpu_pose_opt(C, Tcw));
   matchesInliers_ = 0;
   for (int i = 0; i < C.n; i++) {
     if (C.mps[i] < 0 || C.outlier[i]) continue;
@@ -852,6 +877,7 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
                      hipStream_t s) {
   s_ = s;
   curId_ = C.id;
+  const double t_track = prof_on_ ? now_us() : 0;
   bool bOK;
   // CheckReplacedInLastFrame: no MapPoint is ever replaced on this path (no Fuse, no loops)
   if (state_ == 1) {
@@ -895,12 +921,18 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
     for (int i = 0; i < L.n; i++)  // delete temporal MapPoints (mLastFrame's become dangling)
       if (L.mps[i] >= kTemp) L.mps[i] = -1;
     temps_.clear();
-    if (need_new_keyframe(C)) {
+    MAP_PROF(5, if (need_new_keyframe(C)) {
       create_new_keyframe(C, Tcw);
       st.new_keyframe = 1;
-    }
+    });
     for (int i = 0; i < C.n; i++)
       if (C.mps[i] >= 0 && C.outlier[i]) C.mps[i] = -1;
+  }
+  if (prof_on_) {
+    prof_[7] += now_us() - t_track;
+    prof_[6] = prof_[7];
+    for (int k = 0; k < 6; k++) prof_[6] -= prof_[k];
+    prof_n_++;
   }
   if (state_ == 2 && n_keyframes() <= 5) return 1;  // mpSystem->Reset(); return
   if (C.refKF < 0) C.refKF = refKF_;

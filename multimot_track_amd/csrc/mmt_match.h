@@ -58,6 +58,7 @@ struct CandSet {
   int* idx;
   int* n;
   PointWin* win;
+  int* choice;  // per point: the binding the order-dependent pass settles on (scratch)
 };
 
 // B3 for nframes frames: keys/uR/kdepth/cell_idx at frame stride `cap`, cell_start at

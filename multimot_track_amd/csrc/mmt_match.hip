@@ -9,13 +9,12 @@
 //   k_local_cand    C3 candidates: Frame::isInFrustum (Frame.cc:652-708, PredictScale
 //                   MapPoint.cc:402-417) + ORBmatcher::SearchByProjection(Frame&,
 //                   vector<MapPoint*>, th) ORBmatcher.cc:418-502, one wave per local MapPoint.
-//   k_match_greedy  the order-dependent part of both matchers: a key bound by an earlier point is
-//                   skipped by later ones (`mvpMapPoints[i2]->Observations() > 0`).  One wave
-//                   replays the points in order, 64 at a time: every lane picks its best (and
-//                   second-best) unbound candidate from its sorted list, and the prefix of lanes
-//                   up to the first lane whose choice an earlier lane of the round takes away is
-//                   committed.  C2's rotation-consistency histogram (ComputeThreeMaxima,
-//                   ORBmatcher.cc:2236-2275) runs at the end.
+//   k_match_fix     the order-dependent part of both matchers: a key bound by an earlier point is
+//                   skipped by later ones (`mvpMapPoints[i2]->Observations() > 0`).  One
+//                   1024-thread workgroup iterates "each point's choice given the choices before
+//                   it" to its fixpoint, which is the sequential replay (see the kernel).  C2's
+//                   rotation-consistency histogram (ComputeThreeMaxima, ORBmatcher.cc:2236-2275)
+//                   runs at the end.
 // C1 (DescriptorDistance, ORBmatcher.cc:2279-2295) is the XOR + popcount of eight dwords.
 //
 // Each candidate is ranked by (distance, position in GetFeaturesInArea's order): the reference's
@@ -25,6 +24,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <climits>
 #include <cmath>
 
@@ -190,18 +190,18 @@ __device__ __forceinline__ bool window_cells(const GridFrame& G, float x, float 
   return true;
 }
 
-__device__ __forceinline__ bool key_taken(const uint32_t* bits, int k) {
-  return (bits[k >> 5] >> (k & 31)) & 1u;
-}
-
 // Wave-cooperative candidate scan of one window (uniform arguments): enumerates the keys in
 // GetFeaturesInArea order, applies the level / area / stereo filters (and `taken`, if given),
 // computes the Hamming distance to `dmp` and keeps the K smallest (dist << 20 | order) keys.
 // On return lanes 0..K-1 hold the sorted keys (kNoCand past the end) and key indices; the
 // return value is the number of candidates that passed the filters.
-template <int K>
+struct NoneTaken {
+  __device__ bool operator()(int) const { return false; }
+};
+
+template <int K, typename Taken>
 __device__ int wave_topk(const GridFrame& G, const PointWin& w, const uint32_t (&dmp)[8],
-                         const uint32_t* taken, uint32_t& top_key, int& top_idx) {
+                         const Taken& taken, uint32_t& top_key, int& top_idx) {
   const int lane = threadIdx.x & 63;
   top_key = kNoCand;
   top_idx = -1;
@@ -244,7 +244,7 @@ __device__ int wave_topk(const GridFrame& G, const PointWin& w, const uint32_t (
         if (w.maxLevel >= 0 && kp.octave > w.maxLevel) ok = false;
       }
       if (ok) ok = fabsf(kp.x - w.x) < w.r && fabsf(kp.y - w.y) < w.r;
-      if (ok && taken) ok = !key_taken(taken, k);
+      if (ok) ok = !taken(k);
       if (ok) {
         const float ukr = G.uR[k];
         if (ukr > 0 && fabsf(w.ur - ukr) > w.er) ok = false;
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void k_sbp_frame(SbpArgs a) {
   load_desc8(a.L.mp_desc + 32 * (size_t)i, dmp);
   uint32_t tk;
   int ti;
-  const int passed = wave_topk<kCandK>(C, w, dmp, nullptr, tk, ti);
+  const int passed = wave_topk<kCandK>(C, w, dmp, NoneTaken(), tk, ti);
   store_cands(a.cs, i, passed, tk, ti, w);
 }
 
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(256) void k_local_cand(LocalArgs a) {
   load_desc8(a.pdesc + 32 * (size_t)pj, dmp);
   uint32_t tk;
   int ti;
-  const int passed = wave_topk<kCandK>(C, w, dmp, nullptr, tk, ti);
+  const int passed = wave_topk<kCandK>(C, w, dmp, NoneTaken(), tk, ti);
   store_cands(a.cs, j, passed, tk, ti, w);
 }
 
@@ -492,114 +492,163 @@ __device__ __forceinline__ int rot_bin(float a_last, float a_cur) {
   return bin;
 }
 
-// Points bind in index order.  A binding by a point with observations takes its key for the
-// points after it; one by a point without (a temporal VO point) leaves the key open, and a later
-// point's binding replaces it (the key keeps the last binder; match[] is raised with atomicMax,
-// binders arrive in index order).  Every binding is an event of C2's rotation histogram; an event
-// in a rejected bin clears its key, whoever binds it last (ORBmatcher.cc:2087-2098).
-__global__ __launch_bounds__(64) void k_match_greedy(GreedyArgs a) {
-  __shared__ uint32_t s_taken[kMaxMatchKeys / 32];
-  __shared__ short s_evt[kMaxMatchKeys];  // C2: the key of point i's binding event (-1: none)
+// Points bind in index order: point i takes its best (C3: best + second-best) candidate among
+// the keys no earlier point has taken.  A binding by a point with observations takes its key for
+// the points after it; one by a point without (a temporal VO point) leaves the key open, and a
+// later point's binding replaces it (the key keeps the last binder).  Every binding is an event of
+// C2's rotation histogram; an event in a rejected bin clears its key, whoever binds it last
+// (ORBmatcher.cc:2087-2098).
+//
+// The sequential replay is the unique fixpoint of "every point's choice, given the choices of the
+// points before it", so one 1024-thread workgroup iterates that map in parallel rounds:
+//   1) owner[k] = the smallest index of a point whose current choice takes key k (LDS atomicMin;
+//      -1 for keys bound before the call),
+//   2) every point re-decides from its sorted candidates with "k taken" = owner[k] < i; a point
+//      whose unbound choices run past its kCandK candidates is rescanned over its whole window by
+//      a wave, with the same predicate,
+// until a round changes nothing.  After round r the first r points hold their sequential choice
+// (point 0 depends on nothing, point i only on points < i), so the loop ends within npts + 1
+// rounds; conflicts between neighbouring points are short chains and it ends in a few.
+constexpr int kFixThreads = 1024, kFixWaves = kFixThreads / 64, kFixResCap = 2048;
+
+__device__ __forceinline__ int fix_decide_from_cands(const GreedyArgs& a, int i, const int* owner,
+                                                     int cn, bool& resc) {
+  int best = -1, bestD = 256, sec = -1, secD = 256;
+  const int kk = min(cn, kCandK);
+  for (int e = 0; e < kk; e++) {
+    const int idx = a.cs.idx[(size_t)i * kCandK + e];
+    if (owner[idx] < i) continue;
+    const int d = (int)(a.cs.key[(size_t)i * kCandK + e] >> 20);
+    if (best < 0) {
+      best = idx;
+      bestD = d;
+      if (a.mode == 0) break;
+    } else {
+      sec = idx;
+      secD = d;
+      break;
+    }
+  }
+  resc = cn > kCandK && (best < 0 || (a.mode == 1 && sec < 0));
+  return resc ? -1 : decide(a, best, bestD, sec, secD);
+}
+
+struct OwnerTaken {
+  const int* owner;
+  int i;
+  __device__ bool operator()(int k) const { return owner[k] < i; }
+};
+
+__global__ __launch_bounds__(kFixThreads) void k_match_fix(GreedyArgs a) {
+  extern __shared__ int s_owner[];  // C.n keys
+  __shared__ int s_res[kFixResCap];
   __shared__ int s_hist[HISTO_LENGTH];
   __shared__ int s_ind[3];
-  const int lane = threadIdx.x;
-  const int n = a.C.n;
-  const int nwords = (n + 31) >> 5;
-  const bool rot = a.mode == 0 && a.check_orientation;
-  for (int wd = lane; wd < nwords; wd += 64) {
-    uint32_t bits = 0;
-    if (a.taken_in)
-      for (int b = 0; b < 32; b++) {
-        const int k = wd * 32 + b;
-        if (k < n && a.taken_in[k]) bits |= 1u << b;
-      }
-    s_taken[wd] = bits;
+  __shared__ int s_changed, s_nres, s_more, s_nm, s_removed;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = a.C.n, np = a.npts;
+  int* ch = a.cs.choice;
+  for (int k = tid; k < n; k += kFixThreads) {
+    s_owner[k] = (a.taken_in && a.taken_in[k]) ? -1 : INT_MAX;
+    a.match[k] = -1;
   }
-  for (int k = lane; k < n; k += 64) a.match[k] = -1;
-  if (rot)
-    for (int i = lane; i < a.npts; i += 64) s_evt[i] = -1;
-  if (lane < HISTO_LENGTH) s_hist[lane] = 0;
+  if (tid < HISTO_LENGTH) s_hist[tid] = 0;
+  for (int i = tid; i < np; i += kFixThreads) ch[i] = -1;
+  __syncthreads();
+  for (int round = 0; round <= np + 1; round++) {
+    if (tid == 0) {
+      s_changed = 0;
+      s_more = np;
+    }
+    if (round > 0) {
+      for (int i = tid; i < np; i += kFixThreads) {
+        const int c = ch[i];
+        if (c >= 0 && (!a.obs || a.obs[i])) atomicMin(&s_owner[c], i);
+      }
+    }
+    __syncthreads();
+    // re-decide every point; rescans are queued (in passes of kFixResCap points)
+    int from = 0;
+    for (;;) {
+      if (tid == 0) s_nres = 0;
+      __syncthreads();
+      int next = np;
+      for (int i = from + tid; i < np; i += kFixThreads) {
+        const int cn = a.cs.n[i];
+        if (cn <= 0) continue;
+        bool resc;
+        const int t = fix_decide_from_cands(a, i, s_owner, cn, resc);
+        if (resc) {
+          const int slot = atomicAdd(&s_nres, 1);
+          if (slot < kFixResCap) {
+            s_res[slot] = i;
+          } else {
+            next = min(next, i);  // no room: this point (and the ones after it) next pass
+          }
+          continue;
+        }
+        if (i >= next) continue;
+        if (t != ch[i]) {
+          ch[i] = t;
+          s_changed = 1;
+        }
+      }
+      // the pass covered points [from, cut): the smallest point that found no room starts the
+      // next pass (points past it are re-decided then)
+      if (next < np) atomicMin(&s_more, next);
+      __syncthreads();
+      const int cut = s_more;
+      const int nres = min(s_nres, kFixResCap);
+      for (int r = wave; r < nres; r += kFixWaves) {
+        const int i = s_res[r];
+        if (i >= cut) continue;  // wave-uniform
+        uint32_t dmp[8];
+        load_desc8(a.pdesc + 32 * (size_t)(a.ids ? a.ids[i] : i), dmp);
+        const PointWin w = a.cs.win[i];
+        uint32_t tkey;
+        int ti;
+        wave_topk<2>(a.C, w, dmp, OwnerTaken{s_owner, i}, tkey, ti);
+        const uint32_t k0 = __shfl((int)tkey, 0, 64), k1 = __shfl((int)tkey, 1, 64);
+        const int i0 = __shfl(ti, 0, 64), i1 = __shfl(ti, 1, 64);
+        const int t = decide(a, k0 != kNoCand ? i0 : -1, k0 != kNoCand ? (int)(k0 >> 20) : 256,
+                             k1 != kNoCand ? i1 : -1, k1 != kNoCand ? (int)(k1 >> 20) : 256);
+        if (lane == 0 && t != ch[i]) {
+          ch[i] = t;
+          s_changed = 1;
+        }
+      }
+      __syncthreads();
+      if (cut >= np) break;
+      from = cut;
+      __syncthreads();  // every thread has read s_more
+      if (tid == 0) s_more = np;
+    }
+    if (!s_changed && round > 0) break;
+    __syncthreads();  // every thread has read s_changed
+    for (int k = tid; k < n; k += kFixThreads)
+      if (s_owner[k] != -1) s_owner[k] = INT_MAX;
+    __syncthreads();
+  }
+  // ---- bindings: the key keeps its last binder; nmatches counts every binding
+  if (tid == 0) {
+    s_nm = 0;
+    s_removed = 0;
+  }
   __syncthreads();
   int nm = 0;
-  int b = 0;
-  while (b < a.npts) {
-    const int i = b + lane;
-    int best = -1, bestD = 256, sec = -1, secD = 256;
-    bool act = false, resc = false;
-    const bool tk = i < a.npts && (!a.obs || a.obs[i]);
-    if (i < a.npts) {
-      const int cn = a.cs.n[i];
-      if (cn > 0) {
-        act = true;
-        const int kk = min(cn, kCandK);
-        for (int e = 0; e < kk; e++) {
-          const int idx = a.cs.idx[(size_t)i * kCandK + e];
-          if (key_taken(s_taken, idx)) continue;
-          const int d = (int)(a.cs.key[(size_t)i * kCandK + e] >> 20);
-          if (best < 0) {
-            best = idx;
-            bestD = d;
-            if (a.mode == 0) break;
-          } else {
-            sec = idx;
-            secD = d;
-            break;
-          }
-        }
-        if (cn > kCandK && (best < 0 || (a.mode == 1 && sec < 0))) resc = true;
-      }
+  for (int i = tid; i < np; i += kFixThreads) {
+    const int c = ch[i];
+    if (c >= 0) {
+      atomicMax(&a.match[c], i);
+      nm++;
+      if (a.mode == 0 && a.check_orientation)
+        atomicAdd(&s_hist[rot_bin(a.lkeys[i].angle, a.C.keys[c].angle)], 1);
     }
-    const int tgt = (act && !resc) ? decide(a, best, bestD, sec, secD) : -1;
-    bool conf = false;
-    for (int l = 0; l < 63; l++) {
-      const int t = __shfl(tgt, l, 64);
-      const bool tl = __shfl((int)tk, l, 64) != 0;
-      if (l < lane && t >= 0 && tl && (t == best || (a.mode == 1 && t == sec))) conf = true;
-    }
-    const unsigned long long stop = __ballot(act && (conf || resc));
-    const int c = stop ? (__ffsll((long long)stop) - 1) : min(64, a.npts - b);
-    if (c == 0) {
-      // lane 0's point needs its whole window against the current bindings
-      uint32_t dmp[8];
-      load_desc8(a.pdesc + 32 * (size_t)(a.ids ? a.ids[b] : b), dmp);
-      const PointWin w = a.cs.win[b];
-      uint32_t tkey;
-      int ti;
-      wave_topk<2>(a.C, w, dmp, s_taken, tkey, ti);
-      const uint32_t k0 = __shfl((int)tkey, 0, 64), k1 = __shfl((int)tkey, 1, 64);
-      const int i0 = __shfl(ti, 0, 64), i1 = __shfl(ti, 1, 64);
-      const int t0 = decide(a, k0 != kNoCand ? i0 : -1, k0 != kNoCand ? (int)(k0 >> 20) : 256,
-                            k1 != kNoCand ? i1 : -1, k1 != kNoCand ? (int)(k1 >> 20) : 256);
-      const bool tk0 = __shfl((int)tk, 0, 64) != 0;
-      if (lane == 0) {
-        if (t0 >= 0) {
-          if (tk0) s_taken[t0 >> 5] |= 1u << (t0 & 31);
-          atomicMax(&a.match[t0], b);
-        }
-        if (rot) s_evt[b] = (short)t0;
-      }
-      if (t0 >= 0) nm++;
-      b += 1;
-      __syncthreads();
-      continue;
-    }
-    const bool com = lane < c && tgt >= 0;
-    if (com) {
-      if (tk) atomicOr(&s_taken[tgt >> 5], 1u << (tgt & 31));
-      atomicMax(&a.match[tgt], i);
-    }
-    if (rot && lane < c) s_evt[i] = (short)(com ? tgt : -1);
-    nm += __popcll(__ballot(com));
-    b += c;
-    __syncthreads();
   }
-  if (rot) {
-    for (int i = lane; i < a.npts; i += 64) {
-      const int k = s_evt[i];
-      if (k >= 0) atomicAdd(&s_hist[rot_bin(a.lkeys[i].angle, a.C.keys[k].angle)], 1);
-    }
-    __syncthreads();
-    if (lane == 0) {
+  atomicAdd(&s_nm, nm);
+  __syncthreads();
+  if (a.mode == 0 && a.check_orientation) {
+    if (tid == 0) {
       int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
       for (int h = 0; h < HISTO_LENGTH; h++) {
         const int s = s_hist[h];
@@ -624,29 +673,42 @@ __global__ __launch_bounds__(64) void k_match_greedy(GreedyArgs a) {
       s_ind[1] = ind2;
       s_ind[2] = ind3;
     }
-    // s_taken becomes the bitmap of keys an event in a rejected bin clears
-    for (int wd = lane; wd < nwords; wd += 64) s_taken[wd] = 0;
+    // s_owner becomes the flag of keys an event in a rejected bin clears
+    for (int k = tid; k < n; k += kFixThreads) s_owner[k] = 0;
     __syncthreads();
     int removed = 0;
-    for (int i0 = 0; i0 < a.npts; i0 += 64) {
-      const int i = i0 + lane;
-      bool rm = false;
-      if (i < a.npts) {
-        const int k = s_evt[i];
-        if (k >= 0) {
-          const int bin = rot_bin(a.lkeys[i].angle, a.C.keys[k].angle);
-          rm = bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2];
-          if (rm) atomicOr(&s_taken[k >> 5], 1u << (k & 31));
+    for (int i = tid; i < np; i += kFixThreads) {
+      const int k = ch[i];
+      if (k >= 0) {
+        const int bin = rot_bin(a.lkeys[i].angle, a.C.keys[k].angle);
+        if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
+          s_owner[k] = 1;
+          removed++;
         }
       }
-      removed += __popcll(__ballot(rm));
     }
+    atomicAdd(&s_removed, removed);
     __syncthreads();
-    for (int k = lane; k < n; k += 64)
-      if (key_taken(s_taken, k)) a.match[k] = -1;
-    nm -= removed;
+    for (int k = tid; k < n; k += kFixThreads)
+      if (s_owner[k]) a.match[k] = -1;
   }
-  if (lane == 0) *a.nmatches = nm;
+  if (tid == 0) *a.nmatches = s_nm - s_removed;
+}
+
+static void launch_match_fix(const GreedyArgs& g, hipStream_t st) {
+  // the owner table of kMaxMatchKeys keys needs 64 KB of dynamic LDS (once per device)
+  static std::atomic<uint64_t> attr_set{0};
+  int dev = 0;
+  MMT_HIP(hipGetDevice(&dev));
+  const uint64_t bit = 1ull << (dev & 63);
+  if (!(attr_set.load() & bit)) {
+    MMT_HIP(hipFuncSetAttribute((const void*)k_match_fix,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(int) * kMaxMatchKeys)));
+    attr_set.fetch_or(bit);
+  }
+  hipLaunchKernelGGL(k_match_fix, dim3(1), dim3(kFixThreads), sizeof(int) * (size_t)g.C.n, st, g);
+  MMT_HIP(hipGetLastError());
 }
 
 void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& L, float th,
@@ -679,8 +741,7 @@ void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& 
   g.lkeys = L.keys;
   g.match = match;
   g.nmatches = nmatches;
-  hipLaunchKernelGGL(k_match_greedy, dim3(1), dim3(64), 0, st, g);
-  MMT_HIP(hipGetLastError());
+  launch_match_fix(g, st);
 }
 
 void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointDev* pts,
@@ -715,8 +776,7 @@ void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointD
   g.lkeys = nullptr;
   g.match = match;
   g.nmatches = nmatches;
-  hipLaunchKernelGGL(k_match_greedy, dim3(1), dim3(64), 0, st, g);
-  MMT_HIP(hipGetLastError());
+  launch_match_fix(g, st);
 }
 
 // ------------------------------------------------------------------------------ pool

@@ -238,6 +238,10 @@ class Tracker {
   PnPObject* d_pnp_[kObjSlots] = {};
   PnPBuf pnp_[kObjSlots][kMaxObj];
   bool prof_ = false;
+  // MMT_MAP_PROFILE: host wall time per frame in obj_advance / ego_launch / ego_finish
+  bool hprof_ = false;
+  double hprof_us_[3] = {0, 0, 0};
+  long hprof_n_ = 0;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
   double orb_ms_ = 0;
   long long orb_launches_ = 0, orb_frames_ = 0;

@@ -14,6 +14,9 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "mmt_internal.h"
@@ -115,6 +118,10 @@ static T* dalloc(size_t n) {
 }
 
 Tracker::~Tracker() {
+  if (hprof_ && hprof_n_ > 0)
+    fprintf(stderr, "[mmt tracker profile] %ld frames, host wall us per frame: obj_advance %.1f, "
+            "ego_launch %.1f, ego_finish %.1f\n", hprof_n_, hprof_us_[0] / hprof_n_,
+            hprof_us_[1] / hprof_n_, hprof_us_[2] / hprof_n_);
   for (hipStream_t* q : {&oa_, &ob_})
     if (*q) {
       (void)hipStreamSynchronize(*q);
@@ -163,6 +170,7 @@ T* Tracker::alloc(size_t n) {
 
 void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   cfg_ = cfg;
+  hprof_ = getenv("MMT_MAP_PROFILE") != nullptr;
   engine_ = engine;
   W_ = cfg.width;
   H_ = cfg.height;
@@ -387,6 +395,23 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
     a.n_keys = nkp[f];
     a.f = f;
     a.buf = chunk_buf_;
+    if (hprof_) {
+      auto now = [] {
+        return std::chrono::duration<double, std::micro>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+      };
+      const double t0 = now();
+      obj_advance();
+      const double t1 = now();
+      ego_launch(a, outs[f], st);
+      const double t2 = now();
+      ego_finish(outs[f], st);
+      hprof_us_[0] += t1 - t0;
+      hprof_us_[1] += t2 - t1;
+      hprof_us_[2] += now() - t2;
+      hprof_n_++;
+      continue;
+    }
     obj_advance();  // the previous frame's object path, ahead of this frame's map tracking
     ego_launch(a, outs[f], st);
     ego_finish(outs[f], st);
