@@ -494,7 +494,7 @@ int mmt_pose_optimization(mmt_ctx* ctx, const mmt_pose_opt_problem* pr, float* p
     d.e_scratch = esc.p;
     d.f_scratch = fsc.p;
     MMT_HIP(hipMemcpyAsync(dd.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
-    mmt::launch_pose_opt(dd.p, 1, s);
+    mmt::launch_pose_opt(dd.p, 1, n, s);
     MMT_HIP(hipMemcpyAsync(pose_out, pose.p, 64, hipMemcpyDeviceToHost, s));
     if (n > 0) MMT_HIP(hipMemcpyAsync(outlier_out, outl.p, n, hipMemcpyDeviceToHost, s));
     MMT_HIP(hipMemcpyAsync(n_inliers, ninl.p, sizeof(int), hipMemcpyDeviceToHost, s));

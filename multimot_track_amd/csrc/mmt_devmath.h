@@ -357,16 +357,18 @@ __device__ inline void block_sum_t(const double (&v)[K], double* tile, double* p
 // registers.  Lane k of each wave sums column k, the wave partials meet in `part` (nw * K).
 // out[0..K) is visible to every thread on return.
 constexpr int kTileStride = 65;
+template <int STRIDE = kTileStride>
 __device__ __forceinline__ double* tile_row(double* tile) {
-  return tile + (size_t)(threadIdx.x >> 6) * 64 * kTileStride + (threadIdx.x & 63) * kTileStride;
+  return tile + (size_t)(threadIdx.x >> 6) * 64 * STRIDE + (threadIdx.x & 63) * STRIDE;
 }
 
-template <int K>
+// STRIDE >= K: row stride of the tile in doubles (odd: conflict-free row stores)
+template <int K, int STRIDE = kTileStride>
 __device__ inline void block_sum_tile(double* tile, double* part, double* out, int nw_active = 0) {
-  static_assert(K <= 64, "block_sum_tile: at most 64 values");
+  static_assert(K <= 64 && K <= STRIDE, "block_sum_tile: at most 64 values");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nw = nw_active > 0 ? nw_active : (int)(blockDim.x >> 6);
-  const double* t = tile + (size_t)wave * 64 * kTileStride;
+  const double* t = tile + (size_t)wave * 64 * STRIDE;
   // the rows are the wave's own: a wave-level LDS fence orders them before the column reads
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -378,7 +380,7 @@ __device__ inline void block_sum_tile(double* tile, double* part, double* out, i
     for (int r0 = 0; r0 < 64; r0 += 16) {
       double x[16];
 #pragma unroll
-      for (int j = 0; j < 16; j++) x[j] = t[(r0 + j) * kTileStride + lane];
+      for (int j = 0; j < 16; j++) x[j] = t[(r0 + j) * STRIDE + lane];
 #pragma unroll
       for (int j = 0; j < 16; j++) acc[j & 7] += x[j];
     }

@@ -1085,7 +1085,8 @@ __device__ __forceinline__ void po_linearise(const PoEdgeR& E, const DSE3& T, co
   }
 }
 
-__device__ __forceinline__ PoEdgeR po_load(const PoseOptDesc& D, const int* flags, int i) {
+__device__ __forceinline__ PoEdgeR po_load(const PoseOptDesc& D, const int* flags, int i,
+                                           int fl = 0) {
   PoEdgeR E;
   E.X[0] = D.Xw[3 * i];
   E.X[1] = D.Xw[3 * i + 1];
@@ -1094,7 +1095,7 @@ __device__ __forceinline__ PoEdgeR po_load(const PoseOptDesc& D, const int* flag
   E.obs[1] = D.obs[3 * i + 1];
   E.obs[2] = D.obs[3 * i + 2];
   E.s = D.inv_sigma2[i];
-  E.flags = flags[i];
+  E.flags = flags ? flags[i] : fl;
   return E;
 }
 
@@ -1239,29 +1240,294 @@ __device__ void pose_opt_body(const PoseOptDesc& D, int N, PoSmem& sm) {
   }
 }
 
+
+// The same solve with the edges in registers: kPoThreads threads, IT edges per thread (edge
+// tid + q * kPoThreads), their inputs, last errors and flags held for the whole solve, so a pass
+// issues no memory operation but the reduction.  8 waves keep two per SIMD in flight to hide
+// the FP64 dependency chains of one edge; the 28 sums meet by a butterfly reduce-scatter inside
+// each wave and one LDS exchange (block_sum).
+constexpr int kPoThreads = 512, kPoNone = 8;
+
+constexpr int kPoStride = 29;  // odd row stride of the reduction tile (28 sums)
+
+struct PoSmemR {
+  double tile[(kPoThreads / 64) * 64 * kPoStride];
+  double part[(kPoThreads / 64) * kPoSums];
+  double red[16 * 32];
+  double H[2][32];
+};
+
+// po_linearise for the register path: the edge's contribution goes straight into the thread's
+// row of the reduction tile (stored by its first edge, FIRST, accumulated by the others; an
+// outlier edge contributes zeros), so the 28 sums never occupy registers.
+template <bool FIRST>
+__device__ __forceinline__ void po_linearise_row(const PoEdgeR& E, const DSE3& T,
+                                                 const PoseOptDesc& D, double dM, double dS,
+                                                 double* eo, double* row) {
+  if (E.flags & kPoOutlier) {
+    if (FIRST)
+#pragma unroll
+      for (int k = 0; k < kPoSums; k++) row[k] = 0;
+    return;
+  }
+  double x, y, z, e[3];
+  po_err(E, T, D, e, x, y, z);
+  eo[0] = e[0];
+  eo[1] = e[1];
+  eo[2] = e[2];
+  const bool stereo = E.flags & kPoStereo;
+  const double c = po_chi2(E, e);
+  double r0 = c, r1 = 1.0;
+  if (E.flags & kPoRobust) {
+    const double d = stereo ? dS : dM;
+    huber(c, d * d, d, r0, r1);
+  }
+  row[0] = FIRST ? r0 : row[0] + r0;
+  const double invz = 1.0 / z, invz_2 = invz * invz;
+  double J[3][6];
+  J[0][0] = x * y * invz_2 * D.fx;
+  J[0][1] = -(1 + (x * x * invz_2)) * D.fx;
+  J[0][2] = y * invz * D.fx;
+  J[0][3] = -invz * D.fx;
+  J[0][4] = 0;
+  J[0][5] = x * invz_2 * D.fx;
+  J[1][0] = (1 + y * y * invz_2) * D.fy;
+  J[1][1] = -x * y * invz_2 * D.fy;
+  J[1][2] = -x * invz * D.fy;
+  J[1][3] = 0;
+  J[1][4] = -invz * D.fy;
+  J[1][5] = y * invz_2 * D.fy;
+  J[2][0] = J[0][0] - D.bf * y * invz_2;
+  J[2][1] = J[0][1] + D.bf * x * invz_2;
+  J[2][2] = J[0][2];
+  J[2][3] = J[0][3];
+  J[2][4] = 0;
+  J[2][5] = J[0][5] - D.bf * invz_2;
+  const double w = r1 * (double)E.s;
+  const double se0 = (double)E.s * e[0], se1 = (double)E.s * e[1], se2 = (double)E.s * e[2];
+  int k = 1;
+#pragma unroll
+  for (int a = 0; a < 6; a++)
+#pragma unroll
+    for (int b = 0; b <= a; b++) {
+      double acc = J[0][a] * w * J[0][b] + J[1][a] * w * J[1][b];
+      if (stereo) acc += J[2][a] * w * J[2][b];
+      row[k] = FIRST ? acc : row[k] + acc;
+      k++;
+    }
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+    double g = J[0][a] * se0 + J[1][a] * se1;
+    if (stereo) g += J[2][a] * se2;
+    row[22 + a] = FIRST ? -(r1 * g) : row[22 + a] - r1 * g;
+  }
+}
+
+template <int IT>
+__device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
+  const int tid = threadIdx.x, nw = kPoThreads >> 6;
+  const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
+  PoEdgeR Ed[IT];
+  double er[IT][3];
+#pragma unroll
+  for (int q = 0; q < IT; q++) {
+    const int i = tid + q * kPoThreads;
+    if (i < N) {
+      Ed[q] = po_load(D, nullptr, i, (D.obs[3 * i + 2] < 0 ? 0 : kPoStereo) | kPoRobust);
+    } else {
+      Ed[q] = PoEdgeR{};
+      Ed[q].flags = kPoNone | kPoOutlier;
+    }
+    er[q][0] = er[q][1] = er[q][2] = 0;
+  }
+  DSE3 P;
+  int nBad = 0;
+  double* row = tile_row<kPoStride>(sm.tile);
+#ifdef MMT_PO_PROFILE
+  long long pp[4] = {0, 0, 0, 0}, pt = clock64();
+#define PO_T(k)                     \
+  do {                              \
+    const long long _n = clock64(); \
+    pp[k] += _n - pt;               \
+    pt = _n;                        \
+  } while (0)
+#else
+#define PO_T(k) \
+  do {          \
+  } while (0)
+#endif
+  int npass = 0;
+  auto pass = [&](const DSE3& T, double* out) {
+    PO_T(0);
+    po_linearise_row<true>(Ed[0], T, D, dM, dS, er[0], row);
+#pragma unroll
+    for (int q = 1; q < IT; q++) po_linearise_row<false>(Ed[q], T, D, dM, dS, er[q], row);
+    PO_T(1);
+    block_sum_tile<kPoSums, kPoStride>(sm.tile, sm.part, out, nw);
+    PO_T(2);
+    npass++;
+  };
+  for (int it = 0; it < 4; it++) {
+    P = dse3_from_float(D.Tcw);  // every round restarts from the input pose
+    int hs = 0;
+    pass(P, sm.H[0]);
+    double cur = sm.H[0][0], lam, ni = 2, chk = 0;
+    {
+      double md = 0;
+#pragma unroll
+      for (int a = 0; a < 6; a++) md = fmax(md, fabs(sm.H[0][1 + a * (a + 3) / 2]));
+      lam = 1e-5 * md;
+    }
+    int nRaul = 0;
+    double xb[6] = {0, 0, 0, 0, 0, 0};
+    for (int iter = 0; iter < 10; iter++) {
+      const double ini = cur;
+      int qmax = 0;
+      bool bad = false;
+      for (;;) {
+        const double* Hc = sm.H[hs];
+        double A[21], bs[6];
+#pragma unroll
+        for (int q = 0; q < 21; q++) A[q] = Hc[1 + q];
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+          A[a * (a + 3) / 2] += lam;
+          bs[a] = Hc[22 + a];
+        }
+        const bool ok2 = ldlt6_packed(A, bs);
+#pragma unroll
+        for (int a = 0; a < 6; a++) xb[a] = ok2 ? bs[a] : xb[a];
+        const DSE3 PN = exp_mul(xb, P);
+        pass(PN, sm.H[hs ^ 1]);
+        const double* Ht = sm.H[hs ^ 1];
+        const double lastTrialChi = Ht[0];
+        const double tempChi = ok2 ? Ht[0] : DBL_MAX;
+        double scale = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++) scale += xb[a] * (lam * xb[a] + Hc[22 + a]);
+        scale += 1e-3;
+        const double rho = (cur - tempChi) / scale;
+        const bool accept = rho > 0 && isfinite(tempChi);
+        if (accept) {
+          const double t = 2 * rho - 1;
+          double alpha = 1. - t * t * t;
+          alpha = fmin(alpha, 2. / 3.);
+          lam = lam * fmax(1. / 3., alpha);
+          ni = 2;
+          cur = tempChi;
+          P = PN;
+          hs ^= 1;
+        } else {
+          lam = lam * ni;
+          ni = ni * 2;
+        }
+        qmax++;
+        const bool again = (rho < 0 && qmax < 10);
+        if (!again) {
+          bool ok = true;
+          if (qmax == 10 || rho == 0) ok = false;
+          if (ok) {
+            if ((ini - cur) * 1e3 < ini)
+              nRaul++;
+            else
+              nRaul = 0;
+            if (nRaul >= 3) ok = false;
+          }
+          if (chk < lastTrialChi && iter > 0) ok = false;
+          chk = lastTrialChi;
+          bad = !ok;
+          break;
+        }
+      }
+      if (bad) break;
+    }
+    // re-classification (Optimizer.cc:3266-3322), as pose_opt_body
+    double nb[1] = {0};
+#pragma unroll
+    for (int q = 0; q < IT; q++) {
+      if (Ed[q].flags & kPoNone) continue;
+      if (Ed[q].flags & kPoOutlier) {
+        double x, y, z;
+        po_err(Ed[q], P, D, er[q], x, y, z);
+      }
+      const double c = po_chi2(Ed[q], er[q]);
+      const float thr = (Ed[q].flags & kPoStereo) ? 7.815f : 5.991f;
+      int f = c > (double)thr ? (Ed[q].flags | kPoOutlier) : (Ed[q].flags & ~kPoOutlier);
+      nb[0] += (f & kPoOutlier) ? 1.0 : 0.0;
+      if (it == 2) f &= ~kPoRobust;
+      Ed[q].flags = f;
+    }
+    block_sum<1>(nb, sm.red, sm.H[0], nw);
+    nBad = (int)sm.H[0][0];
+    __syncthreads();  // sm.H[0] is rewritten by the next round's first reduction
+    if (N < 10) break;
+  }
+#pragma unroll
+  for (int q = 0; q < IT; q++) {
+    const int i = tid + q * kPoThreads;
+    if (i < N) D.outlier[i] = (Ed[q].flags & kPoOutlier) ? 1 : 0;
+  }
+  if (tid == 0) {
+    dse3_to_float(P, D.pose_out);
+    *D.n_inliers = N - nBad;
+#ifdef MMT_PO_PROFILE
+    printf("[po profile] N %d passes %d cycles: solve+ctl %lld linearise %lld reduce %lld\n", N,
+           npass, pp[0], pp[1], pp[2]);
+#endif
+  }
+#undef PO_T
+}
+
 }  // namespace
+
+__device__ __forceinline__ bool pose_opt_trivial(const PoseOptDesc& D, int N) {
+  if (N >= 3) return false;
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 16; k++) D.pose_out[k] = D.Tcw[k];
+    *D.n_inliers = 0;
+  }
+  for (int i = threadIdx.x; i < N; i += blockDim.x) D.outlier[i] = 0;
+  return true;
+}
 
 __global__ __launch_bounds__(256) void k_pose_opt(const PoseOptDesc* __restrict__ descs) {
   __shared__ PoSmem sm;
   const PoseOptDesc& D = descs[blockIdx.x];
   const int N = D.n;
-  const int nt = blockDim.x;
-  if (N < 3) {
-    if (threadIdx.x == 0) {
-      for (int k = 0; k < 16; k++) D.pose_out[k] = D.Tcw[k];
-      *D.n_inliers = 0;
-    }
-    for (int i = threadIdx.x; i < N; i += nt) D.outlier[i] = 0;
-    return;
-  }
+  if (pose_opt_trivial(D, N)) return;
   if (N <= kPoseOptMaxEdges)
     pose_opt_body<false>(D, N, sm);
   else
     pose_opt_body<true>(D, N, sm);
 }
 
-void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, hipStream_t st) {
-  hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs);
+template <int IT>
+__global__ __launch_bounds__(kPoThreads) void k_pose_opt_r(const PoseOptDesc* __restrict__ descs) {
+  __shared__ PoSmemR sm;
+  const PoseOptDesc& D = descs[blockIdx.x];
+  const int N = D.n;
+  if (pose_opt_trivial(D, N)) return;
+  if (N > IT * kPoThreads) {  // the host sized the launch for the largest solve
+    if (threadIdx.x == 0) *D.n_inliers = -1;
+    return;
+  }
+  pose_opt_reg<IT>(D, N, sm);
+}
+
+void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, int n_max, hipStream_t st) {
+  static const int variant = [] {  // MMT_PO_VARIANT=0: the LDS kernel for every size (A/B knob)
+    const char* e = getenv("MMT_PO_VARIANT");
+    return e ? atoi(e) : 1;
+  }();
+  if (variant && n_max <= kPoThreads)
+    hipLaunchKernelGGL(k_pose_opt_r<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
+  else if (variant && n_max <= 2 * kPoThreads)
+    hipLaunchKernelGGL(k_pose_opt_r<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
+  else if (variant && n_max <= 4 * kPoThreads)
+    hipLaunchKernelGGL(k_pose_opt_r<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
+  else
+    hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs);
+  MMT_HIP(hipGetLastError());
 }
 
 

@@ -117,10 +117,15 @@ class MapEngine {
   void prepare(MapFrameH& F) const;  // mvpMapPoints / mvbOutlier of a new frame
   // StereoInitialization's map part (Tracking.cc:2531-2575)
   void initialize(MapFrameH& C, const float* Tcw);
-  // Track()'s map branch (Tracking.cc:985-1176); G: the current frame on the device.  Returns 1
-  // when the reference resets the system (LOST with <= 5 keyframes, Tracking.cc:1165-1172).
+  // Track()'s map branch (Tracking.cc:985-1176) up to the pose: TrackWithMotionModel (or its
+  // substitute) and TrackLocalMap; G: the current frame on the device.  Returns 1 when the
+  // reference resets the system (LOST with <= 5 keyframes, Tracking.cc:1165-1172).
   int track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L, float* Tlast, float* vel,
             bool& has_vel, bool& bSecondFrame, MapStatsH& st, hipStream_t s);
+  // the rest of the branch, which the pose does not depend on: VO-match and temporal-point
+  // cleanup, NeedNewKeyFrame / CreateNewKeyFrame (Tracking.cc:1127-1160); host only, so it runs
+  // while the flow solve that starts from the pose is on the GPU
+  void track_finish(MapFrameH& C, MapFrameH& L, const float* Tcw, MapStatsH& st);
   // end of Track: mlRelativeFramePoses.push_back(Tcw * Tref^-1) (Tracking.cc:2481-2489)
   void frame_done(const MapFrameH& C, const float* Tcw);
   int state() const { return state_; }
@@ -180,6 +185,7 @@ class MapEngine {
   bool hasTlr_ = false;
   int matchesInliers_ = 0;
   bool mbVO_ = false;
+  bool pending_ok_ = false;  // track() succeeded, track_finish() pending
   long lastRelocFrameId_ = 0;
   long curId_ = 0;
   int n_good_ = 0;  // non-bad map points

@@ -490,7 +490,7 @@ int MapEngine::gpu_pose_opt(MapFrameH& C, float* Tcw) {
     MMT_HIP(hipMemcpyAsync(d_edges_, h_edges_, sizeof(float) * 7 * (size_t)n,
                            hipMemcpyHostToDevice, s_));
   MMT_HIP(hipMemcpyAsync(d_pod_, h_pod_, sizeof(PoseOptDesc), hipMemcpyHostToDevice, s_));
-  launch_pose_opt(d_pod_, 1, s_);
+  launch_pose_opt(d_pod_, 1, n, s_);
   MMT_HIP(hipMemcpyAsync(h_pose_, d_pose_, 64, hipMemcpyDeviceToHost, s_));
   if (n > 0) MMT_HIP(hipMemcpyAsync(h_outl_, d_outl_, (size_t)n, hipMemcpyDeviceToHost, s_));
   MMT_HIP(hipMemcpyAsync(h_ninl_, d_ninl_, sizeof(int), hipMemcpyDeviceToHost, s_));
@@ -913,6 +913,19 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
     }
     mat4_mul(Tcw, LastTwc, vel);
     has_vel = true;
+  }
+  pending_ok_ = bOK;
+  if (prof_on_) {
+    prof_[7] += now_us() - t_track;
+    prof_n_++;
+  }
+  if (state_ == 2 && n_keyframes() <= 5) return 1;  // mpSystem->Reset(); return
+  return 0;
+}
+
+void MapEngine::track_finish(MapFrameH& C, MapFrameH& L, const float* Tcw, MapStatsH& st) {
+  const double t0 = prof_on_ ? now_us() : 0;
+  if (pending_ok_) {
     for (int i = 0; i < C.n; i++)  // clean VO matches
       if (C.mps[i] >= 0 && mp(C.mps[i]).nObs < 1) {
         C.outlier[i] = 0;
@@ -928,15 +941,13 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
     for (int i = 0; i < C.n; i++)
       if (C.mps[i] >= 0 && C.outlier[i]) C.mps[i] = -1;
   }
+  pending_ok_ = false;
+  if (C.refKF < 0) C.refKF = refKF_;
   if (prof_on_) {
-    prof_[7] += now_us() - t_track;
+    prof_[7] += now_us() - t0;
     prof_[6] = prof_[7];
     for (int k = 0; k < 6; k++) prof_[6] -= prof_[k];
-    prof_n_++;
   }
-  if (state_ == 2 && n_keyframes() <= 5) return 1;  // mpSystem->Reset(); return
-  if (C.refKF < 0) C.refKF = refKF_;
-  return 0;
 }
 
 }  // namespace mmt

@@ -125,6 +125,6 @@ struct PoseOptDesc {
   int* f_scratch;
 };
 constexpr int kPoseOptMaxEdges = 2048;  // edges whose state fits the kernel's LDS
-void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, hipStream_t st);
+void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, int n_max, hipStream_t st);
 
 }  // namespace mmt

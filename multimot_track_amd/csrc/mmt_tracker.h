@@ -131,6 +131,7 @@ class Tracker {
   // ego part of a frame: samples, hand-off, D2 launched on `st` (no wait)
   void ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st);
   // waits for the ego solve, updates the motion model, queues the frame's object path
+  void ego_map_finish(FrameOut& out);
   void ego_finish(FrameOut& out, hipStream_t st);
   void obj_stage_a(ObjFrame& F);    // grouping + B7/B8 + PnP-RANSAC launch (stream oa_)
   void obj_stage_b(ObjFrame& F);    // MM matrix, MM check, model choice, D3 (stream ob_, no wait)
@@ -238,6 +239,7 @@ class Tracker {
   PnPObject* d_pnp_[kObjSlots] = {};
   PnPBuf pnp_[kObjSlots][kMaxObj];
   bool prof_ = false;
+  bool map_finish_pending_ = false;
   // MMT_MAP_PROFILE: host wall time per frame in obj_advance / ego_launch / ego_finish
   bool hprof_ = false;
   double hprof_us_[3] = {0, 0, 0};

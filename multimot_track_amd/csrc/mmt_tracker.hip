@@ -119,7 +119,7 @@ static T* dalloc(size_t n) {
 
 Tracker::~Tracker() {
   if (hprof_ && hprof_n_ > 0)
-    fprintf(stderr, "[mmt tracker profile] %ld frames, host wall us per frame: obj_advance %.1f, "
+    fprintf(stderr, "[mmt tracker profile] %ld frames, host wall us per frame: map finish + obj_advance %.1f, "
             "ego_launch %.1f, ego_finish %.1f\n", hprof_n_, hprof_us_[0] / hprof_n_,
             hprof_us_[1] / hprof_n_, hprof_us_[2] / hprof_n_);
   for (hipStream_t* q : {&oa_, &ob_})
@@ -401,19 +401,23 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
                    std::chrono::steady_clock::now().time_since_epoch()).count();
       };
       const double t0 = now();
-      obj_advance();
-      const double t1 = now();
       ego_launch(a, outs[f], st);
+      const double t1 = now();
+      ego_map_finish(outs[f]);
+      obj_advance();
       const double t2 = now();
       ego_finish(outs[f], st);
-      hprof_us_[0] += t1 - t0;
-      hprof_us_[1] += t2 - t1;
+      hprof_us_[0] += t2 - t1;
+      hprof_us_[1] += t1 - t0;
       hprof_us_[2] += now() - t2;
       hprof_n_++;
       continue;
     }
-    obj_advance();  // the previous frame's object path, ahead of this frame's map tracking
+    // frame f's map branch up to its pose, then its flow solve (D2) on the GPU; while D2 runs the
+    // host finishes the map branch (keyframes) and drives frame f-1's object path
     ego_launch(a, outs[f], st);
+    ego_map_finish(outs[f]);
+    obj_advance();
     ego_finish(outs[f], st);
   }
   obj_flush();  // the chunk's results are complete on return
@@ -503,14 +507,15 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
     const int rr = map_.track(C.m, G, ego_Tinit_, Ls.m, Ls.Tview, V_, hasVelocity_,
                               bSecondFrame_, ms, st);
     ms.state = map_.state();
-    ms.n_keyframes = map_.n_keyframes();
-    ms.n_mappoints = map_.n_mappoints();
     memcpy(ms.Tcw_map, ego_Tinit_, sizeof(ego_Tinit_));
     if (rr == 1) {  // LOST with <= 5 keyframes: mpSystem->Reset(); Track returns (:1165-1172)
+      ms.n_keyframes = map_.n_keyframes();
+      ms.n_mappoints = map_.n_mappoints();
       reset_pending_ = true;
       ego_pending_ = false;
       return;
     }
+    map_finish_pending_ = true;
   }
   C.bSecond = bSecondFrame_;
   // ---- D2 (PoseOptimizationFlow2Cam)
@@ -538,6 +543,17 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   MMT_HIP(hipMemcpyAsync(eh_->Tcw, d_poses_, sizeof(eh_->Tcw), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(eh_->st, d_lmstats_, sizeof(eh_->st), hipMemcpyDeviceToHost, st));
   ego_pending_ = true;
+}
+
+// The map branch's host-only tail (keyframe decision and creation) while D2 runs on the GPU.
+void Tracker::ego_map_finish(FrameOut& out) {
+  if (!map_finish_pending_) return;
+  map_finish_pending_ = false;
+  FrameSlot& C = slot_[cur_];
+  FrameSlot& Ls = slot_[last_];
+  map_.track_finish(C.m, Ls.m, ego_Tinit_, out.map);
+  out.map.n_keyframes = map_.n_keyframes();
+  out.map.n_mappoints = map_.n_mappoints();
 }
 
 void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
