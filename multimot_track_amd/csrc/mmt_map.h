@@ -181,6 +181,7 @@ class MapEngine {
   long lastKFFrameId_ = 0;
   int refKF_ = -1;
   std::vector<int> localKFs_, localPts_, recent_, dirty_;
+  std::vector<std::pair<float, int>> far_;  // UpdateLastFrame's far keys (scratch)
   float Tlr_[16];
   bool hasTlr_ = false;
   int matchesInliers_ = 0;
@@ -192,8 +193,9 @@ class MapEngine {
   hipStream_t s_ = nullptr;
   // MMT_MAP_PROFILE=1: host wall time per stage of track(), printed to stderr at destruction
   bool prof_on_ = false;
-  double prof_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double prof_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   long prof_n_ = 0;
+  double prof_cnt_[4] = {0, 0, 0, 0};
 
   // device / pinned buffers
   std::vector<void*> dallocs_, hallocs_;

@@ -80,12 +80,17 @@ static double now_us() {
 
 MapEngine::~MapEngine() {
   if (prof_on_ && prof_n_ > 0) {
-    static const char* names[8] = {"C2 search", "D1 (motion model)", "local map update",
-                                   "C3 search", "D1 (local map)", "keyframe + mapping",
-                                   "other", "total"};
+    static const char* names[12] = {"C2 search", "D1 (motion model)", "local map update",
+                                    "C3 search", "D1 (local map)", "keyframe + mapping",
+                                    "other", "total", "UpdateLastFrame", "C2 pack",
+                                    "C3 pack", "D1 pack"};
     fprintf(stderr, "[mmt map profile] %ld frames, host wall us per frame:", prof_n_);
-    for (int k = 0; k < 8; k++) fprintf(stderr, " %s %.1f%s", names[k], prof_[k] / prof_n_,
-                                        k < 7 ? "," : "\n");
+    for (int k = 0; k < 12; k++) fprintf(stderr, " %s %.1f%s", names[k], prof_[k] / prof_n_,
+                                         k < 11 ? "," : "\n");
+    fprintf(stderr, "[mmt map profile] per frame: %.1f local keyframes, %.1f local points, "
+            "%.1f C3 edges; %zu map points allocated, %d keyframes at the end\n",
+            prof_cnt_[0] / prof_n_, prof_cnt_[1] / prof_n_, prof_cnt_[2] / prof_n_, pts_.size(),
+            n_keyframes());
   }
   if (s_) (void)hipStreamSynchronize(s_);
   for (void* p : dallocs_) (void)hipFree(p);
@@ -416,6 +421,7 @@ void MapEngine::map_point_culling(int kf) {  // LocalMapping::MapPointCulling (R
 // ------------------------------------------------------------------ GPU stages
 int MapEngine::gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* Tcw,
                                 const MapFrameH& L, const float* Tlast, float th) {
+  const double t_pack = prof_on_ ? now_us() : 0;
   // SearchByProjection(CurrentFrame, LastFrame, th, bMono=false) with mbCheckOrientation
   const int n1 = L.n;
   uint8_t* hk = h_last_;
@@ -435,6 +441,7 @@ int MapEngine::gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* T
       hO[i] = p.nObs > 0;
     }
   }
+  if (prof_on_) prof_[9] += now_us() - t_pack;
   MMT_HIP(hipMemcpyAsync(d_last_, h_last_, last_bytes(n1), hipMemcpyHostToDevice, s_));
   LastFrameDev LD;
   LD.keys = (const mmt_kp*)d_last_;
@@ -454,6 +461,7 @@ int MapEngine::gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* T
 }
 
 int MapEngine::gpu_pose_opt(MapFrameH& C, float* Tcw) {
+  const double t_pack = prof_on_ ? now_us() : 0;
   // Optimizer::PoseOptimization(&mCurrentFrame): the frame's MapPoints in key order
   std::vector<int> idx;
   idx.reserve(C.n);
@@ -473,6 +481,7 @@ int MapEngine::gpu_pose_opt(MapFrameH& C, float* Tcw) {
     s2[e] = cam_.invSigma2[C.kps[i].octave];
     C.outlier[i] = 0;
   }
+  if (prof_on_) prof_[11] += now_us() - t_pack;
   PoseOptDesc& d = *h_pod_;
   memset(&d, 0, sizeof(d));
   d.n = n;
@@ -599,15 +608,12 @@ void MapEngine::frame_done(const MapFrameH& C, const float* Tcw) {
 void MapEngine::update_last_frame(MapFrameH& L, float* Tlast) {  // Tracking.cc:2894-2960
   if (L.refKF >= 0 && hasTlr_) mat4_mul(Tlr_, kfs_[L.refKF].Tcw, Tlast);
   if (lastKFFrameId_ == L.id) return;
-  std::vector<std::pair<float, int>> v;
-  v.reserve(L.n);
-  for (int i = 0; i < L.n; i++)
-    if (L.depth[i] > 0) v.push_back({L.depth[i], i});
-  if (v.empty()) return;
-  std::sort(v.begin(), v.end());
-  int nPoints = 0;
-  for (size_t j = 0; j < v.size(); j++) {
-    const int i = v[j].second;
+  // The reference sorts (depth, index) and walks the prefix up to the first point that is both
+  // beyond thDepth and past the 200th: that prefix is every close point plus the nearest far one,
+  // or the 201 nearest points when fewer than 200 are close.  The temporary points are identities
+  // only (C2 reads them by key index, they die with the frame), so the set is selected in O(n)
+  // instead of sorting the keys.
+  auto make = [&](int i) {
     if (L.mps[i] < 0 || mp(L.mps[i]).nObs < 1) {
       MPoint p;  // MapPoint(x3D, mpMap, &mLastFrame, i): C2 reads its position and descriptor
       unproject(cam_, Tlast, L.kps[i].x, L.kps[i].y, L.depth[i], p.pos);
@@ -615,9 +621,24 @@ void MapEngine::update_last_frame(MapFrameH& L, float* Tlast) {  // Tracking.cc:
       temps_.push_back(p);
       L.mps[i] = kTemp + (int)temps_.size() - 1;
     }
-    nPoints++;
-    if (v[j].first > cam_.thDepth && nPoints > 200) break;
+  };
+  temps_.reserve(L.n);
+  far_.clear();
+  int nclose = 0;
+  for (int i = 0; i < L.n; i++) {
+    const float z = L.depth[i];
+    if (!(z > 0)) continue;
+    if (z > cam_.thDepth) {
+      far_.push_back({z, i});
+    } else {
+      make(i);
+      nclose++;
+    }
   }
+  const size_t need = std::min(far_.size(), (size_t)(nclose >= 200 ? 1 : 201 - nclose));
+  if (need == 0) return;
+  std::nth_element(far_.begin(), far_.begin() + (need - 1), far_.end());
+  for (size_t j = 0; j < need; j++) make(far_[j].second);
 }
 
 // TrackWithMotionModel / TrackReferenceKeyFrame's outlier discard: returns nmatches
@@ -642,7 +663,7 @@ int MapEngine::discard_outliers(MapFrameH& C, int nmatches, int* nmatchesMap) {
 bool MapEngine::track_with_motion_model(MapFrameH& C, const GridFrame& G, float* Tcw,
                                         MapFrameH& L, float* Tlast, const float* vel,
                                         MapStatsH& st) {
-  update_last_frame(L, Tlast);
+  MAP_PROF(8, update_last_frame(L, Tlast));
   mat4_mul(vel, Tlast, Tcw);
   std::fill(C.mps.begin(), C.mps.end(), -1);
   const float th = 15;
@@ -751,6 +772,7 @@ void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
 }
 
 void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const float* Tcw) {
+  const double t_pack = prof_on_ ? now_us() : 0;
   // Tracking::SearchLocalPoints (Tracking.cc:3416-3466)
   for (int i = 0; i < C.n; i++) {
     if (C.mps[i] < 0) continue;
@@ -775,6 +797,7 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
     skip[j] = (p.lastSeen == curId_) || p.bad;
   }
   for (int i = 0; i < C.n; i++) taken[i] = C.mps[i] >= 0 && mp(C.mps[i]).nObs > 0;
+  if (prof_on_) prof_[10] += now_us() - t_pack;
   MMT_HIP(hipMemcpyAsync(d_sel_, h_sel_, 5 * (size_t)m + C.n, hipMemcpyHostToDevice, s_));
   // ORBmatcher(0.8)::SearchByProjection's th: 3 for RGB-D, 5 right after a relocalisation
   const float th = curId_ < lastRelocFrameId_ + 2 ? 5.f : 3.f;
@@ -796,6 +819,10 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
 
 bool MapEngine::track_local_map(MapFrameH& C, const GridFrame& G, float* Tcw) {
   MAP_PROF(2, update_local_keyframes(C); update_local_points());
+  if (prof_on_) {
+    prof_cnt_[0] += localKFs_.size();
+    prof_cnt_[1] += localPts_.size();
+  }
   MAP_PROF(3, search_local_points(C, G, Tcw));
   MAP_PROF(4, gpu_pose_opt(C, Tcw));
   matchesInliers_ = 0;
@@ -947,6 +974,7 @@ void MapEngine::track_finish(MapFrameH& C, MapFrameH& L, const float* Tcw, MapSt
     prof_[7] += now_us() - t0;
     prof_[6] = prof_[7];
     for (int k = 0; k < 6; k++) prof_[6] -= prof_[k];
+    prof_[6] -= prof_[8];
   }
 }
 
