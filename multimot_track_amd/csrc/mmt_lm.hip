@@ -1252,9 +1252,10 @@ constexpr int kPoStride = 29;  // odd row stride of the reduction tile (28 sums)
 
 struct PoSmemR {
   double tile[(kPoThreads / 64) * 64 * kPoStride];
-  double part[(kPoThreads / 64) * kPoSums];
+  double part[2][(kPoThreads / 64) * 32];  // wave partials, double-buffered across passes
+  double Hw[kPoThreads / 64][2][32];        // every wave's own copy of the current / trial sums
   double red[16 * 32];
-  double H[2][32];
+  double H[32];
 };
 
 // po_linearise for the register path: the edge's contribution goes straight into the thread's
@@ -1275,6 +1276,8 @@ __device__ __forceinline__ void po_linearise_row(const PoEdgeR& E, const DSE3& T
   eo[0] = e[0];
   eo[1] = e[1];
   eo[2] = e[2];
+  {  // J and the sums with FMA contraction (the errors and chi2 above keep the reference's rounding)
+#pragma clang fp contract(fast)
   const bool stereo = E.flags & kPoStereo;
   const double c = po_chi2(E, e);
   double r0 = c, r1 = 1.0;
@@ -1321,6 +1324,7 @@ __device__ __forceinline__ void po_linearise_row(const PoEdgeR& E, const DSE3& T
     if (stereo) g += J[2][a] * se2;
     row[22 + a] = FIRST ? -(r1 * g) : row[22 + a] - r1 * g;
   }
+  }
 }
 
 template <int IT>
@@ -1356,26 +1360,57 @@ __device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
   do {          \
   } while (0)
 #endif
-  int npass = 0;
-  auto pass = [&](const DSE3& T, double* out) {
+  int npass = 0, nrej = 0;
+  const int lane = tid & 63, wave = tid >> 6;
+  // one pass: linearise into the tile rows, column sums per wave, one barrier, and every wave adds
+  // the wave partials itself (same order everywhere, so every wave holds the same bits) into its
+  // own LDS copy of the sums, read after a wave-level fence
+  auto pass = [&](const DSE3& T, int buf) {
     PO_T(0);
     po_linearise_row<true>(Ed[0], T, D, dM, dS, er[0], row);
 #pragma unroll
     for (int q = 1; q < IT; q++) po_linearise_row<false>(Ed[q], T, D, dM, dS, er[q], row);
     PO_T(1);
-    block_sum_tile<kPoSums, kPoStride>(sm.tile, sm.part, out, nw);
+    const double* t = sm.tile + (size_t)wave * 64 * kPoStride;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double* part = sm.part[npass & 1];
+    if (lane < kPoSums) {
+      double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int r0 = 0; r0 < 64; r0 += 16) {
+        double x[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) x[j] = t[(r0 + j) * kPoStride + lane];
+#pragma unroll
+        for (int j = 0; j < 16; j++) acc[j & 7] += x[j];
+      }
+      part[wave * 32 + lane] =
+          ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
+    __syncthreads();
+    if (lane < kPoSums) {
+      double sum = 0;
+#pragma unroll
+      for (int w = 0; w < nw; w++) sum += part[w * 32 + lane];
+      sm.Hw[wave][buf][lane] = sum;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     PO_T(2);
     npass++;
   };
   for (int it = 0; it < 4; it++) {
     P = dse3_from_float(D.Tcw);  // every round restarts from the input pose
     int hs = 0;
-    pass(P, sm.H[0]);
-    double cur = sm.H[0][0], lam, ni = 2, chk = 0;
+    pass(P, 0);
+    double cur = sm.Hw[wave][0][0], lam, ni = 2, chk = 0;
     {
       double md = 0;
 #pragma unroll
-      for (int a = 0; a < 6; a++) md = fmax(md, fabs(sm.H[0][1 + a * (a + 3) / 2]));
+      for (int a = 0; a < 6; a++) md = fmax(md, fabs(sm.Hw[wave][0][1 + a * (a + 3) / 2]));
       lam = 1e-5 * md;
     }
     int nRaul = 0;
@@ -1385,7 +1420,7 @@ __device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
       int qmax = 0;
       bool bad = false;
       for (;;) {
-        const double* Hc = sm.H[hs];
+        const double* Hc = sm.Hw[wave][hs];
         double A[21], bs[6];
 #pragma unroll
         for (int q = 0; q < 21; q++) A[q] = Hc[1 + q];
@@ -1398,8 +1433,8 @@ __device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
 #pragma unroll
         for (int a = 0; a < 6; a++) xb[a] = ok2 ? bs[a] : xb[a];
         const DSE3 PN = exp_mul(xb, P);
-        pass(PN, sm.H[hs ^ 1]);
-        const double* Ht = sm.H[hs ^ 1];
+        pass(PN, hs ^ 1);
+        const double* Ht = sm.Hw[wave][hs ^ 1];
         const double lastTrialChi = Ht[0];
         const double tempChi = ok2 ? Ht[0] : DBL_MAX;
         double scale = 0;
@@ -1420,6 +1455,7 @@ __device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
         } else {
           lam = lam * ni;
           ni = ni * 2;
+          nrej++;
         }
         qmax++;
         const bool again = (rho < 0 && qmax < 10);
@@ -1457,9 +1493,9 @@ __device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
       if (it == 2) f &= ~kPoRobust;
       Ed[q].flags = f;
     }
-    block_sum<1>(nb, sm.red, sm.H[0], nw);
-    nBad = (int)sm.H[0][0];
-    __syncthreads();  // sm.H[0] is rewritten by the next round's first reduction
+    block_sum<1>(nb, sm.red, sm.H, nw);
+    nBad = (int)sm.H[0];
+    __syncthreads();  // sm.H is rewritten by the next round's count
     if (N < 10) break;
   }
 #pragma unroll
@@ -1471,8 +1507,8 @@ __device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
     dse3_to_float(P, D.pose_out);
     *D.n_inliers = N - nBad;
 #ifdef MMT_PO_PROFILE
-    printf("[po profile] N %d passes %d cycles: solve+ctl %lld linearise %lld reduce %lld\n", N,
-           npass, pp[0], pp[1], pp[2]);
+    printf("[po profile] N %d passes %d (rejected trials %d) cycles: solve+ctl %lld linearise "
+           "%lld reduce %lld\n", N, npass, nrej, pp[0], pp[1], pp[2]);
 #endif
   }
 #undef PO_T
