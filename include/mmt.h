@@ -27,6 +27,9 @@
  *   mmt_search_local_points
  *                       <- Tracking::SearchLocalPoints Tracking.cc:3416-3466 ->
  *                          ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) :418-502
+ *   mmt_search_by_bow   <- ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&, ...)
+ *                          ORBmatcher.cc:532-663 (TrackReferenceKeyFrame Tracking.cc:2841-2853,
+ *                          Relocalization :3631-3651)
  *   mmt_destroy         <- System::Shutdown / delete
  */
 #ifndef MMT_H
@@ -326,6 +329,38 @@ typedef struct mmt_local_points {
 int mmt_search_local_points(mmt_ctx* ctx, const mmt_match_frame* cur,
                             const mmt_local_points* pts, float th, const uint8_t* taken,
                             int32_t* match_out, float* frustum_out, int* nmatches);
+
+/* DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>, FeatureVector.h) as flat
+ * arrays: node_id ascending; the features of node k are feat[node_start[k] .. node_start[k+1])
+ * in insertion order.  Every frame feature is listed in at most one node (DBoW2's transform puts
+ * each feature in one node at the direct-index level), and a node holds at most 2048 of them. */
+typedef struct mmt_feature_vector {
+  int n_nodes;
+  const uint32_t* node_id;    /* n_nodes              */
+  const int32_t* node_start;  /* n_nodes + 1, from 0  */
+  const int32_t* feat;        /* node_start[n_nodes]  */
+} mmt_feature_vector;
+
+/* A keyframe as SearchByBoW reads it: mvKeysUn (angle), mDescriptors, whether mvpMapPoints[i] holds
+ * a MapPoint that is not bad, and mFeatVec. */
+typedef struct mmt_bow_keyframe {
+  int n;
+  const mmt_kp* kps;
+  const uint8_t* desc;      /* n x 32 */
+  const uint8_t* mp_valid;  /* n      */
+  mmt_feature_vector fv;
+} mmt_bow_keyframe;
+
+/* C4: ORBmatcher(nn_ratio, check_orientation)::SearchByBoW(pKF, F, vpMapPointMatches, ...)
+ * (ORBmatcher.cc:532-663): per common vocabulary node, each keyframe feature with a good MapPoint
+ * takes the closest unmatched frame feature of the node if its distance is <= TH_LOW (50) and below
+ * nn_ratio times the second-best distance; then the rotation-consistency histogram.  match_out[i]
+ * (n_cur) = the keyframe key whose MapPoint now matches frame key i (vpMapPointMatches[i] =
+ * pKF->mvpMapPoints[match_out[i]]), or -1; *nmatches = the return value.  The reference uses
+ * nn_ratio 0.7 in TrackReferenceKeyFrame and 0.75 in Relocalization. */
+int mmt_search_by_bow(mmt_ctx* ctx, const mmt_bow_keyframe* kf, int n_cur, const mmt_kp* cur_kps,
+                      const uint8_t* cur_desc, const mmt_feature_vector* cur_fv, float nn_ratio,
+                      int check_orientation, int32_t* match_out, int* nmatches);
 
 /* Stage timing with HIP events on the launch stream (no reference counterpart: measurement
  * hook for bench.py).  orb_ms sums the batched ORB launch sequences of the tracked chunks. */

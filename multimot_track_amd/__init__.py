@@ -132,6 +132,27 @@ class MmtError(RuntimeError):
     pass
 
 
+class MmtFeatureVector(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int), ("node_id", ctypes.c_void_p),
+                ("node_start", ctypes.c_void_p), ("feat", ctypes.c_void_p)]
+
+
+class MmtBowKeyFrame(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("kps", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("mp_valid", ctypes.c_void_p), ("fv", MmtFeatureVector)]
+
+
+def _feature_vector(v, keep):
+    """(node ids ascending, starts (n_nodes + 1), features) -> MmtFeatureVector."""
+    node, start, feat = (np.ascontiguousarray(v[0], np.uint32), np.ascontiguousarray(v[1], np.int32),
+                         np.ascontiguousarray(v[2], np.int32))
+    keep += [node, start, feat]
+    fv = MmtFeatureVector()
+    fv.n_nodes = len(node)
+    fv.node_id, fv.node_start, fv.feat = node.ctypes.data, start.ctypes.data, feat.ctypes.data
+    return fv
+
+
 def lib():
     """Load libmmt.so; fail loudly (no fallback) when the HIP extension is not built."""
     global _LIB
@@ -182,6 +203,9 @@ def lib():
         L.mmt_search_local_points.argtypes = [vp, ctypes.POINTER(MmtMatchFrame),
                                               ctypes.POINTER(MmtLocalPoints), ctypes.c_float,
                                               vp, vp, vp, vp]
+        L.mmt_search_by_bow.argtypes = [vp, ctypes.POINTER(MmtBowKeyFrame), i32, vp, vp,
+                                        ctypes.POINTER(MmtFeatureVector), ctypes.c_float, i32,
+                                        vp, vp]
         L.mmt_profile_enable.argtypes = [vp, i32]
         L.mmt_profile_read.argtypes = [vp, ctypes.POINTER(MmtProfile), i32]
         _LIB = L
@@ -413,6 +437,29 @@ class Context:
             self._h, ctypes.byref(fr), ctypes.byref(L), th, int(mono), int(check_orientation),
             _p(match), ctypes.byref(nm)))
         return nm.value, match[:fr.n]
+
+    def search_by_bow(self, kf_fv, kf_kps, kf_desc, kf_mp_ok, f_fv, f_kps, f_desc, nnratio=0.7,
+                      check_orientation=True):
+        """ORBmatcher(nnratio, check_orientation)::SearchByBoW(KeyFrame*, Frame&) (C4):
+        (nmatches, match[frame key] = keyframe key or -1).  Feature vectors are (node ids
+        ascending, starts, features)."""
+        keep = []
+        kk = np.ascontiguousarray(kf_kps)
+        kd = np.ascontiguousarray(kf_desc, np.uint8)
+        ok = np.ascontiguousarray(kf_mp_ok, np.uint8)
+        fk = np.ascontiguousarray(f_kps)
+        fd = np.ascontiguousarray(f_desc, np.uint8)
+        K = MmtBowKeyFrame()
+        K.n = len(kk)
+        K.kps, K.desc, K.mp_valid = kk.ctypes.data, kd.ctypes.data, ok.ctypes.data
+        K.fv = _feature_vector(kf_fv, keep)
+        F = _feature_vector(f_fv, keep)
+        match = np.zeros(max(len(fk), 1), np.int32)
+        nm = ctypes.c_int(0)
+        self._check(lib().mmt_search_by_bow(self._h, ctypes.byref(K), len(fk), _p(fk), _p(fd),
+                                            ctypes.byref(F), nnratio, int(check_orientation),
+                                            _p(match), ctypes.byref(nm)))
+        return nm.value, match[:len(fk)]
 
     def search_local_points(self, kps, desc, depth, tcw, Xw, normal, min_dist, max_dist, pdesc,
                             skip, th, taken=None):

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -568,6 +570,79 @@ int mmt_search_by_projection_frame(mmt_ctx* ctx, const mmt_match_frame* cur,
     if (cur->n > 0)
       MMT_HIP(hipMemcpyAsync(match_out, match.p, 4 * (size_t)cur->n, hipMemcpyDeviceToHost, s));
     MMT_HIP(hipMemcpyAsync(nmatches, nm.p, 4, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+  });
+}
+
+// host checks of a feature vector: ascending node ids, monotone starts from 0, features in
+// [0, n); `once` (n bytes, optional) rejects a feature listed twice; nodes of at most max_node
+static void check_feature_vector(const mmt_feature_vector* v, int n, std::vector<uint8_t>* once,
+                                 int max_node) {
+  if (v->n_nodes < 0) throw ArgError("negative node count");
+  if (v->n_nodes == 0) return;
+  if (!v->node_id || !v->node_start || !v->feat) throw ArgError("null feature vector arrays");
+  if (v->node_start[0] != 0) throw ArgError("node_start[0] != 0");
+  for (int k = 0; k < v->n_nodes; k++) {
+    if (k > 0 && !(v->node_id[k - 1] < v->node_id[k])) throw ArgError("node ids not ascending");
+    const int a = v->node_start[k], b = v->node_start[k + 1];
+    if (b < a) throw ArgError("node_start not monotone");
+    if (b - a > max_node) throw ArgError("a vocabulary node holds more than 2048 frame features");
+    for (int q = a; q < b; q++) {
+      const int f = v->feat[q];
+      if (f < 0 || f >= n) throw ArgError("feature index out of range");
+      if (once) {
+        if ((*once)[f]) throw ArgError("a frame feature is listed in two nodes");
+        (*once)[f] = 1;
+      }
+    }
+  }
+}
+
+int mmt_search_by_bow(mmt_ctx* ctx, const mmt_bow_keyframe* kf, int n_cur, const mmt_kp* cur_kps,
+                      const uint8_t* cur_desc, const mmt_feature_vector* cur_fv, float nn_ratio,
+                      int check_orientation, int32_t* match_out, int* nmatches) {
+  if (!ctx || !kf || !cur_fv || !nmatches || kf->n < 0 || n_cur < 0 ||
+      (n_cur > 0 && (!match_out || !cur_kps || !cur_desc)) ||
+      (kf->n > 0 && (!kf->kps || !kf->desc || !kf->mp_valid)))
+    return MMT_EINVAL;
+  return guard(ctx, [&] {
+    check_feature_vector(&kf->fv, kf->n, nullptr, INT32_MAX);
+    std::vector<uint8_t> once((size_t)std::max(n_cur, 1), 0);
+    check_feature_vector(cur_fv, n_cur, &once, mmt::kBowMaxNodeFeatures);
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    hipStream_t s = ctx->stream;
+    const int nk = kf->n, nkn = kf->fv.n_nodes, nfn = cur_fv->n_nodes;
+    const int nkfeat = nkn > 0 ? kf->fv.node_start[nkn] : 0;
+    const int nffeat = nfn > 0 ? cur_fv->node_start[nfn] : 0;
+    DevBuf<mmt_kp> kk(nk), fk(n_cur);
+    DevBuf<uint8_t> kd(32 * (size_t)nk), ok(nk), fd(32 * (size_t)n_cur);
+    DevBuf<uint32_t> kn(nkn), fnode(nfn);
+    DevBuf<int> ks(nkn + 1), kfe(nkfeat), fs(nfn + 1), ffe(nffeat);
+    DevBuf<int> match(n_cur), hist(32), cnt(2);
+    auto up = [&](void* d, const void* h, size_t bytes) {
+      if (bytes) MMT_HIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+    };
+    up(kk.p, kf->kps, sizeof(mmt_kp) * (size_t)nk);
+    up(kd.p, kf->desc, 32 * (size_t)nk);
+    up(ok.p, kf->mp_valid, (size_t)nk);
+    up(fk.p, cur_kps, sizeof(mmt_kp) * (size_t)n_cur);
+    up(fd.p, cur_desc, 32 * (size_t)n_cur);
+    if (nkn > 0) {
+      up(kn.p, kf->fv.node_id, 4 * (size_t)nkn);
+      up(ks.p, kf->fv.node_start, 4 * (size_t)(nkn + 1));
+      up(kfe.p, kf->fv.feat, 4 * (size_t)nkfeat);
+    }
+    if (nfn > 0) {
+      up(fnode.p, cur_fv->node_id, 4 * (size_t)nfn);
+      up(fs.p, cur_fv->node_start, 4 * (size_t)(nfn + 1));
+      up(ffe.p, cur_fv->feat, 4 * (size_t)nffeat);
+    }
+    mmt::BowFeatVec a{nkn, kn.p, ks.p, kfe.p}, b{nfn, fnode.p, fs.p, ffe.p};
+    mmt::launch_search_by_bow(a, kk.p, kd.p, ok.p, b, fk.p, fd.p, n_cur, nn_ratio,
+                              check_orientation, match.p, hist.p, cnt.p, s);
+    if (n_cur > 0)
+      MMT_HIP(hipMemcpyAsync(match_out, match.p, 4 * (size_t)n_cur, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(nmatches, cnt.p + 1, 4, hipMemcpyDeviceToHost, s));
     MMT_HIP(hipStreamSynchronize(s));
   });
 }

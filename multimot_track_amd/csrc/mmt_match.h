@@ -98,6 +98,22 @@ void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointD
                          FrustumRec* fr, const CandSet& cs, int* match, int* nmatches,
                          hipStream_t st, const LocalSel* sel = nullptr);
 
+// C4: ORBmatcher::SearchByBoW(KeyFrame*, Frame&) with caller-supplied DBoW2 FeatureVectors
+// (node ids ascending, per-node feature lists in insertion order, every feature in one node).
+struct BowFeatVec {
+  int n_nodes;
+  const uint32_t* node;
+  const int* start;  // n_nodes + 1
+  const int* feat;
+};
+constexpr int kBowMaxNodeFeatures = 64 * 32;  // frame features one node may hold (lane bitmasks)
+// match (nF ints) receives the keyframe key index per frame key or -1, hist 30 ints and
+// counters 2 ints of scratch; counters[1] = nmatches after the launch.
+void launch_search_by_bow(const BowFeatVec& kf, const mmt_kp* kf_keys, const uint8_t* kf_desc,
+                          const uint8_t* kf_ok, const BowFeatVec& f, const mmt_kp* f_keys,
+                          const uint8_t* f_desc, int nF, float nnratio, int check_orientation,
+                          int* match, int* hist, int* counters, hipStream_t st);
+
 // pool maintenance: scatter n packed (handle, record, descriptor) updates into the pool
 struct alignas(16) PoolUpdate {
   int h;

@@ -779,6 +779,169 @@ void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointD
   launch_match_fix(g, st);
 }
 
+// ------------------------------------------------------------------------------ C4
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) ORBmatcher.cc:532-663.  A frame feature belongs
+// to one vocabulary node, so nodes never compete for features: one wave per keyframe node (its
+// frame node found by binary search), the node's keyframe features replayed in list order.  Per
+// keyframe feature the wave scores every unmatched frame feature of the node at once (lane =
+// position, in chunks of 64), the best is the smallest (distance, position) key (the reference's
+// strict '<' keeps the first of equal distances) and the second-best distance the smallest of the
+// rest, accepted at TH_LOW and the ratio test; the winner's lane marks it matched.
+static constexpr int TH_LOW = 50;  // ORBmatcher.cc:42
+
+struct BowArgs {
+  BowFeatVec kf, f;
+  const mmt_kp* kf_keys;
+  const uint8_t* kf_desc;
+  const uint8_t* kf_ok;
+  const mmt_kp* f_keys;
+  const uint8_t* f_desc;
+  int nF;
+  float ratio;
+  int check_orientation;
+  int* match;
+  int* hist;
+  int* counters;
+};
+
+__global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= a.kf.n_nodes) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const uint32_t id = a.kf.node[k];
+  int lo = 0, hi = a.f.n_nodes;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a.f.node[mid] < id)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  if (lo >= a.f.n_nodes || a.f.node[lo] != id) return;
+  const int fb = a.f.start[lo], fn = a.f.start[lo + 1] - fb;
+  const int nch = (fn + 63) >> 6;  // <= 32 (host-checked)
+  // this lane's frame features (positions lane + 64 c) and their descriptors stay in L1/L2; the
+  // matched flags live in a register bitmask
+  uint32_t taken = 0;
+  int nm = 0;
+  for (int q = a.kf.start[k]; q < a.kf.start[k + 1]; q++) {
+    const int ikf = a.kf.feat[q];
+    if (!a.kf_ok[ikf]) continue;  // pMP == NULL or isBad()
+    uint32_t dk[8];
+    load_desc8(a.kf_desc + 32 * (size_t)ikf, dk);
+    uint32_t k1 = kNoCand;  // lane-local smallest (dist << 16 | position)
+    int d2 = 256;           // lane-local second-smallest distance
+    for (int c = 0; c < nch; c++) {
+      const int p = lane + 64 * c;
+      if (p >= fn || ((taken >> c) & 1u)) continue;
+      uint32_t df[8];
+      load_desc8(a.f_desc + 32 * (size_t)a.f.feat[fb + p], df);
+      int dist = 0;
+#pragma unroll
+      for (int w = 0; w < 8; w++) dist += __popc(dk[w] ^ df[w]);
+      const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)p;
+      if (key < k1) {
+        if (k1 != kNoCand) d2 = min(d2, (int)(k1 >> 16));
+        k1 = key;
+      } else {
+        d2 = min(d2, dist);
+      }
+    }
+    const uint32_t m1 = wave_min_u32(k1);
+    if (m1 == kNoCand) continue;  // bestDist1 = 256 > TH_LOW
+    const int c2 = k1 == m1 ? d2 : (k1 != kNoCand ? (int)(k1 >> 16) : 256);
+    const int best2 = (int)wave_min_u32((uint32_t)c2);
+    const int best1 = (int)(m1 >> 16);
+    if (best1 > TH_LOW || !((float)best1 < a.ratio * (float)best2)) continue;
+    const int p = (int)(m1 & 0xFFFFu);
+    if (lane == (p & 63)) {
+      taken |= 1u << (p >> 6);
+      const int iF = a.f.feat[fb + p];
+      a.match[iF] = ikf;
+      if (a.check_orientation)
+        atomicAdd(&a.hist[rot_bin(a.kf_keys[ikf].angle, a.f_keys[iF].angle)], 1);
+    }
+    nm++;
+  }
+  if (lane == 0 && nm) atomicAdd(&a.counters[0], nm);
+}
+
+// the rotation-consistency filter of SearchByBoW (ORBmatcher.cc:641-660) and nmatches
+__global__ __launch_bounds__(256) void k_bow_rot(BowArgs a) {
+  __shared__ int s_ind[3], s_removed;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    s_removed = 0;
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int h = 0; h < HISTO_LENGTH; h++) {
+      const int s = a.check_orientation ? a.hist[h] : 0;
+      if (s > max1) {
+        max3 = max2; max2 = max1; max1 = s;
+        ind3 = ind2; ind2 = ind1; ind1 = h;
+      } else if (s > max2) {
+        max3 = max2; max2 = s;
+        ind3 = ind2; ind2 = h;
+      } else if (s > max3) {
+        max3 = s;
+        ind3 = h;
+      }
+    }
+    if (max2 < 0.1f * (float)max1) {
+      ind2 = -1;
+      ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+      ind3 = -1;
+    }
+    s_ind[0] = ind1;
+    s_ind[1] = ind2;
+    s_ind[2] = ind3;
+  }
+  __syncthreads();
+  int removed = 0;
+  if (a.check_orientation)
+    for (int i = tid; i < a.nF; i += blockDim.x) {
+      const int m = a.match[i];
+      if (m < 0) continue;
+      const int bin = rot_bin(a.kf_keys[m].angle, a.f_keys[i].angle);
+      if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
+        a.match[i] = -1;
+        removed++;
+      }
+    }
+  if (removed) atomicAdd(&s_removed, removed);
+  __syncthreads();
+  if (tid == 0) a.counters[1] = a.counters[0] - s_removed;
+}
+
+void launch_search_by_bow(const BowFeatVec& kf, const mmt_kp* kf_keys, const uint8_t* kf_desc,
+                          const uint8_t* kf_ok, const BowFeatVec& f, const mmt_kp* f_keys,
+                          const uint8_t* f_desc, int nF, float nnratio, int check_orientation,
+                          int* match, int* hist, int* counters, hipStream_t st) {
+  BowArgs a;
+  a.kf = kf;
+  a.f = f;
+  a.kf_keys = kf_keys;
+  a.kf_desc = kf_desc;
+  a.kf_ok = kf_ok;
+  a.f_keys = f_keys;
+  a.f_desc = f_desc;
+  a.nF = nF;
+  a.ratio = nnratio;
+  a.check_orientation = check_orientation;
+  a.match = match;
+  a.hist = hist;
+  a.counters = counters;
+  if (nF > 0) MMT_HIP(hipMemsetAsync(match, 0xFF, sizeof(int) * (size_t)nF, st));
+  MMT_HIP(hipMemsetAsync(hist, 0, sizeof(int) * HISTO_LENGTH, st));
+  MMT_HIP(hipMemsetAsync(counters, 0, sizeof(int) * 2, st));
+  if (kf.n_nodes > 0 && f.n_nodes > 0) {
+    hipLaunchKernelGGL(k_bow_nodes, dim3((kf.n_nodes + 3) / 4), dim3(256), 0, st, a);
+    MMT_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_bow_rot, dim3(1), dim3(256), 0, st, a);
+  MMT_HIP(hipGetLastError());
+}
+
 // ------------------------------------------------------------------------------ pool
 __global__ void k_pool_scatter(const PoolUpdate* __restrict__ up, int n, LocalPointDev* pool,
                                uint8_t* pool_desc) {

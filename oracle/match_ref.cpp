@@ -313,4 +313,79 @@ int search_local_points(const MatchFrame& C, const float* Tcw, const LocalPoint*
   return nmatches;
 }
 
+// C4: ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) ORBmatcher.cc:532-663, literally: the two
+// feature vectors are walked in node order (equal ids: match the node; otherwise lower_bound the
+// lagging side), inside a node every keyframe feature with a good MapPoint takes the closest frame
+// feature not matched yet (strict '<', so the first of equal distances), accepted at
+// bestDist1 <= TH_LOW and bestDist1 < nnratio * bestDist2 (floats); then the rotation histogram.
+static const int TH_LOW = 50;  // ORBmatcher.cc:42
+
+static int fv_lower_bound(const FeatVec& v, uint32_t id) {
+  return (int)(std::lower_bound(v.node, v.node + v.n_nodes, id) - v.node);
+}
+
+int search_by_bow(const FeatVec& kfv, const Key* kf_keys, const uint8_t* kf_desc,
+                  const uint8_t* kf_mp_ok, const FeatVec& fv, const Key* f_keys,
+                  const uint8_t* f_desc, int nF, float nnratio, bool check_orientation,
+                  int* match) {
+  for (int i = 0; i < nF; i++) match[i] = -1;  // vpMapPointMatches = vector(F.N, NULL)
+  int nmatches = 0;
+  std::vector<int> rotHist[HISTO_LENGTH];
+  const float factor = 1.0f / HISTO_LENGTH;
+  int ki = 0, fi = 0;
+  while (ki < kfv.n_nodes && fi < fv.n_nodes) {
+    if (kfv.node[ki] == fv.node[fi]) {
+      for (int a = kfv.start[ki]; a < kfv.start[ki + 1]; a++) {
+        const int realIdxKF = kfv.feat[a];
+        if (!kf_mp_ok[realIdxKF]) continue;
+        const uint8_t* dKF = kf_desc + 32 * (size_t)realIdxKF;
+        int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+        for (int b = fv.start[fi]; b < fv.start[fi + 1]; b++) {
+          const int realIdxF = fv.feat[b];
+          if (match[realIdxF] >= 0) continue;
+          const int dist = descriptor_distance(dKF, f_desc + 32 * (size_t)realIdxF);
+          if (dist < bestDist1) {
+            bestDist2 = bestDist1;
+            bestDist1 = dist;
+            bestIdxF = realIdxF;
+          } else if (dist < bestDist2) {
+            bestDist2 = dist;
+          }
+        }
+        if (bestDist1 <= TH_LOW) {
+          if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
+            match[bestIdxF] = realIdxKF;
+            if (check_orientation) {
+              float rot = kf_keys[realIdxKF].angle - f_keys[bestIdxF].angle;
+              if (rot < 0.0) rot += 360.0f;
+              int bin = (int)std::round(rot * factor);
+              if (bin == HISTO_LENGTH) bin = 0;
+              rotHist[bin].push_back(bestIdxF);
+            }
+            nmatches++;
+          }
+        }
+      }
+      ki++;
+      fi++;
+    } else if (kfv.node[ki] < fv.node[fi]) {
+      ki = fv_lower_bound(kfv, fv.node[fi]);
+    } else {
+      fi = fv_lower_bound(fv, kfv.node[ki]);
+    }
+  }
+  if (check_orientation) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      if (i == ind1 || i == ind2 || i == ind3) continue;
+      for (int j : rotHist[i]) {
+        match[j] = -1;
+        nmatches--;
+      }
+    }
+  }
+  return nmatches;
+}
+
 }  // namespace oracle

@@ -328,6 +328,32 @@ def search_by_projection_frame(kps, desc, depth, tcw, last_kps, Xw, mp_desc, act
     return nm, match[:len(kps)]
 
 
+def search_by_bow(kf_fv, kf_kps, kf_desc, kf_mp_ok, f_fv, f_kps, f_desc, nnratio=0.7,
+                  check_orientation=True):
+    """C4 SearchByBoW(KeyFrame*, Frame&): kf_fv / f_fv = (node ids ascending, starts, features)."""
+    L = lib()
+    vp = ctypes.c_void_p
+    L.oracle_search_by_bow.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, ctypes.c_int, vp, vp,
+                                       vp, ctypes.c_int, vp, vp, ctypes.c_float, ctypes.c_int, vp]
+
+    def fv(v):
+        node, start, feat = v
+        return (np.ascontiguousarray(node, np.uint32), np.ascontiguousarray(start, np.int32),
+                np.ascontiguousarray(feat, np.int32))
+    kn, ks, kf = fv(kf_fv)
+    fn, fs, ff = fv(f_fv)
+    kk = np.ascontiguousarray(kf_kps, KP_DTYPE)
+    kd = np.ascontiguousarray(kf_desc, np.uint8)
+    ok = np.ascontiguousarray(kf_mp_ok, np.uint8)
+    fk = np.ascontiguousarray(f_kps, KP_DTYPE)
+    fd = np.ascontiguousarray(f_desc, np.uint8)
+    match = np.zeros(max(len(fk), 1), np.int32)
+    nm = L.oracle_search_by_bow(len(kn), _p(kn), _p(ks), _p(kf), _p(kk), _p(kd), _p(ok), len(fn),
+                                _p(fn), _p(fs), _p(ff), len(fk), _p(fk), _p(fd), nnratio,
+                                int(check_orientation), _p(match))
+    return nm, match[:len(fk)]
+
+
 def search_local_points(kps, desc, depth, tcw, Xw, normal, min_dist, max_dist, pdesc, skip, th,
                         K, bf, scale, taken=None):
     L = lib()

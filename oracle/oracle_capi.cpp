@@ -374,4 +374,23 @@ int oracle_search_local_points(int n, const Key* keys, const uint8_t* desc, cons
   return nm;
 }
 
+// C4 probe: feature vectors as (n_nodes, node ids, starts, features) arrays.
+int oracle_search_by_bow(int kf_nodes, const uint32_t* kf_node, const int* kf_start,
+                         const int* kf_feat, const Key* kf_keys, const uint8_t* kf_desc,
+                         const uint8_t* kf_mp_ok, int f_nodes, const uint32_t* f_node,
+                         const int* f_start, const int* f_feat, int nF, const Key* f_keys,
+                         const uint8_t* f_desc, float nnratio, int check_orientation, int* match) {
+  FeatVec a, b;
+  a.n_nodes = kf_nodes;
+  a.node = kf_node;
+  a.start = kf_start;
+  a.feat = kf_feat;
+  b.n_nodes = f_nodes;
+  b.node = f_node;
+  b.start = f_start;
+  b.feat = f_feat;
+  return search_by_bow(a, kf_keys, kf_desc, kf_mp_ok, b, f_keys, f_desc, nF, nnratio,
+                       check_orientation != 0, match);
+}
+
 }  // extern "C"

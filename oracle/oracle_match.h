@@ -77,4 +77,21 @@ bool is_in_frustum(const MatchFrame& F, const float* Tcw, const LocalPoint& p,
 int search_local_points(const MatchFrame& C, const float* Tcw, const LocalPoint* pts, int m,
                         float th, const uint8_t* taken, int* match, FrustumOut* fr);
 
+// DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>) as flat arrays: node ids
+// ascending; the features of node k are feat[start[k] .. start[k + 1]) in insertion order.
+struct FeatVec {
+  int n_nodes = 0;
+  const uint32_t* node = nullptr;
+  const int* start = nullptr;
+  const int* feat = nullptr;
+};
+
+// C4: ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches, ...) ORBmatcher.cc:532-663
+// with ORBmatcher(nnratio, check_orientation).  kf_mp_ok[i]: pKF->mvpMapPoints[i] && !isBad().
+// match[iF] = the keyframe key whose MapPoint is matched to frame key iF, or -1.  Returns nmatches.
+int search_by_bow(const FeatVec& kfv, const Key* kf_keys, const uint8_t* kf_desc,
+                  const uint8_t* kf_mp_ok, const FeatVec& fv, const Key* f_keys,
+                  const uint8_t* f_desc, int nF, float nnratio, bool check_orientation,
+                  int* match);
+
 }  // namespace oracle
