@@ -68,7 +68,7 @@ def _compare_frame(g, o, i):
     pose within 1e-4 (the frame's, the map branch's, each object's), centroids within 1e-3 m (NaN
     on both sides for a solve without points): oracle/compare.py."""
     from oracle import compare
-    p, c, bad = compare.compare_frame(g, o)
+    p, c, bad = compare.compare_frame(g, o)[:3]
     assert not bad, (i, bad)
     assert p < POSE_TOL, (i, p, g["Tcw"], o["Tcw"])
     assert c < CENTRE_TOL, (i, c)
@@ -225,7 +225,7 @@ def test_track_ten_objects_matches_oracle(ctx, oracle_mod):
         s = split_labels(f["sem"])
         o = tr.track(f["bgr"], f["disp"], f["flow"], s)
         g = ctx.track(f["bgr"], f["disp"], f["flow"], s)
-        p, c, bad = compare.compare_frame(g, o)
+        p, c, bad = compare.compare_frame(g, o)[:3]
         assert not bad and p < POSE_TOL and c < CENTRE_TOL, (i, p, c, bad)
         nmax = max(nmax, len(g["objects"]))
         nan_seen = nan_seen or any(ob["n_solve"] == 0 and np.isnan(ob["centre_pre"]).all()
