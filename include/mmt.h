@@ -151,15 +151,6 @@ int mmt_orb_extract_device(mmt_ctx* ctx, const uint8_t* d_gray, int nframes, siz
  * tripped guard is never returned as MMT_OK with truncated keypoints. */
 int mmt_orb_device_status(mmt_ctx* ctx, void* stream);
 
-/* Test hook: OR `flags` into the ORB device error word (as a tripped kernel guard would). */
-int mmt_debug_orb_raise(mmt_ctx* ctx, int flags);
-
-/* Debug: copy an intermediate device buffer of the last ORB run (frame 0..max_batch-1) to the
- * host.  what: 0 pyramid, 1 blurred pyramid (both level-major, unpadded), 2 FAST per-cell
- * counts (int), 3 FAST candidate keys (packed u32), 4 octree output keys (packed u32),
- * 5 octree per-level counts (int), 6 device error flags (int).  Returns bytes written or <0. */
-long mmt_debug_fetch(mmt_ctx* ctx, int what, int frame, void* out, size_t cap);
-
 /* System::TrackRGBD on one frame (host buffers): bgr 8UC3 (w*h*3), disparity*256 u16 (w*h),
  * flow t->t+1 (w*h*2 float), semantic labels (w*h int32, LoadMask-filtered).  Fills `res` and up
  * to objs_cap object motions.  The first call with > 500 keypoints initialises (Tcw = I). */
@@ -169,7 +160,10 @@ int mmt_track_rgbd(mmt_ctx* ctx, const uint8_t* bgr, const uint16_t* disp256,
 
 /* Device-resident chunk of consecutive frames of the context's sequence (pitches in bytes):
  * ORB extraction is batched over the chunk, tracking then runs frame by frame.  res[nframes],
- * objs[nframes * objs_cap] are host arrays. */
+ * objs[nframes * objs_cap] are host arrays.
+ * Errors (both track entry points): a chunk whose ORB run trips a device guard returns
+ * MMT_EDEVICE before any of its frames is tracked, and the context keeps the state of the previous
+ * call, so tracking may continue with the next frames (or restart after mmt_reset). */
 int mmt_track_rgbd_chunk_device(mmt_ctx* ctx, int nframes, const uint8_t* d_bgr,
                                 size_t bgr_pitch, const uint16_t* d_disp, size_t disp_pitch,
                                 const float* d_flow, size_t flow_pitch, const int32_t* d_mask,
@@ -377,6 +371,17 @@ int mmt_reset(mmt_ctx* ctx);
 
 /* Upper bound on keypoints per frame (sum over levels of quota + 3). */
 int mmt_orb_capacity(const mmt_ctx* ctx);
+
+/* ---- Debug and test hooks: not part of the stable interface, no reference counterpart ---- */
+
+/* Test hook: OR `flags` into the ORB device error word (as a tripped kernel guard would). */
+int mmt_debug_orb_raise(mmt_ctx* ctx, int flags);
+
+/* Debug: copy an intermediate device buffer of the last ORB run (frame 0..max_batch-1) to the
+ * host.  what: 0 pyramid, 1 blurred pyramid (both level-major, unpadded), 2 FAST per-cell
+ * counts (int), 3 FAST candidate keys (packed u32), 4 octree output keys (packed u32),
+ * 5 octree per-level counts (int), 6 device error flags (int).  Returns bytes written or <0. */
+long mmt_debug_fetch(mmt_ctx* ctx, int what, int frame, void* out, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -555,7 +555,8 @@ __device__ __forceinline__ void centre_sum_wave(const FlowSolveDesc& D, int N) {
 }
 
 template <int IR>
-__device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int nt, LMSmem& sm) {
+__device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int nt, LMSmem& sm,
+                                             int max_cand) {
   const int tid = threadIdx.x, nw = nt >> 6;
 #ifdef MMT_LM_PROFILE
   long long prof_t = 0;
@@ -772,7 +773,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        ncand = clean ? 4 : 1;
+        ncand = clean ? max_cand : 1;
         kc = 0;
       }
       bool ok2;
@@ -932,7 +933,10 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
 // One workgroup per solve; each workgroup picks the register-item count its own edge count needs,
 // so a small object solved in the same launch as a large one runs the short code path.
 template <int MAXIR>
-__global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict__ descs) {
+// max_cand (1..4): lambda candidates a clean system's solve provides (1: every trial solves for
+// its own lambda, the sequential order; a test knob, candidates are bit-identical to it)
+__global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict__ descs,
+                                                 int max_cand) {
   __shared__ LMSmem sm;
   const FlowSolveDesc& D = descs[blockIdx.x];
   const int N = D.d_n ? min(*D.d_n, D.cap) : min(D.n, D.cap);
@@ -954,9 +958,9 @@ __global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict
   const int nt = min((int)blockDim.x, max(64, (N + 63) / 64 * 64));
   if ((int)threadIdx.x >= nt) return;
   if (N <= nt || MAXIR == 1)
-    flow_lm_body<1>(D, N, nt, sm);
+    flow_lm_body<1>(D, N, nt, sm, max_cand);
   else
-    flow_lm_body<2>(D, N, nt, sm);
+    flow_lm_body<2>(D, N, nt, sm, max_cand);
 }
 
 void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st) {
@@ -971,7 +975,10 @@ void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipSt
   }();
   int threads = std::min(256, std::max(64, (n_hint + 63) / 64 * 64));
   if (force) threads = force;
-  hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs);
+  // MMT_LM_MAX_CAND=1..4 (read per launch; tests compare 1 against the default 4 bit for bit)
+  int max_cand = 4;
+  if (const char* e = getenv("MMT_LM_MAX_CAND")) max_cand = std::min(4, std::max(1, atoi(e)));
+  hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs, max_cand);
 }
 
 size_t flow_scratch_doubles(int cap) { return (size_t)G_COUNT * cap; }

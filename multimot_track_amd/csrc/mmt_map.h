@@ -161,9 +161,11 @@ class MapEngine {
   void map_point_culling(int kf);
   void mark_dirty(int h);
   // GPU stages (synchronous on s_)
-  int gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* Tcw, const MapFrameH& L,
-                       const float* Tlast, float th);
-  int gpu_pose_opt(MapFrameH& C, float* Tcw);
+  int gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
+                      const float* Tlast, float th, float retry_th, int min_matches);
+  void pose_desc_upload(const float* Tcw);
+  MapEdgeArgs edge_args(const GridFrame& G) const;
+  void apply_pose_opt(MapFrameH& C, float* Tcw);
   void gpu_flush_pool();
   template <typename T>
   T* dev(size_t n);
@@ -220,6 +222,8 @@ class MapEngine {
   float* h_pose_ = nullptr;
   uint8_t* h_outl_ = nullptr;
   int* h_ninl_ = nullptr;
+  uint8_t* d_base_ = nullptr;  // C3 -> D1: per key, the position of a binding held before the
+  uint8_t* h_base_ = nullptr;  // search (kcap x 3 floats) and its flag (kcap bytes)
   // C3: point pool, local selection, candidates
   LocalPointDev* d_pool_ = nullptr;
   uint8_t* d_pool_desc_ = nullptr;

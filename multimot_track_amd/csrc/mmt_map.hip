@@ -122,6 +122,8 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
   h_pose_ = pinned<float>(16);
   h_outl_ = pinned<uint8_t>(kcap);
   h_ninl_ = pinned<int>(1);
+  d_base_ = dev<uint8_t>(13 * (size_t)kcap);
+  h_base_ = pinned<uint8_t>(13 * (size_t)kcap);
   prof_on_ = getenv("MMT_MAP_PROFILE") != nullptr;
   frameNextId_ = 0;
   mbVO_ = false;
@@ -419,10 +421,63 @@ void MapEngine::map_point_culling(int kf) {  // LocalMapping::MapPointCulling (R
 }
 
 // ------------------------------------------------------------------ GPU stages
-int MapEngine::gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* Tcw,
-                                const MapFrameH& L, const float* Tlast, float th) {
+// D1's descriptor for an edge list that k_map_edges builds on the device (it writes n): the edge
+// arrays at a fixed capacity of kcap edges
+void MapEngine::pose_desc_upload(const float* Tcw) {
+  PoseOptDesc& d = *h_pod_;
+  memset(&d, 0, sizeof(d));
+  d.n = 0;
+  d.Xw = d_edges_;
+  d.obs = d_edges_ + 3 * (size_t)kcap_;
+  d.inv_sigma2 = d_edges_ + 6 * (size_t)kcap_;
+  memcpy(d.Tcw, Tcw, 64);
+  d.fx = cam_.fx; d.fy = cam_.fy; d.cx = cam_.cx; d.cy = cam_.cy; d.bf = cam_.bf;
+  d.pose_out = d_pose_;
+  d.outlier = d_outl_;
+  d.n_inliers = d_ninl_;
+  d.e_scratch = d_esc_;
+  d.f_scratch = d_fsc_;
+  MMT_HIP(hipMemcpyAsync(d_pod_, h_pod_, sizeof(PoseOptDesc), hipMemcpyHostToDevice, s_));
+}
+
+MapEdgeArgs MapEngine::edge_args(const GridFrame& G) const {
+  MapEdgeArgs e;
+  memset(&e, 0, sizeof(e));
+  e.n = G.n;
+  e.keys = G.keys;
+  e.uR = G.uR;
+  e.match = d_match_;
+  for (int l = 0; l < cam_.nlevels && l < kMaxLevels; l++) e.inv_sigma2[l] = cam_.invSigma2[l];
+  e.X = d_edges_;
+  e.obs = d_edges_ + 3 * (size_t)kcap_;
+  e.s2 = d_edges_ + 6 * (size_t)kcap_;
+  e.desc = d_pod_;
+  return e;
+}
+
+// Optimizer::PoseOptimization's results for the frame's MapPoints (edges in key order): every
+// edge's mvbOutlier is reset, and below 3 edges the pose stays (Optimizer.cc:3160-3253)
+void MapEngine::apply_pose_opt(MapFrameH& C, float* Tcw) {
+  int n = 0;
+  for (int i = 0; i < C.n; i++)
+    if (C.mps[i] >= 0) {
+      C.outlier[i] = 0;
+      n++;
+    }
+  if (n < 3) return;
+  memcpy(Tcw, h_pose_, 64);
+  int e = 0;
+  for (int i = 0; i < C.n; i++)
+    if (C.mps[i] >= 0) C.outlier[i] = h_outl_[e++];
+}
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono=false) with mbCheckOrientation, retried at
+// retry_th while it finds fewer than min_matches (retry_th 0: no retry), then PoseOptimization on
+// its matches when there are at least min_matches -- the whole chain on the device, one sync.
+// Returns nmatches; the pose and outliers are applied when D1 ran.
+int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
+                               const float* Tlast, float th, float retry_th, int min_matches) {
   const double t_pack = prof_on_ ? now_us() : 0;
-  // SearchByProjection(CurrentFrame, LastFrame, th, bMono=false) with mbCheckOrientation
   const int n1 = L.n;
   uint8_t* hk = h_last_;
   float* hX = (float*)(h_last_ + (size_t)n1 * sizeof(mmt_kp));
@@ -430,9 +485,11 @@ int MapEngine::gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* T
   uint8_t* hA = hD + 32 * (size_t)n1;
   uint8_t* hO = hA + n1;
   memcpy(hk, L.kps, sizeof(mmt_kp) * (size_t)n1);
+  int nact = 0;
   for (int i = 0; i < n1; i++) {
     const int h = L.mps[i];
     hA[i] = h >= 0 && !L.outlier[i];
+    nact += hA[i];
     hO[i] = 0;
     if (h >= 0) {
       const MPoint& p = mp(h);
@@ -443,6 +500,7 @@ int MapEngine::gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* T
   }
   if (prof_on_) prof_[9] += now_us() - t_pack;
   MMT_HIP(hipMemcpyAsync(d_last_, h_last_, last_bytes(n1), hipMemcpyHostToDevice, s_));
+  pose_desc_upload(Tcw);
   LastFrameDev LD;
   LD.keys = (const mmt_kp*)d_last_;
   LD.Xw = (const float*)(d_last_ + (size_t)n1 * sizeof(mmt_kp));
@@ -452,63 +510,26 @@ int MapEngine::gpu_search_frame(MapFrameH& C, const GridFrame& G, const float* T
   LD.n = n1;
   memcpy(LD.Tcw, Tlast, 64);
   launch_sbp_frame(G, Tcw, LD, th, 0, 1, c2_, d_match_, d_nm_, s_);
+  if (retry_th > 0)
+    launch_sbp_frame(G, Tcw, LD, retry_th, 0, 1, c2_, d_match_, d_nm_, s_, d_nm_, min_matches);
+  MapEdgeArgs e = edge_args(G);
+  e.nm = d_nm_;
+  e.min_matches = min_matches;
+  e.src_X = LD.Xw;
+  launch_map_edges(e, s_);
+  launch_pose_opt(d_pod_, 1, std::min(C.n, nact), s_);
   MMT_HIP(hipMemcpyAsync(h_match_, d_match_, sizeof(int) * (size_t)C.n, hipMemcpyDeviceToHost, s_));
   MMT_HIP(hipMemcpyAsync(h_nm_, d_nm_, sizeof(int), hipMemcpyDeviceToHost, s_));
-  MMT_HIP(hipStreamSynchronize(s_));
-  for (int i2 = 0; i2 < C.n; i2++)
-    if (h_match_[i2] >= 0) C.mps[i2] = L.mps[h_match_[i2]];
-  return *h_nm_;
-}
-
-int MapEngine::gpu_pose_opt(MapFrameH& C, float* Tcw) {
-  const double t_pack = prof_on_ ? now_us() : 0;
-  // Optimizer::PoseOptimization(&mCurrentFrame): the frame's MapPoints in key order
-  std::vector<int> idx;
-  idx.reserve(C.n);
-  for (int i = 0; i < C.n; i++)
-    if (C.mps[i] >= 0) idx.push_back(i);
-  const int n = (int)idx.size();
-  float* X = h_edges_;
-  float* ob = X + 3 * (size_t)n;
-  float* s2 = ob + 3 * (size_t)n;
-  for (int e = 0; e < n; e++) {
-    const int i = idx[e];
-    const MPoint& p = mp(C.mps[i]);
-    memcpy(X + 3 * (size_t)e, p.pos, 12);
-    ob[3 * e] = C.kps[i].x;
-    ob[3 * e + 1] = C.kps[i].y;
-    ob[3 * e + 2] = C.uR[i];
-    s2[e] = cam_.invSigma2[C.kps[i].octave];
-    C.outlier[i] = 0;
-  }
-  if (prof_on_) prof_[11] += now_us() - t_pack;
-  PoseOptDesc& d = *h_pod_;
-  memset(&d, 0, sizeof(d));
-  d.n = n;
-  d.Xw = d_edges_;
-  d.obs = d_edges_ + 3 * (size_t)n;
-  d.inv_sigma2 = d_edges_ + 6 * (size_t)n;
-  memcpy(d.Tcw, Tcw, 64);
-  d.fx = cam_.fx; d.fy = cam_.fy; d.cx = cam_.cx; d.cy = cam_.cy; d.bf = cam_.bf;
-  d.pose_out = d_pose_;
-  d.outlier = d_outl_;
-  d.n_inliers = d_ninl_;
-  d.e_scratch = d_esc_;
-  d.f_scratch = d_fsc_;
-  if (n > 0)
-    MMT_HIP(hipMemcpyAsync(d_edges_, h_edges_, sizeof(float) * 7 * (size_t)n,
-                           hipMemcpyHostToDevice, s_));
-  MMT_HIP(hipMemcpyAsync(d_pod_, h_pod_, sizeof(PoseOptDesc), hipMemcpyHostToDevice, s_));
-  launch_pose_opt(d_pod_, 1, n, s_);
   MMT_HIP(hipMemcpyAsync(h_pose_, d_pose_, 64, hipMemcpyDeviceToHost, s_));
-  if (n > 0) MMT_HIP(hipMemcpyAsync(h_outl_, d_outl_, (size_t)n, hipMemcpyDeviceToHost, s_));
+  if (C.n > 0) MMT_HIP(hipMemcpyAsync(h_outl_, d_outl_, (size_t)C.n, hipMemcpyDeviceToHost, s_));
   MMT_HIP(hipMemcpyAsync(h_ninl_, d_ninl_, sizeof(int), hipMemcpyDeviceToHost, s_));
   MMT_HIP(hipStreamSynchronize(s_));
-  if (n >= 3) {
-    memcpy(Tcw, h_pose_, 64);
-    for (int e = 0; e < n; e++) C.outlier[idx[e]] = h_outl_[e];
-  }
-  return *h_ninl_;
+  std::fill(C.mps.begin(), C.mps.end(), -1);
+  for (int i2 = 0; i2 < C.n; i2++)
+    if (h_match_[i2] >= 0) C.mps[i2] = L.mps[h_match_[i2]];
+  const int nm = *h_nm_;
+  if (nm >= min_matches) apply_pose_opt(C, Tcw);
+  return nm;
 }
 
 void MapEngine::gpu_flush_pool() {
@@ -668,14 +689,10 @@ bool MapEngine::track_with_motion_model(MapFrameH& C, const GridFrame& G, float*
   std::fill(C.mps.begin(), C.mps.end(), -1);
   const float th = 15;
   int nmatches;
-  MAP_PROF(0, nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, th));
-  if (nmatches < 20) {
-    std::fill(C.mps.begin(), C.mps.end(), -1);
-    MAP_PROF(0, nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, 2 * th));
-  }
+  // C2 at th, again at 2 th below 20 matches, then D1 at 20 or more (Tracking.cc:2962-2990)
+  MAP_PROF(0, nmatches = gpu_frame_chain(C, G, Tcw, L, Tlast, th, 2 * th, 20));
   st.matches_mm = nmatches;
   if (nmatches < 20) return false;
-  MAP_PROF(1, gpu_pose_opt(C, Tcw));
   int nmatchesMap = 0;
   discard_outliers(C, nmatches, &nmatchesMap);
   mbVO_ = nmatchesMap < 20;
@@ -686,12 +703,11 @@ bool MapEngine::track_reference_subst(MapFrameH& C, const GridFrame& G, float* T
                                       const MapFrameH& L, const float* Tlast) {
   std::fill(C.mps.begin(), C.mps.end(), -1);
   memcpy(Tcw, Tlast, 64);
-  const int nmatches = gpu_search_frame(C, G, Tcw, L, Tlast, 15);
+  const int nmatches = gpu_frame_chain(C, G, Tcw, L, Tlast, 15, 0, 15);
   if (nmatches < 15) {
     std::fill(C.mps.begin(), C.mps.end(), -1);
     return false;
   }
-  gpu_pose_opt(C, Tcw);
   int nmatchesMap = 0;
   discard_outliers(C, nmatches, &nmatchesMap);
   return nmatchesMap >= 10;
@@ -796,16 +812,48 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
     ids[j] = localPts_[j];
     skip[j] = (p.lastSeen == curId_) || p.bad;
   }
-  for (int i = 0; i < C.n; i++) taken[i] = C.mps[i] >= 0 && mp(C.mps[i]).nObs > 0;
+  // the keys bound before the search: taken (Observations() > 0) and, for D1's edge list, their
+  // points' positions
+  float* bX = (float*)h_base_;
+  uint8_t* bHas = h_base_ + 12 * (size_t)kcap_;
+  int nbase = 0;
+  for (int i = 0; i < C.n; i++) {
+    const int h = C.mps[i];
+    taken[i] = 0;
+    bHas[i] = h >= 0;
+    if (h >= 0) {
+      const MPoint& p = mp(h);
+      taken[i] = p.nObs > 0;
+      memcpy(bX + 3 * (size_t)i, p.pos, 12);
+      nbase++;
+    }
+  }
   if (prof_on_) prof_[10] += now_us() - t_pack;
   MMT_HIP(hipMemcpyAsync(d_sel_, h_sel_, 5 * (size_t)m + C.n, hipMemcpyHostToDevice, s_));
+  if (C.n > 0) {
+    MMT_HIP(hipMemcpyAsync(d_base_, h_base_, 12 * (size_t)C.n, hipMemcpyHostToDevice, s_));
+    MMT_HIP(hipMemcpyAsync(d_base_ + 12 * (size_t)kcap_, bHas, (size_t)C.n,
+                           hipMemcpyHostToDevice, s_));
+  }
+  pose_desc_upload(Tcw);
   // ORBmatcher(0.8)::SearchByProjection's th: 3 for RGB-D, 5 right after a relocalisation
   const float th = curId_ < lastRelocFrameId_ + 2 ? 5.f : 3.f;
   LocalSel sel{(const int*)d_sel_, d_sel_ + 4 * (size_t)m, d_inview_};
   launch_search_local(G, Tcw, d_pool_, d_pool_desc_, m, th, d_sel_ + 5 * (size_t)m, nullptr, c3_,
                       d_match_, d_nm_, s_, &sel);
+  // D1 over every key bound after the search (Tracking.cc:3189-3200), chained on the device
+  MapEdgeArgs e = edge_args(G);
+  e.pool = d_pool_;
+  e.ids = (const int*)d_sel_;
+  e.has_base = d_base_ + 12 * (size_t)kcap_;
+  e.base_X = (const float*)d_base_;
+  launch_map_edges(e, s_);
+  launch_pose_opt(d_pod_, 1, std::min(C.n, nbase + m), s_);
   MMT_HIP(hipMemcpyAsync(h_match_, d_match_, sizeof(int) * (size_t)C.n, hipMemcpyDeviceToHost, s_));
   if (m > 0) MMT_HIP(hipMemcpyAsync(h_inview_, d_inview_, (size_t)m, hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipMemcpyAsync(h_pose_, d_pose_, 64, hipMemcpyDeviceToHost, s_));
+  if (C.n > 0) MMT_HIP(hipMemcpyAsync(h_outl_, d_outl_, (size_t)C.n, hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipMemcpyAsync(h_ninl_, d_ninl_, sizeof(int), hipMemcpyDeviceToHost, s_));
   MMT_HIP(hipStreamSynchronize(s_));
   for (int j = 0; j < m; j++) {
     if (skip[j]) continue;
@@ -823,8 +871,8 @@ bool MapEngine::track_local_map(MapFrameH& C, const GridFrame& G, float* Tcw) {
     prof_cnt_[0] += localKFs_.size();
     prof_cnt_[1] += localPts_.size();
   }
-  MAP_PROF(3, search_local_points(C, G, Tcw));
-  MAP_PROF(4, gpu_pose_opt(C, Tcw));
+  MAP_PROF(3, search_local_points(C, G, Tcw));  // C3, then D1 on the device
+  MAP_PROF(4, apply_pose_opt(C, Tcw));
   matchesInliers_ = 0;
   for (int i = 0; i < C.n; i++) {
     if (C.mps[i] < 0 || C.outlier[i]) continue;

@@ -80,9 +80,12 @@ struct LastFrameDev {
   int n;
   float Tcw[16];
 };
+// run_if (optional): the call runs only while *run_if < run_lt (C2's retry at a wider window when
+// the first search found too few matches), decided on the device.
 void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& L, float th,
                       int mono, int check_orientation, const CandSet& cs, int* match,
-                      int* nmatches, hipStream_t st);
+                      int* nmatches, hipStream_t st, const int* run_if = nullptr,
+                      int run_lt = 0);
 
 // C3: SearchLocalPoints' isInFrustum pass + SearchByProjection(Frame&, vector<MapPoint*>, th).
 // ids (null: point j is pts[j]) selects the local points from a resident pool, skip (null: the
@@ -113,6 +116,32 @@ void launch_search_by_bow(const BowFeatVec& kf, const mmt_kp* kf_keys, const uin
                           const uint8_t* kf_ok, const BowFeatVec& f, const mmt_kp* f_keys,
                           const uint8_t* f_desc, int nF, float nnratio, int check_orientation,
                           int* match, int* hist, int* counters, hipStream_t st);
+
+// The edge list of Optimizer::PoseOptimization (Optimizer.cc:3160-3230) built on the device from a
+// matcher's output, in key order: key i is an edge when match[i] >= 0 (position src_X[match[i]],
+// or pool[ids[match[i]]].Xw with a pool) or, without a new match, when has_base[i] (base_X[i]);
+// obs = (x, y, uR) of the key, information 1/sigma^2 of its octave.  Nothing is built when
+// *nm < min_matches.  X / obs / s2 hold cap edges; desc->n receives the edge count.
+struct PoseOptDesc;
+struct MapEdgeArgs {
+  int n;
+  const mmt_kp* keys;
+  const float* uR;
+  const int* match;
+  const int* nm;
+  int min_matches;
+  const float* src_X;
+  const LocalPointDev* pool;
+  const int* ids;
+  const uint8_t* has_base;
+  const float* base_X;
+  float inv_sigma2[kMaxLevels];
+  float* X;
+  float* obs;
+  float* s2;
+  PoseOptDesc* desc;
+};
+void launch_map_edges(const MapEdgeArgs& a, hipStream_t st);
 
 // pool maintenance: scatter n packed (handle, record, descriptor) updates into the pool
 struct alignas(16) PoolUpdate {

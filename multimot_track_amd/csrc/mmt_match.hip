@@ -30,6 +30,7 @@
 
 #include "mmt_internal.h"
 #include "mmt_match.h"
+#include "mmt_track.h"
 
 namespace mmt {
 
@@ -316,11 +317,14 @@ struct SbpArgs {
   float th;
   int mono;
   CandSet cs;
+  const int* run_if;
+  int run_lt;
 };
 
 __global__ __launch_bounds__(256) void k_sbp_frame(SbpArgs a) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= a.L.n) return;  // wave-uniform
+  if (a.run_if && *a.run_if >= a.run_lt) return;
   const GridFrame& C = a.C;
   PointWin w = {};
   if (!a.L.active[i]) {
@@ -469,6 +473,8 @@ struct GreedyArgs {
   const mmt_kp* lkeys;       // C2: last-frame keys (angles)
   int* match;                // C.n
   int* nmatches;
+  const int* run_if;         // optional: run only while *run_if < run_lt
+  int run_lt;
 };
 
 // the decision of one point from its best / second-best unbound candidates
@@ -546,6 +552,8 @@ __global__ __launch_bounds__(kFixThreads) void k_match_fix(GreedyArgs a) {
   __shared__ int s_ind[3];
   __shared__ int s_changed, s_nres, s_more, s_nm, s_removed;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // every thread reads the condition before thread 0 may rewrite it (*nmatches, at the end)
+  if (a.run_if && *a.run_if >= a.run_lt) return;
   const int n = a.C.n, np = a.npts;
   int* ch = a.cs.choice;
   for (int k = tid; k < n; k += kFixThreads) {
@@ -713,7 +721,7 @@ static void launch_match_fix(const GreedyArgs& g, hipStream_t st) {
 
 void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& L, float th,
                       int mono, int check_orientation, const CandSet& cs, int* match,
-                      int* nmatches, hipStream_t st) {
+                      int* nmatches, hipStream_t st, const int* run_if, int run_lt) {
   if (C.n > kMaxMatchKeys) throw ArgError("SearchByProjection: more than 16384 current keys");
   if (check_orientation && L.n > kMaxMatchKeys)
     throw ArgError("SearchByProjection: more than 16384 last-frame keys");
@@ -724,6 +732,8 @@ void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& 
   a.th = th;
   a.mono = mono;
   a.cs = cs;
+  a.run_if = run_if;
+  a.run_lt = run_lt;
   if (L.n > 0) {
     hipLaunchKernelGGL(k_sbp_frame, dim3((L.n + 3) / 4), dim3(256), 0, st, a);
     MMT_HIP(hipGetLastError());
@@ -741,6 +751,8 @@ void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& 
   g.lkeys = L.keys;
   g.match = match;
   g.nmatches = nmatches;
+  g.run_if = run_if;
+  g.run_lt = run_lt;
   launch_match_fix(g, st);
 }
 
@@ -776,6 +788,8 @@ void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointD
   g.lkeys = nullptr;
   g.match = match;
   g.nmatches = nmatches;
+  g.run_if = nullptr;
+  g.run_lt = 0;
   launch_match_fix(g, st);
 }
 
@@ -939,6 +953,52 @@ void launch_search_by_bow(const BowFeatVec& kf, const mmt_kp* kf_keys, const uin
     MMT_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(k_bow_rot, dim3(1), dim3(256), 0, st, a);
+  MMT_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------ D1 edges
+// One 1024-thread workgroup: order-preserving compaction of the bound keys, 1024 keys per step.
+__global__ __launch_bounds__(1024) void k_map_edges(MapEdgeArgs a) {
+  __shared__ int s_w[16];
+  const int t = threadIdx.x;
+  const bool build = !a.nm || *a.nm >= a.min_matches;
+  int base = 0;
+  for (int k0 = 0; k0 < (build ? a.n : 0); k0 += 1024) {
+    const int i = k0 + t;
+    int src = -1;  // 0: a new match, 1: a binding held before the search
+    if (i < a.n) {
+      if (a.match[i] >= 0)
+        src = 0;
+      else if (a.has_base && a.has_base[i])
+        src = 1;
+    }
+    int excl = 0;
+    const int tot = grid_block_scan_excl(src >= 0 ? 1 : 0, s_w, excl);
+    if (src >= 0) {
+      const int e = base + excl;
+      const float* X;
+      if (src == 1)
+        X = a.base_X + 3 * (size_t)i;
+      else if (a.pool)
+        X = a.pool[a.ids[a.match[i]]].Xw;
+      else
+        X = a.src_X + 3 * (size_t)a.match[i];
+      a.X[3 * e] = X[0];
+      a.X[3 * e + 1] = X[1];
+      a.X[3 * e + 2] = X[2];
+      const mmt_kp kp = a.keys[i];
+      a.obs[3 * e] = kp.x;
+      a.obs[3 * e + 1] = kp.y;
+      a.obs[3 * e + 2] = a.uR[i];
+      a.s2[e] = a.inv_sigma2[kp.octave];
+    }
+    base += tot;
+  }
+  if (t == 0) a.desc->n = base;
+}
+
+void launch_map_edges(const MapEdgeArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_map_edges, dim3(1), dim3(1024), 0, st, a);
   MMT_HIP(hipGetLastError());
 }
 

@@ -361,8 +361,10 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   // copies the map bookkeeping reads (keys, descriptors, mvuRight, mvDepth)
   launch_stereo_grid(d_kps_, d_nkp_, kcap_, d_depth_, npix, W_, H_, cfg_.bf, grid0_.invW,
                      grid0_.invH, d_uR_, d_kdepth_, d_cell_start_, d_cell_idx_, nframes, st);
-  chunk_buf_ ^= 1;
-  const HostChunk& hc = hc_[chunk_buf_];
+  // the host copies go to the buffer the last frame does not live in; it becomes the current one
+  // only once the chunk's ORB passed its device checks (a failed chunk leaves no trace)
+  const int nbuf = chunk_buf_ ^ 1;
+  const HostChunk& hc = hc_[nbuf];
   MMT_HIP(hipMemcpyAsync(hc.kps, d_kps_, sizeof(mmt_kp) * (size_t)kcap_ * nframes,
                          hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(hc.desc, d_desc_, 32 * (size_t)kcap_ * nframes, hipMemcpyDeviceToHost,
@@ -374,6 +376,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   std::vector<int> nkp(nframes);
   MMT_HIP(hipMemcpyAsync(nkp.data(), d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));
   engine_->check_flags(st);  // synchronises st; throws on a tripped octree guard
+  chunk_buf_ = nbuf;
   if (prof_) {
     float ms = 0;
     MMT_HIP(hipEventElapsedTime(&ms, ev_orb_[0], ev_orb_[1]));

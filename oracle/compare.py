@@ -22,14 +22,17 @@ MAP_INT = ("map_state", "map_matches_mm", "map_inliers_local", "n_keyframes", "n
 
 
 def pose_diff(a, b):
-    """(max abs diff, max diff in float32 ulps of the oracle entry, max diff over the entries
-    that fail both POSE_TOL and POSE_ULPS) of two 4x4 float32 poses."""
+    """(max abs diff, max diff in float32 ulps of the oracle entry over the entries at or above
+    POSE_TOL (0 when none is), max diff over the entries that fail both POSE_TOL and POSE_ULPS)
+    of two 4x4 float32 poses."""
     a = np.asarray(a, np.float32)
     b = np.asarray(b, np.float32)
     d = np.abs(a.astype(np.float64) - b.astype(np.float64))
     ulps = d / np.spacing(np.abs(b)).astype(np.float64)
-    fail = (d >= POSE_TOL) & (ulps > POSE_ULPS)
-    return float(d.max()), float(ulps.max()), float(d[fail].max()) if fail.any() else 0.0
+    big = d >= POSE_TOL
+    fail = big & (ulps > POSE_ULPS)
+    return (float(d.max()), float(ulps[big].max()) if big.any() else 0.0,
+            float(d[fail].max()) if fail.any() else 0.0)
 
 
 def compare_frame(g, o):

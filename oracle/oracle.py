@@ -135,10 +135,12 @@ def flow_solve(obs, flow, depth, tcw_last, init, rp_thres, prior_info, max_iters
     tl = np.ascontiguousarray(tcw_last, np.float32).reshape(16)
     ini = np.ascontiguousarray(init, np.float32).reshape(16)
     pose = np.zeros(16, np.float32)
-    st = np.zeros(3, np.int32)
+    st = np.zeros(6, np.int32)
     rc = L.oracle_flow_solve(len(depth), _p(obs), _p(flow), _p(depth), _p(tl), _p(ini), rp_thres,
                              prior_info, max_iters, K[0], K[1], K[2], K[3], _p(pose), _p(st))
-    return rc, pose.reshape(4, 4), dict(iterations=int(st[0]), inliers=int(st[1]))
+    return rc, pose.reshape(4, 4), dict(iterations=int(st[0]), inliers=int(st[1]),
+                                        rejections=int(st[3]), clean_rejections=int(st[4]),
+                                        max_reject_run=int(st[5]))
 
 
 def pose_optimization(Xw, obs, inv_sigma2, tcw, K, bf):

@@ -153,6 +153,9 @@ int oracle_flow_solve(int n, const float* obs, const float* flow, const float* d
   stats3[0] = st.iterations;
   stats3[1] = st.inliers;
   stats3[2] = st.status;
+  stats3[3] = st.rejections;
+  stats3[4] = st.clean_rejections;
+  stats3[5] = st.max_reject_run;
   return rc;
 }
 

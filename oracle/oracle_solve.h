@@ -22,6 +22,9 @@ struct FlowProblem {
 };
 struct FlowSolveStats {
   int iterations = 0, inliers = 0, status = 0;
+  // test statistics: rejected trials, those on a system without Huber-active edges (where the GPU
+  // serves the next trials from its lambda candidate table) and the longest rejection run
+  int rejections = 0, clean_rejections = 0, max_reject_run = 0;
 };
 int flow_pose_solve(const FlowProblem& p, float pose_out[16], FlowSolveStats* st);
 

@@ -379,6 +379,7 @@ int flow_pose_solve(const FlowProblem& P, float pose_out[16], FlowSolveStats* st
     const double iniChi = currentChi;
     // buildSystem at the current state
     double Hpp[6][6] = {{0}}, bp[6] = {0};
+    bool clean = true;  // no Huber-active edge at this linearisation (test statistic)
     for (int i = 0; i < N; i++) {
       double pc[3];
       se3_map(pose, E[i].Xw, pc);
@@ -390,6 +391,7 @@ int flow_pose_solve(const FlowProblem& P, float pose_out[16], FlowSolveStats* st
       double r0, r1;
       huber(e2, dsqr, delta, r0, r1);
       const double w = kInfo * r1;
+      if (e2 > dsqr) clean = false;
       const double om[2] = {-w * err[2 * i], -w * err[2 * i + 1]};  // rho' * (-Omega e)
       for (int a = 0; a < 6; a++) {
         for (int b = 0; b < 6; b++) Hpp[a][b] += J[0][a] * w * J[0][b] + J[1][a] * w * J[1][b];
@@ -410,7 +412,7 @@ int flow_pose_solve(const FlowProblem& P, float pose_out[16], FlowSolveStats* st
       nBad = 0;
     }
     double rho = 0;
-    int qmax = 0;
+    int qmax = 0, run = 0;
     double lastTrialChi = 0;
     do {
       const SE3 pose_b = pose;
@@ -476,6 +478,11 @@ int flow_pose_solve(const FlowProblem& P, float pose_out[16], FlowSolveStats* st
         ni *= 2;
         pose = pose_b;
         f = fb;
+        if (st) {
+          st->rejections++;
+          if (clean) st->clean_rejections++;  // the next trial's solve differs only in lambda
+          st->max_reject_run = std::max(st->max_reject_run, ++run);
+        }
       }
       qmax++;
     } while (rho < 0 && qmax < 10);

@@ -42,6 +42,30 @@ def test_flow_solve_matches_oracle(ctx, oracle_mod, seed, n, out, ego):
         assert st_g["iterations"] == st_o["iterations"]
 
 
+@pytest.mark.parametrize("seed,n,noise,ego", [(24, 200, 0.0, True), (24, 200, 0.02, False),
+                                               (3, 40, 0.0, False), (24, 40, 0.02, True)])
+def test_flow_solve_rejection_chains_bit_exact(ctx, oracle_mod, seed, n, noise, ego,
+                                               monkeypatch):
+    """The lambda candidate table of the flow LM: after a rejection on a system without
+    Huber-active edges the next trials take their increment and pose from candidates solved in
+    advance for lambda * ni, ...  These problems (large motion, little noise) reject several
+    trials in a row on clean systems (the oracle counts them), so candidates 1-3 are used; the
+    solve must be bit-identical to one that solves every trial for its own lambda
+    (MMT_LM_MAX_CAND=1), and agree with the oracle within 1e-4."""
+    obs, flow, depth, Tl, init, _ = flow_problem(seed, n, outlier_frac=0.0, pix_noise=noise,
+                                                 motion=0.3)
+    args = (0.04, 0.3, 100) if ego else (0.01, 0.5, 200)
+    rc, pose_o, st_o = oracle_mod.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    assert st_o["clean_rejections"] >= 4 and st_o["max_reject_run"] >= 4, st_o
+    status4, pose4, st4 = ctx.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    monkeypatch.setenv("MMT_LM_MAX_CAND", "1")
+    status1, pose1, st1 = ctx.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    assert status4 == status1 == rc == 0
+    assert np.array_equal(pose4, pose1) and st4 == st1
+    assert np.abs(pose4 - pose_o).max() < POSE_TOL
+    assert st4["inliers"] == st_o["inliers"]
+
+
 def test_flow_solve_too_few_edges(ctx):
     obs, flow, depth, Tl, init, _ = flow_problem(8, 2)
     status, _, st = ctx.flow_solve(obs, flow, depth, Tl, init, 0.04, 0.3, 100, K_KITTI)
@@ -194,6 +218,26 @@ def test_track_reports_orb_device_flags(kitti_frames):
     r = c.track(f["bgr"], f["disp"], f["flow"], f["sem"])
     assert r["n_keys"] > 500
     c.close()
+
+
+def test_track_continues_after_device_error(oracle_mod, kitti_frames):
+    """A call whose ORB trips a device guard tracks none of its frames and leaves the context as
+    the previous call left it: tracking the sequence on without mmt_reset matches the oracle
+    tracking it with the failed frame absent."""
+    import multimot_track_amd as M
+    c = M.Context(M.kitti03_config(nfeatures=2000))
+    tr = oracle_mod.Tracker(1242, 375, K_KITTI, 387.5744, 0, 2000)
+    try:
+        for i, f in enumerate(kitti_frames):
+            if i == 2:
+                c.debug_orb_raise(2)
+                with pytest.raises(M.MmtError, match="octree-node-capacity"):
+                    c.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            g = c.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            o = tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            _compare_frame(g, o, i)
+    finally:
+        c.close()
 
 
 def split_labels(sem, parts=5):

@@ -18,8 +18,13 @@ for r in rows:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     q = r.get("Queue_Id", r.get("Stream_Id", "?"))
     ks.append((s, e, q, name.split("(")[0].replace("void ", "")))
+# memory copies (rocprofv3 --memory-copy-trace), shown as "copy <direction> <bytes>"
+for fc in glob.glob(os.path.join(os.path.dirname(f), "*memory_copy_trace.csv")):
+    for r in csv.DictReader(open(fc)):
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        ks.append((s, e, "cp", "copy %s %s B" % (r.get("Direction", "?"), r.get("Size", "?"))))
 ks.sort()
-end = ks[-1][1]
+end = max(k[1] for k in ks)
 t0 = end - tail_ms * 1e6
 busy = {}
 for s, e, q, n in ks:
