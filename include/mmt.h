@@ -17,6 +17,10 @@
  *                       <- the same, over many frames (ORB extraction is stateless per frame)
  *   mmt_track_rgbd      <- System::TrackRGBD(im, depthmap, flowmap, masksem, ...) System.h:73-75,
  *                          System.cc:169-220 -> Tracking::GrabImageRGBD Tracking.cc:438-919
+ *   mmt_track_rgbd_chunk / _chunk_device
+ *                       <- the same over consecutive frames of the sequence (rgbd_tum.cc:158-176
+ *                          calls it once per frame; frames of one sequence are a strict chain,
+ *                          only ORB extraction is batched)
  *   mmt_pose_flow_solve <- Optimizer::PoseOptimizationFlow2Cam / PoseOptimizationFlow2
  *                          Optimizer.h:43-56, Optimizer.cc:396-601 / 2170-2377
  *   mmt_pose_optimization <- Optimizer::PoseOptimization(Frame*) Optimizer.cc:3121-3339
@@ -157,6 +161,21 @@ int mmt_orb_device_status(mmt_ctx* ctx, void* stream);
 int mmt_track_rgbd(mmt_ctx* ctx, const uint8_t* bgr, const uint16_t* disp256,
                    const float* flow_uv, const int32_t* mask, double timestamp,
                    mmt_frame_result* res, mmt_motion* objs, int objs_cap);
+
+/* System::TrackRGBD over nframes consecutive frames in host memory, one pointer per frame and
+ * input (layouts as mmt_track_rgbd): the frames are staged on the device and tracked as one chunk
+ * (batched ORB, then frame by frame), like mmt_track_rgbd_chunk_device.  nframes <=
+ * config.max_batch; res[nframes], objs[nframes * objs_cap].  Frames in pinned memory from
+ * mmt_host_alloc reach the GPU by DMA at full PCIe rate. */
+int mmt_track_rgbd_chunk(mmt_ctx* ctx, int nframes, const uint8_t* const* bgr,
+                         const uint16_t* const* disp256, const float* const* flow_uv,
+                         const int32_t* const* mask, mmt_frame_result* res, mmt_motion* objs,
+                         int objs_cap);
+
+/* Page-locked host memory on the context's device (hipHostMalloc), for frames the caller decodes
+ * and hands to the host-buffer entry points.  NULL on failure; release with mmt_host_free. */
+void* mmt_host_alloc(mmt_ctx* ctx, size_t bytes);
+void mmt_host_free(mmt_ctx* ctx, void* p);
 
 /* Device-resident chunk of consecutive frames of the context's sequence (pitches in bytes):
  * ORB extraction is batched over the chunk, tracking then runs frame by frame.  res[nframes],

@@ -7,7 +7,12 @@
 // mmt_track_rgbd.
 //
 //   rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence [--realtime] [--nfeatures N]
-//            [--device D] [--noise-seed S] [--poses out.txt]
+//            [--device D] [--noise-seed S] [--poses out.txt] [--chunk F] [--threads T]
+//
+// Input decoding (PNG, .flo, text masks) runs on T host threads (default: up to 16) into pinned
+// buffers from mmt_host_alloc, ahead of the tracker, and frames go to the GPU F at a time through
+// mmt_track_rgbd_chunk (batched ORB; default F = 16, --chunk 1 tracks frame by frame, as
+// --realtime does).  The tracking-time statistics then give each frame its chunk's time / F.
 //
 // Differences from the reference binary: the vocabulary is not read (this path
 // never uses BoW); no viewer, no imshow/waitKey; the usleep pacing to the timestamps is off
@@ -22,6 +27,9 @@
 #include <thread>
 #include <vector>
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 
 #include "../../include/mmt.h"
 #include "mmt_io.h"
@@ -172,6 +180,8 @@ int main(int argc, char** argv) {
   int nfeat = -1, device = 0;
   unsigned seed = 0;
   std::string poses_out;
+  int chunk = 16;
+  int threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   for (int i = 1; i < argc; i++) {
     const std::string a = argv[i];
     if (a == "--realtime") realtime = true;
@@ -179,11 +189,14 @@ int main(int argc, char** argv) {
     else if (a == "--device" && i + 1 < argc) device = atoi(argv[++i]);
     else if (a == "--noise-seed" && i + 1 < argc) seed = (unsigned)strtoul(argv[++i], nullptr, 10);
     else if (a == "--poses" && i + 1 < argc) poses_out = argv[++i];
+    else if (a == "--chunk" && i + 1 < argc) chunk = std::max(1, atoi(argv[++i]));
+    else if (a == "--threads" && i + 1 < argc) threads = std::max(1, atoi(argv[++i]));
     else pos.push_back(a);
   }
   if (pos.size() != 3) {
     fprintf(stderr, "\nUsage: ./rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence "
-                    "[--realtime] [--nfeatures N] [--device D] [--noise-seed S] [--poses file]\n");
+                    "[--realtime] [--nfeatures N] [--device D] [--noise-seed S] [--poses file] "
+                    "[--chunk F] [--threads T]\n");
     return 1;
   }
   const std::string settings = pos[1], seq = pos[2];
@@ -246,7 +259,8 @@ int main(int argc, char** argv) {
   cfg.orb_min_th_fast = (int)get("ORBextractor.minThFAST", 7);
   cfg.noise_seed = seed;
   cfg.device_id = device;
-  cfg.max_batch = 1;
+  if (realtime) chunk = 1;  // pacing is per frame
+  cfg.max_batch = chunk;
   cfg.fps = (float)get("Camera.fps", 0);
   // image size from the first frame when the settings omit it
   int w0 = 0, h0 = 0, ch0 = 0, db0 = 0;
@@ -268,9 +282,90 @@ int main(int argc, char** argv) {
   }
   const int W = cfg.width, H = cfg.height;
   const size_t npix = (size_t)W * H;
-  std::vector<int32_t> mask(npix);
-  std::vector<uint16_t> disp(npix);
-  std::vector<mmt_motion> objs(64);
+  const int F = chunk;
+  // ---- decode pipeline: a ring of 2F pinned frame slots filled by `threads` workers in frame
+  // order of claim; the tracker consumes them F at a time
+  struct Slot {
+    uint8_t* bgr = nullptr;
+    uint16_t* disp = nullptr;
+    float* flow = nullptr;
+    int32_t* mask = nullptr;
+    int frame = -1;   // frame held (ready when == the frame asked for)
+    int status = 0;   // 0 ok, 1 image, 2 depth, 3 flow failed
+  };
+  const int R = 2 * F;
+  std::vector<Slot> slots(R);
+  for (Slot& sl : slots) {
+    sl.bgr = (uint8_t*)mmt_host_alloc(ctx, npix * 3);
+    sl.disp = (uint16_t*)mmt_host_alloc(ctx, npix * 2);
+    sl.flow = (float*)mmt_host_alloc(ctx, npix * 8);
+    sl.mask = (int32_t*)mmt_host_alloc(ctx, npix * 4);
+    if (!sl.bgr || !sl.disp || !sl.flow || !sl.mask) {
+      fprintf(stderr, "mmt_host_alloc failed\n");
+      return 1;
+    }
+  }
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<int> next{0};
+  int consumed = 0;  // frames the tracker has released
+  bool stop = false;
+  auto decode = [&](int ni, Slot& sl) {
+    int w, h, ch, db;
+    void* img = nullptr;
+    if (mmt_io_read_png(frame_name(seq, "image", ni, ".png").c_str(), &w, &h, &ch, &db, &img) != 0 ||
+        w != W || h != H || ch != 3 || db != 1) {
+      mmt_io_free(img);
+      return 1;
+    }
+    memcpy(sl.bgr, img, npix * 3);
+    mmt_io_free(img);
+    int dw, dh, dch, ddb;
+    void* dimg = nullptr;
+    if (mmt_io_read_png(frame_name(seq, "depth", ni, ".png").c_str(), &dw, &dh, &dch, &ddb, &dimg) != 0 ||
+        dw != W || dh != H || dch != 1) {
+      mmt_io_free(dimg);
+      return 2;
+    }
+    for (size_t p = 0; p < npix; p++)  // imD.convertTo(CV_32F): the u16 (or u8) samples as read
+      sl.disp[p] = ddb == 2 ? ((uint16_t*)dimg)[p] : ((uint8_t*)dimg)[p];
+    mmt_io_free(dimg);
+    float* flow = nullptr;
+    int fw = 0, fh = 0;
+    if (mmt_io_read_flo(frame_name(seq, "flow", ni, ".flo").c_str(), &fw, &fh, &flow) != 0 ||
+        fw != W || fh != H) {
+      mmt_io_free(flow);
+      return 3;
+    }
+    memcpy(sl.flow, flow, npix * 8);
+    mmt_io_free(flow);
+    std::fill(sl.mask, sl.mask + npix, 0);
+    mmt_io_read_mask(frame_name(seq, "semantic", ni, ".txt").c_str(), H, W, sl.mask);
+    return 0;
+  };
+  std::vector<std::thread> workers;
+  for (int t = 0; t < threads; t++)
+    workers.emplace_back([&] {
+      for (;;) {
+        const int ni = next.fetch_add(1);
+        if (ni >= nImages) return;
+        Slot& sl = slots[ni % R];
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return stop || ni < consumed + R; });  // the slot's last frame left
+          if (stop) return;
+        }
+        const int st = decode(ni, sl);
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          sl.status = st;
+          sl.frame = ni;
+        }
+        cv.notify_all();
+      }
+    });
+  std::vector<mmt_motion> objs(64 * F);
+  std::vector<mmt_frame_result> res(F);
   std::vector<float> track_times(nImages);
   FILE* fp = poses_out.empty() ? nullptr : fopen(poses_out.c_str(), "w");
   float lastTcw[16], lastGt[16];
@@ -278,85 +373,109 @@ int main(int argc, char** argv) {
 
   printf("\n-------\nStart processing sequence ...\nImages in the sequence: %d\n\n", nImages);
   int rc_all = 0;
-  for (int ni = 0; ni < nImages; ni++) {
-    printf("\n=======================================================\n");
-    printf("Processing Frame: %d\n", ni);
-    int w, h, ch, db;
-    void* img = nullptr;
-    void* dimg = nullptr;
-    float* flow = nullptr;
-    int fw = 0, fh = 0;
-    if (mmt_io_read_png(frame_name(seq, "image", ni, ".png").c_str(), &w, &h, &ch, &db, &img) != 0 ||
-        w != W || h != H || ch != 3 || db != 1) {
-      fprintf(stderr, "\nFailed to load image at: %s\n", frame_name(seq, "image", ni, ".png").c_str());
-      rc_all = 1;
-      mmt_io_free(img);
-      break;
+  int done = 0;
+  const auto t_start = std::chrono::steady_clock::now();
+  while (done < nImages && !rc_all) {
+    const int nf = std::min(F, nImages - done);
+    int nok = nf;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      for (int k = 0; k < nf; k++) {
+        Slot& sl = slots[(done + k) % R];
+        cv.wait(lk, [&] { return sl.frame == done + k; });
+        if (sl.status != 0 && nok == nf) nok = k;
+      }
     }
-    int dw, dh, dch, ddb;
-    if (mmt_io_read_png(frame_name(seq, "depth", ni, ".png").c_str(), &dw, &dh, &dch, &ddb, &dimg) != 0 ||
-        dw != W || dh != H || dch != 1) {
-      fprintf(stderr, "\nFailed to load depth at: %s\n", frame_name(seq, "depth", ni, ".png").c_str());
-      rc_all = 1;
-      mmt_io_free(img);
-      mmt_io_free(dimg);
-      break;
+    std::vector<const uint8_t*> pb(nf);
+    std::vector<const uint16_t*> pd(nf);
+    std::vector<const float*> pf(nf);
+    std::vector<const int32_t*> pm(nf);
+    for (int k = 0; k < nf; k++) {
+      const Slot& sl = slots[(done + k) % R];
+      pb[k] = sl.bgr;
+      pd[k] = sl.disp;
+      pf[k] = sl.flow;
+      pm[k] = sl.mask;
     }
-    for (size_t p = 0; p < npix; p++)
-      disp[p] = ddb == 2 ? ((uint16_t*)dimg)[p] : ((uint8_t*)dimg)[p];  // imD.convertTo(CV_32F)
-    if (mmt_io_read_flo(frame_name(seq, "flow", ni, ".flo").c_str(), &fw, &fh, &flow) != 0 ||
-        fw != W || fh != H) {
-      fprintf(stderr, "\nFailed to load flow at: %s\n", frame_name(seq, "flow", ni, ".flo").c_str());
-      rc_all = 1;
-      mmt_io_free(img);
-      mmt_io_free(dimg);
-      mmt_io_free(flow);
-      break;
+    int rc = 0;
+    double tchunk = 0;
+    if (nok > 0) {
+      const auto t1 = std::chrono::steady_clock::now();
+      rc = mmt_track_rgbd_chunk(ctx, nok, pb.data(), pd.data(), pf.data(), pm.data(), res.data(),
+                                objs.data(), 64);
+      tchunk = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     }
-    std::fill(mask.begin(), mask.end(), 0);
-    mmt_io_read_mask(frame_name(seq, "semantic", ni, ".txt").c_str(), H, W, mask.data());
-    const auto t1 = std::chrono::steady_clock::now();
-    mmt_frame_result res;
-    const int rc = mmt_track_rgbd(ctx, (const uint8_t*)img, disp.data(), flow, mask.data(),
-                                  times[ni], &res, objs.data(), (int)objs.size());
-    const auto t2 = std::chrono::steady_clock::now();
-    mmt_io_free(img);
-    mmt_io_free(dimg);
-    mmt_io_free(flow);
     if (rc != 0) {
       fprintf(stderr, "mmt_track_rgbd failed (%d): %s\n", rc, mmt_last_error(ctx));
       rc_all = 1;
       break;
     }
-    const double ttrack = std::chrono::duration<double>(t2 - t1).count();
-    track_times[ni] = (float)ttrack;
-    const float* Tgt = (ni < ngt) ? gt + 16 * ni : nullptr;
-    if (haveLast && res.initialized && Tgt) print_camera_rpe(res.Tcw, lastTcw, Tgt, lastGt);
-    const float* Tlw_gt = (ni > 0 && ni - 1 < ngt) ? gt + 16 * (ni - 1) : nullptr;
-    for (int k = 0; k < res.n_objects && k < (int)objs.size(); k++) {
-      const mmt_motion& m = objs[k];
-      printf("object %d (semantic label %d): %d points, %d RANSAC inliers, %d inliers; motion t = "
-             "[%.4f %.4f %.4f]\n", m.label, m.sem_label, m.n_points, m.n_ransac_inliers,
-             m.n_inliers, m.world_motion[3], m.world_motion[7], m.world_motion[11]);
-      if (ni > 0)
-        print_object_eval(m, Tlw_gt, Tgt, obj_rows[ni - 1], obj_rows[ni]);
+    for (int k = 0; k < nok; k++) {
+      const int ni = done + k;
+      printf("\n=======================================================\n");
+      printf("Processing Frame: %d\n", ni);
+      const mmt_frame_result& r = res[k];
+      const double ttrack = tchunk / nok;
+      track_times[ni] = (float)ttrack;
+      const float* Tgt = (ni < ngt) ? gt + 16 * ni : nullptr;
+      if (haveLast && r.initialized && Tgt) print_camera_rpe(r.Tcw, lastTcw, Tgt, lastGt);
+      const float* Tlw_gt = (ni > 0 && ni - 1 < ngt) ? gt + 16 * (ni - 1) : nullptr;
+      for (int o = 0; o < r.n_objects && o < 64; o++) {
+        const mmt_motion& m = objs[64 * k + o];
+        printf("object %d (semantic label %d): %d points, %d RANSAC inliers, %d inliers; motion t = "
+               "[%.4f %.4f %.4f]\n", m.label, m.sem_label, m.n_points, m.n_ransac_inliers,
+               m.n_inliers, m.world_motion[3], m.world_motion[7], m.world_motion[11]);
+        if (ni > 0)
+          print_object_eval(m, Tlw_gt, Tgt, obj_rows[ni - 1], obj_rows[ni]);
+      }
+      if (fp) {
+        fprintf(fp, "%d", ni);
+        for (int q = 0; q < 16; q++) fprintf(fp, " %.9f", r.Tcw[q]);
+        fprintf(fp, "\n");
+      }
+      if (r.initialized && Tgt) {
+        memcpy(lastTcw, r.Tcw, sizeof(lastTcw));
+        memcpy(lastGt, Tgt, sizeof(lastGt));
+        haveLast = true;
+      }
+      if (realtime) {  // rgbd_tum.cc:180-188 (chunks of one frame)
+        double T = 0;
+        if (ni < nImages - 1) T = times[ni + 1] - times[ni];
+        else if (ni > 0) T = times[ni] - times[ni - 1];
+        if (ttrack < T) std::this_thread::sleep_for(std::chrono::duration<double>(T - ttrack));
+      }
     }
-    if (fp) {
-      fprintf(fp, "%d", ni);
-      for (int k = 0; k < 16; k++) fprintf(fp, " %.9f", res.Tcw[k]);
-      fprintf(fp, "\n");
+    if (nok < nf) {
+      const int ni = done + nok;
+      static const char* what[4] = {"", "image", "depth", "flow"};
+      static const char* sub[4] = {"", "image", "depth", "flow"};
+      static const char* ext[4] = {"", ".png", ".png", ".flo"};
+      const int st = slots[ni % R].status;
+      printf("\n=======================================================\n");
+      printf("Processing Frame: %d\n", ni);
+      fprintf(stderr, "\nFailed to load %s at: %s\n", what[st],
+              frame_name(seq, sub[st], ni, ext[st]).c_str());
+      rc_all = 1;
     }
-    if (res.initialized && Tgt) {
-      memcpy(lastTcw, res.Tcw, sizeof(lastTcw));
-      memcpy(lastGt, Tgt, sizeof(lastGt));
-      haveLast = true;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done += nf;
+      consumed = done;
     }
-    if (realtime) {  // rgbd_tum.cc:180-188
-      double T = 0;
-      if (ni < nImages - 1) T = times[ni + 1] - times[ni];
-      else if (ni > 0) T = times[ni] - times[ni - 1];
-      if (ttrack < T) std::this_thread::sleep_for(std::chrono::duration<double>(T - ttrack));
-    }
+    cv.notify_all();
+  }
+  const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    stop = true;
+  }
+  cv.notify_all();
+  for (std::thread& t : workers) t.join();
+  for (Slot& sl : slots) {
+    mmt_host_free(ctx, sl.bgr);
+    mmt_host_free(ctx, sl.disp);
+    mmt_host_free(ctx, sl.flow);
+    mmt_host_free(ctx, sl.mask);
   }
   if (fp) fclose(fp);
   mmt_destroy(ctx);
@@ -371,5 +490,7 @@ int main(int argc, char** argv) {
   printf("-------------------------------------------------------------------\n");
   printf("median tracking time: %g\n", sorted[nImages / 2]);
   printf("mean tracking time: %g\n", total / nImages);
+  printf("end-to-end (decode + track): %d frames in %.3f s, %.1f frames/s (%d decode threads, "
+         "chunks of %d)\n", nImages, wall, nImages / wall, threads, F);
   return 0;
 }

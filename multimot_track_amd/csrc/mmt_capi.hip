@@ -392,31 +392,82 @@ int mmt_track_rgbd_chunk_device(mmt_ctx* ctx, int nframes, const uint8_t* d_bgr,
   });
 }
 
+// device staging of the host-buffer entry points, nframes frames (frame-major, tight pitches)
+static void ensure_track_staging(mmt_ctx* ctx, int nframes) {
+  if (ctx->t_frames >= nframes) return;
+  const size_t npix = (size_t)ctx->cfg.width * ctx->cfg.height;
+  (void)hipFree(ctx->t_bgr);
+  (void)hipFree(ctx->t_disp);
+  (void)hipFree(ctx->t_flow);
+  (void)hipFree(ctx->t_mask);
+  ctx->t_bgr = nullptr;
+  ctx->t_disp = nullptr;
+  ctx->t_flow = nullptr;
+  ctx->t_mask = nullptr;
+  ctx->t_frames = 0;
+  MMT_HIP(hipMalloc((void**)&ctx->t_bgr, npix * 3 * nframes));
+  MMT_HIP(hipMalloc((void**)&ctx->t_disp, npix * 2 * nframes));
+  MMT_HIP(hipMalloc((void**)&ctx->t_flow, npix * 8 * nframes));
+  MMT_HIP(hipMalloc((void**)&ctx->t_mask, npix * 4 * nframes));
+  ctx->t_frames = nframes;
+}
+
+static void track_host_frames(mmt_ctx* ctx, int nframes, const uint8_t* const* bgr,
+                              const uint16_t* const* disp, const float* const* flow,
+                              const int32_t* const* mask, mmt_frame_result* res, mmt_motion* objs,
+                              int objs_cap) {
+  MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+  ensure_tracker(ctx);
+  ensure_track_staging(ctx, nframes);
+  const size_t npix = (size_t)ctx->cfg.width * ctx->cfg.height;
+  hipStream_t s = ctx->stream;
+  for (int f = 0; f < nframes; f++) {
+    MMT_HIP(hipMemcpyAsync(ctx->t_bgr + npix * 3 * f, bgr[f], npix * 3, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(ctx->t_disp + npix * f, disp[f], npix * 2, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(ctx->t_flow + npix * 2 * f, flow[f], npix * 8, hipMemcpyHostToDevice, s));
+    MMT_HIP(hipMemcpyAsync(ctx->t_mask + npix * f, mask[f], npix * 4, hipMemcpyHostToDevice, s));
+  }
+  std::vector<mmt::FrameOut> outs;
+  ctx->tracker.track_chunk(ctx->t_bgr, npix * 3, ctx->t_disp, npix * 2, ctx->t_flow, npix * 8,
+                           ctx->t_mask, npix * 4, nframes, outs, s);
+  fill_results(outs, res, objs, objs_cap);
+}
+
 int mmt_track_rgbd(mmt_ctx* ctx, const uint8_t* bgr, const uint16_t* disp256,
                    const float* flow_uv, const int32_t* mask, double timestamp,
                    mmt_frame_result* res, mmt_motion* objs, int objs_cap) {
   (void)timestamp;
   if (!ctx || !bgr || !disp256 || !flow_uv || !mask || !res) return MMT_EINVAL;
   return guard(ctx, [&] {
-    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
-    ensure_tracker(ctx);
-    const size_t npix = (size_t)ctx->cfg.width * ctx->cfg.height;
-    if (!ctx->t_bgr) {
-      MMT_HIP(hipMalloc((void**)&ctx->t_bgr, npix * 3));
-      MMT_HIP(hipMalloc((void**)&ctx->t_disp, npix * 2));
-      MMT_HIP(hipMalloc((void**)&ctx->t_flow, npix * 8));
-      MMT_HIP(hipMalloc((void**)&ctx->t_mask, npix * 4));
-    }
-    hipStream_t s = ctx->stream;
-    MMT_HIP(hipMemcpyAsync(ctx->t_bgr, bgr, npix * 3, hipMemcpyHostToDevice, s));
-    MMT_HIP(hipMemcpyAsync(ctx->t_disp, disp256, npix * 2, hipMemcpyHostToDevice, s));
-    MMT_HIP(hipMemcpyAsync(ctx->t_flow, flow_uv, npix * 8, hipMemcpyHostToDevice, s));
-    MMT_HIP(hipMemcpyAsync(ctx->t_mask, mask, npix * 4, hipMemcpyHostToDevice, s));
-    std::vector<mmt::FrameOut> outs;
-    ctx->tracker.track_chunk(ctx->t_bgr, npix * 3, ctx->t_disp, npix * 2, ctx->t_flow, npix * 8,
-                             ctx->t_mask, npix * 4, 1, outs, s);
-    fill_results(outs, res, objs, objs_cap);
+    track_host_frames(ctx, 1, &bgr, &disp256, &flow_uv, &mask, res, objs, objs_cap);
   });
+}
+
+int mmt_track_rgbd_chunk(mmt_ctx* ctx, int nframes, const uint8_t* const* bgr,
+                         const uint16_t* const* disp256, const float* const* flow_uv,
+                         const int32_t* const* mask, mmt_frame_result* res, mmt_motion* objs,
+                         int objs_cap) {
+  if (!ctx || !bgr || !disp256 || !flow_uv || !mask || !res || nframes < 1) return MMT_EINVAL;
+  for (int f = 0; f < nframes; f++)
+    if (!bgr[f] || !disp256[f] || !flow_uv[f] || !mask[f]) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    if (nframes > std::max(1, ctx->cfg.max_batch))
+      throw ArgError("chunk larger than config.max_batch");
+    track_host_frames(ctx, nframes, bgr, disp256, flow_uv, mask, res, objs, objs_cap);
+  });
+}
+
+void* mmt_host_alloc(mmt_ctx* ctx, size_t bytes) {
+  if (!ctx || bytes == 0) return nullptr;
+  void* p = nullptr;
+  if (hipSetDevice(ctx->cfg.device_id) != hipSuccess) return nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void mmt_host_free(mmt_ctx* ctx, void* p) {
+  (void)ctx;
+  if (p) (void)hipHostFree(p);
 }
 
 int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* pr, float* pose_out,

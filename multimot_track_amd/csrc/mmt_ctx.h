@@ -23,4 +23,5 @@ struct mmt_ctx {
   uint16_t* t_disp = nullptr;
   float* t_flow = nullptr;
   int32_t* t_mask = nullptr;
+  int t_frames = 0;  // frames the t_* staging buffers hold
 };
