@@ -109,6 +109,14 @@ class OrbEngine {
   // (GPU_MAX_HW_QUEUES), and streams beyond them end up sharing the caller's queue.
   hipStream_t side_ = nullptr;
   hipEvent_t ev_pyr_ = nullptr, ev_blur_ = nullptr, ev_gray_ = nullptr;
+  // the batch split into parts with launch sequences of their own (MMT_ORB_PARTS, default 1: measured slower at 2 and 4, the window is throughput-bound):
+  // one part's latency-bound launches (resize chain, octree) overlap another's FAST / blur
+  static constexpr int kMaxParts = 4;
+  int parts_ = 1;
+  hipStream_t pstream_[kMaxParts][2] = {};
+  hipEvent_t pev_[kMaxParts][4] = {};  // gray, pyramid, blur, part done
+  void run_part(int f0, int nf, hipStream_t st_main, hipStream_t st_side, hipEvent_t* ev,
+                mmt_kp* d_kps, uint8_t* d_desc, int cap_per_frame, int* d_n);
   int iniTh_ = 20, minTh_ = 7;
   size_t pyr_stride_ = 0;
   std::vector<LevelInfo> lv_;

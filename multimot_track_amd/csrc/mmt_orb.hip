@@ -1088,6 +1088,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kWaves))) 
                                                  const int* __restrict__ cellcnt, int total_slots,
                                                  uint32_t* __restrict__ lkeys,
                                                  uint32_t* __restrict__ knode_g,
+                                                 uint8_t* __restrict__ kq_g,
                                                  uint32_t* __restrict__ okeys, int out_slots,
                                                  int* __restrict__ ocount, int nlevels,
                                                  int ncap, int kcap, int level_begin,
@@ -1146,8 +1147,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kWaves))) 
     // global scratch: knode as u16 in the u32 slots, quadrant bytes after all frames' knode
     uint32_t* lk = lkeys + (size_t)frame * total_slots + L0.key_off;
     uint16_t* knode = (uint16_t*)(knode_g + (size_t)frame * total_slots + L0.key_off);
-    uint8_t* kq = (uint8_t*)(knode_g + (size_t)gridDim.x * total_slots) +
-                  (size_t)frame * total_slots + L0.key_off;
+    uint8_t* kq = kq_g + (size_t)frame * total_slots + L0.key_off;
     OctKeys<uint32_t*, uint16_t*, uint8_t*> kk{lk, knode, kq};
     oct_run(S, kk, L0, cells, cnt, nc, fk, n, outp, ocount_p, ncap, err);
   }
@@ -1526,6 +1526,16 @@ void OrbEngine::release() {
   }
   if (side_) (void)hipStreamDestroy(side_);
   side_ = nullptr;
+  for (int q = 0; q < kMaxParts; q++) {
+    for (int k = 0; k < 2; k++) {
+      if (pstream_[q][k]) (void)hipStreamDestroy(pstream_[q][k]);
+      pstream_[q][k] = nullptr;
+    }
+    for (int k = 0; k < 4; k++) {
+      if (pev_[q][k]) (void)hipEventDestroy(pev_[q][k]);
+      pev_[q][k] = nullptr;
+    }
+  }
 }
 
 template <typename T>
@@ -1744,6 +1754,14 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   MMT_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&ev_pyr_, &ev_blur_, &ev_gray_})
     MMT_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  if (const char* e = getenv("MMT_ORB_PARTS")) parts_ = atoi(e);
+  parts_ = std::max(1, std::min(kMaxParts, parts_));
+  if (parts_ > 1)
+    for (int q = 0; q < parts_; q++) {
+      for (int k = 0; k < 2; k++)
+        MMT_HIP(hipStreamCreateWithFlags(&pstream_[q][k], hipStreamNonBlocking));
+      for (int k = 0; k < 4; k++) MMT_HIP(hipEventCreateWithFlags(&pev_[q][k], hipEventDisableTiming));
+    }
   MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
 }
 
@@ -1756,6 +1774,48 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
   if (d_gray != d_pyr_ || frame_pitch != pyr_stride_)
     MMT_HIP(hipMemcpy2DAsync(d_pyr_, pyr_stride_, d_gray, frame_pitch, lvl0, nframes,
                              hipMemcpyDeviceToDevice, stream));
+  // the batch in parts of at least 16 frames, each on a stream pair of its own once the gray
+  // frames are in; the caller's stream waits for every part
+  const int np = (sched_ & 2) ? 1 : std::max(1, std::min(parts_, nframes / 16));
+  if (np == 1) {
+    run_part(0, nframes, stream, side_, nullptr, d_kps, d_desc, cap_per_frame, d_n);
+    MMT_HIP(hipGetLastError());
+    return;
+  }
+  MMT_HIP(hipEventRecord(ev_gray_, stream));
+  int f0 = 0;
+  for (int q = 0; q < np; q++) {
+    const int nf = nframes / np + (q < nframes % np ? 1 : 0);
+    MMT_HIP(hipStreamWaitEvent(pstream_[q][0], ev_gray_, 0));
+    run_part(f0, nf, pstream_[q][0], pstream_[q][1], pev_[q], d_kps, d_desc, cap_per_frame, d_n);
+    MMT_HIP(hipEventRecord(pev_[q][3], pstream_[q][0]));
+    f0 += nf;
+  }
+  for (int q = 0; q < np; q++) MMT_HIP(hipStreamWaitEvent(stream, pev_[q][3], 0));
+  MMT_HIP(hipGetLastError());
+}
+
+// The launch sequence of frames [f0, f0 + nf) of the batch on a (main, side) stream pair: every
+// per-frame buffer is frame-major, so the part's launches see its frames as frames 0..nf-1 of
+// views offset by f0.  ev: the part's events (nullptr: the engine's own).
+void OrbEngine::run_part(int f0, int nframes, hipStream_t stream, hipStream_t side,
+                         hipEvent_t* ev, mmt_kp* d_kps_all, uint8_t* d_desc_all,
+                         int cap_per_frame, int* d_n_all) {
+  hipEvent_t e_gray = ev ? ev[0] : ev_gray_, e_pyr = ev ? ev[1] : ev_pyr_,
+             e_blur = ev ? ev[2] : ev_blur_;
+  uint8_t* pyr = d_pyr_ + (size_t)f0 * pyr_stride_;
+  uint8_t* blurb = d_blur_ + (size_t)f0 * pyr_stride_;
+  uint32_t* keys = d_keys_ + (size_t)f0 * total_slots_;
+  uint32_t* lkeys = d_lkeys_ + (size_t)f0 * total_slots_;
+  uint32_t* knode = d_knode_ + (size_t)f0 * total_slots_;
+  uint8_t* kq = (uint8_t*)(d_knode_ + (size_t)max_batch_ * total_slots_) +
+                (size_t)f0 * total_slots_;
+  int* cellcnt = d_cellcnt_ + (size_t)f0 * ncells_;
+  uint32_t* okeys = d_okeys_ + (size_t)f0 * out_slots_;
+  int* ocount = d_ocount_ + (size_t)f0 * nlevels_;
+  mmt_kp* d_kps = d_kps_all + (size_t)f0 * cap_per_frame;
+  uint8_t* d_desc = d_desc_all + (size_t)f0 * cap_per_frame * 32;
+  int* d_n = d_n_all + f0;
   // FAST on level 0 needs only the gray frames: it runs on the side stream while the main stream
   // walks the (latency-bound) resize chain; FAST on levels 1.. follows the chain
   const int fs = fast_cols_max_ <= kFSSmall ? kFSSmall : kFSMax;
@@ -1763,30 +1823,30 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
   auto fast = [&](int c0, int c1, hipStream_t st) {
     if (c1 <= c0) return;
     hipLaunchKernelGGL(fs == kFSSmall ? k_fast<kFSSmall> : k_fast<kFSMax>,
-                       dim3((c1 - c0 + 3) / 4, nframes), dim3(256), fast_lds, st, d_pyr_,
-                       pyr_stride_, d_lv_, d_cells_, ncells_, d_keys_, total_slots_, d_cellcnt_,
+                       dim3((c1 - c0 + 3) / 4, nframes), dim3(256), fast_lds, st, pyr,
+                       pyr_stride_, d_lv_, d_cells_, ncells_, keys, total_slots_, cellcnt,
                        iniTh_, minTh_, fast_rows_max_, fast_win_max_, c0, c1);
   };
   auto octree = [&](int l0, int l1, hipStream_t st) {
     // level 0 alone: the full-LDS variant; levels 1..: two workgroups per CU when they fit
     const bool two = l0 > 0 && oct_two_per_cu_;
     hipLaunchKernelGGL(two ? k_octree<8> : k_octree<1>, dim3(nframes, l1 - l0), dim3(1024),
-                       two ? octree_lds1_ : octree_lds_, st, d_lv_, d_cells_, ncells_, d_keys_,
-                       d_cellcnt_, total_slots_, d_lkeys_, d_knode_, d_okeys_, out_slots_,
-                       d_ocount_, nlevels_, node_cap_, two ? key_cap1_ : key_cap_, l0, d_err_);
+                       two ? octree_lds1_ : octree_lds_, st, d_lv_, d_cells_, ncells_, keys,
+                       cellcnt, total_slots_, lkeys, knode, kq, okeys, out_slots_, ocount,
+                       nlevels_, node_cap_, two ? key_cap1_ : key_cap_, l0, d_err_);
   };
   auto resize = [&](int l, hipStream_t st) {
     const LevelInfo& S = lv_[l - 1];
     const LevelInfo& L = lv_[l];
     dim3 grid((L.w + kResizeCols - 1) / kResizeCols, (L.h + kResizeRows - 1) / kResizeRows,
               nframes);
-    hipLaunchKernelGGL(k_resize, grid, dim3(256), rs_lds_[l], st, d_pyr_, pyr_stride_, S.off,
+    hipLaunchKernelGGL(k_resize, grid, dim3(256), rs_lds_[l], st, pyr, pyr_stride_, S.off,
                        S.w, L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l],
                        rs_pitch_[l]);
   };
   auto blur = [&](hipStream_t st) {
-    hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, st, d_pyr_,
-                       d_blur_, pyr_stride_, d_lv_, d_tiles_, ntiles_);
+    hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, st, pyr,
+                       blurb, pyr_stride_, d_lv_, d_tiles_, ntiles_);
   };
   auto cells = [&](int l) { return std::make_pair(lv_[l].cell_begin, lv_[l].cell_end); };
   const int NL = nlevels_;
@@ -1805,37 +1865,36 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
     // Tried and measured equal or slower (the window is throughput-bound once FAST overlaps
     // the chain): FAST per level as each level lands, FAST of levels 1-3 beside the chain, one
     // octree launch for every level, the chain on a high-priority stream.
-    MMT_HIP(hipEventRecord(ev_gray_, stream));
-    MMT_HIP(hipStreamWaitEvent(side_, ev_gray_, 0));
-    fast(cells(0).first, cells(0).second, side_);
-    octree(0, 1, side_);
+    MMT_HIP(hipEventRecord(e_gray, stream));
+    MMT_HIP(hipStreamWaitEvent(side, e_gray, 0));
+    fast(cells(0).first, cells(0).second, side);
+    octree(0, 1, side);
     for (int l = 1; l < NL; l++) resize(l, stream);
-    MMT_HIP(hipEventRecord(ev_pyr_, stream));
-    MMT_HIP(hipStreamWaitEvent(side_, ev_pyr_, 0));
-    blur(side_);
-    MMT_HIP(hipEventRecord(ev_blur_, side_));
+    MMT_HIP(hipEventRecord(e_pyr, stream));
+    MMT_HIP(hipStreamWaitEvent(side, e_pyr, 0));
+    blur(side);
+    MMT_HIP(hipEventRecord(e_blur, side));
     fast(cells(0).second, ncells_, stream);
     if (NL > 1) octree(1, NL, stream);
-    MMT_HIP(hipStreamWaitEvent(stream, ev_blur_, 0));
+    MMT_HIP(hipStreamWaitEvent(stream, e_blur, 0));
   }
   auto orient = [&](int s0, int s1, int write_total, hipStream_t st) {
     const int grid = 8 * ((nframes + 7) / 8) * ((s1 - s0 + 15) / 16);  // see k_orient_desc
-    hipLaunchKernelGGL(k_orient_desc, dim3(grid), dim3(256), 0, st, d_pyr_, d_blur_, pyr_stride_,
-                       d_lv_, nlevels_, d_umax_, d_okeys_, out_slots_, d_ocount_, d_kps, d_desc,
+    hipLaunchKernelGGL(k_orient_desc, dim3(grid), dim3(256), 0, st, pyr, blurb, pyr_stride_,
+                       d_lv_, nlevels_, d_umax_, okeys, out_slots_, ocount, d_kps, d_desc,
                        cap_per_frame, d_n, nframes, s0, s1, write_total);
   };
   if (NL > 1 && !(sched_ & 2)) {
     // level 0's orientation on the side stream (its octree and the blur are done there) while
     // the main stream runs the octree of levels 1..; the main stream's own orientation of levels
     // 1.. writes the totals, then waits for the side stream
-    orient(0, lv_[1].out_off, 0, side_);
-    MMT_HIP(hipEventRecord(ev_pyr_, side_));
+    orient(0, lv_[1].out_off, 0, side);
+    MMT_HIP(hipEventRecord(e_pyr, side));
     orient(lv_[1].out_off, out_slots_, 1, stream);
-    MMT_HIP(hipStreamWaitEvent(stream, ev_pyr_, 0));
+    MMT_HIP(hipStreamWaitEvent(stream, e_pyr, 0));
   } else {
     orient(0, out_slots_, 1, stream);
   }
-  MMT_HIP(hipGetLastError());
 }
 
 void OrbEngine::check_flags(hipStream_t stream) {
