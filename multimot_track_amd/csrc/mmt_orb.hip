@@ -121,25 +121,39 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
   const int sx_lo = xt[dx0].sx, sx_hi = min(xt[dx1 - 1].sx + 1, sw - 1);
   const int sy_lo = yt[y0].sy0, sy_hi = yt[y1 - 1].sy1;
   const int nq = (sx_hi - sx_lo + 4) >> 2;  // dwords per staged row
-  const int items = (sy_hi - sy_lo + 1) * nq;
-  const float inv_nq = 1.0f / (float)nq;
+  const int nrows = sy_hi - sy_lo + 1;
   const uint8_t* s0 = src + (size_t)sy_lo * sw + sx_lo;
   // every staging load is issued before the first LDS store (one memory round trip per
-  // workgroup; the source may be 3 bytes past a row end: next row, next level or slack)
-  auto item_addr = [&](int i, int& lds_off) {
-    int r = (int)((float)i * inv_nq);
-    r -= r * nq > i ? 1 : 0;
-    r += (r + 1) * nq <= i ? 1 : 0;
-    const int q = i - r * nq;
-    lds_off = r * lds_pitch + 4 * q;
-    return s0 + (size_t)r * sw + 4 * q;
+  // workgroup; the source may be 3 bytes past a row end: next row, next level or slack).  Items
+  // (row r, dword q) are row-major, item tid + 256 k for thread tid: the thread's (r, q) and its
+  // addresses advance by the uniform (256 / nq, 256 % nq) with one carry, so there is no per-item
+  // division and no quarter-rate multiply.
+  const int dr = __builtin_amdgcn_readfirstlane(256 / nq), dq = 256 - dr * nq;
+  int r = (int)(((float)tid + 0.5f) / (float)nq);
+  int qq = tid - (int)__umul24((unsigned)r, (unsigned)nq);
+  const uint8_t* sp = s0 + __umul24((unsigned)r, (unsigned)sw) + 4 * qq;
+  int lo = (int)__umul24((unsigned)r, (unsigned)lds_pitch) + 4 * qq;
+  const int s_adv = dr * sw + 4 * dq, l_adv = dr * lds_pitch + 4 * dq;
+  const int s_carry = sw - 4 * nq, l_carry = lds_pitch - 4 * nq;
+  auto advance = [&]() {
+    r += dr;
+    qq += dq;
+    sp += s_adv;
+    lo += l_adv;
+    if (qq >= nq) {
+      qq -= nq;
+      r += 1;
+      sp += s_carry;
+      lo += l_carry;
+    }
   };
   uint32_t v[kResizeStage];
   int off[kResizeStage];
 #pragma unroll
   for (int k = 0; k < kResizeStage; k++) {
-    const int i = tid + 256 * k;
-    if (i < items) __builtin_memcpy(&v[k], item_addr(i, off[k]), 4);
+    off[k] = r < nrows ? lo : -1;
+    if (r < nrows) __builtin_memcpy(&v[k], sp, 4);
+    advance();
   }
   const int dx = dx0 + 4 * tid;
   ResizeX cx[4];
@@ -150,12 +164,11 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
   for (int k = 0; k < kResizeRows; k++) cy[k] = yt[min(y0 + k, dh - 1)];
 #pragma unroll
   for (int k = 0; k < kResizeStage; k++)
-    if (tid + 256 * k < items) *(uint32_t*)(rs_lds + off[k]) = v[k];
-  for (int i = tid + 256 * kResizeStage; i < items; i += 256) {  // wide windows only
-    int o;
+    if (off[k] >= 0) *(uint32_t*)(rs_lds + off[k]) = v[k];
+  for (; r < nrows; advance()) {  // tall windows only
     uint32_t w;
-    __builtin_memcpy(&w, item_addr(i, o), 4);
-    *(uint32_t*)(rs_lds + o) = w;
+    __builtin_memcpy(&w, sp, 4);
+    *(uint32_t*)(rs_lds + lo) = w;
   }
   __syncthreads();
   if (dx >= dx1) return;
@@ -167,16 +180,17 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
   for (int k = 0; k < kResizeRows; k++) {
     const int y = y0 + k;
     if (y >= y1) break;
-    const uint8_t* r0 = rs_lds + (cy[k].sy0 - sy_lo) * lds_pitch;
-    const uint8_t* r1 = rs_lds + (cy[k].sy1 - sy_lo) * lds_pitch;
+    const uint8_t* r0 = rs_lds + __umul24((unsigned)(cy[k].sy0 - sy_lo), (unsigned)lds_pitch);
+    const uint8_t* r1 = rs_lds + __umul24((unsigned)(cy[k].sy1 - sy_lo), (unsigned)lds_pitch);
     uint32_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       // a1 == 0 marks the clamped right edge (dx >= xmax): only S[sx]*2048 contributes (the
       // byte at sx+1 is then multiplied by 0; it lies inside the LDS row pitch)
-      const int h0 = r0[lx[j]] * cx[j].a0 + r0[lx[j] + 1] * cx[j].a1;
-      const int h1 = r1[lx[j]] * cx[j].a0 + r1[lx[j] + 1] * cx[j].a1;
-      int v = (cy[k].b0 * h0 + cy[k].b1 * h1 + (1 << 21)) >> 22;
+      // 24-bit multiplies (full rate): |a|, |b| <= 2048, pixels <= 255, |h| < 2^20
+      const int h0 = __mul24(r0[lx[j]], cx[j].a0) + __mul24(r0[lx[j] + 1], cx[j].a1);
+      const int h1 = __mul24(r1[lx[j]], cx[j].a0) + __mul24(r1[lx[j] + 1], cx[j].a1);
+      int v = (__mul24(cy[k].b0, h0) + __mul24(cy[k].b1, h1) + (1 << 21)) >> 22;
       v = v < 0 ? 0 : (v > 255 ? 255 : v);
       packed |= (uint32_t)v << (8 * j);
     }
@@ -342,7 +356,9 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
 #else
 #define FP_T(k) do {} while (0)
 #endif
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  // wave-uniform (readfirstlane): the cell record and everything derived from it live in SGPRs
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cell = cell_begin + blockIdx.x * 4 + wave;
   if (cell >= cell_end) return;
   uint8_t* tile = fast_lds + wave * fast_wave_lds(kFS, rows_max, win_max);
@@ -355,30 +371,32 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
   const int rows = ci.rows, nq = (ci.cols + 4) >> 2;  // dwords per LDS row (tile shifted by 1)
   {
     // dword copy from one byte before the tile (c0 >= 16; the pyramid allocation has slack for
-    // the <= 3 bytes read past the last row); every load of the first kStage rounds is issued
-    // before the first LDS store
+    // the <= 3 bytes read past the last row).  Lane -> (row offset rsub, dword q) is fixed and
+    // every step moves rps rows down, so the addresses advance by uniform strides: no per-item
+    // division and no quarter-rate 32-bit multiply.  Every load of the first kStage steps is
+    // issued before the first LDS store.
     const float inv_nq = 1.0f / (float)nq;
-    const uint8_t* src = img + (size_t)ci.r0 * L.w + ci.c0 - 1;
-    const int items = rows * nq;
+    const int rps = __builtin_amdgcn_readfirstlane(div_small(64, inv_nq));  // rows per step
+    const int rsub = div_small(lane, inv_nq);
+    const int q = lane - (int)__umul24((unsigned)rsub, (unsigned)nq);
+    const bool act = rsub < rps;
+    const uint8_t* src = img + (size_t)ci.r0 * L.w + ci.c0 - 1 + 4 * q +
+                         __umul24((unsigned)rsub, (unsigned)L.w);
+    const size_t sstep = (size_t)rps * L.w;
+    const int lstep = rps * kFS;
+    uint8_t* ldst = tile + rsub * kFS + 4 * q;
     constexpr int kStage = 8;
     uint32_t v[kStage];
-    int o[kStage];
+    const uint8_t* sp = src;
 #pragma unroll
-    for (int k = 0; k < kStage; k++) {
-      const int i = lane + 64 * k;
-      if (i < items) {
-        const int r = div_small(i, inv_nq), q = i - r * nq;
-        v[k] = ldg32(src + (size_t)r * L.w + 4 * q);
-        o[k] = r * kFS + 4 * q;
-      }
-    }
+    for (int k = 0; k < kStage; k++, sp += sstep)
+      if (act && rsub + k * rps < rows) v[k] = ldg32(sp);
+    uint8_t* lp = ldst;
 #pragma unroll
-    for (int k = 0; k < kStage; k++)
-      if (lane + 64 * k < items) *(uint32_t*)(tile + o[k]) = v[k];
-    for (int i = lane + 64 * kStage; i < items; i += 64) {
-      const int r = div_small(i, inv_nq), q = i - r * nq;
-      *(uint32_t*)(tile + r * kFS + 4 * q) = ldg32(src + (size_t)r * L.w + 4 * q);
-    }
+    for (int k = 0; k < kStage; k++, lp += lstep)
+      if (act && rsub + k * rps < rows) *(uint32_t*)lp = v[k];
+    for (int r = rsub + kStage * rps; act && r < rows; r += rps, sp += sstep, lp += lstep)
+      *(uint32_t*)lp = ldg32(sp);
     for (int i = lane; i < rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
   }
   wave_sync();
@@ -1179,6 +1197,8 @@ __device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
   return v;
 }
 
+typedef float f2x __attribute__((ext_vector_type(2)));
+
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur, size_t pyr_stride,
                                               const LevelInfo* __restrict__ lv,
@@ -1186,7 +1206,8 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
   const uint32_t T0 = 18, T1 = 34, T2 = 48, T3 = 56;
   const uint32_t W1 = T0 | (T1 << 8) | (T2 << 16) | (T3 << 24);  // bytes x-3+j .. x+j
   const uint32_t W2 = T2 | (T1 << 8) | (T0 << 16);               // bytes x+1+j .. x+3+j, 0
-  const int tile_id = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform (readfirstlane): the tile record, its level and the row arithmetic go to SALU
+  const int tile_id = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (tile_id >= ntiles) return;
   const int lane = threadIdx.x & 63;
   const BlurTile t = tiles[tile_id];
@@ -1227,11 +1248,18 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
       d2 = __builtin_amdgcn_perm(s1, s0, selA[2]) | __builtin_amdgcn_perm(s2, s2, selB[2]);
     }
   };
-  uint32_t w[7][4];
+  // Horizontal sums w (<= 256 * 255) go into a 7-row ring as floats, two columns per packed
+  // register; the vertical taps then run as packed fp32 FMA on integers: every product and partial
+  // sum stays below 2^24 (the total is at most 256 * 65280), so the float arithmetic is exact and
+  // equals the u32 formulation.
+  f2x w[7][2];
 #pragma unroll
   for (int i = 0; i < 7; i++)
 #pragma unroll
-    for (int j = 0; j < 4; j++) w[i][j] = 0;
+    for (int j = 0; j < 2; j++) w[i][j] = (f2x){0.f, 0.f};
+  const f2x t0 = {(float)T0, (float)T0}, t1 = {(float)T1, (float)T1};
+  const f2x t2 = {(float)T2, (float)T2}, t3 = {(float)T3, (float)T3};
+  const f2x sc = {1.0f / 65536.0f, 1.0f / 65536.0f}, half = {0.5f, 0.5f};
   const int r_end = y_end + 3;
   int r0 = t.y0 - 3;
   for (; r0 < r_end; r0 += 7) {
@@ -1243,22 +1271,29 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
       const int r = r0 + g;
       if (r >= r_end) break;
       // horizontal sums of the four columns -> ring slot g (rows of this group: slots 0..6)
+      uint32_t hs[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const uint32_t a = j < 3 ? __builtin_amdgcn_alignbyte(d[g][1], d[g][0], 1 + j) : d[g][1];
         const uint32_t bb = j < 3 ? __builtin_amdgcn_alignbyte(d[g][2], d[g][1], 1 + j) : d[g][2];
-        w[g][j] = __builtin_amdgcn_udot4(bb, W2, __builtin_amdgcn_udot4(a, W1, 0u, false), false);
+        hs[j] = __builtin_amdgcn_udot4(bb, W2, __builtin_amdgcn_udot4(a, W1, 0u, false), false);
       }
+      w[g][0] = (f2x){(float)hs[0], (float)hs[1]};
+      w[g][1] = (f2x){(float)hs[2], (float)hs[3]};
       const int yo = r - 3;
       if (yo >= t.y0) {
         // rows yo-3 .. yo+3 live in ring slots g+1 .. g+7 (mod 7)
         uint32_t o[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint32_t v = T0 * (w[(g + 1) % 7][j] + w[g][j]) +
-                             T1 * (w[(g + 2) % 7][j] + w[(g + 6) % 7][j]) +
-                             T2 * (w[(g + 3) % 7][j] + w[(g + 5) % 7][j]) + T3 * w[(g + 4) % 7][j];
-          o[j] = min((v + 32768u) >> 16, 255u);
+        for (int j = 0; j < 2; j++) {
+          f2x v = t3 * w[(g + 4) % 7][j];
+          v = __builtin_elementwise_fma(t2, w[(g + 3) % 7][j] + w[(g + 5) % 7][j], v);
+          v = __builtin_elementwise_fma(t1, w[(g + 2) % 7][j] + w[(g + 6) % 7][j], v);
+          v = __builtin_elementwise_fma(t0, w[(g + 1) % 7][j] + w[g][j], v);
+          // (v + 32768) >> 16 = floor(v / 65536 + 0.5): both steps exact in float
+          const f2x q = __builtin_elementwise_fma(v, sc, half);
+          o[2 * j] = min((uint32_t)q.x, 255u);
+          o[2 * j + 1] = min((uint32_t)q.y, 255u);
         }
         uint8_t* dp = dst + (size_t)yo * L.w + x;
         if (ncols == 4) {
@@ -1410,17 +1445,28 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   const int c0 = 2 * gl - 15, c1 = c0 + 1;
   uint32_t rows[31];
   {
+    // item i = gl + 16 k is (row i / 10, dword i % 10): each step advances (1 row, 6 dwords)
+    // with one carry, so the addresses are running pointers (no division, no 64-bit multiply)
+    constexpr int kQ = kOdBw / 4, kDq = 16 % kQ, kDr = 16 / kQ;
+    static_assert(kDr == 1 && kQ == 10, "step pattern of the staging loop");
     const uint8_t* bsrc = blur + fo + (size_t)(ky - kOdR) * Lw + (kx - kOdR);
+    const uint8_t* bp = bsrc + (gl >= kQ ? Lw + 4 * (gl - kQ) : 4 * gl);
+    int q = gl >= kQ ? gl - kQ : gl;
     uint32_t vb[kOdBLoads];
 #pragma unroll
     for (int k = 0; k < kOdBLoads; k++) {
-      const int i = gl + 16 * k, r = i / (kOdBw / 4), q = i - r * (kOdBw / 4);
-      if (i < kOdBRows * (kOdBw / 4)) vb[k] = ld32(bsrc + (size_t)r * Lw + 4 * q);
+      if (gl + 16 * k < kOdBRows * kQ) vb[k] = ld32(bp);
+      q += kDq;
+      bp += Lw + 4 * kDq;
+      if (q >= kQ) {
+        q -= kQ;
+        bp += Lw - 4 * kQ;
+      }
     }
     // the whole 31 x 32 disc square is inside the level: load it unconditionally, mask later
-    const uint8_t* col = pyr + fo + (size_t)ky * Lw + kx + c0;
+    const uint8_t* col = pyr + fo + (size_t)(ky - 15) * Lw + kx + c0;
 #pragma unroll
-    for (int v = -15; v <= 15; v++) rows[v + 15] = ld16(col + (ptrdiff_t)v * Lw);
+    for (int v = -15; v <= 15; v++, col += Lw) rows[v + 15] = ld16(col);
 #pragma unroll
     for (int k = 0; k < kOdBLoads; k++) {
       const int i = gl + 16 * k;
@@ -1474,8 +1520,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     const float x1 = (float)(int8_t)((pat[r] >> 16) & 0xFFu), y1 = (float)(int8_t)(pat[r] >> 24);
     const float ry0 = x0 * b + y0 * a, rx0 = x0 * a - y0 * b;
     const float ry1 = x1 * b + y1 * a, rx1 = x1 * a - y1 * b;
-    const int v0 = center[__float2int_rn(ry0) * kOdBw + __float2int_rn(rx0)];
-    const int v1 = center[__float2int_rn(ry1) * kOdBw + __float2int_rn(rx1)];
+    const int v0 = center[__mul24(__float2int_rn(ry0), kOdBw) + __float2int_rn(rx0)];
+    const int v1 = center[__mul24(__float2int_rn(ry1), kOdBw) + __float2int_rn(rx1)];
     bits[r] = v0 < v1;
   }
   // round r gives descriptor bytes 2r, 2r+1 (test 16r + gl -> byte 2r + gl/8, bit gl%8);
