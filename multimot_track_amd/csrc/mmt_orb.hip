@@ -121,39 +121,25 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
   const int sx_lo = xt[dx0].sx, sx_hi = min(xt[dx1 - 1].sx + 1, sw - 1);
   const int sy_lo = yt[y0].sy0, sy_hi = yt[y1 - 1].sy1;
   const int nq = (sx_hi - sx_lo + 4) >> 2;  // dwords per staged row
-  const int nrows = sy_hi - sy_lo + 1;
+  const int items = (sy_hi - sy_lo + 1) * nq;
+  const float inv_nq = 1.0f / (float)nq;
   const uint8_t* s0 = src + (size_t)sy_lo * sw + sx_lo;
   // every staging load is issued before the first LDS store (one memory round trip per
-  // workgroup; the source may be 3 bytes past a row end: next row, next level or slack).  Items
-  // (row r, dword q) are row-major, item tid + 256 k for thread tid: the thread's (r, q) and its
-  // addresses advance by the uniform (256 / nq, 256 % nq) with one carry, so there is no per-item
-  // division and no quarter-rate multiply.
-  const int dr = __builtin_amdgcn_readfirstlane(256 / nq), dq = 256 - dr * nq;
-  int r = (int)(((float)tid + 0.5f) / (float)nq);
-  int qq = tid - (int)__umul24((unsigned)r, (unsigned)nq);
-  const uint8_t* sp = s0 + __umul24((unsigned)r, (unsigned)sw) + 4 * qq;
-  int lo = (int)__umul24((unsigned)r, (unsigned)lds_pitch) + 4 * qq;
-  const int s_adv = dr * sw + 4 * dq, l_adv = dr * lds_pitch + 4 * dq;
-  const int s_carry = sw - 4 * nq, l_carry = lds_pitch - 4 * nq;
-  auto advance = [&]() {
-    r += dr;
-    qq += dq;
-    sp += s_adv;
-    lo += l_adv;
-    if (qq >= nq) {
-      qq -= nq;
-      r += 1;
-      sp += s_carry;
-      lo += l_carry;
-    }
+  // workgroup; the source may be 3 bytes past a row end: next row, next level or slack)
+  auto item_addr = [&](int i, int& lds_off) {
+    int r = (int)((float)i * inv_nq);
+    r -= (int)__umul24((unsigned)r, (unsigned)nq) > i ? 1 : 0;
+    r += (int)__umul24((unsigned)(r + 1), (unsigned)nq) <= i ? 1 : 0;
+    const int q = i - (int)__umul24((unsigned)r, (unsigned)nq);  // 24-bit multiplies: full rate
+    lds_off = (int)__umul24((unsigned)r, (unsigned)lds_pitch) + 4 * q;
+    return s0 + __umul24((unsigned)r, (unsigned)sw) + 4 * q;
   };
   uint32_t v[kResizeStage];
   int off[kResizeStage];
 #pragma unroll
   for (int k = 0; k < kResizeStage; k++) {
-    off[k] = r < nrows ? lo : -1;
-    if (r < nrows) __builtin_memcpy(&v[k], sp, 4);
-    advance();
+    const int i = tid + 256 * k;
+    if (i < items) __builtin_memcpy(&v[k], item_addr(i, off[k]), 4);
   }
   const int dx = dx0 + 4 * tid;
   ResizeX cx[4];
@@ -164,11 +150,12 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
   for (int k = 0; k < kResizeRows; k++) cy[k] = yt[min(y0 + k, dh - 1)];
 #pragma unroll
   for (int k = 0; k < kResizeStage; k++)
-    if (off[k] >= 0) *(uint32_t*)(rs_lds + off[k]) = v[k];
-  for (; r < nrows; advance()) {  // tall windows only
+    if (tid + 256 * k < items) *(uint32_t*)(rs_lds + off[k]) = v[k];
+  for (int i = tid + 256 * kResizeStage; i < items; i += 256) {  // wide windows only
+    int o;
     uint32_t w;
-    __builtin_memcpy(&w, sp, 4);
-    *(uint32_t*)(rs_lds + lo) = w;
+    __builtin_memcpy(&w, item_addr(i, o), 4);
+    *(uint32_t*)(rs_lds + o) = w;
   }
   __syncthreads();
   if (dx >= dx1) return;
@@ -1514,14 +1501,18 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   wave_sync();  // the staged window of every group of the wave
   const uint8_t* center = slot_lds + kOdR * kOdBw + kOdR;
   int bits[16];
+  // the rotation as packed fp32 pairs, each product and sum rounded exactly as the scalar
+  // x * a - y * b, x * b + y * a (no contraction): (x a, x b) + (-(y b), y a)
+  const f2x ab = {a, b}, ba = {b, a};
 #pragma unroll
   for (int r = 0; r < 16; r++) {
     const float x0 = (float)(int8_t)(pat[r] & 0xFFu), y0 = (float)(int8_t)((pat[r] >> 8) & 0xFFu);
     const float x1 = (float)(int8_t)((pat[r] >> 16) & 0xFFu), y1 = (float)(int8_t)(pat[r] >> 24);
-    const float ry0 = x0 * b + y0 * a, rx0 = x0 * a - y0 * b;
-    const float ry1 = x1 * b + y1 * a, rx1 = x1 * a - y1 * b;
-    const int v0 = center[__mul24(__float2int_rn(ry0), kOdBw) + __float2int_rn(rx0)];
-    const int v1 = center[__mul24(__float2int_rn(ry1), kOdBw) + __float2int_rn(rx1)];
+    const f2x p0 = (f2x){x0, x0} * ab, q0 = (f2x){y0, y0} * ba;
+    const f2x p1 = (f2x){x1, x1} * ab, q1 = (f2x){y1, y1} * ba;
+    const f2x rr0 = p0 + (f2x){-q0.x, q0.y}, rr1 = p1 + (f2x){-q1.x, q1.y};  // (rx, ry)
+    const int v0 = center[__mul24(__float2int_rn(rr0.y), kOdBw) + __float2int_rn(rr0.x)];
+    const int v1 = center[__mul24(__float2int_rn(rr1.y), kOdBw) + __float2int_rn(rr1.x)];
     bits[r] = v0 < v1;
   }
   // round r gives descriptor bytes 2r, 2r+1 (test 16r + gl -> byte 2r + gl/8, bit gl%8);
