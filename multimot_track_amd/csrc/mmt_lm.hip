@@ -1523,6 +1523,289 @@ __device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
 
 }  // namespace
 
+// The same solve with light trial passes, as the flow LM does it: a trial first evaluates only
+// its errors and robust chi2 (one DPP wave sum and one LDS exchange); the 28-sum linearisation
+// runs only for an accepted trial, at its pose (g2o keeps the linearisation of the accepted
+// state).  A rejected trial changes nothing but lambda (lam *= ni, ni *= 2), so the 6x6 solve runs
+// for the next four lambdas of the rejection chain at once, one per 16-lane group (the same
+// instructions, a different lambda per lane), and a trial after a rejection takes its increment
+// and pose from the wave's candidate table.  Each candidate is computed exactly as the sequential
+// solve for its lambda.  In the bench about 58 % of D1's trials are rejected.
+struct PoSmemL {
+  double tile[(kPoThreads / 64) * 64 * kPoStride];
+  double part[2][(kPoThreads / 64) * 32];  // wave partials of the full pass, double-buffered
+  double lpart[2][kPoThreads / 64];        // wave partials of the light pass, double-buffered
+  double Hw[kPoThreads / 64][2][32];        // every wave's own copy of the current / trial sums
+  double cand[kPoThreads / 64][4][16];      // every wave's lambda candidates (ok, x[6], pose[7])
+  double red[16 * 32];
+  double H[32];
+};
+
+template <int IT>
+__device__ void pose_opt_light(const PoseOptDesc& D, int N, PoSmemL& sm) {
+  const int tid = threadIdx.x, nw = kPoThreads >> 6;
+  const int lane = tid & 63, wave = tid >> 6;
+  const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
+  PoEdgeR Ed[IT];
+  double er[IT][3];
+#pragma unroll
+  for (int q = 0; q < IT; q++) {
+    const int i = tid + q * kPoThreads;
+    if (i < N) {
+      Ed[q] = po_load(D, nullptr, i, (D.obs[3 * i + 2] < 0 ? 0 : kPoStereo) | kPoRobust);
+    } else {
+      Ed[q] = PoEdgeR{};
+      Ed[q].flags = kPoNone | kPoOutlier;
+    }
+    er[q][0] = er[q][1] = er[q][2] = 0;
+  }
+  DSE3 P;
+  int nBad = 0;
+  double* row = tile_row<kPoStride>(sm.tile);
+  int npass = 0, nlight = 0;
+#ifdef MMT_PO_PROFILE
+  int nrej = 0;
+  long long pp[4] = {0, 0, 0, 0}, pt = clock64();
+#define PL_T(k)                     \
+  do {                              \
+    const long long _n = clock64(); \
+    pp[k] += _n - pt;               \
+    pt = _n;                        \
+  } while (0)
+#else
+#define PL_T(k) \
+  do {          \
+  } while (0)
+#endif
+  // full pass: errors and the 28 sums at T into the wave's copy `buf` of the sums
+  auto full = [&](const DSE3& T, int buf) {
+    PL_T(0);
+    po_linearise_row<true>(Ed[0], T, D, dM, dS, er[0], row);
+#pragma unroll
+    for (int q = 1; q < IT; q++) po_linearise_row<false>(Ed[q], T, D, dM, dS, er[q], row);
+    PL_T(1);
+    const double* t = sm.tile + (size_t)wave * 64 * kPoStride;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double* part = sm.part[npass & 1];
+    if (lane < kPoSums) {
+      double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int r0 = 0; r0 < 64; r0 += 16) {
+        double x[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) x[j] = t[(r0 + j) * kPoStride + lane];
+#pragma unroll
+        for (int j = 0; j < 16; j++) acc[j & 7] += x[j];
+      }
+      part[wave * 32 + lane] =
+          ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
+    __syncthreads();
+    if (lane < kPoSums) {
+      double sum = 0;
+#pragma unroll
+      for (int w = 0; w < nw; w++) sum += part[w * 32 + lane];
+      sm.Hw[wave][buf][lane] = sum;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    PL_T(2);
+    npass++;
+  };
+  // light pass: errors and the robust chi2 at T (same per-edge arithmetic as the full pass)
+  auto light = [&](const DSE3& T) {
+    PL_T(0);
+    double c = 0;
+#pragma unroll
+    for (int q = 0; q < IT; q++) {
+      if (Ed[q].flags & kPoOutlier) continue;
+      double x, y, z;
+      po_err(Ed[q], T, D, er[q], x, y, z);
+      const double ch = po_chi2(Ed[q], er[q]);
+      double r0 = ch, r1 = 1.0;
+      if (Ed[q].flags & kPoRobust) {
+        const double d = (Ed[q].flags & kPoStereo) ? dS : dM;
+        huber(ch, d * d, d, r0, r1);
+      }
+      c += r0;
+    }
+    PL_T(1);
+    c = wave_sum_dpp(c);
+    double* lp = sm.lpart[nlight & 1];
+    if (lane == 0) lp[wave] = c;
+    __syncthreads();
+    double sum = 0;
+#pragma unroll
+    for (int w = 0; w < nw; w++) sum += lp[w];
+    PL_T(2);
+    nlight++;
+    return sum;
+  };
+  double* cand = &sm.cand[wave][0][0];
+  for (int it = 0; it < 4; it++) {
+    P = dse3_from_float(D.Tcw);  // every round restarts from the input pose
+    int hs = 0;
+    full(P, 0);
+    double cur = sm.Hw[wave][0][0], lam, ni = 2, chk = 0;
+    {
+      double md = 0;
+#pragma unroll
+      for (int a = 0; a < 6; a++) md = fmax(md, fabs(sm.Hw[wave][0][1 + a * (a + 3) / 2]));
+      lam = 1e-5 * md;
+    }
+    int nRaul = 0;
+    double xb[6] = {0, 0, 0, 0, 0, 0};
+    int kc = 4, ncand = 0;  // candidate table empty
+    for (int iter = 0; iter < 10; iter++) {
+      const double ini = cur;
+      int qmax = 0;
+      bool bad = false;
+      for (;;) {
+        const double* Hc = sm.Hw[wave][hs];
+        if (kc >= ncand) {
+          // ---- the solves of the next four lambdas of the chain, one per 16-lane group
+          const double l1 = lam * ni, n1 = ni * 2, l2 = l1 * n1, n2 = n1 * 2, l3 = l2 * n2;
+          const int g = lane >> 4;
+          const double lg = g == 0 ? lam : g == 1 ? l1 : g == 2 ? l2 : l3;
+          double A[21], bs[6];
+#pragma unroll
+          for (int q = 0; q < 21; q++) A[q] = Hc[1 + q];
+#pragma unroll
+          for (int a = 0; a < 6; a++) {
+            A[a * (a + 3) / 2] += lg;
+            bs[a] = Hc[22 + a];
+          }
+          const bool okg = ldlt6_packed(A, bs);
+          double xg[6];
+#pragma unroll
+          for (int a = 0; a < 6; a++) xg[a] = okg ? bs[a] : xb[a];
+          const DSE3 PG = exp_mul(xg, P);
+          if ((lane & 15) == 0) {
+            double* cw = cand + g * 16;
+            cw[0] = okg ? 1.0 : 0.0;
+#pragma unroll
+            for (int a = 0; a < 6; a++) cw[1 + a] = xg[a];
+            cw[7] = PG.q.w;
+            cw[8] = PG.q.x;
+            cw[9] = PG.q.y;
+            cw[10] = PG.q.z;
+            cw[11] = PG.t[0];
+            cw[12] = PG.t[1];
+            cw[13] = PG.t[2];
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          ncand = 4;
+          kc = 0;
+        }
+        bool ok2;
+        DSE3 PN;
+        {
+          const double* cw = cand + kc * 16;
+          ok2 = cw[0] != 0.0;
+          if (ok2) {
+#pragma unroll
+            for (int a = 0; a < 6; a++) xb[a] = cw[1 + a];
+            PN.q.w = cw[7];
+            PN.q.x = cw[8];
+            PN.q.y = cw[9];
+            PN.q.z = cw[10];
+            PN.t[0] = cw[11];
+            PN.t[1] = cw[12];
+            PN.t[2] = cw[13];
+          } else {
+            PN = exp_mul(xb, P);  // failed solve: the last increment (g2o's stale x)
+          }
+          kc++;
+        }
+        const double lastTrialChi = light(PN);
+        const double tempChi = ok2 ? lastTrialChi : DBL_MAX;
+        double scale = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++) scale += xb[a] * (lam * xb[a] + Hc[22 + a]);
+        scale += 1e-3;
+        const double rho = (cur - tempChi) / scale;
+        const bool accept = rho > 0 && isfinite(tempChi);
+        if (accept) {
+          const double t = 2 * rho - 1;
+          double alpha = 1. - t * t * t;
+          alpha = fmin(alpha, 2. / 3.);
+          lam = lam * fmax(1. / 3., alpha);
+          ni = 2;
+          cur = tempChi;
+          P = PN;
+          full(P, hs ^ 1);  // the accepted state's linearisation
+          hs ^= 1;
+          kc = ncand;  // the table belonged to the old system
+        } else {
+          lam = lam * ni;
+          ni = ni * 2;
+#ifdef MMT_PO_PROFILE
+          nrej++;
+#endif
+        }
+        qmax++;
+        const bool again = (rho < 0 && qmax < 10);
+        if (!again) {
+          bool ok = true;
+          if (qmax == 10 || rho == 0) ok = false;
+          if (ok) {
+            if ((ini - cur) * 1e3 < ini)
+              nRaul++;
+            else
+              nRaul = 0;
+            if (nRaul >= 3) ok = false;
+          }
+          if (chk < lastTrialChi && iter > 0) ok = false;
+          chk = lastTrialChi;
+          bad = !ok;
+          break;
+        }
+      }
+      if (bad) break;
+    }
+    // re-classification (Optimizer.cc:3266-3322): edges that sat the round out get their error at
+    // the optimised pose, the others keep the last computed one (the last trial's)
+    double nb[1] = {0};
+#pragma unroll
+    for (int q = 0; q < IT; q++) {
+      if (Ed[q].flags & kPoNone) continue;
+      if (Ed[q].flags & kPoOutlier) {
+        double x, y, z;
+        po_err(Ed[q], P, D, er[q], x, y, z);
+      }
+      const double c = po_chi2(Ed[q], er[q]);
+      const float thr = (Ed[q].flags & kPoStereo) ? 7.815f : 5.991f;
+      int f = c > (double)thr ? (Ed[q].flags | kPoOutlier) : (Ed[q].flags & ~kPoOutlier);
+      nb[0] += (f & kPoOutlier) ? 1.0 : 0.0;
+      if (it == 2) f &= ~kPoRobust;
+      Ed[q].flags = f;
+    }
+    block_sum<1>(nb, sm.red, sm.H, nw);
+    nBad = (int)sm.H[0];
+    __syncthreads();  // sm.H is rewritten by the next round's count
+    if (N < 10) break;
+  }
+#pragma unroll
+  for (int q = 0; q < IT; q++) {
+    const int i = tid + q * kPoThreads;
+    if (i < N) D.outlier[i] = (Ed[q].flags & kPoOutlier) ? 1 : 0;
+  }
+  if (tid == 0) {
+    dse3_to_float(P, D.pose_out);
+    *D.n_inliers = N - nBad;
+#ifdef MMT_PO_PROFILE
+    printf("[po profile] N %d passes %d (rejected trials %d) cycles: solve+ctl %lld linearise "
+           "%lld reduce %lld light %d\n", N, npass, nrej, pp[0], pp[1], pp[2], nlight);
+#endif
+  }
+#undef PL_T
+}
+
 __device__ __forceinline__ bool pose_opt_trivial(const PoseOptDesc& D, int N) {
   if (N >= 3) return false;
   if (threadIdx.x == 0) {
@@ -1533,15 +1816,31 @@ __device__ __forceinline__ bool pose_opt_trivial(const PoseOptDesc& D, int N) {
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_pose_opt(const PoseOptDesc* __restrict__ descs) {
+// n_lo: counts at or below it belong to another launch (-1: every count)
+__global__ __launch_bounds__(256) void k_pose_opt(const PoseOptDesc* __restrict__ descs,
+                                                  int n_lo) {
   __shared__ PoSmem sm;
   const PoseOptDesc& D = descs[blockIdx.x];
   const int N = D.n;
+  if (N <= n_lo) return;
   if (pose_opt_trivial(D, N)) return;
   if (N <= kPoseOptMaxEdges)
     pose_opt_body<false>(D, N, sm);
   else
     pose_opt_body<true>(D, N, sm);
+}
+
+template <int IT>
+__global__ __launch_bounds__(kPoThreads) void k_pose_opt_l(const PoseOptDesc* __restrict__ descs,
+                                                           int n_lo) {
+  __shared__ PoSmemL sm;
+  const PoseOptDesc& D = descs[blockIdx.x];
+  const int N = D.n;
+  // edge counts outside (n_lo, IT * kPoThreads] belong to another launch (the host launches the
+  // variants whose ranges cover its bound; the count is known on the device only)
+  if (N <= n_lo || N > IT * kPoThreads) return;
+  if (pose_opt_trivial(D, N)) return;
+  pose_opt_light<IT>(D, N, sm);
 }
 
 template <int IT>
@@ -1558,18 +1857,36 @@ __global__ __launch_bounds__(kPoThreads) void k_pose_opt_r(const PoseOptDesc* __
 }
 
 void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, int n_max, hipStream_t st) {
-  static const int variant = [] {  // MMT_PO_VARIANT=0: the LDS kernel for every size (A/B knob)
+  // MMT_PO_VARIANT: 2 (default) light trial passes + lambda candidates, 1 register kernel with a
+  // full pass per trial, 0 the LDS kernel for every size (A/B knobs)
+  static const int variant = [] {
     const char* e = getenv("MMT_PO_VARIANT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
-  if (variant && n_max <= kPoThreads)
+  if (variant == 2) {
+    // the edge count is known on the device only: every variant whose range meets [0, n_max]
+    // is launched and the ones outside the solve's count return at once (n_max is a bound)
+    hipLaunchKernelGGL(k_pose_opt_l<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
+    if (n_max > kPoThreads)
+      hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
+                         kPoThreads);
+    if (n_max > 2 * kPoThreads)
+      hipLaunchKernelGGL(k_pose_opt_l<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
+                         2 * kPoThreads);
+    if (n_max > 4 * kPoThreads) {
+      // beyond the register variants: the LDS kernel, for the solves above 4 * kPoThreads only
+      hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs,
+                         4 * kPoThreads);
+    }
+  } else if (variant == 1 && n_max <= kPoThreads) {
     hipLaunchKernelGGL(k_pose_opt_r<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
-  else if (variant && n_max <= 2 * kPoThreads)
+  } else if (variant == 1 && n_max <= 2 * kPoThreads) {
     hipLaunchKernelGGL(k_pose_opt_r<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
-  else if (variant && n_max <= 4 * kPoThreads)
+  } else if (variant == 1 && n_max <= 4 * kPoThreads) {
     hipLaunchKernelGGL(k_pose_opt_r<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
-  else
-    hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs);
+  } else {
+    hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs, -1);
+  }
   MMT_HIP(hipGetLastError());
 }
 
