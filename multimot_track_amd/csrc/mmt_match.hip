@@ -545,71 +545,143 @@ struct OwnerTaken {
   __device__ bool operator()(int k) const { return owner[k] < i; }
 };
 
-__global__ __launch_bounds__(kFixThreads) void k_match_fix(GreedyArgs a) {
-  extern __shared__ int s_owner[];  // C.n keys
+// A point with candidates, cached in LDS: its candidates packed (distance << 14 | key) in sorted
+// order (0xFFFFFFFF past its count) and its index (bit 31: more candidates than cached, so it
+// may need a rescan).  Rounds then read LDS only.
+constexpr uint32_t kPackNone = 0xFFFFFFFFu;
+
+__device__ __forceinline__ int fix_decide_packed(const GreedyArgs& a, int i, bool big,
+                                                 const uint32_t* pc, const int* owner,
+                                                 bool& resc) {
+  int best = -1, bestD = 256, sec = -1, secD = 256;
+#pragma unroll
+  for (int e = 0; e < kCandK; e++) {
+    const uint32_t v = pc[e];
+    if (v == kPackNone) break;
+    const int idx = (int)(v & 0x3FFFu);
+    if (owner[idx] < i) continue;
+    const int d = (int)(v >> 14);
+    if (best < 0) {
+      best = idx;
+      bestD = d;
+      if (a.mode == 0) break;
+    } else {
+      sec = idx;
+      secD = d;
+      break;
+    }
+  }
+  resc = big && (best < 0 || (a.mode == 1 && sec < 0));
+  return resc ? -1 : decide(a, best, bestD, sec, secD);
+}
+
+__global__ __launch_bounds__(kFixThreads) void k_match_fix(GreedyArgs a, int cache_cap) {
+  extern __shared__ int s_owner[];  // C.n keys, then the cache of cache_cap points
   __shared__ int s_res[kFixResCap];
   __shared__ int s_hist[HISTO_LENGTH];
   __shared__ int s_ind[3];
-  __shared__ int s_changed, s_nres, s_more, s_nm, s_removed;
+  __shared__ int s_changed, s_nres, s_more, s_nm, s_removed, s_nact;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // every thread reads the condition before thread 0 may rewrite it (*nmatches, at the end)
   if (a.run_if && *a.run_if >= a.run_lt) return;
   const int n = a.C.n, np = a.npts;
   int* ch = a.cs.choice;
+  int* s_pid = s_owner + ((n + 3) & ~3);
+  uint32_t* s_cand = (uint32_t*)(s_pid + cache_cap);
   for (int k = tid; k < n; k += kFixThreads) {
     s_owner[k] = (a.taken_in && a.taken_in[k]) ? -1 : INT_MAX;
     a.match[k] = -1;
   }
   if (tid < HISTO_LENGTH) s_hist[tid] = 0;
-  for (int i = tid; i < np; i += kFixThreads) ch[i] = -1;
+  if (tid == 0) s_nact = 0;
   __syncthreads();
+  // ---- the points with candidates go to the LDS cache (any order: every round decides every
+  // point from the same owner table, so their order does not matter)
+  for (int i = tid; i < np; i += kFixThreads) {
+    ch[i] = -1;
+    const int cn = a.cs.n[i];
+    if (cn <= 0) continue;
+    const int slot = atomicAdd(&s_nact, 1);
+    if (slot >= cache_cap) continue;
+    s_pid[slot] = cn > kCandK ? (int)((unsigned)i | 0x80000000u) : i;
+    const int kk = min(cn, kCandK);
+#pragma unroll
+    for (int e = 0; e < kCandK; e++)
+      s_cand[slot * kCandK + e] =
+          e < kk ? ((a.cs.key[(size_t)i * kCandK + e] >> 20) << 14) |
+                       (uint32_t)a.cs.idx[(size_t)i * kCandK + e]
+                 : kPackNone;
+  }
+  __syncthreads();
+  const bool cached = s_nact <= cache_cap;  // uniform: else every round reads the candidates
+  const int nitems = cached ? s_nact : np;  // from global memory, point by point
+#ifdef MMT_MATCH_PROFILE
+  int prof_rounds = 0, prof_resc = 0;
+  long long prof_t0 = clock64();
+#endif
   for (int round = 0; round <= np + 1; round++) {
+#ifdef MMT_MATCH_PROFILE
+    prof_rounds++;
+#endif
     if (tid == 0) {
       s_changed = 0;
-      s_more = np;
+      s_more = nitems;
     }
     if (round > 0) {
-      for (int i = tid; i < np; i += kFixThreads) {
+      for (int it = tid; it < nitems; it += kFixThreads) {
+        const int i = cached ? (s_pid[it] & 0x7FFFFFFF) : it;
         const int c = ch[i];
         if (c >= 0 && (!a.obs || a.obs[i])) atomicMin(&s_owner[c], i);
       }
     }
     __syncthreads();
-    // re-decide every point; rescans are queued (in passes of kFixResCap points)
+    // re-decide every point; rescans are queued (in passes of kFixResCap items)
     int from = 0;
     for (;;) {
       if (tid == 0) s_nres = 0;
       __syncthreads();
-      int next = np;
-      for (int i = from + tid; i < np; i += kFixThreads) {
-        const int cn = a.cs.n[i];
-        if (cn <= 0) continue;
+      int next = nitems;
+      for (int it = from + tid; it < nitems; it += kFixThreads) {
+        int i, t;
         bool resc;
-        const int t = fix_decide_from_cands(a, i, s_owner, cn, resc);
+        if (cached) {
+          const int pid = s_pid[it];
+          i = pid & 0x7FFFFFFF;
+          t = fix_decide_packed(a, i, pid < 0, s_cand + it * kCandK, s_owner, resc);
+        } else {
+          i = it;
+          const int cn = a.cs.n[i];
+          if (cn <= 0) continue;
+          t = fix_decide_from_cands(a, i, s_owner, cn, resc);
+        }
         if (resc) {
           const int slot = atomicAdd(&s_nres, 1);
           if (slot < kFixResCap) {
-            s_res[slot] = i;
+            s_res[slot] = it;
           } else {
-            next = min(next, i);  // no room: this point (and the ones after it) next pass
+            next = min(next, it);  // no room: this item (and the ones after it) next pass
           }
           continue;
         }
-        if (i >= next) continue;
+        if (it >= next) continue;
         if (t != ch[i]) {
           ch[i] = t;
           s_changed = 1;
         }
       }
-      // the pass covered points [from, cut): the smallest point that found no room starts the
-      // next pass (points past it are re-decided then)
-      if (next < np) atomicMin(&s_more, next);
+      // the pass covered items [from, cut): the smallest item that found no room starts the
+      // next pass (items past it are re-decided then)
+      if (next < nitems) atomicMin(&s_more, next);
       __syncthreads();
       const int cut = s_more;
       const int nres = min(s_nres, kFixResCap);
+#ifdef MMT_MATCH_PROFILE
+      prof_resc += nres;
+#endif
       for (int r = wave; r < nres; r += kFixWaves) {
-        const int i = s_res[r];
-        if (i >= cut) continue;  // wave-uniform
+        const int it = s_res[r];
+        if (it >= cut) continue;  // wave-uniform
+        const int i = cached ? (s_pid[it] & 0x7FFFFFFF) : it;
         uint32_t dmp[8];
         load_desc8(a.pdesc + 32 * (size_t)(a.ids ? a.ids[i] : i), dmp);
         const PointWin w = a.cs.win[i];
@@ -626,10 +698,10 @@ __global__ __launch_bounds__(kFixThreads) void k_match_fix(GreedyArgs a) {
         }
       }
       __syncthreads();
-      if (cut >= np) break;
+      if (cut >= nitems) break;
       from = cut;
       __syncthreads();  // every thread has read s_more
-      if (tid == 0) s_more = np;
+      if (tid == 0) s_more = nitems;
     }
     if (!s_changed && round > 0) break;
     __syncthreads();  // every thread has read s_changed
@@ -701,21 +773,30 @@ __global__ __launch_bounds__(kFixThreads) void k_match_fix(GreedyArgs a) {
       if (s_owner[k]) a.match[k] = -1;
   }
   if (tid == 0) *a.nmatches = s_nm - s_removed;
+#ifdef MMT_MATCH_PROFILE
+  if (tid == 0)
+    printf("[match profile] mode %d npts %d keys %d rounds %d rescans %d cycles %lld\n", a.mode,
+           np, n, prof_rounds, prof_resc, clock64() - prof_t0);
+#endif
 }
 
 static void launch_match_fix(const GreedyArgs& g, hipStream_t st) {
-  // the owner table of kMaxMatchKeys keys needs 64 KB of dynamic LDS (once per device)
+  // dynamic LDS: the owner table (C.n keys, up to 64 KB) and the candidate cache (36 bytes per
+  // point with candidates) in what is left of kFixLds
+  constexpr int kFixLds = 150 * 1024;
   static std::atomic<uint64_t> attr_set{0};
   int dev = 0;
   MMT_HIP(hipGetDevice(&dev));
   const uint64_t bit = 1ull << (dev & 63);
   if (!(attr_set.load() & bit)) {
     MMT_HIP(hipFuncSetAttribute((const void*)k_match_fix,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(int) * kMaxMatchKeys)));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kFixLds));
     attr_set.fetch_or(bit);
   }
-  hipLaunchKernelGGL(k_match_fix, dim3(1), dim3(kFixThreads), sizeof(int) * (size_t)g.C.n, st, g);
+  const size_t owner = sizeof(int) * (size_t)((g.C.n + 3) & ~3);
+  const int cap = std::min(g.npts, (int)((kFixLds - owner) / (sizeof(int) * (1 + kCandK))));
+  const size_t lds = owner + sizeof(int) * (size_t)cap * (1 + kCandK);
+  hipLaunchKernelGGL(k_match_fix, dim3(1), dim3(kFixThreads), lds, st, g, cap);
   MMT_HIP(hipGetLastError());
 }
 
