@@ -482,6 +482,10 @@ int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* pr, float* pose_ou
     DevBuf<double> scratch(mmt::flow_scratch_doubles(cap));
     DevBuf<int> st(3);
     DevBuf<mmt::FlowSolveDesc> dd(1);
+    const int groups = mmt::flow_split_groups(n);
+    DevBuf<unsigned long long> gx(groups > 1 ? mmt::kFlowSplitGranules : 1);
+    if (groups > 1)
+      MMT_HIP(hipMemsetAsync(gx.p, 0, sizeof(unsigned long long) * mmt::kFlowSplitGranules, s));
     if (n > 0) {
       MMT_HIP(hipMemcpyAsync(obs.p, pr->obs, 8 * (size_t)n, hipMemcpyHostToDevice, s));
       MMT_HIP(hipMemcpyAsync(flow.p, pr->flow, 8 * (size_t)n, hipMemcpyHostToDevice, s));
@@ -505,12 +509,19 @@ int mmt_pose_flow_solve(mmt_ctx* ctx, const mmt_flow_problem* pr, float* pose_ou
     d.cap = cap;
     d.pose_out = pose.p;
     d.stats = st.p;
+    d.gx = gx.p;
+    d.gx_seq = 1;
     MMT_HIP(hipMemcpyAsync(dd.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
     MMT_HIP(hipMemcpyAsync(pose.p, pr->init, 64, hipMemcpyHostToDevice, s));
-    mmt::launch_flow_lm(dd.p, 1, n, s);
+    if (groups > 1)
+      mmt::launch_flow_lm_split(dd.p, groups, s);
+    else
+      mmt::launch_flow_lm(dd.p, 1, n, s);
     MMT_HIP(hipMemcpyAsync(pose_out, pose.p, 64, hipMemcpyDeviceToHost, s));
     MMT_HIP(hipMemcpyAsync(stats_out, st.p, 12, hipMemcpyDeviceToHost, s));
     MMT_HIP(hipStreamSynchronize(s));
+    if (stats_out[2] == 2)
+      throw mmt::DeviceError("pose flow solve: the split solve's workgroups were not resident together");
   });
 }
 

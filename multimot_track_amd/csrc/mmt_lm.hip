@@ -501,6 +501,66 @@ struct LMSmem {
   double cand[4 * 4 * 16];  // per wave: 4 candidate solves (ok, x[6], pose[7])
 };
 
+// ---- split solve: the G workgroups of one solve meet at every reduction.  Each publishes its
+// workgroup sums (identical in every wave) as 8-byte granules {tag, 32 bits of the value}, two per
+// double, stored write-through by one relaxed agent-scope atomic store each; every wave then reads
+// all G slices with relaxed agent-scope loads until every tag matches, and adds them in workgroup
+// order (the same bits in every wave of every workgroup).  The data is its own flag: no fence, no
+// barrier, no counter (cdna_hip_programming.md §6 G16, R2).  Slots alternate by exchange parity: a
+// workgroup can only rewrite a slot after every workgroup has read it (it needs their next
+// exchange first).  tag = launch salt << 16 | exchange index (from 1), so granules of an earlier
+// launch never match.  Spins are bounded: a workgroup that waits 0.1 s marks itself failed and
+// stops waiting; the solve then reports status 2 (stats[2]) and the host fails loudly.
+struct GridX {
+  unsigned long long* g;  // [2][kFlowSplitMax][128] granules
+  unsigned seq;
+  int b, G, epoch, ntot;
+  bool dead;
+};
+
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+
+// sums over the G workgroups of the values lanes 0..K-1 hold (lane MAXL: maximum instead);
+// every wave calls it with the same values
+__device__ __forceinline__ double gx_sum(GridX& x, double v, int K, int maxl = -1) {
+  const int lane = threadIdx.x & 63;
+  x.epoch++;
+  const unsigned long long tag = (unsigned long long)(((x.seq & 0xFFFFu) << 16) | (x.epoch & 0xFFFF))
+                                 << 32;
+  gu64_t* slot = (gu64_t*)(x.g + (size_t)(x.epoch & 1) * kFlowSplitMax * 128);
+  if (threadIdx.x < 64 && lane < K) {  // wave 0 publishes
+    const unsigned long long bits = __double_as_longlong(v);
+    gu64_t* mine = slot + (size_t)x.b * 128 + 2 * lane;
+    __hip_atomic_store(mine, tag | (bits & 0xFFFFFFFFull), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mine + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  double s = 0;
+  if (x.dead) return 0.0;
+  const unsigned long long t0 = wall_clock64();
+  for (int g = 0; g < x.G; g++) {
+    const gu64_t* src = slot + (size_t)g * 128 + 2 * lane;
+    unsigned long long lo = 0, hi = 0;
+    for (;;) {
+      bool ok = true;
+      if (lane < K) {
+        lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hi = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = (lo & 0xFFFFFFFF00000000ull) == tag && (hi & 0xFFFFFFFF00000000ull) == tag;
+      }
+      if (__all(ok)) break;
+      if (wall_clock64() - t0 > 10000000ull) {  // 0.1 s of the 100 MHz wall clock
+        x.dead = true;
+        return 0.0;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const double t = __longlong_as_double((long long)((hi << 32) | (lo & 0xFFFFFFFFull)));
+    s = lane == maxl ? fmax(s, t) : s + t;
+  }
+  return lane < K ? s : 0.0;
+}
+
 }  // namespace
 
 // One last-frame sample of ObjCentre3D_pre (Tracking.cc:2032-2049): the world point of
@@ -554,9 +614,11 @@ __device__ __forceinline__ void centre_sum_wave(const FlowSolveDesc& D, int N) {
   }
 }
 
-template <int IR>
-__device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int nt, LMSmem& sm,
-                                             int max_cand) {
+// N edges from edge `lo` on (a slice of the solve's edges when SPLIT, which then meets the other
+// workgroups at every reduction through gx)
+template <int IR, bool SPLIT>
+__device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int lo, int nt,
+                                             LMSmem& sm, int max_cand, GridX& gx) {
   const int tid = threadIdx.x, nw = nt >> 6;
 #ifdef MMT_LM_PROFILE
   long long prof_t = 0;
@@ -628,7 +690,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
     for (int k = 0; k < IR; k++) {
       const int i = tid + k * nt;
       if (i < N) {
-        init_item(i, R[k]);
+        init_item(lo + i, R[k]);
         if (k == 0)
           linearise<true>(c, P, R[k], R[k].f[0], R[k].f[1], row, 0.0, R[k].e[0], R[k].e[1],
                           R[k].w, R[k].bl[0], R[k].bl[1], mh, kCacheB ? RB : nullptr);
@@ -639,10 +701,10 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
     }
     for (int i = n_reg + tid; i < N; i += nt) {
       LMItem it;
-      init_item(i, it);
+      init_item(lo + i, it);
       linearise<false>(c, P, it, it.f[0], it.f[1], row, 0.0, it.e[0], it.e[1], it.w, it.bl[0],
                        it.bl[1], mh);
-      item_store(G, cap, i, it);
+      item_store(G, cap, lo + i, it);
     }
     if (tid >= N)
       for (int q = 0; q < kSums; q++) row[q] = 0;
@@ -653,13 +715,19 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   int pb = 0;  // part buffer of the next reduction
   double vc = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
   pb ^= 1;
+  double mhw = 0;  // the largest flow-vertex diagonal of the workgroup's edges
+  for (int w = 0; w < nw; w++) mhw = fmax(mhw, sm.mh[w]);
+  if (SPLIT) {  // the solve's sums, and the largest diagonal in lane 63
+    vc = gx_sum(gx, (tid & 63) == 63 ? mhw : vc, 64, 63);
+    mhw = lane_value(vc, 63);
+  }
   double cur = lane_value(vc, 0), lam, ni = 2, chk = 0;
   {
     double md = 0;
 #pragma unroll
     for (int a = 0; a < 6; a++)
       md = fmax(md, fabs(lane_value(vc, 2 + a * (a + 3) / 2)));  // diagonal (a, a) of the lower triangle
-    for (int w = 0; w < nw; w++) md = fmax(md, sm.mh[w]);
+    md = fmax(md, mhw);
     lam = 1e-5 * md;
   }
   int nbad = 0, iters = 0;
@@ -685,6 +753,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
 #else
       const bool clean = lane_value(vc, 29) == 0;
 #endif
+      double s27 = 0;  // SPLIT: the solve's Schur sums, sum k in lane k
       if (!clean) {
         double v[27];
 #pragma unroll
@@ -694,11 +763,12 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
           if (tid + k * nt < N) schur_terms(c, P, R[k], lam, ilam, v);
         for (int i = n_reg + tid; i < N; i += nt) {
           LMItem it;
-          item_load(G, cap, i, it);
+          item_load(G, cap, lo + i, it);
           schur_terms(c, P, it, lam, ilam, v);
         }
         MMT_LMPROF(4);
         block_sum_t<27>(v, sm.tile, sm.red, sm.S27, nw);
+        if (SPLIT) s27 = gx_sum(gx, (tid & 63) < 27 ? sm.S27[tid & 63] : 0.0, 27);
       }
       MMT_LMPROF(0);
       // the 6x6 solve, computed redundantly by every wave from the sums (no lane-0 section, no
@@ -734,9 +804,9 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
             bs[a] -= d00 * lane_value(vc, 51 + a) + ilg * lane_value(vc, 57 + a);
         } else {
 #pragma unroll
-          for (int k = 0; k < 21; k++) A[k] -= sm.S27[k];
+          for (int k = 0; k < 21; k++) A[k] -= SPLIT ? lane_value(s27, k) : sm.S27[k];
 #pragma unroll
-          for (int a = 0; a < 6; a++) bs[a] -= sm.S27[21 + a];
+          for (int a = 0; a < 6; a++) bs[a] -= SPLIT ? lane_value(s27, 21 + a) : sm.S27[21 + a];
         }
 #pragma unroll
         for (int a = 0; a < 6; a++) A[a * (a + 3) / 2] += lg;  // diagonal (a, a)
@@ -805,23 +875,29 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         for (int k = 0; k < IR; k++) {
           const int i = tid + k * nt;
           if (i < N)
-            trial_terms(c, P, PN, R[k], i, ok2, lam, ilam, xb, s_chi, s_sc,
+            trial_terms(c, P, PN, R[k], lo + i, ok2, lam, ilam, xb, s_chi, s_sc,
                         (kCacheB && k == 0) ? RB : nullptr);
         }
         {  // global items: the next item's loads are in flight while this one computes
           int i = n_reg + tid;
           LMItem it, nx;
-          if (i < N) item_load(G, cap, i, it);
+          if (i < N) item_load(G, cap, lo + i, it);
           for (; i < N; i += nt) {
-            if (i + nt < N) item_load(G, cap, i + nt, nx);
-            trial_terms(c, P, PN, it, i, ok2, lam, ilam, xb, s_chi, s_sc);
-            item_store_trial(G, cap, i, it);
+            if (i + nt < N) item_load(G, cap, lo + i + nt, nx);
+            trial_terms(c, P, PN, it, lo + i, ok2, lam, ilam, xb, s_chi, s_sc);
+            item_store_trial(G, cap, lo + i, it);
             it = nx;
           }
         }
         MMT_LMPROF(5);
         block_sum2(s_chi, s_sc, sm.part[pb], nw, lastTrialChi, scale);
         pb ^= 1;
+        if (SPLIT) {
+          const int l = tid & 63;
+          const double t = gx_sum(gx, l == 0 ? lastTrialChi : l == 1 ? scale : 0.0, 2);
+          lastTrialChi = lane_value(t, 0);
+          scale = lane_value(t, 1);
+        }
       }
       MMT_LMPROF(2);
       // ---- g2o LM step acceptance and termination (every thread, same values)
@@ -875,11 +951,11 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         {
           int i = n_reg + tid;
           LMItem it, nx;
-          if (i < N) item_load(G, cap, i, it);
+          if (i < N) item_load(G, cap, lo + i, it);
           for (; i < N; i += nt) {
-            if (i + nt < N) item_load(G, cap, i + nt, nx);
+            if (i + nt < N) item_load(G, cap, lo + i + nt, nx);
             accept_terms<false>(c, P, it, row);
-            item_store_accept(G, cap, i, it);
+            item_store_accept(G, cap, lo + i, it);
             it = nx;
           }
         }
@@ -887,6 +963,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
           for (int q = 0; q < kSums; q++) row[q] = 0;
         vc = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
         pb ^= 1;
+        if (SPLIT) vc = gx_sum(gx, vc, kSums);
       }
       MMT_LMPROF(3);
 #ifdef MMT_LM_PROFILE
@@ -910,17 +987,24 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
     if (tid + k * nt < N) v[0] += outlier(R[k]);
   for (int i = n_reg + tid; i < N; i += nt) {
     LMItem it;
-    item_load(G, cap, i, it);
+    item_load(G, cap, lo + i, it);
     v[0] += outlier(it);
   }
   block_sum<1>(v, sm.red, sm.S27, nw);
-  const int n_out = N - (int)sm.S27[0];
-  if (D.centre_out && tid < 64) centre_sum_wave(D, N);  // ObjCentre3D_pre, wave 0
+  int n_out = N - (int)sm.S27[0], status = 0;
+  if (SPLIT) {  // the solve's outliers, and whether any workgroup gave up waiting
+    const int l = tid & 63;
+    const double t = gx_sum(gx, l == 0 ? sm.S27[0] : l == 1 ? (gx.dead ? 1.0 : 0.0) : 0.0, 2);
+    n_out = gx.ntot - (int)lane_value(t, 0);
+    status = (gx.dead || lane_value(t, 1) != 0) ? 2 : 0;
+    if (gx.b != 0) return;
+  }
+  if (D.centre_out && tid < 64) centre_sum_wave(D, SPLIT ? gx.ntot : N);  // ObjCentre3D_pre, wave 0
   if (tid == 0) {
     dse3_to_float(P, D.pose_out);
     D.stats[0] = iters;
     D.stats[1] = n_out;
-    D.stats[2] = 0;
+    D.stats[2] = status;
 #ifdef MMT_LM_PROFILE
     printf("lmprof N=%d T=%d iters=%d trials=%lld clean=%lld schur_pass=%lld schur_red=%lld "
            "solve_ld=%lld solve_ldlt=%lld solve_exp=%lld upd_pass=%lld upd_red=%lld decide=%lld\n",
@@ -957,10 +1041,42 @@ __global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict
   // at the barriers), which keeps the reductions' LDS traffic to the rows in use.
   const int nt = min((int)blockDim.x, max(64, (N + 63) / 64 * 64));
   if ((int)threadIdx.x >= nt) return;
+  GridX gx{};
   if (N <= nt || MAXIR == 1)
-    flow_lm_body<1>(D, N, nt, sm, max_cand);
+    flow_lm_body<1, false>(D, N, 0, nt, sm, max_cand, gx);
   else
-    flow_lm_body<2>(D, N, nt, sm, max_cand);
+    flow_lm_body<2, false>(D, N, 0, nt, sm, max_cand, gx);
+}
+
+// One large solve (descs[0]) over gridDim.x <= kFlowSplitMax workgroups, each on a contiguous slice
+// of the edges (lo = b N / G); the LM bookkeeping runs in every workgroup on the exchanged sums.
+// The workgroups must be resident together: one per CU, at most 8 (bounded spins otherwise).
+__global__ __launch_bounds__(256) void k_flow_lm_split(const FlowSolveDesc* __restrict__ descs,
+                                                       int max_cand) {
+  __shared__ LMSmem sm;
+  const FlowSolveDesc& D = descs[0];
+  const int N = D.d_n ? min(*D.d_n, D.cap) : min(D.n, D.cap);
+  const int G = gridDim.x, b = blockIdx.x;
+  if (N < 3) {  // as k_flow_lm, by workgroup 0
+    if (b == 0) {
+      if (threadIdx.x == 0) {
+        D.stats[0] = 0;
+        D.stats[1] = 0;
+        D.stats[2] = 1;
+      }
+      if (D.centre_out && threadIdx.x < 64) centre_sum_wave(D, N);
+    }
+    return;
+  }
+  const int lo = (int)((long long)b * N / G), hi = (int)((long long)(b + 1) * N / G);
+  const int Nl = hi - lo;
+  const int nt = min((int)blockDim.x, max(64, (Nl + 63) / 64 * 64));
+  if ((int)threadIdx.x >= nt) return;
+  GridX gx{D.gx, D.gx_seq, b, G, 0, N, false};
+  if (Nl <= nt)
+    flow_lm_body<1, true>(D, Nl, lo, nt, sm, max_cand, gx);
+  else
+    flow_lm_body<2, true>(D, Nl, lo, nt, sm, max_cand, gx);
 }
 
 void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st) {
@@ -979,6 +1095,24 @@ void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipSt
   int max_cand = 4;
   if (const char* e = getenv("MMT_LM_MAX_CAND")) max_cand = std::min(4, std::max(1, atoi(e)));
   hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs, max_cand);
+}
+
+int flow_split_groups(int n_hint) {
+  const char* e = getenv("MMT_LM_SPLIT");  // read per call (tests switch it)
+  const int force = e ? atoi(e) : -1;
+  if (force == 0) return 1;
+  if (force > 0) return std::min(force, kFlowSplitMax);
+  // about one edge per thread of 256-thread workgroups; small solves stay whole (each exchange
+  // costs about a microsecond of latency)
+  if (n_hint < 512) return 1;
+  return std::min(kFlowSplitMax, (n_hint + 255) / 256);
+}
+
+void launch_flow_lm_split(const FlowSolveDesc* d_desc, int groups, hipStream_t st) {
+  int max_cand = 4;
+  if (const char* e = getenv("MMT_LM_MAX_CAND")) max_cand = std::min(4, std::max(1, atoi(e)));
+  groups = std::max(1, std::min(groups, kFlowSplitMax));
+  hipLaunchKernelGGL(k_flow_lm_split, dim3(groups), dim3(256), 0, st, d_desc, max_cand);
 }
 
 size_t flow_scratch_doubles(int cap) { return (size_t)G_COUNT * cap; }

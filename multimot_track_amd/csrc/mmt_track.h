@@ -92,7 +92,20 @@ struct FlowSolveDesc {
   // last-frame points unprojected with the frame's depth noise (UnprojectStereoObject(i, 1),
   // Frame.cc:1118-1152: noise = gaussian(z^2 / 362.5 * 0.15) with the first draw g0)
   float* centre_out;
+  // split solve (launch_flow_lm_split): the exchange granules of the solve's workgroups
+  // (kFlowSplitGranules 8-byte words, zeroed once at allocation) and this launch's tag salt
+  unsigned long long* gx;
+  unsigned gx_seq;
 };
+
+// A large single solve split over up to kFlowSplitMax workgroups (one slice of the edges each),
+// which meet at every reduction through tagged granules (flow_lm_body).
+constexpr int kFlowSplitMax = 8;
+constexpr int kFlowSplitGranules = 2 * kFlowSplitMax * 128;
+// workgroups launch_flow_lm_split would use for an edge count (1: no split); MMT_LM_SPLIT=0
+// disables the split, MMT_LM_SPLIT=<g> forces g workgroups
+int flow_split_groups(int n_hint);
+void launch_flow_lm_split(const FlowSolveDesc* d_desc, int groups, hipStream_t st);
 
 void launch_gray_depth(const uint8_t* bgr, size_t bgr_pitch, const uint16_t* disp,
                        size_t disp_pitch, uint8_t* gray, size_t gray_pitch, float* depth,

@@ -236,6 +236,8 @@ class Tracker {
   FlowSolveDesc* d_descs_ = nullptr;
   float* d_poses_ = nullptr;
   int* d_lmstats_ = nullptr;
+  unsigned long long* d_gx_ = nullptr;  // the split ego solve's exchange granules
+  unsigned gx_seq_ = 0;
   PnPObject* d_pnp_[kObjSlots] = {};
   PnPBuf pnp_[kObjSlots][kMaxObj];
   bool prof_ = false;

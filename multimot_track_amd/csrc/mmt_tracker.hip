@@ -226,6 +226,8 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   d_descs_ = alloc<FlowSolveDesc>(1);
   d_poses_ = alloc<float>(16);
   d_lmstats_ = alloc<int>(3);
+  d_gx_ = alloc<unsigned long long>(kFlowSplitGranules);
+  MMT_HIP(hipMemset(d_gx_, 0, sizeof(unsigned long long) * kFlowSplitGranules));
   // PnP
   mask_words_ = (ocap_ + 63) / 64;
   for (int q = 0; q < kObjSlots; q++) {
@@ -541,8 +543,15 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   d2.cap = lm_cap_;
   d2.pose_out = d_poses_;
   d2.stats = d_lmstats_;
+  d2.gx = d_gx_;
+  d2.gx_seq = ++gx_seq_;
   MMT_HIP(hipMemcpyAsync(d_descs_, &d2, sizeof(d2), hipMemcpyHostToDevice, st));
-  launch_flow_lm(d_descs_, 1, eh_->n_static[last_], st);
+  // the ego solve (1,500-1,700 edges on KITTI-like frames) split over workgroups
+  const int groups = flow_split_groups(eh_->n_static[last_]);
+  if (groups > 1)
+    launch_flow_lm_split(d_descs_, groups, st);
+  else
+    launch_flow_lm(d_descs_, 1, eh_->n_static[last_], st);
   MMT_HIP(hipMemcpyAsync(eh_->Tcw, d_poses_, sizeof(eh_->Tcw), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(eh_->st, d_lmstats_, sizeof(eh_->st), hipMemcpyDeviceToHost, st));
   ego_pending_ = true;
@@ -595,6 +604,7 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
   } else {
     float Tcw[16];
     memcpy(Tcw, eh_->Tcw, sizeof(Tcw));
+    if (eh_->st[2] == 2) throw DeviceError("D2: the split solve's workgroups were not resident together");
     if (eh_->st[2] != 0) memcpy(Tcw, ego_Tinit_, sizeof(Tcw));  // < 3 edges: pose unchanged
     memcpy(C.Tcw, Tcw, sizeof(Tcw));
     out.ego_iterations = eh_->st[0];

@@ -66,6 +66,45 @@ def test_flow_solve_rejection_chains_bit_exact(ctx, oracle_mod, seed, n, noise, 
     assert st4["inliers"] == st_o["inliers"]
 
 
+@pytest.mark.parametrize("seed,n,out,ego,groups", [
+    (2, 1500, 0.2, True, "0"), (2, 1500, 0.2, True, "2"), (2, 1500, 0.2, True, "8"),
+    (1, 600, 0.1, True, "3"), (4, 3000, 0.3, False, "5"), (6, 37, 0.3, True, "8"),
+    (9, 5, 0.0, True, "8"), (10, 1700, 0.05, True, "7")])
+def test_flow_solve_split_matches_oracle(ctx, oracle_mod, seed, n, out, ego, groups, monkeypatch):
+    """The large ego solve split over workgroups that exchange their sums at every reduction
+    (launch_flow_lm_split): any group count, including slices of no edges (n=5 over 8), agrees
+    with the oracle as the whole solve does (MMT_LM_SPLIT=0)."""
+    monkeypatch.setenv("MMT_LM_SPLIT", groups)
+    obs, flow, depth, Tl, init, _ = flow_problem(seed, n, outlier_frac=out)
+    args = (0.04, 0.3, 100) if ego else (0.01, 0.5, 200)
+    rc, pose_o, st_o = oracle_mod.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    status, pose_g, st_g = ctx.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    assert status == rc == 0
+    assert np.abs(pose_g - pose_o).max() < POSE_TOL
+    assert st_g["inliers"] == st_o["inliers"]
+    if n >= 10:
+        assert st_g["iterations"] == st_o["iterations"]
+
+
+@pytest.mark.parametrize("seed,n,noise,ego", [(24, 1200, 0.0, True), (24, 900, 0.02, False)])
+def test_flow_solve_split_rejection_chains_bit_exact(ctx, oracle_mod, seed, n, noise, ego,
+                                                     monkeypatch):
+    """The split solve's lambda candidates: bit-identical to solving every trial for its own
+    lambda, as in the whole solve."""
+    monkeypatch.setenv("MMT_LM_SPLIT", "4")
+    obs, flow, depth, Tl, init, _ = flow_problem(seed, n, outlier_frac=0.0, pix_noise=noise,
+                                                 motion=0.3)
+    args = (0.04, 0.3, 100) if ego else (0.01, 0.5, 200)
+    rc, pose_o, st_o = oracle_mod.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    status4, pose4, st4 = ctx.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    monkeypatch.setenv("MMT_LM_MAX_CAND", "1")
+    status1, pose1, st1 = ctx.flow_solve(obs, flow, depth, Tl, init, *args, K_KITTI)
+    assert status4 == status1 == rc == 0
+    assert np.array_equal(pose4, pose1) and st4 == st1
+    assert np.abs(pose4 - pose_o).max() < POSE_TOL
+    assert st4["inliers"] == st_o["inliers"]
+
+
 def test_flow_solve_too_few_edges(ctx):
     obs, flow, depth, Tl, init, _ = flow_problem(8, 2)
     status, _, st = ctx.flow_solve(obs, flow, depth, Tl, init, 0.04, 0.3, 100, K_KITTI)
