@@ -244,7 +244,7 @@ class Tracker {
   bool map_finish_pending_ = false;
   // MMT_MAP_PROFILE: host wall time per frame in obj_advance / ego_launch / ego_finish
   bool hprof_ = false;
-  double hprof_us_[3] = {0, 0, 0};
+  double hprof_us_[7] = {0, 0, 0, 0, 0, 0, 0};  // + map finish, stage A, stage B, obj finish
   long hprof_n_ = 0;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
   double orb_ms_ = 0;

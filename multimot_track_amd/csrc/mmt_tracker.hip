@@ -122,6 +122,10 @@ Tracker::~Tracker() {
     fprintf(stderr, "[mmt tracker profile] %ld frames, host wall us per frame: map finish + obj_advance %.1f, "
             "ego_launch %.1f, ego_finish %.1f\n", hprof_n_, hprof_us_[0] / hprof_n_,
             hprof_us_[1] / hprof_n_, hprof_us_[2] / hprof_n_);
+  if (hprof_ && hprof_n_ > 0)
+    fprintf(stderr, "[mmt tracker profile] of which: map finish %.1f, object stage A %.1f, "
+            "stage B %.1f, object results %.1f\n", hprof_us_[3] / hprof_n_,
+            hprof_us_[4] / hprof_n_, hprof_us_[5] / hprof_n_, hprof_us_[6] / hprof_n_);
   for (hipStream_t* q : {&oa_, &ob_})
     if (*q) {
       (void)hipStreamSynchronize(*q);
@@ -409,6 +413,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
       ego_launch(a, outs[f], st);
       const double t1 = now();
       ego_map_finish(outs[f]);
+      hprof_us_[3] += now() - t1;
       obj_advance();
       const double t2 = now();
       ego_finish(outs[f], st);
@@ -432,15 +437,28 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
 // grouping statistics; stage B is device-ordered), then read the results of frames older than
 // kObjLag.  Called while the next ego solve runs.
 void Tracker::obj_advance() {
+  auto now = [] {
+    return std::chrono::duration<double, std::micro>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  const double t0 = hprof_ ? now() : 0;
+  double t1 = t0, t2 = t0;
   if (qa_.active) {
     obj_stage_a(qa_);
+    if (hprof_) t1 = now();
     obj_stage_b(qa_);
+    if (hprof_) t2 = now();
     inflight_.push_back(qa_);
     qa_ = ObjFrame();
   }
   while ((int)inflight_.size() > kObjLag) {
     obj_finish(inflight_.front());
     inflight_.pop_front();
+  }
+  if (hprof_) {
+    hprof_us_[4] += t1 - t0;
+    hprof_us_[5] += t2 - t1;
+    hprof_us_[6] += now() - t2;
   }
 }
 
