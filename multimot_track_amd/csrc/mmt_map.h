@@ -163,7 +163,8 @@ class MapEngine {
   // GPU stages (synchronous on s_)
   int gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
                       const float* Tlast, float th, float retry_th, int min_matches);
-  void pose_desc_upload(const float* Tcw);
+  void pose_desc_fill(uint8_t* h_blk, uint8_t* d_blk, const float* Tcw);
+  size_t out_bytes(int n) const;
   MapEdgeArgs edge_args(const GridFrame& G) const;
   void apply_pose_opt(MapFrameH& C, float* Tcw);
   void gpu_flush_pool();
@@ -201,10 +202,15 @@ class MapEngine {
 
   // device / pinned buffers
   std::vector<void*> dallocs_, hallocs_;
-  // C2: the last frame, packed [kps][Xw][desc][active][obs]
+  // C2's one upload: D1's descriptor (kDescBytes), then the last frame, packed
+  // [kps][Xw][desc][active][obs]
   uint8_t* d_last_ = nullptr;
   uint8_t* h_last_ = nullptr;
   CandSet c2_{};
+  // the one download of a C2 / C3 chain: [nm][ninl][pad][pose 16 floats] (kOutHdr bytes), then
+  // match[kcap] and D1's outlier flags[kcap]; the pointers below point into it
+  uint8_t* d_out_ = nullptr;
+  uint8_t* h_out_ = nullptr;
   int* d_match_ = nullptr;
   int* d_nm_ = nullptr;
   int* h_match_ = nullptr;
@@ -212,7 +218,7 @@ class MapEngine {
   // D1
   float* d_edges_ = nullptr;
   float* h_edges_ = nullptr;
-  PoseOptDesc* d_pod_ = nullptr;
+  PoseOptDesc* d_pod_ = nullptr;  // the current chain's descriptor (in its upload block)
   PoseOptDesc* h_pod_ = nullptr;
   float* d_pose_ = nullptr;
   uint8_t* d_outl_ = nullptr;
@@ -222,8 +228,6 @@ class MapEngine {
   float* h_pose_ = nullptr;
   uint8_t* h_outl_ = nullptr;
   int* h_ninl_ = nullptr;
-  uint8_t* d_base_ = nullptr;  // C3 -> D1: per key, the position of a binding held before the
-  uint8_t* h_base_ = nullptr;  // search (kcap x 3 floats) and its flag (kcap bytes)
   // C3: point pool, local selection, candidates
   LocalPointDev* d_pool_ = nullptr;
   uint8_t* d_pool_desc_ = nullptr;
@@ -231,7 +235,9 @@ class MapEngine {
   PoolUpdate* d_up_ = nullptr;
   PoolUpdate* h_up_ = nullptr;
   int up_cap_ = 0;
-  uint8_t* d_sel_ = nullptr;  // [ids m][skip m][taken kcap]
+  // C3's one upload: [D1 descriptor][ids m][skip m][taken n] and, for D1's edge list, the keys
+  // bound before the search: [positions 3n floats][flags n] (sel_layout)
+  uint8_t* d_sel_ = nullptr;
   uint8_t* h_sel_ = nullptr;
   uint8_t* d_inview_ = nullptr;
   uint8_t* h_inview_ = nullptr;

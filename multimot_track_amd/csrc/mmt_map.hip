@@ -99,31 +99,51 @@ MapEngine::~MapEngine() {
 
 static size_t last_bytes(int n) { return (size_t)n * (sizeof(mmt_kp) + 12 + 32 + 2); }
 
+// every chain (C2 -> D1, C3 -> D1) moves one block up and one block down
+constexpr size_t kDescBytes = 256;  // D1's descriptor at the head of an upload block
+static_assert(sizeof(PoseOptDesc) <= kDescBytes, "PoseOptDesc outgrew its slot");
+constexpr size_t kOutHdr = 128;     // [nm][ninl][pad][pose] at the head of the download block
+static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// C3's upload block for m local points and n keys: offsets of taken (after ids, skip), the base
+// positions and their flags, and the total size
+struct SelLayout {
+  size_t ids, skip, taken, bX, bHas, total;
+  SelLayout(int m, int n) {
+    ids = kDescBytes;
+    skip = ids + 4 * (size_t)m;
+    taken = skip + m;
+    bX = align16(taken + n);
+    bHas = bX + 12 * (size_t)n;
+    total = bHas + n;
+  }
+};
+
+size_t MapEngine::out_bytes(int n) const { return kOutHdr + 4 * (size_t)kcap_ + n; }
+
 void MapEngine::setup(const MapCamH& cam, int kcap) {
   cam_ = cam;
   kcap_ = kcap;
-  d_last_ = dev<uint8_t>(last_bytes(kcap));
-  h_last_ = pinned<uint8_t>(last_bytes(kcap));
+  d_last_ = dev<uint8_t>(kDescBytes + last_bytes(kcap));
+  h_last_ = pinned<uint8_t>(kDescBytes + last_bytes(kcap));
   c2_ = CandSet{dev<uint32_t>((size_t)kcap * kCandK), dev<int>((size_t)kcap * kCandK),
                 dev<int>(kcap), dev<PointWin>(kcap), dev<int>(kcap)};
-  d_match_ = dev<int>(kcap);
-  d_nm_ = dev<int>(1);
-  h_match_ = pinned<int>(kcap);
-  h_nm_ = pinned<int>(1);
+  d_out_ = dev<uint8_t>(kOutHdr + 5 * (size_t)kcap);
+  h_out_ = pinned<uint8_t>(kOutHdr + 5 * (size_t)kcap);
+  d_nm_ = (int*)d_out_;
+  d_ninl_ = (int*)(d_out_ + 4);
+  d_pose_ = (float*)(d_out_ + 16);
+  d_match_ = (int*)(d_out_ + kOutHdr);
+  d_outl_ = d_out_ + kOutHdr + 4 * (size_t)kcap;
+  h_nm_ = (int*)h_out_;
+  h_ninl_ = (int*)(h_out_ + 4);
+  h_pose_ = (float*)(h_out_ + 16);
+  h_match_ = (int*)(h_out_ + kOutHdr);
+  h_outl_ = h_out_ + kOutHdr + 4 * (size_t)kcap;
   d_edges_ = dev<float>(7 * (size_t)kcap);
   h_edges_ = pinned<float>(7 * (size_t)kcap);
-  d_pod_ = dev<PoseOptDesc>(1);
-  h_pod_ = pinned<PoseOptDesc>(1);
-  d_pose_ = dev<float>(16);
-  d_outl_ = dev<uint8_t>(kcap);
-  d_ninl_ = dev<int>(1);
   d_esc_ = dev<double>(3 * (size_t)kcap);
   d_fsc_ = dev<int>(kcap);
-  h_pose_ = pinned<float>(16);
-  h_outl_ = pinned<uint8_t>(kcap);
-  h_ninl_ = pinned<int>(1);
-  d_base_ = dev<uint8_t>(13 * (size_t)kcap);
-  h_base_ = pinned<uint8_t>(13 * (size_t)kcap);
   prof_on_ = getenv("MMT_MAP_PROFILE") != nullptr;
   frameNextId_ = 0;
   mbVO_ = false;
@@ -134,7 +154,7 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
 
 // the local-map buffers grow with the local map; the point pool with the map
 void MapEngine::grow_local(int m) {
-  if (m <= local_cap_) return;
+  if (m <= local_cap_ && d_sel_) return;
   const int cap = std::max(m + 4096, 2 * local_cap_);
   void* old[] = {d_sel_, h_sel_, d_inview_, h_inview_, c3_.key, c3_.idx, c3_.n, c3_.win,
                  c3_.choice};
@@ -151,8 +171,9 @@ void MapEngine::grow_local(int m) {
       dallocs_.erase(it);
     }
   }
-  d_sel_ = dev<uint8_t>((size_t)5 * cap + kcap_);
-  h_sel_ = pinned<uint8_t>((size_t)5 * cap + kcap_);
+  const size_t sel_cap = SelLayout(cap, kcap_).total + 16;
+  d_sel_ = dev<uint8_t>(sel_cap);
+  h_sel_ = pinned<uint8_t>(sel_cap);
   d_inview_ = dev<uint8_t>(cap);
   h_inview_ = pinned<uint8_t>(cap);
   c3_ = CandSet{dev<uint32_t>((size_t)cap * kCandK), dev<int>((size_t)cap * kCandK), dev<int>(cap),
@@ -423,7 +444,9 @@ void MapEngine::map_point_culling(int kf) {  // LocalMapping::MapPointCulling (R
 // ------------------------------------------------------------------ GPU stages
 // D1's descriptor for an edge list that k_map_edges builds on the device (it writes n): the edge
 // arrays at a fixed capacity of kcap edges
-void MapEngine::pose_desc_upload(const float* Tcw) {
+void MapEngine::pose_desc_fill(uint8_t* h_blk, uint8_t* d_blk, const float* Tcw) {
+  h_pod_ = (PoseOptDesc*)h_blk;
+  d_pod_ = (PoseOptDesc*)d_blk;
   PoseOptDesc& d = *h_pod_;
   memset(&d, 0, sizeof(d));
   d.n = 0;
@@ -437,7 +460,6 @@ void MapEngine::pose_desc_upload(const float* Tcw) {
   d.n_inliers = d_ninl_;
   d.e_scratch = d_esc_;
   d.f_scratch = d_fsc_;
-  MMT_HIP(hipMemcpyAsync(d_pod_, h_pod_, sizeof(PoseOptDesc), hipMemcpyHostToDevice, s_));
 }
 
 MapEdgeArgs MapEngine::edge_args(const GridFrame& G) const {
@@ -479,8 +501,8 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
                                const float* Tlast, float th, float retry_th, int min_matches) {
   const double t_pack = prof_on_ ? now_us() : 0;
   const int n1 = L.n;
-  uint8_t* hk = h_last_;
-  float* hX = (float*)(h_last_ + (size_t)n1 * sizeof(mmt_kp));
+  uint8_t* hk = h_last_ + kDescBytes;
+  float* hX = (float*)(hk + (size_t)n1 * sizeof(mmt_kp));
   uint8_t* hD = (uint8_t*)(hX + 3 * (size_t)n1);
   uint8_t* hA = hD + 32 * (size_t)n1;
   uint8_t* hO = hA + n1;
@@ -499,11 +521,12 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
     }
   }
   if (prof_on_) prof_[9] += now_us() - t_pack;
-  MMT_HIP(hipMemcpyAsync(d_last_, h_last_, last_bytes(n1), hipMemcpyHostToDevice, s_));
-  pose_desc_upload(Tcw);
+  pose_desc_fill(h_last_, d_last_, Tcw);
+  MMT_HIP(hipMemcpyAsync(d_last_, h_last_, kDescBytes + last_bytes(n1), hipMemcpyHostToDevice,
+                         s_));
   LastFrameDev LD;
-  LD.keys = (const mmt_kp*)d_last_;
-  LD.Xw = (const float*)(d_last_ + (size_t)n1 * sizeof(mmt_kp));
+  LD.keys = (const mmt_kp*)(d_last_ + kDescBytes);
+  LD.Xw = (const float*)(d_last_ + kDescBytes + (size_t)n1 * sizeof(mmt_kp));
   LD.mp_desc = (const uint8_t*)(LD.Xw + 3 * (size_t)n1);
   LD.active = LD.mp_desc + 32 * (size_t)n1;
   LD.obs = LD.active + n1;
@@ -518,11 +541,7 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
   e.src_X = LD.Xw;
   launch_map_edges(e, s_);
   launch_pose_opt(d_pod_, 1, std::min(C.n, nact), s_);
-  MMT_HIP(hipMemcpyAsync(h_match_, d_match_, sizeof(int) * (size_t)C.n, hipMemcpyDeviceToHost, s_));
-  MMT_HIP(hipMemcpyAsync(h_nm_, d_nm_, sizeof(int), hipMemcpyDeviceToHost, s_));
-  MMT_HIP(hipMemcpyAsync(h_pose_, d_pose_, 64, hipMemcpyDeviceToHost, s_));
-  if (C.n > 0) MMT_HIP(hipMemcpyAsync(h_outl_, d_outl_, (size_t)C.n, hipMemcpyDeviceToHost, s_));
-  MMT_HIP(hipMemcpyAsync(h_ninl_, d_ninl_, sizeof(int), hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
   MMT_HIP(hipStreamSynchronize(s_));
   std::fill(C.mps.begin(), C.mps.end(), -1);
   for (int i2 = 0; i2 < C.n; i2++)
@@ -804,9 +823,10 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
   const int m = (int)localPts_.size();
   grow_local(m);
   gpu_flush_pool();
-  int* ids = (int*)h_sel_;
-  uint8_t* skip = h_sel_ + 4 * (size_t)m;
-  uint8_t* taken = skip + m;
+  const SelLayout sl(m, C.n);
+  int* ids = (int*)(h_sel_ + sl.ids);
+  uint8_t* skip = h_sel_ + sl.skip;
+  uint8_t* taken = h_sel_ + sl.taken;
   for (int j = 0; j < m; j++) {
     const MPoint& p = mp(localPts_[j]);
     ids[j] = localPts_[j];
@@ -814,8 +834,8 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
   }
   // the keys bound before the search: taken (Observations() > 0) and, for D1's edge list, their
   // points' positions
-  float* bX = (float*)h_base_;
-  uint8_t* bHas = h_base_ + 12 * (size_t)kcap_;
+  float* bX = (float*)(h_sel_ + sl.bX);
+  uint8_t* bHas = h_sel_ + sl.bHas;
   int nbase = 0;
   for (int i = 0; i < C.n; i++) {
     const int h = C.mps[i];
@@ -829,31 +849,23 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
     }
   }
   if (prof_on_) prof_[10] += now_us() - t_pack;
-  MMT_HIP(hipMemcpyAsync(d_sel_, h_sel_, 5 * (size_t)m + C.n, hipMemcpyHostToDevice, s_));
-  if (C.n > 0) {
-    MMT_HIP(hipMemcpyAsync(d_base_, h_base_, 12 * (size_t)C.n, hipMemcpyHostToDevice, s_));
-    MMT_HIP(hipMemcpyAsync(d_base_ + 12 * (size_t)kcap_, bHas, (size_t)C.n,
-                           hipMemcpyHostToDevice, s_));
-  }
-  pose_desc_upload(Tcw);
+  pose_desc_fill(h_sel_, d_sel_, Tcw);
+  MMT_HIP(hipMemcpyAsync(d_sel_, h_sel_, sl.total, hipMemcpyHostToDevice, s_));
   // ORBmatcher(0.8)::SearchByProjection's th: 3 for RGB-D, 5 right after a relocalisation
   const float th = curId_ < lastRelocFrameId_ + 2 ? 5.f : 3.f;
-  LocalSel sel{(const int*)d_sel_, d_sel_ + 4 * (size_t)m, d_inview_};
-  launch_search_local(G, Tcw, d_pool_, d_pool_desc_, m, th, d_sel_ + 5 * (size_t)m, nullptr, c3_,
+  LocalSel sel{(const int*)(d_sel_ + sl.ids), d_sel_ + sl.skip, d_inview_};
+  launch_search_local(G, Tcw, d_pool_, d_pool_desc_, m, th, d_sel_ + sl.taken, nullptr, c3_,
                       d_match_, d_nm_, s_, &sel);
   // D1 over every key bound after the search (Tracking.cc:3189-3200), chained on the device
   MapEdgeArgs e = edge_args(G);
   e.pool = d_pool_;
-  e.ids = (const int*)d_sel_;
-  e.has_base = d_base_ + 12 * (size_t)kcap_;
-  e.base_X = (const float*)d_base_;
+  e.ids = (const int*)(d_sel_ + sl.ids);
+  e.has_base = d_sel_ + sl.bHas;
+  e.base_X = (const float*)(d_sel_ + sl.bX);
   launch_map_edges(e, s_);
   launch_pose_opt(d_pod_, 1, std::min(C.n, nbase + m), s_);
-  MMT_HIP(hipMemcpyAsync(h_match_, d_match_, sizeof(int) * (size_t)C.n, hipMemcpyDeviceToHost, s_));
+  MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
   if (m > 0) MMT_HIP(hipMemcpyAsync(h_inview_, d_inview_, (size_t)m, hipMemcpyDeviceToHost, s_));
-  MMT_HIP(hipMemcpyAsync(h_pose_, d_pose_, 64, hipMemcpyDeviceToHost, s_));
-  if (C.n > 0) MMT_HIP(hipMemcpyAsync(h_outl_, d_outl_, (size_t)C.n, hipMemcpyDeviceToHost, s_));
-  MMT_HIP(hipMemcpyAsync(h_ninl_, d_ninl_, sizeof(int), hipMemcpyDeviceToHost, s_));
   MMT_HIP(hipStreamSynchronize(s_));
   for (int j = 0; j < m; j++) {
     if (skip[j]) continue;

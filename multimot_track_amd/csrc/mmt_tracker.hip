@@ -228,8 +228,11 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // scratch: the ego solve (caller stream) and the object solves (ob_, one D3 launch at a time)
   d_lm_scratch_ = alloc<double>(flow_scratch_doubles(lmcap) * (1 + kMaxObj));
   d_descs_ = alloc<FlowSolveDesc>(1);
-  d_poses_ = alloc<float>(16);
-  d_lmstats_ = alloc<int>(3);
+  // D2's pose and stats in one block, brought back by one copy into EgoHost::Tcw / st
+  static_assert(offsetof(EgoHost, st) == offsetof(EgoHost, Tcw) + 16 * sizeof(float),
+                "EgoHost::st must follow Tcw");
+  d_poses_ = alloc<float>(20);
+  d_lmstats_ = (int*)(d_poses_ + 16);
   d_gx_ = alloc<unsigned long long>(kFlowSplitGranules);
   MMT_HIP(hipMemset(d_gx_, 0, sizeof(unsigned long long) * kFlowSplitGranules));
   // PnP
@@ -570,8 +573,8 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
     launch_flow_lm_split(d_descs_, groups, st);
   else
     launch_flow_lm(d_descs_, 1, eh_->n_static[last_], st);
-  MMT_HIP(hipMemcpyAsync(eh_->Tcw, d_poses_, sizeof(eh_->Tcw), hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(eh_->st, d_lmstats_, sizeof(eh_->st), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(eh_->Tcw, d_poses_, sizeof(eh_->Tcw) + sizeof(eh_->st),
+                         hipMemcpyDeviceToHost, st));
   ego_pending_ = true;
 }
 
