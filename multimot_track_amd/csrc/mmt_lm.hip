@@ -1991,19 +1991,26 @@ __global__ __launch_bounds__(kPoThreads) void k_pose_opt_r(const PoseOptDesc* __
 }
 
 void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, int n_max, hipStream_t st) {
-  // MMT_PO_VARIANT: 2 (default) light trial passes + lambda candidates, 1 register kernel with a
-  // full pass per trial, 0 the LDS kernel for every size (A/B knobs)
+  // MMT_PO_VARIANT: 2 (default) light trial passes + lambda candidates, the two-edge variant for
+  // every count up to 2 * kPoThreads (one launch fewer: the map chains' bound n_max is always
+  // above kPoThreads); 3 the same with the one-edge variant for counts up to kPoThreads; 1
+  // register kernel with a full pass per trial; 0 the LDS kernel for every size (A/B knobs).
+  // One kernel holding several variants spills (580 B per lane), so each is a launch of its own.
   static const int variant = [] {
     const char* e = getenv("MMT_PO_VARIANT");
     return e ? atoi(e) : 2;
   }();
-  if (variant == 2) {
+  if (variant == 2 || variant == 3) {
     // the edge count is known on the device only: every variant whose range meets [0, n_max]
     // is launched and the ones outside the solve's count return at once (n_max is a bound)
-    hipLaunchKernelGGL(k_pose_opt_l<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
-    if (n_max > kPoThreads)
-      hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
-                         kPoThreads);
+    if (variant == 3) {
+      hipLaunchKernelGGL(k_pose_opt_l<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
+      if (n_max > kPoThreads)
+        hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
+                           kPoThreads);
+    } else {
+      hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
+    }
     if (n_max > 2 * kPoThreads)
       hipLaunchKernelGGL(k_pose_opt_l<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
                          2 * kPoThreads);

@@ -74,7 +74,15 @@ __device__ __forceinline__ int wg_compact_slot(bool keep, int* s_w, int& base) {
   return slot;
 }
 
-// B2 (+ mvSiftDepthTmp) for one frame; single workgroup of 1024 threads.
+// B2 (+ mvSiftDepthTmp) for one frame; single workgroup of 1024 threads.  Each thread takes up to
+// kSsItems consecutive keys per round and issues all their key loads, then all their depth, label
+// and flow gathers, before anything waits: two memory round trips per round (a key count up to
+// 4,096 is one round), not three per 1,024 keys.  The flow is gathered for every key and used
+// only where the label and depth keep it.
+constexpr int kSsItems = 4;
+
+__device__ __forceinline__ int block_scan_excl(int v, int* s_w, int& excl);
+
 __global__ __launch_bounds__(1024) void k_static_samples(const mmt_kp* __restrict__ kps,
                                                          const int* __restrict__ nkp,
                                                          const float* __restrict__ depth,
@@ -84,30 +92,55 @@ __global__ __launch_bounds__(1024) void k_static_samples(const mmt_kp* __restric
   __shared__ int s_w[16];
   const int n = *nkp;
   int base = 0;
-  for (int r0 = 0; r0 < n; r0 += blockDim.x) {
-    const int i = r0 + threadIdx.x;
-    bool keep = false;
-    float kx = 0, ky = 0, fxe = 0, fye = 0, d = 0;
-    if (i < n) {
-      kx = kps[i].x;
-      ky = kps[i].y;
-      const int x = (int)kx, y = (int)ky;
-      const size_t p = (size_t)y * W + x;
-      d = depth[p];
-      if (mask[p] == 0 && !(d > 40 || d <= 0)) {
-        const float2 fl = flow[p];
-        fxe = fl.x;
-        fye = fl.y;
-        keep = fxe != 0 && fye != 0 && kx + fxe < W && ky + fye < H && kx < W && ky < H;
+  for (int r0 = 0; r0 < n; r0 += kSsItems * (int)blockDim.x) {
+    const int i0 = r0 + kSsItems * (int)threadIdx.x;
+    float kx[kSsItems], ky[kSsItems], d[kSsItems];
+    int lab[kSsItems];
+    float2 fl[kSsItems];
+#pragma unroll
+    for (int k = 0; k < kSsItems; k++) {
+      kx[k] = ky[k] = 0;
+      if (i0 + k < n) {
+        kx[k] = kps[i0 + k].x;
+        ky[k] = kps[i0 + k].y;
       }
     }
-    const int slot = wg_compact_slot(keep, s_w, base);
-    if (keep && slot < out.cap) {
-      out.keys[slot] = make_float2(kx, ky);
-      out.corres[slot] = make_float2(kx + fxe, ky + fye);
-      out.flow[slot] = make_float2(fxe, fye);
-      out.depth[slot] = d;  // > 0 here, mvSiftDepthTmp (Frame.cc:312-324)
+#pragma unroll
+    for (int k = 0; k < kSsItems; k++) {
+      d[k] = 0;
+      lab[k] = 1;
+      fl[k] = make_float2(0.f, 0.f);
+      if (i0 + k < n) {
+        const size_t p = (size_t)(int)ky[k] * W + (int)kx[k];
+        d[k] = depth[p];
+        lab[k] = mask[p];
+        fl[k] = flow[p];
+      }
     }
+    int cnt = 0;
+    bool keep[kSsItems];
+#pragma unroll
+    for (int k = 0; k < kSsItems; k++) {
+      const float fxe = fl[k].x, fye = fl[k].y;
+      keep[k] = i0 + k < n && lab[k] == 0 && !(d[k] > 40 || d[k] <= 0) && fxe != 0 && fye != 0 &&
+                kx[k] + fxe < W && ky[k] + fye < H && kx[k] < W && ky[k] < H;
+      cnt += keep[k] ? 1 : 0;
+    }
+    int excl;
+    const int tot = block_scan_excl(cnt, s_w, excl);
+    int slot = base + excl;
+#pragma unroll
+    for (int k = 0; k < kSsItems; k++) {
+      if (!keep[k]) continue;
+      if (slot < out.cap) {
+        out.keys[slot] = make_float2(kx[k], ky[k]);
+        out.corres[slot] = make_float2(kx[k] + fl[k].x, ky[k] + fl[k].y);
+        out.flow[slot] = fl[k];
+        out.depth[slot] = d[k];  // > 0 here, mvSiftDepthTmp (Frame.cc:312-324)
+      }
+      slot++;
+    }
+    base += tot;
   }
   if (threadIdx.x == 0) *out.count = min(base, out.cap);
 }

@@ -118,6 +118,18 @@ static T* dalloc(size_t n) {
 }
 
 Tracker::~Tracker() {
+  if (ow_.joinable()) {
+    obj_drain(true);
+    {
+      std::lock_guard<std::mutex> lk(om_);
+      o_stop_ = true;
+    }
+    ocv_.notify_all();
+    ow_.join();
+  }
+  for (auto& e : ev_slot_)
+    for (hipEvent_t& x : e)
+      if (x) (void)hipEventDestroy(x);
   if (hprof_ && hprof_n_ > 0)
     fprintf(stderr, "[mmt tracker profile] %ld frames, host wall us per frame: map finish + obj_advance %.1f, "
             "ego_launch %.1f, ego_finish %.1f\n", hprof_n_, hprof_us_[0] / hprof_n_,
@@ -316,14 +328,194 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // high-priority stream, which the runtime maps to a separate queue.
   int lo = 0, hi = 0;
   MMT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  MMT_HIP(hipStreamCreateWithPriority(&oa_, hipStreamNonBlocking, lo));
+  // The RANSAC stream is confined to every 4th CU (MMT_RANSAC_CU_MASK=0: all CUs, low priority).
+  // Its kernels are grids of hundreds of one-wave workgroups at 256 VGPRs; spread over the whole
+  // chip they leave no CU with a free SIMD for the ego chain's and D3's workgroups (256-thread
+  // solves at 256 VGPRs + 230 AGPRs need all four SIMDs of a CU), which then wait for the RANSAC
+  // kernels to drain.
+  const char* cm = getenv("MMT_RANSAC_CU_MASK");
+  if (!(cm && atoi(cm) == 0)) {
+    int ncu = 0;
+    MMT_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg.device_id));
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; c += 4) mask[c / 32] |= 1u << (c % 32);
+    MMT_HIP(hipExtStreamCreateWithCUMask(&oa_, (uint32_t)mask.size(), mask.data()));
+  } else {
+    MMT_HIP(hipStreamCreateWithPriority(&oa_, hipStreamNonBlocking, lo));
+  }
   MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, hi));
   MMT_HIP(hipHostMalloc((void**)&eh_, sizeof(EgoHost), hipHostMallocDefault));
   memset(eh_, 0, sizeof(EgoHost));
+  for (auto& e : ev_slot_)
+    for (hipEvent_t& x : e)
+      if (!x) MMT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
   reset();
+  device_ = cfg.device_id;
+  const char* ot = getenv("MMT_OBJ_THREAD");  // 0: the object path inline (one host thread)
+  ow_on_ = !(ot && atoi(ot) == 0);
+  if (ow_on_ && !ow_.joinable()) ow_ = std::thread([this] { obj_worker_main(); });
+}
+
+// ------------------------------------------------------------------ object worker
+void Tracker::obj_job(ObjFrame& F) {
+  auto now = [] {
+    return std::chrono::duration<double, std::micro>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  const double t0 = hprof_ ? now() : 0;
+  obj_stage_a(F);
+  const double t1 = hprof_ ? now() : 0;
+  obj_stage_b(F);
+  if (hprof_) {
+    hprof_us_[4] += t1 - t0;
+    hprof_us_[5] += now() - t1;
+  }
+  // everything this job enqueued that reads its two frame slots
+  for (int s : {F.cur, F.last}) {
+    MMT_HIP(hipEventRecord(ev_slot_[s][0], oa_));
+    MMT_HIP(hipEventRecord(ev_slot_[s][1], ob_));
+  }
+}
+
+void Tracker::obj_worker_main() {
+  (void)hipSetDevice(device_);
+  auto guarded = [this](auto&& fn) {
+    int kind = 0;
+    std::string msg;
+    try {
+      fn();
+    } catch (const DeviceError& e) {
+      kind = 1;
+      msg = e.msg;
+    } catch (const ArgError& e) {
+      kind = 2;
+      msg = e.msg;
+    } catch (const std::exception& e) {
+      kind = 1;
+      msg = e.what();
+    } catch (...) {
+      kind = 1;
+      msg = "object worker: unknown exception";
+    }
+    if (kind) {
+      std::lock_guard<std::mutex> lk(om_);
+      if (!o_err_kind_) {
+        o_err_kind_ = kind;
+        o_err_ = msg;
+      }
+    }
+  };
+  auto now = [] {
+    return std::chrono::duration<double, std::micro>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  std::unique_lock<std::mutex> lk(om_);
+  for (;;) {
+    ocv_.wait(lk, [&] {
+      return o_stop_ || !oq_.empty() ||
+             (!inflight_.empty() && (inflight_.front().seq <= o_need_fin_ || o_discard_));
+    });
+    if (o_stop_ && oq_.empty()) return;
+    if (!oq_.empty()) {
+      ObjFrame F = oq_.front();
+      oq_.pop_front();
+      if (!o_discard_ && !o_err_kind_) {
+        lk.unlock();
+        guarded([&] { obj_job(F); });
+        lk.lock();
+      }
+      inflight_.push_back(F);
+    }
+    // finish in order: beyond the lag, what the main thread waits for, or everything when the
+    // jobs are dropped
+    while (!inflight_.empty() &&
+           ((int)inflight_.size() > kObjLag || inflight_.front().seq <= o_need_fin_ ||
+            o_discard_ || o_err_kind_)) {
+      ObjFrame G = inflight_.front();
+      inflight_.pop_front();
+      if (!o_discard_ && !o_err_kind_) {
+        lk.unlock();
+        const double t0 = hprof_ ? now() : 0;
+        guarded([&] { obj_finish(G); });
+        if (hprof_) hprof_us_[6] += now() - t0;
+        lk.lock();
+      }
+      o_finished_ = G.seq;
+      odone_.notify_all();
+    }
+  }
+}
+
+void Tracker::obj_check() {
+  int kind = 0;
+  std::string msg;
+  {
+    std::lock_guard<std::mutex> lk(om_);
+    kind = o_err_kind_;
+    msg = o_err_;
+    o_err_kind_ = 0;
+    o_err_.clear();
+  }
+  if (kind == 1) throw DeviceError(msg);
+  if (kind == 2) throw ArgError(msg);
+}
+
+void Tracker::obj_submit(const ObjFrame& F0) {
+  obj_check();
+  ObjFrame F = F0;
+  {
+    std::lock_guard<std::mutex> lk(om_);
+    F.seq = ++o_handed_;
+    oq_.push_back(F);
+  }
+  slot_job_[F.cur] = slot_job_[F.last] = F.seq;
+  ocv_.notify_one();
+}
+
+void Tracker::slot_wait(int s, hipStream_t st) {
+  const long k = slot_job_[s];
+  if (k == 0) return;
+  {
+    std::unique_lock<std::mutex> lk(om_);
+    if (o_finished_ < k) {
+      o_need_fin_ = std::max(o_need_fin_, k);
+      ocv_.notify_one();
+      odone_.wait(lk, [&] { return o_finished_ >= k; });
+    }
+  }
+  obj_check();
+  // the job is frames old: its device work has normally finished, and a wait would put a barrier
+  // packet on the ego queue for nothing
+  for (hipEvent_t e : ev_slot_[s]) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipErrorNotReady)
+      MMT_HIP(hipStreamWaitEvent(st, e, 0));
+    else if (q != hipSuccess)
+      MMT_HIP(q);
+  }
+  slot_job_[s] = 0;
+}
+
+void Tracker::obj_drain(bool discard) {
+  if (!ow_.joinable()) return;
+  {
+    std::unique_lock<std::mutex> lk(om_);
+    if (discard) o_discard_ = true;
+    o_need_fin_ = o_handed_;
+    ocv_.notify_one();
+    odone_.wait(lk, [&] { return o_finished_ >= o_handed_; });
+    o_discard_ = false;
+    if (discard) {
+      o_err_kind_ = 0;
+      o_err_.clear();
+    }
+  }
+  if (!discard) obj_check();
 }
 
 void Tracker::reset() {
+  obj_drain(true);
+  for (long& k : slot_job_) k = 0;
   if (oa_) MMT_HIP(hipStreamSynchronize(oa_));
   if (ob_) MMT_HIP(hipStreamSynchronize(ob_));
   state_ = 0;
@@ -334,7 +526,10 @@ void Tracker::reset() {
   last_ = kSlots - 1;
   ego_pending_ = false;
   qa_ = ObjFrame();
-  inflight_.clear();
+  {
+    std::lock_guard<std::mutex> lk(om_);  // the worker is idle (drained), its queue empty
+    inflight_.clear();
+  }
   obj_slot_next_ = 0;
   for (FrameSlot& F : slot_) {
     F.nModLabel.clear();
@@ -397,7 +592,9 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   // Two chains per sequence: ego (samples, hand-off, D2 of frame f needs frame f-1's pose) on
   // `st`, and objects (grouping, PnP, D3 of frame f need frame f's pose and frame f-1's objects)
   // on ost_.  Frame f's ego solve runs on the GPU while the host drives frame f-1's object path.
+  try {
   for (int f = 0; f < nframes; f++) {
+    if (ow_on_) slot_wait(cur_, st);  // the slot this frame's ego path writes
     FrameArgs a;
     a.depth = d_depth_ + npix * f;
     a.flow = (const float2*)((const uint8_t*)d_flow + flow_pitch * f);
@@ -417,9 +614,13 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
       const double t1 = now();
       ego_map_finish(outs[f]);
       hprof_us_[3] += now() - t1;
-      obj_advance();
+      if (!ow_on_) obj_advance();
       const double t2 = now();
       ego_finish(outs[f], st);
+      if (ow_on_ && qa_.active) {
+        obj_submit(qa_);
+        qa_ = ObjFrame();
+      }
       hprof_us_[0] += t2 - t1;
       hprof_us_[1] += t1 - t0;
       hprof_us_[2] += now() - t2;
@@ -430,10 +631,22 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
     // host finishes the map branch (keyframes) and drives frame f-1's object path
     ego_launch(a, outs[f], st);
     ego_map_finish(outs[f]);
-    obj_advance();
+    if (!ow_on_) obj_advance();
     ego_finish(outs[f], st);
+    if (ow_on_ && qa_.active) {  // the frame's object path, on the worker
+      obj_submit(qa_);
+      qa_ = ObjFrame();
+    }
   }
-  obj_flush();  // the chunk's results are complete on return
+  } catch (...) {
+    obj_drain(true);  // no job may outlive the call (they write into `outs`)
+    throw;
+  }
+  // the chunk's results are complete on return
+  if (ow_on_)
+    obj_drain(false);
+  else
+    obj_flush();
 }
 
 // Enqueue the queued frame's whole object path (stage A's host decisions need one wait for the

@@ -13,7 +13,7 @@ rows = list(csv.DictReader(open(f)))
 ks = []
 for r in rows:
     name = r.get("Kernel_Name", r.get("KernelName", ""))
-    if "mmt::" not in name:
+    if "mmt::" not in name and "rocclr_copy" not in name:
         continue
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     q = r.get("Queue_Id", r.get("Stream_Id", "?"))
