@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <set>
 #include <utility>
@@ -126,6 +127,11 @@ class MapEngine {
   // cleanup, NeedNewKeyFrame / CreateNewKeyFrame (Tracking.cc:1127-1160); host only, so it runs
   // while the flow solve that starts from the pose is on the GPU
   void track_finish(MapFrameH& C, MapFrameH& L, const float* Tcw, MapStatsH& st);
+  // host work to run while the next device chain (C2 or C3 + D1) of track() executes, once: the
+  // tracker hands the previous frame's object path here, which would otherwise wait for the GPU
+  // beside the ego solve.  Returns whether it is still pending (track() ran no chain).
+  void set_overlap(std::function<void()> fn) { overlap_ = std::move(fn); }
+  bool overlap_pending() const { return (bool)overlap_; }
   // end of Track: mlRelativeFramePoses.push_back(Tcw * Tref^-1) (Tracking.cc:2481-2489)
   void frame_done(const MapFrameH& C, const float* Tcw);
   int state() const { return state_; }
@@ -133,6 +139,13 @@ class MapEngine {
   int n_mappoints() const { return n_good_; }
 
  private:
+  std::function<void()> overlap_;
+  void run_overlap() {
+    if (!overlap_) return;
+    std::function<void()> fn = std::move(overlap_);
+    overlap_ = nullptr;
+    fn();
+  }
   static constexpr int kTemp = 1 << 29;
   MPoint& mp(int h) { return h >= kTemp ? temps_[h - kTemp] : pts_[h]; }
   bool track_with_motion_model(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,

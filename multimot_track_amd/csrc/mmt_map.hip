@@ -542,6 +542,7 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
   launch_map_edges(e, s_);
   launch_pose_opt(d_pod_, 1, std::min(C.n, nact), s_);
   MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
+  run_overlap();
   MMT_HIP(hipStreamSynchronize(s_));
   std::fill(C.mps.begin(), C.mps.end(), -1);
   for (int i2 = 0; i2 < C.n; i2++)
@@ -866,6 +867,7 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
   launch_pose_opt(d_pod_, 1, std::min(C.n, nbase + m), s_);
   MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
   if (m > 0) MMT_HIP(hipMemcpyAsync(h_inview_, d_inview_, (size_t)m, hipMemcpyDeviceToHost, s_));
+  run_overlap();
   MMT_HIP(hipStreamSynchronize(s_));
   for (int j = 0; j < m; j++) {
     if (skip[j]) continue;

@@ -264,6 +264,9 @@ class Tracker {
   double hprof_us_[7] = {0, 0, 0, 0, 0, 0, 0};  // + map finish, stage A, stage B, obj finish
   long hprof_n_ = 0;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
+  // the previous frame's object path inside the first map chain of the frame (MMT_OBJ_OVERLAP)
+  bool overlap_obj_ = false;
+  bool obj_ran_ = false;
   // object worker
   bool ow_on_ = false;
   int device_ = 0;

@@ -343,7 +343,8 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   } else {
     MMT_HIP(hipStreamCreateWithPriority(&oa_, hipStreamNonBlocking, lo));
   }
-  MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, hi));
+  const char* dp = getenv("MMT_D3_PRIO");  // 0: the D3 stream at normal priority (A/B knob)
+  MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, dp && atoi(dp) == 0 ? 0 : hi));
   MMT_HIP(hipHostMalloc((void**)&eh_, sizeof(EgoHost), hipHostMallocDefault));
   memset(eh_, 0, sizeof(EgoHost));
   for (auto& e : ev_slot_)
@@ -351,8 +352,15 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
       if (!x) MMT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
   reset();
   device_ = cfg.device_id;
-  const char* ot = getenv("MMT_OBJ_THREAD");  // 0: the object path inline (one host thread)
-  ow_on_ = !(ot && atoi(ot) == 0);
+  // MMT_OBJ_THREAD=1: the object path's host side on a worker thread.  Off by default: C3 is
+  // bound by the device chains, not the host (853 fps either way), and the hand-offs cost C2
+  // about 2 % (tools/env_ab_quick.sh)
+  // MMT_OBJ_OVERLAP=1: the object path inside the first map chain (measured slower: 836 against
+  // 850 fps, tools/env_ab_quick.sh)
+  const char* oo = getenv("MMT_OBJ_OVERLAP");
+  overlap_obj_ = oo && atoi(oo) == 1;
+  const char* ot = getenv("MMT_OBJ_THREAD");
+  ow_on_ = ot && atoi(ot) == 1;
   if (ow_on_ && !ow_.joinable()) ow_ = std::thread([this] { obj_worker_main(); });
 }
 
@@ -595,6 +603,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   try {
   for (int f = 0; f < nframes; f++) {
     if (ow_on_) slot_wait(cur_, st);  // the slot this frame's ego path writes
+    obj_ran_ = false;
     FrameArgs a;
     a.depth = d_depth_ + npix * f;
     a.flow = (const float2*)((const uint8_t*)d_flow + flow_pitch * f);
@@ -614,7 +623,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
       const double t1 = now();
       ego_map_finish(outs[f]);
       hprof_us_[3] += now() - t1;
-      if (!ow_on_) obj_advance();
+      if (!ow_on_ && !obj_ran_) obj_advance();
       const double t2 = now();
       ego_finish(outs[f], st);
       if (ow_on_ && qa_.active) {
@@ -631,7 +640,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
     // host finishes the map branch (keyframes) and drives frame f-1's object path
     ego_launch(a, outs[f], st);
     ego_map_finish(outs[f]);
-    if (!ow_on_) obj_advance();
+    if (!ow_on_ && !obj_ran_) obj_advance();  // when no map chain took it
     ego_finish(outs[f], st);
     if (ow_on_ && qa_.active) {  // the frame's object path, on the worker
       obj_submit(qa_);
@@ -653,6 +662,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
 // grouping statistics; stage B is device-ordered), then read the results of frames older than
 // kObjLag.  Called while the next ego solve runs.
 void Tracker::obj_advance() {
+  obj_ran_ = true;
   auto now = [] {
     return std::chrono::duration<double, std::micro>(
                std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -743,8 +753,11 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
     G.cell_idx = d_cell_idx_ + (size_t)kcap_ * a.f;
     G.n = a.n_keys;
     MapStatsH& ms = out.map;
+    // the previous frame's object path runs while the first map chain is on the GPU
+    if (!ow_on_ && overlap_obj_) map_.set_overlap([this] { obj_advance(); });
     const int rr = map_.track(C.m, G, ego_Tinit_, Ls.m, Ls.Tview, V_, hasVelocity_,
                               bSecondFrame_, ms, st);
+    map_.set_overlap(nullptr);  // not taken (no chain ran): the loop runs it
     ms.state = map_.state();
     memcpy(ms.Tcw_map, ego_Tinit_, sizeof(ego_Tinit_));
     if (rr == 1) {  // LOST with <= 5 keyframes: mpSystem->Reset(); Track returns (:1165-1172)
