@@ -432,6 +432,51 @@ __device__ __forceinline__ void accept_terms(const Cam& c, const DSE3& PN, LMIte
                    it.bl[1], mh, Bnext);
 }
 
+// the split solve's fused trial pass: back-substitution and errors as trial_terms, and the
+// linearisation at the trial state (PN, f + xl) as the accepted trial's pass 2 would compute it,
+// into the tile row: [0] the trial's chi2 term, [1] its scale term, the rest the system the next
+// trial uses if this one is accepted.  The new robust weight, landmark gradient and w J stay
+// pending (pw, pb, Bnext) until the decision; f, w and bl of the item are untouched.
+template <bool FIRST>
+__device__ __forceinline__ void spec_terms(const Cam& c, const DSE3& P, const DSE3& PN, LMItem& it,
+                                           int i, bool ok2, double lam, double ilam,
+                                           const double* xb, double* row, double& pw,
+                                           double& pb0, double& pb1, const double* Bcur,
+                                           double* Bnext) {
+  const double bl0 = it.bl[0], bl1 = it.bl[1];
+  if (ok2) {
+    const double w = it.w, h = w + c.pinfo;
+    double c0 = bl0, c1 = bl1;
+    if (Bcur) {
+#pragma unroll
+      for (int a = 0; a < 6; a++) {
+        c0 -= Bcur[a] * xb[a];
+        c1 -= Bcur[6 + a] * xb[a];
+      }
+    } else {
+      double x, y, z;
+      map(P, it.X, x, y, z);
+      double J[2][6];
+      jac(x, y, drcp(z), c.fx, c.fy, J);
+#pragma unroll
+      for (int a = 0; a < 6; a++) {
+        c0 -= w * J[0][a] * xb[a];
+        c1 -= w * J[1][a] * xb[a];
+      }
+    }
+    const double ihl = drcp(h + lam);
+    double xl0 = c0 * ihl - h * c1 * ihl * ilam;
+    if (i > 0) xl0 += c0 * ilam;  // stride-2 spill of landmark i-1's third Dinv row
+    it.xl[0] = xl0;
+    it.xl[1] = c1 * ilam;
+  }
+  const double xl0 = it.xl[0], xl1 = it.xl[1];
+  const double sc = xl0 * (lam * xl0 + bl0) + xl1 * (lam * xl1 + bl1);
+  double mh = 0;
+  linearise<FIRST>(c, PN, it, it.f[0] + xl0, it.f[1] + xl1, row, sc, it.e[0], it.e[1], pw, pb0,
+                   pb1, mh, Bnext);
+}
+
 #ifdef MMT_LM_PROFILE
 #define MMT_LMPROF(k)                  \
   do {                                 \
@@ -618,7 +663,8 @@ __device__ __forceinline__ void centre_sum_wave(const FlowSolveDesc& D, int N) {
 // workgroups at every reduction through gx)
 template <int IR, bool SPLIT>
 __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int lo, int nt,
-                                             LMSmem& sm, int max_cand, GridX& gx) {
+                                             LMSmem& sm, int max_cand, GridX& gx,
+                                             bool spec_ok = false) {
   const int tid = threadIdx.x, nw = nt >> 6;
 #ifdef MMT_LM_PROFILE
   long long prof_t = 0;
@@ -627,6 +673,12 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
 #endif
   double* G = D.scratch;  // items beyond IR * blockDim
   const int cap = D.cap;
+  // split solve with every workgroup's edges in registers (at most 2 x 256 per slice, the same
+  // answer in every workgroup): a trial is one fused pass (errors + the linearisation at the trial
+  // state) and one exchange, instead of a light pass, an exchange, and for accepted trials a
+  // second pass and exchange.  The ego solve accepts nearly every trial (22 of 24), so the
+  // speculative linearisation is almost never wasted.
+  const bool spec = SPLIT && spec_ok && (gx.ntot + gx.G - 1) / gx.G <= 2 * 256;
   Cam c;
   c.fx = D.fx;
   c.fy = D.fy;
@@ -867,9 +919,34 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         kc++;
       }
       MMT_LMPROF(1);
-      // ---- pass 1: flow back-substitution and the trial's errors (chi2 and scale sums only)
       double lastTrialChi, scale;
-      {
+      // split solve, every edge in registers: one fused pass and one exchange per trial (below)
+      double vn = 0;                        // the trial's sums; the next system if accepted
+      double pw[IR], pb0[IR], pb1[IR];      // pending w, bl of the register items
+      double RBn[12];                       // pending w J of register item 0
+      if (spec) {
+#pragma unroll
+        for (int k = 0; k < IR; k++) {
+          const int i = tid + k * nt;
+          if (i < N) {
+            if (k == 0)
+              spec_terms<true>(c, P, PN, R[k], lo + i, ok2, lam, ilam, xb, row, pw[k], pb0[k],
+                               pb1[k], kCacheB ? RB : nullptr, RBn);
+            else
+              spec_terms<false>(c, P, PN, R[k], lo + i, ok2, lam, ilam, xb, row, pw[k], pb0[k],
+                                pb1[k], nullptr, nullptr);
+          }
+        }
+        if (tid >= N)
+          for (int q = 0; q < kSums; q++) row[q] = 0;
+        MMT_LMPROF(5);
+        vn = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
+        pb ^= 1;
+        vn = gx_sum(gx, vn, kSums);
+        lastTrialChi = lane_value(vn, 0);
+        scale = lane_value(vn, 1);
+      } else {
+      // ---- pass 1: flow back-substitution and the trial's errors (chi2 and scale sums only)
         double s_chi = 0, s_sc = 0;
 #pragma unroll
         for (int k = 0; k < IR; k++) {
@@ -937,7 +1014,23 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         iters = iter + 1;
         bad = !ok;
       }
-      if (accept) {
+      if (accept && spec) {
+        // the fused pass already linearised at the accepted state: take the flow step and the
+        // pending state, and the trial's sums become the current system
+#pragma unroll
+        for (int k = 0; k < IR; k++)
+          if (tid + k * nt < N) {
+            R[k].f[0] += R[k].xl[0];
+            R[k].f[1] += R[k].xl[1];
+            R[k].w = pw[k];
+            R[k].bl[0] = pb0[k];
+            R[k].bl[1] = pb1[k];
+          }
+        if (kCacheB && tid < N)
+#pragma unroll
+          for (int a = 0; a < 12; a++) RB[a] = RBn[a];
+        vc = vn;
+      } else if (accept) {
         // ---- pass 2: take the flow step and linearise at the accepted state (the system of the
         // next trial); rejected trials skip it, so they cost the errors and two sums only
 #pragma unroll
@@ -1052,7 +1145,7 @@ __global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict
 // of the edges (lo = b N / G); the LM bookkeeping runs in every workgroup on the exchanged sums.
 // The workgroups must be resident together: one per CU, at most 8 (bounded spins otherwise).
 __global__ __launch_bounds__(256) void k_flow_lm_split(const FlowSolveDesc* __restrict__ descs,
-                                                       int max_cand) {
+                                                       int max_cand, int spec) {
   __shared__ LMSmem sm;
   const FlowSolveDesc& D = descs[0];
   const int N = D.d_n ? min(*D.d_n, D.cap) : min(D.n, D.cap);
@@ -1074,9 +1167,9 @@ __global__ __launch_bounds__(256) void k_flow_lm_split(const FlowSolveDesc* __re
   if ((int)threadIdx.x >= nt) return;
   GridX gx{D.gx, D.gx_seq, b, G, 0, N, false};
   if (Nl <= nt)
-    flow_lm_body<1, true>(D, Nl, lo, nt, sm, max_cand, gx);
+    flow_lm_body<1, true>(D, Nl, lo, nt, sm, max_cand, gx, spec != 0);
   else
-    flow_lm_body<2, true>(D, Nl, lo, nt, sm, max_cand, gx);
+    flow_lm_body<2, true>(D, Nl, lo, nt, sm, max_cand, gx, spec != 0);
 }
 
 void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipStream_t st) {
@@ -1112,7 +1205,9 @@ void launch_flow_lm_split(const FlowSolveDesc* d_desc, int groups, hipStream_t s
   int max_cand = 4;
   if (const char* e = getenv("MMT_LM_MAX_CAND")) max_cand = std::min(4, std::max(1, atoi(e)));
   groups = std::max(1, std::min(groups, kFlowSplitMax));
-  hipLaunchKernelGGL(k_flow_lm_split, dim3(groups), dim3(256), 0, st, d_desc, max_cand);
+  const char* e = getenv("MMT_LM_SPEC");  // 0: two passes and two exchanges per trial
+  const int spec = !(e && atoi(e) == 0);
+  hipLaunchKernelGGL(k_flow_lm_split, dim3(groups), dim3(256), 0, st, d_desc, max_cand, spec);
 }
 
 size_t flow_scratch_doubles(int cap) { return (size_t)G_COUNT * cap; }
