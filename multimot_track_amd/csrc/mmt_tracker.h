@@ -265,7 +265,7 @@ class Tracker {
   long hprof_n_ = 0;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
   // the previous frame's object path inside the first map chain of the frame (MMT_OBJ_OVERLAP)
-  bool overlap_obj_ = false;
+  bool overlap_obj_ = true;
   bool obj_ran_ = false;
   // object worker
   bool ow_on_ = false;

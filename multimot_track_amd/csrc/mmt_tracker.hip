@@ -352,13 +352,12 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
       if (!x) MMT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
   reset();
   device_ = cfg.device_id;
-  // MMT_OBJ_THREAD=1: the object path's host side on a worker thread.  Off by default: C3 is
-  // bound by the device chains, not the host (853 fps either way), and the hand-offs cost C2
-  // about 2 % (tools/env_ab_quick.sh)
-  // MMT_OBJ_OVERLAP=1: the object path inside the first map chain (measured slower: 836 against
-  // 850 fps, tools/env_ab_quick.sh)
+  // MMT_OBJ_THREAD=1: the object path's host side on a worker thread (903 against 895 fps
+  // inline, 905 with the overlap above, which needs no thread: off by default)
+  // MMT_OBJ_OVERLAP (default 1): the previous frame's object path inside the first map chain of
+  // the frame, while its kernels run (C3 895 -> 905 fps, tools/ab_interleave.py, 4 rounds)
   const char* oo = getenv("MMT_OBJ_OVERLAP");
-  overlap_obj_ = oo && atoi(oo) == 1;
+  overlap_obj_ = !(oo && atoi(oo) == 0);
   const char* ot = getenv("MMT_OBJ_THREAD");
   ow_on_ = ot && atoi(ot) == 1;
   if (ow_on_ && !ow_.joinable()) ow_ = std::thread([this] { obj_worker_main(); });
