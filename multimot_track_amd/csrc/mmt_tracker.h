@@ -96,7 +96,7 @@ class Tracker {
   // the frame's pose and the previous frame's labels; stage B (motion-model matrix from the
   // previous frame's D3 output, MM check, model choice, D3 on ob_) runs entirely on the device,
   // ordered behind the RANSAC by an event and behind the previous frame's D3 by the stream, so the
-  // host enqueues both stages at once and only reads the results kObjLag frames later (finish).
+  // host enqueues both stages at once and only reads the results obj_lag_ frames later (finish).
   struct ObjFrame {
     bool active = false;
     long seq = 0;  // job number (obj_submit)
@@ -181,11 +181,16 @@ class Tracker {
   int state_ = 0, cur_ = 0, last_ = 2;
   bool bFirstFrame_ = false, bSecondFrame_ = false, hasVelocity_ = false;
   float V_[16] = {0};
-  // frame slots: the ego frame, the frames whose object path is in flight (up to kObjLag + 1) and
-  // their last frames; 8 leaves room to spare
-  static constexpr int kSlots = 8;
-  static constexpr int kObjSlots = 4;  // object-pipeline buffers (frames in flight + 1)
-  static constexpr int kObjLag = 2;    // frames between enqueueing a frame's D3 and reading it
+  // frame slots: the ego frame, the frames whose object path is in flight (up to obj_lag_ + 1) and
+  // their last frames.  A frame's D3 reads its last frame's slot until the frame is finished,
+  // obj_lag_ + 1 frames later, after that iteration's ego path has written its own slot: the
+  // slot count must exceed obj_lag_ + 2.
+  static constexpr int kSlots = 12;
+  // object-pipeline buffers: at least the frames in flight (obj_lag_ + 1) plus one
+  static constexpr int kObjSlots = 8;
+  static constexpr int kObjLagMax = kObjSlots - 2;
+  // frames between enqueueing a frame's D3 and reading it (MMT_OBJ_LAG, 1..kObjLagMax)
+  int obj_lag_ = 4;
   FrameSlot slot_[kSlots];
   // ego in flight; its device->host results land in pinned memory so the copies stay
   // asynchronous while the host drives the previous frame's object path

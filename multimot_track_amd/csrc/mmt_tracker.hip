@@ -356,6 +356,11 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // inline, 905 with the overlap above, which needs no thread: off by default)
   // MMT_OBJ_OVERLAP (default 1): the previous frame's object path inside the first map chain of
   // the frame, while its kernels run (C3 895 -> 905 fps, tools/ab_interleave.py, 4 rounds)
+  // MMT_OBJ_LAG: frames between enqueueing a frame's object path and reading its results (default
+  // 4: the D3 chain's slow stretches no longer stall the host; interleaved A/B 905 / 915 / 920 fps
+  // at 2 / 3 / 4)
+  static_assert(kSlots > kObjLagMax + 2, "frame slots too few for the object lag");
+  if (const char* ol = getenv("MMT_OBJ_LAG")) obj_lag_ = std::max(1, std::min(kObjLagMax, atoi(ol)));
   const char* oo = getenv("MMT_OBJ_OVERLAP");
   overlap_obj_ = !(oo && atoi(oo) == 0);
   const char* ot = getenv("MMT_OBJ_THREAD");
@@ -436,7 +441,7 @@ void Tracker::obj_worker_main() {
     // finish in order: beyond the lag, what the main thread waits for, or everything when the
     // jobs are dropped
     while (!inflight_.empty() &&
-           ((int)inflight_.size() > kObjLag || inflight_.front().seq <= o_need_fin_ ||
+           ((int)inflight_.size() > obj_lag_ || inflight_.front().seq <= o_need_fin_ ||
             o_discard_ || o_err_kind_)) {
       ObjFrame G = inflight_.front();
       inflight_.pop_front();
@@ -659,7 +664,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
 
 // Enqueue the queued frame's whole object path (stage A's host decisions need one wait for the
 // grouping statistics; stage B is device-ordered), then read the results of frames older than
-// kObjLag.  Called while the next ego solve runs.
+// obj_lag_.  Called while the next ego solve runs.
 void Tracker::obj_advance() {
   obj_ran_ = true;
   auto now = [] {
@@ -676,7 +681,7 @@ void Tracker::obj_advance() {
     inflight_.push_back(qa_);
     qa_ = ObjFrame();
   }
-  while ((int)inflight_.size() > kObjLag) {
+  while ((int)inflight_.size() > obj_lag_) {
     obj_finish(inflight_.front());
     inflight_.pop_front();
   }
