@@ -1100,9 +1100,10 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
     D.stats[2] = status;
 #ifdef MMT_LM_PROFILE
     printf("lmprof N=%d T=%d iters=%d trials=%lld clean=%lld schur_pass=%lld schur_red=%lld "
-           "solve_ld=%lld solve_ldlt=%lld solve_exp=%lld upd_pass=%lld upd_red=%lld decide=%lld\n",
+           "solve_ld=%lld solve_ldlt=%lld solve_exp=%lld upd_pass=%lld upd_red=%lld decide=%lld "
+           "blk=%d stats=%p\n",
            N, nt, iters, sm.prof[6], sm.prof[7], sm.prof[4], sm.prof[0], sm.prof[8], sm.prof[9],
-           sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3]);
+           sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3], (int)blockIdx.x, (void*)D.stats);
 #endif
   }
 }
