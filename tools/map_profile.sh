@@ -10,6 +10,7 @@ MMT_MAP_PROFILE=1 timeout -k 10 300 python bench.py --steps 6 --warmup 1 --chunk
 grep "profile\]" gpurun_out/mapprof_$TAG.err
 cat gpurun_out/mapprof_$TAG.json
 fi
+[ -n "$SKIP_RP" ] && exit 0
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 6 --warmup 1 --chunk 64 --no-cpu > gpurun_out/mapprof_rp_$TAG.json 2> gpurun_out/mapprof_rp_$TAG.err
 cp "$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' -print -quit)" gpurun_out/kstats_$TAG.csv
 rm -rf gpurun_out/prof_$TAG
