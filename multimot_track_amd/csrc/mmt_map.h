@@ -140,6 +140,7 @@ class MapEngine {
 
  private:
   std::function<void()> overlap_;
+  std::vector<int> kf_count_, kf_touched_;  // update_local_keyframes' counter
   void run_overlap() {
     if (!overlap_) return;
     std::function<void()> fn = std::move(overlap_);

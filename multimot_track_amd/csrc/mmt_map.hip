@@ -734,27 +734,34 @@ bool MapEngine::track_reference_subst(MapFrameH& C, const GridFrame& G, float* T
 }
 
 void MapEngine::update_local_keyframes(MapFrameH& C) {  // Tracking::UpdateLocalKeyFrames
-  std::map<int, int> counter;
+  // keyframeCounter (a std::map keyed by KeyFrame*, here by keyframe id): counts in a flat array,
+  // then the touched ids in ascending order, as the map would iterate them
+  if (kf_count_.size() < kfs_.size()) kf_count_.resize(kfs_.size(), 0);
+  kf_touched_.clear();
   for (int i = 0; i < C.n; i++) {
     if (C.mps[i] < 0) continue;
     const MPoint& p = mp(C.mps[i]);
     if (!p.bad) {
-      for (const auto& kv : p.obs) counter[kv.first]++;
+      for (const auto& kv : p.obs)
+        if (kf_count_[kv.first]++ == 0) kf_touched_.push_back(kv.first);
     } else {
       C.mps[i] = -1;
     }
   }
-  if (counter.empty()) return;
+  if (kf_touched_.empty()) return;
+  std::sort(kf_touched_.begin(), kf_touched_.end());
   int mx = 0, kmax = -1;
   localKFs_.clear();
-  for (const auto& kv : counter) {
-    KFrame& K = kfs_[kv.first];
+  for (const int id : kf_touched_) {
+    const int cnt = kf_count_[id];
+    kf_count_[id] = 0;
+    KFrame& K = kfs_[id];
     if (K.bad) continue;
-    if (kv.second > mx) {
-      mx = kv.second;
-      kmax = kv.first;
+    if (cnt > mx) {
+      mx = cnt;
+      kmax = id;
     }
-    localKFs_.push_back(kv.first);
+    localKFs_.push_back(id);
     K.trackRef = curId_;
   }
   const size_t n0 = localKFs_.size();
