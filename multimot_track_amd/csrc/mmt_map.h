@@ -61,7 +61,7 @@ struct MPoint {
   bool bad = false;
   bool trackInView = false;
   bool dirty = false;  // pool record out of date
-  long trackRef = 0, lastSeen = 0;
+  long lastSeen = 0;  // real points: mirrored in MapEngine::hot_ (the per-frame scans read that)
   int obs_index(int kf) const {
     for (const auto& o : obs)
       if (o.first == kf) return o.second;
@@ -191,6 +191,15 @@ class MapEngine {
   MapCamH cam_;
   int kcap_ = 0;
   std::vector<MPoint> pts_, temps_;
+  // the fields the per-frame local-map scans read, one compact record per real point (pts_ index):
+  // UpdateLocalPoints walks ~13k point references and SearchLocalPoints ~4.4k, at random, and a
+  // 12-byte record keeps them in cache where the 136-byte MPoint does not
+  struct PtHot {
+    int trackRef = 0;  // mnTrackReferenceForFrame
+    int lastSeen = 0;  // mnLastFrameSeen
+    uint8_t bad = 0;
+  };
+  std::vector<PtHot> hot_;
   std::vector<KFrame> kfs_;
   int state_ = 0;
   long frameNextId_ = 0;

@@ -183,6 +183,7 @@ void MapEngine::grow_local(int m) {
 
 void MapEngine::reset() {
   pts_.clear();
+  hot_.clear();
   temps_.clear();
   kfs_.clear();
   state_ = 0;
@@ -226,6 +227,7 @@ int MapEngine::new_point_kf(const float* pos, int kf) {  // MapPoint(Pos, pRefKF
   p.firstKFid = kfs_[kf].id;
   p.refKF = kf;
   pts_.push_back(p);
+  hot_.push_back(PtHot());
   n_good_++;
   const int h = (int)pts_.size() - 1;
   mark_dirty(h);
@@ -247,6 +249,7 @@ void MapEngine::set_bad(int h) {  // MapPoint::SetBadFlag
   MPoint& p = mp(h);
   if (!p.bad && h < kTemp) n_good_--;
   p.bad = true;
+  if (h < kTemp) hot_[h].bad = 1;
   const std::vector<std::pair<int, int>> o = p.obs;
   p.obs.clear();
   for (const auto& kv : o) kfs_[kv.first].mps[kv.second] = -1;
@@ -688,11 +691,13 @@ int MapEngine::discard_outliers(MapFrameH& C, int nmatches, int* nmatchesMap) {
   for (int i = 0; i < C.n; i++) {
     if (C.mps[i] < 0) continue;
     if (C.outlier[i]) {
-      MPoint& p = mp(C.mps[i]);
+      const int h = C.mps[i];
+      MPoint& p = mp(h);
       C.mps[i] = -1;
       C.outlier[i] = 0;
       p.trackInView = false;
       p.lastSeen = curId_;
+      if (h < kTemp) hot_[h].lastSeen = (int)curId_;
       nmatches--;
     } else if (mp(C.mps[i]).nObs > 0) {
       (*nmatchesMap)++;
@@ -804,12 +809,13 @@ void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
   localPts_.clear();
   for (int kf : localKFs_)
     for (int h : kfs_[kf].mps) {
-      if (h < 0) continue;
-      MPoint& p = mp(h);
-      if (p.trackRef == curId_) continue;
-      if (!p.bad) {
+      // keyframes hold real points only (Track clears the VO points before a keyframe is made)
+      if (h < 0 || h >= kTemp) continue;
+      PtHot& q = hot_[h];
+      if (q.trackRef == (int)curId_) continue;
+      if (!q.bad) {
         localPts_.push_back(h);
-        p.trackRef = curId_;
+        q.trackRef = (int)curId_;
       }
     }
 }
@@ -819,12 +825,14 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
   // Tracking::SearchLocalPoints (Tracking.cc:3416-3466)
   for (int i = 0; i < C.n; i++) {
     if (C.mps[i] < 0) continue;
-    MPoint& p = mp(C.mps[i]);
+    const int h = C.mps[i];
+    MPoint& p = mp(h);
     if (p.bad) {
       C.mps[i] = -1;
     } else {
       p.visible++;
       p.lastSeen = curId_;
+      if (h < kTemp) hot_[h].lastSeen = (int)curId_;
       p.trackInView = false;
     }
   }
@@ -836,9 +844,10 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
   uint8_t* skip = h_sel_ + sl.skip;
   uint8_t* taken = h_sel_ + sl.taken;
   for (int j = 0; j < m; j++) {
-    const MPoint& p = mp(localPts_[j]);
-    ids[j] = localPts_[j];
-    skip[j] = (p.lastSeen == curId_) || p.bad;
+    const int h = localPts_[j];
+    const PtHot& q = hot_[h];
+    ids[j] = h;
+    skip[j] = q.lastSeen == (int)curId_ || q.bad;
   }
   // the keys bound before the search: taken (Observations() > 0) and, for D1's edge list, their
   // points' positions
