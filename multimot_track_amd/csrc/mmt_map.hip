@@ -445,6 +445,12 @@ void MapEngine::map_point_culling(int kf) {  // LocalMapping::MapPointCulling (R
 }
 
 // ------------------------------------------------------------------ GPU stages
+// MMT_MAP_EDGES_FUSED=0: D1's edge list by a k_map_edges launch of its own (A/B knob, read per
+// call); by default the matcher kernel builds it
+static bool edges_fused() {
+  const char* e = getenv("MMT_MAP_EDGES_FUSED");
+  return !(e && atoi(e) == 0);
+}
 // D1's descriptor for an edge list that k_map_edges builds on the device (it writes n): the edge
 // arrays at a fixed capacity of kcap edges
 void MapEngine::pose_desc_fill(uint8_t* h_blk, uint8_t* d_blk, const float* Tcw) {
@@ -535,14 +541,18 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
   LD.obs = LD.active + n1;
   LD.n = n1;
   memcpy(LD.Tcw, Tlast, 64);
-  launch_sbp_frame(G, Tcw, LD, th, 0, 1, c2_, d_match_, d_nm_, s_);
-  if (retry_th > 0)
-    launch_sbp_frame(G, Tcw, LD, retry_th, 0, 1, c2_, d_match_, d_nm_, s_, d_nm_, min_matches);
+  // D1's edges are built by the matcher kernels from their final bindings
   MapEdgeArgs e = edge_args(G);
   e.nm = d_nm_;
   e.min_matches = min_matches;
   e.src_X = LD.Xw;
-  launch_map_edges(e, s_);
+  const bool fused = edges_fused();
+  launch_sbp_frame(G, Tcw, LD, th, 0, 1, c2_, d_match_, d_nm_, s_, nullptr, 0,
+                   fused ? &e : nullptr);
+  if (retry_th > 0)
+    launch_sbp_frame(G, Tcw, LD, retry_th, 0, 1, c2_, d_match_, d_nm_, s_, d_nm_, min_matches,
+                     fused ? &e : nullptr);
+  if (!fused) launch_map_edges(e, s_);
   launch_pose_opt(d_pod_, 1, std::min(C.n, nact), s_);
   MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
   run_overlap();
@@ -871,15 +881,17 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
   // ORBmatcher(0.8)::SearchByProjection's th: 3 for RGB-D, 5 right after a relocalisation
   const float th = curId_ < lastRelocFrameId_ + 2 ? 5.f : 3.f;
   LocalSel sel{(const int*)(d_sel_ + sl.ids), d_sel_ + sl.skip, d_inview_};
-  launch_search_local(G, Tcw, d_pool_, d_pool_desc_, m, th, d_sel_ + sl.taken, nullptr, c3_,
-                      d_match_, d_nm_, s_, &sel);
-  // D1 over every key bound after the search (Tracking.cc:3189-3200), chained on the device
+  // D1 over every key bound after the search (Tracking.cc:3189-3200), chained on the device: the
+  // matcher kernel builds its edge list from the final bindings
   MapEdgeArgs e = edge_args(G);
   e.pool = d_pool_;
   e.ids = (const int*)(d_sel_ + sl.ids);
   e.has_base = d_sel_ + sl.bHas;
   e.base_X = (const float*)(d_sel_ + sl.bX);
-  launch_map_edges(e, s_);
+  const bool fused = edges_fused();
+  launch_search_local(G, Tcw, d_pool_, d_pool_desc_, m, th, d_sel_ + sl.taken, nullptr, c3_,
+                      d_match_, d_nm_, s_, &sel, fused ? &e : nullptr);
+  if (!fused) launch_map_edges(e, s_);
   launch_pose_opt(d_pod_, 1, std::min(C.n, nbase + m), s_);
   MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
   if (m > 0) MMT_HIP(hipMemcpyAsync(h_inview_, d_inview_, (size_t)m, hipMemcpyDeviceToHost, s_));

@@ -80,12 +80,15 @@ struct LastFrameDev {
   int n;
   float Tcw[16];
 };
+struct MapEdgeArgs;
 // run_if (optional): the call runs only while *run_if < run_lt (C2's retry at a wider window when
-// the first search found too few matches), decided on the device.
+// the first search found too few matches), decided on the device.  edges (optional): the matcher
+// kernel also builds D1's edge list from its final bindings (k_map_edges' work, no launch of its
+// own); a call that does not run leaves the previous call's list.
 void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& L, float th,
                       int mono, int check_orientation, const CandSet& cs, int* match,
                       int* nmatches, hipStream_t st, const int* run_if = nullptr,
-                      int run_lt = 0);
+                      int run_lt = 0, const MapEdgeArgs* edges = nullptr);
 
 // C3: SearchLocalPoints' isInFrustum pass + SearchByProjection(Frame&, vector<MapPoint*>, th).
 // ids (null: point j is pts[j]) selects the local points from a resident pool, skip (null: the
@@ -99,7 +102,8 @@ struct LocalSel {
 void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointDev* pts,
                          const uint8_t* pdesc, int m, float th, const uint8_t* taken,
                          FrustumRec* fr, const CandSet& cs, int* match, int* nmatches,
-                         hipStream_t st, const LocalSel* sel = nullptr);
+                         hipStream_t st, const LocalSel* sel = nullptr,
+                         const MapEdgeArgs* edges = nullptr);
 
 // C4: ORBmatcher::SearchByBoW(KeyFrame*, Frame&) with caller-supplied DBoW2 FeatureVectors
 // (node ids ascending, per-node feature lists in insertion order, every feature in one node).

@@ -475,6 +475,8 @@ struct GreedyArgs {
   int* nmatches;
   const int* run_if;         // optional: run only while *run_if < run_lt
   int run_lt;
+  int build_edges;           // D1's edge list from the final bindings (map_edges_body), in-kernel
+  MapEdgeArgs edges;
 };
 
 // the decision of one point from its best / second-best unbound candidates
@@ -549,6 +551,46 @@ struct OwnerTaken {
 // order (0xFFFFFFFF past its count) and its index (bit 31: more candidates than cached, so it
 // may need a rescan).  Rounds then read LDS only.
 constexpr uint32_t kPackNone = 0xFFFFFFFFu;
+
+// D1's edge list in key order (k_map_edges; also the tail of k_match_fix): a key with a new match
+// takes its point's position, a key bound before the search its held position; nothing is built
+// below min_matches (build false).  One 1024-thread workgroup; writes desc->n.
+__device__ __forceinline__ void map_edges_body(const MapEdgeArgs& a, bool build, int* s_w) {
+  const int t = threadIdx.x;
+  int base = 0;
+  for (int k0 = 0; k0 < (build ? a.n : 0); k0 += 1024) {
+    const int i = k0 + t;
+    int src = -1;  // 0: a new match, 1: a binding held before the search
+    if (i < a.n) {
+      if (a.match[i] >= 0)
+        src = 0;
+      else if (a.has_base && a.has_base[i])
+        src = 1;
+    }
+    int excl = 0;
+    const int tot = grid_block_scan_excl(src >= 0 ? 1 : 0, s_w, excl);
+    if (src >= 0) {
+      const int e = base + excl;
+      const float* X;
+      if (src == 1)
+        X = a.base_X + 3 * (size_t)i;
+      else if (a.pool)
+        X = a.pool[a.ids[a.match[i]]].Xw;
+      else
+        X = a.src_X + 3 * (size_t)a.match[i];
+      a.X[3 * e] = X[0];
+      a.X[3 * e + 1] = X[1];
+      a.X[3 * e + 2] = X[2];
+      const mmt_kp kp = a.keys[i];
+      a.obs[3 * e] = kp.x;
+      a.obs[3 * e + 1] = kp.y;
+      a.obs[3 * e + 2] = a.uR[i];
+      a.s2[e] = a.inv_sigma2[kp.octave];
+    }
+    base += tot;
+  }
+  if (t == 0) a.desc->n = base;
+}
 
 __device__ __forceinline__ int fix_decide_packed(const GreedyArgs& a, int i, bool big,
                                                  const uint32_t* pc, const int* owner,
@@ -773,6 +815,11 @@ __global__ __launch_bounds__(kFixThreads) void k_match_fix(GreedyArgs a, int cac
       if (s_owner[k]) a.match[k] = -1;
   }
   if (tid == 0) *a.nmatches = s_nm - s_removed;
+  if (a.build_edges) {
+    __shared__ int s_we[16];
+    __syncthreads();  // the final bindings (a.match) and the count
+    map_edges_body(a.edges, s_nm - s_removed >= a.edges.min_matches, s_we);
+  }
 #ifdef MMT_MATCH_PROFILE
   if (tid == 0)
     printf("[match profile] mode %d npts %d keys %d rounds %d rescans %d cycles %lld\n", a.mode,
@@ -802,7 +849,8 @@ static void launch_match_fix(const GreedyArgs& g, hipStream_t st) {
 
 void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& L, float th,
                       int mono, int check_orientation, const CandSet& cs, int* match,
-                      int* nmatches, hipStream_t st, const int* run_if, int run_lt) {
+                      int* nmatches, hipStream_t st, const int* run_if, int run_lt,
+                      const MapEdgeArgs* edges) {
   if (C.n > kMaxMatchKeys) throw ArgError("SearchByProjection: more than 16384 current keys");
   if (check_orientation && L.n > kMaxMatchKeys)
     throw ArgError("SearchByProjection: more than 16384 last-frame keys");
@@ -834,13 +882,15 @@ void launch_sbp_frame(const GridFrame& C, const float* Tcw, const LastFrameDev& 
   g.nmatches = nmatches;
   g.run_if = run_if;
   g.run_lt = run_lt;
+  g.build_edges = edges != nullptr;
+  if (edges) g.edges = *edges;
   launch_match_fix(g, st);
 }
 
 void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointDev* pts,
                          const uint8_t* pdesc, int m, float th, const uint8_t* taken,
                          FrustumRec* fr, const CandSet& cs, int* match, int* nmatches,
-                         hipStream_t st, const LocalSel* sel) {
+                         hipStream_t st, const LocalSel* sel, const MapEdgeArgs* edges) {
   if (C.n > kMaxMatchKeys) throw ArgError("SearchByProjection: more than 16384 current keys");
   LocalArgs a;
   a.C = C;
@@ -871,6 +921,8 @@ void launch_search_local(const GridFrame& C, const float* Tcw, const LocalPointD
   g.nmatches = nmatches;
   g.run_if = nullptr;
   g.run_lt = 0;
+  g.build_edges = edges != nullptr;
+  if (edges) g.edges = *edges;
   launch_match_fix(g, st);
 }
 
@@ -1041,41 +1093,7 @@ void launch_search_by_bow(const BowFeatVec& kf, const mmt_kp* kf_keys, const uin
 // One 1024-thread workgroup: order-preserving compaction of the bound keys, 1024 keys per step.
 __global__ __launch_bounds__(1024) void k_map_edges(MapEdgeArgs a) {
   __shared__ int s_w[16];
-  const int t = threadIdx.x;
-  const bool build = !a.nm || *a.nm >= a.min_matches;
-  int base = 0;
-  for (int k0 = 0; k0 < (build ? a.n : 0); k0 += 1024) {
-    const int i = k0 + t;
-    int src = -1;  // 0: a new match, 1: a binding held before the search
-    if (i < a.n) {
-      if (a.match[i] >= 0)
-        src = 0;
-      else if (a.has_base && a.has_base[i])
-        src = 1;
-    }
-    int excl = 0;
-    const int tot = grid_block_scan_excl(src >= 0 ? 1 : 0, s_w, excl);
-    if (src >= 0) {
-      const int e = base + excl;
-      const float* X;
-      if (src == 1)
-        X = a.base_X + 3 * (size_t)i;
-      else if (a.pool)
-        X = a.pool[a.ids[a.match[i]]].Xw;
-      else
-        X = a.src_X + 3 * (size_t)a.match[i];
-      a.X[3 * e] = X[0];
-      a.X[3 * e + 1] = X[1];
-      a.X[3 * e + 2] = X[2];
-      const mmt_kp kp = a.keys[i];
-      a.obs[3 * e] = kp.x;
-      a.obs[3 * e + 1] = kp.y;
-      a.obs[3 * e + 2] = a.uR[i];
-      a.s2[e] = a.inv_sigma2[kp.octave];
-    }
-    base += tot;
-  }
-  if (t == 0) a.desc->n = base;
+  map_edges_body(a, !a.nm || *a.nm >= a.min_matches, s_w);
 }
 
 void launch_map_edges(const MapEdgeArgs& a, hipStream_t st) {
