@@ -452,6 +452,83 @@ __device__ __forceinline__ double dpp_add(double v) {
   return v + __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
+// ---- register reduce-scatter of 64 doubles per lane (gfx950 v_permlane32/16_swap + DPP): after
+// six halving steps every lane holds the wave's sum of one value index, a permutation of 0..63
+// that wave_rs_index() reads off once.  No LDS; the sums never leave registers.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const unsigned long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// x, y swapped across the lane halves of 32 (W = 32) or of 16 within each 32 (W = 16), then added:
+// one half of the lanes holds x's pair sums, the other y's
+template <int W>
+__device__ __forceinline__ double swap_add(double x, double y) {
+  const unsigned long long bx = __double_as_longlong(x), by = __double_as_longlong(y);
+  unsigned xl, yl, xh, yh;
+  if (W == 32) {
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)bx, (unsigned)by, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(bx >> 32), (unsigned)(by >> 32),
+                                                     false, false);
+    xl = lo[0]; yl = lo[1]; xh = hi[0]; yh = hi[1];
+  } else {
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)bx, (unsigned)by, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(bx >> 32), (unsigned)(by >> 32),
+                                                     false, false);
+    xl = lo[0]; yl = lo[1]; xh = hi[0]; yh = hi[1];
+  }
+  return __longlong_as_double(((unsigned long long)xh << 32) | xl) +
+         __longlong_as_double(((unsigned long long)yh << 32) | yl);
+}
+
+// a lane with BIT clear keeps x and sends y to its DPP partner (CTRL pairs it with a lane that
+// has BIT set), which keeps y
+template <int CTRL, int BIT>
+__device__ __forceinline__ double pair_add(double x, double y, int lane) {
+  const bool up = lane & BIT;
+  return (up ? y : x) + dpp_mov<CTRL>(up ? x : y);
+}
+
+__device__ __forceinline__ double wave_reduce_scatter64(double (&v)[64]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 32; k++) v[k] = swap_add<32>(v[k], v[k + 32]);
+#pragma unroll
+  for (int k = 0; k < 16; k++) v[k] = swap_add<16>(v[k], v[k + 16]);
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = pair_add<0x128, 8>(v[k], v[k + 8], lane);  // row_ror:8
+#pragma unroll
+  for (int k = 0; k < 4; k++) v[k] = pair_add<0x141, 4>(v[k], v[k + 4], lane);  // row_half_mirror
+#pragma unroll
+  for (int k = 0; k < 2; k++) v[k] = pair_add<0x4E, 2>(v[k], v[k + 2], lane);   // quad [2,3,0,1]
+  return pair_add<0xB1, 1>(v[0], v[1], lane);                                   // quad [1,0,3,2]
+}
+
+// the value index this lane ends with in wave_reduce_scatter64 (one-hot probe: lane 0 holds
+// k + 1 at index k, every other lane zeros)
+__device__ __forceinline__ int wave_rs_index() {
+  const int lane = threadIdx.x & 63;
+  double v[64];
+#pragma unroll
+  for (int k = 0; k < 64; k++) v[k] = lane == 0 ? (double)(k + 1) : 0.0;
+  return (int)wave_reduce_scatter64(v) - 1;
+}
+
+// Workgroup sums of 64 doubles per thread held in registers (v[63] a pad), returned as
+// block_sum_tile_lanes returns them: sum k in lane k, the same in every wave.  idx =
+// wave_rs_index(); `part` holds 64 * nw doubles; one barrier.
+__device__ inline double block_sum_regs64(double (&v)[64], double* part, int nw, int idx) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  part[wave * 64 + idx] = wave_reduce_scatter64(v);
+  __syncthreads();
+  double t = 0;
+  for (int w = 0; w < nw; w++) t += part[w * 64 + lane];
+  return t;
+}
+
 // wave sum of a double, wave-uniform result: quad swaps (xor 1, xor 2), half-row and row mirrors
 // give every lane its 16-lane row sum, then the four row sums are added from lanes 0/16/32/48 in
 // a fixed order.  Inactive lanes must hold 0.

@@ -540,7 +540,7 @@ struct LMSmem {
   long long prof[12];
   double red[16 * 32];
   double tile[4 * 64 * kTileStride];  // block_sum_rows / block_sum_t tiles (blockDim <= 256)
-  double part[2][4 * kSums];  // double-buffered: waves read one while a fast wave fills the other
+  double part[2][4 * 64];  // double-buffered: waves read one while a fast wave fills the other
   double S27[32];
   double mh[16];
   double cand[4 * 4 * 16];  // per wave: 4 candidate solves (ok, x[6], pose[7])
@@ -679,6 +679,12 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   // second pass and exchange.  The ego solve accepts nearly every trial (22 of 24), so the
   // speculative linearisation is almost never wasted.
   const bool spec = SPLIT && spec_ok && (gx.ntot + gx.G - 1) / gx.G <= 2 * 256;
+  // the one-workgroup solves (D3) reduce the accepted trial's 63 sums in registers
+  // (the one-edge path: with two register edges the kernel would spill); max_cand bit 8 turns it
+  // on (MMT_LM_REGSUM, A/B knob)
+  const bool kRegSums = !SPLIT && IR == 1 && (max_cand & 256);
+  max_cand &= 255;
+  const int rs_idx = kRegSums ? wave_rs_index() : 0;
   Cam c;
   c.fx = D.fx;
   c.fy = D.fy;
@@ -1030,6 +1036,35 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
 #pragma unroll
           for (int a = 0; a < 12; a++) RB[a] = RBn[a];
         vc = vn;
+      } else if (IR == 1 && !SPLIT && accept && kRegSums) {
+        // ---- pass 2 with its sums in registers: the thread's edges accumulate into vals, and a
+        // register reduce-scatter (block_sum_regs64) replaces the LDS tile
+        double vals[64];
+#pragma unroll
+        for (int k = 0; k < IR; k++)
+          if (tid + k * nt < N) {
+            if (k == 0)
+              accept_terms<true>(c, P, R[k], vals, kCacheB ? RB : nullptr);
+            else
+              accept_terms<false>(c, P, R[k], vals);
+          }
+        {
+          int i = n_reg + tid;
+          LMItem it, nx;
+          if (i < N) item_load(G, cap, lo + i, it);
+          for (; i < N; i += nt) {
+            if (i + nt < N) item_load(G, cap, lo + i + nt, nx);
+            accept_terms<false>(c, P, it, vals);
+            item_store_accept(G, cap, lo + i, it);
+            it = nx;
+          }
+        }
+        if (tid >= N)
+#pragma unroll
+          for (int q = 0; q < 64; q++) vals[q] = 0;
+        vals[63] = 0;
+        vc = block_sum_regs64(vals, sm.part[pb], nw, rs_idx);
+        pb ^= 1;
       } else if (accept) {
         // ---- pass 2: take the flow step and linearise at the accepted state (the system of the
         // next trial); rejected trials skip it, so they cost the errors and two sums only
@@ -1054,6 +1089,13 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         }
         if (tid >= N)
           for (int q = 0; q < kSums; q++) row[q] = 0;
+#ifdef MMT_LM_PROFILE
+        if (tid == 0) {  // pass 2's edge work, apart from its reduction (decide keeps the rest)
+          const long long now = clock64();
+          sm.prof[10] += now - prof_t;
+          prof_t = now;
+        }
+#endif
         vc = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
         pb ^= 1;
         if (SPLIT) vc = gx_sum(gx, vc, kSums);
@@ -1101,9 +1143,10 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
 #ifdef MMT_LM_PROFILE
     printf("lmprof N=%d T=%d iters=%d trials=%lld clean=%lld schur_pass=%lld schur_red=%lld "
            "solve_ld=%lld solve_ldlt=%lld solve_exp=%lld upd_pass=%lld upd_red=%lld decide=%lld "
-           "blk=%d stats=%p\n",
+           "blk=%d stats=%p pass2=%lld\n",
            N, nt, iters, sm.prof[6], sm.prof[7], sm.prof[4], sm.prof[0], sm.prof[8], sm.prof[9],
-           sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3], (int)blockIdx.x, (void*)D.stats);
+           sm.prof[1], sm.prof[5], sm.prof[2], sm.prof[3], (int)blockIdx.x, (void*)D.stats,
+           sm.prof[10]);
 #endif
   }
 }
@@ -1188,6 +1231,9 @@ void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipSt
   // MMT_LM_MAX_CAND=1..4 (read per launch; tests compare 1 against the default 4 bit for bit)
   int max_cand = 4;
   if (const char* e = getenv("MMT_LM_MAX_CAND")) max_cand = std::min(4, std::max(1, atoi(e)));
+  // MMT_LM_REGSUM=0: the accepted trial's sums through the LDS tile (A/B knob, read per launch)
+  const char* rs = getenv("MMT_LM_REGSUM");
+  if (!(rs && atoi(rs) == 0)) max_cand |= 256;
   hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs, max_cand);
 }
 

@@ -191,6 +191,7 @@ class Tracker {
   static constexpr int kObjLagMax = kObjSlots - 2;
   // frames between enqueueing a frame's D3 and reading it (MMT_OBJ_LAG, 1..kObjLagMax)
   int obj_lag_ = 4;
+  int d3_iters_ = 200;  // PoseOptimizationFlow2's optimize(200) (Optimizer.cc:2292)
   FrameSlot slot_[kSlots];
   // ego in flight; its device->host results land in pinned memory so the copies stay
   // asynchronous while the host drives the previous frame's object path

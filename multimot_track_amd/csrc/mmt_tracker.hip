@@ -361,6 +361,9 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // at 2 / 3 / 4)
   static_assert(kSlots > kObjLagMax + 2, "frame slots too few for the object lag");
   if (const char* ol = getenv("MMT_OBJ_LAG")) obj_lag_ = std::max(1, std::min(kObjLagMax, atoi(ol)));
+  // MMT_DEBUG_D3_ITERS: caps D3's LM iterations (the reference's 200), for bottleneck analysis
+  // only: it changes the object results
+  if (const char* di = getenv("MMT_DEBUG_D3_ITERS")) d3_iters_ = std::max(1, atoi(di));
   const char* oo = getenv("MMT_OBJ_OVERLAP");
   overlap_obj_ = !(oo && atoi(oo) == 0);
   const char* ot = getenv("MMT_OBJ_THREAD");
@@ -1055,7 +1058,7 @@ void Tracker::obj_stage_b(ObjFrame& F) {
     memcpy(d.Tcw_last, Ls.Tview, sizeof(d.Tcw_last));
     d.rp_thres = 0.01f;
     d.use_noise = 0;
-    d.max_iters = 200;
+    d.max_iters = d3_iters_;
     d.prior_info = 0.5;
     d.fx = cfg_.fx; d.fy = cfg_.fy; d.cx = cfg_.cx; d.cy = cfg_.cy;
     d.scratch = d_lm_scratch_ + flow_scratch_doubles(lm_cap_) * (1 + i);
