@@ -683,8 +683,9 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   // (the one-edge path: with two register edges the kernel would spill); max_cand bit 8 turns it
   // on (MMT_LM_REGSUM, A/B knob)
   const bool kRegSums = !SPLIT && IR == 1 && (max_cand & 256);
+  const bool kSpecRegSums = SPLIT && IR == 1 && (max_cand & 256);  // the split solve's fused pass
   max_cand &= 255;
-  const int rs_idx = kRegSums ? wave_rs_index() : 0;
+  const int rs_idx = (kRegSums || kSpecRegSums) ? wave_rs_index() : 0;
   Cam c;
   c.fx = D.fx;
   c.fy = D.fy;
@@ -930,7 +931,23 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
       double vn = 0;                        // the trial's sums; the next system if accepted
       double pw[IR], pb0[IR], pb1[IR];      // pending w, bl of the register items
       double RBn[12];                       // pending w J of register item 0
-      if (spec) {
+      if (IR == 1 && spec && kSpecRegSums) {
+        // the fused pass with its sums in registers (as D3's pass 2)
+        double vals[64];
+        if (tid < N)
+          spec_terms<true>(c, P, PN, R[0], lo + tid, ok2, lam, ilam, xb, vals, pw[0], pb0[0],
+                           pb1[0], kCacheB ? RB : nullptr, RBn);
+        else
+#pragma unroll
+          for (int q = 0; q < 64; q++) vals[q] = 0;
+        vals[63] = 0;
+        MMT_LMPROF(5);
+        vn = block_sum_regs64(vals, sm.part[pb], nw, rs_idx);
+        pb ^= 1;
+        vn = gx_sum(gx, vn, kSums);
+        lastTrialChi = lane_value(vn, 0);
+        scale = lane_value(vn, 1);
+      } else if (spec) {
 #pragma unroll
         for (int k = 0; k < IR; k++) {
           const int i = tid + k * nt;
@@ -1254,6 +1271,8 @@ void launch_flow_lm_split(const FlowSolveDesc* d_desc, int groups, hipStream_t s
   groups = std::max(1, std::min(groups, kFlowSplitMax));
   const char* e = getenv("MMT_LM_SPEC");  // 0: two passes and two exchanges per trial
   const int spec = !(e && atoi(e) == 0);
+  const char* rs = getenv("MMT_LM_REGSUM");  // 0: the fused pass's sums through the LDS tile
+  if (!(rs && atoi(rs) == 0)) max_cand |= 256;
   hipLaunchKernelGGL(k_flow_lm_split, dim3(groups), dim3(256), 0, st, d_desc, max_cand, spec);
 }
 
