@@ -185,12 +185,12 @@ class Tracker {
   // their last frames.  A frame's D3 reads its last frame's slot until the frame is finished,
   // obj_lag_ + 1 frames later, after that iteration's ego path has written its own slot: the
   // slot count must exceed obj_lag_ + 2.
-  static constexpr int kSlots = 12;
+  static constexpr int kSlots = 22;
   // object-pipeline buffers: at least the frames in flight (obj_lag_ + 1) plus one
-  static constexpr int kObjSlots = 8;
+  static constexpr int kObjSlots = 18;
   static constexpr int kObjLagMax = kObjSlots - 2;
   // frames between enqueueing a frame's D3 and reading it (MMT_OBJ_LAG, 1..kObjLagMax)
-  int obj_lag_ = 4;
+  int obj_lag_ = 16;
   int d3_iters_ = 200;  // PoseOptimizationFlow2's optimize(200) (Optimizer.cc:2292)
   FrameSlot slot_[kSlots];
   // ego in flight; its device->host results land in pinned memory so the copies stay

@@ -357,8 +357,9 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // MMT_OBJ_OVERLAP (default 1): the previous frame's object path inside the first map chain of
   // the frame, while its kernels run (C3 895 -> 905 fps, tools/ab_interleave.py, 4 rounds)
   // MMT_OBJ_LAG: frames between enqueueing a frame's object path and reading its results (default
-  // 4: the D3 chain's slow stretches no longer stall the host; interleaved A/B 905 / 915 / 920 fps
-  // at 2 / 3 / 4)
+  // 16: the D3 chain's slow stretches no longer stall the host; interleaved A/B 905 / 915 / 920 fps
+  // at 2 / 3 / 4, then 932 / 937 / 944 / 950 / 956 / 964 at 4 / 6 / 8 / 10 / 14 / 18, flat from
+  // there to 32)
   static_assert(kSlots > kObjLagMax + 2, "frame slots too few for the object lag");
   if (const char* ol = getenv("MMT_OBJ_LAG")) obj_lag_ = std::max(1, std::min(kObjLagMax, atoi(ol)));
   // MMT_DEBUG_D3_ITERS: caps D3's LM iterations (the reference's 200), for bottleneck analysis
