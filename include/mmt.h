@@ -34,6 +34,12 @@
  *   mmt_search_by_bow   <- ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&, ...)
  *                          ORBmatcher.cc:532-663 (TrackReferenceKeyFrame Tracking.cc:2841-2853,
  *                          Relocalization :3631-3651)
+ *   mmt_fuse_candidates <- ORBmatcher::Fuse(KeyFrame*, const vector<MapPoint*>&, th)'s search,
+ *                          ORBmatcher.cc:1200-1324 (LocalMapping::SearchInNeighbors
+ *                          LocalMapping.cc:458-538)
+ *   mmt_local_bundle_adjustment
+ *                       <- Optimizer::LocalBundleAdjustment's two optimisation rounds and inlier
+ *                          test, Optimizer.cc:3394-3631 (LocalMapping.cc:81-84)
  *   mmt_destroy         <- System::Shutdown / delete
  */
 #ifndef MMT_H
@@ -374,6 +380,53 @@ typedef struct mmt_bow_keyframe {
 int mmt_search_by_bow(mmt_ctx* ctx, const mmt_bow_keyframe* kf, int n_cur, const mmt_kp* cur_kps,
                       const uint8_t* cur_desc, const mmt_feature_vector* cur_fv, float nn_ratio,
                       int check_orientation, int32_t* match_out, int* nmatches);
+
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th)'s per-point search (ORBmatcher.cc:1200-1324): the point
+ * projected with the keyframe's pose (cur->Tcw), KeyFrame::IsInImage, the scale-invariance
+ * distances (0.8 mfMinDistance, 1.2 mfMaxDistance), the 60-degree viewing angle, PredictScale, then
+ * the keyframe keys in radius th * scale[level] at the predicted level or one below, gated by the
+ * reprojection error (7.8 stereo, 5.99 monocular, times 1/sigma^2), and the closest descriptor
+ * (first of equal distances).  best_idx / best_dist (m) = that key and its distance, or -1 / 256;
+ * the reference fuses when best_dist <= 50.  The keyframe is a mmt_match_frame (its depth map
+ * gives mvuRight); pts->skip is ignored (the caller skips bad points and points already in the
+ * keyframe, ORBmatcher.cc:1224). */
+int mmt_fuse_candidates(mmt_ctx* ctx, const mmt_match_frame* kf, const mmt_local_points* pts,
+                        float th, int32_t* best_idx, int32_t* best_dist);
+
+/* The graph of Optimizer::LocalBundleAdjustment (Optimizer.cc:3408-3541): keyframe vertices
+ * (Tcw, fixed: the fixed cameras and keyframe 0), map points, and one edge per observation, listed
+ * point by point (e_pt non-decreasing) with each point's observations in keyframe order. */
+typedef struct mmt_ba_problem {
+  int n_kf, n_pt, n_edge;
+  const float* Tcw;            /* n_kf x 16 row-major                                  */
+  const uint8_t* fixed;        /* n_kf                                                 */
+  const float* Xw;             /* n_pt x 3                                             */
+  const int32_t* e_pt;         /* n_edge                                               */
+  const int32_t* e_kf;         /* n_edge                                               */
+  const float* e_obs;          /* n_edge x (u, v, uR): keypoint and mvuRight (< 0: monocular,
+                                  EdgeSE3ProjectXYZ; else EdgeStereoSE3ProjectXYZ)     */
+  const float* e_inv_sigma2;   /* n_edge: mvInvLevelSigma2[octave] (the information)   */
+} mmt_ba_problem;
+
+/* LocalBundleAdjustment's solve (Optimizer.cc:3547-3631; g2o LM with BlockSolver_6_3, Huber
+ * sqrt(5.991) / sqrt(7.815) in the first 5 iterations, the bad edges set aside, 10 more without the
+ * kernel) on the GPU.  Tcw_out (n_kf x 16) and Xw_out (n_pt x 3) = Converter::toCvMat of the final
+ * estimates; erase_out (n_edge) = the final inlier test failed (the observation the reference
+ * erases); stats (5) = iterations of round 1, of round 2, LM trials of round 1, of round 2, erased
+ * edges.  Camera from the context's configuration. */
+int mmt_local_bundle_adjustment(mmt_ctx* ctx, const mmt_ba_problem* problem, float* Tcw_out,
+                                float* Xw_out, uint8_t* erase_out, int32_t* stats);
+
+/* LocalMapping counters of the context's tracker (no reference counterpart: test and profiling
+ * hook).  Times are host wall microseconds, collected with MMT_MAP_PROFILE=1. */
+typedef struct mmt_map_counters {
+  int64_t n_ba, n_fused, n_culled, n_ba_erased, ba_trials, ba_edges, ba_kfs, ba_pts, ba_max_opt,
+      fuse_launches, fuse_queries, fuse_relaunches;
+  double lm_us, ba_us, fuse_us;
+  int64_t d2_split_fallbacks;  /* ego flow solves re-run on one workgroup because the split
+                                  solve's workgroups were not resident together             */
+} mmt_map_counters;
+int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out);
 
 /* Stage timing with HIP events on the launch stream (no reference counterpart: measurement
  * hook for bench.py).  orb_ms sums the batched ORB launch sequences of the tracked chunks. */

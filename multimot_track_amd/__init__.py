@@ -99,6 +99,21 @@ class MmtPnPsolverState(ctypes.Structure):
                 ("best_Tcw", ctypes.c_float * 16), ("best_mask", ctypes.c_void_p)]
 
 
+class MmtBAProblem(ctypes.Structure):
+    _fields_ = [("n_kf", ctypes.c_int), ("n_pt", ctypes.c_int), ("n_edge", ctypes.c_int),
+                ("Tcw", ctypes.c_void_p), ("fixed", ctypes.c_void_p), ("Xw", ctypes.c_void_p),
+                ("e_pt", ctypes.c_void_p), ("e_kf", ctypes.c_void_p), ("e_obs", ctypes.c_void_p),
+                ("e_inv_sigma2", ctypes.c_void_p)]
+
+
+class MmtMapCounters(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in (
+        "n_ba", "n_fused", "n_culled", "n_ba_erased", "ba_trials", "ba_edges", "ba_kfs",
+        "ba_pts", "ba_max_opt", "fuse_launches", "fuse_queries", "fuse_relaunches")] + \
+        [(k, ctypes.c_double) for k in ("lm_us", "ba_us", "fuse_us")] + \
+        [("d2_split_fallbacks", ctypes.c_int64)]
+
+
 class MmtProfile(ctypes.Structure):
     _fields_ = [("orb_ms", ctypes.c_double), ("orb_launches", ctypes.c_int64),
                 ("orb_frames", ctypes.c_int64)]
@@ -482,6 +497,56 @@ class Context:
             self._h, ctypes.byref(fr), ctypes.byref(P), th,
             tk.ctypes.data if tk is not None else None, _p(match), _p(frus), ctypes.byref(nm)))
         return nm.value, match[:fr.n], frus[:P.m]
+
+    def fuse_candidates(self, kps, desc, depth, tcw, Xw, normal, min_dist, max_dist, pdesc,
+                        th=3.0):
+        """ORBmatcher::Fuse(pKF, vpMapPoints, th)'s per-point search against the keyframe (kps,
+        desc, depth, tcw): (best key index, best distance) per point, -1 / 256 for none."""
+        keep = []
+        fr = self._match_frame(kps, desc, depth, tcw, keep)
+        arrs = [np.ascontiguousarray(a, np.float32) for a in (Xw, normal, min_dist, max_dist)]
+        pd = np.ascontiguousarray(pdesc, np.uint8)
+        m = len(arrs[2])
+        sk = np.zeros(max(m, 1), np.uint8)
+        P = MmtLocalPoints()
+        P.m = m
+        P.Xw, P.normal, P.min_dist, P.max_dist = [a.ctypes.data for a in arrs]
+        P.desc, P.skip = pd.ctypes.data, sk.ctypes.data
+        idx = np.zeros(max(m, 1), np.int32)
+        dist = np.zeros(max(m, 1), np.int32)
+        self._check(lib().mmt_fuse_candidates(self._h, ctypes.byref(fr), ctypes.byref(P),
+                                              ctypes.c_float(th), _p(idx), _p(dist)))
+        return idx[:m], dist[:m]
+
+    def local_bundle_adjustment(self, P):
+        """Optimizer::LocalBundleAdjustment's solve on a problem dict (keys T, fixed, X, pt, kf,
+        obs, s, as oracle.Tracker.captured_ba): (T (n_kf, 4, 4), X (n_pt, 3), erase (n_edge,),
+        stats dict) like oracle.local_ba."""
+        T = np.ascontiguousarray(P["T"], np.float32)
+        fx = np.ascontiguousarray(P["fixed"], np.uint8)
+        X = np.ascontiguousarray(P["X"], np.float32)
+        ept = np.ascontiguousarray(P["pt"], np.int32)
+        ekf = np.ascontiguousarray(P["kf"], np.int32)
+        eo = np.ascontiguousarray(P["obs"], np.float32)
+        es = np.ascontiguousarray(P["s"], np.float32)
+        nk, npt, ne = len(fx), len(X), len(ept)
+        B = MmtBAProblem(nk, npt, ne, T.ctypes.data, fx.ctypes.data, X.ctypes.data,
+                         ept.ctypes.data, ekf.ctypes.data, eo.ctypes.data, es.ctypes.data)
+        To = np.zeros((max(nk, 1), 4, 4), np.float32)
+        Xo = np.zeros((max(npt, 1), 3), np.float32)
+        er = np.zeros(max(ne, 1), np.uint8)
+        st = np.zeros(5, np.int32)
+        self._check(lib().mmt_local_bundle_adjustment(self._h, ctypes.byref(B), _p(To), _p(Xo),
+                                                      _p(er), _p(st)))
+        return To[:nk], Xo[:npt], er[:ne], dict(iterations=(int(st[0]), int(st[1])),
+                                                 trials=(int(st[2]), int(st[3])),
+                                                 n_erase=int(st[4]))
+
+    def map_counters(self):
+        """LocalMapping counters of the context's tracker (mmt_map_counters_read)."""
+        c = MmtMapCounters()
+        self._check(lib().mmt_map_counters_read(self._h, ctypes.byref(c)))
+        return {k: getattr(c, k) for k, _ in MmtMapCounters._fields_}
 
     def pnp_ransac(self, pts3, pts2, K, max_iters=500, reproj=0.3, conf=0.98):
         pts3 = np.ascontiguousarray(pts3, np.float32)

@@ -667,6 +667,142 @@ static void check_feature_vector(const mmt_feature_vector* v, int n, std::vector
   }
 }
 
+int mmt_fuse_candidates(mmt_ctx* ctx, const mmt_match_frame* kf, const mmt_local_points* pts,
+                        float th, int32_t* best_idx, int32_t* best_dist) {
+  if (!ctx || !kf || !pts || pts->m < 0 || (pts->m > 0 && (!best_idx || !best_dist || !pts->Xw ||
+                                                           !pts->normal || !pts->min_dist ||
+                                                           !pts->max_dist || !pts->desc)))
+    return MMT_EINVAL;
+  return guard(ctx, [&] {
+    check_match_frame(ctx, kf, true);
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    hipStream_t s = ctx->stream;
+    DevMatchFrame F(ctx, kf, true);
+    const int m = pts->m;
+    std::vector<mmt::LocalPointDev> hp(std::max(m, 1));
+    std::vector<mmt::FuseQuery> hq(std::max(m, 1));
+    for (int j = 0; j < m; j++) {
+      mmt::LocalPointDev& p = hp[j];
+      memset(&p, 0, sizeof(p));
+      memcpy(p.Xw, pts->Xw + 3 * (size_t)j, 12);
+      memcpy(p.normal, pts->normal + 3 * (size_t)j, 12);
+      p.min_dist = pts->min_dist[j];
+      p.max_dist = pts->max_dist[j];
+      hq[j] = mmt::FuseQuery{0, j};
+    }
+    mmt::FuseKF K;
+    memset(&K, 0, sizeof(K));
+    K.keys = F.G.keys;
+    K.desc = F.G.desc;
+    K.uR = F.G.uR;
+    K.cell_start = F.G.cell_start;
+    K.cell_idx = F.G.cell_idx;
+    K.n = kf->n;
+    memcpy(K.Tcw, kf->Tcw, 64);
+    for (int r = 0; r < 3; r++) {  // KeyFrame::SetPose: Ow = -Rcw^T tcw
+      double acc = 0;
+      for (int k = 0; k < 3; k++) acc += (double)kf->Tcw[4 * k + r] * (double)kf->Tcw[4 * k + 3];
+      K.Ow[r] = -(float)acc;
+    }
+    mmt::FuseCam c;
+    memset(&c, 0, sizeof(c));
+    const mmt_config& cf = ctx->cfg;
+    c.fx = cf.fx; c.fy = cf.fy; c.cx = cf.cx; c.cy = cf.cy; c.bf = cf.bf;
+    c.W = (float)cf.width;
+    c.H = (float)cf.height;
+    c.invW = F.G.invW;
+    c.invH = F.G.invH;
+    c.logScale = F.G.logScale;
+    c.th = th;
+    c.nlevels = ctx->orb.nlevels;
+    for (int l = 0; l < c.nlevels && l < mmt::kMaxLevels; l++) {
+      c.scale[l] = ctx->orb.scale[l];
+      c.invSigma2[l] = ctx->orb.invSigma2[l];
+    }
+    DevBuf<mmt::LocalPointDev> dp(m);
+    DevBuf<uint8_t> pd(32 * (size_t)std::max(m, 1));
+    DevBuf<mmt::FuseKF> dk(1);
+    DevBuf<mmt::FuseQuery> dq(m);
+    DevBuf<int2> out(m);
+    MMT_HIP(hipMemcpyAsync(dk.p, &K, sizeof(K), hipMemcpyHostToDevice, s));
+    if (m > 0) {
+      MMT_HIP(hipMemcpyAsync(dp.p, hp.data(), sizeof(mmt::LocalPointDev) * (size_t)m,
+                             hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(pd.p, pts->desc, 32 * (size_t)m, hipMemcpyHostToDevice, s));
+      MMT_HIP(hipMemcpyAsync(dq.p, hq.data(), sizeof(mmt::FuseQuery) * (size_t)m,
+                             hipMemcpyHostToDevice, s));
+    }
+    mmt::launch_fuse_cand(dk.p, dq.p, m, dp.p, pd.p, c, out.p, s);
+    std::vector<int2> ho(std::max(m, 1));
+    if (m > 0)
+      MMT_HIP(hipMemcpyAsync(ho.data(), out.p, sizeof(int2) * (size_t)m, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+    for (int j = 0; j < m; j++) {
+      best_idx[j] = ho[j].x;
+      best_dist[j] = ho[j].y;
+    }
+  });
+}
+
+int mmt_local_bundle_adjustment(mmt_ctx* ctx, const mmt_ba_problem* p, float* Tcw_out,
+                                float* Xw_out, uint8_t* erase_out, int32_t* stats) {
+  if (!ctx || !p || !stats || p->n_kf < 0 || p->n_pt < 0 || p->n_edge < 0 ||
+      (p->n_kf > 0 && (!p->Tcw || !p->fixed || !Tcw_out)) ||
+      (p->n_pt > 0 && (!p->Xw || !Xw_out)) ||
+      (p->n_edge > 0 && (!p->e_pt || !p->e_kf || !p->e_obs || !p->e_inv_sigma2 || !erase_out)))
+    return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    mmt::BAHostProblem P;
+    P.n_kf = p->n_kf;
+    P.n_pt = p->n_pt;
+    P.n_edge = p->n_edge;
+    P.Tcw = p->Tcw;
+    P.fixed = p->fixed;
+    P.Xw = p->Xw;
+    P.e_pt = p->e_pt;
+    P.e_kf = p->e_kf;
+    P.e_obs = p->e_obs;
+    P.e_s = p->e_inv_sigma2;
+    const mmt_config& c = ctx->cfg;
+    P.fx = c.fx; P.fy = c.fy; P.cx = c.cx; P.cy = c.cy; P.bf = c.bf;
+    mmt::BARunner runner;
+    std::vector<float> T(16 * (size_t)std::max(p->n_kf, 1)), X(3 * (size_t)std::max(p->n_pt, 1));
+    std::vector<uint8_t> er(std::max(p->n_edge, 1));
+    int st[5] = {0, 0, 0, 0, 0};
+    runner.run(P, ctx->stream, T.data(), X.data(), er.data(), st);
+    if (p->n_kf > 0) memcpy(Tcw_out, T.data(), 64 * (size_t)p->n_kf);
+    if (p->n_pt > 0) memcpy(Xw_out, X.data(), 12 * (size_t)p->n_pt);
+    if (p->n_edge > 0) memcpy(erase_out, er.data(), (size_t)p->n_edge);
+    for (int i = 0; i < 5; i++) stats[i] = st[i];
+  });
+}
+
+int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out) {
+  if (!ctx || !out) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    memset(out, 0, sizeof(*out));
+    if (!ctx->tracker_ready) return;
+    const mmt::MappingStats& m = ctx->tracker.mapping_stats();
+    out->n_ba = m.n_ba;
+    out->n_fused = m.n_fused;
+    out->n_culled = m.n_culled;
+    out->n_ba_erased = m.n_ba_erased;
+    out->ba_trials = m.ba_trials;
+    out->ba_edges = m.ba_edges;
+    out->ba_kfs = m.ba_kfs;
+    out->ba_pts = m.ba_pts;
+    out->ba_max_opt = m.ba_max_opt;
+    out->fuse_launches = m.fuse_launches;
+    out->fuse_queries = m.fuse_queries;
+    out->fuse_relaunches = m.fuse_relaunches;
+    out->lm_us = m.lm_us;
+    out->ba_us = m.ba_us;
+    out->fuse_us = m.fuse_us;
+    out->d2_split_fallbacks = ctx->tracker.split_fallbacks();
+  });
+}
+
 int mmt_search_by_bow(mmt_ctx* ctx, const mmt_bow_keyframe* kf, int n_cur, const mmt_kp* cur_kps,
                       const uint8_t* cur_desc, const mmt_feature_vector* cur_fv, float nn_ratio,
                       int check_orientation, int32_t* match_out, int* nmatches) {

@@ -561,6 +561,7 @@ struct GridX {
   unsigned seq;
   int b, G, epoch, ntot;
   bool dead;
+  unsigned long long spin;  // wall-clock ticks a wait may last
 };
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -594,7 +595,7 @@ __device__ __forceinline__ double gx_sum(GridX& x, double v, int K, int maxl = -
         ok = (lo & 0xFFFFFFFF00000000ull) == tag && (hi & 0xFFFFFFFF00000000ull) == tag;
       }
       if (__all(ok)) break;
-      if (wall_clock64() - t0 > 10000000ull) {  // 0.1 s of the 100 MHz wall clock
+      if (wall_clock64() - t0 > x.spin) {  // 0.1 s of the 100 MHz wall clock by default
         x.dead = true;
         return 0.0;
       }
@@ -1226,7 +1227,7 @@ __global__ __launch_bounds__(256) void k_flow_lm_split(const FlowSolveDesc* __re
   const int Nl = hi - lo;
   const int nt = min((int)blockDim.x, max(64, (Nl + 63) / 64 * 64));
   if ((int)threadIdx.x >= nt) return;
-  GridX gx{D.gx, D.gx_seq, b, G, 0, N, false};
+  GridX gx{D.gx, D.gx_seq, b, G, 0, N, false, D.gx_spin ? D.gx_spin : 10000000ull};
   if (Nl <= nt)
     flow_lm_body<1, true>(D, Nl, lo, nt, sm, max_cand, gx, spec != 0);
   else

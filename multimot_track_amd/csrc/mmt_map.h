@@ -5,8 +5,10 @@
 // Reference: MapPoint.cc, KeyFrame.cc, Map.cc; Tracking.cc:985-1176 (Track's map branch),
 // 2531-2575 (StereoInitialization), 2766-3612 (CheckReplacedInLastFrame, UpdateLastFrame,
 // TrackWithMotionModel, TrackReferenceKeyFrame, TrackLocalMap, NeedNewKeyFrame, CreateNewKeyFrame,
-// SearchLocalPoints, UpdateLocalMap); LocalMapping.cc:131-208 (ProcessNewKeyFrame,
-// MapPointCulling, run synchronously after each new keyframe).
+// SearchLocalPoints, UpdateLocalMap); LocalMapping.cc:61-87, 131-208, 458-538, 636-700
+// (ProcessNewKeyFrame, MapPointCulling, SearchInNeighbors with ORBmatcher::Fuse,
+// LocalBundleAdjustment (Optimizer.cc:3341-3666), KeyFrameCulling, run synchronously after each new
+// keyframe; mmt_localmap.hip).
 //
 // The bookkeeping (observations, covisibility graph, spanning tree, local map, keyframe policy)
 // is host C++ where the reference keeps it; the data-parallel parts run on the GPU through the
@@ -15,10 +17,9 @@
 // updated by scatter as points are created or refined) and PoseOptimization (k_pose_opt).
 // Pinned choices and deviations (the same in oracle/oracle_map.h):
 //  * maps and sets keyed by KeyFrame* iterate in keyframe creation order;
-//  * LocalMapping runs synchronously (always idle for NeedNewKeyFrame) and does
-//    ProcessNewKeyFrame without the BoW conversion, then MapPointCulling; CreateNewMapPoints needs
-//    the missing vocabulary, SearchInNeighbors / LocalBundleAdjustment / KeyFrameCulling are
-//    SURVEY 8(f)-3;
+//  * LocalMapping runs synchronously (always idle for NeedNewKeyFrame, never aborted) and does
+//    ProcessNewKeyFrame without the BoW conversion, MapPointCulling, SearchInNeighbors, the local
+//    BA (GPU, mmt_ba.hip) and KeyFrameCulling; CreateNewMapPoints needs the missing vocabulary;
 //  * TrackReferenceKeyFrame's SearchByBoW and Relocalization (BoW database) become
 //    SearchByProjection against the last frame at the last frame's pose (th 15) + the reference's
 //    PoseOptimization and acceptance tests.
@@ -32,6 +33,7 @@
 #include <utility>
 #include <vector>
 
+#include "mmt_ba.h"
 #include "mmt_internal.h"
 #include "mmt_match.h"
 #include "mmt_track.h"
@@ -62,6 +64,9 @@ struct MPoint {
   bool trackInView = false;
   bool dirty = false;  // pool record out of date
   long lastSeen = 0;  // real points: mirrored in MapEngine::hot_ (the per-frame scans read that)
+  int replaced = -1;  // mpReplaced
+  long fuseCand = 0, baLocal = 0;  // mnFuseCandidateForKF, mnBALocalForKF
+  int desc_ver = 0;   // bumped by ComputeDistinctiveDescriptors (Fuse results read it)
   int obs_index(int kf) const {
     for (const auto& o : obs)
       if (o.first == kf) return o.second;
@@ -84,6 +89,16 @@ struct KFrame {
   std::set<int> children;
   long trackRef = 0;
   bool bad = false;
+  long fuseTarget = 0, baLocal = 0, baFixed = 0;  // mnFuseTargetForKF, mnBALocalForKF, mnBAFixedForKF
+  FuseKF dev{};  // the keyframe's keys, descriptors, mvuRight and grid on the device (KF store)
+};
+
+// LocalMapping counters (tests, profiling)
+struct MappingStats {
+  long n_ba = 0, n_fused = 0, n_culled = 0, n_ba_erased = 0, ba_trials = 0, ba_edges = 0,
+       ba_kfs = 0, ba_pts = 0, ba_max_opt = 0, fuse_launches = 0, fuse_queries = 0,
+       fuse_relaunches = 0;
+  double lm_us = 0, ba_us = 0, fuse_us = 0;  // host wall time (MMT_MAP_PROFILE)
 };
 
 // The map-path view of one Frame: its ORB output and B3 arrays (host copies of the device ones)
@@ -137,6 +152,10 @@ class MapEngine {
   int state() const { return state_; }
   int n_keyframes() const;
   int n_mappoints() const { return n_good_; }
+  // the current frame on the device (B3 grid, keys, descriptors): the keyframe made from it copies
+  // them into the keyframe store, where Fuse reads them
+  void set_frame_grid(const GridFrame& G) { G_ = G; }
+  const MappingStats& mapping_stats() const { return mstats_; }
 
  private:
   std::function<void()> overlap_;
@@ -174,6 +193,22 @@ class MapEngine {
   void process_new_keyframe(int kf);
   void map_point_culling(int kf);
   void mark_dirty(int h);
+  void mark_bad(int h);  // mbBad, the map's point count, the per-frame scan record
+  // ---- LocalMapping after ProcessNewKeyFrame / MapPointCulling (mmt_localmap.hip)
+  void local_mapping(int kf);
+  void search_in_neighbors(int kf);
+  // ORBmatcher::Fuse(kfl[i], pts, 3) for every i in order; candidates from the GPU
+  void fuse_sequence(const std::vector<int>& kfl, const std::vector<int>& pts);
+  void fuse_apply(int kf, int h, int bestIdx, int bestDist);
+  void local_bundle_adjustment(int kf);
+  void keyframe_culling(int kf);
+  void replace(int h, int by);
+  void erase_observation(int h, int kf);
+  void kf_set_bad(int kf);
+  void erase_connection(int kf, int other);
+  void set_pose(int kf, const float* Tcw);
+  void kf_store_add(int kf);
+  void fuse_launch(const std::vector<int>& kft_kf, const std::vector<FuseQuery>& q, int2* res);
   // GPU stages (synchronous on s_)
   int gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
                       const float* Tlast, float th, float retry_th, int min_matches);
@@ -181,7 +216,7 @@ class MapEngine {
   size_t out_bytes(int n) const;
   MapEdgeArgs edge_args(const GridFrame& G) const;
   void apply_pose_opt(MapFrameH& C, float* Tcw);
-  void gpu_flush_pool();
+  void gpu_flush_pool(hipStream_t st = nullptr);
   template <typename T>
   T* dev(size_t n);
   template <typename T>
@@ -266,6 +301,38 @@ class MapEngine {
   uint8_t* h_inview_ = nullptr;
   CandSet c3_{};
   int local_cap_ = 0;
+  // ---- LocalMapping
+  GridFrame G_{};
+  MappingStats mstats_;
+  hipStream_t lm_s_ = nullptr;  // LocalMapping's stream (beside the ego solve)
+  std::vector<uint8_t*> kf_blocks_;  // keyframe store: blocks of kKFBlock records
+  size_t kf_rec_bytes_ = 0;
+  static constexpr int kKFBlock = 64;
+  uint8_t* d_fup_ = nullptr;  // Fuse upload: [FuseKF table][queries]
+  uint8_t* h_fup_ = nullptr;
+  size_t fup_cap_ = 0;
+  int2* d_fres_ = nullptr;
+  int2* h_fres_ = nullptr;
+  size_t fres_cap_ = 0;
+  BARunner ba_;  // the local BA's buffers and launch
+  void grow_dev(uint8_t*& d, uint8_t*& h, size_t& cap, size_t need);
 };
+
+// ------------------------------------------------------------------ buffers
+template <typename T>
+inline T* MapEngine::dev(size_t n) {
+  T* p = nullptr;
+  MMT_HIP(hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T)));
+  dallocs_.push_back(p);
+  return p;
+}
+
+template <typename T>
+inline T* MapEngine::pinned(size_t n) {
+  T* p = nullptr;
+  MMT_HIP(hipHostMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault));
+  hallocs_.push_back(p);
+  return p;
+}
 
 }  // namespace mmt

@@ -49,23 +49,6 @@ static float norm3(const float* v) {
   return (float)std::sqrt(s);
 }
 
-// ------------------------------------------------------------------ buffers
-template <typename T>
-T* MapEngine::dev(size_t n) {
-  T* p = nullptr;
-  MMT_HIP(hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T)));
-  dallocs_.push_back(p);
-  return p;
-}
-
-template <typename T>
-T* MapEngine::pinned(size_t n) {
-  T* p = nullptr;
-  MMT_HIP(hipHostMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault));
-  hallocs_.push_back(p);
-  return p;
-}
-
 #define MAP_PROF(k, stmt)                       \
   do {                                          \
     const double _t0 = prof_on_ ? now_us() : 0; \
@@ -93,6 +76,10 @@ MapEngine::~MapEngine() {
             n_keyframes());
   }
   if (s_) (void)hipStreamSynchronize(s_);
+  if (lm_s_) {
+    (void)hipStreamSynchronize(lm_s_);
+    (void)hipStreamDestroy(lm_s_);
+  }
   for (void* p : dallocs_) (void)hipFree(p);
   for (void* p : hallocs_) (void)hipHostFree(p);
 }
@@ -145,6 +132,11 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
   d_esc_ = dev<double>(3 * (size_t)kcap);
   d_fsc_ = dev<int>(kcap);
   prof_on_ = getenv("MMT_MAP_PROFILE") != nullptr;
+  MMT_HIP(hipStreamCreateWithFlags(&lm_s_, hipStreamNonBlocking));
+  // keyframe store record: keys, descriptors, mvuRight, grid (cell starts + key lists)
+  kf_rec_bytes_ = align16(sizeof(mmt_kp) * (size_t)kcap) + 32 * (size_t)kcap +
+                  align16(4 * (size_t)kcap) + align16(4 * (size_t)(kGridCells + 1)) +
+                  align16(4 * (size_t)kcap);
   frameNextId_ = 0;
   mbVO_ = false;
   matchesInliers_ = 0;
@@ -245,11 +237,16 @@ void MapEngine::add_observation(int h, int kf, int idx) {  // MapPoint::AddObser
     p.nObs++;
 }
 
-void MapEngine::set_bad(int h) {  // MapPoint::SetBadFlag
+void MapEngine::mark_bad(int h) {
   MPoint& p = mp(h);
   if (!p.bad && h < kTemp) n_good_--;
   p.bad = true;
   if (h < kTemp) hot_[h].bad = 1;
+}
+
+void MapEngine::set_bad(int h) {  // MapPoint::SetBadFlag
+  MPoint& p = mp(h);
+  mark_bad(h);
   const std::vector<std::pair<int, int>> o = p.obs;
   p.obs.clear();
   for (const auto& kv : o) kfs_[kv.first].mps[kv.second] = -1;
@@ -290,6 +287,7 @@ void MapEngine::compute_distinctive(int h) {  // MapPoint::ComputeDistinctiveDes
     }
   }
   memcpy(p.desc, Dv[bi], 32);
+  p.desc_ver++;
   mark_dirty(h);
 }
 
@@ -565,7 +563,8 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
   return nm;
 }
 
-void MapEngine::gpu_flush_pool() {
+void MapEngine::gpu_flush_pool(hipStream_t st) {
+  if (!st) st = s_;
   // grow the pool with the map, then scatter the changed records
   if ((int)pts_.size() > pool_cap_) {
     const int cap = std::max((int)pts_.size() + 8192, 2 * pool_cap_);
@@ -575,10 +574,10 @@ void MapEngine::gpu_flush_pool() {
     MMT_HIP(hipMalloc((void**)&nd, 32 * (size_t)cap));
     if (pool_cap_ > 0) {
       MMT_HIP(hipMemcpyAsync(np, d_pool_, sizeof(LocalPointDev) * (size_t)pool_cap_,
-                             hipMemcpyDeviceToDevice, s_));
+                             hipMemcpyDeviceToDevice, st));
       MMT_HIP(hipMemcpyAsync(nd, d_pool_desc_, 32 * (size_t)pool_cap_, hipMemcpyDeviceToDevice,
-                             s_));
-      MMT_HIP(hipStreamSynchronize(s_));
+                             st));
+      MMT_HIP(hipStreamSynchronize(st));
       auto drop = [&](void* p) {
         dallocs_.erase(std::find(dallocs_.begin(), dallocs_.end(), p));
         (void)hipFree(p);
@@ -595,7 +594,7 @@ void MapEngine::gpu_flush_pool() {
   const int nd = (int)dirty_.size();
   if (nd == 0) return;
   if (nd > up_cap_) {
-    MMT_HIP(hipStreamSynchronize(s_));
+    MMT_HIP(hipStreamSynchronize(st));
     if (d_up_) {
       dallocs_.erase(std::find(dallocs_.begin(), dallocs_.end(), (void*)d_up_));
       hallocs_.erase(std::find(hallocs_.begin(), hallocs_.end(), (void*)h_up_));
@@ -620,14 +619,15 @@ void MapEngine::gpu_flush_pool() {
     p.dirty = false;
   }
   MMT_HIP(hipMemcpyAsync(d_up_, h_up_, sizeof(PoolUpdate) * (size_t)nd, hipMemcpyHostToDevice,
-                         s_));
-  launch_pool_scatter(d_up_, nd, d_pool_, d_pool_desc_, s_);
+                         st));
+  launch_pool_scatter(d_up_, nd, d_pool_, d_pool_desc_, st);
   dirty_.clear();
 }
 
 // ------------------------------------------------------------------ Tracking
 void MapEngine::initialize(MapFrameH& C, const float* Tcw) {
   const int kf = new_keyframe(C, Tcw);
+  kf_store_add(kf);
   for (int i = 0; i < C.n; i++) {
     const float z = C.depth[i];
     if (z > 0) {
@@ -643,6 +643,7 @@ void MapEngine::initialize(MapFrameH& C, const float* Tcw) {
   }
   process_new_keyframe(kf);
   map_point_culling(kf);
+  local_mapping(kf);
   lastKFFrameId_ = C.id;
   localKFs_.assign(1, kf);
   localPts_.clear();
@@ -952,6 +953,7 @@ bool MapEngine::need_new_keyframe(const MapFrameH& C) {  // Tracking::NeedNewKey
 
 void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracking.cc:3333-3414
   const int kf = new_keyframe(C, Tcw);
+  kf_store_add(kf);
   refKF_ = kf;
   C.refKF = kf;
   std::vector<std::pair<float, int>> v;
@@ -986,6 +988,7 @@ void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracki
   }
   process_new_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKF), processed at once
   map_point_culling(kf);
+  local_mapping(kf);
   lastKFFrameId_ = C.id;
 }
 
@@ -996,8 +999,11 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
   curId_ = C.id;
   const double t_track = prof_on_ ? now_us() : 0;
   bool bOK;
-  // CheckReplacedInLastFrame: no MapPoint is ever replaced on this path (no Fuse, no loops)
   if (state_ == 1) {
+    // CheckReplacedInLastFrame (Tracking.cc:2766-2781): one level of MapPoint::GetReplaced
+    for (int i = 0; i < L.n; i++)
+      if (L.mps[i] >= 0 && L.mps[i] < kTemp && pts_[L.mps[i]].replaced >= 0)
+        L.mps[i] = pts_[L.mps[i]].replaced;
     if (!has_vel || C.id < lastRelocFrameId_ + 2) {
       bSecondFrame = true;
       bOK = track_reference_subst(C, G, Tcw, L, Tlast);

@@ -157,4 +157,30 @@ struct alignas(16) PoolUpdate {
 void launch_pool_scatter(const PoolUpdate* up, int n, LocalPointDev* pool, uint8_t* pool_desc,
                          hipStream_t st);
 
+// ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th) candidates (ORBmatcher.cc:1200-1324): per
+// (keyframe, point) query the best key of the keyframe (Hamming distance, first in
+// GetFeaturesInArea order) among those the reference would compare; out[q] = (key, distance), or
+// (-1, 256).  The map-changing part of Fuse is the host's.
+struct FuseKF {  // one keyframe as Fuse reads it: its Frame grid, keys, mvuRight and pose
+  const mmt_kp* keys;
+  const uint8_t* desc;
+  const float* uR;
+  const int* cell_start;
+  const int* cell_idx;
+  float Tcw[16];
+  float Ow[3];
+  int n;
+};
+struct FuseQuery {
+  int kft;  // index into the launch's keyframe table
+  int h;    // map point (pool record)
+};
+struct FuseCam {
+  float fx, fy, cx, cy, bf, W, H, invW, invH, logScale, th;
+  int nlevels;
+  float scale[kMaxLevels], invSigma2[kMaxLevels];
+};
+void launch_fuse_cand(const FuseKF* kfs, const FuseQuery* q, int nq, const LocalPointDev* pool,
+                      const uint8_t* pool_desc, const FuseCam& cam, int2* out, hipStream_t st);
+
 }  // namespace mmt

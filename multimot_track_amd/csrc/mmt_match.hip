@@ -1122,4 +1122,154 @@ void launch_pool_scatter(const PoolUpdate* up, int n, LocalPointDev* pool, uint8
   MMT_HIP(hipGetLastError());
 }
 
+// ------------------------------------------------------------------------------ Fuse candidates
+// ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th) ORBmatcher.cc:1200-1324: the projection,
+// image / distance / viewing-angle tests, PredictScale and the best key in the window (levels
+// predicted - 1 .. predicted, the reprojection-error gate of stereo / monocular keys, the first of
+// equal Hamming distances).  Everything here depends on the point and the keyframe only; what the
+// match does to the map (AddObservation / MapPoint::Replace, order-dependent) is the host's.
+// One wave per (keyframe, point) query.
+struct FuseArgs {
+  const FuseKF* kfs;
+  const FuseQuery* q;
+  int nq;
+  const LocalPointDev* pool;
+  const uint8_t* pool_desc;
+  FuseCam cam;
+  int2* out;
+};
+
+__global__ __launch_bounds__(256) void k_fuse_cand(FuseArgs a) {
+  const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qi >= a.nq) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const FuseQuery Q = a.q[qi];
+  const FuseKF& K = a.kfs[Q.kft];
+  const LocalPointDev p = a.pool[Q.h];
+  const FuseCam& c = a.cam;
+  int2 res = make_int2(-1, 256);
+  float p3Dc[3];
+  pose_xform(K.Tcw, p.Xw, p3Dc);
+  bool ok = !(p3Dc[2] < 0.0f);
+  float u = 0, v = 0, ur = 0, radius = 0;
+  int npl = 0;
+  if (ok) {
+    const float invz = 1 / p3Dc[2];
+    const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+    u = c.fx * x + c.cx;
+    v = c.fy * y + c.cy;
+    ok = u >= 0.f && u < c.W && v >= 0.f && v < c.H;  // KeyFrame::IsInImage
+    if (ok) {
+      ur = u - c.bf * invz;
+      const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+      float PO[3];
+      double n2 = 0;
+      for (int k = 0; k < 3; k++) {
+        PO[k] = p.Xw[k] - K.Ow[k];
+        n2 += (double)PO[k] * (double)PO[k];
+      }
+      const float dist3D = (float)sqrt(n2);
+      ok = !(dist3D < minDistance || dist3D > maxDistance);
+      if (ok) {
+        double dot = 0;
+        for (int k = 0; k < 3; k++) dot += (double)PO[k] * (double)p.normal[k];
+        ok = !(dot < 0.5 * (double)dist3D);  // viewing angle under 60 degrees
+      }
+      if (ok) {
+        const float ratio = p.max_dist / dist3D;  // MapPoint::PredictScale(dist3D, pKF)
+        const float ls = (float)log((double)ratio) / c.logScale;
+        npl = isfinite(ls) ? (int)ceilf(ls) : INT_MIN;
+        if (npl < 0) npl = 0;
+        else if (npl >= c.nlevels) npl = c.nlevels - 1;
+        radius = c.th * c.scale[npl];
+      }
+    }
+  }
+  int cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
+  if (ok && isfinite(u) && isfinite(v)) {  // KeyFrame::GetFeaturesInArea's cell range
+    cx0 = max(0, (int)floorf((u - 0.f - radius) * c.invW));
+    cx1 = min(kGridCols - 1, (int)ceilf((u - 0.f + radius) * c.invW));
+    cy0 = max(0, (int)floorf((v - 0.f - radius) * c.invH));
+    cy1 = min(kGridRows - 1, (int)ceilf((v - 0.f + radius) * c.invH));
+    if (cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0) ok = false;
+  } else {
+    ok = false;
+  }
+  if (ok) {
+    uint32_t dmp[8];
+    load_desc8(a.pool_desc + 32 * (size_t)Q.h, dmp);
+    const int nseg = cx1 - cx0 + 1;
+    int sb = 0, sl = 0;
+    if (lane < nseg) {
+      const int base = (cx0 + lane) * kGridRows;
+      sb = K.cell_start[base + cy0];
+      sl = K.cell_start[base + cy1 + 1] - sb;
+    }
+    int pre = sl;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(pre, o, 64);
+      if (lane >= o) pre += y;
+    }
+    const int total = __shfl(pre, nseg - 1, 64);
+    pre -= sl;
+    uint32_t best = kNoCand;
+    int bidx = -1;
+    for (int p0 = 0; p0 < total; p0 += 64) {
+      const int pp = p0 + lane;
+      int s = 0;
+      for (int q = 1; q < nseg; q++) {
+        const int pq = __shfl(pre, q, 64);
+        if (pq <= pp) s = q;
+      }
+      const int seg_b = __shfl(sb, s, 64), seg_p = __shfl(pre, s, 64);
+      if (pp < total) {
+        const int k = K.cell_idx[seg_b + pp - seg_p];
+        const mmt_kp kp = K.keys[k];
+        bool g = fabsf(kp.x - u) < radius && fabsf(kp.y - v) < radius;
+        if (g) g = !(kp.octave < npl - 1 || kp.octave > npl);
+        if (g) {
+          const float ex = u - kp.x, ey = v - kp.y;
+          const float kr = K.uR[k];
+          if (kr >= 0) {
+            const float er = ur - kr;
+            const float e2 = ex * ex + ey * ey + er * er;
+            g = !((double)(e2 * c.invSigma2[kp.octave]) > 7.8);
+          } else {
+            const float e2 = ex * ex + ey * ey;
+            g = !((double)(e2 * c.invSigma2[kp.octave]) > 5.99);
+          }
+        }
+        if (g) {
+          const uint4* dk = reinterpret_cast<const uint4*>(K.desc + 32 * (size_t)k);
+          const uint4 da = dk[0], db = dk[1];
+          const int dist = __popc(da.x ^ dmp[0]) + __popc(da.y ^ dmp[1]) +
+                           __popc(da.z ^ dmp[2]) + __popc(da.w ^ dmp[3]) +
+                           __popc(db.x ^ dmp[4]) + __popc(db.y ^ dmp[5]) +
+                           __popc(db.z ^ dmp[6]) + __popc(db.w ^ dmp[7]);
+          const uint32_t key = ((uint32_t)dist << 20) | (uint32_t)pp;
+          if (key < best) {
+            best = key;
+            bidx = k;
+          }
+        }
+      }
+    }
+    const uint32_t m = wave_min_u32(best);
+    if (m != kNoCand) {
+      const int ol = __ffsll((long long)__ballot(best == m)) - 1;
+      res = make_int2(__shfl(bidx, ol, 64), (int)(m >> 20));
+    }
+  }
+  if (lane == 0) a.out[qi] = res;
+}
+
+void launch_fuse_cand(const FuseKF* kfs, const FuseQuery* q, int nq, const LocalPointDev* pool,
+                      const uint8_t* pool_desc, const FuseCam& cam, int2* out, hipStream_t st) {
+  if (nq <= 0) return;
+  FuseArgs a{kfs, q, nq, pool, pool_desc, cam, out};
+  hipLaunchKernelGGL(k_fuse_cand, dim3((nq + 3) / 4), dim3(256), 0, st, a);
+  MMT_HIP(hipGetLastError());
+}
+
 }  // namespace mmt

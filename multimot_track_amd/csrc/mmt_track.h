@@ -96,6 +96,9 @@ struct FlowSolveDesc {
   // (kFlowSplitGranules 8-byte words, zeroed once at allocation) and this launch's tag salt
   unsigned long long* gx;
   unsigned gx_seq;
+  // spin bound of the exchange waits in 100 MHz wall-clock ticks (0: 0.1 s); a test hook shortens
+  // it to force the not-resident status
+  unsigned long long gx_spin;
 };
 
 // A large single solve split over up to kFlowSplitMax workgroups (one slice of the edges each),

@@ -75,6 +75,8 @@ class Tracker {
   const mmt_kp* kps() const { return d_kps_; }
   const int* nkp() const { return d_nkp_; }
   int kcap() const { return kcap_; }
+  const MappingStats& mapping_stats() const { return map_.mapping_stats(); }
+  long split_fallbacks() const { return split_fallbacks_; }
 
  private:
   struct FrameSlot {
@@ -261,6 +263,8 @@ class Tracker {
   int* d_lmstats_ = nullptr;
   unsigned long long* d_gx_ = nullptr;  // the split ego solve's exchange granules
   unsigned gx_seq_ = 0;
+  long split_fallbacks_ = 0;  // D2 split solves re-run on one workgroup (residency not met)
+  unsigned long long split_spin_ = 0;  // MMT_DEBUG_SPLIT_SPIN (0: the kernel's 0.1 s)
   PnPObject* d_pnp_[kObjSlots] = {};
   PnPBuf pnp_[kObjSlots][kMaxObj];
   bool prof_ = false;

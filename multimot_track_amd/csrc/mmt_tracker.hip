@@ -358,13 +358,17 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // the frame, while its kernels run (C3 895 -> 905 fps, tools/ab_interleave.py, 4 rounds)
   // MMT_OBJ_LAG: frames between enqueueing a frame's object path and reading its results (default
   // 16: the D3 chain's slow stretches no longer stall the host; interleaved A/B 905 / 915 / 920 fps
-  // at 2 / 3 / 4, then 932 / 937 / 944 / 950 / 956 / 964 at 4 / 6 / 8 / 10 / 14 / 18, flat from
-  // there to 32)
+  // at 2 / 3 / 4, then 932 / 937 / 944 / 950 / 956 / 964 at 4 / 6 / 8 / 10 / 14 / 18; the lags
+  // above 16 and the "flat to 32" sweep were measured with more object slots than this build's
+  // kObjSlots = 18, which caps the lag at 16)
   static_assert(kSlots > kObjLagMax + 2, "frame slots too few for the object lag");
   if (const char* ol = getenv("MMT_OBJ_LAG")) obj_lag_ = std::max(1, std::min(kObjLagMax, atoi(ol)));
   // MMT_DEBUG_D3_ITERS: caps D3's LM iterations (the reference's 200), for bottleneck analysis
   // only: it changes the object results
   if (const char* di = getenv("MMT_DEBUG_D3_ITERS")) d3_iters_ = std::max(1, atoi(di));
+  // MMT_DEBUG_SPLIT_SPIN: the split ego solve's exchange spin bound in wall-clock ticks (test
+  // hook: a tiny bound forces the not-resident status and so the one-workgroup re-run)
+  if (const char* ss = getenv("MMT_DEBUG_SPLIT_SPIN")) split_spin_ = strtoull(ss, nullptr, 10);
   const char* oo = getenv("MMT_OBJ_OVERLAP");
   overlap_obj_ = !(oo && atoi(oo) == 0);
   const char* ot = getenv("MMT_OBJ_THREAD");
@@ -534,6 +538,7 @@ void Tracker::reset() {
   for (long& k : slot_job_) k = 0;
   if (oa_) MMT_HIP(hipStreamSynchronize(oa_));
   if (ob_) MMT_HIP(hipStreamSynchronize(ob_));
+  if (d_err_) MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));  // a bad label does not outlive a reset
   state_ = 0;
   bFirstFrame_ = false;  // uninitialised member in the reference (Tracking.h:180): pinned false
   bSecondFrame_ = false;
@@ -657,6 +662,15 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   }
   } catch (...) {
     obj_drain(true);  // no job may outlive the call (they write into `outs`)
+    // the inline path: frames still in flight (and the queued one) point into `outs`, which dies
+    // with this call; let their device work finish and drop them (the object pipeline restarts)
+    if (oa_) (void)hipStreamSynchronize(oa_);
+    if (ob_) (void)hipStreamSynchronize(ob_);
+    {
+      std::lock_guard<std::mutex> lk(om_);
+      inflight_.clear();
+    }
+    qa_ = ObjFrame();
     throw;
   }
   // the chunk's results are complete on return
@@ -746,6 +760,15 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   // mCurrentFrame.mvObjKeys: the frame's own samples, or the hand-off once bFirstFrame is set
   MMT_HIP(hipMemcpyAsync(&eh_->nlast_obj, handoff ? Ls.ob.count : C.ob.count, sizeof(int),
                          hipMemcpyDeviceToHost, st));
+  // the frame on the device as the matchers (and a keyframe made from it) read it
+  GridFrame G = grid0_;
+  G.keys = a.kps;
+  G.desc = d_desc_ + 32 * (size_t)kcap_ * a.f;
+  G.uR = d_uR_ + (size_t)kcap_ * a.f;
+  G.cell_start = d_cell_start_ + (size_t)(kGridCells + 1) * a.f;
+  G.cell_idx = d_cell_idx_ + (size_t)kcap_ * a.f;
+  G.n = a.n_keys;
+  map_.set_frame_grid(G);
   if (state_ == 0) {
     ego_pending_ = false;
     return;
@@ -753,13 +776,6 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   // ---- ORB-SLAM2 map tracking (Tracking.cc:985-1176): the initial pose of the flow solve; it
   // may reset mLastFrame's pose (UpdateLastFrame), which the rest of this frame reads
   {
-    GridFrame G = grid0_;
-    G.keys = a.kps;
-    G.desc = d_desc_ + 32 * (size_t)kcap_ * a.f;
-    G.uR = d_uR_ + (size_t)kcap_ * a.f;
-    G.cell_start = d_cell_start_ + (size_t)(kGridCells + 1) * a.f;
-    G.cell_idx = d_cell_idx_ + (size_t)kcap_ * a.f;
-    G.n = a.n_keys;
     MapStatsH& ms = out.map;
     // the previous frame's object path runs while the first map chain is on the GPU
     if (!ow_on_ && overlap_obj_) map_.set_overlap([this] { obj_advance(); });
@@ -800,6 +816,12 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   d2.stats = d_lmstats_;
   d2.gx = d_gx_;
   d2.gx_seq = ++gx_seq_;
+  d2.gx_spin = split_spin_;
+  // the granule tags carry 16 bits of gx_seq_: two launches with the same salt are always
+  // separated by a wrap, where the granules are cleared (a slot no launch has rewritten since the
+  // previous use of the salt could otherwise match)
+  if ((gx_seq_ & 0xFFFFu) == 0)
+    MMT_HIP(hipMemsetAsync(d_gx_, 0, sizeof(unsigned long long) * kFlowSplitGranules, st));
   MMT_HIP(hipMemcpyAsync(d_descs_, &d2, sizeof(d2), hipMemcpyHostToDevice, st));
   // the ego solve (1,500-1,700 edges on KITTI-like frames) split over workgroups
   const int groups = flow_split_groups(eh_->n_static[last_]);
@@ -859,7 +881,17 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
   } else {
     float Tcw[16];
     memcpy(Tcw, eh_->Tcw, sizeof(Tcw));
-    if (eh_->st[2] == 2) throw DeviceError("D2: the split solve's workgroups were not resident together");
+    if (eh_->st[2] == 2) {
+      // the split solve's workgroups were not resident together within its spin bound (other
+      // streams or processes held the CUs): the same solve on one workgroup, from the unchanged
+      // descriptor
+      launch_flow_lm(d_descs_, 1, eh_->n_static[last_], st);
+      MMT_HIP(hipMemcpyAsync(eh_->Tcw, d_poses_, sizeof(eh_->Tcw) + sizeof(eh_->st),
+                             hipMemcpyDeviceToHost, st));
+      MMT_HIP(hipStreamSynchronize(st));
+      split_fallbacks_++;
+      memcpy(Tcw, eh_->Tcw, sizeof(Tcw));
+    }
     if (eh_->st[2] != 0) memcpy(Tcw, ego_Tinit_, sizeof(Tcw));  // < 3 edges: pose unchanged
     memcpy(C.Tcw, Tcw, sizeof(Tcw));
     out.ego_iterations = eh_->st[0];
@@ -930,7 +962,11 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   MMT_HIP(hipMemcpyAsync(H.hist, d_hist_[q], sizeof(H.hist), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(&H.err, d_err_, sizeof(int), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
-  if (H.err) throw ArgError("semantic label outside [0, 15] on the object path");
+  if (H.err) {
+    MMT_HIP(hipMemsetAsync(d_err_, 0, sizeof(int), st));  // the next frame starts clean
+    MMT_HIP(hipStreamSynchronize(st));
+    throw ArgError("semantic label outside [0, 15] on the object path");
+  }
   const LabelStats* stats = H.stats;
   const int* hist = H.hist;
   // ---- B7 decisions (Tracking.cc:1424-1536); labels ascending = UniLab order

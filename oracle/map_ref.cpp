@@ -15,47 +15,6 @@
 
 namespace oracle {
 
-// ------------------------------------------------------------------ pose helpers
-static void m4_mul(const float* A, const float* B, float* C) {
-  float R[16];
-  for (int r = 0; r < 4; r++)
-    for (int c = 0; c < 4; c++) {
-      double s = 0;
-      for (int k = 0; k < 4; k++) s += (double)A[4 * r + k] * (double)B[4 * k + c];
-      R[4 * r + c] = (float)s;
-    }
-  memcpy(C, R, sizeof(R));
-}
-
-// Frame::UpdatePoseMatrices / KeyFrame::SetPose: Ow = -Rcw^T tcw
-static void cam_centre(const float* T, float* Ow) {
-  for (int r = 0; r < 3; r++) {
-    double s = 0;
-    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)T[4 * k + 3];
-    Ow[r] = -(float)s;
-  }
-}
-
-// Frame::UnprojectStereo (Frame.cc:1064-1079) / KeyFrame::UnprojectStereo: Rwc * x3Dc + Ow
-static void unproject(const MapCam& c, const float* T, float u, float v, float z, float* out) {
-  const float x = (u - c.cx) * z * c.invfx;
-  const float y = (v - c.cy) * z * c.invfy;
-  const float xc[3] = {x, y, z};
-  float Ow[3];
-  cam_centre(T, Ow);
-  for (int r = 0; r < 3; r++) {
-    double s = 0;
-    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)xc[k];
-    out[r] = (float)s + Ow[r];
-  }
-}
-
-static float norm3(const float* v) {
-  double s = 0;
-  for (int k = 0; k < 3; k++) s += (double)v[k] * (double)v[k];
-  return (float)std::sqrt(s);
-}
-
 // ------------------------------------------------------------------ setup
 void MapTracker::init(const MapCam& c) {
   cam = c;
@@ -217,7 +176,10 @@ int MapTracker::new_keyframe(const std::vector<Key>& keys, const std::vector<uin
   k.depth = C.depth;
   k.desc = desc;
   k.mps = C.mps;
-  kfs.push_back(k);
+  MatchFrame G;  // mGrid: the frame's grid, copied (KeyFrame.cc:48-54)
+  build_grid(keys, desc, C, G);
+  k.grid = std::move(G.grid);
+  kfs.push_back(std::move(k));
   return (int)kfs.size() - 1;
 }
 
@@ -363,6 +325,7 @@ void MapTracker::initialize(const std::vector<Key>& keys, const std::vector<uint
   }
   process_new_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKFini), processed at once
   map_point_culling(kf);
+  local_mapping(kf);
   lastKFFrameId_ = C.id;
   lastKF_ = kf;
   localKFs_.assign(1, kf);
@@ -746,6 +709,7 @@ void MapTracker::create_new_keyframe(const std::vector<Key>& keys,
   }
   process_new_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKF), processed at once
   map_point_culling(kf);
+  local_mapping(kf);
   lastKFFrameId_ = C.id;
   lastKF_ = kf;
 }
@@ -756,8 +720,11 @@ int MapTracker::track(const std::vector<Key>& keys, const std::vector<uint8_t>& 
                       bool& has_vel, bool& bSecondFrame, MapStats& st) {
   curId_ = C.id;
   bool bOK;
-  // CheckReplacedInLastFrame: no MapPoint is ever replaced here (no Fuse / loop closing)
   if (state_ == 1) {
+    // CheckReplacedInLastFrame (Tracking.cc:2766-2781): one level of MapPoint::GetReplaced
+    for (size_t i = 0; i < L.mps.size(); i++)
+      if (L.mps[i] >= 0 && L.mps[i] < kTemp && mp(L.mps[i]).replaced >= 0)
+        L.mps[i] = mp(L.mps[i]).replaced;
     if (!has_vel || C.id < lastRelocFrameId_ + 2) {
       bSecondFrame = true;
       bOK = track_reference_subst(keys, desc, C, Tcw, lkeys, L, Tlast);

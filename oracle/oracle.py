@@ -248,6 +248,36 @@ class Tracker:
             _LIB.oracle_tracker_destroy(self._h)
             self._h = None
 
+    def map_stats(self):
+        """LocalMapping counters (oracle/mapping_ref.cpp)."""
+        out = np.zeros(9, np.int64)
+        lib().oracle_tracker_map_stats(ctypes.c_void_p(self._h), _p(out))
+        keys = ("n_ba", "n_fused", "n_culled", "n_ba_erased", "ba_trials", "ba_edges", "ba_kfs",
+                "ba_pts", "ba_max_opt_kfs")
+        return {k: int(v) for k, v in zip(keys, out)}
+
+    def capture_ba(self, which):
+        """Record the problem of this tracker's which-th LocalBundleAdjustment (0-based)."""
+        lib().oracle_tracker_capture_ba(ctypes.c_void_p(self._h), which)
+
+    def captured_ba(self):
+        """The captured LocalBundleAdjustment problem as a dict of arrays, or None."""
+        L = lib()
+        sz = np.zeros(3, np.int32)
+        L.oracle_tracker_captured_ba(ctypes.c_void_p(self._h), _p(sz), None, None, None, None,
+                                     None, None, None)
+        nk, npt, ne = (int(v) for v in sz)
+        if ne == 0 and nk == 0:
+            return None
+        P = dict(T=np.zeros((nk, 4, 4), np.float32), fixed=np.zeros(nk, np.uint8),
+                 X=np.zeros((npt, 3), np.float32), pt=np.zeros(ne, np.int32),
+                 kf=np.zeros(ne, np.int32), obs=np.zeros((ne, 3), np.float32),
+                 s=np.zeros(ne, np.float32))
+        L.oracle_tracker_captured_ba(ctypes.c_void_p(self._h), _p(sz), _p(P["T"]),
+                                     _p(P["fixed"]), _p(P["X"]), _p(P["pt"]), _p(P["kf"]),
+                                     _p(P["obs"]), _p(P["s"]))
+        return P
+
     def track(self, bgr, disp, flow, mask):
         bgr = np.ascontiguousarray(bgr, np.uint8)
         disp = np.ascontiguousarray(disp, np.uint16)
@@ -273,6 +303,52 @@ class Tracker:
                     map_matches_mm=int(info[8]), map_inliers_local=int(info[9]),
                     n_keyframes=int(info[10]), n_mappoints=int(info[11]),
                     new_keyframe=int(info[12]), Tcw_map=tcw[16:].reshape(4, 4).copy())
+
+
+def fuse_candidates(kps, desc, depth, tcw, Xw, normal, min_dist, max_dist, pdesc, K, bf,
+                    w, h, nfeatures=2000, th=3.0):
+    """ORBmatcher::Fuse's per-point search against one keyframe (oracle/mapping_ref.cpp):
+    (best key index, best distance) per point, -1 / 256 for none."""
+    c = orb_config(nfeatures)
+    scale = np.ascontiguousarray(c["scale"], np.float32)
+    inv_s2 = np.ascontiguousarray(np.float32(1.0) / c["sigma2"], np.float32)  # 1.0f / sigma2
+    kps = np.ascontiguousarray(kps)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    depth = np.ascontiguousarray(depth, np.float32)
+    tcw = np.ascontiguousarray(tcw, np.float32)
+    arrs = [np.ascontiguousarray(a, np.float32) for a in (Xw, normal, min_dist, max_dist)]
+    pd = np.ascontiguousarray(pdesc, np.uint8)
+    m = len(arrs[2])
+    idx = np.zeros(max(m, 1), np.int32)
+    dist = np.zeros(max(m, 1), np.int32)
+    cam = np.array([K[0], K[1], K[2], K[3], bf], np.float32)
+    lib().oracle_fuse_candidates(w, h, _p(cam), len(scale), _p(scale), _p(inv_s2), len(kps),
+                                 _p(kps), _p(desc), _p(depth), _p(tcw), m, _p(arrs[0]),
+                                 _p(arrs[1]), _p(arrs[2]), _p(arrs[3]), _p(pd),
+                                 ctypes.c_float(th), _p(idx), _p(dist))
+    return idx[:m], dist[:m]
+
+
+def local_ba(P, K, bf):
+    """Optimizer::LocalBundleAdjustment's solve (oracle/ba_ref.cpp) on a problem dict (the keys of
+    Tracker.captured_ba).  Returns (T (n_kf, 4, 4), X (n_pt, 3), erase (n_edge,), stats dict)."""
+    nk, npt, ne = len(P["fixed"]), len(P["X"]), len(P["pt"])
+    T = np.ascontiguousarray(P["T"], np.float32)
+    X = np.ascontiguousarray(P["X"], np.float32)
+    To = np.zeros((nk, 4, 4), np.float32)
+    Xo = np.zeros((npt, 3), np.float32)
+    er = np.zeros(max(ne, 1), np.uint8)
+    st = np.zeros(5, np.int32)
+    cam = np.array([K[0], K[1], K[2], K[3], bf], np.float32)
+    lib().oracle_local_ba(nk, npt, ne, _p(T), _p(np.ascontiguousarray(P["fixed"], np.uint8)),
+                          _p(X), _p(np.ascontiguousarray(P["pt"], np.int32)),
+                          _p(np.ascontiguousarray(P["kf"], np.int32)),
+                          _p(np.ascontiguousarray(P["obs"], np.float32)),
+                          _p(np.ascontiguousarray(P["s"], np.float32)), _p(cam), _p(To), _p(Xo),
+                          _p(er), _p(st))
+    stats = dict(iterations=(int(st[0]), int(st[1])), trials=(int(st[2]), int(st[3])),
+                 n_erase=int(st[4]))
+    return To, Xo, er[:ne], stats
 
 
 # ---------------------------------------------------------------- B3 / C1-C3 (match_ref.cpp)

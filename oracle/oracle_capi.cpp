@@ -3,7 +3,9 @@
 // through ctypes.  Never linked into the product library.
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
+#include <map>
 
 #include "oracle_common.h"
 #include "oracle_match.h"
@@ -125,6 +127,7 @@ int oracle_orb_extract(const uint8_t* gray, int w, int h, int nfeatures, float s
 }  // extern "C"
 
 // ------------------------------------------------------------------ tracker / solve probes
+#include "oracle_map.h"
 #include "oracle_solve.h"
 #include "oracle_track.h"
 
@@ -249,6 +252,127 @@ void* oracle_tracker_create(int w, int h, float fx, float fy, float cx, float cy
 }
 
 void oracle_tracker_destroy(void* t) { delete (OTracker*)t; }
+
+// LocalMapping counters: [BAs, fused, culled keyframes, BA-erased observations, BA trials, BA
+// edges, BA keyframe vertices, BA points, largest count of optimised keyframes]
+void oracle_tracker_map_stats(void* tp, long long* out) {
+  const MapTracker::MappingStats& m = ((OTracker*)tp)->map.mstats;
+  const long v[9] = {m.n_ba, m.n_fused, m.n_culled, m.n_ba_erased, m.ba_trials, m.ba_edges,
+                     m.ba_kfs, m.ba_pts, m.ba_max_opt_kfs};
+  for (int i = 0; i < 9; i++) out[i] = v[i];
+}
+
+// Records the problem and result of the which-th LocalBundleAdjustment (0-based) of this tracker,
+// as probe fixtures for the GPU solver.
+struct BACapture {
+  int want = -1, seen = 0, got = 0;
+  std::vector<float> T, X, obs, s, rT, rX;
+  std::vector<uint8_t> fixed, erase;
+  std::vector<int> pt, kf;
+  int n_kf = 0, n_pt = 0, n_edge = 0, it[2] = {0, 0}, tr[2] = {0, 0};
+};
+static std::map<void*, BACapture> g_cap;
+
+void oracle_tracker_capture_ba(void* tp, int which) {
+  BACapture& c = g_cap[tp];
+  c = BACapture();
+  c.want = which;
+  ((OTracker*)tp)->map.ba_hook = [tp](const BAProblem& P, const BAResult& R) {
+    BACapture& c = g_cap[tp];
+    if (c.seen++ != c.want) return;
+    c.got = 1;
+    c.n_kf = P.n_kf; c.n_pt = P.n_pt; c.n_edge = P.n_edge;
+    c.T.assign(P.Tcw, P.Tcw + 16 * (size_t)P.n_kf);
+    c.fixed.assign(P.fixed, P.fixed + P.n_kf);
+    c.X.assign(P.Xw, P.Xw + 3 * (size_t)P.n_pt);
+    c.pt.assign(P.e_pt, P.e_pt + P.n_edge);
+    c.kf.assign(P.e_kf, P.e_kf + P.n_edge);
+    c.obs.assign(P.e_obs, P.e_obs + 3 * (size_t)P.n_edge);
+    c.s.assign(P.e_inv_sigma2, P.e_inv_sigma2 + P.n_edge);
+    c.rT = R.Tcw; c.rX = R.Xw; c.erase = R.erase;
+    c.it[0] = R.iterations[0]; c.it[1] = R.iterations[1];
+    c.tr[0] = R.trials[0]; c.tr[1] = R.trials[1];
+  };
+}
+
+// sizes[3] = n_kf, n_pt, n_edge (0s until captured); with non-null arrays, copies the problem out
+int oracle_tracker_captured_ba(void* tp, int* sizes, float* T, uint8_t* fixed, float* X, int* pt,
+                               int* kf, float* obs, float* s) {
+  BACapture& c = g_cap[tp];
+  sizes[0] = c.got ? c.n_kf : 0;
+  sizes[1] = c.got ? c.n_pt : 0;
+  sizes[2] = c.got ? c.n_edge : 0;
+  if (!c.got || !T) return c.got;
+  memcpy(T, c.T.data(), 4 * c.T.size());
+  memcpy(fixed, c.fixed.data(), c.fixed.size());
+  memcpy(X, c.X.data(), 4 * c.X.size());
+  memcpy(pt, c.pt.data(), 4 * c.pt.size());
+  memcpy(kf, c.kf.data(), 4 * c.kf.size());
+  memcpy(obs, c.obs.data(), 4 * c.obs.size());
+  memcpy(s, c.s.data(), 4 * c.s.size());
+  return 1;
+}
+
+// ORBmatcher::Fuse's per-point search against one keyframe (mapping_ref.cpp).  kps n, desc n x 32,
+// depth W x H (mvuRight / the grid as the frame's), Tcw; points m: pos, normal, min/max distance,
+// descriptor.  cam: fx fy cx cy bf; scale / inv_sigma2 nlevels.
+int oracle_fuse_candidates(int W, int H, const float* cam, int nlevels, const float* scale,
+                           const float* inv_sigma2, int n, const Key* kps, const uint8_t* desc,
+                           const float* depth, const float* Tcw, int m, const float* pos,
+                           const float* normal, const float* min_dist, const float* max_dist,
+                           const uint8_t* pdesc, float th, int* best_idx, int* best_dist) {
+  MapCam mc;
+  mc.W = W; mc.H = H;
+  mc.fx = cam[0]; mc.fy = cam[1]; mc.cx = cam[2]; mc.cy = cam[3]; mc.bf = cam[4];
+  mc.nlevels = nlevels;
+  mc.scale.assign(scale, scale + nlevels);
+  mc.invSigma2.assign(inv_sigma2, inv_sigma2 + nlevels);
+  mc.logScale = (float)std::log((double)scale[nlevels > 1 ? 1 : 0]);
+  MatchFrame G;
+  G.n = n;
+  G.keys = kps;
+  G.bf = mc.bf;
+  frame_stereo_grid(G, depth, W, H);
+  OKeyFrame K;
+  K.keys.assign(kps, kps + n);
+  K.uR = G.uR;
+  K.depth = G.depth;
+  K.desc.assign(desc, desc + 32 * (size_t)n);
+  K.grid = G.grid;
+  memcpy(K.Tcw, Tcw, 64);
+  cam_centre(Tcw, K.Ow);
+  for (int j = 0; j < m; j++) {
+    OMapPoint p;
+    memcpy(p.pos, pos + 3 * (size_t)j, 12);
+    memcpy(p.normal, normal + 3 * (size_t)j, 12);
+    p.minDist = min_dist[j];
+    p.maxDist = max_dist[j];
+    memcpy(p.desc, pdesc + 32 * (size_t)j, 32);
+    best_dist[j] = fuse_candidate(K, mc, p, th, &best_idx[j]);
+  }
+  return 0;
+}
+
+// LocalBundleAdjustment's solve on a caller-given problem (ba_ref.cpp).  stats: [iterations of
+// round 1, of round 2, trials of round 1, of round 2, erased edges]
+int oracle_local_ba(int n_kf, int n_pt, int n_edge, const float* T, const uint8_t* fixed,
+                    const float* X, const int* pt, const int* kf, const float* obs, const float* s,
+                    const float* cam, float* T_out, float* X_out, uint8_t* erase, int* stats) {
+  BAProblem P;
+  P.n_kf = n_kf; P.n_pt = n_pt; P.n_edge = n_edge;
+  P.Tcw = T; P.fixed = fixed; P.Xw = X; P.e_pt = pt; P.e_kf = kf; P.e_obs = obs;
+  P.e_inv_sigma2 = s;
+  P.fx = cam[0]; P.fy = cam[1]; P.cx = cam[2]; P.cy = cam[3]; P.bf = cam[4];
+  BAResult R;
+  local_ba_solve(P, R);
+  memcpy(T_out, R.Tcw.data(), 4 * R.Tcw.size());
+  memcpy(X_out, R.Xw.data(), 4 * R.Xw.size());
+  memcpy(erase, R.erase.data(), R.erase.size());
+  stats[0] = R.iterations[0]; stats[1] = R.iterations[1];
+  stats[2] = R.trials[0]; stats[3] = R.trials[1];
+  stats[4] = R.n_erase;
+  return 0;
+}
 
 // Tracks one frame.  info: [initialized, n_keys, n_static, n_obj_samples, ego_iters,
 // ego_inliers, n_objects, map_state, map_matches_mm, map_inliers_local, n_keyframes,

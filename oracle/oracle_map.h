@@ -10,15 +10,21 @@
 //   TrackLocalMap / SearchLocalPoints / UpdateLocalMap / UpdateLocalKeyFrames / UpdateLocalPoints
 //                                                src/Tracking.cc:3189-3240, 3416-3612
 //   NeedNewKeyFrame / CreateNewKeyFrame          src/Tracking.cc:3243-3414
-//   LocalMapping::ProcessNewKeyFrame / MapPointCulling  src/LocalMapping.cc:131-208 (run
-//                                                synchronously after every new keyframe)
+//   LocalMapping::ProcessNewKeyFrame / MapPointCulling  src/LocalMapping.cc:131-208, SearchInNeighbors
+//   (+ ORBmatcher::Fuse, MapPoint::Replace)     src/LocalMapping.cc:458-538, ORBmatcher.cc:1200-1350,
+//                                                MapPoint.cc:111-215
+//   Optimizer::LocalBundleAdjustment             src/Optimizer.cc:3341-3666 (solve: ba_ref.cpp)
+//   LocalMapping::KeyFrameCulling + KeyFrame::SetBadFlag  src/LocalMapping.cc:636-700,
+//                                                KeyFrame.cc:453-567 (all run synchronously after
+//                                                every new keyframe, LocalMapping.cc:61-87)
 // Pinned choices:
 //  * std::map / std::set keyed by KeyFrame* iterate in keyframe creation order (the reference's
 //    order is the heap's);
-//  * LocalMapping runs synchronously and is always idle when Tracking asks (AcceptKeyFrames);
-//    of its steps only ProcessNewKeyFrame (without the BoW conversion) and MapPointCulling run:
-//    CreateNewMapPoints needs the BoW vocabulary (missing), SearchInNeighbors / LocalBundleAdjustment
-//    / KeyFrameCulling are SURVEY 8(f)-3 and out of this row;
+//  * LocalMapping runs synchronously and is always idle when Tracking asks (AcceptKeyFrames):
+//    ProcessNewKeyFrame (without the BoW conversion), MapPointCulling, SearchInNeighbors,
+//    LocalBundleAdjustment (no abort: mbAbortBA stays false) and KeyFrameCulling run to completion
+//    after every new keyframe; CreateNewMapPoints needs SearchForTriangulation, i.e. the BoW
+//    vocabulary (missing), and is skipped;
 //  * TrackReferenceKeyFrame's SearchByBoW (and Relocalization, whose candidates come from the BoW
 //    database) needs the missing vocabulary: both are replaced by SearchByProjection against the
 //    last frame at the last frame's pose (th 15, orientation check), then PoseOptimization and the
@@ -26,13 +32,17 @@
 //  * map points whose unprojection is not finite (depth +inf where the disparity is 0) project to
 //    no pixel (the reference would index the grid with an undefined float -> int conversion).
 #pragma once
+#include <cmath>
 #include <cstdint>
+#include <cstring>
+#include <functional>
 #include <map>
 #include <set>
 #include <vector>
 
 #include "oracle_common.h"
 #include "oracle_match.h"
+#include "oracle_solve.h"
 
 namespace oracle {
 
@@ -60,6 +70,8 @@ struct OMapPoint {
   float minDist = 0, maxDist = 0;
   long trackRefForFrame = 0, lastFrameSeen = 0;
   bool trackInView = false;
+  int replaced = -1;                 // mpReplaced
+  long fuseCandForKF = 0, baLocalForKF = 0;  // mnFuseCandidateForKF, mnBALocalForKF
 };
 
 struct OKeyFrame {
@@ -77,6 +89,8 @@ struct OKeyFrame {
   std::set<int> children;
   long trackRefForFrame = 0;
   bool bad = false;
+  long fuseTargetForKF = 0, baLocalForKF = 0, baFixedForKF = 0;
+  std::vector<std::vector<int>> grid;  // mGrid (the frame's, copied), [ix * kGridRows + iy]
 };
 
 // Map-path fields of one Frame (Frame.h): its keys and descriptors live in OFrame.
@@ -97,6 +111,54 @@ struct MapStats {
   int new_keyframe = 0;
   float Tcw_map[16];        // pose after the map branch (the initial estimate of PoseOptimizationFlow2Cam)
 };
+
+// ------------------------------------------------------------------ pose helpers
+inline void m4_mul(const float* A, const float* B, float* C) {
+  float R[16];
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) {
+      double s = 0;
+      for (int k = 0; k < 4; k++) s += (double)A[4 * r + k] * (double)B[4 * k + c];
+      R[4 * r + c] = (float)s;
+    }
+  memcpy(C, R, sizeof(R));
+}
+
+// Frame::UpdatePoseMatrices / KeyFrame::SetPose: Ow = -Rcw^T tcw
+inline void cam_centre(const float* T, float* Ow) {
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)T[4 * k + 3];
+    Ow[r] = -(float)s;
+  }
+}
+
+// Frame::UnprojectStereo (Frame.cc:1064-1079) / KeyFrame::UnprojectStereo: Rwc * x3Dc + Ow
+inline void unproject(const MapCam& c, const float* T, float u, float v, float z, float* out) {
+  const float x = (u - c.cx) * z * c.invfx;
+  const float y = (v - c.cy) * z * c.invfy;
+  const float xc[3] = {x, y, z};
+  float Ow[3];
+  cam_centre(T, Ow);
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)T[4 * k + r] * (double)xc[k];
+    out[r] = (float)s + Ow[r];
+  }
+}
+
+inline float norm3(const float* v) {
+  double s = 0;
+  for (int k = 0; k < 3; k++) s += (double)v[k] * (double)v[k];
+  return (float)std::sqrt(s);
+}
+
+
+// KeyFrame::GetFeaturesInArea and ORBmatcher::Fuse's per-point search (mapping_ref.cpp)
+std::vector<int> kf_features_in_area(const OKeyFrame& K, const MapCam& cam, float x, float y,
+                                     float r);
+int fuse_candidate(const OKeyFrame& K, const MapCam& cam, const OMapPoint& p, float th,
+                   int* bestIdx);
 
 class MapTracker {
  public:
@@ -130,6 +192,12 @@ class MapTracker {
   std::vector<OMapPoint> temps;  // temporal VO points (handles kTemp + i)
   std::vector<OKeyFrame> kfs;
   static constexpr int kTemp = 1 << 29;
+  // test hook: called with each LocalBundleAdjustment problem and its result (probe fixtures)
+  std::function<void(const BAProblem&, const BAResult&)> ba_hook;
+  struct MappingStats {
+    long n_ba = 0, n_fused = 0, n_culled = 0, n_ba_erased = 0;
+    long ba_trials = 0, ba_edges = 0, ba_kfs = 0, ba_pts = 0, ba_max_opt_kfs = 0;
+  } mstats;
   OMapPoint& mp(int h) { return h >= kTemp ? temps[h - kTemp] : pts[h]; }
 
  private:
@@ -155,6 +223,18 @@ class MapTracker {
                            MapFrame& C, const float* Tcw);
   void process_new_keyframe(int kf);
   void map_point_culling(int kf);
+  // the rest of LocalMapping::Run's iteration (LocalMapping.cc:68-87)
+  void local_mapping(int kf);
+  void search_in_neighbors(int kf);
+  int fuse(int kf, const std::vector<int>& pts, float th);
+  void local_bundle_adjustment(int kf);
+  void keyframe_culling(int kf);
+  void replace(int h, int by);
+  void erase_observation(int h, int kf);
+  void kf_set_bad(int kf);
+  void erase_connection(int kf, int other);
+  void set_pose(int kf, const float* Tcw);
+  std::vector<int> best_covisibles(int kf, int n) const;
   void update_last_frame(const std::vector<Key>& lkeys, const std::vector<uint8_t>& ldesc,
                          MapFrame& L, float* Tlast);
   int new_keyframe(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,

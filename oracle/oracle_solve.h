@@ -41,6 +41,29 @@ struct PoseOptProblem {
 // returns nInitialCorrespondences - nBad (0 and pose untouched below 3 edges); outlier[i] = mvbOutlier
 int pose_optimization(const PoseOptProblem& p, float pose_out[16], uint8_t* outlier);
 
+// Optimizer::LocalBundleAdjustment's solve (Optimizer.cc:3394-3665): keyframe poses (VertexSE3Expmap,
+// fixed or not) and map points (VertexSBAPointXYZ, marginalised) joined by EdgeSE3ProjectXYZ (uR < 0)
+// / EdgeStereoSE3ProjectXYZ edges.  The caller lists the edges point by point, each point's
+// observations in keyframe order (the reference's edge creation order, mono and stereo mixed).
+struct BAProblem {
+  int n_kf = 0, n_pt = 0, n_edge = 0;
+  const float* Tcw = nullptr;        // n_kf x 16 row-major
+  const uint8_t* fixed = nullptr;    // n_kf
+  const float* Xw = nullptr;         // n_pt x 3
+  const int* e_pt = nullptr;         // n_edge
+  const int* e_kf = nullptr;         // n_edge
+  const float* e_obs = nullptr;      // n_edge x (u, v, uR)
+  const float* e_inv_sigma2 = nullptr;  // n_edge: mvInvLevelSigma2[octave]
+  float fx = 0, fy = 0, cx = 0, cy = 0, bf = 0;
+};
+struct BAResult {
+  std::vector<float> Tcw, Xw;   // Converter::toCvMat of every vertex's final estimate
+  std::vector<uint8_t> erase;   // the final inlier check failed (vToErase)
+  int n_erase = 0;
+  int iterations[2] = {0, 0}, trials[2] = {0, 0};  // optimize(5), optimize(10)
+};
+int local_ba_solve(const BAProblem& p, BAResult& out);
+
 float cv_rng_first_gaussian(uint64_t seed);
 float noisy_depth(float z, float g0);
 

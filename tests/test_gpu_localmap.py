@@ -1,0 +1,166 @@
+"""GPU parity of the synchronous LocalMapping steps against the CPU
+oracle:
+  * LocalBundleAdjustment's solve (Optimizer.cc:3394-3631) through mmt_local_bundle_adjustment
+    (one persistent GPU workgroup, csrc/mmt_ba.hip) vs oracle/ba_ref.cpp, on synthetic graphs and
+    on graphs captured from the oracle's own tracking run;
+  * ORBmatcher::Fuse's per-point search (ORBmatcher.cc:1200-1324) through mmt_fuse_candidates
+    (k_fuse_cand) vs oracle/mapping_ref.cpp;
+  * the whole LocalMapping (SearchInNeighbors + Fuse replay, local BA, KeyFrameCulling) inside the
+    tracker over a C3 sequence: per-frame parity and LocalMapping counters equal to the oracle's.
+
+Tolerance: keyframe poses and map points within 1e-4 (max abs entry; the sums run in another
+association than the checker's); erase flags, LM iteration and trial counts, Fuse key indices and
+distances exact."""
+import numpy as np
+import pytest
+
+from ba_problems import BF, ba_problem
+from synth_problems import K_KITTI
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import multimot_track_amd as M
+    c = M.Context(M.kitti03_config(nfeatures=2000, max_batch=8))
+    yield c
+    c.close()
+
+
+def _compare_ba(ctx, oracle_mod, P):
+    To, Xo, eo, so = oracle_mod.local_ba(P, K_KITTI, BF)
+    Tg, Xg, eg, sg = ctx.local_bundle_adjustment(P)
+    assert sg == so, (sg, so)
+    assert np.array_equal(eg, eo), (np.nonzero(eg != eo)[0][:10], eg.sum(), eo.sum())
+    assert np.abs(Tg - To).max() < TOL
+    assert np.abs(Xg - Xo).max() < TOL
+    return so
+
+
+@pytest.mark.parametrize("seed,kw", [
+    (10, dict()),
+    (11, dict(n_kf=10, n_fixed=3, n_pt=2500, obs_per_pt=(1, 6))),
+    (12, dict(n_kf=4, n_fixed=1, n_pt=300, mono_frac=0.6, outlier_frac=0.1)),
+    (13, dict(n_kf=18, n_fixed=4, n_pt=4000, obs_per_pt=(2, 8))),   # 14 optimised: 84 rows (LDS)
+    (14, dict(n_kf=24, n_fixed=2, n_pt=3000, obs_per_pt=(2, 6))),   # 21 optimised: 126 rows (HBM)
+    (15, dict(n_kf=3, n_fixed=3, n_pt=200)),                        # no optimised keyframe
+    (16, dict(n_kf=5, n_fixed=0, kf0_local=False, pose_noise=0.05, pix_noise=1.5)),
+])
+def test_local_ba_matches_oracle(ctx, oracle_mod, seed, kw):
+    P, _, _ = ba_problem(seed, **kw)
+    _compare_ba(ctx, oracle_mod, P)
+
+
+def test_local_ba_empty_and_edgeless(ctx, oracle_mod):
+    P, _, _ = ba_problem(20, n_kf=3, n_fixed=1, n_pt=50)
+    E = dict(P)
+    for k in ("pt", "kf", "s"):
+        E[k] = P[k][:0]
+    E["obs"] = P["obs"][:0]
+    _compare_ba(ctx, oracle_mod, E)
+
+
+def test_local_ba_rejects_unsorted_edges(ctx):
+    import multimot_track_amd as M
+    P, _, _ = ba_problem(21, n_pt=50)
+    P["pt"] = P["pt"][::-1].copy()
+    with pytest.raises(M.MmtError):
+        ctx.local_bundle_adjustment(P)
+
+
+@pytest.fixture(scope="module")
+def c3_seq():
+    import torch
+    from multimot_track_amd import scene
+    return scene.kitti_like_sequence(120, 1242, 375, n_objects=3, seed=1003,
+                                     device=torch.device("cuda:0"))
+
+
+def test_local_ba_on_tracker_graphs(ctx, oracle_mod, c3_seq):
+    """The graphs LocalMapping builds while the oracle tracks the bench's C3 sequence (the 2nd,
+    5th and 9th local BA): the GPU solve agrees with the checker's."""
+    from multimot_track_amd import scene
+    got = 0
+    for which in (1, 4, 8):
+        tr = oracle_mod.Tracker(1242, 375, K_KITTI, BF, 0, 2000)
+        tr.capture_ba(which)
+        for i in range(120):
+            f = scene.to_numpy_frames({k: c3_seq[k][i:i + 1] for k in ("bgr", "disp", "flow", "mask")})[0]
+            tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            P = tr.captured_ba()
+            if P is not None:
+                break
+        assert P is not None
+        st = _compare_ba(ctx, oracle_mod, P)
+        assert len(P["pt"]) > 500 and st["iterations"][0] >= 1
+        got += 1
+    assert got == 3
+
+
+def test_fuse_candidates_match_oracle(ctx, oracle_mod, kitti_frames):
+    """Random map points around the keyframe's keys (positions, normals, scale bounds,
+    descriptors perturbed) against keyframe 0 of kitti_sample: key index and distance bit-exact."""
+    f = kitti_frames[0]
+    gray = oracle_mod.gray_from_bgr(f["bgr"])
+    kps, desc = oracle_mod.orb_extract(gray, 2000)
+    d = f["disp"].astype(np.float64)
+    with np.errstate(divide="ignore"):
+        depth = (BF / (d / 256.0)).astype(np.float32)
+    fx, fy, cx, cy = K_KITTI
+    rng = np.random.default_rng(7)
+    m = 3000
+    sel = rng.integers(0, len(kps), m)
+    u = kps["x"][sel] + rng.normal(scale=2.0, size=m)
+    v = kps["y"][sel] + rng.normal(scale=2.0, size=m)
+    z = rng.uniform(2.0, 60.0, m)
+    X = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    nrm = X / np.linalg.norm(X, axis=1, keepdims=True) + rng.normal(scale=0.3, size=(m, 3))
+    dist = np.linalg.norm(X, axis=1)
+    maxd = dist * 1.2 ** rng.integers(0, 8, m) * rng.uniform(0.7, 1.3, m)
+    mind = maxd / 1.2 ** 7
+    pd = desc[sel].copy()
+    flip = rng.integers(0, 256, size=(m, 4))
+    for b in range(4):
+        pd[np.arange(m), flip[:, b] // 8] ^= (1 << (flip[:, b] % 8)).astype(np.uint8)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = [0.1, -0.05, 0.3]
+    io, do = oracle_mod.fuse_candidates(kps, desc, depth, T, X, nrm, mind, maxd, pd, K_KITTI, BF,
+                                        1242, 375)
+    ig, dg = ctx.fuse_candidates(kps, desc, depth, T, X, nrm, mind, maxd, pd)
+    assert np.array_equal(ig, io) and np.array_equal(dg, do)
+    assert (do <= 50).sum() > 500  # many would fuse
+
+
+def test_tracker_local_mapping_matches_oracle(oracle_mod, c3_seq):
+    """120 frames of the C3 sequence through the bench's entry point (64-frame chunks) with the
+    synchronous LocalMapping on the GPU path: every frame within the bar and the LocalMapping
+    counters (local BAs, fused points, culled keyframes, erased observations) equal to the
+    oracle's."""
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    from oracle import compare
+    n, C = 120, 64
+    seq = c3_seq
+    ctx = M.Context(M.kitti03_config(1242, 375, 2000, max_batch=C))
+    got = []
+    try:
+        for s0 in range(0, n, C):
+            sl = slice(s0, min(n, s0 + C))
+            got += ctx.track_chunk_device(seq["bgr"][sl], seq["disp"][sl], seq["flow"][sl],
+                                          seq["mask"][sl])
+        gc = ctx.map_counters()
+    finally:
+        ctx.close()
+    tr = oracle_mod.Tracker(1242, 375, K_KITTI, BF, 0, 2000)
+    ora = []
+    for i in range(n):
+        f = scene.to_numpy_frames({k: seq[k][i:i + 1] for k in ("bgr", "disp", "flow", "mask")})[0]
+        ora.append(tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]))
+    oc = tr.map_stats()
+    rec = compare.parity_record(got, ora)
+    assert rec["first_divergent_frame"] is None, rec
+    for k in ("n_ba", "n_fused", "n_culled", "n_ba_erased", "ba_trials", "ba_edges", "ba_pts"):
+        assert gc[k] == oc[k], (k, gc[k], oc[k])
+    assert oc["n_ba"] > 5 and oc["n_fused"] > 50

@@ -347,3 +347,53 @@ def test_track_c3_long_sequence_matches_oracle(oracle_mod):
     assert rec["first_divergent_frame"] is None, rec
     assert sum(g["new_keyframe"] for g in got) > 20 and all(g["map_state"] == 1 for g in got)
     assert min(len(g["objects"]) for g in got[1:]) >= 1
+
+
+def test_split_solve_fallback_matches_oracle(oracle_mod, monkeypatch):
+    """The split ego solve needs its workgroups resident together; when an exchange wait exceeds
+    its bound (forced here with a one-tick bound, MMT_DEBUG_SPLIT_SPIN) the solve reports it and the
+    tracker re-runs it on one workgroup: the frames still match the oracle."""
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    from oracle import compare
+    monkeypatch.setenv("MMT_DEBUG_SPLIT_SPIN", "1")
+    monkeypatch.setenv("MMT_LM_SPLIT", "4")
+    seq = scene.kitti_like_sequence(24, 1242, 375, n_objects=0, seed=1003, device="cpu")
+    frames = scene.to_numpy_frames(seq)
+    ctx = M.Context(M.kitti03_config(1242, 375, 2000, max_batch=8))
+    tr = oracle_mod.Tracker(1242, 375, K_KITTI, 387.5744, 0, 2000)
+    try:
+        for i, f in enumerate(frames):
+            g = ctx.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            o = tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            p, c, bad = compare.compare_frame(g, o)[:3]
+            assert not bad and p < POSE_TOL, (i, p, bad)
+        assert ctx.map_counters()["d2_split_fallbacks"] > 5
+    finally:
+        ctx.close()
+
+
+def test_error_mid_chunk_then_track_on():
+    """A frame with a semantic label above 15 fails its chunk (MmtError); the frames of the
+    object pipeline that the failed call left in flight are dropped, and the context tracks the
+    next chunk (no job may keep pointers into the failed call's results)."""
+    import torch
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    dev = torch.device("cuda:0")
+    seq = scene.kitti_like_sequence(24, 1242, 375, n_objects=3, seed=1003, device=dev)
+    ctx = M.Context(M.kitti03_config(1242, 375, 2000, max_batch=12))
+    try:
+        bad = seq["mask"][:12].clone()
+        bad[6][bad[6] > 0] = 20
+        with pytest.raises(M.MmtError):
+            ctx.track_chunk_device(seq["bgr"][:12], seq["disp"][:12], seq["flow"][:12], bad)
+        out = ctx.track_chunk_device(seq["bgr"][12:], seq["disp"][12:], seq["flow"][12:],
+                                     seq["mask"][12:])
+        assert len(out) == 12 and all(np.isfinite(o["Tcw"]).all() for o in out)
+        ctx.reset()
+        out = ctx.track_chunk_device(seq["bgr"][:12], seq["disp"][:12], seq["flow"][:12],
+                                     seq["mask"][:12])
+        assert out[-1]["map_state"] == 1
+    finally:
+        ctx.close()
