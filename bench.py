@@ -9,8 +9,15 @@ host thread each; SURVEY 8(e) allows several sequences per device), seeds 1003 +
 
 A "step" = System::TrackRGBD over one chunk of `--chunk` consecutive frames of the sequence:
 batched ORB extraction for the chunk, then per frame everything the reference does on this path
-(mmt_track_rgbd_chunk_device).  Frames are processed in order, so the tracker state carries
-across steps exactly as in rgbd_mmt.
+(mmt_track_rgbd_chunk_device), including the synchronous LocalMapping of every new keyframe
+(SearchInNeighbors + Fuse, local bundle adjustment, keyframe culling).  Frames are processed in
+order, so the tracker state carries across steps exactly as in rgbd_mmt.  By default the object
+results are deferred (mmt_set_deferred_objects): the object pipeline keeps running across steps
+instead of draining at every chunk boundary, each frame's object motions arrive with a later
+step's results, and the timed region ends with mmt_flush_objects, so every timed frame's objects
+are computed inside it (--immediate: drain at every step).  `one_frame_per_call` times the
+reference-shaped call pattern (one frame per mmt_track_rgbd_chunk_device call, deferred objects)
+on the frames after the timed region.
 
 Multi-GPU: one process per GPU, independent sequences, no data-path collective; barrier + device
 sync bracket the timed region; time = MAX over ranks; value = frames of all ranks / that time
@@ -101,6 +108,11 @@ def parse_args(argv=None):
     ap.add_argument("--c2-steps", type=int, default=3,
                     help="timed steps of the C2 (ego-only) leg (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--immediate", action="store_true",
+                    help="every step returns its frames' own object motions (drains the object "
+                         "pipeline at each chunk boundary)")
+    ap.add_argument("--single-frames", type=int, default=256,
+                    help="frames of the one-frame-per-call leg (0: skip)")
     ap.add_argument("--dry", action="store_true", help="CPU rehearsal of the rank logic")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args(argv)
@@ -133,6 +145,22 @@ def frames_from_raw(raw, C):
     res, objs = raw
     mo = M.MAX_OBJECTS
     return [M._frame_dict(res[i], objs[i * mo:(i + 1) * mo]) for i in range(C)]
+
+
+def assemble(raws, C, flushed=()):
+    """Per-frame dicts in frame order with each frame's own object motions: results of deferred
+    calls carry the objects of an earlier frame (objects_frame), the flush the rest."""
+    frames, objs = [], {}
+    for raw in raws:
+        for d in frames_from_raw(raw, C):
+            frames.append(d)
+            if d["objects_frame"] >= 0:
+                objs[d["objects_frame"]] = d["objects"]
+    for f, o in flushed:
+        objs[f] = o
+    for d in frames:
+        d["objects"] = objs.get(d["frame_index"], [])
+    return frames
 
 
 def seq_frame_numpy(seq, i):
@@ -308,6 +336,9 @@ def main(argv=None):
     cfg = M.kitti03_config(W, H, NF, max_batch=C, device_id=local)
     ctxs = [M.Context(cfg) for _ in range(K)]
     ctx = ctxs[0]
+    if not args.immediate:
+        for c in ctxs:
+            c.set_deferred_objects(True)
     lv = ctx.levels()
     # dedicated (non-default) streams: the library launches on them and records its HIP events
     # on them; torch.cuda.synchronize below waits for all of them
@@ -338,6 +369,12 @@ def main(argv=None):
     shard.barrier(world, dev)
     t0 = time.perf_counter()
     results = [step(args.warmup + i) for i in range(args.steps)]
+    flushed = []
+    if not args.immediate:  # the timed frames' last object motions, inside the timed region
+        if pool is None:
+            flushed = ctx.flush_objects()
+        else:
+            flushed = [f.result() for f in [pool.submit(c.flush_objects) for c in ctxs]][0]
     torch.cuda.synchronize(dev)
     shard.barrier(world, dev)
     elapsed = time.perf_counter() - t0
@@ -346,11 +383,19 @@ def main(argv=None):
     frames_all = shard.sum_over_ranks(args.steps * C * K, world, dev)
 
     # per-frame outputs of the timed region (sanity: every frame tracked, objects found)
-    res, objs = results[-1]
-    n_obj_last = int(res[C - 1].n_objects)
-    tracked = sum(int(res_[f].initialized) for res_, _ in results for f in range(C))
+    all_frames = assemble(warm + results, C, flushed)
+    timed_frames = all_frames[args.warmup * C:]
+    n_obj_last = len(timed_frames[-1]["objects"])
+    tracked = sum(int(d["initialized"]) for d in timed_frames)
     gt = seq["Tcw"][-1]
-    ego_err = float(np.abs(np.array(res[C - 1].Tcw[:]).reshape(4, 4) - gt).max())
+    ego_err = float(np.abs(timed_frames[-1]["Tcw"] - gt).max())
+    mc = ctx.map_counters()
+    local_mapping = {k: int(mc[k]) for k in ("n_ba", "n_fused", "n_culled", "n_ba_erased",
+                                             "ba_trials", "ba_edges", "ba_pts", "ba_max_opt",
+                                             "fuse_launches", "fuse_queries", "fuse_relaunches",
+                                             "d2_split_fallbacks")}
+    local_mapping["keyframes_last_frame"] = int(timed_frames[-1]["n_keyframes"])
+    local_mapping["mappoints_last_frame"] = int(timed_frames[-1]["n_mappoints"])
 
     if rank == 0:
         value = frames_all / elapsed
@@ -359,7 +404,34 @@ def main(argv=None):
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         key = "%dx%d_n%d_b%d" % (W, H, NF, C)
         traffic = load_traffic(args.traffic_file, key)
-        cpu, parity, c2 = None, None, None
+        cpu, parity, c2, single = None, None, None, None
+        if world == 1 and args.single_frames > 0:
+            # the reference-shaped call pattern: one frame per call (rgbd_tum.cc's loop), objects
+            # deferred; a fresh sequence context over the frames after the timed region
+            ns = args.single_frames
+            s1 = render(shard.sequence_seed(1003, 0), ns + 8)
+            sctx = M.Context(M.kitti03_config(W, H, NF, max_batch=8, device_id=local))
+            sctx.set_deferred_objects(True)
+            for i in range(8):  # initialisation and warm-up
+                sctx.track_chunk_device(s1["bgr"][i:i + 1], s1["disp"][i:i + 1],
+                                        s1["flow"][i:i + 1], s1["mask"][i:i + 1],
+                                        streams[0].cuda_stream, parse=False)
+            torch.cuda.synchronize(dev)
+            ts = time.perf_counter()
+            for i in range(8, 8 + ns):
+                sctx.track_chunk_device(s1["bgr"][i:i + 1], s1["disp"][i:i + 1],
+                                        s1["flow"][i:i + 1], s1["mask"][i:i + 1],
+                                        streams[0].cuda_stream, parse=False)
+            sctx.flush_objects()
+            torch.cuda.synchronize(dev)
+            ts = time.perf_counter() - ts
+            single = {"value": round(ns / ts, 2), "unit": "frames/s",
+                      "ms_per_frame": round(ts / ns * 1e3, 4), "frames": ns,
+                      "sample": "frames 8-%d of the C3 sequence, one frame per "
+                                "mmt_track_rgbd_chunk_device call, deferred object results, "
+                                "flush inside the timed region" % (7 + ns)}
+            sctx.close()
+            del s1
         if world == 1 and args.c2_steps > 0:
             # C2 (ego only): same camera and sequence seed, mask == 0
             nc2 = (1 + args.c2_steps) * C
@@ -376,9 +448,7 @@ def main(argv=None):
                   "frames": args.c2_steps * C, "timed_from": C}
             c2ctx.close()
         if world == 1 and not args.no_cpu:
-            gpu_frames = []
-            for raw in warm + results:
-                gpu_frames.extend(frames_from_raw(raw, C))
+            gpu_frames = all_frames
             timed_from = args.warmup * C
             n_t, t_t, parity = cpu_leg(args, seq, gpu_frames, timed_from, W, H, NF)
             fps1 = n_t / t_t if t_t > 0 else 0.0
@@ -418,7 +488,9 @@ def main(argv=None):
                        "sequences_per_gpu": K, "parallelism": "dp%d" % world,
                        "frames_tracked": tracked, "objects_last_frame": n_obj_last,
                        "ego_abs_err_last_frame": round(ego_err, 5),
-                       "scene_render_s": round(t_gen, 2), "c2": c2},
+                       "scene_render_s": round(t_gen, 2), "c2": c2,
+                       "object_results": "immediate" if args.immediate else "deferred",
+                       "local_mapping": local_mapping, "one_frame_per_call": single},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,

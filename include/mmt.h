@@ -59,6 +59,11 @@ extern "C" {
 #define MMT_EDEVICE (-5)
 #define MMT_ESTATE (-77)
 
+/* Most object motions a frame reports (semantic labels 1..15).  mmt_frame_result.n_objects is
+ * the frame's full count; an objs_cap below it receives the first objs_cap motions only, so size
+ * the motion arrays with MMT_MAX_OBJECTS per frame. */
+#define MMT_MAX_OBJECTS 15
+
 /* Settings of kitti03.yaml (Camera.*, ThDepth, ORBextractor.*) plus build-side knobs. */
 typedef struct mmt_config {
   int width, height;              /* Camera.width / Camera.height                       */
@@ -101,7 +106,8 @@ typedef struct mmt_motion {
   float centre_pre[3];      /* ObjCentre3D_pre (Tracking.cc:2032-2049): mean world point of
                                the solve's last-frame samples, noisy depth (UnprojectStereoObject
                                (j, 1)); the object-speed estimate of Tracking.cc:2186 uses it.
-                               0 when the solve had fewer than 3 correspondences          */
+                               The reference computes it before the solve whatever the count:
+                               1-2 samples give their mean, none gives NaN (0 * (1 / 0))   */
 } mmt_motion;
 
 /* Per-frame tracking result (the Tcw cv::Mat returned by System::TrackRGBD + counters). */
@@ -122,6 +128,10 @@ typedef struct mmt_frame_result {
   int32_t new_keyframe;     /* this frame became a keyframe                              */
   float Tcw_map[16];        /* row-major pose of the map branch (PoseOptimization's output,
                                the initial estimate of PoseOptimizationFlow2Cam)        */
+  int32_t frame_index;      /* this frame's index in the sequence (frames since the reset) */
+  int32_t objects_frame;    /* the frame whose object motions n_objects / objs describe: this
+                               frame, or with deferred object results an earlier one (-1:
+                               none in this slot)                                        */
 } mmt_frame_result;
 
 typedef struct mmt_ctx mmt_ctx;
@@ -440,6 +450,21 @@ int mmt_profile_read(mmt_ctx* ctx, mmt_profile* out, int reset);
 
 /* Forget the sequence (Tracking::Reset). */
 int mmt_reset(mmt_ctx* ctx);
+
+/* Deferred object results (no reference counterpart; for callers that track one frame, or one
+ * short chunk, per call).  By default every mmt_track_rgbd* call returns each frame with its own
+ * object motions, which drains the object pipeline (PnP-RANSAC, PoseOptimizationFlow2 per object)
+ * at the end of every call.  With on = 1 a call returns each frame's pose and map state at once,
+ * and in the object fields of its results the motions of the frames whose object path has
+ * finished, oldest first (res[i].objects_frame names the frame; -1: none yet): every frame's
+ * motions arrive exactly once, in order, up to 17 frames later.  mmt_flush_objects finishes the
+ * pipeline and returns the remaining records (res[k].objects_frame, n_objects and objs[k *
+ * objs_cap ..] only), at most res_cap per call: *n = records written, 0 when none remain.
+ * Turning the mode off flushes (and drops) the records still owed; mmt_reset drops them.
+ * MMT_EINVAL when the host object worker (MMT_OBJ_THREAD=1) is on. */
+int mmt_set_deferred_objects(mmt_ctx* ctx, int on);
+int mmt_flush_objects(mmt_ctx* ctx, mmt_frame_result* res, mmt_motion* objs, int objs_cap,
+                      int res_cap, int* n);
 
 /* Upper bound on keypoints per frame (sum over levels of quota + 3). */
 int mmt_orb_capacity(const mmt_ctx* ctx);

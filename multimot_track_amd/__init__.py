@@ -50,7 +50,8 @@ class MmtFrameResult(ctypes.Structure):
                 ("n_objects", ctypes.c_int32), ("map_state", ctypes.c_int32),
                 ("map_matches_mm", ctypes.c_int32), ("map_inliers_local", ctypes.c_int32),
                 ("n_keyframes", ctypes.c_int32), ("n_mappoints", ctypes.c_int32),
-                ("new_keyframe", ctypes.c_int32), ("Tcw_map", ctypes.c_float * 16)]
+                ("new_keyframe", ctypes.c_int32), ("Tcw_map", ctypes.c_float * 16),
+                ("frame_index", ctypes.c_int32), ("objects_frame", ctypes.c_int32)]
 
 
 class MmtFlowProblem(ctypes.Structure):
@@ -140,7 +141,8 @@ def _frame_dict(r, objs):
                 ego_inliers=r.ego_inliers, objects=out, map_state=r.map_state,
                 map_matches_mm=r.map_matches_mm, map_inliers_local=r.map_inliers_local,
                 n_keyframes=r.n_keyframes, n_mappoints=r.n_mappoints,
-                new_keyframe=r.new_keyframe, Tcw_map=_mat(r.Tcw_map))
+                new_keyframe=r.new_keyframe, Tcw_map=_mat(r.Tcw_map),
+                frame_index=r.frame_index, objects_frame=r.objects_frame)
 
 
 class MmtError(RuntimeError):
@@ -541,6 +543,27 @@ class Context:
         return To[:nk], Xo[:npt], er[:ne], dict(iterations=(int(st[0]), int(st[1])),
                                                  trials=(int(st[2]), int(st[3])),
                                                  n_erase=int(st[4]))
+
+    def set_deferred_objects(self, on=True):
+        """mmt_set_deferred_objects: frames return at once, object motions when they are ready
+        (each result's objects / objects_frame)."""
+        self._check(lib().mmt_set_deferred_objects(self._h, 1 if on else 0))
+
+    def flush_objects(self):
+        """mmt_flush_objects until empty: [(objects_frame, objects)] in frame order."""
+        out = []
+        cap = 32
+        while True:
+            res = (MmtFrameResult * cap)()
+            objs = (MmtMotion * (cap * MAX_OBJECTS))()
+            n = ctypes.c_int(0)
+            self._check(lib().mmt_flush_objects(self._h, res, objs, MAX_OBJECTS, cap,
+                                                ctypes.byref(n)))
+            if n.value == 0:
+                return out
+            for i in range(n.value):
+                d = _frame_dict(res[i], objs[i * MAX_OBJECTS:(i + 1) * MAX_OBJECTS])
+                out.append((d["objects_frame"], d["objects"]))
 
     def map_counters(self):
         """LocalMapping counters of the context's tracker (mmt_map_counters_read)."""

@@ -281,12 +281,13 @@ __global__ __launch_bounds__(kBAThreads) void k_local_ba(BADesc d) {
     w.level[e] = 0;
     w.err[3 * (size_t)e] = w.err[3 * (size_t)e + 1] = w.err[3 * (size_t)e + 2] = 0;
   }
-  for (int q = tid; q < n6 + 3 * d.n_pt; q += kBAThreads) w.x[q] = 0;
   __syncthreads();
 
   for (int round = 0; round < 2; round++) {
     const bool robust = round == 0;
     const int iters = round == 0 ? 5 : 10;
+    // the solver's x starts at zero in each round (a failed first solve re-applies it)
+    for (int q = tid; q < n6 + 3 * d.n_pt; q += kBAThreads) w.x[q] = 0;
     if (round == 1) {
       // check inlier observations (Optimizer.cc:3559-3590): the last computed error, the current
       // depth; every kernel dropped

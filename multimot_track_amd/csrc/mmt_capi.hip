@@ -334,6 +334,8 @@ static void fill_results(const std::vector<mmt::FrameOut>& outs, mmt_frame_resul
     r.n_mappoints = o.map.n_mappoints;
     r.new_keyframe = o.map.new_keyframe;
     memcpy(r.Tcw_map, o.map.Tcw_map, sizeof(r.Tcw_map));
+    r.frame_index = (int32_t)o.seq;
+    r.objects_frame = (int32_t)o.obj_seq;
     if (!objs) continue;
     for (int i = 0; i < (int)o.objects.size() && i < objs_cap; i++) {
       const mmt::ObjOut& s = o.objects[i];
@@ -379,6 +381,41 @@ int mmt_reset(mmt_ctx* ctx) {
   return guard(ctx, [&] {
     ensure_tracker(ctx);
     ctx->tracker.reset();
+    ctx->flushed.clear();
+  });
+}
+
+int mmt_set_deferred_objects(mmt_ctx* ctx, int on) {
+  if (!ctx) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ensure_tracker(ctx);
+    ctx->tracker.set_deferred(on != 0);
+    if (!on) ctx->flushed.clear();
+  });
+}
+
+int mmt_flush_objects(mmt_ctx* ctx, mmt_frame_result* res, mmt_motion* objs, int objs_cap,
+                      int res_cap, int* n) {
+  if (!ctx || !res || !n || res_cap < 1 || objs_cap < 0) return MMT_EINVAL;
+  *n = 0;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ensure_tracker(ctx);
+    if (ctx->flushed.empty()) {
+      std::vector<mmt::FrameOut> outs;
+      ctx->tracker.flush_deferred(outs);
+      for (auto& o : outs) ctx->flushed.push_back(std::move(o));
+    }
+    std::vector<mmt::FrameOut> part;
+    while (!ctx->flushed.empty() && (int)part.size() < res_cap) {
+      part.push_back(std::move(ctx->flushed.front()));
+      ctx->flushed.pop_front();
+    }
+    for (auto& o : part) o.seq = -1;  // flush records carry objects only
+    memset(res, 0, sizeof(mmt_frame_result) * (size_t)part.size());
+    fill_results(part, res, objs, objs_cap);
+    *n = (int)part.size();
   });
 }
 

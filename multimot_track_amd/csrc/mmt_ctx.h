@@ -1,5 +1,7 @@
 // multimot_track_amd/csrc/mmt_ctx.h -- the opaque mmt_ctx behind include/mmt.h.
 #pragma once
+#include <deque>
+
 #include "mmt_internal.h"
 #include "mmt_tracker.h"
 
@@ -24,4 +26,5 @@ struct mmt_ctx {
   float* t_flow = nullptr;
   int32_t* t_mask = nullptr;
   int t_frames = 0;  // frames the t_* staging buffers hold
+  std::deque<mmt::FrameOut> flushed;  // mmt_flush_objects records not yet handed out
 };

@@ -503,6 +503,8 @@ void MapEngine::local_mapping(int kf) {
   search_in_neighbors(kf);
   if (n_keyframes() > 2) local_bundle_adjustment(kf);
   keyframe_culling(kf);
+  // the keyframe-store copies read the chunk's frame buffers: done before the next chunk's ORB
+  MMT_HIP(hipStreamSynchronize(lm_s_));
   if (prof_on_) mstats_.lm_us += now_us() - t0;
 }
 

@@ -35,6 +35,10 @@ struct FrameOut {
   int n_keys = 0, n_obj_samples = 0, ego_iterations = 0, ego_inliers = 0;
   std::vector<ObjOut> objects;
   MapStatsH map;
+  long seq = -1;        // the frame's index in the sequence (frames tracked since the reset)
+  long obj_seq = -1;    // the frame whose object motions `objects` holds (deferred mode: an
+                        // earlier one, or -1 for none); = seq otherwise
+  bool obj_pending = false;  // deferred record: the frame's object path has not finished yet
 };
 
 float rng_first_gaussian(uint64_t seed);
@@ -62,6 +66,13 @@ class Tracker {
   ~Tracker();
   void setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk);
   void reset();
+  // Deferred object results: a call returns every frame's ego pose and map state, and the object
+  // motions of the frames whose object path has finished, oldest first (FrameOut::obj_seq), so the
+  // object pipeline keeps running across calls instead of draining at the end of each.
+  // flush_deferred finishes the pipeline and returns the remaining records.
+  void set_deferred(bool on);
+  bool deferred() const { return defer_; }
+  void flush_deferred(std::vector<FrameOut>& outs);
   // Frames of one sequence, device-resident, processed in order (ORB batched over the chunk).
   void track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t* d_disp,
                    size_t disp_pitch, const float* d_flow, size_t flow_pitch,
@@ -208,6 +219,10 @@ class Tracker {
   float ego_Tinit_[16];
   EgoHost* eh_ = nullptr;
   ObjFrame qa_;                  // ego done, object path not yet enqueued
+  bool defer_ = false;
+  long frame_seq_ = 0;           // frames tracked since the reset
+  std::deque<FrameOut> dq_;      // deferred object records, frame order (stable addresses)
+  void deliver_deferred(std::vector<FrameOut>& outs, bool all);
   std::deque<ObjFrame> inflight_;  // object path enqueued, results not yet read
   int obj_slot_next_ = 0;
   // Pinned host side of the object path, one per object slot: every host<->device transfer of the

@@ -552,6 +552,8 @@ void Tracker::reset() {
     inflight_.clear();
   }
   obj_slot_next_ = 0;
+  dq_.clear();
+  frame_seq_ = 0;
   for (FrameSlot& F : slot_) {
     F.nModLabel.clear();
     F.nSemPosition.clear();
@@ -671,13 +673,53 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
       inflight_.clear();
     }
     qa_ = ObjFrame();
+    dq_.clear();  // deferred records of frames whose pipeline was dropped
     throw;
   }
-  // the chunk's results are complete on return
+  // the chunk's results are complete on return (deferred mode: the finished object records)
   if (ow_on_)
     obj_drain(false);
-  else
+  else if (!defer_)
     obj_flush();
+  if (defer_) {
+    deliver_deferred(outs, false);
+  } else {
+    for (FrameOut& o : outs) o.obj_seq = o.seq;
+  }
+}
+
+void Tracker::set_deferred(bool on) {
+  if (on && ow_on_) throw ArgError("deferred object results need the inline object path (MMT_OBJ_THREAD=0)");
+  if (on == defer_) return;
+  if (!on) {  // results still owed are lost to a caller who turns the mode off: finish them first
+    std::vector<FrameOut> drop;
+    flush_deferred(drop);
+  }
+  defer_ = on;
+}
+
+// the finished records, oldest first, one per output slot (all: every record, the pipeline
+// having been flushed)
+void Tracker::deliver_deferred(std::vector<FrameOut>& outs, bool all) {
+  size_t f = 0;
+  while (!dq_.empty() && !dq_.front().obj_pending && (all || f < outs.size())) {
+    if (f == outs.size()) outs.emplace_back();
+    outs[f].objects = std::move(dq_.front().objects);
+    outs[f].obj_seq = dq_.front().seq;
+    dq_.pop_front();
+    f++;
+  }
+  for (; f < outs.size(); f++) {
+    outs[f].objects.clear();
+    outs[f].obj_seq = -1;
+  }
+}
+
+void Tracker::flush_deferred(std::vector<FrameOut>& outs) {
+  outs.clear();
+  if (!defer_) return;
+  obj_flush();
+  deliver_deferred(outs, true);
 }
 
 // Enqueue the queued frame's whole object path (stage A's host decisions need one wait for the
@@ -732,6 +774,7 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   FrameSlot& C = slot_[cur_];
   FrameSlot& Ls = slot_[last_];
   out = FrameOut();
+  out.seq = frame_seq_++;
   out.n_keys = a.n_keys;
   // ---- the Frame's map fields (Frame ctor: mnId, B3 arrays, empty mvpMapPoints)
   {
@@ -849,6 +892,10 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
   FrameSlot& C = slot_[cur_];
   FrameSlot& Ls = slot_[last_];
   MMT_HIP(hipStreamSynchronize(st));
+  if (defer_) {  // every frame's object record, in frame order (finished at once without a job)
+    dq_.emplace_back();
+    dq_.back().seq = out.seq;
+  }
   out.n_obj_samples = eh_->nlast_obj;
   bool advance = true;
   if (reset_pending_) {
@@ -911,7 +958,8 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
     qa_.cur = cur_;
     qa_.last = last_;
     qa_.nobj = eh_->nlast_obj > 0 ? -1 : 0;  // -1: grouping decides
-    qa_.out = &out;
+    qa_.out = defer_ ? &dq_.back() : &out;
+    qa_.out->obj_pending = true;
   }
   ego_pending_ = false;
   if (advance) {
@@ -1140,6 +1188,7 @@ void Tracker::obj_finish(ObjFrame& F) {
   const int nobj = F.nobj, q = F.slot;
   FrameOut& out = *F.out;
   F.active = false;
+  out.obj_pending = false;
   if (nobj <= 0) return;
   MMT_HIP(hipEventSynchronize(ev_d3_[q]));
   const ObjHost& H = *oh_[q];

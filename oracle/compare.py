@@ -21,28 +21,32 @@ MAP_INT = ("map_state", "map_matches_mm", "map_inliers_local", "n_keyframes", "n
            "new_keyframe")
 
 
-def pose_diff(a, b):
+def pose_diff(a, b, counts=None):
     """(max abs diff, max diff in float32 ulps of the oracle entry over the entries at or above
     POSE_TOL (0 when none is), max diff over the entries that fail both POSE_TOL and POSE_ULPS)
-    of two 4x4 float32 poses."""
+    of two 4x4 float32 poses.  counts (optional dict): "entries" += 16, "ulp_only" += the entries
+    that pass only by the ulp clause (at or above POSE_TOL, within POSE_ULPS ulps)."""
     a = np.asarray(a, np.float32)
     b = np.asarray(b, np.float32)
     d = np.abs(a.astype(np.float64) - b.astype(np.float64))
     ulps = d / np.spacing(np.abs(b)).astype(np.float64)
     big = d >= POSE_TOL
     fail = big & (ulps > POSE_ULPS)
+    if counts is not None:
+        counts["entries"] = counts.get("entries", 0) + d.size
+        counts["ulp_only"] = counts.get("ulp_only", 0) + int((big & ~fail).sum())
     return (float(d.max()), float(ulps[big].max()) if big.any() else 0.0,
             float(d[fail].max()) if fail.any() else 0.0)
 
 
-def compare_frame(g, o):
+def compare_frame(g, o, counts=None):
     """(max pose diff, max centre diff, [integer mismatch descriptions], max pose diff in ulps,
-    max diff of entries failing both bars) of one frame."""
+    max diff of entries failing both bars) of one frame; counts as in pose_diff."""
     bad = []
     for k in FRAME_INT + MAP_INT:
         if k in g and k in o and int(g[k]) != int(o[k]):
             bad.append("%s %r != %r" % (k, g[k], o[k]))
-    pose, ulps, over = pose_diff(g["Tcw"], o["Tcw"])
+    pose, ulps, over = pose_diff(g["Tcw"], o["Tcw"], counts)
     pairs = []
     if "Tcw_map" in g and "Tcw_map" in o:
         pairs.append((g["Tcw_map"], o["Tcw_map"]))
@@ -61,7 +65,7 @@ def compare_frame(g, o):
         elif not np.isnan(ca).all():
             centre = max(centre, float(np.nanmax(np.abs(ca - cb))))
     for a, b in pairs:
-        p, u, v = pose_diff(a, b)
+        p, u, v = pose_diff(a, b, counts)
         pose, ulps, over = max(pose, p), max(ulps, u), max(over, v)
     return pose, centre, bad, ulps, over
 
@@ -74,8 +78,9 @@ def parity_record(gpu_frames, oracle_frames, first_frame=0):
     nbad = 0
     first = None
     why = None
+    counts = {"entries": 0, "ulp_only": 0}
     for i in range(n):
-        p, c, bad, u, over = compare_frame(gpu_frames[i], oracle_frames[i])
+        p, c, bad, u, over = compare_frame(gpu_frames[i], oracle_frames[i], counts)
         max_pose = max(max_pose, p)
         max_centre = max(max_centre, c)
         max_ulps = max(max_ulps, u)
@@ -89,4 +94,5 @@ def parity_record(gpu_frames, oracle_frames, first_frame=0):
             "max_pose_diff_ulps": max_ulps, "max_centre_diff": max_centre,
             "int_mismatch_frames": nbad, "first_divergent_frame": first,
             "first_divergence": why, "pose_tol": POSE_TOL, "pose_tol_ulps": POSE_ULPS,
+            "pose_entries": counts["entries"], "pose_entries_ulp_only": counts["ulp_only"],
             "centre_tol": CENTRE_TOL}
