@@ -8,11 +8,15 @@
 //
 //   rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence [--realtime] [--nfeatures N]
 //            [--device D] [--noise-seed S] [--poses out.txt] [--chunk F] [--threads T]
+//            [--deferred-objects]
 //
 // Input decoding (PNG, .flo, text masks) runs on T host threads (default: up to 16) into pinned
 // buffers from mmt_host_alloc, ahead of the tracker, and frames go to the GPU F at a time through
 // mmt_track_rgbd_chunk (batched ORB; default F = 16, --chunk 1 tracks frame by frame, as
 // --realtime does).  The tracking-time statistics then give each frame its chunk's time / F.
+// --deferred-objects (mmt_set_deferred_objects) keeps the object pipeline running across calls:
+// each frame's camera lines print at once and its object lines when its motions are ready
+// ("Objects of Frame: n", up to 17 frames later; the rest after the last frame).
 //
 // Differences from the reference binary: the vocabulary is not read (this path
 // never uses BoW); no viewer, no imshow/waitKey; the usleep pacing to the timestamps is off
@@ -177,6 +181,7 @@ bool exists(const std::string& p) {
 int main(int argc, char** argv) {
   std::vector<std::string> pos;
   bool realtime = false;
+  bool deferred = false;
   int nfeat = -1, device = 0;
   unsigned seed = 0;
   std::string poses_out;
@@ -185,6 +190,7 @@ int main(int argc, char** argv) {
   for (int i = 1; i < argc; i++) {
     const std::string a = argv[i];
     if (a == "--realtime") realtime = true;
+    else if (a == "--deferred-objects") deferred = true;
     else if (a == "--nfeatures" && i + 1 < argc) nfeat = atoi(argv[++i]);
     else if (a == "--device" && i + 1 < argc) device = atoi(argv[++i]);
     else if (a == "--noise-seed" && i + 1 < argc) seed = (unsigned)strtoul(argv[++i], nullptr, 10);
@@ -196,7 +202,7 @@ int main(int argc, char** argv) {
   if (pos.size() != 3) {
     fprintf(stderr, "\nUsage: ./rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence "
                     "[--realtime] [--nfeatures N] [--device D] [--noise-seed S] [--poses file] "
-                    "[--chunk F] [--threads T]\n");
+                    "[--chunk F] [--threads T] [--deferred-objects]\n");
     return 1;
   }
   const std::string settings = pos[1], seq = pos[2];
@@ -371,6 +377,25 @@ int main(int argc, char** argv) {
   float lastTcw[16], lastGt[16];
   bool haveLast = false;
 
+  // the object lines of frame r.objects_frame (this frame's own unless deferred)
+  auto print_objects = [&](const mmt_frame_result& r, const mmt_motion* mo, bool tag) {
+    const int of = r.objects_frame;
+    if (of < 0) return;
+    if (tag) printf("Objects of Frame: %d\n", of);
+    const float* Tgt = (of < ngt) ? gt + 16 * of : nullptr;
+    const float* Tlw_gt = (of > 0 && of - 1 < ngt) ? gt + 16 * (of - 1) : nullptr;
+    for (int o = 0; o < r.n_objects && o < 64; o++) {
+      const mmt_motion& m = mo[o];
+      printf("object %d (semantic label %d): %d points, %d RANSAC inliers, %d inliers; motion t = "
+             "[%.4f %.4f %.4f]\n", m.label, m.sem_label, m.n_points, m.n_ransac_inliers,
+             m.n_inliers, m.world_motion[3], m.world_motion[7], m.world_motion[11]);
+      if (of > 0) print_object_eval(m, Tlw_gt, Tgt, obj_rows[of - 1], obj_rows[of]);
+    }
+  };
+  if (deferred && mmt_set_deferred_objects(ctx, 1) != 0) {
+    fprintf(stderr, "mmt_set_deferred_objects failed: %s\n", mmt_last_error(ctx));
+    return 1;
+  }
   printf("\n-------\nStart processing sequence ...\nImages in the sequence: %d\n\n", nImages);
   int rc_all = 0;
   int done = 0;
@@ -419,15 +444,7 @@ int main(int argc, char** argv) {
       track_times[ni] = (float)ttrack;
       const float* Tgt = (ni < ngt) ? gt + 16 * ni : nullptr;
       if (haveLast && r.initialized && Tgt) print_camera_rpe(r.Tcw, lastTcw, Tgt, lastGt);
-      const float* Tlw_gt = (ni > 0 && ni - 1 < ngt) ? gt + 16 * (ni - 1) : nullptr;
-      for (int o = 0; o < r.n_objects && o < 64; o++) {
-        const mmt_motion& m = objs[64 * k + o];
-        printf("object %d (semantic label %d): %d points, %d RANSAC inliers, %d inliers; motion t = "
-               "[%.4f %.4f %.4f]\n", m.label, m.sem_label, m.n_points, m.n_ransac_inliers,
-               m.n_inliers, m.world_motion[3], m.world_motion[7], m.world_motion[11]);
-        if (ni > 0)
-          print_object_eval(m, Tlw_gt, Tgt, obj_rows[ni - 1], obj_rows[ni]);
-      }
+      print_objects(r, objs.data() + 64 * k, deferred);
       if (fp) {
         fprintf(fp, "%d", ni);
         for (int q = 0; q < 16; q++) fprintf(fp, " %.9f", r.Tcw[q]);
@@ -463,6 +480,18 @@ int main(int argc, char** argv) {
       consumed = done;
     }
     cv.notify_all();
+  }
+  if (deferred && rc_all == 0) {  // the object motions still owed
+    for (;;) {
+      int n = 0;
+      if (mmt_flush_objects(ctx, res.data(), objs.data(), 64, (int)res.size(), &n) != 0) {
+        fprintf(stderr, "mmt_flush_objects failed: %s\n", mmt_last_error(ctx));
+        rc_all = 1;
+        break;
+      }
+      if (n == 0) break;
+      for (int k = 0; k < n; k++) print_objects(res[k], objs.data() + 64 * k, true);
+    }
   }
   const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
   {

@@ -208,8 +208,61 @@ def test_track_synthetic_c2_ego_only_matches_oracle(oracle_mod):
 
 
 def test_track_synthetic_c5_1080p_matches_oracle(oracle_mod):
-    """BASELINE C5 geometry: 1920x1080, 8000 features, 8 moving boxes."""
+    """BASELINE C5 geometry: 1920x1080, 8000 features, 8 moving boxes.  Eight car-sized boxes
+    in the scene's 15 m street occlude each other and the B7 filters (fewer than 100 samples,
+    beyond 25 m) drop some; test_track_c5_eight_motions_long_matches_oracle below tracks eight
+    object motions in every frame."""
     assert _synthetic_parity(1920, 1080, 8000, 8, 4, 2000) >= 4
+
+
+def _long_parity(oracle_mod, w, h, nfeat, n, seed, objects, lanes=None, parts=1, chunk=32):
+    """n frames through the bench's entry point (chunks of `chunk` frames) against the oracle
+    frame by frame; objects split into `parts` rigid column bands (split_labels)."""
+    import torch
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    from oracle import compare
+    seq = scene.kitti_like_sequence(n, w, h, n_objects=objects, seed=seed, device="cuda:0",
+                                    lanes=lanes)
+    frames = scene.to_numpy_frames(seq)
+    if parts > 1:
+        for f in frames:
+            f["sem"] = split_labels(f["sem"], parts)
+    dev = torch.device("cuda:0")
+    T = lambda k: torch.from_numpy(np.stack([f[k] for f in frames]))  # noqa: E731
+    bgr, disp = T("bgr").to(dev), T("disp").view(torch.int16).to(dev)
+    flow, mask = T("flow").to(dev), T("sem").to(dev)
+    ctx = M.Context(M.kitti03_config(w, h, nfeat, max_batch=chunk))
+    got = []
+    try:
+        for s0 in range(0, n, chunk):
+            sl = slice(s0, min(n, s0 + chunk))
+            got += ctx.track_chunk_device(bgr[sl], disp[sl], flow[sl], mask[sl])
+    finally:
+        ctx.close()
+    tr = oracle_mod.Tracker(w, h, K_KITTI, 387.5744, 0, nfeat)
+    ora = [tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]) for f in frames]
+    rec = compare.parity_record(got, ora)
+    assert rec["first_divergent_frame"] is None, rec
+    return got, rec
+
+
+def test_track_c5_eight_motions_long_matches_oracle(oracle_mod):
+    """C5's eight object motions at 1920x1080 with 8000 features over 100 frames: two boxes,
+    each split into four rigid column bands with labels of their own (eight rigid moving
+    objects), every one solved in every tracked frame and every frame within the bar."""
+    got, rec = _long_parity(oracle_mod, 1920, 1080, 8000, 100, 2000, 2,
+                            lanes=[(-3.0, 12.0), (3.4, 9.0)], parts=4)
+    assert all(len(g["objects"]) == 8 for g in got[1:])
+    assert rec["frames"] == 100
+
+
+@pytest.mark.parametrize("w,h,seed", [(1241, 376, 1000), (1226, 370, 1005)])
+def test_track_c4_sizes_long_matches_oracle(oracle_mod, w, h, seed):
+    """BASELINE C4 geometries (KITTI 00 at 1241x376, 05/07 at 1226x370), 4000 features, ego + 3
+    moving boxes, over 100 frames (keyframes, local BA, fusion and culling included)."""
+    got, rec = _long_parity(oracle_mod, w, h, 4000, 100, seed, 3)
+    assert rec["frames"] == 100 and got[-1]["n_keyframes"] > 2
 
 
 @pytest.mark.parametrize("seed,n,out,mono", [(0, 400, 0.15, 0.2), (1, 1500, 0.2, 0.1),
