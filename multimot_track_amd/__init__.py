@@ -225,6 +225,13 @@ def lib():
                                         vp, vp]
         L.mmt_profile_enable.argtypes = [vp, i32]
         L.mmt_profile_read.argtypes = [vp, ctypes.POINTER(MmtProfile), i32]
+        L.mmt_fuse_candidates.argtypes = [vp, ctypes.POINTER(MmtMatchFrame),
+                                          ctypes.POINTER(MmtLocalPoints), ctypes.c_float, vp, vp]
+        L.mmt_local_bundle_adjustment.argtypes = [vp, ctypes.POINTER(MmtBAProblem), vp, vp, vp,
+                                                  vp]
+        L.mmt_map_counters_read.argtypes = [vp, ctypes.POINTER(MmtMapCounters)]
+        L.mmt_set_deferred_objects.argtypes = [vp, i32]
+        L.mmt_flush_objects.argtypes = [vp, vp, vp, i32, i32, vp]
         _LIB = L
     return _LIB
 

@@ -40,3 +40,12 @@ def test_create_without_gpu_fails_cleanly():
     import multimot_track_amd as M
     with pytest.raises(M.MmtError):
         M.Context(M.kitti03_config())
+
+
+def test_every_called_entry_point_has_argtypes():
+    """Every mmt_* entry point the Python plumbing calls declares its ctypes argtypes (without
+    them ctypes passes the 64-bit context handle as a C int, a host segfault on the GPU box)."""
+    src = open(os.path.join(ROOT, "multimot_track_amd", "__init__.py")).read()
+    called = set(re.findall(r"lib\(\)\.(mmt_\w+)\(", src))
+    declared = set(re.findall(r"L\.(mmt_\w+)\.argtypes", src))
+    assert called and not called - declared, sorted(called - declared)
