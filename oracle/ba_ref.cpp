@@ -207,7 +207,6 @@ static int optimize(const BAProblem& P, const Cam& cam, std::vector<BAEdge>& E, 
   for (int j = 0; j < nP; j++)
     if (ptUsed[j]) pList.push_back(j);
   if (kList.empty() && pList.empty()) return 0;  // "0 vertices to optimize"
-  if (getenv("ORACLE_BA_PERTURB")) std::reverse(act.begin(), act.end());  // experiment only
   const int nk = (int)kList.size(), n6 = 6 * nk;
   // each point's active edges, in edge order
   std::vector<std::vector<int>> ptEdges(nP);
