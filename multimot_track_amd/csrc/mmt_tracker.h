@@ -128,15 +128,11 @@ class Tracker {
     int f;    // index in the chunk
     int buf;  // host chunk buffer of the frame's map arrays
   };
+  // One object's PnP buffers in one object slot: what stage B and D3 read after the RANSAC (the
+  // gathered correspondences, the inlier lists, the D3 edge list and the results).
   struct PnPBuf {
     float* pts3;
     float2* pts2;
-    int* subsets;
-    double* models;
-    double* hrec;
-    double* hout;
-    int* good;
-    unsigned long long* masks;
     int* inliers;
     int* mm_inliers;
     int* subset;
@@ -282,6 +278,18 @@ class Tracker {
   unsigned long long split_spin_ = 0;  // MMT_DEBUG_SPLIT_SPIN (0: the kernel's 0.1 s)
   PnPObject* d_pnp_[kObjSlots] = {};
   PnPBuf pnp_[kObjSlots][kMaxObj];
+  // The RANSAC-only scratch of an object index (subset draws, hypothesis records and models,
+  // inlier counts and masks), shared by the object slots: only the RANSAC kernels touch it, and
+  // they all run on oa_, so stream order keeps one frame's RANSAC off another's scratch.
+  struct PnPScratch {
+    int* subsets;
+    double* models;
+    double* hrec;
+    double* hout;
+    int* good;
+    unsigned long long* masks;
+  };
+  PnPScratch pnp_scr_[kMaxObj];
   bool prof_ = false;
   bool map_finish_pending_ = false;
   // MMT_MAP_PROFILE: host wall time per frame in obj_advance / ego_launch / ego_finish

@@ -262,12 +262,6 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     PnPBuf& b = pnp_[q][o];
     b.pts3 = alloc<float>(3 * (size_t)ocap_);
     b.pts2 = alloc<float2>(ocap_);
-    b.subsets = alloc<int>(5 * kRansacIters);
-    b.models = alloc<double>(6 * kRansacIters);
-    b.hrec = alloc<double>((size_t)kHypRec * kRansacIters);
-    b.hout = alloc<double>((size_t)3 * kHypOut * kRansacIters);
-    b.good = alloc<int>(kRansacIters);
-    b.masks = alloc<unsigned long long>((size_t)kRansacIters * mask_words_);
     b.inliers = alloc<int>(ocap_);
     b.mm_inliers = alloc<int>(ocap_);
     b.subset = alloc<int>(ocap_);
@@ -275,6 +269,15 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     b.result = d_r_[q]->res + 8 * o;
     b.Rt = d_Rt_[q] + 12 * o;
   }
+  }
+  for (int o = 0; o < kMaxObj; o++) {
+    PnPScratch& r = pnp_scr_[o];
+    r.subsets = alloc<int>(5 * kRansacIters);
+    r.models = alloc<double>(6 * kRansacIters);
+    r.hrec = alloc<double>((size_t)kHypRec * kRansacIters);
+    r.hout = alloc<double>((size_t)3 * kHypOut * kRansacIters);
+    r.good = alloc<int>(kRansacIters);
+    r.masks = alloc<unsigned long long>((size_t)kRansacIters * mask_words_);
   }
   // ---- map tracking: B3 grids of the chunk on the device, their host copies, the map engine
   d_uR_ = alloc<float>((size_t)kcap_ * max_chunk);
@@ -1079,6 +1082,7 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   for (int i = 0; i < nobj; i++) {
     const int l = objLabelsNew[i];
     PnPBuf& b = pnp_[q][i];
+    const PnPScratch& r = pnp_scr_[i];
     PnPObject& o = F.po[i];
     memset(&o, 0, sizeof(o));
     o.n = &d_stats_[q][l].members;
@@ -1093,9 +1097,9 @@ void Tracker::obj_stage_a(ObjFrame& F) {
     F.members[i] = stats[l].members;
     const std::vector<int>& sub = cached_subsets(std::max(stats[l].members, 1));
     memcpy(H.subsets[i], sub.data(), sizeof(H.subsets[i]));
-    MMT_HIP(hipMemcpyAsync(b.subsets, H.subsets[i], sizeof(H.subsets[i]), hipMemcpyHostToDevice,
+    MMT_HIP(hipMemcpyAsync(r.subsets, H.subsets[i], sizeof(H.subsets[i]), hipMemcpyHostToDevice,
                            st));
-    o.subsets = b.subsets;
+    o.subsets = r.subsets;
     for (size_t k = 0; k < Ls.nModLabel.size(); k++)
       if (Ls.nModLabel[k] == LabId[i]) {
         F.PreObjID[i] = (int)k;
@@ -1104,11 +1108,11 @@ void Tracker::obj_stage_a(ObjFrame& F) {
     o.use_mm = F.PreObjID[i] >= 0;
     o.pts3 = b.pts3;
     o.pts2 = b.pts2;
-    o.models = b.models;
-    o.hrec = b.hrec;
-    o.hout = b.hout;
-    o.good = b.good;
-    o.masks = b.masks;
+    o.models = r.models;
+    o.hrec = r.hrec;
+    o.hout = r.hout;
+    o.good = r.good;
+    o.masks = r.masks;
     o.mask_words = mask_words_;
     o.inliers = b.inliers;
     o.mm_inliers = b.mm_inliers;
