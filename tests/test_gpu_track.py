@@ -494,3 +494,42 @@ def test_deferred_objects_match_immediate():
         for x, y in zip(oa, ob):
             for k in x:
                 assert np.array_equal(np.asarray(x[k]), np.asarray(y[k]), equal_nan=True), (i, k)
+
+
+@pytest.mark.parametrize("k", [2, 4])
+def test_contexts_from_threads_match_oracle(oracle_mod, k):
+    """`bench.py --seqs-per-gpu K`'s setup: K contexts on one GPU, each tracking its own sequence
+    on its own stream from its own host thread (the C-ABI releases the GIL), 64 frames each in
+    chunks of 16; every context matches the oracle frame by frame, so contexts share no state."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    import multimot_track_amd as M
+    from multimot_track_amd import scene, shard
+    from oracle import compare
+    n, C, dev = 64, 16, torch.device("cuda:0")
+    seqs = [scene.kitti_like_sequence(n, 1242, 375, n_objects=3, device=dev,
+                                      seed=shard.sequence_seed(1003, j)) for j in range(k)]
+    ctxs = [M.Context(M.kitti03_config(nfeatures=2000, max_batch=C)) for _ in range(k)]
+    streams = [torch.cuda.Stream(dev) for _ in range(k)]
+    torch.cuda.synchronize(dev)
+
+    def run(j):
+        s, out = seqs[j], []
+        for s0 in range(0, n, C):
+            sl = slice(s0, s0 + C)
+            out += ctxs[j].track_chunk_device(s["bgr"][sl], s["disp"][sl], s["flow"][sl],
+                                              s["mask"][sl], streams[j].cuda_stream)
+        return out
+
+    try:
+        with ThreadPoolExecutor(max_workers=k) as pool:
+            got = list(pool.map(run, range(k)))
+    finally:
+        for c in ctxs:
+            c.close()
+    for j in range(k):
+        frames = scene.to_numpy_frames(seqs[j])
+        tr = oracle_mod.Tracker(1242, 375, K_KITTI, 387.5744, 0, 2000)
+        ora = [tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]) for f in frames]
+        rec = compare.parity_record(got[j], ora)
+        assert rec["frames"] == n and rec["first_divergent_frame"] is None, (j, rec)
