@@ -679,12 +679,14 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
   // state) and one exchange, instead of a light pass, an exchange, and for accepted trials a
   // second pass and exchange.  The ego solve accepts nearly every trial (22 of 24), so the
   // speculative linearisation is almost never wasted.
-  const bool spec = SPLIT && spec_ok && (gx.ntot + gx.G - 1) / gx.G <= 2 * 256;
+  // The one-workgroup solves (D3) take the same fused pass when they have one edge per thread
+  // (spec_ok: MMT_LM_SPEC1, default on).
+  const bool spec = spec_ok && (SPLIT ? (gx.ntot + gx.G - 1) / gx.G <= 2 * 256 : IR == 1 && N <= nt);
   // the one-workgroup solves (D3) reduce the accepted trial's 63 sums in registers
   // (the one-edge path: with two register edges the kernel would spill); max_cand bit 8 turns it
   // on (MMT_LM_REGSUM, A/B knob)
   const bool kRegSums = !SPLIT && IR == 1 && (max_cand & 256);
-  const bool kSpecRegSums = SPLIT && IR == 1 && (max_cand & 256);  // the split solve's fused pass
+  const bool kSpecRegSums = IR == 1 && (max_cand & 256);  // the fused pass's sums in registers
   max_cand &= 255;
   const int rs_idx = (kRegSums || kSpecRegSums) ? wave_rs_index() : 0;
   Cam c;
@@ -945,7 +947,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         MMT_LMPROF(5);
         vn = block_sum_regs64(vals, sm.part[pb], nw, rs_idx);
         pb ^= 1;
-        vn = gx_sum(gx, vn, kSums);
+        if (SPLIT) vn = gx_sum(gx, vn, kSums);
         lastTrialChi = lane_value(vn, 0);
         scale = lane_value(vn, 1);
       } else if (spec) {
@@ -966,7 +968,7 @@ __device__ __forceinline__ void flow_lm_body(const FlowSolveDesc& D, int N, int 
         MMT_LMPROF(5);
         vn = block_sum_tile_lanes<kSums>(sm.tile, sm.part[pb], nw);
         pb ^= 1;
-        vn = gx_sum(gx, vn, kSums);
+        if (SPLIT) vn = gx_sum(gx, vn, kSums);
         lastTrialChi = lane_value(vn, 0);
         scale = lane_value(vn, 1);
       } else {
@@ -1197,10 +1199,11 @@ __global__ __launch_bounds__(256) void k_flow_lm(const FlowSolveDesc* __restrict
   const int nt = min((int)blockDim.x, max(64, (N + 63) / 64 * 64));
   if ((int)threadIdx.x >= nt) return;
   GridX gx{};
+  const bool spec = (max_cand & 512) != 0;
   if (N <= nt || MAXIR == 1)
-    flow_lm_body<1, false>(D, N, 0, nt, sm, max_cand, gx);
+    flow_lm_body<1, false>(D, N, 0, nt, sm, max_cand, gx, spec);
   else
-    flow_lm_body<2, false>(D, N, 0, nt, sm, max_cand, gx);
+    flow_lm_body<2, false>(D, N, 0, nt, sm, max_cand, gx, spec);
 }
 
 // One large solve (descs[0]) over gridDim.x <= kFlowSplitMax workgroups, each on a contiguous slice
@@ -1252,6 +1255,9 @@ void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipSt
   // MMT_LM_REGSUM=0: the accepted trial's sums through the LDS tile (A/B knob, read per launch)
   const char* rs = getenv("MMT_LM_REGSUM");
   if (!(rs && atoi(rs) == 0)) max_cand |= 256;
+  // MMT_LM_SPEC1=0: two passes and two reductions per trial instead of the fused pass (A/B knob)
+  const char* s1 = getenv("MMT_LM_SPEC1");
+  if (!(s1 && atoi(s1) == 0)) max_cand |= 512;
   hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs, max_cand);
 }
 
