@@ -319,20 +319,27 @@ __global__ __launch_bounds__(kBAThreads) void k_local_ba(BADesc d) {
     if (nact > 0) {
       double lambda = 0, ni = 2, chk = 0;
       int nBad = 0;
+      // The errors and chi2 of the current estimate are those of the last trial when it was
+      // accepted: T5 computed them at that very state, in the same loop and reduction order as
+      // the pass below, so the pass is skipped then (bit-identical).
+      bool fresh = false;
+      double currentChi = 0;
       for (int iter = 0; iter < iters; iter++) {
         // ---- computeActiveErrors + activeRobustChi2
-        double part = 0;
-        for (int e = tid; e < d.n_edge; e += kBAThreads) {
-          if (w.level[e]) continue;
-          const bool st = !(d.e_obs[3 * (size_t)e + 2] < 0);
-          const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], st,
-                                      w.pose[d.e_kf[e]], &w.X[3 * (size_t)d.e_pt[e]], cam,
-                                      &w.err[3 * (size_t)e]);
-          double r0 = c, r1;
-          if (robust) huber_rho(c, st ? dStereo : dMono, r0, r1);
-          part += r0;
+        if (!fresh) {
+          double part = 0;
+          for (int e = tid; e < d.n_edge; e += kBAThreads) {
+            if (w.level[e]) continue;
+            const bool st = !(d.e_obs[3 * (size_t)e + 2] < 0);
+            const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], st,
+                                        w.pose[d.e_kf[e]], &w.X[3 * (size_t)d.e_pt[e]], cam,
+                                        &w.err[3 * (size_t)e]);
+            double r0 = c, r1;
+            if (robust) huber_rho(c, st ? dStereo : dMono, r0, r1);
+            part += r0;
+          }
+          currentChi = wg_sum1(part, s_part);
         }
-        double currentChi = wg_sum1(part, s_part);
         const double iniChi = currentChi;
         // ---- buildSystem, point pass: H_ll, b_l per point; H_pl per edge
         for (int j = tid; j < d.n_pt; j += kBAThreads) {
@@ -656,7 +663,8 @@ __global__ __launch_bounds__(kBAThreads) void k_local_ba(BADesc d) {
           rho = currentChi - tempChi;
           scale += 1e-3;
           rho /= scale;
-          if (rho > 0 && isfinite(tempChi)) {
+          fresh = rho > 0 && isfinite(tempChi);
+          if (fresh) {
             double alpha = 1. - pow((2 * rho - 1), 3);
             alpha = fmin(alpha, 2. / 3.);
             lambda *= fmax(1. / 3., alpha);
