@@ -114,18 +114,21 @@ def test_fuse_candidates_match_oracle(ctx, oracle_mod, kitti_frames):
     sel = rng.integers(0, len(kps), m)
     u = kps["x"][sel] + rng.normal(scale=2.0, size=m)
     v = kps["y"][sel] + rng.normal(scale=2.0, size=m)
-    z = rng.uniform(2.0, 60.0, m)
+    # the key's own depth where it has one (the stereo check of Fuse compares uR), else random
+    kd = depth[kps["y"][sel].astype(int), kps["x"][sel].astype(int)].astype(np.float64)
+    z = np.where(np.isfinite(kd) & (kd > 0.5) & (kd < 80), kd, rng.uniform(2.0, 60.0, m))
     X = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
-    nrm = X / np.linalg.norm(X, axis=1, keepdims=True) + rng.normal(scale=0.3, size=(m, 3))
+    nrm = X / np.linalg.norm(X, axis=1, keepdims=True) + rng.normal(scale=0.1, size=(m, 3))
     dist = np.linalg.norm(X, axis=1)
-    maxd = dist * 1.2 ** rng.integers(0, 8, m) * rng.uniform(0.7, 1.3, m)
+    # scale bounds around the selected key's octave (PredictScale within a level of it for most)
+    maxd = dist * 1.2 ** (kps["octave"][sel] + rng.uniform(-1.5, 1.5, m))
     mind = maxd / 1.2 ** 7
     pd = desc[sel].copy()
     flip = rng.integers(0, 256, size=(m, 4))
     for b in range(4):
         pd[np.arange(m), flip[:, b] // 8] ^= (1 << (flip[:, b] % 8)).astype(np.uint8)
     T = np.eye(4, dtype=np.float32)
-    T[:3, 3] = [0.1, -0.05, 0.3]
+    T[:3, 3] = [0.01, -0.005, 0.03]
     io, do = oracle_mod.fuse_candidates(kps, desc, depth, T, X, nrm, mind, maxd, pd, K_KITTI, BF,
                                         1242, 375)
     ig, dg = ctx.fuse_candidates(kps, desc, depth, T, X, nrm, mind, maxd, pd)
