@@ -278,6 +278,29 @@ class Tracker:
                                      _p(P["obs"]), _p(P["s"]))
         return P
 
+    def capture_d3(self, frame, obj):
+        """Record the D3 problem (PoseOptimizationFlow2 of one object) of object obj in this
+        tracker's frame-th track() call (0-based)."""
+        L = lib()
+        L.oracle_tracker_capture_d3.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int]
+        L.oracle_tracker_capture_d3(self._h, frame, obj)
+
+    def captured_d3(self):
+        """The captured D3 problem (obs, flow, depth, tcw_last, init as flow_solve takes them,
+        with rp_thres 0.01, prior_info 0.5, max_iters 200), or None."""
+        L = lib()
+        n = np.zeros(1, np.int32)
+        L.oracle_tracker_captured_d3(ctypes.c_void_p(self._h), _p(n), None, None, None, None, None)
+        if n[0] < 0:
+            return None
+        m = int(n[0])
+        P = dict(obs=np.zeros((m, 2), np.float32), flow=np.zeros((m, 2), np.float32),
+                 depth=np.zeros(m, np.float32), tcw_last=np.zeros((4, 4), np.float32),
+                 init=np.zeros((4, 4), np.float32))
+        L.oracle_tracker_captured_d3(ctypes.c_void_p(self._h), _p(n), _p(P["obs"]), _p(P["flow"]),
+                                     _p(P["depth"]), _p(P["tcw_last"]), _p(P["init"]))
+        return P
+
     def track(self, bgr, disp, flow, mask):
         bgr = np.ascontiguousarray(bgr, np.uint8)
         disp = np.ascontiguousarray(disp, np.uint16)

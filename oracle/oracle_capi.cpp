@@ -295,6 +295,47 @@ void oracle_tracker_capture_ba(void* tp, int which) {
   };
 }
 
+// D3 problem capture (test hook): the problem of object `obj` in the `frame`-th track() call
+struct D3Capture {
+  long frame = -1;
+  int obj = -1, got = 0, n = 0;
+  std::vector<float> obs, flow, depth;
+  float Tl[16], init[16];
+};
+static std::map<void*, D3Capture> g_d3;
+
+void oracle_tracker_capture_d3(void* tp, long frame, int obj) {
+  D3Capture& c = g_d3[tp];
+  c = D3Capture();
+  c.frame = frame;
+  c.obj = obj;
+  ((OTracker*)tp)->d3_hook = [tp](const FlowProblem& p, long f, int o) {
+    D3Capture& c = g_d3[tp];
+    if (f != c.frame || o != c.obj) return;
+    c.got = 1;
+    c.n = p.n;
+    c.obs.assign(p.obs, p.obs + 2 * (size_t)p.n);
+    c.flow.assign(p.flow, p.flow + 2 * (size_t)p.n);
+    c.depth.assign(p.depth, p.depth + p.n);
+    memcpy(c.Tl, p.Tcw_last, sizeof(c.Tl));
+    memcpy(c.init, p.init, sizeof(c.init));
+  };
+}
+
+// *n = edges (-1 until captured); with non-null arrays, copies the problem out
+int oracle_tracker_captured_d3(void* tp, int* n, float* obs, float* flow, float* depth, float* Tl,
+                               float* init) {
+  D3Capture& c = g_d3[tp];
+  *n = c.got ? c.n : -1;
+  if (!c.got || !obs) return c.got;
+  memcpy(obs, c.obs.data(), 4 * c.obs.size());
+  memcpy(flow, c.flow.data(), 4 * c.flow.size());
+  memcpy(depth, c.depth.data(), 4 * c.depth.size());
+  memcpy(Tl, c.Tl, sizeof(c.Tl));
+  memcpy(init, c.init, sizeof(c.init));
+  return 1;
+}
+
 // sizes[3] = n_kf, n_pt, n_edge (0s until captured); with non-null arrays, copies the problem out
 int oracle_tracker_captured_ba(void* tp, int* sizes, float* T, uint8_t* fixed, float* X, int* pt,
                                int* kf, float* obs, float* s) {

@@ -2,10 +2,12 @@
 #pragma once
 #include <array>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "oracle_common.h"
 #include "oracle_map.h"
+#include "oracle_solve.h"
 
 namespace oracle {
 
@@ -74,6 +76,9 @@ class OTracker {
   float V[16] = {0};
   float g0 = 0;
   OFrame L;  // mLastFrame
+  long n_tracked = 0;  // track() calls (test hook below)
+  // test hook: every D3 problem (frame = track() call index, object index) before its solve
+  std::function<void(const FlowProblem&, long frame, int obj)> d3_hook;
 };
 
 }  // namespace oracle

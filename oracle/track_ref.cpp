@@ -155,6 +155,7 @@ void OTracker::init(const TrackParams& p, const OrbConfig& orb) {
 int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
                     const int32_t* mask, FrameResult& out) {
   const int W = P.width, H = P.height;
+  const long frame_no = n_tracked++;
   if (reset_pending) {  // System::TrackRGBD -> Tracking::Reset (System.cc:203-211)
     map.reset();
     state = 0;
@@ -477,6 +478,7 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
     fp.fx = P.fx; fp.fy = P.fy; fp.cx = P.cx; fp.cy = P.cy;
     float X[16];
     FlowSolveStats st;
+    if (d3_hook) d3_hook(fp, frame_no, (int)oi);
     const bool solved = flow_pose_solve(fp, X, &st) == 0;
     if (!solved) mat4_eye(X);
     // ObjCentre3D_pre (Tracking.cc:2032-2049): float sum, in order, of the last frame's
