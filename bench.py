@@ -394,6 +394,9 @@ def main(argv=None):
                                              "ba_trials", "ba_edges", "ba_pts", "ba_max_opt",
                                              "fuse_launches", "fuse_queries", "fuse_relaunches",
                                              "d2_split_fallbacks")}
+    if mc["lm_us"] > 0:  # host wall times, collected with MMT_MAP_PROFILE=1
+        for k in ("lm_us", "ba_us", "fuse_us"):
+            local_mapping[k] = round(float(mc[k]), 1)
     local_mapping["keyframes_last_frame"] = int(timed_frames[-1]["n_keyframes"])
     local_mapping["mappoints_last_frame"] = int(timed_frames[-1]["n_mappoints"])
 

@@ -435,7 +435,9 @@ void MapEngine::local_bundle_adjustment(int kf) {  // Optimizer::LocalBundleAdju
   std::vector<float> Tout(16 * (size_t)nK), Xout(3 * (size_t)nP);
   std::vector<uint8_t> er(std::max(nE, 1));
   int st[5];
+  const double tb = prof_on_ ? now_us() : 0;
   ba_.run(P, lm_s_, Tout.data(), Xout.data(), er.data(), st);
+  if (prof_on_) mstats_.basolve_us += now_us() - tb;
   mstats_.n_ba++;
   mstats_.ba_trials += st[2] + st[3];
   mstats_.ba_edges += nE;
@@ -501,11 +503,21 @@ void MapEngine::local_mapping(int kf) {
   const double t0 = prof_on_ ? now_us() : 0;
   // CreateNewMapPoints: SearchForTriangulation needs the BoW vocabulary (skipped, see above)
   search_in_neighbors(kf);
+  const double t1 = prof_on_ ? now_us() : 0;
   if (n_keyframes() > 2) local_bundle_adjustment(kf);
+  const double t2 = prof_on_ ? now_us() : 0;
   keyframe_culling(kf);
+  const double t3 = prof_on_ ? now_us() : 0;
   // the keyframe-store copies read the chunk's frame buffers: done before the next chunk's ORB
   MMT_HIP(hipStreamSynchronize(lm_s_));
-  if (prof_on_) mstats_.lm_us += now_us() - t0;
+  if (prof_on_) {
+    const double t4 = now_us();
+    mstats_.lm_us += t4 - t0;
+    mstats_.sin_us += t1 - t0;
+    mstats_.cull_us += t3 - t2;
+    mstats_.lmsync_us += t4 - t3;
+    mstats_.n_lm++;
+  }
 }
 
 }  // namespace mmt

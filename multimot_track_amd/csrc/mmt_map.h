@@ -99,6 +99,9 @@ struct MappingStats {
        ba_kfs = 0, ba_pts = 0, ba_max_opt = 0, fuse_launches = 0, fuse_queries = 0,
        fuse_relaunches = 0;
   double lm_us = 0, ba_us = 0, fuse_us = 0;  // host wall time (MMT_MAP_PROFILE)
+  // finer host wall times of the keyframe path (MMT_MAP_PROFILE; printed at destruction)
+  double kfnew_us = 0, pnk_us = 0, sin_us = 0, basolve_us = 0, cull_us = 0, lmsync_us = 0;
+  long n_lm = 0;
 };
 
 // The map-path view of one Frame: its ORB output and B3 arrays (host copies of the device ones)

@@ -70,6 +70,17 @@ MapEngine::~MapEngine() {
     fprintf(stderr, "[mmt map profile] %ld frames, host wall us per frame:", prof_n_);
     for (int k = 0; k < 12; k++) fprintf(stderr, " %s %.1f%s", names[k], prof_[k] / prof_n_,
                                          k < 11 ? "," : "\n");
+    if (mstats_.n_lm > 0) {
+      const double n = (double)mstats_.n_lm;
+      fprintf(stderr, "[mmt localmapping profile] %ld keyframes, host wall us per keyframe: "
+              "ProcessNewKeyFrame+MapPointCulling %.1f, SearchInNeighbors %.1f (Fuse launches "
+              "%.1f), LocalBundleAdjustment %.1f (solve %.1f), KeyFrameCulling %.1f, final sync "
+              "%.1f, LocalMapping total %.1f; CreateNewKeyFrame with all of it %.1f\n", mstats_.n_lm,
+              mstats_.pnk_us / n,
+              mstats_.sin_us / n, mstats_.fuse_us / n, mstats_.ba_us / n,
+              mstats_.basolve_us / n, mstats_.cull_us / n, mstats_.lmsync_us / n,
+              mstats_.lm_us / n, mstats_.kfnew_us / n);
+    }
     fprintf(stderr, "[mmt map profile] per frame: %.1f local keyframes, %.1f local points, "
             "%.1f C3 edges; %zu map points allocated, %d keyframes at the end\n",
             prof_cnt_[0] / prof_n_, prof_cnt_[1] / prof_n_, prof_cnt_[2] / prof_n_, pts_.size(),
@@ -986,8 +997,10 @@ void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracki
       if (v[j].first > cam_.thDepth && nPoints > 200) break;
     }
   }
+  const double tp = prof_on_ ? now_us() : 0;
   process_new_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKF), processed at once
   map_point_culling(kf);
+  if (prof_on_) mstats_.pnk_us += now_us() - tp;
   local_mapping(kf);
   lastKFFrameId_ = C.id;
 }
@@ -1058,7 +1071,9 @@ void MapEngine::track_finish(MapFrameH& C, MapFrameH& L, const float* Tcw, MapSt
       if (L.mps[i] >= kTemp) L.mps[i] = -1;
     temps_.clear();
     MAP_PROF(5, if (need_new_keyframe(C)) {
+      const double tk = prof_on_ ? now_us() : 0;
       create_new_keyframe(C, Tcw);
+      if (prof_on_) mstats_.kfnew_us += now_us() - tk;
       st.new_keyframe = 1;
     });
     for (int i = 0; i < C.n; i++)
