@@ -1,6 +1,6 @@
 // multimot_track_amd/csrc/mmt_ba.h -- the solve of Optimizer::LocalBundleAdjustment
-// (reference src/Optimizer.cc:3394-3665) on the GPU: one persistent workgroup per call
-// (mmt_ba.hip).  The host (mmt_localmap.hip) builds the graph exactly as the reference does
+// (reference src/Optimizer.cc:3394-3665) on the GPU: a chain of short kernels per LM trial with
+// the LM state on the device, or one persistent workgroup (MMT_BA_ONEWG=1) (mmt_ba.hip).  The host (mmt_localmap.hip) builds the graph exactly as the reference does
 // (local keyframes, fixed keyframes, points, edges point by point in observation order) and
 // applies the results (erase, SetPose, SetWorldPos).
 #pragma once
@@ -72,6 +72,11 @@ class BARunner {
   size_t up_cap_ = 0, dn_cap_ = 0;
   double* d_ws_ = nullptr;
   size_t ws_cap_ = 0;
+  uint8_t* d_ws2_ = nullptr;  // the multi-kernel solve's workspace
+  size_t ws2_cap_ = 0;
+  int* h_flag_ = nullptr;     // pinned: the solve's done flag
 };
+
+size_t ba2_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt, int n_blk, int gP);
 
 }  // namespace mmt

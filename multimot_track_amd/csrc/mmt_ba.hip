@@ -718,12 +718,712 @@ __global__ __launch_bounds__(kBAThreads) void k_local_ba(BADesc d) {
   if (tid == 0) d.stats[4] = nerase;
 }
 
+namespace {
+// ================================================================== multi-kernel solve (default)
+// The same LM as k_local_ba spread over the chip: one LM trial is a chain of short kernels on the
+// caller's stream (points, keyframe-pair blocks and keyframes in parallel; the reduced camera
+// system and the LM decision in one workgroup each), with the LM state in device memory.  The host
+// enqueues trials in batches and reads the state's done flag after each batch; every kernel of a
+// finished solve returns at once.  k_local_ba ran the whole solve on one CU (10-11 ms per local
+// BA of the C3 sequence); spread, a trial costs a few microseconds per kernel.
+//   per iteration (need_lin):  k_ba2_lin   one thread per point: errors, robust chi2, H_ll, b_l,
+//                                          H_pl and the edge's pose terms (J_p^T w J_p, J_p^T w e)
+//                              k_ba2_kfsum one workgroup per optimised keyframe: H_pp, b_p
+//   per trial:                 k_ba2_p1    one thread per point: (H_ll + lambda I)^-1, Y, H_pl D^-1 b_l
+//                              k_ba2_p2    one workgroup per keyframe-pair block / keyframe: Schur sums
+//                              k_ba2_p3    one workgroup: the reduced system, LDL^T, increments, trial poses
+//                              k_ba2_p4    one thread per point: point increments, trial errors, chi2
+//                              k_ba2_p5    one workgroup: the LM decision (rho, lambda, Raul's stop,
+//                                          the chi2-increase stop), iteration and round bookkeeping
+// The estimates are double-buffered (current / trial, swapped on acceptance), so a rejected trial
+// needs no restore.  Every reduction has a fixed order: the solve is deterministic.
+
+constexpr int kMkThreads = 256;
+constexpr int kMkWaves = kMkThreads / 64;
+constexpr int kMkSolveThreads = 512;
+constexpr int kMkDecideThreads = 1024;
+
+struct BAState {
+  int done, round, iter, qmax, need_lin, lam_init, cb, ok2, nBad, nact;
+  int it_done[2], trials[2];
+  double lambda, ni, chk, currentChi, iniChi, scale_p;
+};
+
+struct BAWork2 {
+  BAState* st;
+  DSE3* pose;       // [2][n_kf]: the current estimate (buffer st->cb) and the trial
+  double* X;        // [2][3 n_pt]
+  double* Hll;      // 9 n_pt
+  double* bl;       // 3 n_pt
+  double* Dinv;     // 9 n_pt
+  double* err;      // 3 n_edge: the last computed errors
+  double* Hpl;      // 18 n_edge
+  double* Hpe;      // 27 n_edge: the edge's J_p^T w J_p (21, upper triangle) and J_p^T w (-e) (6)
+  double* Y;        // 18 n_edge
+  double* cv;       // 6 n_edge
+  double* Hpp;      // 36 n_opt
+  double* bp;       // 6 n_opt
+  double* cvs;      // 6 n_opt: the keyframe's sum of H_pl D^-1 b_l
+  double* Sblk;     // 36 n_blk
+  double* x;        // 6 n_opt + 3 n_pt (g2o's _x: poses, then points)
+  double* S;        // n6 x n6 when the reduced system does not fit in LDS
+  double* vec;      // 3 n6 (idem)
+  double* linpart;  // 2 per point workgroup: chi2, largest active H_ll diagonal
+  double* p4part;   // 2 per point workgroup: trial chi2, scale
+  uint8_t* level;   // n_edge
+  uint8_t* kf_act;  // n_kf: optimised keyframe with an active edge this round
+  uint8_t* pt_act;  // n_pt
+  int gP;           // point workgroups
+};
+
+// workgroup sums of K <= 64 values per thread, fixed order (DPP wave sums, then the waves in
+// order); sum q lands in out[q] (LDS), visible to every thread on return
+template <int K, int NW>
+__device__ __forceinline__ void wg_sumK(const double (&v)[K], double* part, double* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double mine = 0;
+#pragma unroll
+  for (int q = 0; q < K; q++) {
+    const double s = wave_sum_dpp(v[q]);
+    if (lane == q) mine = s;
+  }
+  if (lane < K) part[wave * K + lane] = mine;
+  __syncthreads();
+  if ((int)threadIdx.x < K) {
+    double s = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) s += part[w * K + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+template <int NW>
+__device__ __forceinline__ double wg_maxN(double v, double* part) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) part[wave] = v;
+  __syncthreads();
+  double m = 0;
+#pragma unroll
+  for (int w = 0; w < NW; w++) m = fmax(m, part[w]);
+  __syncthreads();
+  return m;
+}
+
+// computeLambdaInit over the round's vertices: 1e-5 x the largest diagonal entry of the active
+// optimised keyframes' H_pp and the active points' H_ll (the latter from k_ba2_lin's partials)
+__device__ __forceinline__ double ba2_lambda_init(const BADesc& d, const BAWork2& w) {
+  double m = 0;
+  for (int g = 0; g < w.gP; g++) m = fmax(m, w.linpart[2 * g + 1]);
+  for (int a = 0; a < d.n_opt; a++)
+    if (w.kf_act[d.opt_kf[a]])
+      for (int r = 0; r < 6; r++) m = fmax(m, fabs(w.Hpp[36 * (size_t)a + 7 * r]));
+  return 1e-5 * m;
+}
+
+__device__ __forceinline__ Cam ba_cam(const BADesc& d) { return Cam{d.fx, d.fy, d.cx, d.cy, d.bf}; }
+
+// thHuberMono = sqrt(5.991) stored as a float (Optimizer.cc:3457-3458)
+__device__ __forceinline__ double huber_mono() { return (double)(float)sqrt(5.991); }
+__device__ __forceinline__ double huber_stereo() { return (double)(float)sqrt(7.815); }
+
+__global__ __launch_bounds__(kMkThreads) void k_ba2_init(BADesc d, BAWork2 w) {
+  const int gt = blockIdx.x * kMkThreads + threadIdx.x, gs = gridDim.x * kMkThreads;
+  const size_t n6 = 6 * (size_t)d.n_opt;
+  for (int j = gt; j < d.n_pt; j += gs) {
+    for (int r = 0; r < 3; r++) {
+      w.X[3 * (size_t)j + r] = (double)d.Xw[3 * (size_t)j + r];
+      w.x[n6 + 3 * (size_t)j + r] = 0;
+    }
+    w.pt_act[j] = d.pt_start[j + 1] > d.pt_start[j] ? 1 : 0;
+  }
+  for (int e = gt; e < d.n_edge; e += gs) {
+    w.level[e] = 0;
+    w.err[3 * (size_t)e] = w.err[3 * (size_t)e + 1] = w.err[3 * (size_t)e + 2] = 0;
+  }
+  if (blockIdx.x == 0) {
+    for (int k = threadIdx.x; k < d.n_kf; k += kMkThreads) {
+      w.pose[k] = dse3_from_float(d.Tcw + 16 * (size_t)k);
+      w.kf_act[k] = 0;
+    }
+    for (int q = threadIdx.x; q < (int)n6; q += kMkThreads) w.x[q] = 0;
+    __syncthreads();
+    for (int a = threadIdx.x; a < d.n_opt; a += kMkThreads)
+      if (d.kf_start[a + 1] > d.kf_start[a]) w.kf_act[d.opt_kf[a]] = 1;
+    if (threadIdx.x == 0) {
+      BAState& s = *w.st;
+      memset(&s, 0, sizeof(s));
+      s.need_lin = 1;
+      s.lam_init = 1;
+      s.ni = 2;
+      s.done = d.n_edge == 0 ? 1 : 0;
+    }
+  }
+}
+
+// computeActiveErrors + activeRobustChi2 + buildSystem's point side, one thread per point
+__global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
+  __shared__ double s_part[2 * kMkWaves];
+  const BAState* st = w.st;
+  if (st->done || !st->need_lin) return;
+  const bool robust = st->round == 0;
+  const int cb = st->cb;
+  const Cam cam = ba_cam(d);
+  const double dMono = huber_mono(), dStereo = huber_stereo();
+  const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
+  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
+  const int j = blockIdx.x * kMkThreads + threadIdx.x;
+  double chi = 0, mx = 0;
+  if (j < d.n_pt) {
+    double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b3[3] = {0, 0, 0};
+    const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
+    for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
+      if (w.level[e]) continue;
+      const int k = d.e_kf[e];
+      const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
+      const double s = (double)d.e_s[e];
+      double er[3];
+      const double c = edge_error(d.e_obs + 3 * (size_t)e, s, stereo, pose[k], X, cam, er);
+#pragma unroll
+      for (int r = 0; r < 3; r++) w.err[3 * (size_t)e + r] = er[r];
+      double r0 = c, r1 = 1.0;
+      if (robust) huber_rho(c, stereo ? dStereo : dMono, r0, r1);
+      chi += r0;
+      double Jp[3][6], Jl[3][3];
+      edge_jac<true>(stereo, pose[k], X, cam, Jp, Jl);
+      const int rows = stereo ? 3 : 2;
+      const double wt = r1 * s;
+      double om[3];
+#pragma unroll
+      for (int r = 0; r < 3; r++) om[r] = r < rows ? -(s * er[r]) * r1 : 0.0;
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+#pragma unroll
+        for (int b = 0; b < 3; b++) {
+          double acc = 0;
+          _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) acc += Jl[r][a] * wt * Jl[r][b];
+          hl[3 * a + b] += acc;
+        }
+        double g = 0;
+        _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) g += Jl[r][a] * om[r];
+        b3[a] += g;
+      }
+      if (d.opt_of[k] >= 0) {
+        double* hpl = &w.Hpl[18 * (size_t)e];
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+          for (int b = 0; b < 3; b++) {
+            double acc = 0;
+            _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) acc += Jp[r][a] * wt * Jl[r][b];
+            hpl[3 * a + b] = acc;
+          }
+        double* hpe = &w.Hpe[27 * (size_t)e];
+        int q = 0;
+#pragma unroll
+        for (int r0 = 0; r0 < 6; r0++)
+#pragma unroll
+          for (int c0 = r0; c0 < 6; c0++) {
+            double v = 0;
+            _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) v += Jp[r][r0] * wt * Jp[r][c0];
+            hpe[q++] = v;
+          }
+#pragma unroll
+        for (int r0 = 0; r0 < 6; r0++) {
+          double g = 0;
+          _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) g += Jp[r][r0] * (-(s * er[r]) * r1);
+          hpe[21 + r0] = g;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 9; q++) w.Hll[9 * (size_t)j + q] = hl[q];
+#pragma unroll
+    for (int q = 0; q < 3; q++) w.bl[3 * (size_t)j + q] = b3[q];
+    if (w.pt_act[j]) mx = fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8])));
+  }
+  const double cs = wave_sum_dpp(chi);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) s_part[wave] = cs;
+  const double m = wg_maxN<kMkWaves>(mx, s_part + kMkWaves);  // its barrier orders s_part too
+  if (threadIdx.x == 0) {
+    double t = 0;
+#pragma unroll
+    for (int q = 0; q < kMkWaves; q++) t += s_part[q];
+    w.linpart[2 * blockIdx.x] = t;
+    w.linpart[2 * blockIdx.x + 1] = m;
+  }
+}
+
+// buildSystem's keyframe side: one workgroup per optimised keyframe sums its active edges' pose terms
+__global__ __launch_bounds__(kMkThreads) void k_ba2_kfsum(BADesc d, BAWork2 w) {
+  __shared__ double s_part[27 * kMkWaves];
+  __shared__ double s_out[32];
+  const BAState* st = w.st;
+  if (st->done || !st->need_lin) return;
+  const int a = blockIdx.x;
+  double acc[27];
+#pragma unroll
+  for (int q = 0; q < 27; q++) acc[q] = 0;
+  for (int t = d.kf_start[a] + threadIdx.x; t < d.kf_start[a + 1]; t += kMkThreads) {
+    const int e = d.kf_edges[t];
+    if (w.level[e]) continue;
+    const double* h = &w.Hpe[27 * (size_t)e];
+#pragma unroll
+    for (int q = 0; q < 27; q++) acc[q] += h[q];
+  }
+  wg_sumK<27, kMkWaves>(acc, s_part, s_out);
+  const int q = threadIdx.x;
+  if (q < 21) {
+    int r0 = 0, k = q;
+    while (k >= 6 - r0) {
+      k -= 6 - r0;
+      r0++;
+    }
+    const int c0 = r0 + k;
+    w.Hpp[36 * (size_t)a + 6 * r0 + c0] = s_out[q];
+    w.Hpp[36 * (size_t)a + 6 * c0 + r0] = s_out[q];
+  } else if (q < 27) {
+    w.bp[6 * (size_t)a + q - 21] = s_out[q];
+  }
+}
+
+// trial step 1, one thread per active point: D^-1 = (H_ll + lambda I)^-1 (Eigen's cofactor
+// inverse), and per active edge to an optimised keyframe Y = H_pl D^-1 and H_pl D^-1 b_l
+__global__ __launch_bounds__(kMkThreads) void k_ba2_p1(BADesc d, BAWork2 w) {
+  const BAState* st = w.st;
+  if (st->done) return;
+  const int j = blockIdx.x * kMkThreads + threadIdx.x;
+  if (j >= d.n_pt || !w.pt_act[j]) return;
+  const double lambda = st->lam_init ? ba2_lambda_init(d, w) : st->lambda;
+  double Dm[9], Di[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) Dm[q] = w.Hll[9 * (size_t)j + q] + ((q % 4) == 0 ? lambda : 0.0);
+  inverse3(Dm, Di);
+#pragma unroll
+  for (int q = 0; q < 9; q++) w.Dinv[9 * (size_t)j + q] = Di[q];
+  const double* b3 = &w.bl[3 * (size_t)j];
+  double db[3];
+#pragma unroll
+  for (int a = 0; a < 3; a++) db[a] = Di[3 * a] * b3[0] + Di[3 * a + 1] * b3[1] + Di[3 * a + 2] * b3[2];
+  for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
+    if (w.level[e] || d.opt_of[d.e_kf[e]] < 0) continue;
+    const double* B = &w.Hpl[18 * (size_t)e];
+    double* Ye = &w.Y[18 * (size_t)e];
+    double* ce = &w.cv[6 * (size_t)e];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+      const double b0 = B[3 * r], b1 = B[3 * r + 1], b2 = B[3 * r + 2];
+#pragma unroll
+      for (int c = 0; c < 3; c++) Ye[3 * r + c] = b0 * Di[c] + b1 * Di[3 + c] + b2 * Di[6 + c];
+      ce[r] = b0 * db[0] + b1 * db[1] + b2 * db[2];
+    }
+  }
+}
+
+// trial step 2: the Schur sums, one workgroup per keyframe-pair block (its (edge, edge) triples)
+// and one per optimised keyframe (its edges' H_pl D^-1 b_l)
+__global__ __launch_bounds__(kMkThreads) void k_ba2_p2(BADesc d, BAWork2 w) {
+  __shared__ double s_part[36 * kMkWaves];
+  __shared__ double s_out[64];
+  const BAState* st = w.st;
+  if (st->done) return;
+  if ((int)blockIdx.x < d.n_blk) {
+    const int bk = blockIdx.x;
+    double acc[36];
+#pragma unroll
+    for (int q = 0; q < 36; q++) acc[q] = 0;
+    for (int t = d.blk_start[bk] + threadIdx.x; t < d.blk_start[bk + 1]; t += kMkThreads) {
+      const int2 tr = d.trip[t];
+      if (w.level[tr.x] || w.level[tr.y]) continue;
+      const double* Ye = &w.Y[18 * (size_t)tr.x];
+      const double* B2 = &w.Hpl[18 * (size_t)tr.y];
+      double h2[18];
+#pragma unroll
+      for (int q = 0; q < 18; q++) h2[q] = B2[q];
+#pragma unroll
+      for (int r = 0; r < 6; r++) {
+        const double y0 = Ye[3 * r], y1 = Ye[3 * r + 1], y2 = Ye[3 * r + 2];
+#pragma unroll
+        for (int c = 0; c < 6; c++) acc[6 * r + c] += y0 * h2[3 * c] + y1 * h2[3 * c + 1] + y2 * h2[3 * c + 2];
+      }
+    }
+    wg_sumK<36, kMkWaves>(acc, s_part, s_out);
+    if (threadIdx.x < 36) w.Sblk[36 * (size_t)bk + threadIdx.x] = s_out[threadIdx.x];
+  } else {
+    const int a = blockIdx.x - d.n_blk;
+    double cs[6] = {0, 0, 0, 0, 0, 0};
+    for (int t = d.kf_start[a] + threadIdx.x; t < d.kf_start[a + 1]; t += kMkThreads) {
+      const int e = d.kf_edges[t];
+      if (w.level[e]) continue;
+#pragma unroll
+      for (int r = 0; r < 6; r++) cs[r] += w.cv[6 * (size_t)e + r];
+    }
+    wg_sumK<6, kMkWaves>(cs, s_part, s_out);
+    if (threadIdx.x < 6) w.cvs[6 * (size_t)a + threadIdx.x] = s_out[threadIdx.x];
+  }
+}
+
+// trial step 3, one workgroup: the reduced camera system H_pp + lambda I - sum Y H_pl^T (upper
+// triangle, mirrored), b_schur, LDL^T right-looking (for every entry the left-looking sequence of
+// operations of the CPU checker), the substitutions on one wave, the increment (stale on a zero
+// pivot, as g2o re-applies its _x), the trial poses and the poses' share of the LM scale term
+__global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w) {
+  __shared__ double s_S[kLdsRows * kLdsRows];
+  __shared__ double s_vec[3 * kLdsRows];
+  __shared__ int s_ok;
+  BAState* stp = w.st;
+  if (stp->done) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n6 = 6 * d.n_opt;
+  const bool lam_init = stp->lam_init != 0, need_lin = stp->need_lin != 0;
+  const int cb = stp->cb;
+  const double lambda = lam_init ? ba2_lambda_init(d, w) : stp->lambda;
+  double* S = n6 <= kLdsRows ? s_S : w.S;
+  double* bs = n6 <= kLdsRows ? s_vec : w.vec;
+  double* Dg = bs + n6;
+  double* yv = Dg + n6;
+  for (int q = tid; q < n6 * n6; q += kMkSolveThreads) S[q] = 0;
+  __syncthreads();
+  for (int q = tid; q < d.n_blk * 36; q += kMkSolveThreads) {
+    const int bk = q / 36, k = q % 36, r = k / 6, c = k % 6;
+    const int a = d.blk_ab[2 * bk], b = d.blk_ab[2 * bk + 1];
+    double base = 0;
+    if (a == b) base = w.Hpp[36 * (size_t)a + k] + (r == c ? lambda : 0.0);
+    if (a < b || r <= c) S[(size_t)(6 * a + r) * n6 + 6 * b + c] = base - w.Sblk[36 * (size_t)bk + k];
+  }
+  for (int i = tid; i < n6; i += kMkSolveThreads) bs[i] = w.bp[i] - w.cvs[i];
+  if (tid == 0) s_ok = 1;
+  __syncthreads();
+  for (int q = tid; q < n6 * n6; q += kMkSolveThreads) {
+    const int i = q / n6, j = q % n6;
+    if (i > j) S[q] = S[(size_t)j * n6 + i];
+  }
+  __syncthreads();
+  bool ok = true;
+  for (int k = 0; k < n6; k++) {
+    const double dk = S[(size_t)k * n6 + k];
+    if (dk == 0) {  // uniform: every thread reads the same value
+      ok = false;
+      break;
+    }
+    if (tid == 0) Dg[k] = dk;
+    for (int i = k + 1 + tid; i < n6; i += kMkSolveThreads) S[(size_t)i * n6 + k] /= dk;
+    __syncthreads();
+    const int m = n6 - k - 1;
+    for (int q = tid; q < m * m; q += kMkSolveThreads) {
+      const int i = k + 1 + q / m, jj = k + 1 + q % m;
+      if (jj <= i) S[(size_t)i * n6 + jj] -= S[(size_t)i * n6 + k] * S[(size_t)jj * n6 + k] * dk;
+    }
+    __syncthreads();
+  }
+  if (!ok) {
+    if (tid == 0) s_ok = 0;
+  } else if (wave == 0) {
+    for (int i = lane; i < n6; i += 64) yv[i] = bs[i];
+    wave_sync_lds();
+    for (int c = 0; c < n6; c++) {
+      const double yc = yv[c];
+      for (int i = c + 1 + lane; i < n6; i += 64) yv[i] -= S[(size_t)i * n6 + c] * yc;
+      wave_sync_lds();
+    }
+    for (int i = lane; i < n6; i += 64) yv[i] /= Dg[i];
+    wave_sync_lds();
+    for (int r = n6 - 1; r > 0; r--) {
+      const double yr = yv[r];
+      for (int i = lane; i < r; i += 64) yv[i] -= S[(size_t)r * n6 + i] * yr;
+      wave_sync_lds();
+    }
+    for (int i = lane; i < n6; i += 64) w.x[i] = yv[i];
+  }
+  __syncthreads();
+  const bool ok2 = s_ok != 0;
+  // the trial poses: exp(x_p) * pose for the round's optimised keyframes, the others unchanged
+  const DSE3* cur = w.pose + (size_t)cb * d.n_kf;
+  DSE3* tri = w.pose + (size_t)(1 - cb) * d.n_kf;
+  for (int k = tid; k < d.n_kf; k += kMkSolveThreads) {
+    const int a = d.opt_of[k];
+    if (a >= 0 && w.kf_act[k]) {
+      double u[6];
+#pragma unroll
+      for (int r = 0; r < 6; r++) u[r] = w.x[6 * a + r];
+      tri[k] = dse3_mul(dse3_exp(u), cur[k]);
+    } else {
+      tri[k] = cur[k];
+    }
+  }
+  if (tid == 0) {
+    double sp = 0;
+    for (int a = 0; a < d.n_opt; a++) {
+      if (!w.kf_act[d.opt_kf[a]]) continue;
+      for (int r = 0; r < 6; r++) {
+        const double xv = w.x[6 * a + r];
+        sp += xv * (lambda * xv + w.bp[6 * (size_t)a + r]);
+      }
+    }
+    BAState& s = *stp;
+    if (need_lin) {
+      double c = 0;
+      for (int g = 0; g < w.gP; g++) c += w.linpart[2 * g];
+      s.currentChi = c;
+      s.iniChi = c;
+    }
+    if (lam_init) {
+      s.lam_init = 0;
+      s.ni = 2;
+      s.nBad = 0;
+    }
+    s.lambda = lambda;
+    s.ok2 = ok2 ? 1 : 0;
+    s.scale_p = sp;
+  }
+}
+
+// trial step 4, one thread per point: x_l = D^-1 (b_l - H_pl^T x_p) (stale on a failed solve),
+// the trial point, the errors of its active edges at the trial state, chi2 and the scale term
+__global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
+  __shared__ double s_part[2 * kMkWaves];
+  const BAState* st = w.st;
+  if (st->done) return;
+  const int cb = st->cb, nb = 1 - cb;
+  const bool ok2 = st->ok2 != 0, robust = st->round == 0;
+  const double lambda = st->lambda;
+  const Cam cam = ba_cam(d);
+  const double dMono = huber_mono(), dStereo = huber_stereo();
+  const size_t n6 = 6 * (size_t)d.n_opt;
+  const DSE3* tri = w.pose + (size_t)nb * d.n_kf;
+  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
+  double* Xt = w.X + (size_t)nb * 3 * d.n_pt;
+  const int j = blockIdx.x * kMkThreads + threadIdx.x;
+  double chi = 0, sc = 0;
+  if (j < d.n_pt) {
+    double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
+    if (w.pt_act[j]) {
+      double* xl = &w.x[n6 + 3 * (size_t)j];
+      if (ok2) {
+        double cl[3] = {w.bl[3 * (size_t)j], w.bl[3 * (size_t)j + 1], w.bl[3 * (size_t)j + 2]};
+        for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
+          const int a = d.opt_of[d.e_kf[e]];
+          if (w.level[e] || a < 0) continue;
+          const double* B = &w.Hpl[18 * (size_t)e];
+#pragma unroll
+          for (int c = 0; c < 3; c++)
+#pragma unroll
+            for (int r = 0; r < 6; r++) cl[c] += B[3 * r + c] * (-w.x[6 * a + r]);
+        }
+        const double* Di = &w.Dinv[9 * (size_t)j];
+#pragma unroll
+        for (int a = 0; a < 3; a++) xl[a] = Di[3 * a] * cl[0] + Di[3 * a + 1] * cl[1] + Di[3 * a + 2] * cl[2];
+      }
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const double xv = xl[r];
+        sc += xv * (lambda * xv + w.bl[3 * (size_t)j + r]);
+        X[r] += xv;
+      }
+      for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
+        if (w.level[e]) continue;
+        const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
+        const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], stereo, tri[d.e_kf[e]],
+                                    X, cam, &w.err[3 * (size_t)e]);
+        double r0 = c, r1;
+        if (robust) huber_rho(c, stereo ? dStereo : dMono, r0, r1);
+        chi += r0;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 3; r++) Xt[3 * (size_t)j + r] = X[r];
+  }
+  const double a = wave_sum_dpp(chi), b = wave_sum_dpp(sc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_part[2 * wave] = a;
+    s_part[2 * wave + 1] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t0 = 0, t1 = 0;
+#pragma unroll
+    for (int q = 0; q < kMkWaves; q++) {
+      t0 += s_part[2 * q];
+      t1 += s_part[2 * q + 1];
+    }
+    w.p4part[2 * blockIdx.x] = t0;
+    w.p4part[2 * blockIdx.x + 1] = t1;
+  }
+}
+
+// trial step 5, one workgroup: OptimizationAlgorithmLevenberg::solve's decision for the trial,
+// the end of the iteration (SparseOptimizer::optimize's stops), the switch to the second round
+// (the inlier check of Optimizer.cc:3559-3590 on the last computed errors) and the end of the solve
+__global__ __launch_bounds__(kMkDecideThreads) void k_ba2_p5(BADesc d, BAWork2 w) {
+  __shared__ int s_round_end;
+  __shared__ double s_part[kMkDecideThreads / 64];
+  BAState* stp = w.st;
+  if (stp->done) return;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    BAState& s = *stp;
+    double tc = 0, sc = 0;
+    for (int g = 0; g < w.gP; g++) {
+      tc += w.p4part[2 * g];
+      sc += w.p4part[2 * g + 1];
+    }
+    double tempChi = tc;
+    const double lastTrialChi = tempChi;
+    if (!s.ok2) tempChi = DBL_MAX;
+    double scale = s.scale_p + sc;
+    double rho = s.currentChi - tempChi;
+    scale += 1e-3;
+    rho /= scale;
+    if (rho > 0 && isfinite(tempChi)) {
+      double alpha = 1. - pow((2 * rho - 1), 3);
+      alpha = fmin(alpha, 2. / 3.);
+      s.lambda *= fmax(1. / 3., alpha);
+      s.ni = 2;
+      s.currentChi = tempChi;
+      s.cb = 1 - s.cb;  // the trial becomes the current estimate
+    } else {
+      s.lambda *= s.ni;
+      s.ni *= 2;
+    }
+    s.qmax++;
+    s.trials[s.round]++;
+    int round_end = 0;
+    if (rho < 0 && s.qmax < 10) {
+      s.need_lin = 0;  // another trial of this iteration
+    } else {
+      bool ok = true;
+      if (s.qmax == 10 || rho == 0) ok = false;
+      if (ok) {
+        if ((s.iniChi - s.currentChi) * 1e3 < s.iniChi)
+          s.nBad++;
+        else
+          s.nBad = 0;
+        if (s.nBad >= 3) ok = false;
+      }
+      if (s.chk < lastTrialChi && s.iter > 0) ok = false;
+      s.chk = lastTrialChi;
+      s.it_done[s.round] = s.iter + 1;
+      s.iter++;
+      s.qmax = 0;
+      s.need_lin = 1;
+      if (!ok || s.iter == (s.round == 0 ? 5 : 10)) round_end = 1;
+    }
+    if (round_end && s.round == 1) {
+      s.done = 1;
+      round_end = 0;
+    }
+    s_round_end = round_end;
+  }
+  __syncthreads();
+  if (!s_round_end) return;
+  // ---- round 2: the observations that fail the inlier test on the last computed errors (or sit
+  // behind the camera) set aside (level 1), every kernel dropped, the solver's x reset
+  const int cb = stp->cb;
+  const Cam cam = ba_cam(d);
+  (void)cam;
+  const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
+  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
+  for (int e = tid; e < d.n_edge; e += kMkDecideThreads) {
+    const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
+    const double chi = edge_chi2(&w.err[3 * (size_t)e], (double)d.e_s[e], stereo);
+    double pc[3];
+    se3_map(pose[d.e_kf[e]], &Xc[3 * (size_t)d.e_pt[e]], pc);
+    if (chi > (stereo ? 7.815 : 5.991) || !(pc[2] > 0.0)) w.level[e] = 1;
+  }
+  for (int k = tid; k < d.n_kf; k += kMkDecideThreads) w.kf_act[k] = 0;
+  const size_t n6 = 6 * (size_t)d.n_opt;
+  for (size_t q = tid; q < n6 + 3 * (size_t)d.n_pt; q += kMkDecideThreads) w.x[q] = 0;
+  __syncthreads();
+  int nact = 0;
+  for (int j = tid; j < d.n_pt; j += kMkDecideThreads) {
+    uint8_t a = 0;
+    for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++)
+      if (w.level[e] == 0) {
+        a = 1;
+        if (d.opt_of[d.e_kf[e]] >= 0) w.kf_act[d.e_kf[e]] = 1;  // every writer stores 1
+      }
+    w.pt_act[j] = a;
+    nact += a;
+  }
+  double na = wave_sum_dpp((double)nact);
+  if ((tid & 63) == 0) s_part[tid >> 6] = na;
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0;
+    for (int q = 0; q < kMkDecideThreads / 64; q++) t += s_part[q];
+    BAState& s = *stp;
+    s.round = 1;
+    s.iter = 0;
+    s.qmax = 0;
+    s.need_lin = 1;
+    s.lam_init = 1;
+    s.lambda = 0;
+    s.ni = 2;
+    s.chk = 0;
+    s.nBad = 0;
+    s.nact = (int)t;
+    if (t == 0) s.done = 1;
+  }
+}
+
+// the erase test (Optimizer.cc:3603-3631) and the recovered estimates
+__global__ __launch_bounds__(kMkDecideThreads) void k_ba2_finish(BADesc d, BAWork2 w) {
+  __shared__ double s_part[kMkDecideThreads / 64];
+  const int tid = threadIdx.x;
+  const int cb = w.st->cb;
+  const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
+  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
+  int nerase = 0;
+  for (int e = tid; e < d.n_edge; e += kMkDecideThreads) {
+    const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
+    const double chi = edge_chi2(&w.err[3 * (size_t)e], (double)d.e_s[e], stereo);
+    double pc[3];
+    se3_map(pose[d.e_kf[e]], &Xc[3 * (size_t)d.e_pt[e]], pc);
+    const bool er = chi > (stereo ? 7.815 : 5.991) || !(pc[2] > 0.0);
+    d.erase[e] = er ? 1 : 0;
+    nerase += er;
+  }
+  for (int k = tid; k < d.n_kf; k += kMkDecideThreads) dse3_to_float(pose[k], d.T_out + 16 * (size_t)k);
+  for (int q = tid; q < 3 * d.n_pt; q += kMkDecideThreads) d.X_out[q] = (float)Xc[q];
+  const double na = wave_sum_dpp((double)nerase);
+  if ((tid & 63) == 0) s_part[tid >> 6] = na;
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0;
+    for (int q = 0; q < kMkDecideThreads / 64; q++) t += s_part[q];
+    const BAState& s = *w.st;
+    d.stats[0] = s.it_done[0];
+    d.stats[1] = s.it_done[1];
+    d.stats[2] = s.trials[0];
+    d.stats[3] = s.trials[1];
+    d.stats[4] = (int)t;
+  }
+}
+
+}  // namespace
+
 size_t ba_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt) {
   const size_t n6 = 6 * (size_t)n_opt;
   const size_t nd = 14 * (size_t)n_kf + (3 + 3 + 9 + 3 + 9) * (size_t)n_pt +
                     (3 + 18 + 18 + 6) * (size_t)n_edge + 42 * (size_t)n_opt + n6 + 3 * (size_t)n_pt +
                     n6 * n6 + 3 * n6;
   return 8 * nd + (size_t)n_edge + n_kf + n_pt + 64;
+}
+
+size_t ba2_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt, int n_blk, int gP) {
+  auto a = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t n6 = 6 * (size_t)n_opt;
+  return a(sizeof(BAState)) + a(sizeof(DSE3) * 2 * (size_t)n_kf) + a(8 * 6 * (size_t)n_pt) +
+         a(8 * 9 * (size_t)n_pt) + a(8 * 3 * (size_t)n_pt) + a(8 * 9 * (size_t)n_pt) +
+         a(8 * 3 * (size_t)n_edge) + a(8 * 18 * (size_t)n_edge) + a(8 * 27 * (size_t)n_edge) +
+         a(8 * 18 * (size_t)n_edge) + a(8 * 6 * (size_t)n_edge) + a(8 * 36 * (size_t)n_opt) +
+         a(8 * 6 * (size_t)n_opt) + a(8 * 6 * (size_t)n_opt) + a(8 * 36 * (size_t)n_blk) +
+         a(8 * (n6 + 3 * (size_t)n_pt)) + a(8 * n6 * n6) + a(8 * 3 * n6) + 2 * a(8 * 2 * (size_t)gP) +
+         a((size_t)n_edge) + a((size_t)n_kf) + a((size_t)n_pt) + 64;
 }
 
 void launch_local_ba(const BADesc& d, hipStream_t st) {
@@ -735,6 +1435,8 @@ void launch_local_ba(const BADesc& d, hipStream_t st) {
 static size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 BARunner::~BARunner() {
+  if (d_ws2_) (void)hipFree(d_ws2_);
+  if (h_flag_) (void)hipHostFree(h_flag_);
   if (d_up_) (void)hipFree(d_up_);
   if (d_dn_) (void)hipFree(d_dn_);
   if (d_ws_) (void)hipFree(d_ws_);
@@ -856,7 +1558,81 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
   d.X_out = (float*)(d_dn_ + o_X);
   d.erase = d_dn_ + o_er;
   d.stats = (int*)(d_dn_ + o_st);
-  launch_local_ba(d, st);
+  static const bool onewg = [] {  // MMT_BA_ONEWG=1: the one-workgroup kernel (A/B and fallback)
+    const char* e = getenv("MMT_BA_ONEWG");
+    return e && atoi(e) != 0;
+  }();
+  if (onewg) {
+    launch_local_ba(d, st);
+  } else {
+    const int gP = std::max(1, (nP + kMkThreads - 1) / kMkThreads);
+    const int n6 = 6 * nO, nblk = (int)blocks.size();
+    const size_t wsb2 = ba2_workspace_bytes(nK, nP, nE, nO, nblk, gP);
+    if (wsb2 > ws2_cap_ || !d_ws2_) {
+      MMT_HIP(hipStreamSynchronize(st));
+      if (d_ws2_) (void)hipFree(d_ws2_);
+      ws2_cap_ = wsb2 + (wsb2 >> 1);
+      MMT_HIP(hipMalloc((void**)&d_ws2_, ws2_cap_));
+    }
+    if (!h_flag_) MMT_HIP(hipHostMalloc((void**)&h_flag_, 64, hipHostMallocDefault));
+    BAWork2 w;
+    uint8_t* p = d_ws2_;
+    auto take = [&](size_t bytes) {
+      uint8_t* r = p;
+      p += al16(bytes);
+      return r;
+    };
+    w.st = (BAState*)take(sizeof(BAState));
+    w.pose = (DSE3*)take(sizeof(DSE3) * 2 * (size_t)nK);
+    w.X = (double*)take(8 * 6 * (size_t)nP);
+    w.Hll = (double*)take(8 * 9 * (size_t)nP);
+    w.bl = (double*)take(8 * 3 * (size_t)nP);
+    w.Dinv = (double*)take(8 * 9 * (size_t)nP);
+    w.err = (double*)take(8 * 3 * (size_t)nE);
+    w.Hpl = (double*)take(8 * 18 * (size_t)nE);
+    w.Hpe = (double*)take(8 * 27 * (size_t)nE);
+    w.Y = (double*)take(8 * 18 * (size_t)nE);
+    w.cv = (double*)take(8 * 6 * (size_t)nE);
+    w.Hpp = (double*)take(8 * 36 * (size_t)nO);
+    w.bp = (double*)take(8 * 6 * (size_t)nO);
+    w.cvs = (double*)take(8 * 6 * (size_t)nO);
+    w.Sblk = (double*)take(8 * 36 * (size_t)nblk);
+    w.x = (double*)take(8 * ((size_t)n6 + 3 * (size_t)nP));
+    w.S = (double*)take(8 * (size_t)n6 * n6);
+    w.vec = (double*)take(8 * 3 * (size_t)n6);
+    w.linpart = (double*)take(8 * 2 * (size_t)gP);
+    w.p4part = (double*)take(8 * 2 * (size_t)gP);
+    w.level = take((size_t)nE);
+    w.kf_act = take((size_t)nK);
+    w.pt_act = take((size_t)nP);
+    w.gP = gP;
+    hipLaunchKernelGGL(k_ba2_init, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+    MMT_HIP(hipGetLastError());
+    // A trial is at most 7 launches; a solve at most 5 x 10 + 10 x 10 trials.  The first batch
+    // covers a typical solve (about 15 trials on the C3 sequence), later ones are short.
+    int slots = 0;
+    for (bool done = nE == 0; !done;) {
+      const int batch = slots == 0 ? 16 : 4;
+      for (int b = 0; b < batch; b++) {
+        hipLaunchKernelGGL(k_ba2_lin, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        if (nO > 0) hipLaunchKernelGGL(k_ba2_kfsum, dim3(nO), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p1, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        if (nblk + nO > 0)
+          hipLaunchKernelGGL(k_ba2_p2, dim3(nblk + nO), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p3, dim3(1), dim3(kMkSolveThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p4, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p5, dim3(1), dim3(kMkDecideThreads), 0, st, d, w);
+      }
+      MMT_HIP(hipGetLastError());
+      slots += batch;
+      MMT_HIP(hipMemcpyAsync(h_flag_, &w.st->done, sizeof(int), hipMemcpyDeviceToHost, st));
+      MMT_HIP(hipStreamSynchronize(st));
+      done = *h_flag_ != 0;
+      if (!done && slots >= 160) throw DeviceError("local BA: the LM did not finish in 150 trials");
+    }
+    hipLaunchKernelGGL(k_ba2_finish, dim3(1), dim3(kMkDecideThreads), 0, st, d, w);
+    MMT_HIP(hipGetLastError());
+  }
   MMT_HIP(hipMemcpyAsync(h_dn_, d_dn_, dn, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
   memcpy(T_out, h_dn_, 64 * (size_t)nK);

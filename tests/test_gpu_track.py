@@ -243,6 +243,11 @@ def _long_parity(oracle_mod, w, h, nfeat, n, seed, objects, lanes=None, parts=1,
     tr = oracle_mod.Tracker(w, h, K_KITTI, 387.5744, 0, nfeat)
     ora = [tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]) for f in frames]
     rec = compare.parity_record(got, ora)
+    print(rec)
+    if rec["first_divergent_frame"] is not None:  # the frames up to the divergence
+        k = rec["first_divergent_frame"]
+        print("up to frame", k, compare.parity_record(got[:k], ora[:k]))
+        print("gpu", got[k]["objects"], "\noracle", ora[k]["objects"])
     assert rec["first_divergent_frame"] is None, rec
     return got, rec
 
