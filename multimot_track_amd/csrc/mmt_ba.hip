@@ -31,6 +31,8 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <cstdio>
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -747,6 +749,7 @@ struct BAState {
   int done, round, iter, qmax, need_lin, lam_init, cb, ok2, nBad, nact;
   int it_done[2], trials[2];
   double lambda, ni, chk, currentChi, iniChi, scale_p;
+  long long prof[8];  // k_ba2_p3 phase times (wall clock ticks, 100 MHz), summed over trials
 };
 
 struct BAWork2 {
@@ -768,6 +771,14 @@ struct BAWork2 {
   double* x;        // 6 n_opt + 3 n_pt (g2o's _x: poses, then points)
   double* S;        // n6 x n6 when the reduced system does not fit in LDS
   double* vec;      // 3 n6 (idem)
+  const int4* kitem;        // keyframe items: (optimised keyframe, kf_edges range of <= 256)
+  const int* kitem_start;   // n_opt + 1: each optimised keyframe's items
+  const int4* bitem;        // block items: (block, trip range of <= 256)
+  const int* bitem_start;   // n_blk + 1
+  int n_kitem, n_bitem;
+  double* Hpart;    // 27 per keyframe item: its edges' pose terms
+  double* Spart;    // 36 per block item: its triples' sum of Y H_pl^T
+  double* cvpart;   // 6 per keyframe item: its edges' H_pl D^-1 b_l
   double* linpart;  // 2 per point workgroup: chi2, largest active H_ll diagonal
   double* p4part;   // 2 per point workgroup: trial chi2, scale
   uint8_t* level;   // n_edge
@@ -814,13 +825,33 @@ __device__ __forceinline__ double wg_maxN(double v, double* part) {
 
 // computeLambdaInit over the round's vertices: 1e-5 x the largest diagonal entry of the active
 // optimised keyframes' H_pp and the active points' H_ll (the latter from k_ba2_lin's partials)
-__device__ __forceinline__ double ba2_lambda_init(const BADesc& d, const BAWork2& w) {
-  double m = 0;
-  for (int g = 0; g < w.gP; g++) m = fmax(m, w.linpart[2 * g + 1]);
-  for (int a = 0; a < d.n_opt; a++)
-    if (w.kf_act[d.opt_kf[a]])
-      for (int r = 0; r < 6; r++) m = fmax(m, fabs(w.Hpp[36 * (size_t)a + 7 * r]));
-  return 1e-5 * m;
+// the upper-triangle index of H_pp entry (r, r) in the 21 pose terms (rows r0, columns c0 >= r0)
+__device__ __forceinline__ int ba2_diag_q(int r) { return 6 * r - r * (r - 1) / 2; }
+
+// keyframe a's sum of pose term q over its items, in item order (k_ba2_p1 and k_ba2_p3 both
+// compute H_pp this way: the same bits)
+__device__ __forceinline__ double ba2_hsum(const BAWork2& w, int a, int q) {
+  double s = 0;
+  for (int it = w.kitem_start[a]; it < w.kitem_start[a + 1]; it++) s += w.Hpart[27 * (size_t)it + q];
+  return s;
+}
+
+// computed by wave 0 (lanes over the point workgroups and the (keyframe, diagonal) pairs) and
+// returned to every thread of the workgroup through `sh` (one barrier)
+__device__ __forceinline__ double ba2_lambda_init(const BADesc& d, const BAWork2& w, double* sh) {
+  if (threadIdx.x < 64) {
+    double m = 0;
+    for (int g = threadIdx.x; g < w.gP; g += 64) m = fmax(m, w.linpart[2 * g + 1]);
+    for (int q = threadIdx.x; q < 6 * d.n_opt; q += 64) {
+      const int a = q / 6;
+      if (w.kf_act[d.opt_kf[a]]) m = fmax(m, fabs(ba2_hsum(w, a, ba2_diag_q(q % 6))));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (threadIdx.x == 0) *sh = 1e-5 * m;
+  }
+  __syncthreads();
+  return *sh;
 }
 
 __device__ __forceinline__ Cam ba_cam(const BADesc& d) { return Cam{d.fx, d.fy, d.cx, d.cy, d.bf}; }
@@ -957,37 +988,28 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
   }
 }
 
-// buildSystem's keyframe side: one workgroup per optimised keyframe sums its active edges' pose terms
+// buildSystem's keyframe side: one workgroup per keyframe item (<= 256 edges of one optimised
+// keyframe, one per thread) sums its active edges' pose terms into Hpart
 __global__ __launch_bounds__(kMkThreads) void k_ba2_kfsum(BADesc d, BAWork2 w) {
   __shared__ double s_part[27 * kMkWaves];
   __shared__ double s_out[32];
   const BAState* st = w.st;
   if (st->done || !st->need_lin) return;
-  const int a = blockIdx.x;
+  const int4 it = w.kitem[blockIdx.x];
+  const int t = it.y + threadIdx.x;
   double acc[27];
 #pragma unroll
   for (int q = 0; q < 27; q++) acc[q] = 0;
-  for (int t = d.kf_start[a] + threadIdx.x; t < d.kf_start[a + 1]; t += kMkThreads) {
+  if (t < it.z) {
     const int e = d.kf_edges[t];
-    if (w.level[e]) continue;
-    const double* h = &w.Hpe[27 * (size_t)e];
+    if (!w.level[e]) {
+      const double* h = &w.Hpe[27 * (size_t)e];
 #pragma unroll
-    for (int q = 0; q < 27; q++) acc[q] += h[q];
+      for (int q = 0; q < 27; q++) acc[q] = h[q];
+    }
   }
   wg_sumK<27, kMkWaves>(acc, s_part, s_out);
-  const int q = threadIdx.x;
-  if (q < 21) {
-    int r0 = 0, k = q;
-    while (k >= 6 - r0) {
-      k -= 6 - r0;
-      r0++;
-    }
-    const int c0 = r0 + k;
-    w.Hpp[36 * (size_t)a + 6 * r0 + c0] = s_out[q];
-    w.Hpp[36 * (size_t)a + 6 * c0 + r0] = s_out[q];
-  } else if (q < 27) {
-    w.bp[6 * (size_t)a + q - 21] = s_out[q];
-  }
+  if (threadIdx.x < 27) w.Hpart[27 * (size_t)blockIdx.x + threadIdx.x] = s_out[threadIdx.x];
 }
 
 // trial step 1, one thread per active point: D^-1 = (H_ll + lambda I)^-1 (Eigen's cofactor
@@ -995,9 +1017,10 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_kfsum(BADesc d, BAWork2 w) {
 __global__ __launch_bounds__(kMkThreads) void k_ba2_p1(BADesc d, BAWork2 w) {
   const BAState* st = w.st;
   if (st->done) return;
+  __shared__ double s_lam;
+  const double lambda = st->lam_init ? ba2_lambda_init(d, w, &s_lam) : st->lambda;
   const int j = blockIdx.x * kMkThreads + threadIdx.x;
   if (j >= d.n_pt || !w.pt_act[j]) return;
-  const double lambda = st->lam_init ? ba2_lambda_init(d, w) : st->lambda;
   double Dm[9], Di[9];
 #pragma unroll
   for (int q = 0; q < 9; q++) Dm[q] = w.Hll[9 * (size_t)j + q] + ((q % 4) == 0 ? lambda : 0.0);
@@ -1023,46 +1046,53 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p1(BADesc d, BAWork2 w) {
   }
 }
 
-// trial step 2: the Schur sums, one workgroup per keyframe-pair block (its (edge, edge) triples)
-// and one per optimised keyframe (its edges' H_pl D^-1 b_l)
+// trial step 2: the Schur sums, one workgroup per block item (<= 256 (edge, edge) triples of one
+// keyframe-pair block, one per thread) and per keyframe item (its edges' H_pl D^-1 b_l)
 __global__ __launch_bounds__(kMkThreads) void k_ba2_p2(BADesc d, BAWork2 w) {
   __shared__ double s_part[36 * kMkWaves];
   __shared__ double s_out[64];
   const BAState* st = w.st;
   if (st->done) return;
-  if ((int)blockIdx.x < d.n_blk) {
-    const int bk = blockIdx.x;
+  if ((int)blockIdx.x < w.n_bitem) {
+    const int4 it = w.bitem[blockIdx.x];
+    const int t = it.y + threadIdx.x;
     double acc[36];
 #pragma unroll
     for (int q = 0; q < 36; q++) acc[q] = 0;
-    for (int t = d.blk_start[bk] + threadIdx.x; t < d.blk_start[bk + 1]; t += kMkThreads) {
+    if (t < it.z) {
       const int2 tr = d.trip[t];
-      if (w.level[tr.x] || w.level[tr.y]) continue;
-      const double* Ye = &w.Y[18 * (size_t)tr.x];
-      const double* B2 = &w.Hpl[18 * (size_t)tr.y];
-      double h2[18];
+      if (!w.level[tr.x] && !w.level[tr.y]) {
+        const double* Ye = &w.Y[18 * (size_t)tr.x];
+        const double* B2 = &w.Hpl[18 * (size_t)tr.y];
+        double h2[18], y[18];
 #pragma unroll
-      for (int q = 0; q < 18; q++) h2[q] = B2[q];
+        for (int q = 0; q < 18; q++) {
+          h2[q] = B2[q];
+          y[q] = Ye[q];
+        }
 #pragma unroll
-      for (int r = 0; r < 6; r++) {
-        const double y0 = Ye[3 * r], y1 = Ye[3 * r + 1], y2 = Ye[3 * r + 2];
+        for (int r = 0; r < 6; r++)
 #pragma unroll
-        for (int c = 0; c < 6; c++) acc[6 * r + c] += y0 * h2[3 * c] + y1 * h2[3 * c + 1] + y2 * h2[3 * c + 2];
+          for (int c = 0; c < 6; c++)
+            acc[6 * r + c] = y[3 * r] * h2[3 * c] + y[3 * r + 1] * h2[3 * c + 1] + y[3 * r + 2] * h2[3 * c + 2];
       }
     }
     wg_sumK<36, kMkWaves>(acc, s_part, s_out);
-    if (threadIdx.x < 36) w.Sblk[36 * (size_t)bk + threadIdx.x] = s_out[threadIdx.x];
+    if (threadIdx.x < 36) w.Spart[36 * (size_t)blockIdx.x + threadIdx.x] = s_out[threadIdx.x];
   } else {
-    const int a = blockIdx.x - d.n_blk;
+    const int ki = blockIdx.x - w.n_bitem;
+    const int4 it = w.kitem[ki];
+    const int t = it.y + threadIdx.x;
     double cs[6] = {0, 0, 0, 0, 0, 0};
-    for (int t = d.kf_start[a] + threadIdx.x; t < d.kf_start[a + 1]; t += kMkThreads) {
+    if (t < it.z) {
       const int e = d.kf_edges[t];
-      if (w.level[e]) continue;
+      if (!w.level[e]) {
 #pragma unroll
-      for (int r = 0; r < 6; r++) cs[r] += w.cv[6 * (size_t)e + r];
+        for (int r = 0; r < 6; r++) cs[r] = w.cv[6 * (size_t)e + r];
+      }
     }
     wg_sumK<6, kMkWaves>(cs, s_part, s_out);
-    if (threadIdx.x < 6) w.cvs[6 * (size_t)a + threadIdx.x] = s_out[threadIdx.x];
+    if (threadIdx.x < 6) w.cvpart[6 * (size_t)ki + threadIdx.x] = s_out[threadIdx.x];
   }
 }
 
@@ -1073,20 +1103,54 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p2(BADesc d, BAWork2 w) {
 __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w) {
   __shared__ double s_S[kLdsRows * kLdsRows];
   __shared__ double s_vec[3 * kLdsRows];
+  __shared__ double s_vec2[2];
   __shared__ int s_ok;
   BAState* stp = w.st;
   if (stp->done) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n6 = 6 * d.n_opt;
+  long long pt[6];
+  pt[0] = wall_clock64();
   const bool lam_init = stp->lam_init != 0, need_lin = stp->need_lin != 0;
   const int cb = stp->cb;
-  const double lambda = lam_init ? ba2_lambda_init(d, w) : stp->lambda;
+  __shared__ double s_lam;
+  const double lambda = lam_init ? ba2_lambda_init(d, w, &s_lam) : stp->lambda;
   double* S = n6 <= kLdsRows ? s_S : w.S;
   double* bs = n6 <= kLdsRows ? s_vec : w.vec;
   double* Dg = bs + n6;
   double* yv = Dg + n6;
+  // the item partials summed in item order: H_pp, b_p, sum of H_pl D^-1 b_l, the block sums
+  for (int q = tid; q < d.n_opt * 27; q += kMkSolveThreads) {
+    const int a = q / 27, k = q % 27;
+    const double v = ba2_hsum(w, a, k);
+    if (k < 21) {
+      int r0 = 0, kk = k;
+      while (kk >= 6 - r0) {
+        kk -= 6 - r0;
+        r0++;
+      }
+      const int c0 = r0 + kk;
+      w.Hpp[36 * (size_t)a + 6 * r0 + c0] = v;
+      w.Hpp[36 * (size_t)a + 6 * c0 + r0] = v;
+    } else {
+      w.bp[6 * (size_t)a + k - 21] = v;
+    }
+  }
+  for (int q = tid; q < d.n_opt * 6; q += kMkSolveThreads) {
+    const int a = q / 6, k = q % 6;
+    double v = 0;
+    for (int it = w.kitem_start[a]; it < w.kitem_start[a + 1]; it++) v += w.cvpart[6 * (size_t)it + k];
+    w.cvs[q] = v;
+  }
+  for (int q = tid; q < d.n_blk * 36; q += kMkSolveThreads) {
+    const int bk = q / 36, k = q % 36;
+    double v = 0;
+    for (int it = w.bitem_start[bk]; it < w.bitem_start[bk + 1]; it++) v += w.Spart[36 * (size_t)it + k];
+    w.Sblk[q] = v;
+  }
   for (int q = tid; q < n6 * n6; q += kMkSolveThreads) S[q] = 0;
   __syncthreads();
+  pt[1] = wall_clock64();
   for (int q = tid; q < d.n_blk * 36; q += kMkSolveThreads) {
     const int bk = q / 36, k = q % 36, r = k / 6, c = k % 6;
     const int a = d.blk_ab[2 * bk], b = d.blk_ab[2 * bk + 1];
@@ -1102,7 +1166,59 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
     if (i > j) S[q] = S[(size_t)j * n6 + i];
   }
   __syncthreads();
+  __shared__ double s_Lrow[64 * 64];  // L row-major (the backward substitution), n6 <= 64
   bool ok = true;
+  pt[2] = pt[3] = wall_clock64();
+  if (n6 <= 64) {
+    // One wave, lane i = row i.  S holds the upper triangle row-major, i.e. the lower triangle
+    // column-major: entry (i, j), i >= j, at S[j n6 + i], so a column is one coalesced LDS row.
+    // Step k: L(i, k) = S(i, k) / d_k in lane i, broadcast to the update of column jj by readlane;
+    // every entry sees the left-looking sequence of operations of the CPU checker.
+    if (wave == 0) {
+      for (int k = 0; k < n6 && ok; k++) {
+        const double dk = S[(size_t)k * n6 + k];
+        if (dk == 0) {
+          ok = false;
+          break;
+        }
+        double lik = 0;
+        if (lane > k && lane < n6) {
+          lik = S[(size_t)k * n6 + lane] / dk;
+          S[(size_t)k * n6 + lane] = lik;
+          s_Lrow[lane * 64 + k] = lik;
+        }
+        if (lane == 0) Dg[k] = dk;
+        for (int jj = k + 1; jj < n6; jj++) {
+          const double ljk = lane_value(lik, jj);
+          if (lane >= jj && lane < n6) S[(size_t)jj * n6 + lane] -= lik * ljk * dk;
+        }
+        wave_sync_lds();
+      }
+      pt[3] = wall_clock64();
+      if (!ok) {
+        if (lane == 0) s_ok = 0;
+      } else {
+        double y = lane < n6 ? bs[lane] : 0.0;
+        double lnext = lane < n6 ? S[lane] : 0.0;
+        for (int c = 0; c < n6; c++) {  // forward, L(i, c) = S[c n6 + i]
+          const double l = lnext;
+          if (c + 1 < n6 && lane < n6) lnext = S[(size_t)(c + 1) * n6 + lane];
+          const double yc = lane_value(y, c);
+          if (lane > c && lane < n6) y -= l * yc;
+        }
+        if (lane < n6) y /= Dg[lane];
+        for (int r = n6 - 1; r > 0; r--) {  // backward, L(r, i) = s_Lrow[r][i]
+          const double yr = lane_value(y, r);
+          if (lane < r) y -= s_Lrow[r * 64 + lane] * yr;
+        }
+        if (lane < n6) w.x[lane] = y;
+      }
+    }
+  } else {
+  // One barrier per column: step k reads column k of the (updated) lower triangle, each thread
+  // forms the L entries it needs itself (L(i, k) = S(i, k) / d_k, the same rounding as a stored
+  // one), updates its entries of the trailing lower triangle, and L(i, k) is kept in the upper
+  // triangle at (k, i), which no step reads any more.
   for (int k = 0; k < n6; k++) {
     const double dk = S[(size_t)k * n6 + k];
     if (dk == 0) {  // uniform: every thread reads the same value
@@ -1110,35 +1226,57 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
       break;
     }
     if (tid == 0) Dg[k] = dk;
-    for (int i = k + 1 + tid; i < n6; i += kMkSolveThreads) S[(size_t)i * n6 + k] /= dk;
-    __syncthreads();
-    const int m = n6 - k - 1;
-    for (int q = tid; q < m * m; q += kMkSolveThreads) {
-      const int i = k + 1 + q / m, jj = k + 1 + q % m;
-      if (jj <= i) S[(size_t)i * n6 + jj] -= S[(size_t)i * n6 + k] * S[(size_t)jj * n6 + k] * dk;
+    // 64 row slots x 8 column lanes
+    for (int i = k + 1 + (tid >> 3); i < n6; i += kMkSolveThreads / 8) {
+      const double lik = S[(size_t)i * n6 + k] / dk;
+      for (int jj = k + 1 + (tid & 7); jj <= i; jj += 8)
+        S[(size_t)i * n6 + jj] -= lik * (S[(size_t)jj * n6 + k] / dk) * dk;
+      if ((tid & 7) == 0) S[(size_t)k * n6 + i] = lik;
     }
     __syncthreads();
   }
+  pt[3] = wall_clock64();
   if (!ok) {
     if (tid == 0) s_ok = 0;
   } else if (wave == 0) {
-    for (int i = lane; i < n6; i += 64) yv[i] = bs[i];
-    wave_sync_lds();
-    for (int c = 0; c < n6; c++) {
-      const double yc = yv[c];
-      for (int i = c + 1 + lane; i < n6; i += 64) yv[i] -= S[(size_t)i * n6 + c] * yc;
+    // substitutions with y in registers (lane i: rows i, i + 64), y[c] broadcast by readlane
+    double y0 = lane < n6 ? bs[lane] : 0.0, y1 = lane + 64 < n6 ? bs[lane + 64] : 0.0;
+    if (n6 <= 128) {
+      for (int c = 0; c < n6; c++) {  // forward, L(i, c) = S(c, i)
+        const double yc = c < 64 ? lane_value(y0, c) : lane_value(y1, c - 64);
+        if (lane > c && lane < n6) y0 -= S[(size_t)c * n6 + lane] * yc;
+        if (lane + 64 > c && lane + 64 < n6) y1 -= S[(size_t)c * n6 + lane + 64] * yc;
+      }
+      if (lane < n6) y0 /= Dg[lane];
+      if (lane + 64 < n6) y1 /= Dg[lane + 64];
+      for (int r = n6 - 1; r > 0; r--) {  // backward, L(r, i) = S(i, r)
+        const double yr = r < 64 ? lane_value(y0, r) : lane_value(y1, r - 64);
+        if (lane < r) y0 -= S[(size_t)lane * n6 + r] * yr;
+        if (lane + 64 < r) y1 -= S[(size_t)(lane + 64) * n6 + r] * yr;
+      }
+      if (lane < n6) w.x[lane] = y0;
+      if (lane + 64 < n6) w.x[lane + 64] = y1;
+    } else {
+      for (int i = lane; i < n6; i += 64) yv[i] = bs[i];
       wave_sync_lds();
-    }
-    for (int i = lane; i < n6; i += 64) yv[i] /= Dg[i];
-    wave_sync_lds();
-    for (int r = n6 - 1; r > 0; r--) {
-      const double yr = yv[r];
-      for (int i = lane; i < r; i += 64) yv[i] -= S[(size_t)r * n6 + i] * yr;
+      for (int c = 0; c < n6; c++) {
+        const double yc = yv[c];
+        for (int i = c + 1 + lane; i < n6; i += 64) yv[i] -= S[(size_t)c * n6 + i] * yc;
+        wave_sync_lds();
+      }
+      for (int i = lane; i < n6; i += 64) yv[i] /= Dg[i];
       wave_sync_lds();
+      for (int r = n6 - 1; r > 0; r--) {
+        const double yr = yv[r];
+        for (int i = lane; i < r; i += 64) yv[i] -= S[(size_t)i * n6 + r] * yr;
+        wave_sync_lds();
+      }
+      for (int i = lane; i < n6; i += 64) w.x[i] = yv[i];
     }
-    for (int i = lane; i < n6; i += 64) w.x[i] = yv[i];
+  }
   }
   __syncthreads();
+  pt[4] = wall_clock64();
   const bool ok2 = s_ok != 0;
   // the trial poses: exp(x_p) * pose for the round's optimised keyframes, the others unchanged
   const DSE3* cur = w.pose + (size_t)cb * d.n_kf;
@@ -1154,21 +1292,30 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
       tri[k] = cur[k];
     }
   }
-  if (tid == 0) {
-    double sp = 0;
-    for (int a = 0; a < d.n_opt; a++) {
-      if (!w.kf_act[d.opt_kf[a]]) continue;
-      for (int r = 0; r < 6; r++) {
-        const double xv = w.x[6 * a + r];
-        sp += xv * (lambda * xv + w.bp[6 * (size_t)a + r]);
+  // the poses' share of the scale term and the iteration's chi2, by wave 0 (fixed order)
+  if (wave == 0) {
+    double sp = 0, c = 0;
+    for (int i = lane; i < n6; i += 64)
+      if (w.kf_act[d.opt_kf[i / 6]]) {
+        const double xv = w.x[i];
+        sp += xv * (lambda * xv + w.bp[i]);
       }
+    if (need_lin)
+      for (int g = lane; g < w.gP; g += 64) c += w.linpart[2 * g];
+    sp = wave_sum_dpp(sp);
+    c = wave_sum_dpp(c);
+    if (lane == 0) {
+      s_vec2[0] = sp;
+      s_vec2[1] = c;
     }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double sp = s_vec2[0];
     BAState& s = *stp;
     if (need_lin) {
-      double c = 0;
-      for (int g = 0; g < w.gP; g++) c += w.linpart[2 * g];
-      s.currentChi = c;
-      s.iniChi = c;
+      s.currentChi = s_vec2[1];
+      s.iniChi = s_vec2[1];
     }
     if (lam_init) {
       s.lam_init = 0;
@@ -1176,6 +1323,8 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
       s.nBad = 0;
     }
     s.lambda = lambda;
+    pt[5] = wall_clock64();
+    for (int q = 0; q < 5; q++) s.prof[q] += pt[q + 1] - pt[q];
     s.ok2 = ok2 ? 1 : 0;
     s.scale_p = sp;
   }
@@ -1261,16 +1410,27 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
 __global__ __launch_bounds__(kMkDecideThreads) void k_ba2_p5(BADesc d, BAWork2 w) {
   __shared__ int s_round_end;
   __shared__ double s_part[kMkDecideThreads / 64];
+  __shared__ double s_sum[2];
   BAState* stp = w.st;
   if (stp->done) return;
   const int tid = threadIdx.x;
+  if (tid < 64) {  // the trial's chi2 and scale over the point workgroups (wave 0, fixed order)
+    double a = 0, b = 0;
+    for (int g = tid; g < w.gP; g += 64) {
+      a += w.p4part[2 * g];
+      b += w.p4part[2 * g + 1];
+    }
+    a = wave_sum_dpp(a);
+    b = wave_sum_dpp(b);
+    if (tid == 0) {
+      s_sum[0] = a;
+      s_sum[1] = b;
+    }
+  }
+  __syncthreads();
   if (tid == 0) {
     BAState& s = *stp;
-    double tc = 0, sc = 0;
-    for (int g = 0; g < w.gP; g++) {
-      tc += w.p4part[2 * g];
-      sc += w.p4part[2 * g + 1];
-    }
+    const double tc = s_sum[0], sc = s_sum[1];
     double tempChi = tc;
     const double lastTrialChi = tempChi;
     if (!s.ok2) tempChi = DBL_MAX;
@@ -1454,8 +1614,25 @@ void BARunner::grow(uint8_t*& d, uint8_t*& h, size_t& cap, size_t need, hipStrea
   MMT_HIP(hipHostMalloc((void**)&h, cap, hipHostMallocDefault));
 }
 
+namespace {
+double ba_now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// MMT_BA_PROFILE=1: host wall time of BARunner::run's phases, printed every 32 solves
+struct BAHostProf {
+  bool on = getenv("MMT_BA_PROFILE") != nullptr;
+  double t[5] = {0, 0, 0, 0, 0};  // layout, launches, waits, finish, total
+  long long p3[5] = {0, 0, 0, 0, 0};  // k_ba2_p3 phases (ticks of 10 ns)
+  long n = 0, slots = 0;
+};
+BAHostProf g_ba_prof;
+}  // namespace
+
 void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* X_out,
                    uint8_t* erase, int* stats) {
+  BAHostProf& hp = g_ba_prof;
+  const double tp0 = hp.on ? ba_now_us() : 0;
   const int nK = P.n_kf, nP = P.n_pt, nE = P.n_edge;
   for (int i = 0; i < nE; i++)
     if (P.e_pt[i] < 0 || P.e_pt[i] >= nP || P.e_kf[i] < 0 || P.e_kf[i] >= nK ||
@@ -1469,35 +1646,61 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     }
   const int nO = (int)opt_kf.size();
   std::vector<int> pt_start(nP + 1, 0), kf_start(nO + 1, 0), kf_edges;
-  std::vector<std::vector<int>> kfe(nO);
-  std::map<std::pair<int, int>, std::vector<int2>> blocks;
-  for (int a = 0; a < nO; a++) blocks[{a, a}];  // every diagonal block carries H_pp + lambda I
+  // the Schur triples grouped by keyframe-pair block (a <= b, blocks in (a, b) order, triples in
+  // point order): counted, then placed; every diagonal block exists (it carries H_pp + lambda I)
+  std::vector<int> bcnt((size_t)nO * nO, 0), kcnt(nO, 0);
   std::vector<std::pair<int, int>> col;
-  for (int j = 0, e = 0; j < nP; j++) {
+  auto point_col = [&](int& e, int j) {  // point j's edges to optimised keyframes, pose order
     col.clear();
     for (; e < nE && P.e_pt[e] == j; e++) {
       const int a = opt_of[P.e_kf[e]];
-      if (a < 0) continue;
-      kfe[a].push_back(e);
-      col.push_back({a, e});
+      if (a >= 0) col.push_back({a, e});
     }
-    pt_start[j + 1] = e;
     std::sort(col.begin(), col.end());  // pose-index order, as g2o's H_pl column
-    for (size_t p1 = 0; p1 < col.size(); p1++)
+  };
+  for (int j = 0, e = 0; j < nP; j++) {
+    point_col(e, j);
+    pt_start[j + 1] = e;
+    for (size_t p1 = 0; p1 < col.size(); p1++) {
+      kcnt[col[p1].first]++;
+      for (size_t p2 = p1; p2 < col.size(); p2++) bcnt[(size_t)col[p1].first * nO + col[p2].first]++;
+    }
+  }
+  std::vector<int> bid((size_t)nO * nO, -1), blk_ab, blk_start{0};
+  for (int a = 0; a < nO; a++)
+    for (int b = a; b < nO; b++)
+      if (a == b || bcnt[(size_t)a * nO + b] > 0) {
+        bid[(size_t)a * nO + b] = (int)blk_ab.size() / 2;
+        blk_ab.push_back(a);
+        blk_ab.push_back(b);
+        blk_start.push_back(blk_start.back() + bcnt[(size_t)a * nO + b]);
+      }
+  const int nblocks = (int)blk_ab.size() / 2;
+  for (int a = 0; a < nO; a++) kf_start[a + 1] = kf_start[a] + kcnt[a];
+  std::vector<int2> trip(blk_start.back());
+  kf_edges.resize(kf_start[nO]);
+  std::vector<int> bfill(blk_start.begin(), blk_start.end() - 1), kfill(kf_start.begin(), kf_start.end() - 1);
+  for (int j = 0, e = 0; j < nP; j++) {
+    point_col(e, j);
+    for (size_t p1 = 0; p1 < col.size(); p1++) {
+      kf_edges[kfill[col[p1].first]++] = col[p1].second;
       for (size_t p2 = p1; p2 < col.size(); p2++)
-        blocks[{col[p1].first, col[p2].first}].push_back(make_int2(col[p1].second, col[p2].second));
+        trip[bfill[bid[(size_t)col[p1].first * nO + col[p2].first]]++] =
+            make_int2(col[p1].second, col[p2].second);
+    }
   }
+  // work items of the multi-kernel solve: <= 256 edges of one keyframe, <= 256 triples of one block
+  std::vector<int4> kitem, bitem;
+  std::vector<int> kitem_start{0}, bitem_start{0};
   for (int a = 0; a < nO; a++) {
-    kf_edges.insert(kf_edges.end(), kfe[a].begin(), kfe[a].end());
-    kf_start[a + 1] = (int)kf_edges.size();
+    for (int t = kf_start[a]; t < kf_start[a + 1]; t += 256)
+      kitem.push_back(make_int4(a, t, std::min(t + 256, kf_start[a + 1]), 0));
+    kitem_start.push_back((int)kitem.size());
   }
-  std::vector<int> blk_ab, blk_start{0};
-  std::vector<int2> trip;
-  for (const auto& b : blocks) {
-    blk_ab.push_back(b.first.first);
-    blk_ab.push_back(b.first.second);
-    trip.insert(trip.end(), b.second.begin(), b.second.end());
-    blk_start.push_back((int)trip.size());
+  for (size_t bk = 0; bk + 1 < blk_start.size(); bk++) {
+    for (int t = blk_start[bk]; t < blk_start[bk + 1]; t += 256)
+      bitem.push_back(make_int4((int)bk, t, std::min(t + 256, blk_start[bk + 1]), 0));
+    bitem_start.push_back((int)bitem.size());
   }
   struct Seg {
     size_t bytes;
@@ -1509,7 +1712,9 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
                       {4 * (size_t)nE, P.e_kf},           {12 * (size_t)nE, P.e_obs},
                       {4 * (size_t)nE, P.e_s},            {4 * kf_start.size(), kf_start.data()},
                       {4 * kf_edges.size(), kf_edges.data()}, {4 * blk_ab.size(), blk_ab.data()},
-                      {4 * blk_start.size(), blk_start.data()}, {8 * trip.size(), trip.data()}};
+                      {4 * blk_start.size(), blk_start.data()}, {8 * trip.size(), trip.data()},
+                      {16 * kitem.size(), kitem.data()}, {4 * kitem_start.size(), kitem_start.data()},
+                      {16 * bitem.size(), bitem.data()}, {4 * bitem_start.size(), bitem_start.data()}};
   constexpr int nseg = sizeof(segs) / sizeof(segs[0]);
   size_t off[nseg], tot = 0;
   for (int i = 0; i < nseg; i++) {
@@ -1536,7 +1741,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
   d.n_pt = nP;
   d.n_edge = nE;
   d.n_opt = nO;
-  d.n_blk = (int)blocks.size();
+  d.n_blk = nblocks;
   const uint8_t* u = d_up_;
   d.Tcw = (const float*)(u + off[0]);
   d.opt_of = (const int*)(u + off[1]);
@@ -1566,8 +1771,9 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     launch_local_ba(d, st);
   } else {
     const int gP = std::max(1, (nP + kMkThreads - 1) / kMkThreads);
-    const int n6 = 6 * nO, nblk = (int)blocks.size();
-    const size_t wsb2 = ba2_workspace_bytes(nK, nP, nE, nO, nblk, gP);
+    const int n6 = 6 * nO, nblk = nblocks;
+    const size_t wsb2 = ba2_workspace_bytes(nK, nP, nE, nO, nblk, gP) +
+                        8 * (27 + 6) * kitem.size() + 8 * 36 * bitem.size() + 64 * 3;
     if (wsb2 > ws2_cap_ || !d_ws2_) {
       MMT_HIP(hipStreamSynchronize(st));
       if (d_ws2_) (void)hipFree(d_ws2_);
@@ -1597,6 +1803,15 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.bp = (double*)take(8 * 6 * (size_t)nO);
     w.cvs = (double*)take(8 * 6 * (size_t)nO);
     w.Sblk = (double*)take(8 * 36 * (size_t)nblk);
+    w.kitem = (const int4*)(u + off[14]);
+    w.kitem_start = (const int*)(u + off[15]);
+    w.bitem = (const int4*)(u + off[16]);
+    w.bitem_start = (const int*)(u + off[17]);
+    w.n_kitem = (int)kitem.size();
+    w.n_bitem = (int)bitem.size();
+    w.Hpart = (double*)take(8 * 27 * kitem.size());
+    w.Spart = (double*)take(8 * 36 * bitem.size());
+    w.cvpart = (double*)take(8 * 6 * kitem.size());
     w.x = (double*)take(8 * ((size_t)n6 + 3 * (size_t)nP));
     w.S = (double*)take(8 * (size_t)n6 * n6);
     w.vec = (double*)take(8 * 3 * (size_t)n6);
@@ -1606,6 +1821,8 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.kf_act = take((size_t)nK);
     w.pt_act = take((size_t)nP);
     w.gP = gP;
+    const double tp1 = hp.on ? ba_now_us() : 0;
+    double t_launch = 0, t_wait = 0;
     hipLaunchKernelGGL(k_ba2_init, dim3(gP), dim3(kMkThreads), 0, st, d, w);
     MMT_HIP(hipGetLastError());
     // A trial is at most 7 launches; a solve at most 5 x 10 + 10 x 10 trials.  The first batch
@@ -1613,12 +1830,14 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     int slots = 0;
     for (bool done = nE == 0; !done;) {
       const int batch = slots == 0 ? 16 : 4;
+      const double tl = hp.on ? ba_now_us() : 0;
       for (int b = 0; b < batch; b++) {
         hipLaunchKernelGGL(k_ba2_lin, dim3(gP), dim3(kMkThreads), 0, st, d, w);
-        if (nO > 0) hipLaunchKernelGGL(k_ba2_kfsum, dim3(nO), dim3(kMkThreads), 0, st, d, w);
+        if (w.n_kitem > 0)
+          hipLaunchKernelGGL(k_ba2_kfsum, dim3(w.n_kitem), dim3(kMkThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p1, dim3(gP), dim3(kMkThreads), 0, st, d, w);
-        if (nblk + nO > 0)
-          hipLaunchKernelGGL(k_ba2_p2, dim3(nblk + nO), dim3(kMkThreads), 0, st, d, w);
+        if (w.n_bitem + w.n_kitem > 0)
+          hipLaunchKernelGGL(k_ba2_p2, dim3(w.n_bitem + w.n_kitem), dim3(kMkThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p3, dim3(1), dim3(kMkSolveThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p4, dim3(gP), dim3(kMkThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p5, dim3(1), dim3(kMkDecideThreads), 0, st, d, w);
@@ -1626,12 +1845,26 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
       MMT_HIP(hipGetLastError());
       slots += batch;
       MMT_HIP(hipMemcpyAsync(h_flag_, &w.st->done, sizeof(int), hipMemcpyDeviceToHost, st));
+      const double tw = hp.on ? ba_now_us() : 0;
       MMT_HIP(hipStreamSynchronize(st));
+      if (hp.on) {
+        t_launch += tw - tl;
+        t_wait += ba_now_us() - tw;
+      }
       done = *h_flag_ != 0;
       if (!done && slots >= 160) throw DeviceError("local BA: the LM did not finish in 150 trials");
     }
     hipLaunchKernelGGL(k_ba2_finish, dim3(1), dim3(kMkDecideThreads), 0, st, d, w);
     MMT_HIP(hipGetLastError());
+    if (hp.on) {
+      hp.t[0] += tp1 - tp0;
+      hp.t[1] += t_launch;
+      hp.t[2] += t_wait;
+      hp.slots += slots;
+      BAState hs;
+      MMT_HIP(hipMemcpy(&hs, w.st, sizeof(hs), hipMemcpyDeviceToHost));
+      for (int q = 0; q < 5; q++) hp.p3[q] += hs.prof[q];
+    }
   }
   MMT_HIP(hipMemcpyAsync(h_dn_, d_dn_, dn, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipStreamSynchronize(st));
@@ -1639,6 +1872,19 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
   memcpy(X_out, h_dn_ + o_X, 12 * (size_t)nP);
   memcpy(erase, h_dn_ + o_er, (size_t)nE);
   memcpy(stats, h_dn_ + o_st, 5 * sizeof(int));
+  if (hp.on) {
+    hp.t[4] += ba_now_us() - tp0;
+    if (++hp.n % 32 == 0)
+      fprintf(stderr, "[mmt ba profile] %ld solves, host us per solve: layout + upload %.1f, "
+              "launches %.1f, waits %.1f, total %.1f; %.1f trial slots per solve\n", hp.n,
+              hp.t[0] / hp.n, hp.t[1] / hp.n, hp.t[2] / hp.n, hp.t[4] / hp.n,
+              (double)hp.slots / hp.n);
+    if (hp.on && hp.n % 32 == 0)
+      fprintf(stderr, "[mmt ba profile] k_ba2_p3 us per solve: partials %.1f, assembly %.1f, "
+              "LDL^T %.1f, substitutions %.1f, poses + state %.1f\n", hp.p3[0] * 0.01 / hp.n,
+              hp.p3[1] * 0.01 / hp.n, hp.p3[2] * 0.01 / hp.n, hp.p3[3] * 0.01 / hp.n,
+              hp.p3[4] * 0.01 / hp.n);
+  }
 }
 
 }  // namespace mmt

@@ -37,5 +37,6 @@ if only_mmt:
 with open(out, "w") as f:
     f.write("kernel,calls,total_us,avg_us,percent\n")
     for n, c, t, a, p in rows:
-        f.write('"%s",%d,%.3f,%.3f,%.2f\n' % (n.split("(")[0], c, t, a, p))
+        f.write('"%s",%d,%.3f,%.3f,%.2f\n' % (n.replace("(anonymous namespace)::", "").split("(")[0],
+                                                c, t, a, p))
 print(open(out).read())
