@@ -747,6 +747,7 @@ constexpr int kMkDecideThreads = 1024;
 
 struct BAState {
   int done, round, iter, qmax, need_lin, lam_init, cb, ok2, nBad, nact;
+  int spec_ok;  // the last trial was accepted: k_ba2_p4 linearised at it, no k_ba2_lin needed
   int it_done[2], trials[2];
   double lambda, ni, chk, currentChi, iniChi, scale_p;
   long long prof[8];  // k_ba2_p3 phase times (wall clock ticks, 100 MHz), summed over trials
@@ -756,12 +757,13 @@ struct BAWork2 {
   BAState* st;
   DSE3* pose;       // [2][n_kf]: the current estimate (buffer st->cb) and the trial
   double* X;        // [2][3 n_pt]
-  double* Hll;      // 9 n_pt
-  double* bl;       // 3 n_pt
+  // the linearisation at the current estimate (buffer st->cb) and at the trial (k_ba2_p4)
+  double* Hll;      // [2][9 n_pt]
+  double* bl;       // [2][3 n_pt]
   double* Dinv;     // 9 n_pt
   double* err;      // 3 n_edge: the last computed errors
-  double* Hpl;      // 18 n_edge
-  double* Hpe;      // 27 n_edge: the edge's J_p^T w J_p (21, upper triangle) and J_p^T w (-e) (6)
+  double* Hpl;      // [2][18 n_edge]
+  double* Hpe;      // [2][27 n_edge]: the edge's J_p^T w J_p (21, upper triangle), J_p^T w (-e) (6)
   double* Y;        // 18 n_edge
   double* cv;       // 6 n_edge
   double* Hpp;      // 36 n_opt
@@ -894,22 +896,19 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_init(BADesc d, BAWork2 w) {
   }
 }
 
-// computeActiveErrors + activeRobustChi2 + buildSystem's point side, one thread per point
-__global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
-  __shared__ double s_part[2 * kMkWaves];
-  const BAState* st = w.st;
-  if (st->done || !st->need_lin) return;
-  const bool robust = st->round == 0;
-  const int cb = st->cb;
+// computeActiveErrors + activeRobustChi2 + buildSystem's point side for point j at (pose, X):
+// its active edges' errors (stored), robust chi2 (returned), H_ll and b_l of the point, H_pl and
+// the pose terms of each edge, into linearisation buffer `lb`; *mx = the largest H_ll diagonal
+__device__ __forceinline__ double ba2_lin_point(const BADesc& d, const BAWork2& w, int j,
+                                               const DSE3* pose, const double (&X)[3], bool robust,
+                                               int lb, double* mx) {
   const Cam cam = ba_cam(d);
   const double dMono = huber_mono(), dStereo = huber_stereo();
-  const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
-  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
-  const int j = blockIdx.x * kMkThreads + threadIdx.x;
-  double chi = 0, mx = 0;
-  if (j < d.n_pt) {
+  double* Hpl_b = w.Hpl + (size_t)lb * 18 * d.n_edge;
+  double* Hpe_b = w.Hpe + (size_t)lb * 27 * d.n_edge;
+  double chi = 0;
+  {
     double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b3[3] = {0, 0, 0};
-    const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
     for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
       if (w.level[e]) continue;
       const int k = d.e_kf[e];
@@ -942,7 +941,7 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
         b3[a] += g;
       }
       if (d.opt_of[k] >= 0) {
-        double* hpl = &w.Hpl[18 * (size_t)e];
+        double* hpl = &Hpl_b[18 * (size_t)e];
 #pragma unroll
         for (int a = 0; a < 6; a++)
 #pragma unroll
@@ -951,7 +950,7 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
             _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) acc += Jp[r][a] * wt * Jl[r][b];
             hpl[3 * a + b] = acc;
           }
-        double* hpe = &w.Hpe[27 * (size_t)e];
+        double* hpe = &Hpe_b[27 * (size_t)e];
         int q = 0;
 #pragma unroll
         for (int r0 = 0; r0 < 6; r0++)
@@ -969,11 +968,34 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
         }
       }
     }
+    double* Hll_b = w.Hll + (size_t)lb * 9 * d.n_pt;
+    double* bl_b = w.bl + (size_t)lb * 3 * d.n_pt;
 #pragma unroll
-    for (int q = 0; q < 9; q++) w.Hll[9 * (size_t)j + q] = hl[q];
+    for (int q = 0; q < 9; q++) Hll_b[9 * (size_t)j + q] = hl[q];
 #pragma unroll
-    for (int q = 0; q < 3; q++) w.bl[3 * (size_t)j + q] = b3[q];
-    if (w.pt_act[j]) mx = fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8])));
+    for (int q = 0; q < 3; q++) bl_b[3 * (size_t)j + q] = b3[q];
+    *mx = fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8])));
+  }
+  return chi;
+}
+
+// the linearisation at the current estimate, one thread per point (the start of each round, and an
+// iteration that follows a rejected trial; after an accepted one k_ba2_p4 has linearised already)
+__global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
+  __shared__ double s_part[2 * kMkWaves];
+  const BAState* st = w.st;
+  if (st->done || !st->need_lin || st->spec_ok) return;
+  const bool robust = st->round == 0;
+  const int cb = st->cb;
+  const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
+  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
+  const int j = blockIdx.x * kMkThreads + threadIdx.x;
+  double chi = 0, mx = 0;
+  if (j < d.n_pt) {
+    const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
+    double m = 0;
+    chi = ba2_lin_point(d, w, j, pose, X, robust, cb, &m);
+    if (w.pt_act[j]) mx = m;
   }
   const double cs = wave_sum_dpp(chi);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1003,7 +1025,7 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_kfsum(BADesc d, BAWork2 w) {
   if (t < it.z) {
     const int e = d.kf_edges[t];
     if (!w.level[e]) {
-      const double* h = &w.Hpe[27 * (size_t)e];
+      const double* h = &w.Hpe[(size_t)st->cb * 27 * d.n_edge + 27 * (size_t)e];
 #pragma unroll
       for (int q = 0; q < 27; q++) acc[q] = h[q];
     }
@@ -1021,19 +1043,23 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p1(BADesc d, BAWork2 w) {
   const double lambda = st->lam_init ? ba2_lambda_init(d, w, &s_lam) : st->lambda;
   const int j = blockIdx.x * kMkThreads + threadIdx.x;
   if (j >= d.n_pt || !w.pt_act[j]) return;
+  const int cb = st->cb;
+  const double* Hll_c = w.Hll + (size_t)cb * 9 * d.n_pt;
+  const double* bl_c = w.bl + (size_t)cb * 3 * d.n_pt;
+  const double* Hpl_c = w.Hpl + (size_t)cb * 18 * d.n_edge;
   double Dm[9], Di[9];
 #pragma unroll
-  for (int q = 0; q < 9; q++) Dm[q] = w.Hll[9 * (size_t)j + q] + ((q % 4) == 0 ? lambda : 0.0);
+  for (int q = 0; q < 9; q++) Dm[q] = Hll_c[9 * (size_t)j + q] + ((q % 4) == 0 ? lambda : 0.0);
   inverse3(Dm, Di);
 #pragma unroll
   for (int q = 0; q < 9; q++) w.Dinv[9 * (size_t)j + q] = Di[q];
-  const double* b3 = &w.bl[3 * (size_t)j];
+  const double* b3 = &bl_c[3 * (size_t)j];
   double db[3];
 #pragma unroll
   for (int a = 0; a < 3; a++) db[a] = Di[3 * a] * b3[0] + Di[3 * a + 1] * b3[1] + Di[3 * a + 2] * b3[2];
   for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
     if (w.level[e] || d.opt_of[d.e_kf[e]] < 0) continue;
-    const double* B = &w.Hpl[18 * (size_t)e];
+    const double* B = &Hpl_c[18 * (size_t)e];
     double* Ye = &w.Y[18 * (size_t)e];
     double* ce = &w.cv[6 * (size_t)e];
 #pragma unroll
@@ -1063,7 +1089,7 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p2(BADesc d, BAWork2 w) {
       const int2 tr = d.trip[t];
       if (!w.level[tr.x] && !w.level[tr.y]) {
         const double* Ye = &w.Y[18 * (size_t)tr.x];
-        const double* B2 = &w.Hpl[18 * (size_t)tr.y];
+        const double* B2 = &w.Hpl[(size_t)st->cb * 18 * d.n_edge + 18 * (size_t)tr.y];
         double h2[18], y[18];
 #pragma unroll
         for (int q = 0; q < 18; q++) {
@@ -1112,6 +1138,7 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
   long long pt[6];
   pt[0] = wall_clock64();
   const bool lam_init = stp->lam_init != 0, need_lin = stp->need_lin != 0;
+  const bool lin_ran = need_lin && !stp->spec_ok;
   const int cb = stp->cb;
   __shared__ double s_lam;
   const double lambda = lam_init ? ba2_lambda_init(d, w, &s_lam) : stp->lambda;
@@ -1300,7 +1327,7 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
         const double xv = w.x[i];
         sp += xv * (lambda * xv + w.bp[i]);
       }
-    if (need_lin)
+    if (lin_ran)
       for (int g = lane; g < w.gP; g += 64) c += w.linpart[2 * g];
     sp = wave_sum_dpp(sp);
     c = wave_sum_dpp(c);
@@ -1313,10 +1340,8 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
   if (tid == 0) {
     const double sp = s_vec2[0];
     BAState& s = *stp;
-    if (need_lin) {
-      s.currentChi = s_vec2[1];
-      s.iniChi = s_vec2[1];
-    }
+    if (lin_ran) s.currentChi = s_vec2[1];
+    if (need_lin) s.iniChi = s.currentChi;  // the iteration's start (after an accepted trial: its chi2)
     if (lam_init) {
       s.lam_init = 0;
       s.ni = 2;
@@ -1339,12 +1364,12 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
   const int cb = st->cb, nb = 1 - cb;
   const bool ok2 = st->ok2 != 0, robust = st->round == 0;
   const double lambda = st->lambda;
-  const Cam cam = ba_cam(d);
-  const double dMono = huber_mono(), dStereo = huber_stereo();
   const size_t n6 = 6 * (size_t)d.n_opt;
   const DSE3* tri = w.pose + (size_t)nb * d.n_kf;
   const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
   double* Xt = w.X + (size_t)nb * 3 * d.n_pt;
+  const double* bl_c = w.bl + (size_t)cb * 3 * d.n_pt;
+  const double* Hpl_c = w.Hpl + (size_t)cb * 18 * d.n_edge;
   const int j = blockIdx.x * kMkThreads + threadIdx.x;
   double chi = 0, sc = 0;
   if (j < d.n_pt) {
@@ -1352,11 +1377,11 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
     if (w.pt_act[j]) {
       double* xl = &w.x[n6 + 3 * (size_t)j];
       if (ok2) {
-        double cl[3] = {w.bl[3 * (size_t)j], w.bl[3 * (size_t)j + 1], w.bl[3 * (size_t)j + 2]};
+        double cl[3] = {bl_c[3 * (size_t)j], bl_c[3 * (size_t)j + 1], bl_c[3 * (size_t)j + 2]};
         for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
           const int a = d.opt_of[d.e_kf[e]];
           if (w.level[e] || a < 0) continue;
-          const double* B = &w.Hpl[18 * (size_t)e];
+          const double* B = &Hpl_c[18 * (size_t)e];
 #pragma unroll
           for (int c = 0; c < 3; c++)
 #pragma unroll
@@ -1369,18 +1394,13 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
 #pragma unroll
       for (int r = 0; r < 3; r++) {
         const double xv = xl[r];
-        sc += xv * (lambda * xv + w.bl[3 * (size_t)j + r]);
+        sc += xv * (lambda * xv + bl_c[3 * (size_t)j + r]);
         X[r] += xv;
       }
-      for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
-        if (w.level[e]) continue;
-        const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
-        const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], stereo, tri[d.e_kf[e]],
-                                    X, cam, &w.err[3 * (size_t)e]);
-        double r0 = c, r1;
-        if (robust) huber_rho(c, stereo ? dStereo : dMono, r0, r1);
-        chi += r0;
-      }
+      // the trial's errors and chi2, and the linearisation at the trial state (the next
+      // iteration's system if the trial is accepted) into the other buffer
+      double m;
+      chi = ba2_lin_point(d, w, j, tri, X, robust, nb, &m);
     }
 #pragma unroll
     for (int r = 0; r < 3; r++) Xt[3 * (size_t)j + r] = X[r];
@@ -1444,10 +1464,12 @@ __global__ __launch_bounds__(kMkDecideThreads) void k_ba2_p5(BADesc d, BAWork2 w
       s.lambda *= fmax(1. / 3., alpha);
       s.ni = 2;
       s.currentChi = tempChi;
-      s.cb = 1 - s.cb;  // the trial becomes the current estimate
+      s.cb = 1 - s.cb;  // the trial (and its linearisation) becomes the current estimate
+      s.spec_ok = 1;
     } else {
       s.lambda *= s.ni;
       s.ni *= 2;
+      s.spec_ok = 0;
     }
     s.qmax++;
     s.trials[s.round]++;
@@ -1517,6 +1539,7 @@ __global__ __launch_bounds__(kMkDecideThreads) void k_ba2_p5(BADesc d, BAWork2 w
     for (int q = 0; q < kMkDecideThreads / 64; q++) t += s_part[q];
     BAState& s = *stp;
     s.round = 1;
+    s.spec_ok = 0;
     s.iter = 0;
     s.qmax = 0;
     s.need_lin = 1;
@@ -1578,8 +1601,8 @@ size_t ba2_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt, int n_blk,
   auto a = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t n6 = 6 * (size_t)n_opt;
   return a(sizeof(BAState)) + a(sizeof(DSE3) * 2 * (size_t)n_kf) + a(8 * 6 * (size_t)n_pt) +
-         a(8 * 9 * (size_t)n_pt) + a(8 * 3 * (size_t)n_pt) + a(8 * 9 * (size_t)n_pt) +
-         a(8 * 3 * (size_t)n_edge) + a(8 * 18 * (size_t)n_edge) + a(8 * 27 * (size_t)n_edge) +
+         a(8 * 18 * (size_t)n_pt) + a(8 * 6 * (size_t)n_pt) + a(8 * 9 * (size_t)n_pt) +
+         a(8 * 3 * (size_t)n_edge) + a(8 * 36 * (size_t)n_edge) + a(8 * 54 * (size_t)n_edge) +
          a(8 * 18 * (size_t)n_edge) + a(8 * 6 * (size_t)n_edge) + a(8 * 36 * (size_t)n_opt) +
          a(8 * 6 * (size_t)n_opt) + a(8 * 6 * (size_t)n_opt) + a(8 * 36 * (size_t)n_blk) +
          a(8 * (n6 + 3 * (size_t)n_pt)) + a(8 * n6 * n6) + a(8 * 3 * n6) + 2 * a(8 * 2 * (size_t)gP) +
@@ -1791,12 +1814,12 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.st = (BAState*)take(sizeof(BAState));
     w.pose = (DSE3*)take(sizeof(DSE3) * 2 * (size_t)nK);
     w.X = (double*)take(8 * 6 * (size_t)nP);
-    w.Hll = (double*)take(8 * 9 * (size_t)nP);
-    w.bl = (double*)take(8 * 3 * (size_t)nP);
+    w.Hll = (double*)take(8 * 2 * 9 * (size_t)nP);
+    w.bl = (double*)take(8 * 2 * 3 * (size_t)nP);
     w.Dinv = (double*)take(8 * 9 * (size_t)nP);
     w.err = (double*)take(8 * 3 * (size_t)nE);
-    w.Hpl = (double*)take(8 * 18 * (size_t)nE);
-    w.Hpe = (double*)take(8 * 27 * (size_t)nE);
+    w.Hpl = (double*)take(8 * 2 * 18 * (size_t)nE);
+    w.Hpe = (double*)take(8 * 2 * 27 * (size_t)nE);
     w.Y = (double*)take(8 * 18 * (size_t)nE);
     w.cv = (double*)take(8 * 6 * (size_t)nE);
     w.Hpp = (double*)take(8 * 36 * (size_t)nO);
