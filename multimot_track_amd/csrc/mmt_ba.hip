@@ -1193,72 +1193,69 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
     if (i > j) S[q] = S[(size_t)j * n6 + i];
   }
   __syncthreads();
-  __shared__ double s_Lrow[64 * 64];  // L row-major (the backward substitution), n6 <= 64
+  // Blocked LDL^T over the 6 x 6 keyframe blocks, on the lower triangle (row-major).  Every entry
+  // receives exactly the scalar algorithm's operations in the scalar order (the subtraction of
+  // L(i, c) L(j, c) D(c) for c ascending, then for an off-diagonal the division by D(j)): the
+  // diagonal block is factored by one wave, the panel below it one row per thread, the trailing
+  // blocks one entry per thread, three barriers per block column.  L is also copied into the upper
+  // triangle (L(i, c) at (c, i)) for the forward substitution's coalesced reads.
   bool ok = true;
-  pt[2] = pt[3] = wall_clock64();
-  if (n6 <= 64) {
-    // One wave, lane i = row i.  S holds the upper triangle row-major, i.e. the lower triangle
-    // column-major: entry (i, j), i >= j, at S[j n6 + i], so a column is one coalesced LDS row.
-    // Step k: L(i, k) = S(i, k) / d_k in lane i, broadcast to the update of column jj by readlane;
-    // every entry sees the left-looking sequence of operations of the CPU checker.
+  pt[2] = wall_clock64();
+  for (int K = 0; K < d.n_opt; K++) {
+    const int k0 = 6 * K;
     if (wave == 0) {
-      for (int k = 0; k < n6 && ok; k++) {
-        const double dk = S[(size_t)k * n6 + k];
+      for (int c = 0; c < 6 && ok; c++) {
+        const int kc = k0 + c;
+        double dk = S[(size_t)kc * n6 + kc];
+        for (int m = k0; m < kc; m++) dk -= S[(size_t)kc * n6 + m] * S[(size_t)kc * n6 + m] * Dg[m];
         if (dk == 0) {
           ok = false;
           break;
         }
-        double lik = 0;
-        if (lane > k && lane < n6) {
-          lik = S[(size_t)k * n6 + lane] / dk;
-          S[(size_t)k * n6 + lane] = lik;
-          s_Lrow[lane * 64 + k] = lik;
+        const int r = k0 + lane;
+        if (lane > c && lane < 6) {
+          double v = S[(size_t)r * n6 + kc];
+          for (int m = k0; m < kc; m++) v -= S[(size_t)r * n6 + m] * S[(size_t)kc * n6 + m] * Dg[m];
+          const double l = v / dk;
+          S[(size_t)r * n6 + kc] = l;
+          S[(size_t)kc * n6 + r] = l;
         }
-        if (lane == 0) Dg[k] = dk;
-        for (int jj = k + 1; jj < n6; jj++) {
-          const double ljk = lane_value(lik, jj);
-          if (lane >= jj && lane < n6) S[(size_t)jj * n6 + lane] -= lik * ljk * dk;
+        if (lane == 0) {
+          S[(size_t)kc * n6 + kc] = dk;
+          Dg[kc] = dk;
         }
         wave_sync_lds();
       }
-      pt[3] = wall_clock64();
-      if (!ok) {
-        if (lane == 0) s_ok = 0;
-      } else {
-        double y = lane < n6 ? bs[lane] : 0.0;
-        double lnext = lane < n6 ? S[lane] : 0.0;
-        for (int c = 0; c < n6; c++) {  // forward, L(i, c) = S[c n6 + i]
-          const double l = lnext;
-          if (c + 1 < n6 && lane < n6) lnext = S[(size_t)(c + 1) * n6 + lane];
-          const double yc = lane_value(y, c);
-          if (lane > c && lane < n6) y -= l * yc;
-        }
-        if (lane < n6) y /= Dg[lane];
-        for (int r = n6 - 1; r > 0; r--) {  // backward, L(r, i) = s_Lrow[r][i]
-          const double yr = lane_value(y, r);
-          if (lane < r) y -= s_Lrow[r * 64 + lane] * yr;
-        }
-        if (lane < n6) w.x[lane] = y;
-      }
+      if (!ok && lane == 0) s_ok = 0;
     }
-  } else {
-  // One barrier per column: step k reads column k of the (updated) lower triangle, each thread
-  // forms the L entries it needs itself (L(i, k) = S(i, k) / d_k, the same rounding as a stored
-  // one), updates its entries of the trailing lower triangle, and L(i, k) is kept in the upper
-  // triangle at (k, i), which no step reads any more.
-  for (int k = 0; k < n6; k++) {
-    const double dk = S[(size_t)k * n6 + k];
-    if (dk == 0) {  // uniform: every thread reads the same value
+    __syncthreads();
+    if (s_ok == 0) {
       ok = false;
       break;
     }
-    if (tid == 0) Dg[k] = dk;
-    // 64 row slots x 8 column lanes
-    for (int i = k + 1 + (tid >> 3); i < n6; i += kMkSolveThreads / 8) {
-      const double lik = S[(size_t)i * n6 + k] / dk;
-      for (int jj = k + 1 + (tid & 7); jj <= i; jj += 8)
-        S[(size_t)i * n6 + jj] -= lik * (S[(size_t)jj * n6 + k] / dk) * dk;
-      if ((tid & 7) == 0) S[(size_t)k * n6 + i] = lik;
+    // the panel: L(i, k0 + c) for the rows below the block, one row per thread
+    for (int i = k0 + 6 + tid; i < n6; i += kMkSolveThreads) {
+      double l[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        double v = S[(size_t)i * n6 + k0 + c];
+        for (int m = 0; m < c; m++) v -= l[m] * S[(size_t)(k0 + c) * n6 + k0 + m] * Dg[k0 + m];
+        l[c] = v / Dg[k0 + c];
+        S[(size_t)i * n6 + k0 + c] = l[c];
+        S[(size_t)(k0 + c) * n6 + i] = l[c];
+      }
+    }
+    __syncthreads();
+    // the trailing lower triangle: (i, j), k0 + 6 <= j <= i, minus the block's six terms in order
+    const int m0 = k0 + 6, mt = n6 - m0;
+    for (int q = tid; q < mt * mt; q += kMkSolveThreads) {
+      const int i = m0 + q / mt, jj = m0 + q % mt;
+      if (jj > i) continue;
+      double v = S[(size_t)i * n6 + jj];
+#pragma unroll
+      for (int c = 0; c < 6; c++)
+        v -= S[(size_t)i * n6 + k0 + c] * S[(size_t)jj * n6 + k0 + c] * Dg[k0 + c];
+      S[(size_t)i * n6 + jj] = v;
     }
     __syncthreads();
   }
@@ -1266,20 +1263,21 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
   if (!ok) {
     if (tid == 0) s_ok = 0;
   } else if (wave == 0) {
-    // substitutions with y in registers (lane i: rows i, i + 64), y[c] broadcast by readlane
+    // substitutions with y in registers (lane i: rows i, i + 64), y[c] broadcast by readlane;
+    // forward reads L(i, c) at (c, i) (upper copy), backward L(r, i) at (r, i): coalesced rows
     double y0 = lane < n6 ? bs[lane] : 0.0, y1 = lane + 64 < n6 ? bs[lane + 64] : 0.0;
     if (n6 <= 128) {
-      for (int c = 0; c < n6; c++) {  // forward, L(i, c) = S(c, i)
+      for (int c = 0; c < n6; c++) {
         const double yc = c < 64 ? lane_value(y0, c) : lane_value(y1, c - 64);
         if (lane > c && lane < n6) y0 -= S[(size_t)c * n6 + lane] * yc;
         if (lane + 64 > c && lane + 64 < n6) y1 -= S[(size_t)c * n6 + lane + 64] * yc;
       }
       if (lane < n6) y0 /= Dg[lane];
       if (lane + 64 < n6) y1 /= Dg[lane + 64];
-      for (int r = n6 - 1; r > 0; r--) {  // backward, L(r, i) = S(i, r)
+      for (int r = n6 - 1; r > 0; r--) {
         const double yr = r < 64 ? lane_value(y0, r) : lane_value(y1, r - 64);
-        if (lane < r) y0 -= S[(size_t)lane * n6 + r] * yr;
-        if (lane + 64 < r) y1 -= S[(size_t)(lane + 64) * n6 + r] * yr;
+        if (lane < r) y0 -= S[(size_t)r * n6 + lane] * yr;
+        if (lane + 64 < r) y1 -= S[(size_t)r * n6 + lane + 64] * yr;
       }
       if (lane < n6) w.x[lane] = y0;
       if (lane + 64 < n6) w.x[lane + 64] = y1;
@@ -1295,12 +1293,11 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
       wave_sync_lds();
       for (int r = n6 - 1; r > 0; r--) {
         const double yr = yv[r];
-        for (int i = lane; i < r; i += 64) yv[i] -= S[(size_t)i * n6 + r] * yr;
+        for (int i = lane; i < r; i += 64) yv[i] -= S[(size_t)r * n6 + i] * yr;
         wave_sync_lds();
       }
       for (int i = lane; i < n6; i += 64) w.x[i] = yv[i];
     }
-  }
   }
   __syncthreads();
   pt[4] = wall_clock64();
