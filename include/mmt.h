@@ -438,6 +438,12 @@ typedef struct mmt_map_counters {
 } mmt_map_counters;
 int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out);
 
+/* Visualisation hook (no reference counterpart; Tracking.cc:684-783 draws these into feat.png):
+ * the static samples (mvSiftKeys, B2) and the object samples (mvObjKeys with vSemObjLabel, B1)
+ * of the last frame the context tracked, xy as n x 2 floats.  Counts clipped to the caps. */
+int mmt_frame_samples(mmt_ctx* ctx, float* static_xy, int static_cap, int* n_static,
+                      float* obj_xy, int32_t* obj_label, int obj_cap, int* n_obj);
+
 /* Stage timing with HIP events on the launch stream (no reference counterpart: measurement
  * hook for bench.py).  orb_ms sums the batched ORB launch sequences of the tracked chunks. */
 typedef struct mmt_profile {

@@ -39,7 +39,7 @@ CXX = os.environ.get("CXX", "g++")
 def build_cli(force=False, verbose=True):
     """Host-only pieces above the C-ABI: libmmt_io.so (sequence decoding) and the rgbd_mmt
     drop-in executable (links libmmt.so through an $ORIGIN rpath)."""
-    srcs = [os.path.join(CLI, f) for f in ("mmt_io.cpp", "mmt_io.h", "rgbd_mmt.cpp")]
+    srcs = [os.path.join(CLI, f) for f in ("mmt_io.cpp", "mmt_io.h", "mmt_viz.h", "rgbd_mmt.cpp")]
     newest = max(os.path.getmtime(s) for s in srcs + [OUT])
     cmds = []
     if force or not os.path.exists(IO_LIB) or os.path.getmtime(IO_LIB) < newest:

@@ -276,6 +276,54 @@ int mmt_io_yaml_float(const char* path, const char* key, double* value) {
   return -1;
 }
 
+int mmt_io_write_png_bgr(const char* path, const uint8_t* bgr, int w, int h) {
+  if (!path || !bgr || w <= 0 || h <= 0) return -1;
+  std::vector<uint8_t> raw((size_t)h * (3 * (size_t)w + 1));
+  for (int y = 0; y < h; y++) {
+    uint8_t* row = &raw[(size_t)y * (3 * (size_t)w + 1)];
+    row[0] = 0;  // filter: none
+    const uint8_t* src = bgr + (size_t)y * 3 * w;
+    for (int x = 0; x < w; x++) {
+      row[1 + 3 * x] = src[3 * x + 2];
+      row[2 + 3 * x] = src[3 * x + 1];
+      row[3 + 3 * x] = src[3 * x];
+    }
+  }
+  uLongf zlen = compressBound((uLong)raw.size());
+  std::vector<uint8_t> z(zlen);
+  if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 3) != Z_OK) return -2;
+  FILE* f = fopen(path, "wb");
+  if (!f) return -3;
+  auto put32 = [&](std::vector<uint8_t>& v, uint32_t x) {
+    v.push_back((uint8_t)(x >> 24));
+    v.push_back((uint8_t)(x >> 16));
+    v.push_back((uint8_t)(x >> 8));
+    v.push_back((uint8_t)x);
+  };
+  auto chunk = [&](const char* type, const uint8_t* data, size_t n) {
+    std::vector<uint8_t> c;
+    put32(c, (uint32_t)n);
+    c.insert(c.end(), type, type + 4);
+    c.insert(c.end(), data, data + n);
+    const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), c.data() + 4, (uInt)(n + 4));
+    put32(c, crc);
+    return fwrite(c.data(), 1, c.size(), f) == c.size();
+  };
+  static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+  std::vector<uint8_t> ihdr;
+  put32(ihdr, (uint32_t)w);
+  put32(ihdr, (uint32_t)h);
+  ihdr.push_back(8);  // bit depth
+  ihdr.push_back(2);  // colour type RGB
+  ihdr.push_back(0);
+  ihdr.push_back(0);
+  ihdr.push_back(0);
+  bool ok = fwrite(sig, 1, 8, f) == 8 && chunk("IHDR", ihdr.data(), ihdr.size()) &&
+            chunk("IDAT", z.data(), zlen) && chunk("IEND", nullptr, 0);
+  ok = (fclose(f) == 0) && ok;
+  return ok ? 0 : -4;
+}
+
 void mmt_io_free(void* p) { free(p); }
 
 }  // extern "C"

@@ -38,6 +38,10 @@ int mmt_io_read_object_poses(const char* path, float** out, int* n);
 /* The `Key: value` scalars of an OpenCV FileStorage YAML settings file (kitti03.yaml). */
 int mmt_io_yaml_float(const char* path, const char* key, double* value);
 
+/* cv::imwrite(path, img) for an 8-bit BGR image (w*h*3, row-major, no padding): a PNG with RGB
+ * samples, filter 0, zlib deflate.  0 on success. */
+int mmt_io_write_png_bgr(const char* path, const uint8_t* bgr, int w, int h);
+
 void mmt_io_free(void* p);
 
 #ifdef __cplusplus

@@ -8,7 +8,7 @@
 //
 //   rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence [--realtime] [--nfeatures N]
 //            [--device D] [--noise-seed S] [--poses out.txt] [--chunk F] [--threads T]
-//            [--deferred-objects]
+//            [--deferred-objects] [--viz DIR]
 //
 // Input decoding (PNG, .flo, text masks) runs on T host threads (default: up to 16) into pinned
 // buffers from mmt_host_alloc, ahead of the tracker, and frames go to the GPU F at a time through
@@ -17,6 +17,14 @@
 // --deferred-objects (mmt_set_deferred_objects) keeps the object pipeline running across calls:
 // each frame's camera lines print at once and its object lines when its motions are ready
 // ("Objects of Frame: n", up to 17 frames later; the rest after the last frame).
+// --viz DIR writes the reference's visual artifacts (Tracking.cc:684-878) into DIR: traj.png
+// (camera positions of every frame as red squares, object centroids as label-coloured circles,
+// seen from above) and, for the last frame, feat.png (static samples and object samples over
+// the image) and speed.png (the ground-truth boxes of the tracked objects).  The reference
+// rewrites feat.png and speed.png every frame, so its final files show the last frame too.
+// Differences: no text (no font renderer; the numbers are in the evaluation lines), and the
+// object centroids are ObjCentre3D_pre (the solve's last-frame centroid, which mmt_motion
+// carries) instead of vObjCentre3D.
 //
 // Differences from the reference binary: the vocabulary is not read (this path
 // never uses BoW); no viewer, no imshow/waitKey; the usleep pacing to the timestamps is off
@@ -37,6 +45,7 @@
 
 #include "../../include/mmt.h"
 #include "mmt_io.h"
+#include "mmt_viz.h"
 
 namespace {
 
@@ -170,6 +179,8 @@ std::string frame_name(const std::string& dir, const char* sub, int i, const cha
   return dir + "/" + sub + "/" + buf + ext;
 }
 
+int cvRound(float v) { return (int)std::lrint(v); }  // round half to even, as cvRound
+
 bool exists(const std::string& p) {
   FILE* f = fopen(p.c_str(), "rb");
   if (f) fclose(f);
@@ -184,7 +195,7 @@ int main(int argc, char** argv) {
   bool deferred = false;
   int nfeat = -1, device = 0;
   unsigned seed = 0;
-  std::string poses_out;
+  std::string poses_out, viz_dir;
   int chunk = 16;
   int threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   for (int i = 1; i < argc; i++) {
@@ -197,12 +208,13 @@ int main(int argc, char** argv) {
     else if (a == "--poses" && i + 1 < argc) poses_out = argv[++i];
     else if (a == "--chunk" && i + 1 < argc) chunk = std::max(1, atoi(argv[++i]));
     else if (a == "--threads" && i + 1 < argc) threads = std::max(1, atoi(argv[++i]));
+    else if (a == "--viz" && i + 1 < argc) viz_dir = argv[++i];
     else pos.push_back(a);
   }
   if (pos.size() != 3) {
     fprintf(stderr, "\nUsage: ./rgbd_mmt path_to_vocabulary path_to_settings path_to_sequence "
                     "[--realtime] [--nfeatures N] [--device D] [--noise-seed S] [--poses file] "
-                    "[--chunk F] [--threads T] [--deferred-objects]\n");
+                    "[--chunk F] [--threads T] [--deferred-objects] [--viz DIR]\n");
     return 1;
   }
   const std::string settings = pos[1], seq = pos[2];
@@ -377,10 +389,40 @@ int main(int argc, char** argv) {
   float lastTcw[16], lastGt[16];
   bool haveLast = false;
 
+  // traj.png (Tracking.cc:811-877): 600 x 800 (rgbd_tum.cc:111), scale 12, origin (300, 120)
+  viz::Canvas traj(600, 800);
+  const int sta_x = 300, sta_y = 120, radi = 2, thic = 2;
+  const float vscale = 12;
+  auto traj_camera = [&](const float* Tcw) {
+    float Twc[16];
+    inv4(Tcw, Twc);
+    const int x = int(Twc[3] * vscale) + sta_x, y = int(Twc[11] * vscale) + sta_y;
+    traj.rectangle(x, y, x + 10, y + 10, viz::BGR{0, 0, 255}, thic);
+    traj.rectangle(10, 30, 550, 60, viz::BGR{0, 0, 0}, -1);
+  };
+  auto traj_objects = [&](const mmt_frame_result& r, const mmt_motion* mo) {
+    for (int o = 0; o < r.n_objects && o < 64; o++) {
+      const float* c = mo[o].centre_pre;
+      if (!(std::isfinite(c[0]) && std::isfinite(c[2]))) continue;
+      bool known;
+      const viz::BGR col = viz::traj_colour(mo[o].sem_label, &known);
+      if (known) traj.circle(int(c[0] * vscale) + sta_x, int(c[2] * vscale) + sta_y, radi, col, thic);
+    }
+  };
+  const bool viz_on = !viz_dir.empty();
+  int viz_last = -1;  // the last frame tracked (feat.png, speed.png)
+  std::vector<int> viz_labels;  // its objects' semantic labels
   // the object lines of frame r.objects_frame (this frame's own unless deferred)
   auto print_objects = [&](const mmt_frame_result& r, const mmt_motion* mo, bool tag) {
     const int of = r.objects_frame;
     if (of < 0) return;
+    if (viz_on) {
+      traj_objects(r, mo);
+      if (of == viz_last) {
+        viz_labels.clear();
+        for (int o = 0; o < r.n_objects && o < 64; o++) viz_labels.push_back(mo[o].sem_label);
+      }
+    }
     if (tag) printf("Objects of Frame: %d\n", of);
     const float* Tgt = (of < ngt) ? gt + 16 * of : nullptr;
     const float* Tlw_gt = (of > 0 && of - 1 < ngt) ? gt + 16 * (of - 1) : nullptr;
@@ -444,6 +486,10 @@ int main(int argc, char** argv) {
       track_times[ni] = (float)ttrack;
       const float* Tgt = (ni < ngt) ? gt + 16 * ni : nullptr;
       if (haveLast && r.initialized && Tgt) print_camera_rpe(r.Tcw, lastTcw, Tgt, lastGt);
+      if (viz_on) {
+        traj_camera(r.Tcw);
+        viz_last = ni;
+      }
       print_objects(r, objs.data() + 64 * k, deferred);
       if (fp) {
         fprintf(fp, "%d", ni);
@@ -494,6 +540,47 @@ int main(int argc, char** argv) {
     }
   }
   const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+  if (viz_on && rc_all == 0 && viz_last >= 0) {
+    // feat.png (Tracking.cc:684-783): every second static sample off the mask in red, the
+    // object samples of the frame's tracked objects in their label colours
+    const Slot& sl = slots[viz_last % R];
+    viz::Canvas feat(W, H), speed(W, H);
+    memcpy(feat.px.data(), sl.bgr, npix * 3);
+    std::vector<float> sxy(2 * npix / 4 + 64), oxy(2 * npix / 4 + 64);
+    std::vector<int32_t> olab(npix / 4 + 64);
+    int ns = 0, no = 0;
+    if (mmt_frame_samples(ctx, sxy.data(), (int)(sxy.size() / 2), &ns, oxy.data(), olab.data(),
+                          (int)olab.size(), &no) == 0) {
+      for (int i = 0; i < ns; i += 2) {
+        const int x = (int)sxy[2 * i], y = (int)sxy[2 * i + 1];
+        if (x < 0 || y < 0 || x >= W || y >= H || sl.mask[(size_t)y * W + x] != 0) continue;
+        feat.circle(cvRound(sxy[2 * i]), cvRound(sxy[2 * i + 1]), 3, viz::BGR{0, 0, 255}, 1);
+      }
+      for (int i = 0; i < no; i++) {
+        if (std::find(viz_labels.begin(), viz_labels.end(), olab[i]) == viz_labels.end()) continue;
+        bool known;
+        const viz::BGR col = viz::feat_colour(olab[i], &known);
+        if (known) feat.circle(cvRound(oxy[2 * i]), cvRound(oxy[2 * i + 1]), 3, col, 1);
+      }
+    }
+    // speed.png (Tracking.cc:785-809): the gray image, the ground-truth box of each tracked object
+    for (size_t p = 0; p < npix; p++) {
+      const uint8_t* c = sl.bgr + 3 * p;
+      // mImGray: RGB2GRAY on the BGR image, so B takes the R weight
+      const uint8_t g = (uint8_t)((c[0] * 4899 + c[1] * 9617 + c[2] * 1868 + 8192) >> 14);
+      speed.px[3 * p] = speed.px[3 * p + 1] = speed.px[3 * p + 2] = g;
+    }
+    for (const float* row : obj_rows[viz_last])
+      if (std::find(viz_labels.begin(), viz_labels.end(), (int)row[1]) != viz_labels.end())
+        speed.rectangle((int)row[2], (int)row[3], (int)row[4], (int)row[5], viz::BGR{0, 140, 255}, 2);
+    const std::string d = viz_dir + "/";
+    if (mmt_io_write_png_bgr((d + "feat.png").c_str(), feat.px.data(), W, H) != 0 ||
+        mmt_io_write_png_bgr((d + "speed.png").c_str(), speed.px.data(), W, H) != 0 ||
+        mmt_io_write_png_bgr((d + "traj.png").c_str(), traj.px.data(), traj.w, traj.h) != 0) {
+      fprintf(stderr, "failed to write the visual artifacts into %s\n", viz_dir.c_str());
+      rc_all = 1;
+    }
+  }
   {
     std::lock_guard<std::mutex> lk(mu);
     stop = true;

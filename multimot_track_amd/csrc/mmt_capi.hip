@@ -815,6 +815,18 @@ int mmt_local_bundle_adjustment(mmt_ctx* ctx, const mmt_ba_problem* p, float* Tc
   });
 }
 
+int mmt_frame_samples(mmt_ctx* ctx, float* static_xy, int static_cap, int* n_static,
+                      float* obj_xy, int32_t* obj_label, int obj_cap, int* n_obj) {
+  if (!ctx || !n_static || !n_obj || static_cap < 0 || obj_cap < 0) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    *n_static = *n_obj = 0;
+    if (!ctx->tracker_ready) return;
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ctx->tracker.frame_samples(static_xy, static_cap, n_static, obj_xy, obj_label, obj_cap, n_obj,
+                               ctx->stream);
+  });
+}
+
 int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out) {
   if (!ctx || !out) return MMT_EINVAL;
   return guard(ctx, [&] {

@@ -88,6 +88,10 @@ class Tracker {
   int kcap() const { return kcap_; }
   const MappingStats& mapping_stats() const { return map_.mapping_stats(); }
   long split_fallbacks() const { return split_fallbacks_; }
+  // the last tracked frame's static samples (mvSiftKeys) and object samples (mvObjKeys,
+  // vSemObjLabel), copied to the host (visualisation hook); counts clipped to the caps
+  void frame_samples(float* sxy, int scap, int* ns, float* oxy, int32_t* olab, int ocap, int* no,
+                     hipStream_t st);
 
  private:
   struct FrameSlot {

@@ -691,6 +691,28 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   }
 }
 
+void Tracker::frame_samples(float* sxy, int scap, int* ns, float* oxy, int32_t* olab, int ocap,
+                            int* no, hipStream_t st) {
+  *ns = *no = 0;
+  if (state_ == 0 && frame_seq_ == 0) return;
+  const FrameSlot& L = slot_[last_];
+  int c[2] = {0, 0};
+  MMT_HIP(hipMemcpyAsync(&c[0], L.st.count, sizeof(int), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(&c[1], L.ob.count, sizeof(int), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipStreamSynchronize(st));
+  const int n0 = std::max(0, std::min(c[0], std::min(scap, L.st.cap)));
+  const int n1 = std::max(0, std::min(c[1], std::min(ocap, L.ob.cap)));
+  if (n0 > 0 && sxy)
+    MMT_HIP(hipMemcpyAsync(sxy, L.st.keys, sizeof(float2) * n0, hipMemcpyDeviceToHost, st));
+  if (n1 > 0 && oxy)
+    MMT_HIP(hipMemcpyAsync(oxy, L.ob.keys, sizeof(float2) * n1, hipMemcpyDeviceToHost, st));
+  if (n1 > 0 && olab)
+    MMT_HIP(hipMemcpyAsync(olab, L.ob.label, sizeof(int32_t) * n1, hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipStreamSynchronize(st));
+  *ns = n0;
+  *no = n1;
+}
+
 void Tracker::set_deferred(bool on) {
   if (on && ow_on_) throw ArgError("deferred object results need the inline object path (MMT_OBJ_THREAD=0)");
   if (on == defer_) return;

@@ -116,3 +116,30 @@ def object_eval(ob, Tlw_gt, Tcw_gt, rows, i):
     E = np.linalg.inv(M) @ H
     t_rpe, t_gt = np.linalg.norm(E[:3, 3]), np.linalg.norm(H[:3, 3])
     return (sp_est * 36, sp_gt * 36, abs(sp_est - sp_gt) * 36, t_rpe / t_gt * 100)
+
+
+def test_cli_writes_the_visual_artifacts(tmp_path):
+    """rgbd_mmt --viz (Tracking.cc:684-878): traj.png (600 x 800, the camera squares in red),
+    feat.png and speed.png at the image size for the last frame: feat.png is the image with
+    red static samples and label-coloured object samples drawn over it, speed.png the gray
+    image with orange ground-truth boxes."""
+    n = write_sequence(str(tmp_path))
+    exe = os.path.join(ROOT, "multimot_track_amd", "rgbd_mmt")
+    vd = tmp_path / "viz"
+    vd.mkdir()
+    r = subprocess.run([exe, "ORBvoc.txt", str(tmp_path / "settings.yaml"), str(tmp_path),
+                        "--nfeatures", "2000", "--viz", str(vd)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    traj = np.asarray(Image.open(vd / "traj.png").convert("RGB"))
+    feat = np.asarray(Image.open(vd / "feat.png").convert("RGB"))
+    speed = np.asarray(Image.open(vd / "speed.png").convert("RGB"))
+    assert traj.shape == (800, 600, 3) and feat.shape == (375, 1242, 3) == speed.shape
+    red = (traj[:, :, 0] == 255) & (traj[:, :, 1] == 0) & (traj[:, :, 2] == 0)
+    assert red.sum() > 4 * 10 * n // 2  # one square outline per frame
+    img = load_kitti_frame(n - 1)["bgr"][:, :, ::-1]
+    changed = np.any(feat != img, axis=2)
+    assert 200 < changed.sum() < 0.5 * changed.size  # drawn over the image
+    orange = (speed[:, :, 0] == 255) & (speed[:, :, 1] == 140) & (speed[:, :, 2] == 0)
+    g = speed[:, :, 0] == speed[:, :, 1]
+    assert g.mean() > 0.9 and orange.sum() > 0

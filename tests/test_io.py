@@ -29,6 +29,7 @@ def io():
     L.mmt_io_read_poses.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ip]
     L.mmt_io_yaml_float.argtypes = [ctypes.c_char_p, ctypes.c_char_p,
                                     ctypes.POINTER(ctypes.c_double)]
+    L.mmt_io_write_png_bgr.argtypes = [ctypes.c_char_p, vp, ctypes.c_int, ctypes.c_int]
     L.mmt_io_free.argtypes = [vp]
     return L
 
@@ -87,6 +88,21 @@ def test_png_rejects_garbage(io, tmp_path):
     p.write_bytes(b"not a png at all")
     assert read_png(io, str(p))[0] < 0
     assert read_png(io, str(tmp_path / "missing.png"))[0] < 0
+
+
+def test_png_writer_round_trips_through_pil_and_the_reader(io, tmp_path):
+    """cv::imwrite of a BGR image (rgbd_mmt --viz's feat.png / speed.png / traj.png): PIL reads
+    the RGB it stored, and mmt_io_read_png reads back the BGR bytes."""
+    from PIL import Image
+    rng = np.random.default_rng(5)
+    bgr = rng.integers(0, 256, (41, 67, 3), dtype=np.uint8)
+    p = str(tmp_path / "w.png")
+    assert io.mmt_io_write_png_bgr(p.encode(), bgr.ctypes.data, 67, 41) == 0
+    assert np.array_equal(np.asarray(Image.open(p).convert("RGB")), bgr[:, :, ::-1])
+    rc, got = read_png(io, p)
+    assert rc == 0 and np.array_equal(got, bgr)
+    assert io.mmt_io_write_png_bgr(str(tmp_path / "no" / "dir.png").encode(), bgr.ctypes.data,
+                                   67, 41) < 0
 
 
 def test_flo_round_trip(io, tmp_path):
