@@ -390,7 +390,8 @@ void MapEngine::local_bundle_adjustment(int kf) {  // Optimizer::LocalBundleAdju
   std::vector<int> verts = local;
   verts.insert(verts.end(), fixedKFs.begin(), fixedKFs.end());
   const int nK = (int)verts.size(), nP = (int)lpts.size();
-  std::map<int, int> vIdx;
+  std::vector<int>& vIdx = ba_vidx_;  // keyframe -> vertex, -1 elsewhere (reset below)
+  if (vIdx.size() < kfs_.size()) vIdx.resize(kfs_.size(), -1);
   std::vector<float> Tv(16 * (size_t)nK), Xv(3 * (size_t)nP);
   std::vector<uint8_t> fixed(nK);
   int nO = 0;
@@ -411,7 +412,7 @@ void MapEngine::local_bundle_adjustment(int kf) {  // Optimizer::LocalBundleAdju
       if (Ki.bad) continue;
       const mmt_kp& kp = Ki.keys[kv.second];
       e_pt.push_back(j);
-      e_kf.push_back(vIdx.at(kv.first));
+      e_kf.push_back(vIdx[kv.first]);
       e_kfid.push_back(kv.first);
       e_obs.push_back(kp.x);
       e_obs.push_back(kp.y);
@@ -420,6 +421,7 @@ void MapEngine::local_bundle_adjustment(int kf) {  // Optimizer::LocalBundleAdju
     }
   }
   const int nE = (int)e_pt.size();
+  for (int v = 0; v < nK; v++) vIdx[verts[v]] = -1;  // every edge's keyframe is a vertex
   BAHostProblem P;
   P.n_kf = nK;
   P.n_pt = nP;

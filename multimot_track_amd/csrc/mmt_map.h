@@ -318,6 +318,7 @@ class MapEngine {
   int2* h_fres_ = nullptr;
   size_t fres_cap_ = 0;
   BARunner ba_;  // the local BA's buffers and launch
+  std::vector<int> ba_vidx_;  // keyframe -> BA vertex while a local BA's graph is built
   void grow_dev(uint8_t*& d, uint8_t*& h, size_t& cap, size_t need);
 };
 
