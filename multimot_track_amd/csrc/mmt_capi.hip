@@ -803,7 +803,7 @@ int mmt_local_bundle_adjustment(mmt_ctx* ctx, const mmt_ba_problem* p, float* Tc
     P.e_s = p->e_inv_sigma2;
     const mmt_config& c = ctx->cfg;
     P.fx = c.fx; P.fy = c.fy; P.cx = c.cx; P.cy = c.cy; P.bf = c.bf;
-    mmt::BARunner runner;
+    mmt::BARunner& runner = ctx->ba;
     std::vector<float> T(16 * (size_t)std::max(p->n_kf, 1)), X(3 * (size_t)std::max(p->n_pt, 1));
     std::vector<uint8_t> er(std::max(p->n_edge, 1));
     int st[5] = {0, 0, 0, 0, 0};

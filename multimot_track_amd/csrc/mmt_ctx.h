@@ -2,6 +2,7 @@
 #pragma once
 #include <deque>
 
+#include "mmt_ba.h"
 #include "mmt_internal.h"
 #include "mmt_tracker.h"
 
@@ -21,6 +22,7 @@ struct mmt_ctx {
   // tracking (one sequence per context)
   mmt::Tracker tracker;
   bool tracker_ready = false;
+  mmt::BARunner ba;  // mmt_local_bundle_adjustment's buffers (kept across calls)
   uint8_t* t_bgr = nullptr;
   uint16_t* t_disp = nullptr;
   float* t_flow = nullptr;
