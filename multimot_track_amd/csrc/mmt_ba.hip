@@ -787,6 +787,7 @@ struct BAWork2 {
   uint8_t* kf_act;  // n_kf: optimised keyframe with an active edge this round
   uint8_t* pt_act;  // n_pt
   int gP;           // point workgroups
+  int spec;         // k_ba2_p4<true>: the trial kernel linearises at the trial state
 };
 
 // workgroup sums of K <= 64 values per thread, fixed order (DPP wave sums, then the waves in
@@ -1354,6 +1355,10 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
 
 // trial step 4, one thread per point: x_l = D^-1 (b_l - H_pl^T x_p) (stale on a failed solve),
 // the trial point, the errors of its active edges at the trial state, chi2 and the scale term
+// SPEC (MMT_BA_SPEC=1): also linearise at the trial state, so an accepted trial needs no
+// k_ba2_lin; measured slower (the linearisation's registers slow every trial more than the launch
+// it saves), off by default
+template <bool SPEC>
 __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
   __shared__ double s_part[2 * kMkWaves];
   const BAState* st = w.st;
@@ -1394,10 +1399,24 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
         sc += xv * (lambda * xv + bl_c[3 * (size_t)j + r]);
         X[r] += xv;
       }
-      // the trial's errors and chi2, and the linearisation at the trial state (the next
-      // iteration's system if the trial is accepted) into the other buffer
-      double m;
-      chi = ba2_lin_point(d, w, j, tri, X, robust, nb, &m);
+      if (SPEC) {
+        // the trial's errors and chi2, and the linearisation at the trial state (the next
+        // iteration's system if the trial is accepted) into the other buffer
+        double m;
+        chi = ba2_lin_point(d, w, j, tri, X, robust, nb, &m);
+      } else {  // the trial's errors and chi2
+        const Cam cam = ba_cam(d);
+        const double dMono = huber_mono(), dStereo = huber_stereo();
+        for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
+          if (w.level[e]) continue;
+          const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
+          const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], stereo,
+                                      tri[d.e_kf[e]], X, cam, &w.err[3 * (size_t)e]);
+          double r0 = c, r1;
+          if (robust) huber_rho(c, stereo ? dStereo : dMono, r0, r1);
+          chi += r0;
+        }
+      }
     }
 #pragma unroll
     for (int r = 0; r < 3; r++) Xt[3 * (size_t)j + r] = X[r];
@@ -1461,8 +1480,8 @@ __global__ __launch_bounds__(kMkDecideThreads) void k_ba2_p5(BADesc d, BAWork2 w
       s.lambda *= fmax(1. / 3., alpha);
       s.ni = 2;
       s.currentChi = tempChi;
-      s.cb = 1 - s.cb;  // the trial (and its linearisation) becomes the current estimate
-      s.spec_ok = 1;
+      s.cb = 1 - s.cb;  // the trial (and its linearisation, with SPEC) becomes the current estimate
+      s.spec_ok = w.spec;
     } else {
       s.lambda *= s.ni;
       s.ni *= 2;
@@ -1841,6 +1860,11 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.kf_act = take((size_t)nK);
     w.pt_act = take((size_t)nP);
     w.gP = gP;
+    static const int spec = [] {
+      const char* e = getenv("MMT_BA_SPEC");
+      return e && atoi(e) != 0 ? 1 : 0;
+    }();
+    w.spec = spec;
     const double tp1 = hp.on ? ba_now_us() : 0;
     double t_launch = 0, t_wait = 0;
     hipLaunchKernelGGL(k_ba2_init, dim3(gP), dim3(kMkThreads), 0, st, d, w);
@@ -1859,7 +1883,10 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
         if (w.n_bitem + w.n_kitem > 0)
           hipLaunchKernelGGL(k_ba2_p2, dim3(w.n_bitem + w.n_kitem), dim3(kMkThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p3, dim3(1), dim3(kMkSolveThreads), 0, st, d, w);
-        hipLaunchKernelGGL(k_ba2_p4, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        if (w.spec)
+          hipLaunchKernelGGL(k_ba2_p4<true>, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        else
+          hipLaunchKernelGGL(k_ba2_p4<false>, dim3(gP), dim3(kMkThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p5, dim3(1), dim3(kMkDecideThreads), 0, st, d, w);
       }
       MMT_HIP(hipGetLastError());
