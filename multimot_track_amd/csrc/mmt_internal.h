@@ -93,6 +93,10 @@ class OrbEngine {
   // 4 output truncated).  Reads them on `stream` (synchronising it); throws DeviceError and
   // clears them when any is set.
   void check_flags(hipStream_t stream);
+  // the error word as read by the caller (after a sync): 0 returns, otherwise the word is cleared
+  // on the device and the same DeviceError as check_flags is thrown
+  void check_flags_value(int flags, hipStream_t stream);
+  const int* err_word() const { return d_err_; }
   void raise_flags(int flags, hipStream_t stream);
 
  private:

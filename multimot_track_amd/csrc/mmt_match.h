@@ -63,10 +63,24 @@ struct CandSet {
 
 // B3 for nframes frames: keys/uR/kdepth/cell_idx at frame stride `cap`, cell_start at
 // kGridCells + 1, depth map at depth_pitch floats.
+// Optional host outputs of B3 (device-accessible pinned buffers at the same frame stride `cap`):
+// keys, descriptors (read from ddesc), uR, depths of the valid entries, nkp[0..nframes) and, at
+// nkp[nframes], the word at err_src (the ORB engine's error flags).
+struct B3HostOut {
+  mmt_kp* kps;
+  uint8_t* desc;
+  float* uR;
+  float* kdepth;
+  int* nkp;
+  const uint8_t* ddesc;
+  const int* err_src;
+};
+// the LDS budget of the grid build's cell lists (larger capacities sort in HBM)
+constexpr size_t kStereoGridLds = 48 * 1024;
 void launch_stereo_grid(const mmt_kp* keys, const int* nkp, int cap, const float* depth,
                         size_t depth_pitch, int W, int H, float bf, float invW, float invH,
                         float* uR, float* kdepth, int* cell_start, int* cell_idx, int nframes,
-                        hipStream_t st);
+                        hipStream_t st, const B3HostOut* ho = nullptr);
 
 // C2: SearchByProjection(Frame&, const Frame&, th, bMono) candidates + greedy replay.
 struct LastFrameDev {

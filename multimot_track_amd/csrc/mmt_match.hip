@@ -96,15 +96,22 @@ __device__ __forceinline__ void pose_centre(const float* T, float* o) {  // -R^T
 }
 
 // ------------------------------------------------------------------------------ B3
+// One workgroup per frame.  LDS: the frame's cell counts, then (LDS variant) the cell lists, built
+// and sorted in LDS and written out once, coalesced; the global variant (capacities above the LDS
+// budget) sorts in place in HBM.  With `ho` set, the frame's keys, descriptors, uR and depths go
+// straight into the caller's pinned host buffers (n valid entries, 16-byte stores), with its key
+// count and the ORB error word: the host copies of the chunk need no copy launches of their own.
+template <bool LDS>
 __global__ __launch_bounds__(1024) void k_stereo_grid(const mmt_kp* __restrict__ keys,
                                                       const int* __restrict__ nkp, int cap,
                                                       const float* __restrict__ depth,
                                                       size_t depth_pitch, int W, float bf,
                                                       float invW, float invH, float* uR,
                                                       float* kdepth, int* cell_start,
-                                                      int* cell_idx) {
+                                                      int* cell_idx, B3HostOut ho) {
   __shared__ int s_cnt[kGridCells];
   __shared__ int s_w[16];
+  extern __shared__ int s_idx[];  // LDS: cap entries
   const int f = blockIdx.x, t = threadIdx.x;
   keys += (size_t)f * cap;
   depth += (size_t)f * depth_pitch;
@@ -125,8 +132,27 @@ __global__ __launch_bounds__(1024) void k_stereo_grid(const mmt_kp* __restrict__
     }
     kdepth[i] = dd;
     uR[i] = ur;
+    if (ho.uR) {
+      ho.uR[(size_t)f * cap + i] = ur;
+      ho.kdepth[(size_t)f * cap + i] = dd;
+    }
     const int c = grid_cell(x, y, invW, invH);
     if (c >= 0) atomicAdd(&s_cnt[c], 1);
+  }
+  if (ho.kps) {
+    // keys (7 words each: one word per thread, consecutive lanes on consecutive words) and
+    // descriptors (two 16-byte halves) of the valid entries
+    static_assert(sizeof(mmt_kp) == 28, "mmt_kp layout");
+    const uint32_t* k1 = (const uint32_t*)keys;
+    uint32_t* hk = (uint32_t*)(ho.kps + (size_t)f * cap);
+    for (int i = t; i < 7 * n; i += blockDim.x) hk[i] = k1[i];
+    const uint4* d4 = (const uint4*)(ho.ddesc + (size_t)f * cap * 32);
+    uint4* hd = (uint4*)(ho.desc + (size_t)f * cap * 32);
+    for (int i = t; i < 2 * n; i += blockDim.x) hd[i] = d4[i];
+    if (t == 0) {
+      ho.nkp[f] = nkp[f];
+      if (f == 0) ho.nkp[gridDim.x] = *ho.err_src;
+    }
   }
   __syncthreads();
   // exclusive scan over the 3072 cells, three per thread (blockDim == 1024)
@@ -140,36 +166,51 @@ __global__ __launch_bounds__(1024) void k_stereo_grid(const mmt_kp* __restrict__
   cell_start[3 * t + 1] = excl + a0;
   cell_start[3 * t + 2] = excl + a0 + a1;
   if (t == 0) cell_start[kGridCells] = tot;
+  // cell c's list is [start(c), s_cnt[c]) once the scatter is done: keep the starts in registers
+  const int b0 = excl, b1 = excl + a0, b2 = excl + a0 + a1;
   __syncthreads();
+  int* list = LDS ? s_idx : cell_idx;
   for (int i = t; i < n; i += blockDim.x) {
     const int c = grid_cell(keys[i].x, keys[i].y, invW, invH);
-    if (c >= 0) cell_idx[atomicAdd(&s_cnt[c], 1)] = i;
+    if (c >= 0) list[atomicAdd(&s_cnt[c], 1)] = i;
   }
   __threadfence_block();
   __syncthreads();
   // restore ascending key order inside each cell (cells hold a handful of keys)
-  for (int c = t; c < kGridCells; c += blockDim.x) {
-    const int b = cell_start[c], e = s_cnt[c];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int b = k == 0 ? b0 : (k == 1 ? b1 : b2), e = s_cnt[3 * t + k];
     for (int p = b + 1; p < e; p++) {
-      const int v = cell_idx[p];
+      const int v = list[p];
       int q = p - 1;
-      while (q >= b && cell_idx[q] > v) {
-        cell_idx[q + 1] = cell_idx[q];
+      while (q >= b && list[q] > v) {
+        list[q + 1] = list[q];
         q--;
       }
-      cell_idx[q + 1] = v;
+      list[q + 1] = v;
     }
+  }
+  if (LDS) {
+    __syncthreads();
+    for (int p = t; p < tot; p += blockDim.x) cell_idx[p] = s_idx[p];
   }
 }
 
 void launch_stereo_grid(const mmt_kp* keys, const int* nkp, int cap, const float* depth,
                         size_t depth_pitch, int W, int H, float bf, float invW, float invH,
                         float* uR, float* kdepth, int* cell_start, int* cell_idx, int nframes,
-                        hipStream_t st) {
+                        hipStream_t st, const B3HostOut* ho) {
   (void)H;
   if (nframes <= 0) return;
-  hipLaunchKernelGGL(k_stereo_grid, dim3(nframes), dim3(1024), 0, st, keys, nkp, cap, depth,
-                     depth_pitch, W, bf, invW, invH, uR, kdepth, cell_start, cell_idx);
+  B3HostOut h{};
+  if (ho) h = *ho;
+  const size_t lds = sizeof(int) * (size_t)cap;
+  if (lds <= kStereoGridLds)
+    hipLaunchKernelGGL(k_stereo_grid<true>, dim3(nframes), dim3(1024), lds, st, keys, nkp, cap,
+                       depth, depth_pitch, W, bf, invW, invH, uR, kdepth, cell_start, cell_idx, h);
+  else
+    hipLaunchKernelGGL(k_stereo_grid<false>, dim3(nframes), dim3(1024), 0, st, keys, nkp, cap,
+                       depth, depth_pitch, W, bf, invW, invH, uR, kdepth, cell_start, cell_idx, h);
   MMT_HIP(hipGetLastError());
 }
 

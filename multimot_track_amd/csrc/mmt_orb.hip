@@ -1938,6 +1938,10 @@ void OrbEngine::check_flags(hipStream_t stream) {
   int flags = 0;
   MMT_HIP(hipMemcpyAsync(&flags, d_err_, sizeof(int), hipMemcpyDeviceToHost, stream));
   MMT_HIP(hipStreamSynchronize(stream));
+  check_flags_value(flags, stream);
+}
+
+void OrbEngine::check_flags_value(int flags, hipStream_t stream) {
   if (flags == 0) return;
   MMT_HIP(hipMemsetAsync(d_err_, 0, sizeof(int), stream));
   MMT_HIP(hipStreamSynchronize(stream));

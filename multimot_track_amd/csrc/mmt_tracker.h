@@ -116,6 +116,7 @@ class Tracker {
   // host enqueues both stages at once and only reads the results obj_lag_ frames later (finish).
   struct ObjFrame {
     bool active = false;
+    bool a_launched = false;  // obj_stage_a_launch ran
     long seq = 0;  // job number (obj_submit)
     int cur = 0, last = 0, slot = 0, nobj = 0;
     FrameOut* out = nullptr;
@@ -152,6 +153,9 @@ class Tracker {
   void ego_map_finish(FrameOut& out);
   void ego_finish(FrameOut& out, hipStream_t st);
   void obj_stage_a(ObjFrame& F);    // grouping + B7/B8 + PnP-RANSAC launch (stream oa_)
+  void obj_stage_a_launch(ObjFrame& F);  // its first half: the grouping kernel and its read-back
+  void obj_stage_a_decide(ObjFrame& F);  // its second half: B7/B8 on the host, the RANSAC launch
+  void obj_advance_launch();        // obj_advance's first step (stage A's launch), on its own
   void obj_stage_b(ObjFrame& F);    // MM matrix, MM check, model choice, D3 (stream ob_, no wait)
   void obj_finish(ObjFrame& F);     // waits for the frame's D3, object motions, results
   void obj_advance();               // enqueue the queued frame's object path, finish old frames
@@ -185,6 +189,8 @@ class Tracker {
     uint8_t* desc = nullptr;
     float* uR = nullptr;
     float* kdepth = nullptr;
+    int* nkp = nullptr;  // [max_chunk] key counts, then the ORB error word
+    B3HostOut dev;       // the same buffers as the device addresses them (k_stereo_grid writes)
   };
   HostChunk hc_[2];
   int chunk_buf_ = 0;
@@ -252,6 +258,7 @@ class Tracker {
   double* d_Rt_[kObjSlots] = {};
   FlowSolveDesc* d_descs3_[kObjSlots] = {};  // D3 solves of the slot's frame
   hipEvent_t ev_ransac_[kObjSlots] = {};
+  hipEvent_t ev_grp_[kObjSlots] = {};  // the grouping statistics are on the host
   hipEvent_t ev_d3_[kObjSlots] = {};
   // subset draws depend only on the point count: cache the last few counts
   struct SubsetCache {
@@ -303,6 +310,8 @@ class Tracker {
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
   // the previous frame's object path inside the first map chain of the frame (MMT_OBJ_OVERLAP)
   bool overlap_obj_ = true;
+  bool obj_split_ = false;  // MMT_OBJ_SPLIT
+  bool b3_host_ = true;    // MMT_B3_HOST
   bool obj_ran_ = false;
   // object worker
   bool ow_on_ = false;

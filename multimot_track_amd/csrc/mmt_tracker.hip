@@ -148,10 +148,11 @@ Tracker::~Tracker() {
   for (ObjHost* h : oh_)
     if (h) (void)hipHostFree(h);
   for (HostChunk& h : hc_)
-    for (void* p : {(void*)h.kps, (void*)h.desc, (void*)h.uR, (void*)h.kdepth})
+    for (void* p : {(void*)h.kps, (void*)h.desc, (void*)h.uR, (void*)h.kdepth, (void*)h.nkp})
       if (p) (void)hipHostFree(p);
   for (int q = 0; q < kObjSlots; q++) {
     if (ev_ransac_[q]) (void)hipEventDestroy(ev_ransac_[q]);
+    if (ev_grp_[q]) (void)hipEventDestroy(ev_grp_[q]);
     if (ev_d3_[q]) (void)hipEventDestroy(ev_d3_[q]);
   }
   for (hipEvent_t& e : ev_orb_)
@@ -257,6 +258,7 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   if (!oh_[q]) MMT_HIP(hipHostMalloc((void**)&oh_[q], sizeof(ObjHost), hipHostMallocDefault));
   memset(oh_[q], 0, sizeof(ObjHost));
   if (!ev_ransac_[q]) MMT_HIP(hipEventCreateWithFlags(&ev_ransac_[q], hipEventDisableTiming));
+  if (!ev_grp_[q]) MMT_HIP(hipEventCreateWithFlags(&ev_grp_[q], hipEventDisableTiming));
   if (!ev_d3_[q]) MMT_HIP(hipEventCreateWithFlags(&ev_d3_[q], hipEventDisableTiming));
   for (int o = 0; o < kMaxObj; o++) {
     PnPBuf& b = pnp_[q][o];
@@ -294,6 +296,14 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
                             hipHostMallocDefault));
       MMT_HIP(hipHostMalloc((void**)&h.kdepth, sizeof(float) * (size_t)kcap_ * max_chunk,
                             hipHostMallocDefault));
+      MMT_HIP(hipHostMalloc((void**)&h.nkp, sizeof(int) * ((size_t)max_chunk + 1),
+                            hipHostMallocDefault));
+      memset(&h.dev, 0, sizeof(h.dev));
+      MMT_HIP(hipHostGetDevicePointer((void**)&h.dev.kps, h.kps, 0));
+      MMT_HIP(hipHostGetDevicePointer((void**)&h.dev.desc, h.desc, 0));
+      MMT_HIP(hipHostGetDevicePointer((void**)&h.dev.uR, h.uR, 0));
+      MMT_HIP(hipHostGetDevicePointer((void**)&h.dev.kdepth, h.kdepth, 0));
+      MMT_HIP(hipHostGetDevicePointer((void**)&h.dev.nkp, h.nkp, 0));
     }
   }
   {
@@ -372,6 +382,15 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // MMT_DEBUG_SPLIT_SPIN: the split ego solve's exchange spin bound in wall-clock ticks (test
   // hook: a tiny bound forces the not-resident status and so the one-workgroup re-run)
   if (const char* ss = getenv("MMT_DEBUG_SPLIT_SPIN")) split_spin_ = strtoull(ss, nullptr, 10);
+  // MMT_OBJ_SPLIT=1: the overlap above in two steps (C2: the grouping launch; C3: the rest);
+  // measured slower, off by default (interleaved A/B: C3 888 against 903 frames/s, one frame per
+  // call 1.90-1.93 against 1.77-1.83 ms).  MMT_B3_HOST (default 1): k_stereo_grid writes the
+  // chunk's host copies itself (one frame per call 1.90-1.93 against 2.01-2.22 ms with the
+  // capacity-sized copies; C3 within noise, 888 against 894)
+  const char* os = getenv("MMT_OBJ_SPLIT");
+  obj_split_ = os && atoi(os) == 1;
+  const char* bh = getenv("MMT_B3_HOST");
+  b3_host_ = !(bh && atoi(bh) == 0);
   const char* oo = getenv("MMT_OBJ_OVERLAP");
   overlap_obj_ = !(oo && atoi(oo) == 0);
   const char* ot = getenv("MMT_OBJ_THREAD");
@@ -587,25 +606,39 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
                     d_depth_, npix, (int)npix, nframes, cfg_.bf, st);
   engine_->run(gray, nframes, gpitch, d_kps_, d_desc_, kcap_, d_nkp_, st);
   if (prof_) MMT_HIP(hipEventRecord(ev_orb_[1], st));
-  // B3 (ComputeStereoFromRGBD + AssignFeaturesToGrid) of every frame of the chunk, and the host
-  // copies the map bookkeeping reads (keys, descriptors, mvuRight, mvDepth)
-  launch_stereo_grid(d_kps_, d_nkp_, kcap_, d_depth_, npix, W_, H_, cfg_.bf, grid0_.invW,
-                     grid0_.invH, d_uR_, d_kdepth_, d_cell_start_, d_cell_idx_, nframes, st);
-  // the host copies go to the buffer the last frame does not live in; it becomes the current one
-  // only once the chunk's ORB passed its device checks (a failed chunk leaves no trace)
+  // B3 (ComputeStereoFromRGBD + AssignFeaturesToGrid) of every frame of the chunk; the same
+  // kernel writes the host copies the map bookkeeping reads (keys, descriptors, mvuRight,
+  // mvDepth, the key counts and the ORB error word) into pinned memory, valid entries only.  They
+  // go to the buffer the last frame does not live in; it becomes the current one only once the
+  // chunk's ORB passed its device checks (a failed chunk leaves no trace)
   const int nbuf = chunk_buf_ ^ 1;
   const HostChunk& hc = hc_[nbuf];
-  MMT_HIP(hipMemcpyAsync(hc.kps, d_kps_, sizeof(mmt_kp) * (size_t)kcap_ * nframes,
-                         hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(hc.desc, d_desc_, 32 * (size_t)kcap_ * nframes, hipMemcpyDeviceToHost,
-                         st));
-  MMT_HIP(hipMemcpyAsync(hc.uR, d_uR_, sizeof(float) * (size_t)kcap_ * nframes,
-                         hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(hc.kdepth, d_kdepth_, sizeof(float) * (size_t)kcap_ * nframes,
-                         hipMemcpyDeviceToHost, st));
   std::vector<int> nkp(nframes);
-  MMT_HIP(hipMemcpyAsync(nkp.data(), d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));
-  engine_->check_flags(st);  // synchronises st; throws on a tripped octree guard
+  if (b3_host_) {
+    B3HostOut ho = hc.dev;
+    ho.ddesc = d_desc_;
+    ho.err_src = engine_->err_word();
+    launch_stereo_grid(d_kps_, d_nkp_, kcap_, d_depth_, npix, W_, H_, cfg_.bf, grid0_.invW,
+                       grid0_.invH, d_uR_, d_kdepth_, d_cell_start_, d_cell_idx_, nframes, st,
+                       &ho);
+    MMT_HIP(hipStreamSynchronize(st));
+    engine_->check_flags_value(hc.nkp[nframes], st);  // throws on a tripped octree guard
+    std::copy(hc.nkp, hc.nkp + nframes, nkp.begin());
+  } else {  // MMT_B3_HOST=0: capacity-sized copies after the kernel (A/B)
+    launch_stereo_grid(d_kps_, d_nkp_, kcap_, d_depth_, npix, W_, H_, cfg_.bf, grid0_.invW,
+                       grid0_.invH, d_uR_, d_kdepth_, d_cell_start_, d_cell_idx_, nframes, st);
+    MMT_HIP(hipMemcpyAsync(hc.kps, d_kps_, sizeof(mmt_kp) * (size_t)kcap_ * nframes,
+                           hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipMemcpyAsync(hc.desc, d_desc_, 32 * (size_t)kcap_ * nframes,
+                           hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipMemcpyAsync(hc.uR, d_uR_, sizeof(float) * (size_t)kcap_ * nframes,
+                           hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipMemcpyAsync(hc.kdepth, d_kdepth_, sizeof(float) * (size_t)kcap_ * nframes,
+                           hipMemcpyDeviceToHost, st));
+    MMT_HIP(hipMemcpyAsync(hc.nkp, d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));
+    engine_->check_flags(st);  // synchronises st; throws on a tripped octree guard
+    std::copy(hc.nkp, hc.nkp + nframes, nkp.begin());
+  }
   chunk_buf_ = nbuf;
   if (prof_) {
     float ms = 0;
@@ -750,6 +783,10 @@ void Tracker::flush_deferred(std::vector<FrameOut>& outs) {
 // Enqueue the queued frame's whole object path (stage A's host decisions need one wait for the
 // grouping statistics; stage B is device-ordered), then read the results of frames older than
 // obj_lag_.  Called while the next ego solve runs.
+void Tracker::obj_advance_launch() {
+  if (qa_.active) obj_stage_a_launch(qa_);
+}
+
 void Tracker::obj_advance() {
   obj_ran_ = true;
   auto now = [] {
@@ -846,7 +883,16 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   {
     MapStatsH& ms = out.map;
     // the previous frame's object path runs while the first map chain is on the GPU
-    if (!ow_on_ && overlap_obj_) map_.set_overlap([this] { obj_advance(); });
+    // in two steps: the grouping kernel goes out inside the first map chain (C2), the host
+    // decisions, the RANSAC, D3 and the old frames' results inside the second (C3), whose kernels
+    // then run while the host works; a frame without C3 finishes them after the map branch
+    if (!ow_on_ && overlap_obj_ && obj_split_)
+      map_.set_overlap([this] {
+        obj_advance_launch();
+        map_.set_overlap([this] { obj_advance(); });
+      });
+    else if (!ow_on_ && overlap_obj_)  // MMT_OBJ_SPLIT=0: all of it inside the first chain
+      map_.set_overlap([this] { obj_advance(); });
     const int rr = map_.track(C.m, G, ego_Tinit_, Ls.m, Ls.Tview, V_, hasVelocity_,
                               bSecondFrame_, ms, st);
     map_.set_overlap(nullptr);  // not taken (no chain ran): the loop runs it
@@ -997,9 +1043,16 @@ void Tracker::ego_finish(FrameOut& out, hipStream_t st) {
 }
 
 void Tracker::obj_stage_a(ObjFrame& F) {
+  obj_stage_a_launch(F);
+  obj_stage_a_decide(F);
+}
+
+void Tracker::obj_stage_a_launch(ObjFrame& F) {
   FrameSlot& C = slot_[F.cur];
   FrameSlot& Ls = slot_[F.last];
   hipStream_t st = oa_;
+  if (F.a_launched) return;
+  F.a_launched = true;
   F.slot = obj_slot_next_;
   obj_slot_next_ = (obj_slot_next_ + 1) % kObjSlots;
   const int q = F.slot;
@@ -1034,7 +1087,18 @@ void Tracker::obj_stage_a(ObjFrame& F) {
   MMT_HIP(hipMemcpyAsync(H.stats, d_stats_[q], sizeof(H.stats), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(H.hist, d_hist_[q], sizeof(H.hist), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(&H.err, d_err_, sizeof(int), hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipStreamSynchronize(st));
+  MMT_HIP(hipEventRecord(ev_grp_[q], st));
+}
+
+void Tracker::obj_stage_a_decide(ObjFrame& F) {
+  FrameSlot& C = slot_[F.cur];
+  FrameSlot& Ls = slot_[F.last];
+  hipStream_t st = oa_;
+  if (!F.a_launched) obj_stage_a_launch(F);
+  if (F.nobj == 0) return;  // no object samples carried into this frame
+  const int q = F.slot;
+  ObjHost& H = *oh_[q];
+  MMT_HIP(hipEventSynchronize(ev_grp_[q]));
   if (H.err) {
     MMT_HIP(hipMemsetAsync(d_err_, 0, sizeof(int), st));  // the next frame starts clean
     MMT_HIP(hipStreamSynchronize(st));

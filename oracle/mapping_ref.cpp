@@ -12,6 +12,7 @@
 // (KeyFrame.cc:553-608, 174-182, 70-84).  cv::Mat float arithmetic as in map_ref.cpp.  Containers
 // keyed by KeyFrame* / MapPoint* iterate in creation order (oracle_map.h).
 
+#include <cstdlib>
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -415,10 +416,16 @@ void MapTracker::keyframe_culling(int kf) {  // LocalMapping::KeyFrameCulling (R
 }
 
 void MapTracker::local_mapping(int kf) {
+  // ORACLE_LM_STEPS (diagnostics only, default 7): bit 1 SearchInNeighbors, 2 the local BA,
+  // 4 KeyFrameCulling
+  static const int steps = [] {
+    const char* e = getenv("ORACLE_LM_STEPS");
+    return e ? atoi(e) : 7;
+  }();
   // CreateNewMapPoints: needs SearchForTriangulation (BoW), skipped (oracle_map.h)
-  search_in_neighbors(kf);
-  if (n_keyframes() > 2) local_bundle_adjustment(kf);
-  keyframe_culling(kf);
+  if (steps & 1) search_in_neighbors(kf);
+  if ((steps & 2) && n_keyframes() > 2) local_bundle_adjustment(kf);
+  if (steps & 4) keyframe_culling(kf);
 }
 
 }  // namespace oracle

@@ -1,12 +1,14 @@
 """Per-frame kernel timeline of a filtered rocprofv3 kernel trace (columns Kernel_Name, Queue_Id,
 Start_Timestamp, End_Timestamp, as tools/one_frame_bench.py under `rocprofv3 --kernel-trace`):
-frames are cut at every `k_gray_depth` launch (one per call in the one-frame pattern).  Prints, for
+frames are cut at every launch of the kernel named by MMT_CUT (default `k_gray_depth`, one per
+call in the one-frame pattern; `k_static_samples` cuts the frames of a chunked run).  Prints, for
 the frames asked, each kernel's start offset, duration, the idle gap before it on its queue and
 its name; and over all frames the device time and launch count per kernel name per frame, and
 the busy fraction of the frame's wall time.
 Usage: frame_timeline.py trace.csv [frame numbers to list, e.g. 30 31]"""
 import collections
 import csv
+import os
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
@@ -17,7 +19,8 @@ for r in rows:
     name = name.replace("(anonymous namespace)::", "")
     ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"], name))
 ks.sort()
-cuts = [i for i, k in enumerate(ks) if k[3].startswith("k_gray_depth")]
+cut = os.environ.get("MMT_CUT", "k_gray_depth")
+cuts = [i for i, k in enumerate(ks) if k[3].startswith(cut)]
 tot = collections.defaultdict(float)
 cnt = collections.defaultdict(int)
 walls, busy = [], []
