@@ -17,16 +17,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--start", type=int, default=8)
+    ap.add_argument("--objects", type=int, default=3)
+    ap.add_argument("--immediate", action="store_true", help="object results at every call")
     a = ap.parse_args()
     import torch
     import multimot_track_amd as M
     from multimot_track_amd import scene, shard
     dev = torch.device("cuda:0")
     n = a.start + a.frames
-    s = scene.kitti_like_sequence(n, 1242, 375, n_objects=3, seed=shard.sequence_seed(1003, 0),
-                                  device=dev)
+    s = scene.kitti_like_sequence(n, 1242, 375, n_objects=a.objects,
+                                  seed=shard.sequence_seed(1003, 0), device=dev)
     ctx = M.Context(M.kitti03_config(1242, 375, 2000, max_batch=8))
-    ctx.set_deferred_objects(True)
+    ctx.set_deferred_objects(not a.immediate)
     st = torch.cuda.current_stream(dev).cuda_stream
 
     def call(i):
@@ -43,7 +45,8 @@ def main():
         raw = call(i)
         t.append(time.perf_counter() - t0)
         kf.append(int(raw[0][0].new_keyframe))
-    ctx.flush_objects()
+    if not a.immediate:
+        ctx.flush_objects()
     torch.cuda.synchronize(dev)
     t_all = time.perf_counter() - t_all
     t, kf = np.array(t) * 1e3, np.array(kf, bool)
