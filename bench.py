@@ -399,6 +399,10 @@ def main(argv=None):
             local_mapping[k] = round(float(mc[k]), 1)
     local_mapping["keyframes_last_frame"] = int(timed_frames[-1]["n_keyframes"])
     local_mapping["mappoints_last_frame"] = int(timed_frames[-1]["n_mappoints"])
+    # the timed contexts are done: the legs below run beside no other context of this process (a
+    # context's streams share the process's hardware queues with every other context's)
+    for c in ctxs:
+        c.close()
 
     if rank == 0:
         value = frames_all / elapsed

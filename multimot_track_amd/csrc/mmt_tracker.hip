@@ -336,18 +336,21 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     for (int l = 0; l < t.nlevels; l++) G.scale[l] = t.scale[l];
     G.logScale = mc.logScale;
   }
-  // The two object stages need hardware queues of their own (streams beyond the runtime's
-  // GPU_MAX_HW_QUEUES share queues and serialise): the D3 stage, the longest chain, gets a
-  // high-priority stream, which the runtime maps to a separate queue.
+  // The two object stages run on streams of their own (streams beyond the runtime's
+  // GPU_MAX_HW_QUEUES share hardware queues; a priority class other than normal gets a queue of
+  // its own: the RANSAC stream is low priority).
   int lo = 0, hi = 0;
   MMT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  // The RANSAC stream is confined to every 4th CU (MMT_RANSAC_CU_MASK=0: all CUs, low priority).
-  // Its kernels are grids of hundreds of one-wave workgroups at 256 VGPRs; spread over the whole
-  // chip they leave no CU with a free SIMD for the ego chain's and D3's workgroups (256-thread
-  // solves at 256 VGPRs + 230 AGPRs need all four SIMDs of a CU), which then wait for the RANSAC
-  // kernels to drain.
+  // MMT_RANSAC_CU_MASK=1: the RANSAC stream confined to every 4th CU (otherwise every CU, low
+  // priority).  Its kernels are grids of hundreds of one-wave workgroups at 256 VGPRs; spread over
+  // the whole chip they can leave no CU with a free SIMD for the ego chain's workgroups.
+  // MMT_D3_PRIO=1: the D3 stream at high priority (otherwise normal).  Round 3 chose both for the
+  // chunked bench; measured again with LocalMapping (interleaved A/B, tools/ab_interleave.py and
+  // tools/one_frame_bench.py): chunked C3 895 (both on) against 896 frames/s (both off), one frame
+  // per call 1.77 against 1.49 ms (the high-priority D3 queue and the masked RANSAC grids delay
+  // the ego chain's one-workgroup solves: k_pose_opt_l<4> 5 -> 100+ µs beside k_pnp_hyp)
   const char* cm = getenv("MMT_RANSAC_CU_MASK");
-  if (!(cm && atoi(cm) == 0)) {
+  if (cm && atoi(cm) == 1) {
     int ncu = 0;
     MMT_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg.device_id));
     std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
@@ -356,8 +359,9 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   } else {
     MMT_HIP(hipStreamCreateWithPriority(&oa_, hipStreamNonBlocking, lo));
   }
-  const char* dp = getenv("MMT_D3_PRIO");  // 0: the D3 stream at normal priority (A/B knob)
-  MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, dp && atoi(dp) == 0 ? 0 : hi));
+  const char* dp = getenv("MMT_D3_PRIO");  // 1 high, 0 normal, otherwise low
+  const int d3p = dp && atoi(dp) == 1 ? hi : (dp && atoi(dp) == 0 ? 0 : lo);
+  MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, d3p));
   MMT_HIP(hipHostMalloc((void**)&eh_, sizeof(EgoHost), hipHostMallocDefault));
   memset(eh_, 0, sizeof(EgoHost));
   for (auto& e : ev_slot_)

@@ -29,7 +29,7 @@ def main():
                                   seed=shard.sequence_seed(1003, 0), device=dev)
     ctx = M.Context(M.kitti03_config(1242, 375, 2000, max_batch=8))
     ctx.set_deferred_objects(not a.immediate)
-    st = torch.cuda.current_stream(dev).cuda_stream
+    st = torch.cuda.Stream(dev).cuda_stream  # a stream of the caller's, as bench.py's leg
 
     def call(i):
         return ctx.track_chunk_device(s["bgr"][i:i + 1], s["disp"][i:i + 1], s["flow"][i:i + 1],
