@@ -784,6 +784,7 @@ struct BAWork2 {
   double* linpart;  // 2 per point workgroup: chi2, largest active H_ll diagonal
   double* p4part;   // 2 per point workgroup: trial chi2, scale
   uint8_t* level;   // n_edge
+  int* eopt;        // n_edge: the edge's optimised-keyframe index, -1 for a fixed keyframe
   uint8_t* kf_act;  // n_kf: optimised keyframe with an active edge this round
   uint8_t* pt_act;  // n_pt
   int gP;           // point workgroups
@@ -875,6 +876,7 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_init(BADesc d, BAWork2 w) {
   }
   for (int e = gt; e < d.n_edge; e += gs) {
     w.level[e] = 0;
+    w.eopt[e] = d.opt_of[d.e_kf[e]];
     w.err[3 * (size_t)e] = w.err[3 * (size_t)e + 1] = w.err[3 * (size_t)e + 2] = 0;
   }
   if (blockIdx.x == 0) {
@@ -1059,7 +1061,7 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p1(BADesc d, BAWork2 w) {
 #pragma unroll
   for (int a = 0; a < 3; a++) db[a] = Di[3 * a] * b3[0] + Di[3 * a + 1] * b3[1] + Di[3 * a + 2] * b3[2];
   for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
-    if (w.level[e] || d.opt_of[d.e_kf[e]] < 0) continue;
+    if (w.level[e] || w.eopt[e] < 0) continue;
     const double* B = &Hpl_c[18 * (size_t)e];
     double* Ye = &w.Y[18 * (size_t)e];
     double* ce = &w.cv[6 * (size_t)e];
@@ -1379,17 +1381,24 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
     if (w.pt_act[j]) {
       double* xl = &w.x[n6 + 3 * (size_t)j];
       if (ok2) {
+        // the loads that depend on j alone first (D^-1), then per edge its H_pl block issued with
+        // its keyframe index, before the branch on it (the block exists for every edge)
+        double Di[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) Di[q] = w.Dinv[9 * (size_t)j + q];
         double cl[3] = {bl_c[3 * (size_t)j], bl_c[3 * (size_t)j + 1], bl_c[3 * (size_t)j + 2]};
         for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
-          const int a = d.opt_of[d.e_kf[e]];
-          if (w.level[e] || a < 0) continue;
-          const double* B = &Hpl_c[18 * (size_t)e];
+          const int a = w.eopt[e];
+          const bool on = !w.level[e] && a >= 0;
+          double B[18];
+#pragma unroll
+          for (int q = 0; q < 18; q++) B[q] = Hpl_c[18 * (size_t)e + q];
+          if (!on) continue;
 #pragma unroll
           for (int c = 0; c < 3; c++)
 #pragma unroll
             for (int r = 0; r < 6; r++) cl[c] += B[3 * r + c] * (-w.x[6 * a + r]);
         }
-        const double* Di = &w.Dinv[9 * (size_t)j];
 #pragma unroll
         for (int a = 0; a < 3; a++) xl[a] = Di[3 * a] * cl[0] + Di[3 * a + 1] * cl[1] + Di[3 * a + 2] * cl[2];
       }
@@ -1622,7 +1631,7 @@ size_t ba2_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt, int n_blk,
          a(8 * 18 * (size_t)n_edge) + a(8 * 6 * (size_t)n_edge) + a(8 * 36 * (size_t)n_opt) +
          a(8 * 6 * (size_t)n_opt) + a(8 * 6 * (size_t)n_opt) + a(8 * 36 * (size_t)n_blk) +
          a(8 * (n6 + 3 * (size_t)n_pt)) + a(8 * n6 * n6) + a(8 * 3 * n6) + 2 * a(8 * 2 * (size_t)gP) +
-         a((size_t)n_edge) + a((size_t)n_kf) + a((size_t)n_pt) + 64;
+         a((size_t)n_edge) + a(4 * (size_t)n_edge) + a((size_t)n_kf) + a((size_t)n_pt) + 64;
 }
 
 void launch_local_ba(const BADesc& d, hipStream_t st) {
@@ -1857,6 +1866,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.linpart = (double*)take(8 * 2 * (size_t)gP);
     w.p4part = (double*)take(8 * 2 * (size_t)gP);
     w.level = take((size_t)nE);
+    w.eopt = (int*)take(4 * (size_t)nE);
     w.kf_act = take((size_t)nK);
     w.pt_act = take((size_t)nP);
     w.gP = gP;
