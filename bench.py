@@ -113,6 +113,9 @@ def parse_args(argv=None):
                          "pipeline at each chunk boundary)")
     ap.add_argument("--single-frames", type=int, default=256,
                     help="frames of the one-frame-per-call leg (0: skip)")
+    ap.add_argument("--rank-parity-frames", type=int, default=192,
+                    help="frames of every sequence checked against the oracle on lines with "
+                         "several sequences or ranks (0: skip)")
     ap.add_argument("--dry", action="store_true", help="CPU rehearsal of the rank logic")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args(argv)
@@ -249,6 +252,31 @@ def cpu_multi_leg(args, render, W, H, NF, fps1):
                       "per-core rates" % (K, 2002 + K, args.cpu_seqs_seconds)}
 
 
+def rank_parity(args, seqs, seq_frames, rank, K, W, H, NF):
+    """The oracle over the first --rank-parity-frames frames of each of this rank's sequences
+    (one core each, after the timed region), compared with the GPU's frames: a compact parity
+    record per sequence for multi-sequence and multi-rank lines."""
+    from concurrent.futures import ThreadPoolExecutor
+    from multimot_track_amd import shard
+    from oracle import compare, oracle as O
+    O.build()
+    n = min(args.rank_parity_frames, len(seq_frames[0]))
+    frames = [[seq_frame_numpy(seqs[k], i) for i in range(n)] for k in range(K)]
+
+    def one(k):  # the oracle's C calls release the GIL: one thread per sequence
+        tr = O.Tracker(W, H, (721.5377, 721.5377, 609.5593, 172.8540), 387.5744, 0, NF)
+        ofr = [tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]) for f in frames[k]]
+        rec = compare.parity_record(seq_frames[k][:n], ofr)
+        return {"rank": rank, "sequence": k, "seed": shard.sequence_seed(1003, rank * K + k),
+                "frames": rec["frames"], "first_divergent_frame": rec["first_divergent_frame"],
+                "max_pose_diff": rec["max_pose_diff"],
+                "int_mismatch_frames": rec["int_mismatch_frames"],
+                "lm_stop_flips": rec["lm_stop_flips"],
+                "map_tracked": sum(int(d["map_state"] == 1) for d in seq_frames[k][:n])}
+    with ThreadPoolExecutor(max_workers=K) as ex:
+        return list(ex.map(one, range(K)))
+
+
 # ------------------------------------------------------------------ dry rehearsal
 def run_dry(args, rank, world):
     """The rank logic of the real run on CPU (gloo): per-rank seed, barrier-bracketed timed
@@ -357,10 +385,10 @@ def main(argv=None):
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(max_workers=K)
 
-    def step(i):
+    def step(i):  # the raw results of every sequence of this rank
         if pool is None:
-            return step_k(0, i)
-        return [f.result() for f in [pool.submit(step_k, k, i) for k in range(K)]][0]
+            return [step_k(0, i)]
+        return [f.result() for f in [pool.submit(step_k, k, i) for k in range(K)]]
 
     warm = [step(i) for i in range(args.warmup)]
     torch.cuda.synchronize(dev)
@@ -369,12 +397,12 @@ def main(argv=None):
     shard.barrier(world, dev)
     t0 = time.perf_counter()
     results = [step(args.warmup + i) for i in range(args.steps)]
-    flushed = []
+    flushed = [[] for _ in range(K)]
     if not args.immediate:  # the timed frames' last object motions, inside the timed region
         if pool is None:
-            flushed = ctx.flush_objects()
+            flushed = [ctx.flush_objects()]
         else:
-            flushed = [f.result() for f in [pool.submit(c.flush_objects) for c in ctxs]][0]
+            flushed = [f.result() for f in [pool.submit(c.flush_objects) for c in ctxs]]
     torch.cuda.synchronize(dev)
     shard.barrier(world, dev)
     elapsed = time.perf_counter() - t0
@@ -382,11 +410,16 @@ def main(argv=None):
     elapsed = shard.max_over_ranks(elapsed, world, dev)
     frames_all = shard.sum_over_ranks(args.steps * C * K, world, dev)
 
-    # per-frame outputs of the timed region (sanity: every frame tracked, objects found)
-    all_frames = assemble(warm + results, C, flushed)
+    # per-frame outputs of every sequence (sanity: every timed frame tracked by the map, objects
+    # found); a line whose timed frames are not all tracked is marked invalid
+    seq_frames = [assemble([r[k] for r in warm + results], C, flushed[k]) for k in range(K)]
+    all_frames = seq_frames[0]
     timed_frames = all_frames[args.warmup * C:]
     n_obj_last = len(timed_frames[-1]["objects"])
-    tracked = sum(int(d["initialized"]) for d in timed_frames)
+    tracked_rank = sum(int(d["initialized"]) for f in seq_frames for d in f[args.warmup * C:])
+    tracked = int(shard.sum_over_ranks(tracked_rank, world, dev))
+    lost_first = [next((args.warmup * C + i for i, d in enumerate(f[args.warmup * C:])
+                        if not d["initialized"]), None) for f in seq_frames]
     gt = seq["Tcw"][-1]
     ego_err = float(np.abs(timed_frames[-1]["Tcw"] - gt).max())
     mc = ctx.map_counters()
@@ -403,6 +436,15 @@ def main(argv=None):
     # context's streams share the process's hardware queues with every other context's)
     for c in ctxs:
         c.close()
+    # every rank's sequences checked against the oracle over their first frames (several sequences
+    # or ranks: the N = 1 line's CPU leg below checks the one sequence over more frames)
+    rank_par = None
+    if (world > 1 or K > 1) and args.rank_parity_frames > 0:
+        rank_par = rank_parity(args, seqs, seq_frames, rank, K, W, H, NF)
+        if world > 1:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, rank_par)
+            rank_par = [r for g in gathered for r in g]
 
     if rank == 0:
         value = frames_all / elapsed
@@ -481,9 +523,12 @@ def main(argv=None):
                                                                                          tt2)
             if args.cpu_seqs > 0:
                 cpu["multi"] = cpu_multi_leg(args, lambda sd, n: render(sd, n), W, H, NF, fps1)
+        frames_timed = int(frames_all)
         out = {
             "metric": METRIC,
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "frames_timed": frames_timed, "frames_tracked": tracked,
+            "valid": tracked == frames_timed,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -507,7 +552,13 @@ def main(argv=None):
                          "orb_share_of_step": round(prof["orb_ms"] / (elapsed * 1e3), 4)},
             "cpu_baseline": cpu,
             "parity": parity,
+            "rank_parity": rank_par,
         }
+        if tracked != frames_timed:
+            out["invalid_reason"] = (
+                "map tracking lost on %d of the %d timed frames (first lost frame per sequence of "
+                "rank 0: %s): the timed region did not run the tracked path on every frame"
+                % (frames_timed - tracked, frames_timed, lost_first))
         print(json.dumps(out), flush=True)
     for c in ctxs:
         c.close()

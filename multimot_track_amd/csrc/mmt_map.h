@@ -248,6 +248,11 @@ class MapEngine {
   std::vector<std::pair<float, int>> far_;  // UpdateLastFrame's far keys (scratch)
   float Tlr_[16];
   bool hasTlr_ = false;
+  // the keyframe this frame created and its pose before its LocalMapping ran: the reference's
+  // mapping thread adjusts the keyframe after Track() has stored mlRelativeFramePoses against it,
+  // so frame_done reads this pose (the LocalMapping itself overlaps the flow solve here)
+  int snapKF_ = -1;
+  float snapTwc_[16];
   int matchesInliers_ = 0;
   bool mbVO_ = false;
   bool pending_ok_ = false;  // track() succeeded, track_finish() pending

@@ -199,6 +199,7 @@ void MapEngine::reset() {
   recent_.clear();
   dirty_.clear();
   hasTlr_ = false;
+  snapKF_ = -1;
   n_good_ = 0;
 }
 
@@ -666,8 +667,12 @@ void MapEngine::initialize(MapFrameH& C, const float* Tcw) {
 }
 
 void MapEngine::frame_done(const MapFrameH& C, const float* Tcw) {
+  const int snap = snapKF_;
+  snapKF_ = -1;
   if (C.refKF < 0) return;
-  mat4_mul(Tcw, kfs_[C.refKF].Twc, Tlr_);  // Tcr = mTcw * mpReferenceKF->GetPoseInverse()
+  // Tcr = mTcw * mpReferenceKF->GetPoseInverse(), with the keyframe's pose as Track() leaves it
+  // (before the mapping thread's local BA of a keyframe this frame inserted)
+  mat4_mul(Tcw, C.refKF == snap ? snapTwc_ : kfs_[C.refKF].Twc, Tlr_);
   hasTlr_ = true;
 }
 
@@ -997,6 +1002,8 @@ void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracki
       if (v[j].first > cam_.thDepth && nPoints > 200) break;
     }
   }
+  snapKF_ = kf;
+  memcpy(snapTwc_, kfs_[kf].Twc, sizeof(snapTwc_));
   const double tp = prof_on_ ? now_us() : 0;
   process_new_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKF), processed at once
   map_point_culling(kf);

@@ -34,6 +34,7 @@ void MapTracker::reset() {
   kfNextId_ = 0;
   lastKFFrameId_ = 0;
   lastKF_ = -1;
+  pendingKF_ = -1;
   refKF_ = -1;
   localKFs_.clear();
   localPts_.clear();
@@ -323,9 +324,7 @@ void MapTracker::initialize(const std::vector<Key>& keys, const std::vector<uint
       C.mps[i] = h;
     }
   }
-  process_new_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKFini), processed at once
-  map_point_culling(kf);
-  local_mapping(kf);
+  insert_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKFini)
   lastKFFrameId_ = C.id;
   lastKF_ = kf;
   localKFs_.assign(1, kf);
@@ -337,10 +336,24 @@ void MapTracker::initialize(const std::vector<Key>& keys, const std::vector<uint
   state_ = 1;
 }
 
+// LocalMapping::InsertKeyFrame: the mapping thread's iteration for this keyframe runs in
+// frame_done, after the frame's Track() (pinned, oracle_map.h)
+void MapTracker::insert_keyframe(int kf) { pendingKF_ = kf; }
+
 void MapTracker::frame_done(const MapFrame& C, const float* Tcw) {
-  if (C.refKF < 0) return;
-  m4_mul(Tcw, kfs[C.refKF].Twc, Tlr_);  // Tcr = mTcw * mpReferenceKF->GetPoseInverse()
-  hasTlr_ = true;
+  if (C.refKF >= 0) {
+    m4_mul(Tcw, kfs[C.refKF].Twc, Tlr_);  // Tcr = mTcw * mpReferenceKF->GetPoseInverse()
+    hasTlr_ = true;
+  }
+  // the mapping thread's iteration for the keyframe this frame inserted (pinned: it runs to
+  // completion after the frame's Track(), before the next frame is tracked)
+  if (pendingKF_ >= 0) {
+    const int kf = pendingKF_;
+    pendingKF_ = -1;
+    process_new_keyframe(kf);
+    map_point_culling(kf);
+    local_mapping(kf);
+  }
 }
 
 void MapTracker::update_last_frame(const std::vector<Key>& lkeys,
@@ -707,9 +720,7 @@ void MapTracker::create_new_keyframe(const std::vector<Key>& keys,
       if (v[j].first > cam.thDepth && nPoints > 200) break;
     }
   }
-  process_new_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKF), processed at once
-  map_point_culling(kf);
-  local_mapping(kf);
+  insert_keyframe(kf);  // mpLocalMapper->InsertKeyFrame(pKF)
   lastKFFrameId_ = C.id;
   lastKF_ = kf;
 }

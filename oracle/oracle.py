@@ -256,6 +256,24 @@ class Tracker:
                 "ba_pts", "ba_max_opt_kfs")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def map_dump(self):
+        """The map as flat arrays (oracle_tracker_map_dump): keyframes (id, frame, bad, parent)
+        and poses, points (pos, min/max distance; bad, nObs, refKF, firstKFid, replaced),
+        observations in CSR (keyframe, key index, octave; key x, y, depth, uR)."""
+        L = lib()
+        sz = np.zeros(3, np.int32)
+        h = ctypes.c_void_p(self._h)
+        L.oracle_tracker_map_dump(h, _p(sz), None, None, None, None, None, None, None)
+        nk, npt, no = (int(v) for v in sz)
+        D = dict(kf_i=np.zeros((nk, 4), np.int64), kf_T=np.zeros((nk, 4, 4), np.float32),
+                 pt_f=np.zeros((npt, 5), np.float32), pt_i=np.zeros((npt, 5), np.int32),
+                 obs_start=np.zeros(npt + 1, np.int32), obs_i=np.zeros((no, 3), np.int32),
+                 obs_f=np.zeros((no, 4), np.float32))
+        L.oracle_tracker_map_dump(h, _p(sz), _p(D["kf_i"]), _p(D["kf_T"]), _p(D["pt_f"]),
+                                  _p(D["pt_i"]), _p(D["obs_start"]), _p(D["obs_i"]),
+                                  _p(D["obs_f"]))
+        return D
+
     def capture_ba(self, which):
         """Record the problem of this tracker's which-th LocalBundleAdjustment (0-based)."""
         lib().oracle_tracker_capture_ba(ctypes.c_void_p(self._h), which)

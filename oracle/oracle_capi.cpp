@@ -336,6 +336,47 @@ int oracle_tracker_captured_d3(void* tp, int* n, float* obs, float* flow, float*
   return 1;
 }
 
+// The tracker's map as flat arrays (diagnostics and invariant tests).  sizes[3] = keyframes,
+// map points, observations.  With non-null arrays: kf_i per keyframe (id, frame id, bad, parent),
+// kf_T 16 floats each; pt_f per point (pos 3, min/max distance 2); pt_i per point (bad, nObs,
+// refKF, firstKFid, replaced); obs_start n_pt + 1 (CSR); per observation obs_i (keyframe, key
+// index, key octave), obs_f (key x, y, depth, uR).
+int oracle_tracker_map_dump(void* tp, int* sizes, long long* kf_i, float* kf_T, float* pt_f,
+                            int* pt_i, int* obs_start, int* obs_i, float* obs_f) {
+  const MapTracker& M = ((OTracker*)tp)->map;
+  size_t nobs = 0;
+  for (const OMapPoint& p : M.pts) nobs += p.obs.size();
+  sizes[0] = (int)M.kfs.size();
+  sizes[1] = (int)M.pts.size();
+  sizes[2] = (int)nobs;
+  if (!kf_i) return 0;
+  for (size_t k = 0; k < M.kfs.size(); k++) {
+    const OKeyFrame& K = M.kfs[k];
+    kf_i[4 * k] = K.id; kf_i[4 * k + 1] = K.frameId; kf_i[4 * k + 2] = K.bad;
+    kf_i[4 * k + 3] = K.parent;
+    memcpy(kf_T + 16 * k, K.Tcw, 64);
+  }
+  size_t o = 0;
+  for (size_t j = 0; j < M.pts.size(); j++) {
+    const OMapPoint& p = M.pts[j];
+    memcpy(pt_f + 5 * j, p.pos, 12);
+    pt_f[5 * j + 3] = p.minDist; pt_f[5 * j + 4] = p.maxDist;
+    pt_i[5 * j] = p.bad; pt_i[5 * j + 1] = p.nObs; pt_i[5 * j + 2] = p.refKF;
+    pt_i[5 * j + 3] = p.firstKFid; pt_i[5 * j + 4] = p.replaced;
+    obs_start[j] = (int)o;
+    for (const auto& kv : p.obs) {
+      const OKeyFrame& K = M.kfs[kv.first];
+      obs_i[3 * o] = kv.first; obs_i[3 * o + 1] = kv.second;
+      obs_i[3 * o + 2] = K.keys[kv.second].octave;
+      obs_f[4 * o] = K.keys[kv.second].x; obs_f[4 * o + 1] = K.keys[kv.second].y;
+      obs_f[4 * o + 2] = K.depth[kv.second]; obs_f[4 * o + 3] = K.uR[kv.second];
+      o++;
+    }
+  }
+  obs_start[M.pts.size()] = (int)o;
+  return 0;
+}
+
 // sizes[3] = n_kf, n_pt, n_edge (0s until captured); with non-null arrays, copies the problem out
 int oracle_tracker_captured_ba(void* tp, int* sizes, float* T, uint8_t* fixed, float* X, int* pt,
                                int* kf, float* obs, float* s) {

@@ -23,8 +23,13 @@
 //  * LocalMapping runs synchronously and is always idle when Tracking asks (AcceptKeyFrames):
 //    ProcessNewKeyFrame (without the BoW conversion), MapPointCulling, SearchInNeighbors,
 //    LocalBundleAdjustment (no abort: mbAbortBA stays false) and KeyFrameCulling run to completion
-//    after every new keyframe; CreateNewMapPoints needs SearchForTriangulation, i.e. the BoW
-//    vocabulary (missing), and is skipped;
+//    for every new keyframe once the frame that inserted it has finished Track() (its flow solve
+//    and the mlRelativeFramePoses entry against the keyframe's pose as Track left it,
+//    Tracking.cc:2481-2489), before the next frame: the mapping thread only receives the keyframe
+//    in CreateNewKeyFrame (InsertKeyFrame, Tracking.cc:3408), so the local BA's correction of the
+//    keyframe reaches the last frame through Tlr in UpdateLastFrame, as in the reference;
+//    CreateNewMapPoints needs SearchForTriangulation, i.e. the BoW vocabulary (missing), and is
+//    skipped;
 //  * TrackReferenceKeyFrame's SearchByBoW (and Relocalization, whose candidates come from the BoW
 //    database) needs the missing vocabulary: both are replaced by SearchByProjection against the
 //    last frame at the last frame's pose (th 15, orientation check), then PoseOptimization and the
@@ -221,6 +226,7 @@ class MapTracker {
   bool need_new_keyframe(const MapFrame& C);
   void create_new_keyframe(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
                            MapFrame& C, const float* Tcw);
+  void insert_keyframe(int kf);  // LocalMapping::InsertKeyFrame: processed in frame_done
   void process_new_keyframe(int kf);
   void map_point_culling(int kf);
   // the rest of LocalMapping::Run's iteration (LocalMapping.cc:68-87)
@@ -256,6 +262,7 @@ class MapTracker {
   int kfNextId_ = 0;
   long lastKFFrameId_ = 0;  // mnLastKeyFrameId
   int lastKF_ = -1;
+  int pendingKF_ = -1;      // inserted keyframe whose LocalMapping runs in frame_done
   int refKF_ = -1;          // mpReferenceKF
   std::vector<int> localKFs_, localPts_;
   std::vector<int> temporal_;  // mlpTemporalPoints

@@ -518,6 +518,8 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
   memcpy(out.Tcw, C.Tcw, sizeof(out.Tcw));
   out.initialized = map.state() == 1;
   map.frame_done(C.m, C.Tcw);  // mlRelativeFramePoses (Tracking.cc:2481-2489)
+  out.map.n_keyframes = map.n_keyframes();  // after the inserted keyframe's LocalMapping
+  out.map.n_mappoints = map.n_mappoints();
 
   // ---- B9: last-frame hand-off (Tracking.cc:2463-2477)
   L = C;
