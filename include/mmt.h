@@ -438,6 +438,27 @@ typedef struct mmt_map_counters {
 } mmt_map_counters;
 int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out);
 
+/* The tracker's map as flat arrays (no reference counterpart: the map invariant tests and the
+ * map-graph parity against the CPU oracle read it).  Keyframes and map points are numbered in
+ * creation order (the reference's mnId order).  sizes[7] (out): keyframes, map points,
+ * observations, connections, ordered covisibles, children, keyframe map-point slots.  With
+ * out == NULL only the sizes are written; otherwise every array must hold its size. */
+typedef struct mmt_map_dump_arrays {
+  int64_t* kf_i;          /* n_kf x 4: mnId, mnFrameId, isBad, parent (-1: none)             */
+  float* kf_T;            /* n_kf x 16: Tcw                                                   */
+  int32_t* kf_mps_start;  /* n_kf + 1: CSR offsets into kf_mps                                */
+  int32_t* kf_mps;        /* slots: mvpMapPoints (map point number or -1)                     */
+  float* pt_f;            /* n_pt x 5: world position, mfMinDistance, mfMaxDistance             */
+  int32_t* pt_i;          /* n_pt x 5: isBad, nObs, mpRefKF, mnFirstKFid, mpReplaced (-1)     */
+  int32_t* obs_start;     /* n_pt + 1: CSR offsets into obs_i / obs_f (mObservations)          */
+  int32_t* obs_i;         /* n_obs x 3: keyframe, key index, key octave                        */
+  float* obs_f;           /* n_obs x 4: key x, y, mvDepth, mvuRight                            */
+  int32_t* conn;          /* n_conn x 3: keyframe, other, weight (mConnectedKeyFrameWeights)   */
+  int32_t* ord;           /* n_ord x 3: keyframe, other, weight (mvpOrderedConnectedKeyFrames) */
+  int32_t* child;         /* n_child x 2: keyframe, child (mspChildrens)                        */
+} mmt_map_dump_arrays;
+int mmt_map_dump(mmt_ctx* ctx, int32_t* sizes, const mmt_map_dump_arrays* out);
+
 /* Visualisation hook (no reference counterpart; Tracking.cc:684-783 draws these into feat.png):
  * the static samples (mvSiftKeys, B2) and the object samples (mvObjKeys with vSemObjLabel, B1)
  * of the last frame the context tracked, xy as n x 2 floats.  Counts clipped to the caps. */

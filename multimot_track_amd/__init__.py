@@ -115,6 +115,29 @@ class MmtMapCounters(ctypes.Structure):
         [("d2_split_fallbacks", ctypes.c_int64)]
 
 
+MAP_DUMP_FIELDS = (("kf_i", np.int64, 4), ("kf_T", np.float32, 16), ("kf_mps_start", np.int32, 1),
+                   ("kf_mps", np.int32, 1), ("pt_f", np.float32, 5), ("pt_i", np.int32, 5),
+                   ("obs_start", np.int32, 1), ("obs_i", np.int32, 3), ("obs_f", np.float32, 4),
+                   ("conn", np.int32, 3), ("ord", np.int32, 3), ("child", np.int32, 2))
+
+
+class MmtMapDumpArrays(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k, _, _ in MAP_DUMP_FIELDS]
+
+
+def map_dump_arrays(sizes):
+    """numpy arrays for mmt_map_dump's sizes[7] (keyframes, points, observations, connections,
+    ordered covisibles, children, keyframe slots) and the struct pointing at them."""
+    nk, npt, nob, nc, no, nch, nsl = (int(v) for v in sizes)
+    rows = dict(kf_i=nk, kf_T=nk, kf_mps_start=nk + 1, kf_mps=nsl, pt_f=npt, pt_i=npt,
+                obs_start=npt + 1, obs_i=nob, obs_f=nob, conn=nc, ord=no, child=nch)
+    D = {k: np.zeros((max(rows[k], 1), w) if w > 1 else max(rows[k], 1), dt)
+         for k, dt, w in MAP_DUMP_FIELDS}
+    st = MmtMapDumpArrays(**{k: D[k].ctypes.data_as(ctypes.c_void_p).value
+                             for k, _, _ in MAP_DUMP_FIELDS})
+    return {k: D[k][:rows[k]] for k in D}, D, st
+
+
 class MmtProfile(ctypes.Structure):
     _fields_ = [("orb_ms", ctypes.c_double), ("orb_launches", ctypes.c_int64),
                 ("orb_frames", ctypes.c_int64)]
@@ -230,6 +253,7 @@ def lib():
         L.mmt_local_bundle_adjustment.argtypes = [vp, ctypes.POINTER(MmtBAProblem), vp, vp, vp,
                                                   vp]
         L.mmt_map_counters_read.argtypes = [vp, ctypes.POINTER(MmtMapCounters)]
+        L.mmt_map_dump.argtypes = [vp, vp, ctypes.POINTER(MmtMapDumpArrays)]
         L.mmt_set_deferred_objects.argtypes = [vp, i32]
         L.mmt_flush_objects.argtypes = [vp, vp, vp, i32, i32, vp]
         _LIB = L
@@ -571,6 +595,19 @@ class Context:
             for i in range(n.value):
                 d = _frame_dict(res[i], objs[i * MAX_OBJECTS:(i + 1) * MAX_OBJECTS])
                 out.append((d["objects_frame"], d["objects"]))
+
+    def map_dump(self):
+        """The tracker's map as flat arrays (mmt_map_dump): keyframes (id, frame, bad, parent)
+        and poses, each keyframe's map-point slots (CSR), points (position, min/max distance;
+        bad, nObs, refKF, firstKFid, replaced), observations (CSR: keyframe, key index, octave;
+        key x, y, depth, uR), connections, ordered covisibles (keyframe, other, weight) and
+        spanning-tree children (keyframe, child)."""
+        sz = np.zeros(7, np.int32)
+        self._check(lib().mmt_map_dump(self._h, _p(sz), None))
+        out, keep, st = map_dump_arrays(sz)
+        self._check(lib().mmt_map_dump(self._h, _p(sz), ctypes.byref(st)))
+        del keep
+        return out
 
     def map_counters(self):
         """LocalMapping counters of the context's tracker (mmt_map_counters_read)."""

@@ -852,6 +852,17 @@ int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out) {
   });
 }
 
+int mmt_map_dump(mmt_ctx* ctx, int32_t* sizes, const mmt_map_dump_arrays* out) {
+  if (!ctx || !sizes) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    if (!ctx->tracker_ready) {
+      memset(sizes, 0, 7 * sizeof(int32_t));
+      return;
+    }
+    ctx->tracker.map().dump(sizes, out);
+  });
+}
+
 int mmt_search_by_bow(mmt_ctx* ctx, const mmt_bow_keyframe* kf, int n_cur, const mmt_kp* cur_kps,
                       const uint8_t* cur_desc, const mmt_feature_vector* cur_fv, float nn_ratio,
                       int check_orientation, int32_t* match_out, int* nmatches) {

@@ -159,6 +159,8 @@ class MapEngine {
   // them into the keyframe store, where Fuse reads them
   void set_frame_grid(const GridFrame& G) { G_ = G; }
   const MappingStats& mapping_stats() const { return mstats_; }
+  // the map as flat arrays (mmt_map_dump, include/mmt.h): sizes[7]; arrays written when out != 0
+  void dump(int32_t* sizes, const mmt_map_dump_arrays* out) const;
 
  private:
   std::function<void()> overlap_;

@@ -636,6 +636,64 @@ void MapEngine::gpu_flush_pool(hipStream_t st) {
   dirty_.clear();
 }
 
+// ------------------------------------------------------------------ map dump (tests)
+void MapEngine::dump(int32_t* sizes, const mmt_map_dump_arrays* out) const {
+  long nobs = 0, nconn = 0, nord = 0, nchild = 0, nslots = 0;
+  for (const MPoint& p : pts_) nobs += (long)p.obs.size();
+  for (const KFrame& K : kfs_) {
+    nconn += (long)K.conn.size();
+    nord += (long)K.ordered.size();
+    nchild += (long)K.children.size();
+    nslots += (long)K.mps.size();
+  }
+  const long n[7] = {(long)kfs_.size(), (long)pts_.size(), nobs, nconn, nord, nchild, nslots};
+  for (int i = 0; i < 7; i++) sizes[i] = (int32_t)n[i];
+  if (!out) return;
+  long c = 0, o = 0, ch = 0, sl = 0;
+  for (size_t k = 0; k < kfs_.size(); k++) {
+    const KFrame& K = kfs_[k];
+    int64_t* ki = out->kf_i + 4 * k;
+    ki[0] = K.id; ki[1] = K.frameId; ki[2] = K.bad; ki[3] = K.parent;
+    memcpy(out->kf_T + 16 * k, K.Tcw, 64);
+    out->kf_mps_start[k] = (int32_t)sl;
+    for (int h : K.mps) out->kf_mps[sl++] = h;
+    for (const auto& kv : K.conn) {
+      int32_t* e = out->conn + 3 * c++;
+      e[0] = (int32_t)k; e[1] = kv.first; e[2] = kv.second;
+    }
+    for (int q : K.ordered) {
+      int32_t* e = out->ord + 3 * o++;
+      const auto it = K.conn.find(q);
+      e[0] = (int32_t)k; e[1] = q; e[2] = it == K.conn.end() ? -1 : it->second;
+    }
+    for (int q : K.children) {
+      int32_t* e = out->child + 2 * ch++;
+      e[0] = (int32_t)k; e[1] = q;
+    }
+  }
+  out->kf_mps_start[kfs_.size()] = (int32_t)sl;
+  long b = 0;
+  for (size_t j = 0; j < pts_.size(); j++) {
+    const MPoint& p = pts_[j];
+    float* f = out->pt_f + 5 * j;
+    memcpy(f, p.pos, 12);
+    f[3] = p.minDist; f[4] = p.maxDist;
+    int32_t* pi = out->pt_i + 5 * j;
+    pi[0] = p.bad; pi[1] = p.nObs; pi[2] = p.refKF; pi[3] = p.firstKFid; pi[4] = p.replaced;
+    out->obs_start[j] = (int32_t)b;
+    for (const auto& ob : p.obs) {
+      const KFrame& K = kfs_[ob.first];
+      int32_t* oi = out->obs_i + 3 * b;
+      float* of = out->obs_f + 4 * b;
+      oi[0] = ob.first; oi[1] = ob.second; oi[2] = K.keys[ob.second].octave;
+      of[0] = K.keys[ob.second].x; of[1] = K.keys[ob.second].y;
+      of[2] = K.depth[ob.second]; of[3] = K.uR[ob.second];
+      b++;
+    }
+  }
+  out->obs_start[pts_.size()] = (int32_t)b;
+}
+
 // ------------------------------------------------------------------ Tracking
 void MapEngine::initialize(MapFrameH& C, const float* Tcw) {
   const int kf = new_keyframe(C, Tcw);

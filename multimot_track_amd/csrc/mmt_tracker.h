@@ -87,6 +87,7 @@ class Tracker {
   const int* nkp() const { return d_nkp_; }
   int kcap() const { return kcap_; }
   const MappingStats& mapping_stats() const { return map_.mapping_stats(); }
+  const MapEngine& map() const { return map_; }
   long split_fallbacks() const { return split_fallbacks_; }
   // the last tracked frame's static samples (mvSiftKeys) and object samples (mvObjKeys,
   // vSemObjLabel), copied to the host (visualisation hook); counts clipped to the caps

@@ -231,6 +231,27 @@ def ransac_subsets(count, iters):
     return out.reshape(iters, 5)
 
 
+_MAP_DUMP_FIELDS = (("kf_i", np.int64, 4), ("kf_T", np.float32, 16),
+                    ("kf_mps_start", np.int32, 1), ("kf_mps", np.int32, 1),
+                    ("pt_f", np.float32, 5), ("pt_i", np.int32, 5), ("obs_start", np.int32, 1),
+                    ("obs_i", np.int32, 3), ("obs_f", np.float32, 4), ("conn", np.int32, 3),
+                    ("ord", np.int32, 3), ("child", np.int32, 2))
+
+
+class _MapDump(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k, _, _ in _MAP_DUMP_FIELDS]
+
+
+def _map_dump_arrays(sizes):
+    nk, npt, nob, nc, no, nch, nsl = (int(v) for v in sizes)
+    rows = dict(kf_i=nk, kf_T=nk, kf_mps_start=nk + 1, kf_mps=nsl, pt_f=npt, pt_i=npt,
+                obs_start=npt + 1, obs_i=nob, obs_f=nob, conn=nc, ord=no, child=nch)
+    D = {k: np.zeros((max(rows[k], 1), w) if w > 1 else max(rows[k], 1), dt)
+         for k, dt, w in _MAP_DUMP_FIELDS}
+    st = _MapDump(**{k: D[k].ctypes.data_as(ctypes.c_void_p).value for k, _, _ in _MAP_DUMP_FIELDS})
+    return {k: D[k][:rows[k]] for k in D}, D, st
+
+
 class Tracker:
     """CPU restatement of System::TrackRGBD (oracle/track_ref.cpp)."""
 
@@ -257,22 +278,16 @@ class Tracker:
         return {k: int(v) for k, v in zip(keys, out)}
 
     def map_dump(self):
-        """The map as flat arrays (oracle_tracker_map_dump): keyframes (id, frame, bad, parent)
-        and poses, points (pos, min/max distance; bad, nObs, refKF, firstKFid, replaced),
-        observations in CSR (keyframe, key index, octave; key x, y, depth, uR)."""
+        """The map as flat arrays, in the layout of the product's mmt_map_dump (include/mmt.h)."""
         L = lib()
-        sz = np.zeros(3, np.int32)
+        sz = np.zeros(7, np.int32)
         h = ctypes.c_void_p(self._h)
-        L.oracle_tracker_map_dump(h, _p(sz), None, None, None, None, None, None, None)
-        nk, npt, no = (int(v) for v in sz)
-        D = dict(kf_i=np.zeros((nk, 4), np.int64), kf_T=np.zeros((nk, 4, 4), np.float32),
-                 pt_f=np.zeros((npt, 5), np.float32), pt_i=np.zeros((npt, 5), np.int32),
-                 obs_start=np.zeros(npt + 1, np.int32), obs_i=np.zeros((no, 3), np.int32),
-                 obs_f=np.zeros((no, 4), np.float32))
-        L.oracle_tracker_map_dump(h, _p(sz), _p(D["kf_i"]), _p(D["kf_T"]), _p(D["pt_f"]),
-                                  _p(D["pt_i"]), _p(D["obs_start"]), _p(D["obs_i"]),
-                                  _p(D["obs_f"]))
-        return D
+        L.oracle_tracker_map_dump.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_tracker_map_dump(h, _p(sz), None)
+        out, keep, st = _map_dump_arrays(sz)
+        L.oracle_tracker_map_dump(h, _p(sz), ctypes.byref(st))
+        del keep
+        return out
 
     def capture_ba(self, which):
         """Record the problem of this tracker's which-th LocalBundleAdjustment (0-based)."""

@@ -336,44 +336,79 @@ int oracle_tracker_captured_d3(void* tp, int* n, float* obs, float* flow, float*
   return 1;
 }
 
-// The tracker's map as flat arrays (diagnostics and invariant tests).  sizes[3] = keyframes,
-// map points, observations.  With non-null arrays: kf_i per keyframe (id, frame id, bad, parent),
-// kf_T 16 floats each; pt_f per point (pos 3, min/max distance 2); pt_i per point (bad, nObs,
-// refKF, firstKFid, replaced); obs_start n_pt + 1 (CSR); per observation obs_i (keyframe, key
-// index, key octave), obs_f (key x, y, depth, uR).
-int oracle_tracker_map_dump(void* tp, int* sizes, long long* kf_i, float* kf_T, float* pt_f,
-                            int* pt_i, int* obs_start, int* obs_i, float* obs_f) {
+// The tracker's map as flat arrays, laid out as the product's mmt_map_dump (include/mmt.h):
+// sizes[7] = keyframes, map points, observations, connections, ordered covisibles, children,
+// keyframe map-point slots; the arrays (a struct of pointers, field for field
+// mmt_map_dump_arrays) are written when out is non-null.
+struct OracleMapDump {
+  long long* kf_i;
+  float* kf_T;
+  int* kf_mps_start;
+  int* kf_mps;
+  float* pt_f;
+  int* pt_i;
+  int* obs_start;
+  int* obs_i;
+  float* obs_f;
+  int* conn;
+  int* ord;
+  int* child;
+};
+
+int oracle_tracker_map_dump(void* tp, int* sizes, const OracleMapDump* out) {
   const MapTracker& M = ((OTracker*)tp)->map;
-  size_t nobs = 0;
-  for (const OMapPoint& p : M.pts) nobs += p.obs.size();
-  sizes[0] = (int)M.kfs.size();
-  sizes[1] = (int)M.pts.size();
-  sizes[2] = (int)nobs;
-  if (!kf_i) return 0;
+  long nobs = 0, nconn = 0, nord = 0, nchild = 0, nslots = 0;
+  for (const OMapPoint& p : M.pts) nobs += (long)p.obs.size();
+  for (const OKeyFrame& K : M.kfs) {
+    nconn += (long)K.conn.size();
+    nord += (long)K.ordered.size();
+    nchild += (long)K.children.size();
+    nslots += (long)K.mps.size();
+  }
+  const long n[7] = {(long)M.kfs.size(), (long)M.pts.size(), nobs, nconn, nord, nchild, nslots};
+  for (int i = 0; i < 7; i++) sizes[i] = (int)n[i];
+  if (!out) return 0;
+  long c = 0, o = 0, ch = 0, sl = 0;
   for (size_t k = 0; k < M.kfs.size(); k++) {
     const OKeyFrame& K = M.kfs[k];
-    kf_i[4 * k] = K.id; kf_i[4 * k + 1] = K.frameId; kf_i[4 * k + 2] = K.bad;
-    kf_i[4 * k + 3] = K.parent;
-    memcpy(kf_T + 16 * k, K.Tcw, 64);
-  }
-  size_t o = 0;
-  for (size_t j = 0; j < M.pts.size(); j++) {
-    const OMapPoint& p = M.pts[j];
-    memcpy(pt_f + 5 * j, p.pos, 12);
-    pt_f[5 * j + 3] = p.minDist; pt_f[5 * j + 4] = p.maxDist;
-    pt_i[5 * j] = p.bad; pt_i[5 * j + 1] = p.nObs; pt_i[5 * j + 2] = p.refKF;
-    pt_i[5 * j + 3] = p.firstKFid; pt_i[5 * j + 4] = p.replaced;
-    obs_start[j] = (int)o;
-    for (const auto& kv : p.obs) {
-      const OKeyFrame& K = M.kfs[kv.first];
-      obs_i[3 * o] = kv.first; obs_i[3 * o + 1] = kv.second;
-      obs_i[3 * o + 2] = K.keys[kv.second].octave;
-      obs_f[4 * o] = K.keys[kv.second].x; obs_f[4 * o + 1] = K.keys[kv.second].y;
-      obs_f[4 * o + 2] = K.depth[kv.second]; obs_f[4 * o + 3] = K.uR[kv.second];
-      o++;
+    long long* ki = out->kf_i + 4 * k;
+    ki[0] = K.id; ki[1] = K.frameId; ki[2] = K.bad; ki[3] = K.parent;
+    memcpy(out->kf_T + 16 * k, K.Tcw, 64);
+    out->kf_mps_start[k] = (int)sl;
+    for (int h : K.mps) out->kf_mps[sl++] = h;
+    for (const auto& kv : K.conn) {
+      int* e = out->conn + 3 * c++;
+      e[0] = (int)k; e[1] = kv.first; e[2] = kv.second;
+    }
+    for (size_t q = 0; q < K.ordered.size(); q++) {
+      int* e = out->ord + 3 * o++;
+      e[0] = (int)k; e[1] = K.ordered[q]; e[2] = K.orderedW[q];
+    }
+    for (int q : K.children) {
+      int* e = out->child + 2 * ch++;
+      e[0] = (int)k; e[1] = q;
     }
   }
-  obs_start[M.pts.size()] = (int)o;
+  out->kf_mps_start[M.kfs.size()] = (int)sl;
+  long b = 0;
+  for (size_t j = 0; j < M.pts.size(); j++) {
+    const OMapPoint& p = M.pts[j];
+    memcpy(out->pt_f + 5 * j, p.pos, 12);
+    out->pt_f[5 * j + 3] = p.minDist; out->pt_f[5 * j + 4] = p.maxDist;
+    int* pi = out->pt_i + 5 * j;
+    pi[0] = p.bad; pi[1] = p.nObs; pi[2] = p.refKF; pi[3] = p.firstKFid; pi[4] = p.replaced;
+    out->obs_start[j] = (int)b;
+    for (const auto& kv : p.obs) {
+      const OKeyFrame& K = M.kfs[kv.first];
+      int* oi = out->obs_i + 3 * b;
+      float* of = out->obs_f + 4 * b;
+      oi[0] = kv.first; oi[1] = kv.second; oi[2] = K.keys[kv.second].octave;
+      of[0] = K.keys[kv.second].x; of[1] = K.keys[kv.second].y;
+      of[2] = K.depth[kv.second]; of[3] = K.uR[kv.second];
+      b++;
+    }
+  }
+  out->obs_start[M.pts.size()] = (int)b;
   return 0;
 }
 

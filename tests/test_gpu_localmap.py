@@ -45,6 +45,8 @@ def _compare_ba(ctx, oracle_mod, P):
     (12, dict(n_kf=4, n_fixed=1, n_pt=300, mono_frac=0.6, outlier_frac=0.1)),
     (13, dict(n_kf=18, n_fixed=4, n_pt=4000, obs_per_pt=(2, 8))),   # 14 optimised: 84 rows (LDS)
     (14, dict(n_kf=24, n_fixed=2, n_pt=3000, obs_per_pt=(2, 6))),   # 21 optimised: 126 rows (HBM)
+    (17, dict(n_kf=30, n_fixed=3, n_pt=3000, obs_per_pt=(2, 6))),   # 26 optimised: 156 rows, the
+                                                                    # substitution path past 128
     (15, dict(n_kf=3, n_fixed=3, n_pt=200)),                        # no optimised keyframe
     (16, dict(n_kf=5, n_fixed=0, kf0_local=False, pose_noise=0.05, pix_noise=1.5)),
 ])
@@ -167,3 +169,35 @@ def test_tracker_local_mapping_matches_oracle(oracle_mod, c3_seq):
     for k in ("n_ba", "n_fused", "n_culled", "n_ba_erased", "ba_trials", "ba_edges", "ba_pts"):
         assert gc[k] == oc[k], (k, gc[k], oc[k])
     assert oc["n_ba"] > 5 and oc["n_fused"] > 50
+
+
+def test_tracker_map_graph_matches_oracle(oracle_mod, c3_seq):
+    """The whole map graph, not only the per-frame outputs: after every keyframe's LocalMapping
+    (one frame per mmt_track_rgbd call) the product's map (mmt_map_dump) equals the oracle's --
+    keyframes, their map-point slots, every observation, covisibility weights and order, the
+    spanning tree -- with keyframe poses and point positions within the bar, and both pass the
+    independent structural checks of tests/map_invariants.py."""
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    from map_invariants import check_map, same_map
+    n = 90
+    ctx = M.Context(M.kitti03_config(1242, 375, 2000, max_batch=4))
+    tr = oracle_mod.Tracker(1242, 375, K_KITTI, BF, 0, 2000)
+    checks = 0
+    try:
+        for i in range(n):
+            f = scene.to_numpy_frames({k: c3_seq[k][i:i + 1] for k in ("bgr", "disp", "flow", "mask")})[0]
+            g = ctx.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            o = tr.track(f["bgr"], f["disp"], f["flow"], f["sem"])
+            assert g["new_keyframe"] == o["new_keyframe"], i
+            if o["new_keyframe"] or i == 0:
+                Dg, Do = ctx.map_dump(), tr.map_dump()
+                diff, fmax = same_map(Dg, Do)
+                assert diff == [] and fmax < TOL, (i, diff, fmax)
+                newest = len(Do["kf_i"]) - 1
+                assert check_map(Dg, newest=newest) == [], i
+                assert check_map(Do, newest=newest) == [], i
+                checks += 1
+    finally:
+        ctx.close()
+    assert checks > 12

@@ -1,0 +1,66 @@
+"""The oracle's map (oracle/map_ref.cpp, mapping_ref.cpp) against the structural invariants of
+tests/map_invariants.py after every LocalMapping (CPU, no GPU): a check written independently of
+the oracle's restatement of MapPoint / KeyFrame / LocalMapping bookkeeping."""
+import numpy as np
+import pytest
+
+from map_invariants import check_map
+
+
+def _half_res_camera():
+    # KITTI-03's camera at half resolution: the map logic is resolution-independent and the
+    # CPU renderer is four times faster
+    from multimot_track_amd import scene
+    K = {k: v * 0.5 for k, v in scene.KITTI03.items()}
+    return K, 621, 188
+
+
+@pytest.mark.parametrize("seed,objects,nframes", [(1003, 3, 70)])
+def test_oracle_map_invariants_after_every_local_mapping(oracle_mod, seed, objects, nframes):
+    from multimot_track_amd import scene
+    K, W, H = _half_res_camera()
+    R = scene.SequenceRenderer(scene.StreetScene(objects, seed), W, H, K=K)
+    tr = oracle_mod.Tracker(W, H, (K["fx"], K["fy"], K["cx"], K["cy"]), K["bf"], 0, 1000)
+    n_kf_checks = 0
+    for i in range(nframes):
+        b, d, f, m = R.frame(i)
+        r = tr.track(b.numpy(), d.numpy().view(np.uint16), f.numpy(), m.numpy())
+        assert r["map_state"] == 1, i
+        if r["new_keyframe"] or i == 0:
+            D = tr.map_dump()
+            newest = len(D["kf_i"]) - 1
+            v = check_map(D, newest=newest)
+            assert v == [], (i, v[:10], len(v))
+            n_kf_checks += 1
+    st = tr.map_stats()
+    assert n_kf_checks > 10 and st["n_ba"] > 8 and st["n_fused"] > 0 and st["n_ba_erased"] > 0
+
+
+def test_map_invariants_catch_corruption(oracle_mod):
+    """The checker is not vacuous: each kind of corruption of a valid map dump is reported."""
+    from multimot_track_amd import scene
+    K, W, H = _half_res_camera()
+    R = scene.SequenceRenderer(scene.StreetScene(3, 1003), W, H, K=K)
+    tr = oracle_mod.Tracker(W, H, (K["fx"], K["fy"], K["cx"], K["cy"]), K["bf"], 0, 1000)
+    for i in range(12):
+        b, d, f, m = R.frame(i)
+        tr.track(b.numpy(), d.numpy().view(np.uint16), f.numpy(), m.numpy())
+    D = tr.map_dump()
+    assert check_map(D) == []
+    good = np.nonzero((D["pt_i"][:, 0] == 0) & (np.diff(D["obs_start"]) >= 2))[0]
+    j = int(good[0])
+
+    def corrupt(fn):
+        E = {k: v.copy() for k, v in D.items()}
+        fn(E)
+        return check_map(E)
+    assert any("nObs" in v for v in corrupt(lambda E: E["pt_i"].__setitem__((j, 1), 99)))
+    assert any("refKF" in v for v in corrupt(lambda E: E["pt_i"].__setitem__((j, 2), 10 ** 6)))
+    o = D["obs_start"][j]
+    k, idx = D["obs_i"][o, :2]
+    assert any("slot holds" in v for v in
+               corrupt(lambda E: E["kf_mps"].__setitem__(E["kf_mps_start"][k] + idx, -1)))
+    kk = int(np.nonzero(D["kf_i"][:, 0] > 0)[0][-1])
+    assert any("parent" in v for v in corrupt(lambda E: E["kf_i"].__setitem__((kk, 3), kk)))
+    assert any("sorted" in v or "not in its weights" in v for v in
+               corrupt(lambda E: E["ord"].__setitem__((0, 2), E["ord"][0, 2] + 1000)))
