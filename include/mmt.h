@@ -487,7 +487,9 @@ int mmt_reset(mmt_ctx* ctx);
  * motions arrive exactly once, in order, up to 17 frames later.  mmt_flush_objects finishes the
  * pipeline and returns the remaining records (res[k].objects_frame, n_objects and objs[k *
  * objs_cap ..] only), at most res_cap per call: *n = records written, 0 when none remain.
- * Turning the mode off flushes (and drops) the records still owed; mmt_reset drops them.
+ * Turning the mode off flushes (and drops) the records still owed; mmt_reset drops them.  While
+ * a flush has records left for a later mmt_flush_objects call, every mmt_track_rgbd* call returns
+ * MMT_ESTATE (it would deliver newer frames' motions first).
  * MMT_EINVAL when the host object worker (MMT_OBJ_THREAD=1) is on. */
 int mmt_set_deferred_objects(mmt_ctx* ctx, int on);
 int mmt_flush_objects(mmt_ctx* ctx, mmt_frame_result* res, mmt_motion* objs, int objs_cap,

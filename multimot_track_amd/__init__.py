@@ -582,8 +582,11 @@ class Context:
 
     def flush_objects(self):
         """mmt_flush_objects until empty: [(objects_frame, objects)] in frame order."""
+        return self.flush_objects_part(cap=32, until_empty=True)
+
+    def flush_objects_part(self, cap=32, until_empty=False):
+        """One mmt_flush_objects call with res_cap = cap (or calls until none remain)."""
         out = []
-        cap = 32
         while True:
             res = (MmtFrameResult * cap)()
             objs = (MmtMotion * (cap * MAX_OBJECTS))()
@@ -595,6 +598,8 @@ class Context:
             for i in range(n.value):
                 d = _frame_dict(res[i], objs[i * MAX_OBJECTS:(i + 1) * MAX_OBJECTS])
                 out.append((d["objects_frame"], d["objects"]))
+            if not until_empty:
+                return out
 
     def map_dump(self):
         """The tracker's map as flat arrays (mmt_map_dump): keyframes (id, frame, bad, parent)

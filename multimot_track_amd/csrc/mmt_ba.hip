@@ -1381,19 +1381,18 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
     if (w.pt_act[j]) {
       double* xl = &w.x[n6 + 3 * (size_t)j];
       if (ok2) {
-        // the loads that depend on j alone first (D^-1), then per edge its H_pl block issued with
-        // its keyframe index, before the branch on it (the block exists for every edge)
+        // the loads that depend on j alone first (D^-1); an edge's H_pl block only for the edges
+        // of the level to an optimised keyframe (ba2_lin_point writes no block for the others)
         double Di[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) Di[q] = w.Dinv[9 * (size_t)j + q];
         double cl[3] = {bl_c[3 * (size_t)j], bl_c[3 * (size_t)j + 1], bl_c[3 * (size_t)j + 2]};
         for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
           const int a = w.eopt[e];
-          const bool on = !w.level[e] && a >= 0;
+          if (w.level[e] || a < 0) continue;
           double B[18];
 #pragma unroll
           for (int q = 0; q < 18; q++) B[q] = Hpl_c[18 * (size_t)e + q];
-          if (!on) continue;
 #pragma unroll
           for (int c = 0; c < 3; c++)
 #pragma unroll

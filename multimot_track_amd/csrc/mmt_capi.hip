@@ -419,12 +419,21 @@ int mmt_flush_objects(mmt_ctx* ctx, mmt_frame_result* res, mmt_motion* objs, int
   });
 }
 
+// Records a partial mmt_flush_objects left for a later call: tracking more frames before they
+// are drained would deliver newer frames' motions ahead of them (the header promises order).
+static int flush_owed(mmt_ctx* ctx) {
+  if (ctx->flushed.empty()) return 0;
+  ctx->err = "mmt_flush_objects has undelivered records: drain it before tracking more frames";
+  return MMT_ESTATE;
+}
+
 int mmt_track_rgbd_chunk_device(mmt_ctx* ctx, int nframes, const uint8_t* d_bgr,
                                 size_t bgr_pitch, const uint16_t* d_disp, size_t disp_pitch,
                                 const float* d_flow, size_t flow_pitch, const int32_t* d_mask,
                                 size_t mask_pitch, mmt_frame_result* res, mmt_motion* objs,
                                 int objs_cap, void* stream) {
   if (!ctx || !d_bgr || !d_disp || !d_flow || !d_mask || !res || nframes < 1) return MMT_EINVAL;
+  if (const int rc = flush_owed(ctx)) return rc;
   return guard(ctx, [&] {
     MMT_HIP(hipSetDevice(ctx->cfg.device_id));
     ensure_tracker(ctx);
@@ -482,6 +491,7 @@ int mmt_track_rgbd(mmt_ctx* ctx, const uint8_t* bgr, const uint16_t* disp256,
                    mmt_frame_result* res, mmt_motion* objs, int objs_cap) {
   (void)timestamp;
   if (!ctx || !bgr || !disp256 || !flow_uv || !mask || !res) return MMT_EINVAL;
+  if (const int rc = flush_owed(ctx)) return rc;
   return guard(ctx, [&] {
     track_host_frames(ctx, 1, &bgr, &disp256, &flow_uv, &mask, res, objs, objs_cap);
   });
@@ -494,6 +504,7 @@ int mmt_track_rgbd_chunk(mmt_ctx* ctx, int nframes, const uint8_t* const* bgr,
   if (!ctx || !bgr || !disp256 || !flow_uv || !mask || !res || nframes < 1) return MMT_EINVAL;
   for (int f = 0; f < nframes; f++)
     if (!bgr[f] || !disp256[f] || !flow_uv[f] || !mask[f]) return MMT_EINVAL;
+  if (const int rc = flush_owed(ctx)) return rc;
   return guard(ctx, [&] {
     if (nframes > std::max(1, ctx->cfg.max_batch))
       throw ArgError("chunk larger than config.max_batch");

@@ -344,7 +344,8 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // MMT_RANSAC_CU_MASK=1: the RANSAC stream confined to every 4th CU (otherwise every CU, low
   // priority).  Its kernels are grids of hundreds of one-wave workgroups at 256 VGPRs; spread over
   // the whole chip they can leave no CU with a free SIMD for the ego chain's workgroups.
-  // MMT_D3_PRIO=1: the D3 stream at high priority (otherwise normal).  Round 3 chose both for the
+  // MMT_D3_PRIO: the D3 stream's priority, 0 or unset low (the default), 1 high, 2 normal (the
+  // measured worst: a normal-priority stream shares the ego chain's queue).  Round 3 chose both for the
   // chunked bench; measured again with LocalMapping (interleaved A/B, tools/ab_interleave.py and
   // tools/one_frame_bench.py): chunked C3 895 (both on) against 896 frames/s (both off), one frame
   // per call 1.77 against 1.49 ms (the high-priority D3 queue and the masked RANSAC grids delay
@@ -359,8 +360,9 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   } else {
     MMT_HIP(hipStreamCreateWithPriority(&oa_, hipStreamNonBlocking, lo));
   }
-  const char* dp = getenv("MMT_D3_PRIO");  // 1 high, 0 normal, otherwise low
-  const int d3p = dp && atoi(dp) == 1 ? hi : (dp && atoi(dp) == 0 ? 0 : lo);
+  const char* dp = getenv("MMT_D3_PRIO");  // 1 high, 2 normal, otherwise (0, unset) low
+  const int d3v = dp ? atoi(dp) : 0;
+  const int d3p = d3v == 1 ? hi : (d3v == 2 ? 0 : lo);
   MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, d3p));
   MMT_HIP(hipHostMalloc((void**)&eh_, sizeof(EgoHost), hipHostMallocDefault));
   memset(eh_, 0, sizeof(EgoHost));

@@ -516,6 +516,41 @@ def test_deferred_objects_match_immediate():
                 assert np.array_equal(np.asarray(x[k]), np.asarray(y[k]), equal_nan=True), (i, k)
 
 
+def test_partial_flush_blocks_tracking_until_drained():
+    """A flush that leaves records for a later call (res_cap below the records owed) keeps the
+    order promise: tracking is refused with MMT_ESTATE until the records are drained, then goes
+    on with every record delivered once, in frame order."""
+    import torch
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    n = 12
+    seq = scene.kitti_like_sequence(n, 1242, 375, n_objects=3, seed=1003,
+                                    device=torch.device("cuda:0"))
+    c = M.Context(M.kitti03_config(1242, 375, 2000, max_batch=8))
+    sl = lambda a, b: [seq[k][a:b] for k in ("bgr", "disp", "flow", "mask")]  # noqa: E731
+    try:
+        c.set_deferred_objects(True)
+        got = []
+        for i in range(8):
+            r = c.track_chunk_device(*sl(i, i + 1))[0]
+            if r["objects_frame"] >= 0:
+                got.append(r["objects_frame"])
+        part = c.flush_objects_part(cap=1)
+        assert len(part) == 1
+        got += [f for f, _ in part]
+        with pytest.raises(M.MmtError, match="undelivered"):
+            c.track_chunk_device(*sl(8, 9))
+        got += [f for f, _ in c.flush_objects()]
+        for i in range(8, n):
+            r = c.track_chunk_device(*sl(i, i + 1))[0]
+            if r["objects_frame"] >= 0:
+                got.append(r["objects_frame"])
+        got += [f for f, _ in c.flush_objects()]
+    finally:
+        c.close()
+    assert got == list(range(n))
+
+
 @pytest.mark.parametrize("k", [2, 4])
 def test_contexts_from_threads_match_oracle(oracle_mod, k):
     """`bench.py --seqs-per-gpu K`'s setup: K contexts on one GPU, each tracking its own sequence
