@@ -113,6 +113,9 @@ def parse_args(argv=None):
                          "pipeline at each chunk boundary)")
     ap.add_argument("--single-frames", type=int, default=256,
                     help="frames of the one-frame-per-call leg (0: skip)")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave it; more queues measured "
+                         "slower: K=8 1461 / 733 / 299 frames/s at 4 / 16 / 32)")
     ap.add_argument("--rank-parity-frames", type=int, default=192,
                     help="frames of every sequence checked against the oracle on lines with "
                          "several sequences or ranks (0: skip)")
@@ -319,6 +322,11 @@ def main(argv=None):
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return self_launch(args)
 
+    # GPU_MAX_HW_QUEUES (hardware queues the HIP runtime multiplexes a process's streams onto,
+    # default 4; every context drives 5 streams) is read at HIP init: set before torch touches the
+    # device.  More queues measured slower (profiles/r05_hwq_sweep.txt).
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
     import torch
     import torch.distributed as dist
     from multimot_track_amd import shard
@@ -538,6 +546,7 @@ def main(argv=None):
                                    "association + ego + %d object motions)" % args.objects,
                        "width": W, "height": H, "orb_features": NF, "chunk_frames": C,
                        "sequences_per_gpu": K, "parallelism": "dp%d" % world,
+                       "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "frames_tracked": tracked, "objects_last_frame": n_obj_last,
                        "ego_abs_err_last_frame": round(ego_err, 5),
                        "scene_render_s": round(t_gen, 2), "c2": c2,

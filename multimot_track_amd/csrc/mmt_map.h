@@ -20,9 +20,11 @@
 //  * LocalMapping runs synchronously (always idle for NeedNewKeyFrame, never aborted) and does
 //    ProcessNewKeyFrame without the BoW conversion, MapPointCulling, SearchInNeighbors, the local
 //    BA (GPU, mmt_ba.hip) and KeyFrameCulling; CreateNewMapPoints needs the missing vocabulary;
-//  * TrackReferenceKeyFrame's SearchByBoW and Relocalization (BoW database) become
-//    SearchByProjection against the last frame at the last frame's pose (th 15) + the reference's
-//    PoseOptimization and acceptance tests.
+//  * TrackReferenceKeyFrame's SearchByBoW becomes SearchByProjection against the last frame at the
+//    last frame's pose (th 15) + the reference's PoseOptimization and acceptance tests;
+//  * Relocalization (BoW database + PnPsolver) becomes a search of the reference keyframe's and
+//    its best covisibles' map points at the motion model's prediction from the last frame, with
+//    the reference's acceptance tests (relocalization_subst).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -177,6 +179,8 @@ class MapEngine {
                                float* Tlast, const float* vel, MapStatsH& st);
   bool track_reference_subst(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
                              const float* Tlast);
+  bool relocalization_subst(MapFrameH& C, const GridFrame& G, float* Tcw, const float* Tlast,
+                            const float* vel);
   bool track_local_map(MapFrameH& C, const GridFrame& G, float* Tcw);
   int discard_outliers(MapFrameH& C, int nmatches, int* nmatchesMap);
   void update_last_frame(MapFrameH& L, float* Tlast);
@@ -215,8 +219,10 @@ class MapEngine {
   void kf_store_add(int kf);
   void fuse_launch(const std::vector<int>& kft_kf, const std::vector<FuseQuery>& q, int2* res);
   // GPU stages (synchronous on s_)
+  // retry_below (-1: min_matches): the retry at retry_th runs below this many matches
   int gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
-                      const float* Tlast, float th, float retry_th, int min_matches);
+                      const float* Tlast, float th, float retry_th, int min_matches,
+                      int retry_below = -1);
   void pose_desc_fill(uint8_t* h_blk, uint8_t* d_blk, const float* Tcw);
   size_t out_bytes(int n) const;
   MapEdgeArgs edge_args(const GridFrame& G) const;

@@ -517,7 +517,9 @@ void MapEngine::apply_pose_opt(MapFrameH& C, float* Tcw) {
 // its matches when there are at least min_matches -- the whole chain on the device, one sync.
 // Returns nmatches; the pose and outliers are applied when D1 ran.
 int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
-                               const float* Tlast, float th, float retry_th, int min_matches) {
+                               const float* Tlast, float th, float retry_th, int min_matches,
+                               int retry_below) {
+  if (retry_below < 0) retry_below = min_matches;
   const double t_pack = prof_on_ ? now_us() : 0;
   const int n1 = L.n;
   uint8_t* hk = h_last_ + kDescBytes;
@@ -560,7 +562,7 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
   launch_sbp_frame(G, Tcw, LD, th, 0, 1, c2_, d_match_, d_nm_, s_, nullptr, 0,
                    fused ? &e : nullptr);
   if (retry_th > 0)
-    launch_sbp_frame(G, Tcw, LD, retry_th, 0, 1, c2_, d_match_, d_nm_, s_, d_nm_, min_matches,
+    launch_sbp_frame(G, Tcw, LD, retry_th, 0, 1, c2_, d_match_, d_nm_, s_, d_nm_, retry_below,
                      fused ? &e : nullptr);
   if (!fused) launch_map_edges(e, s_);
   launch_pose_opt(d_pod_, 1, std::min(C.n, nact), s_);
@@ -821,6 +823,54 @@ bool MapEngine::track_reference_subst(MapFrameH& C, const GridFrame& G, float* T
   int nmatchesMap = 0;
   discard_outliers(C, nmatches, &nmatchesMap);
   return nmatchesMap >= 10;
+}
+
+// Relocalization substitute (pinned deviation, as oracle/map_ref.cpp relocalization_subst): the
+// reference keyframe and its best 10 covisibles as candidates, each searched as TrackWithMotionModel
+// searches the last frame (the keyframe as the last frame, th 15, again at 30 below 20 matches, at
+// the pose the motion model predicts from the last, flow-tracked, frame), then the reference's
+// acceptance of Tracking.cc:3700-3770 (PoseOptimization: fewer than 10 inliers -> next candidate;
+// outliers dropped; 50 inliers or more -> relocalised).
+bool MapEngine::relocalization_subst(MapFrameH& C, const GridFrame& G, float* Tcw,
+                                     const float* Tlast, const float* vel) {
+  std::vector<int> cand;
+  if (refKF_ >= 0 && !kfs_[refKF_].bad) cand.push_back(refKF_);
+  if (refKF_ >= 0) {
+    const std::vector<int>& o = kfs_[refKF_].ordered;
+    for (size_t q = 0; q < o.size() && q < 10; q++)
+      if (!kfs_[o[q]].bad) cand.push_back(o[q]);
+  }
+  float Tpred[16];
+  mat4_mul(vel, Tlast, Tpred);
+  for (int k : cand) {
+    const KFrame& K = kfs_[k];
+    MapFrameH V;  // the keyframe as a last frame: its good map points, no outliers
+    V.id = K.frameId;
+    V.n = (int)K.keys.size();
+    V.kps = K.keys.data();
+    V.desc = K.desc.data();
+    V.uR = K.uR.data();
+    V.depth = K.depth.data();
+    V.mps = K.mps;
+    for (int& h : V.mps)
+      if (h >= 0 && pts_[h].bad) h = -1;
+    V.outlier.assign(V.mps.size(), 0);
+    memcpy(Tcw, Tpred, 64);
+    const int nm = gpu_frame_chain(C, G, Tcw, V, K.Tcw, 15, 30, 15, 20);
+    if (nm < 15) continue;
+    int nGood = 0;
+    for (int i = 0; i < C.n; i++) nGood += C.mps[i] >= 0 && !C.outlier[i];
+    if (nGood < 10) continue;
+    for (int i = 0; i < C.n; i++)
+      if (C.mps[i] >= 0 && C.outlier[i]) {
+        C.mps[i] = -1;
+        C.outlier[i] = 0;
+      }
+    if (nGood >= 50) return true;
+  }
+  std::fill(C.mps.begin(), C.mps.end(), -1);
+  memcpy(Tcw, Tpred, 64);
+  return false;
 }
 
 void MapEngine::update_local_keyframes(MapFrameH& C) {  // Tracking::UpdateLocalKeyFrames
@@ -1094,7 +1144,7 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
       }
     }
   } else {
-    bOK = track_reference_subst(C, G, Tcw, L, Tlast);  // Relocalization (substitute)
+    bOK = relocalization_subst(C, G, Tcw, Tlast, vel);  // Relocalization (substitute)
     if (bOK) lastRelocFrameId_ = C.id;
   }
   C.refKF = refKF_;

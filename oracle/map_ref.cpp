@@ -517,6 +517,57 @@ bool MapTracker::track_reference_subst(const std::vector<Key>& keys,
   return nmatchesMap >= 10;
 }
 
+// Relocalization substitute (pinned deviation, oracle_map.h).  The reference (Tracking.cc:3614-3776)
+// takes its candidate keyframes from the BoW database and its pose hypotheses from SearchByBoW +
+// PnPsolver, neither possible without ORBvoc.txt.  Here the candidates are the reference keyframe
+// and its best 10 covisibles in order (GetBestCovisibilityKeyFrames), the hypothesis is the pose
+// the motion model predicts from the last frame (the flow-solved pose of every frame keeps being
+// tracked while the map is lost), and each candidate's map points are searched as
+// TrackWithMotionModel searches the last frame's (the keyframe as the last frame: th 15, again at
+// 30 below 20 matches; below 15 the candidate is discarded, the reference's test after
+// SearchByBoW).  Then the reference's acceptance: PoseOptimization, fewer than 10 inliers -> next
+// candidate, outliers dropped, 50 inliers or more -> relocalised.  The reference's extra
+// SearchByProjection(F, KF, sFound, 10 / 3, 100 / 64) rounds for 10-49 inliers are not restated
+// (the candidate's points were already searched in a wide window at the predicted pose).
+bool MapTracker::relocalization_subst(const std::vector<Key>& keys,
+                                      const std::vector<uint8_t>& desc, MapFrame& C, float* Tcw,
+                                      const float* Tlast, const float* vel) {
+  std::vector<int> cand;
+  if (refKF_ >= 0 && !kfs[refKF_].bad) cand.push_back(refKF_);
+  if (refKF_ >= 0)
+    for (int k : best_covisibles(refKF_, 10))
+      if (!kfs[k].bad) cand.push_back(k);
+  float Tpred[16];
+  m4_mul(vel, Tlast, Tpred);
+  for (int k : cand) {
+    const OKeyFrame& K = kfs[k];
+    MapFrame V;  // the keyframe as a last frame: its good map points, no outliers
+    V.mps = K.mps;
+    for (int& h : V.mps)
+      if (h >= 0 && mp(h).bad) h = -1;
+    V.outlier.assign(V.mps.size(), 0);
+    std::fill(C.mps.begin(), C.mps.end(), -1);
+    memcpy(Tcw, Tpred, 64);
+    int nmatches = search_frame(keys, desc, C, Tcw, K.keys, V, K.Tcw, 15);
+    if (nmatches < 20) {
+      std::fill(C.mps.begin(), C.mps.end(), -1);
+      nmatches = search_frame(keys, desc, C, Tcw, K.keys, V, K.Tcw, 30);
+    }
+    if (nmatches < 15) continue;
+    const int nGood = pose_optimization(keys, C, Tcw);
+    if (nGood < 10) continue;
+    for (size_t i = 0; i < C.mps.size(); i++)
+      if (C.mps[i] >= 0 && C.outlier[i]) {
+        C.mps[i] = -1;
+        C.outlier[i] = 0;
+      }
+    if (nGood >= 50) return true;
+  }
+  std::fill(C.mps.begin(), C.mps.end(), -1);
+  memcpy(Tcw, Tpred, 64);
+  return false;
+}
+
 void MapTracker::update_local_keyframes(MapFrame& C) {  // Tracking::UpdateLocalKeyFrames
   std::map<int, int> counter;
   for (size_t i = 0; i < C.mps.size(); i++) {
@@ -748,7 +799,7 @@ int MapTracker::track(const std::vector<Key>& keys, const std::vector<uint8_t>& 
       }
     }
   } else {
-    bOK = track_reference_subst(keys, desc, C, Tcw, lkeys, L, Tlast);  // Relocalization
+    bOK = relocalization_subst(keys, desc, C, Tcw, Tlast, vel);  // Relocalization
     if (bOK) lastRelocFrameId_ = C.id;
   }
   C.refKF = refKF_;

@@ -30,10 +30,14 @@
 //    keyframe reaches the last frame through Tlr in UpdateLastFrame, as in the reference;
 //    CreateNewMapPoints needs SearchForTriangulation, i.e. the BoW vocabulary (missing), and is
 //    skipped;
-//  * TrackReferenceKeyFrame's SearchByBoW (and Relocalization, whose candidates come from the BoW
-//    database) needs the missing vocabulary: both are replaced by SearchByProjection against the
-//    last frame at the last frame's pose (th 15, orientation check), then PoseOptimization and the
-//    reference's own acceptance tests;
+//  * TrackReferenceKeyFrame's SearchByBoW needs the missing vocabulary: it is replaced by
+//    SearchByProjection against the last frame at the last frame's pose (th 15, orientation
+//    check), then PoseOptimization and the reference's own acceptance tests;
+//  * Relocalization (candidates from the BoW database, hypotheses from SearchByBoW + PnPsolver)
+//    likewise: the candidates are the reference keyframe and its best 10 covisibles, the
+//    hypothesis the motion model's prediction from the last (flow-tracked) frame, each
+//    candidate's map points searched as TrackWithMotionModel searches the last frame's, then
+//    the reference's acceptance (PoseOptimization, >= 10 inliers, outliers dropped, >= 50);
 //  * map points whose unprojection is not finite (depth +inf where the disparity is 0) project to
 //    no pixel (the reference would index the grid with an undefined float -> int conversion).
 #pragma once
@@ -213,6 +217,8 @@ class MapTracker {
   bool track_reference_subst(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
                              MapFrame& C, float* Tcw, const std::vector<Key>& lkeys,
                              const MapFrame& L, const float* Tlast);
+  bool relocalization_subst(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                            MapFrame& C, float* Tcw, const float* Tlast, const float* vel);
   bool track_local_map(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
                        MapFrame& C, float* Tcw);
   int search_frame(const std::vector<Key>& keys, const std::vector<uint8_t>& desc, MapFrame& C,

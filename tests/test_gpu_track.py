@@ -422,6 +422,39 @@ def test_track_c3_long_sequence_matches_oracle(oracle_mod):
     assert om["n_ba"] > 60
 
 
+def test_lost_frame_and_relocalization_match_oracle(oracle_mod):
+    """A textureless frame (no ORB keys) loses map tracking and the relocalization substitute
+    recovers on the next frame (the reference keyframe's and its covisibles' map points at the
+    motion model's prediction, Tracking.cc:3700-3770's acceptance): the GPU tracker takes the
+    same LOST -> OK path as the oracle, frame by frame within the bar."""
+    import torch
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    from oracle import compare
+    n, C = 56, 16
+    dev = torch.device("cuda:0")
+    seq = scene.kitti_like_sequence(n, 1242, 375, n_objects=3, seed=1003, device=dev)
+    seq["bgr"][40] = 128
+    ctx = M.Context(M.kitti03_config(1242, 375, 2000, max_batch=C))
+    got = []
+    try:
+        for s0 in range(0, n, C):
+            sl = slice(s0, min(n, s0 + C))
+            got += ctx.track_chunk_device(seq["bgr"][sl], seq["disp"][sl], seq["flow"][sl],
+                                          seq["mask"][sl])
+    finally:
+        ctx.close()
+    tr = oracle_mod.Tracker(1242, 375, K_KITTI, 387.5744, 0, 2000)
+    ora = []
+    for i in range(n):
+        f = scene.to_numpy_frames({k: seq[k][i:i + 1] for k in ("bgr", "disp", "flow", "mask")})[0]
+        ora.append(tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]))
+    rec = compare.parity_record(got, ora)
+    assert rec["first_divergent_frame"] is None, rec
+    st = [g["map_state"] for g in got]
+    assert st[40] == 2 and all(v == 1 for v in st[:40] + st[41:]), st
+
+
 def test_split_solve_fallback_matches_oracle(oracle_mod, monkeypatch):
     """The split ego solve needs its workgroups resident together; when an exchange wait exceeds
     its bound (forced here with a one-tick bound, MMT_DEBUG_SPLIT_SPIN) the solve reports it and the

@@ -64,3 +64,24 @@ def test_map_invariants_catch_corruption(oracle_mod):
     assert any("parent" in v for v in corrupt(lambda E: E["kf_i"].__setitem__((kk, 3), kk)))
     assert any("sorted" in v or "not in its weights" in v for v in
                corrupt(lambda E: E["ord"].__setitem__((0, 2), E["ord"][0, 2] + 1000)))
+
+
+def test_oracle_relocalization_recovers_after_lost_frame(oracle_mod):
+    """A frame without texture (no ORB keys) loses map tracking; the relocalization substitute
+    (oracle/map_ref.cpp relocalization_subst: the reference keyframe's and its covisibles' map
+    points at the motion model's prediction, the reference's acceptance tests) recovers on the
+    next frame, and the map passes the invariant checks after it."""
+    from multimot_track_amd import scene
+    K, W, H = _half_res_camera()
+    R = scene.SequenceRenderer(scene.StreetScene(3, 1003), W, H, K=K)
+    tr = oracle_mod.Tracker(W, H, (K["fx"], K["fy"], K["cx"], K["cy"]), K["bf"], 0, 1000)
+    states = []
+    for i in range(43):
+        b, d, f, m = R.frame(i)
+        b = b.numpy()
+        if i == 40:
+            b = np.full_like(b, 128)
+        r = tr.track(b, d.numpy().view(np.uint16), f.numpy(), m.numpy())
+        states.append(r["map_state"])
+    assert states[:40] == [1] * 40 and states[40] == 2 and states[41:] == [1, 1]
+    assert check_map(tr.map_dump()) == []
