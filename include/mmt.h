@@ -435,8 +435,16 @@ typedef struct mmt_map_counters {
   double lm_us, ba_us, fuse_us;
   int64_t d2_split_fallbacks;  /* ego flow solves re-run on one workgroup because the split
                                   solve's workgroups were not resident together             */
+  int64_t n_reparent;          /* spanning-tree children re-parented by KeyFrame::SetBadFlag
+                                  (KeyFrame.cc:480-537) when KeyFrameCulling culls a keyframe */
 } mmt_map_counters;
 int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out);
+
+/* Test knob (no reference counterpart): LocalMapping::KeyFrameCulling's redundancy ratio, a
+ * keyframe is culled when more than ratio x its close map points are seen by 3 other keyframes
+ * (0.9 in the reference, LocalMapping.cc:697; the default).  The synthetic sequences never reach
+ * 0.9, so the culling tests lower it to exercise KeyFrame::SetBadFlag. */
+int mmt_set_keyframe_culling_ratio(mmt_ctx* ctx, double ratio);
 
 /* The tracker's map as flat arrays (no reference counterpart: the map invariant tests and the
  * map-graph parity against the CPU oracle read it).  Keyframes and map points are numbered in

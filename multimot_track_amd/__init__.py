@@ -112,7 +112,7 @@ class MmtMapCounters(ctypes.Structure):
         "n_ba", "n_fused", "n_culled", "n_ba_erased", "ba_trials", "ba_edges", "ba_kfs",
         "ba_pts", "ba_max_opt", "fuse_launches", "fuse_queries", "fuse_relaunches")] + \
         [(k, ctypes.c_double) for k in ("lm_us", "ba_us", "fuse_us")] + \
-        [("d2_split_fallbacks", ctypes.c_int64)]
+        [("d2_split_fallbacks", ctypes.c_int64), ("n_reparent", ctypes.c_int64)]
 
 
 MAP_DUMP_FIELDS = (("kf_i", np.int64, 4), ("kf_T", np.float32, 16), ("kf_mps_start", np.int32, 1),
@@ -254,6 +254,7 @@ def lib():
                                                   vp]
         L.mmt_map_counters_read.argtypes = [vp, ctypes.POINTER(MmtMapCounters)]
         L.mmt_map_dump.argtypes = [vp, vp, ctypes.POINTER(MmtMapDumpArrays)]
+        L.mmt_set_keyframe_culling_ratio.argtypes = [vp, ctypes.c_double]
         L.mmt_set_deferred_objects.argtypes = [vp, i32]
         L.mmt_flush_objects.argtypes = [vp, vp, vp, i32, i32, vp]
         _LIB = L
@@ -600,6 +601,10 @@ class Context:
                 out.append((d["objects_frame"], d["objects"]))
             if not until_empty:
                 return out
+
+    def set_keyframe_culling_ratio(self, ratio):
+        """Test knob: KeyFrameCulling's redundancy ratio (0.9 in the reference)."""
+        self._check(lib().mmt_set_keyframe_culling_ratio(self._h, float(ratio)))
 
     def map_dump(self):
         """The tracker's map as flat arrays (mmt_map_dump): keyframes (id, frame, bad, parent)

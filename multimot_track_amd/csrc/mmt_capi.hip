@@ -860,6 +860,16 @@ int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out) {
     out->ba_us = m.ba_us;
     out->fuse_us = m.fuse_us;
     out->d2_split_fallbacks = ctx->tracker.split_fallbacks();
+    out->n_reparent = m.n_reparent;
+  });
+}
+
+int mmt_set_keyframe_culling_ratio(mmt_ctx* ctx, double ratio) {
+  if (!ctx || !(ratio >= 0)) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ensure_tracker(ctx);
+    ctx->tracker.set_cull_ratio(ratio);
   });
 }
 

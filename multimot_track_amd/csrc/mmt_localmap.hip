@@ -177,6 +177,7 @@ void MapEngine::kf_set_bad(int kf) {  // KeyFrame::SetBadFlag (mbNotErase is nev
     if (!bContinue) break;
     kfs_[pC].parent = pP;  // ChangeParent
     kfs_[pP].children.insert(pC);
+    mstats_.n_reparent++;
     cand.insert(pC);
     K.children.erase(pC);
   }
@@ -184,6 +185,7 @@ void MapEngine::kf_set_bad(int kf) {  // KeyFrame::SetBadFlag (mbNotErase is nev
     for (int ch : K.children) {
       kfs_[ch].parent = K.parent;
       kfs_[K.parent].children.insert(ch);
+      mstats_.n_reparent++;
     }
     kfs_[K.parent].children.erase(kf);
   }
@@ -494,7 +496,7 @@ void MapEngine::keyframe_culling(int kf) {  // LocalMapping::KeyFrameCulling (RG
         if (nObs >= thObs) nRedundant++;
       }
     }
-    if (nRedundant > 0.9 * nMPs) {
+    if (nRedundant > cull_ratio_ * nMPs) {  // 0.9 (LocalMapping.cc:697) unless a test sets it
       kf_set_bad(k);
       mstats_.n_culled++;
     }

@@ -99,7 +99,7 @@ struct KFrame {
 struct MappingStats {
   long n_ba = 0, n_fused = 0, n_culled = 0, n_ba_erased = 0, ba_trials = 0, ba_edges = 0,
        ba_kfs = 0, ba_pts = 0, ba_max_opt = 0, fuse_launches = 0, fuse_queries = 0,
-       fuse_relaunches = 0;
+       fuse_relaunches = 0, n_reparent = 0;
   double lm_us = 0, ba_us = 0, fuse_us = 0;  // host wall time (MMT_MAP_PROFILE)
   // finer host wall times of the keyframe path (MMT_MAP_PROFILE; printed at destruction)
   double kfnew_us = 0, pnk_us = 0, sin_us = 0, basolve_us = 0, cull_us = 0, lmsync_us = 0;
@@ -161,6 +161,8 @@ class MapEngine {
   // them into the keyframe store, where Fuse reads them
   void set_frame_grid(const GridFrame& G) { G_ = G; }
   const MappingStats& mapping_stats() const { return mstats_; }
+  // test knob: KeyFrameCulling's redundancy ratio (0.9 in the reference, LocalMapping.cc:697)
+  void set_cull_ratio(double r) { cull_ratio_ = r; }
   // the map as flat arrays (mmt_map_dump, include/mmt.h): sizes[7]; arrays written when out != 0
   void dump(int32_t* sizes, const mmt_map_dump_arrays* out) const;
 
@@ -320,6 +322,7 @@ class MapEngine {
   // ---- LocalMapping
   GridFrame G_{};
   MappingStats mstats_;
+  double cull_ratio_ = 0.9;
   hipStream_t lm_s_ = nullptr;  // LocalMapping's stream (beside the ego solve)
   std::vector<uint8_t*> kf_blocks_;  // keyframe store: blocks of kKFBlock records
   size_t kf_rec_bytes_ = 0;

@@ -88,6 +88,7 @@ class Tracker {
   int kcap() const { return kcap_; }
   const MappingStats& mapping_stats() const { return map_.mapping_stats(); }
   const MapEngine& map() const { return map_; }
+  void set_cull_ratio(double r) { map_.set_cull_ratio(r); }
   long split_fallbacks() const { return split_fallbacks_; }
   // the last tracked frame's static samples (mvSiftKeys) and object samples (mvObjKeys,
   // vSemObjLabel), copied to the host (visualisation hook); counts clipped to the caps

@@ -204,6 +204,7 @@ void MapTracker::kf_set_bad(int kf) {  // KeyFrame::SetBadFlag (mbNotErase is ne
     if (!bContinue) break;
     kfs[pC].parent = pP;  // ChangeParent
     kfs[pP].children.insert(pC);
+    mstats.n_reparent++;
     cand.insert(pC);
     K.children.erase(pC);
   }
@@ -211,6 +212,7 @@ void MapTracker::kf_set_bad(int kf) {  // KeyFrame::SetBadFlag (mbNotErase is ne
     for (int ch : K.children) {
       kfs[ch].parent = K.parent;
       kfs[K.parent].children.insert(ch);
+      mstats.n_reparent++;
     }
     kfs[K.parent].children.erase(kf);
   }
@@ -408,7 +410,7 @@ void MapTracker::keyframe_culling(int kf) {  // LocalMapping::KeyFrameCulling (R
         if (nObs >= thObs) nRedundant++;
       }
     }
-    if (nRedundant > 0.9 * nMPs) {
+    if (nRedundant > cullRatio * nMPs) {  // 0.9 (LocalMapping.cc:697) unless a test sets it
       kf_set_bad(k);
       mstats.n_culled++;
     }

@@ -271,11 +271,17 @@ class Tracker:
 
     def map_stats(self):
         """LocalMapping counters (oracle/mapping_ref.cpp)."""
-        out = np.zeros(9, np.int64)
+        out = np.zeros(10, np.int64)
         lib().oracle_tracker_map_stats(ctypes.c_void_p(self._h), _p(out))
         keys = ("n_ba", "n_fused", "n_culled", "n_ba_erased", "ba_trials", "ba_edges", "ba_kfs",
-                "ba_pts", "ba_max_opt_kfs")
+                "ba_pts", "ba_max_opt_kfs", "n_reparent")
         return {k: int(v) for k, v in zip(keys, out)}
+
+    def set_cull_ratio(self, r):
+        """Test knob: KeyFrameCulling's redundancy ratio (0.9 in the reference)."""
+        L = lib()
+        L.oracle_tracker_set_cull_ratio.argtypes = [ctypes.c_void_p, ctypes.c_double]
+        L.oracle_tracker_set_cull_ratio(self._h, float(r))
 
     def map_dump(self):
         """The map as flat arrays, in the layout of the product's mmt_map_dump (include/mmt.h)."""

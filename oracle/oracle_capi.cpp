@@ -254,13 +254,16 @@ void* oracle_tracker_create(int w, int h, float fx, float fy, float cx, float cy
 void oracle_tracker_destroy(void* t) { delete (OTracker*)t; }
 
 // LocalMapping counters: [BAs, fused, culled keyframes, BA-erased observations, BA trials, BA
-// edges, BA keyframe vertices, BA points, largest count of optimised keyframes]
+// edges, BA keyframe vertices, BA points, largest count of optimised keyframes, re-parented
+// spanning-tree children]
 void oracle_tracker_map_stats(void* tp, long long* out) {
   const MapTracker::MappingStats& m = ((OTracker*)tp)->map.mstats;
-  const long v[9] = {m.n_ba, m.n_fused, m.n_culled, m.n_ba_erased, m.ba_trials, m.ba_edges,
-                     m.ba_kfs, m.ba_pts, m.ba_max_opt_kfs};
-  for (int i = 0; i < 9; i++) out[i] = v[i];
+  const long v[10] = {m.n_ba, m.n_fused, m.n_culled, m.n_ba_erased, m.ba_trials, m.ba_edges,
+                      m.ba_kfs, m.ba_pts, m.ba_max_opt_kfs, m.n_reparent};
+  for (int i = 0; i < 10; i++) out[i] = v[i];
 }
+
+void oracle_tracker_set_cull_ratio(void* tp, double r) { ((OTracker*)tp)->map.cullRatio = r; }
 
 // Records the problem and result of the which-th LocalBundleAdjustment (0-based) of this tracker,
 // as probe fixtures for the GPU solver.

@@ -204,10 +204,11 @@ class MapTracker {
   // test hook: called with each LocalBundleAdjustment problem and its result (probe fixtures)
   std::function<void(const BAProblem&, const BAResult&)> ba_hook;
   struct MappingStats {
-    long n_ba = 0, n_fused = 0, n_culled = 0, n_ba_erased = 0;
+    long n_ba = 0, n_fused = 0, n_culled = 0, n_ba_erased = 0, n_reparent = 0;
     long ba_trials = 0, ba_edges = 0, ba_kfs = 0, ba_pts = 0, ba_max_opt_kfs = 0;
   } mstats;
   OMapPoint& mp(int h) { return h >= kTemp ? temps[h - kTemp] : pts[h]; }
+  double cullRatio = 0.9;  // KeyFrameCulling's redundancy ratio (test knob; LocalMapping.cc:697)
 
  private:
   bool track_with_motion_model(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,

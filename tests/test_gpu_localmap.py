@@ -201,3 +201,41 @@ def test_tracker_map_graph_matches_oracle(oracle_mod, c3_seq):
     finally:
         ctx.close()
     assert checks > 12
+
+
+def test_keyframe_culling_and_reparenting_match_oracle(oracle_mod):
+    """KeyFrameCulling (LocalMapping.cc:653-720) and KeyFrame::SetBadFlag's spanning-tree
+    re-parenting (KeyFrame.cc:453-545) on the GPU path.  The reference's 0.9 redundancy ratio is
+    never reached by the synthetic drives, so both sides lower it to 0.3 through the test knob
+    (mmt_set_keyframe_culling_ratio / oracle set_cull_ratio) on a slow half-resolution drive:
+    the product culls the same keyframes and re-parents the same children as the oracle, and the
+    whole map graph equals the oracle's after every keyframe."""
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    from map_invariants import check_map, same_map
+    Kc = {k: v * 0.5 for k, v in scene.KITTI03.items()}
+    W, H = 621, 188
+    R = scene.SequenceRenderer(scene.StreetScene(3, 1003, speed=0.3), W, H, K=Kc)
+    cfg = M.kitti03_config(W, H, 1000)
+    cfg.fx, cfg.fy, cfg.cx, cfg.cy, cfg.bf = Kc["fx"], Kc["fy"], Kc["cx"], Kc["cy"], Kc["bf"]
+    ctx = M.Context(cfg)
+    tr = oracle_mod.Tracker(W, H, (Kc["fx"], Kc["fy"], Kc["cx"], Kc["cy"]), Kc["bf"], 0, 1000)
+    ctx.set_keyframe_culling_ratio(0.3)
+    tr.set_cull_ratio(0.3)
+    try:
+        for i in range(60):
+            b, d, f, m = R.frame(i)
+            args = (b.numpy(), d.numpy().view(np.uint16), f.numpy(), m.numpy())
+            g = ctx.track(*args)
+            o = tr.track(*args)
+            assert g["new_keyframe"] == o["new_keyframe"] and g["map_state"] == o["map_state"], i
+            if o["new_keyframe"]:
+                Dg, Do = ctx.map_dump(), tr.map_dump()
+                diff, fmax = same_map(Dg, Do)
+                assert diff == [] and fmax < TOL, (i, diff, fmax)
+                assert check_map(Dg, newest=len(Dg["kf_i"]) - 1) == [], i
+        so, sg = tr.map_stats(), ctx.map_counters()
+        assert so["n_culled"] >= 2 and so["n_reparent"] >= 1, so
+        assert (sg["n_culled"], sg["n_reparent"]) == (so["n_culled"], so["n_reparent"])
+    finally:
+        ctx.close()

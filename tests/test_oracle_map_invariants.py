@@ -85,3 +85,27 @@ def test_oracle_relocalization_recovers_after_lost_frame(oracle_mod):
         states.append(r["map_state"])
     assert states[:40] == [1] * 40 and states[40] == 2 and states[41:] == [1, 1]
     assert check_map(tr.map_dump()) == []
+
+
+def test_oracle_keyframe_culling_reparents_and_keeps_invariants(oracle_mod):
+    """KeyFrameCulling (LocalMapping.cc:653-720) with KeyFrame::SetBadFlag's re-parenting
+    (KeyFrame.cc:453-545).  The synthetic sequences never reach the reference's 0.9 redundancy
+    ratio, so the test lowers it (the test knob, oracle set_cull_ratio / the product's
+    mmt_set_keyframe_culling_ratio) on a slow drive: keyframes are culled, spanning-tree children
+    are re-parented, and the map passes every invariant after each LocalMapping."""
+    from multimot_track_amd import scene
+    K, W, H = _half_res_camera()
+    R = scene.SequenceRenderer(scene.StreetScene(3, 1003, speed=0.3), W, H, K=K)
+    tr = oracle_mod.Tracker(W, H, (K["fx"], K["fy"], K["cx"], K["cy"]), K["bf"], 0, 1000)
+    tr.set_cull_ratio(0.3)
+    for i in range(60):
+        b, d, f, m = R.frame(i)
+        r = tr.track(b.numpy(), d.numpy().view(np.uint16), f.numpy(), m.numpy())
+        assert r["map_state"] == 1, i
+        if r["new_keyframe"]:
+            D = tr.map_dump()
+            assert check_map(D, newest=len(D["kf_i"]) - 1) == [], i
+    st = tr.map_stats()
+    assert st["n_culled"] >= 2 and st["n_reparent"] >= 1, st
+    D = tr.map_dump()
+    assert int(D["kf_i"][:, 2].sum()) == st["n_culled"]
