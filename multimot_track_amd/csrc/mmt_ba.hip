@@ -734,9 +734,10 @@ namespace {
 //   per trial:                 k_ba2_p1    one thread per point: (H_ll + lambda I)^-1, Y, H_pl D^-1 b_l
 //                              k_ba2_p2    one workgroup per keyframe-pair block / keyframe: Schur sums
 //                              k_ba2_p3    one workgroup: the reduced system, LDL^T, increments, trial poses
-//                              k_ba2_p4    one thread per point: point increments, trial errors, chi2
-//                              k_ba2_p5    one workgroup: the LM decision (rho, lambda, Raul's stop,
-//                                          the chi2-increase stop), iteration and round bookkeeping
+//                              k_ba2_p4    one thread per point: point increments, trial errors, chi2;
+//                                          its last workgroup then takes the LM decision (rho,
+//                                          lambda, Raul's stop, the chi2-increase stop) and the
+//                                          iteration and round bookkeeping (ba2_decide)
 // The estimates are double-buffered (current / trial, swapped on acceptance), so a rejected trial
 // needs no restore.  Every reduction has a fixed order: the solve is deterministic.
 
@@ -783,6 +784,7 @@ struct BAWork2 {
   double* cvpart;   // 6 per keyframe item: its edges' H_pl D^-1 b_l
   double* linpart;  // 2 per point workgroup: chi2, largest active H_ll diagonal
   double* p4part;   // 2 per point workgroup: trial chi2, scale
+  unsigned* p4cnt;  // k_ba2_p4's workgroups done with the trial (the last one decides, then resets)
   uint8_t* level;   // n_edge
   int* eopt;        // n_edge: the edge's optimised-keyframe index, -1 for a fixed keyframe
   uint8_t* kf_act;  // n_kf: optimised keyframe with an active edge this round
@@ -889,6 +891,7 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_init(BADesc d, BAWork2 w) {
     for (int a = threadIdx.x; a < d.n_opt; a += kMkThreads)
       if (d.kf_start[a + 1] > d.kf_start[a]) w.kf_act[d.opt_kf[a]] = 1;
     if (threadIdx.x == 0) {
+      *w.p4cnt = 0;
       BAState& s = *w.st;
       memset(&s, 0, sizeof(s));
       s.need_lin = 1;
@@ -1355,6 +1358,136 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
   }
 }
 
+// trial step 5, one workgroup: OptimizationAlgorithmLevenberg::solve's decision for the trial,
+// the end of the iteration (SparseOptimizer::optimize's stops), the switch to the second round
+// (the inlier check of Optimizer.cc:3559-3590 on the last computed errors) and the end of the solve
+// (every thread of one workgroup of NT threads; k_ba2_p4's last workgroup runs it)
+template <int NT>
+__device__ void ba2_decide(const BADesc& d, const BAWork2& w) {
+  __shared__ int s_round_end;
+  __shared__ double s_part[NT / 64];
+  __shared__ double s_sum[2];
+  BAState* stp = w.st;
+  const int tid = threadIdx.x;
+  if (tid < 64) {  // the trial's chi2 and scale over the point workgroups (wave 0, fixed order)
+    double a = 0, b = 0;
+    for (int g = tid; g < w.gP; g += 64) {
+      a += w.p4part[2 * g];
+      b += w.p4part[2 * g + 1];
+    }
+    a = wave_sum_dpp(a);
+    b = wave_sum_dpp(b);
+    if (tid == 0) {
+      s_sum[0] = a;
+      s_sum[1] = b;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    BAState& s = *stp;
+    const double tc = s_sum[0], sc = s_sum[1];
+    double tempChi = tc;
+    const double lastTrialChi = tempChi;
+    if (!s.ok2) tempChi = DBL_MAX;
+    double scale = s.scale_p + sc;
+    double rho = s.currentChi - tempChi;
+    scale += 1e-3;
+    rho /= scale;
+    if (rho > 0 && isfinite(tempChi)) {
+      double alpha = 1. - pow((2 * rho - 1), 3);
+      alpha = fmin(alpha, 2. / 3.);
+      s.lambda *= fmax(1. / 3., alpha);
+      s.ni = 2;
+      s.currentChi = tempChi;
+      s.cb = 1 - s.cb;  // the trial (and its linearisation, with SPEC) becomes the current estimate
+      s.spec_ok = w.spec;
+    } else {
+      s.lambda *= s.ni;
+      s.ni *= 2;
+      s.spec_ok = 0;
+    }
+    s.qmax++;
+    s.trials[s.round]++;
+    int round_end = 0;
+    if (rho < 0 && s.qmax < 10) {
+      s.need_lin = 0;  // another trial of this iteration
+    } else {
+      bool ok = true;
+      if (s.qmax == 10 || rho == 0) ok = false;
+      if (ok) {
+        if ((s.iniChi - s.currentChi) * 1e3 < s.iniChi)
+          s.nBad++;
+        else
+          s.nBad = 0;
+        if (s.nBad >= 3) ok = false;
+      }
+      if (s.chk < lastTrialChi && s.iter > 0) ok = false;
+      s.chk = lastTrialChi;
+      s.it_done[s.round] = s.iter + 1;
+      s.iter++;
+      s.qmax = 0;
+      s.need_lin = 1;
+      if (!ok || s.iter == (s.round == 0 ? 5 : 10)) round_end = 1;
+    }
+    if (round_end && s.round == 1) {
+      s.done = 1;
+      round_end = 0;
+    }
+    s_round_end = round_end;
+  }
+  __syncthreads();
+  if (!s_round_end) return;
+  // ---- round 2: the observations that fail the inlier test on the last computed errors (or sit
+  // behind the camera) set aside (level 1), every kernel dropped, the solver's x reset
+  const int cb = stp->cb;
+  const Cam cam = ba_cam(d);
+  (void)cam;
+  const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
+  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
+  for (int e = tid; e < d.n_edge; e += NT) {
+    const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
+    const double chi = edge_chi2(&w.err[3 * (size_t)e], (double)d.e_s[e], stereo);
+    double pc[3];
+    se3_map(pose[d.e_kf[e]], &Xc[3 * (size_t)d.e_pt[e]], pc);
+    if (chi > (stereo ? 7.815 : 5.991) || !(pc[2] > 0.0)) w.level[e] = 1;
+  }
+  for (int k = tid; k < d.n_kf; k += NT) w.kf_act[k] = 0;
+  const size_t n6 = 6 * (size_t)d.n_opt;
+  for (size_t q = tid; q < n6 + 3 * (size_t)d.n_pt; q += NT) w.x[q] = 0;
+  __syncthreads();
+  int nact = 0;
+  for (int j = tid; j < d.n_pt; j += NT) {
+    uint8_t a = 0;
+    for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++)
+      if (w.level[e] == 0) {
+        a = 1;
+        if (d.opt_of[d.e_kf[e]] >= 0) w.kf_act[d.e_kf[e]] = 1;  // every writer stores 1
+      }
+    w.pt_act[j] = a;
+    nact += a;
+  }
+  double na = wave_sum_dpp((double)nact);
+  if ((tid & 63) == 0) s_part[tid >> 6] = na;
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0;
+    for (int q = 0; q < NT / 64; q++) t += s_part[q];
+    BAState& s = *stp;
+    s.round = 1;
+    s.spec_ok = 0;
+    s.iter = 0;
+    s.qmax = 0;
+    s.need_lin = 1;
+    s.lam_init = 1;
+    s.lambda = 0;
+    s.ni = 2;
+    s.chk = 0;
+    s.nBad = 0;
+    s.nact = (int)t;
+    if (t == 0) s.done = 1;
+  }
+}
+
 // trial step 4, one thread per point: x_l = D^-1 (b_l - H_pl^T x_p) (stale on a failed solve),
 // the trial point, the errors of its active edges at the trial state, chi2 and the scale term
 // SPEC (MMT_BA_SPEC=1): also linearise at the trial state, so an accepted trial needs no
@@ -1363,6 +1496,7 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
 template <bool SPEC>
 __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
   __shared__ double s_part[2 * kMkWaves];
+  __shared__ int s_last;
   const BAState* st = w.st;
   if (st->done) return;
   const int cb = st->cb, nb = 1 - cb;
@@ -1445,136 +1579,18 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
     }
     w.p4part[2 * blockIdx.x] = t0;
     w.p4part[2 * blockIdx.x + 1] = t1;
-  }
-}
-
-// trial step 5, one workgroup: OptimizationAlgorithmLevenberg::solve's decision for the trial,
-// the end of the iteration (SparseOptimizer::optimize's stops), the switch to the second round
-// (the inlier check of Optimizer.cc:3559-3590 on the last computed errors) and the end of the solve
-__global__ __launch_bounds__(kMkDecideThreads) void k_ba2_p5(BADesc d, BAWork2 w) {
-  __shared__ int s_round_end;
-  __shared__ double s_part[kMkDecideThreads / 64];
-  __shared__ double s_sum[2];
-  BAState* stp = w.st;
-  if (stp->done) return;
-  const int tid = threadIdx.x;
-  if (tid < 64) {  // the trial's chi2 and scale over the point workgroups (wave 0, fixed order)
-    double a = 0, b = 0;
-    for (int g = tid; g < w.gP; g += 64) {
-      a += w.p4part[2 * g];
-      b += w.p4part[2 * g + 1];
-    }
-    a = wave_sum_dpp(a);
-    b = wave_sum_dpp(b);
-    if (tid == 0) {
-      s_sum[0] = a;
-      s_sum[1] = b;
-    }
+    // the last workgroup to finish takes the trial's decision (k_ba2_p5's work, one launch fewer
+    // per trial): its partials published by an agent-scope release, the count, and the last
+    // one's acquire before it reads every partial
+    __threadfence();
+    const unsigned done = atomicAdd(w.p4cnt, 1u);
+    s_last = done == (unsigned)gridDim.x - 1;
+    if (s_last) __threadfence();
   }
   __syncthreads();
-  if (tid == 0) {
-    BAState& s = *stp;
-    const double tc = s_sum[0], sc = s_sum[1];
-    double tempChi = tc;
-    const double lastTrialChi = tempChi;
-    if (!s.ok2) tempChi = DBL_MAX;
-    double scale = s.scale_p + sc;
-    double rho = s.currentChi - tempChi;
-    scale += 1e-3;
-    rho /= scale;
-    if (rho > 0 && isfinite(tempChi)) {
-      double alpha = 1. - pow((2 * rho - 1), 3);
-      alpha = fmin(alpha, 2. / 3.);
-      s.lambda *= fmax(1. / 3., alpha);
-      s.ni = 2;
-      s.currentChi = tempChi;
-      s.cb = 1 - s.cb;  // the trial (and its linearisation, with SPEC) becomes the current estimate
-      s.spec_ok = w.spec;
-    } else {
-      s.lambda *= s.ni;
-      s.ni *= 2;
-      s.spec_ok = 0;
-    }
-    s.qmax++;
-    s.trials[s.round]++;
-    int round_end = 0;
-    if (rho < 0 && s.qmax < 10) {
-      s.need_lin = 0;  // another trial of this iteration
-    } else {
-      bool ok = true;
-      if (s.qmax == 10 || rho == 0) ok = false;
-      if (ok) {
-        if ((s.iniChi - s.currentChi) * 1e3 < s.iniChi)
-          s.nBad++;
-        else
-          s.nBad = 0;
-        if (s.nBad >= 3) ok = false;
-      }
-      if (s.chk < lastTrialChi && s.iter > 0) ok = false;
-      s.chk = lastTrialChi;
-      s.it_done[s.round] = s.iter + 1;
-      s.iter++;
-      s.qmax = 0;
-      s.need_lin = 1;
-      if (!ok || s.iter == (s.round == 0 ? 5 : 10)) round_end = 1;
-    }
-    if (round_end && s.round == 1) {
-      s.done = 1;
-      round_end = 0;
-    }
-    s_round_end = round_end;
-  }
-  __syncthreads();
-  if (!s_round_end) return;
-  // ---- round 2: the observations that fail the inlier test on the last computed errors (or sit
-  // behind the camera) set aside (level 1), every kernel dropped, the solver's x reset
-  const int cb = stp->cb;
-  const Cam cam = ba_cam(d);
-  (void)cam;
-  const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
-  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
-  for (int e = tid; e < d.n_edge; e += kMkDecideThreads) {
-    const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
-    const double chi = edge_chi2(&w.err[3 * (size_t)e], (double)d.e_s[e], stereo);
-    double pc[3];
-    se3_map(pose[d.e_kf[e]], &Xc[3 * (size_t)d.e_pt[e]], pc);
-    if (chi > (stereo ? 7.815 : 5.991) || !(pc[2] > 0.0)) w.level[e] = 1;
-  }
-  for (int k = tid; k < d.n_kf; k += kMkDecideThreads) w.kf_act[k] = 0;
-  const size_t n6 = 6 * (size_t)d.n_opt;
-  for (size_t q = tid; q < n6 + 3 * (size_t)d.n_pt; q += kMkDecideThreads) w.x[q] = 0;
-  __syncthreads();
-  int nact = 0;
-  for (int j = tid; j < d.n_pt; j += kMkDecideThreads) {
-    uint8_t a = 0;
-    for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++)
-      if (w.level[e] == 0) {
-        a = 1;
-        if (d.opt_of[d.e_kf[e]] >= 0) w.kf_act[d.e_kf[e]] = 1;  // every writer stores 1
-      }
-    w.pt_act[j] = a;
-    nact += a;
-  }
-  double na = wave_sum_dpp((double)nact);
-  if ((tid & 63) == 0) s_part[tid >> 6] = na;
-  __syncthreads();
-  if (tid == 0) {
-    double t = 0;
-    for (int q = 0; q < kMkDecideThreads / 64; q++) t += s_part[q];
-    BAState& s = *stp;
-    s.round = 1;
-    s.spec_ok = 0;
-    s.iter = 0;
-    s.qmax = 0;
-    s.need_lin = 1;
-    s.lam_init = 1;
-    s.lambda = 0;
-    s.ni = 2;
-    s.chk = 0;
-    s.nBad = 0;
-    s.nact = (int)t;
-    if (t == 0) s.done = 1;
-  }
+  if (!s_last) return;
+  ba2_decide<kMkThreads>(d, w);
+  if (threadIdx.x == 0) *w.p4cnt = 0;
 }
 
 // the erase test (Optimizer.cc:3603-3631) and the recovered estimates
@@ -1630,7 +1646,7 @@ size_t ba2_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt, int n_blk,
          a(8 * 18 * (size_t)n_edge) + a(8 * 6 * (size_t)n_edge) + a(8 * 36 * (size_t)n_opt) +
          a(8 * 6 * (size_t)n_opt) + a(8 * 6 * (size_t)n_opt) + a(8 * 36 * (size_t)n_blk) +
          a(8 * (n6 + 3 * (size_t)n_pt)) + a(8 * n6 * n6) + a(8 * 3 * n6) + 2 * a(8 * 2 * (size_t)gP) +
-         a((size_t)n_edge) + a(4 * (size_t)n_edge) + a((size_t)n_kf) + a((size_t)n_pt) + 64;
+         a((size_t)n_edge) + a(4 * (size_t)n_edge) + a((size_t)n_kf) + a((size_t)n_pt) + a(16) + 64;
 }
 
 void launch_local_ba(const BADesc& d, hipStream_t st) {
@@ -1864,6 +1880,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.vec = (double*)take(8 * 3 * (size_t)n6);
     w.linpart = (double*)take(8 * 2 * (size_t)gP);
     w.p4part = (double*)take(8 * 2 * (size_t)gP);
+    w.p4cnt = (unsigned*)take(16);
     w.level = take((size_t)nE);
     w.eopt = (int*)take(4 * (size_t)nE);
     w.kf_act = take((size_t)nK);
@@ -1878,7 +1895,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     double t_launch = 0, t_wait = 0;
     hipLaunchKernelGGL(k_ba2_init, dim3(gP), dim3(kMkThreads), 0, st, d, w);
     MMT_HIP(hipGetLastError());
-    // A trial is at most 7 launches; a solve at most 5 x 10 + 10 x 10 trials.  The first batch
+    // A trial is at most 6 launches; a solve at most 5 x 10 + 10 x 10 trials.  The first batch
     // covers a typical solve (about 15 trials on the C3 sequence), later ones are short.
     int slots = 0;
     for (bool done = nE == 0; !done;) {
@@ -1896,7 +1913,6 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
           hipLaunchKernelGGL(k_ba2_p4<true>, dim3(gP), dim3(kMkThreads), 0, st, d, w);
         else
           hipLaunchKernelGGL(k_ba2_p4<false>, dim3(gP), dim3(kMkThreads), 0, st, d, w);
-        hipLaunchKernelGGL(k_ba2_p5, dim3(1), dim3(kMkDecideThreads), 0, st, d, w);
       }
       MMT_HIP(hipGetLastError());
       slots += batch;

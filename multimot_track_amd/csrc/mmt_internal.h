@@ -128,6 +128,10 @@ class OrbEngine {
   std::vector<int> xtab_off_, ytab_off_;
   std::vector<int> rs_pitch_, rs_lds_;  // k_resize LDS row pitch and bytes per level
   int sched_ = 0;  // MMT_ORB_SCHED=2: one stream (standalone kernel times for profiling)
+  // FAST cells per wave (MMT_FAST_CPW, default 1): with more, each wave's next tile loads are in
+  // flight during its current cell; measured 0.918 / 0.928 / 0.940 / 0.951 ms per 128-frame window
+  // at 1 / 2 / 4 / 8 (round 5), so one cell per wave stays the default
+  int fast_cpw_ = 1;
   LevelInfo* d_lv_ = nullptr;
   CellInfo* d_cells_ = nullptr;
   ResizeX* d_xtab_ = nullptr;

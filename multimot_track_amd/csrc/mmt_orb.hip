@@ -314,12 +314,76 @@ __host__ __device__ constexpr int fast_wave_lds(int kFS, int rows_max, int win_m
   return ((2 * rows_max * kFS + 2 * win_max) + 15) & ~15;
 }
 
-// One wave per (cell, frame); four cells per workgroup.  Cell = the submatrix the reference hands
-// to cv::FAST (ORBextractor.cc:791-816).  The wave stages the cell in its own LDS tile (row
-// stride kFS, tile column c at LDS column c + 1 so the detection window starts on a dword) and
-// keeps an arc-strength map of the same shape, zero except at the candidates of the current
-// pass, so out-of-window NMS neighbours read 0 without bounds checks.  Per threshold (iniTh,
-// then minTh if the cell came out empty, ORBextractor.cc:809-816):
+// Lane -> (row offset rsub, dword q) map of a cell's tile copy: one dword per lane per step, every
+// step rps rows down, so the addresses advance by uniform strides (no per-item division and no
+// quarter-rate 32-bit multiply).  src starts one byte before the tile (c0 >= 16; the pyramid
+// allocation has slack for the <= 3 bytes read past the last row).
+struct FastTileMap {
+  const uint8_t* src;
+  size_t sstep;
+  int rps, rsub, q, act;  // act: the lane copies (an int: no padding bytes to move on a copy)
+};
+
+__device__ __forceinline__ FastTileMap fast_tile_map(const CellInfo& c, const LevelInfo& L,
+                                                     const uint8_t* fbase, int lane) {
+  FastTileMap m;
+  const int nq = (c.cols + 4) >> 2;  // dwords per LDS row (tile shifted by 1)
+  const float inv_nq = 1.0f / (float)nq;
+  m.rps = __builtin_amdgcn_readfirstlane(div_small(64, inv_nq));  // rows per step
+  m.rsub = div_small(lane, inv_nq);
+  m.q = lane - (int)__umul24((unsigned)m.rsub, (unsigned)nq);
+  m.act = m.rsub < m.rps;
+  m.src = fbase + L.off + (size_t)c.r0 * L.w + c.c0 - 1 + 4 * m.q +
+          __umul24((unsigned)m.rsub, (unsigned)L.w);
+  m.sstep = (size_t)m.rps * L.w;
+  return m;
+}
+
+constexpr int kFastStage = 6;  // tile row steps held in registers (36 rows of a <= 40-byte-wide tile)
+
+__device__ __forceinline__ void fast_tile_fetch(const FastTileMap& m, int rows,
+                                                uint32_t (&v)[kFastStage]) {
+  const uint8_t* sp = m.src;
+#pragma unroll
+  for (int k = 0; k < kFastStage; k++, sp += m.sstep)
+    if (m.act && m.rsub + k * m.rps < rows) v[k] = ldg32(sp);
+}
+
+template <int kFS>
+__device__ __forceinline__ void fast_tile_store(const FastTileMap& m, int rows,
+                                                const uint32_t (&v)[kFastStage], uint8_t* tile) {
+  uint8_t* lp = tile + m.rsub * kFS + 4 * m.q;
+  const int lstep = m.rps * kFS;
+#pragma unroll
+  for (int k = 0; k < kFastStage; k++, lp += lstep)
+    if (m.act && m.rsub + k * m.rps < rows) *(uint32_t*)lp = v[k];
+  // rows past the register stage (tall cells of wide tiles): copied here, synchronously
+  const uint8_t* sp = m.src + kFastStage * m.sstep;
+  for (int r = m.rsub + kFastStage * m.rps; m.act && r < rows; r += m.rps, sp += m.sstep, lp += lstep)
+    *(uint32_t*)lp = ldg32(sp);
+}
+
+// Workgroup -> (cell group, frame): the hardware deals consecutive workgroups to the 8 XCDs in
+// turn; this gives each XCD a contiguous run of (frame, cell group) jobs instead, so cells that
+// share halo rows (vertical neighbours of one frame) meet in the same L2.
+__device__ __forceinline__ void fast_job(int& xg, int& frame) {
+  const int gx = gridDim.x, total = gx * gridDim.y;
+  const int lin = blockIdx.y * gx + blockIdx.x;
+  int j = lin;
+  if ((total & 7) == 0) j = (lin & 7) * (total >> 3) + (lin >> 3);
+  frame = j / gx;
+  xg = j - frame * gx;
+}
+
+// One wave per cell at a time, four waves per workgroup; the grid's waves walk the cells of
+// [cell_begin, cell_end) with a stride of one grid round (one cell per wave by default,
+// MMT_FAST_CPW for more).  Cell = the submatrix the reference hands to cv::FAST (ORBextractor.cc:791-816).
+// The wave stages the cell in its own LDS tile (row stride kFS, tile column c at LDS column c + 1
+// so the detection window starts on a dword) and keeps an arc-strength map of the same shape, zero
+// except at the candidates of the current pass, so out-of-window NMS neighbours read 0 without
+// bounds checks.  With several cells per wave, the next cell's record and tile loads are issued
+// before the current cell's passes and land in registers meanwhile.
+// Per threshold (iniTh, then minTh if the cell came out empty, ORBextractor.cc:809-816):
 //  1) compass pre-test at th over the window, four pixels per lane (one aligned dword of the
 //     window row, packed u16 arithmetic): a 9-arc covers two adjacent compass points (0/4/8/12),
 //     so a pixel whose pairs all fail has M <= th and is no corner; survivors are compacted in
@@ -346,163 +410,157 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, s
   const int lane = threadIdx.x & 63;
   // wave-uniform (readfirstlane): the cell record and everything derived from it live in SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int cell = cell_begin + blockIdx.x * 4 + wave;
+  int xg, frame;
+  fast_job(xg, frame);
+  const int cstep = gridDim.x * 4;
+  int cell = cell_begin + xg * 4 + wave;
   if (cell >= cell_end) return;
   uint8_t* tile = fast_lds + wave * fast_wave_lds(kFS, rows_max, win_max);
   uint8_t* arcm = tile + rows_max * kFS;
   uint16_t* cand_list = (uint16_t*)(arcm + rows_max * kFS);
-  const CellInfo ci = cells[cell];
-  const int frame = blockIdx.y;
-  const LevelInfo L = lv[ci.level];
-  const uint8_t* img = pyr + (size_t)frame * pyr_stride + L.off;
-  const int rows = ci.rows, nq = (ci.cols + 4) >> 2;  // dwords per LDS row (tile shifted by 1)
-  {
-    // dword copy from one byte before the tile (c0 >= 16; the pyramid allocation has slack for
-    // the <= 3 bytes read past the last row).  Lane -> (row offset rsub, dword q) is fixed and
-    // every step moves rps rows down, so the addresses advance by uniform strides: no per-item
-    // division and no quarter-rate 32-bit multiply.  Every load of the first kStage steps is
-    // issued before the first LDS store.
-    const float inv_nq = 1.0f / (float)nq;
-    const int rps = __builtin_amdgcn_readfirstlane(div_small(64, inv_nq));  // rows per step
-    const int rsub = div_small(lane, inv_nq);
-    const int q = lane - (int)__umul24((unsigned)rsub, (unsigned)nq);
-    const bool act = rsub < rps;
-    const uint8_t* src = img + (size_t)ci.r0 * L.w + ci.c0 - 1 + 4 * q +
-                         __umul24((unsigned)rsub, (unsigned)L.w);
-    const size_t sstep = (size_t)rps * L.w;
-    const int lstep = rps * kFS;
-    uint8_t* ldst = tile + rsub * kFS + 4 * q;
-    constexpr int kStage = 8;
-    uint32_t v[kStage];
-    const uint8_t* sp = src;
-#pragma unroll
-    for (int k = 0; k < kStage; k++, sp += sstep)
-      if (act && rsub + k * rps < rows) v[k] = ldg32(sp);
-    uint8_t* lp = ldst;
-#pragma unroll
-    for (int k = 0; k < kStage; k++, lp += lstep)
-      if (act && rsub + k * rps < rows) *(uint32_t*)lp = v[k];
-    for (int r = rsub + kStage * rps; act && r < rows; r += rps, sp += sstep, lp += lstep)
-      *(uint32_t*)lp = ldg32(sp);
-    for (int i = lane; i < rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
-  }
-  wave_sync();
-  FP_T(0);
-  const int R = rows - 6, C = ci.cols - 6;  // detection window: tile rows 3..R+2, cols 3..C+2
-  // pre-test lane mapping: gs groups of four pixels per row (power of two), 64 / gs rows per step
-  const int G = (C + 3) >> 2, lgg = G <= 8 ? 3 : 4;
-  const int grp = lane & ((1 << lgg) - 1), rsub = lane >> lgg, rstep = 64 >> lgg;
-  const int nvalid = C - 4 * grp;  // window pixels of this lane's group
-  const uint32_t colmask = grp < G ? (nvalid >= 4 ? 0xFu : (1u << nvalid) - 1u) : 0u;
+  const uint8_t* fbase = pyr + (size_t)frame * pyr_stride;
   const uint32_t* t32 = (const uint32_t*)tile;
   constexpr int kRow32 = kFS / 4;  // dwords per LDS row
-  uint32_t* out = keys + (size_t)frame * total_slots + ci.slot_off;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  int count = 0, ncand = 0;
-  for (int pass = 0; pass < 2; pass++) {
-    const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
-    const uint32_t th2 = (uint32_t)th | ((uint32_t)th << 16);
-    if (pass && minTh > iniTh) {  // pass 0's candidates are then no subset of pass 1's
-      for (int i = lane; i < rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
-      wave_sync();
+  CellInfo ci = cells[cell];
+  FastTileMap tm = fast_tile_map(ci, lv[ci.level], fbase, lane);
+  uint32_t v[kFastStage];
+  fast_tile_fetch(tm, ci.rows, v);
+  for (;;) {
+    fast_tile_store<kFS>(tm, ci.rows, v, tile);
+    for (int i = lane; i < ci.rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
+    wave_sync();
+    // the next cell's record and tile: in flight during this cell's passes
+    const int next = cell + cstep;
+    const bool more = next < cell_end;
+    CellInfo cn = ci;
+    FastTileMap tn = tm;
+    if (more) {
+      cn = cells[next];
+      tn = fast_tile_map(cn, lv[cn.level], fbase, lane);
+      fast_tile_fetch(tn, cn.rows, v);
     }
-    // (with minTh <= iniTh, pass 0's candidates are pass 1's too and their arc strengths, which
-    // do not depend on the threshold, stay valid in the map)
-    ncand = 0;
-    // two wave steps per iteration: the ten dword reads of both are in flight together
-    for (int r0 = 0; r0 < R; r0 += 2 * rstep) {
-      uint32_t m[2];
-      int base[2];
+    FP_T(0);
+    const int R = ci.rows - 6, C = ci.cols - 6;  // detection window: tile rows 3..R+2, cols 3..C+2
+    // pre-test lane mapping: gs groups of four pixels per row (power of two), 64 / gs rows per step
+    const int G = (C + 3) >> 2, lgg = G <= 8 ? 3 : 4;
+    const int grp = lane & ((1 << lgg) - 1), rsub = lane >> lgg, rstep = 64 >> lgg;
+    const int nvalid = C - 4 * grp;  // window pixels of this lane's group
+    const uint32_t colmask = grp < G ? (nvalid >= 4 ? 0xFu : (1u << nvalid) - 1u) : 0u;
+    uint32_t* out = keys + (size_t)frame * total_slots + ci.slot_off;
+    int count = 0, ncand = 0;
+    for (int pass = 0; pass < 2; pass++) {
+      const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
+      const uint32_t th2 = (uint32_t)th | ((uint32_t)th << 16);
+      if (pass && minTh > iniTh) {  // pass 0's candidates are then no subset of pass 1's
+        for (int i = lane; i < ci.rows * (kFS / 4); i += 64) *(uint32_t*)(arcm + 4 * i) = 0u;
+        wave_sync();
+      }
+      // (with minTh <= iniTh, pass 0's candidates are pass 1's too and their arc strengths, which
+      // do not depend on the threshold, stay valid in the map)
+      ncand = 0;
+      // two wave steps per iteration: the ten dword reads of both are in flight together
+      for (int r0 = 0; r0 < R; r0 += 2 * rstep) {
+        uint32_t m[2];
+        int base[2];
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
-        const int wr = r0 + u * rstep + rsub;
-        base[u] = (wr + 3) * kRow32 + 1 + grp;  // dword of window pixels 4 grp .. 4 grp + 3
-        m[u] = 0;
-        if (wr < R && colmask) {
-          const int bb = base[u];
-          const uint32_t c = t32[bb], cp = t32[bb - 1], cn = t32[bb + 1];
-          const uint32_t up = t32[bb - 3 * kRow32], dn = t32[bb + 3 * kRow32];
-          m[u] = compass4(c, dn, __builtin_amdgcn_alignbyte(cn, c, 3), up,
-                          __builtin_amdgcn_alignbyte(c, cp, 1), th2) & colmask;
+        for (int u = 0; u < 2; u++) {
+          const int wr = r0 + u * rstep + rsub;
+          base[u] = (wr + 3) * kRow32 + 1 + grp;  // dword of window pixels 4 grp .. 4 grp + 3
+          m[u] = 0;
+          if (wr < R && colmask) {
+            const int bb = base[u];
+            const uint32_t c = t32[bb], cp = t32[bb - 1], cn4 = t32[bb + 1];
+            const uint32_t up = t32[bb - 3 * kRow32], dn = t32[bb + 3 * kRow32];
+            m[u] = compass4(c, dn, __builtin_amdgcn_alignbyte(cn4, c, 3), up,
+                            __builtin_amdgcn_alignbyte(c, cp, 1), th2) & colmask;
+          }
+        }
+        // candidates of step 0 precede those of step 1 (row-major): one scan of n0 + (n1 << 16)
+        const int n0 = __popc(m[0]), n1 = __popc(m[1]);
+        const int incl = wave_incl_scan(n0 | (n1 << 16));
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        int slot0 = ncand + (incl & 0xFFFF) - n0;
+        int slot1 = ncand + (tot & 0xFFFF) + (incl >> 16) - n1;
+        ncand += (tot & 0xFFFF) + (tot >> 16);
+        uint32_t ma = m[0], mb = m[1];
+        while (ma) {
+          cand_list[slot0++] = (uint16_t)(4 * base[0] + __builtin_ctz(ma));
+          ma &= ma - 1;
+        }
+        while (mb) {
+          cand_list[slot1++] = (uint16_t)(4 * base[1] + __builtin_ctz(mb));
+          mb &= mb - 1;
         }
       }
-      // candidates of step 0 precede those of step 1 (row-major): one scan of n0 + (n1 << 16)
-      const int n0 = __popc(m[0]), n1 = __popc(m[1]);
-      const int incl = wave_incl_scan(n0 | (n1 << 16));
-      const int tot = __builtin_amdgcn_readlane(incl, 63);
-      int slot0 = ncand + (incl & 0xFFFF) - n0;
-      int slot1 = ncand + (tot & 0xFFFF) + (incl >> 16) - n1;
-      ncand += (tot & 0xFFFF) + (tot >> 16);
-      uint32_t ma = m[0], mb = m[1];
-      while (ma) {
-        cand_list[slot0++] = (uint16_t)(4 * base[0] + __builtin_ctz(ma));
-        ma &= ma - 1;
+      wave_sync();
+      FP_T(1 + 3 * pass);
+      // arc strengths into the map; corners (M > th) are compacted in place at the front of the
+      // candidate list (a write never passes the iteration's reads), keeping row-major order
+      int ncorner = 0;
+      for (int k0 = 0; k0 < ncand; k0 += 64) {
+        const int k = k0 + lane;
+        int p = 0, mm = 0;
+        if (k < ncand) {
+          p = cand_list[k];
+          mm = arc_strength<kFS>(tile + p);
+          arcm[p] = (uint8_t)(mm < 0 ? 0 : mm);
+        }
+        const bool corner = k < ncand && mm > th;
+        const unsigned long long bc = __ballot(corner);
+        if (corner) cand_list[ncorner + __popcll(bc & lt)] = (uint16_t)p;
+        ncorner += __popcll(bc);
       }
-      while (mb) {
-        cand_list[slot1++] = (uint16_t)(4 * base[1] + __builtin_ctz(mb));
-        mb &= mb - 1;
-      }
-    }
-    wave_sync();
-    FP_T(1 + 3 * pass);
-    // arc strengths into the map; corners (M > th) are compacted in place at the front of the
-    // candidate list (a write never passes the iteration's reads), keeping row-major order
-    int ncorner = 0;
-    for (int k0 = 0; k0 < ncand; k0 += 64) {
-      const int k = k0 + lane;
-      int p = 0, mm = 0;
-      if (k < ncand) {
-        p = cand_list[k];
-        mm = arc_strength<kFS>(tile + p);
-        arcm[p] = (uint8_t)(mm < 0 ? 0 : mm);
-      }
-      const bool corner = k < ncand && mm > th;
-      const unsigned long long bc = __ballot(corner);
-      if (corner) cand_list[ncorner + __popcll(bc & lt)] = (uint16_t)p;
-      ncorner += __popcll(bc);
-    }
-    wave_sync();
-    FP_T(2 + 3 * pass);
-    int base = 0;
-    for (int k0 = 0; k0 < ncorner; k0 += 64) {  // cell-local 3x3 NMS over the corners
-      const int k = k0 + lane;
-      bool keep = false;
-      int sc = 0, p = 0;
-      if (k < ncorner) {
-        p = cand_list[k];
-        const uint8_t* a = arcm + p;
-        sc = a[0] - 1;
-        const int n8[8] = {a[-kFS - 1], a[-kFS], a[-kFS + 1], a[-1],
-                           a[1],        a[kFS - 1], a[kFS], a[kFS + 1]};
-        int nmax = 0;
+      wave_sync();
+      FP_T(2 + 3 * pass);
+      int base = 0;
+      for (int k0 = 0; k0 < ncorner; k0 += 64) {  // cell-local 3x3 NMS over the corners
+        const int k = k0 + lane;
+        bool keep = false;
+        int sc = 0, p = 0;
+        if (k < ncorner) {
+          p = cand_list[k];
+          const uint8_t* a = arcm + p;
+          sc = a[0] - 1;
+          const int n8[8] = {a[-kFS - 1], a[-kFS], a[-kFS + 1], a[-1],
+                             a[1],        a[kFS - 1], a[kFS], a[kFS + 1]};
+          int nmax = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) nmax = max(nmax, n8[j] > th ? n8[j] - 1 : 0);
-        keep = sc > nmax;
+          for (int j = 0; j < 8; j++) nmax = max(nmax, n8[j] > th ? n8[j] - 1 : 0);
+          keep = sc > nmax;
+        }
+        const unsigned long long bal = __ballot(keep);
+        if (keep) {
+          const int tr = p / kFS, tc = p - tr * kFS - 1;  // LDS column = tile column + 1
+          const uint32_t x = (uint32_t)(ci.c0 - kMinBorder + tc);
+          const uint32_t y = (uint32_t)(ci.r0 - kMinBorder + tr);
+          const int slot = base + __popcll(bal & lt);
+          if (slot < ci.slot_cap) out[slot] = (y << 20) | (x << 8) | (uint32_t)sc;
+        }
+        base += __popcll(bal);
       }
-      const unsigned long long bal = __ballot(keep);
-      if (keep) {
-        const int tr = p / kFS, tc = p - tr * kFS - 1;  // LDS column = tile column + 1
-        const uint32_t x = (uint32_t)(ci.c0 - kMinBorder + tc);
-        const uint32_t y = (uint32_t)(ci.r0 - kMinBorder + tr);
-        const int slot = base + __popcll(bal & lt);
-        if (slot < ci.slot_cap) out[slot] = (y << 20) | (x << 8) | (uint32_t)sc;
-      }
-      base += __popcll(bal);
+      count = base;
+      FP_T(3 + 3 * pass);
+#ifdef MMT_FAST_PROFILE
+      fp[7] = ncand;
+#endif
+      if (count > 0) break;
+      wave_sync();
     }
-    count = base;
-    FP_T(3 + 3 * pass);
 #ifdef MMT_FAST_PROFILE
-    fp[7] = ncand;
+    if (lane == 0 && frame == 0 && cell % 37 == 0)
+      printf("fastprof cell %d lvl %d: copy %lld pre %lld arc %lld nms %lld | pass2 pre %lld arc %lld nms %lld | ncand %lld cnt %d\n",
+             cell, ci.level, fp[0], fp[1], fp[2], fp[3], fp[4], fp[5], fp[6], fp[7], count);
+    for (int k = 0; k < 8; k++) fp[k] = 0;
 #endif
-    if (count > 0) break;
+    if (lane == 0) cellcnt[(size_t)frame * ncells + cell] = min(count, ci.slot_cap);
+    if (!more) break;
+    // every lane is done with this cell's tile, map and candidates before the next store
     wave_sync();
+    cell = next;
+    ci = cn;
+    tm = tn;
   }
-#ifdef MMT_FAST_PROFILE
-  if (lane == 0 && frame == 0 && cell % 37 == 0)
-    printf("fastprof cell %d lvl %d: copy %lld pre %lld arc %lld nms %lld | pass2 pre %lld arc %lld nms %lld | ncand %lld cnt %d\n",
-           cell, ci.level, fp[0], fp[1], fp[2], fp[3], fp[4], fp[5], fp[6], fp[7], count);
-#endif
-  if (lane == 0) cellcnt[(size_t)frame * ncells + cell] = min(count, ci.slot_cap);
 }
 
 // ---------------------------------------------------------------- octree helpers
@@ -1171,8 +1229,8 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 // columns and walks the band: per row it loads the twelve source bytes around its columns as
 // three (unaligned) dwords, forms the four 7-tap horizontal sums with byte-aligned extracts and
 // two v_dot4_u32_u8 each, keeps the last seven rows of sums in a register ring (rows unrolled by
-// seven, so the ring never moves), and stores its four outputs as one dword.  No LDS, no
-// barriers.  Lanes whose columns touch the level edge gather their bytes with REFLECT_101.
+// seven, so the ring never moves), and stores its four outputs as one dword.  Source rows are
+// loaded seven rows ahead into a register ring of their own.  No LDS, no barriers.  Lanes whose columns touch the level edge gather their bytes with REFLECT_101.
 #ifndef MMT_BLUR_BAND
 #define MMT_BLUR_BAND 32
 #endif
@@ -1202,10 +1260,13 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
   const size_t fo = (size_t)blockIdx.y * pyr_stride + L.off;
   const uint8_t* img = pyr + fo;
   uint8_t* dst = blur + fo;
-  const int x = t.x0 + 4 * lane;  // first of this lane's four columns
-  if (x >= L.w) return;
+  // first of this lane's four columns; the lane that would hold the row's last 1-3 columns takes
+  // the last four instead (it rewrites 1-3 outputs of its neighbour with the same values), so every
+  // lane stores one dword and no store sits on a divergent path (levels are >= 62 columns wide)
+  const int xl = t.x0 + 4 * lane;
+  if (xl >= L.w) return;
+  const int x = min(xl, L.w - 4);
   const int y_end = min(t.y0 + kBlurBand, L.h);
-  const int ncols = min(4, L.w - x);
   const bool edge = x < 4 || x + 8 > L.w;  // the 12 loaded bytes x-4 .. x+7 leave the row
   // Every lane loads three dwords at `base`; edge lanes then pick their REFLECT_101 bytes out of
   // those 12 with v_perm (all reflected positions lie inside [base, base + 12)).
@@ -1221,18 +1282,21 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
       selB[k >> 2] |= b << (8 * (k & 3));
     }
   }
-  auto load_row = [&](int r, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
+  // raw row load (three aligned-or-clamped dwords at `base`); edge lanes pick their REFLECT_101
+  // bytes when the row is consumed, so no instruction waits on a load at issue time
+  auto load_row = [&](int r, uint32_t (&d)[3]) {
     const int sy = reflect101(min(r, L.h + 2), L.h);
     const uint8_t* srow = img + (size_t)sy * L.w + base;
-    const uint32_t s0 = ld32(srow), s1 = ld32(srow + 4), s2 = ld32(srow + 8);
-    if (!edge) {
-      d0 = s0;
-      d1 = s1;
-      d2 = s2;
-    } else {
-      d0 = __builtin_amdgcn_perm(s1, s0, selA[0]) | __builtin_amdgcn_perm(s2, s2, selB[0]);
-      d1 = __builtin_amdgcn_perm(s1, s0, selA[1]) | __builtin_amdgcn_perm(s2, s2, selB[1]);
-      d2 = __builtin_amdgcn_perm(s1, s0, selA[2]) | __builtin_amdgcn_perm(s2, s2, selB[2]);
+    d[0] = ld32(srow);
+    d[1] = ld32(srow + 4);
+    d[2] = ld32(srow + 8);
+  };
+  auto fix_row = [&](uint32_t (&d)[3]) {
+    if (edge) {
+      const uint32_t s0 = d[0], s1 = d[1], s2 = d[2];
+      d[0] = __builtin_amdgcn_perm(s1, s0, selA[0]) | __builtin_amdgcn_perm(s2, s2, selB[0]);
+      d[1] = __builtin_amdgcn_perm(s1, s0, selA[1]) | __builtin_amdgcn_perm(s2, s2, selB[1]);
+      d[2] = __builtin_amdgcn_perm(s1, s0, selA[2]) | __builtin_amdgcn_perm(s2, s2, selB[2]);
     }
   };
   // Horizontal sums w (<= 256 * 255) go into a 7-row ring as floats, two columns per packed
@@ -1248,50 +1312,67 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
   const f2x t2 = {(float)T2, (float)T2}, t3 = {(float)T3, (float)T3};
   const f2x sc = {1.0f / 65536.0f, 1.0f / 65536.0f}, half = {0.5f, 0.5f};
   const int r_end = y_end + 3;
-  int r0 = t.y0 - 3;
-  for (; r0 < r_end; r0 += 7) {
-    uint32_t d[7][3];
+  // Source rows in a 7-slot register ring, loaded seven rows ahead: the load of row r + 7 is
+  // issued as soon as row r has been consumed, so every row's load has six rows of work to hide
+  // behind.  A full band (every band but a level's last) runs as straight-line code with
+  // compile-time row bounds: the compiler's wait counts then stay exact from row to row (any
+  // branch join or loop back edge in between makes it drain every outstanding load); a level's
+  // last band takes the rolled loop.
+  auto row = [&](uint32_t (&dg)[3], int g) {
+    fix_row(dg);
+    // horizontal sums of the four columns -> ring slot g (rows of this group: slots 0..6)
+    uint32_t hs[4];
 #pragma unroll
-    for (int g = 0; g < 7; g++) load_row(min(r0 + g, r_end - 1), d[g][0], d[g][1], d[g][2]);
+    for (int j = 0; j < 4; j++) {
+      const uint32_t a = j < 3 ? __builtin_amdgcn_alignbyte(dg[1], dg[0], 1 + j) : dg[1];
+      const uint32_t bb = j < 3 ? __builtin_amdgcn_alignbyte(dg[2], dg[1], 1 + j) : dg[2];
+      hs[j] = __builtin_amdgcn_udot4(bb, W2, __builtin_amdgcn_udot4(a, W1, 0u, false), false);
+    }
+    w[g][0] = (f2x){(float)hs[0], (float)hs[1]};
+    w[g][1] = (f2x){(float)hs[2], (float)hs[3]};
+  };
+  auto emit = [&](int g, int yo) {
+    // rows yo-3 .. yo+3 live in ring slots g+1 .. g+7 (mod 7)
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      f2x v = t3 * w[(g + 4) % 7][j];
+      v = __builtin_elementwise_fma(t2, w[(g + 3) % 7][j] + w[(g + 5) % 7][j], v);
+      v = __builtin_elementwise_fma(t1, w[(g + 2) % 7][j] + w[(g + 6) % 7][j], v);
+      v = __builtin_elementwise_fma(t0, w[(g + 1) % 7][j] + w[g][j], v);
+      // (v + 32768) >> 16 = floor(v / 65536 + 0.5): both steps exact in float
+      const f2x q = __builtin_elementwise_fma(v, sc, half);
+      o[2 * j] = min((uint32_t)q.x, 255u);
+      o[2 * j + 1] = min((uint32_t)q.y, 255u);
+    }
+    const uint32_t packed = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+    __builtin_memcpy(dst + (size_t)yo * L.w + x, &packed, 4);
+  };
+  uint32_t d[7][3];
+  int r0 = t.y0 - 3;
+  if (y_end - t.y0 == kBlurBand) {
+    constexpr int kRows = kBlurBand + 6;  // source rows of a full band
+#pragma unroll
+    for (int g = 0; g < 7; g++) load_row(r0 + g, d[g]);
+#pragma unroll
+    for (int i = 0; i < kRows; i++) {
+      const int g = i % 7;
+      row(d[g], g);
+      if (i + 7 < kRows) load_row(r0 + i + 7, d[g]);
+      if (i >= 6) emit(g, r0 + i - 3);  // output row yo = r - 3 >= t.y0
+    }
+    return;
+  }
+#pragma unroll
+  for (int g = 0; g < 7; g++) load_row(min(r0 + g, r_end - 1), d[g]);
+  for (; r0 < r_end; r0 += 7) {
 #pragma unroll
     for (int g = 0; g < 7; g++) {
       const int r = r0 + g;
       if (r >= r_end) break;
-      // horizontal sums of the four columns -> ring slot g (rows of this group: slots 0..6)
-      uint32_t hs[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t a = j < 3 ? __builtin_amdgcn_alignbyte(d[g][1], d[g][0], 1 + j) : d[g][1];
-        const uint32_t bb = j < 3 ? __builtin_amdgcn_alignbyte(d[g][2], d[g][1], 1 + j) : d[g][2];
-        hs[j] = __builtin_amdgcn_udot4(bb, W2, __builtin_amdgcn_udot4(a, W1, 0u, false), false);
-      }
-      w[g][0] = (f2x){(float)hs[0], (float)hs[1]};
-      w[g][1] = (f2x){(float)hs[2], (float)hs[3]};
-      const int yo = r - 3;
-      if (yo >= t.y0) {
-        // rows yo-3 .. yo+3 live in ring slots g+1 .. g+7 (mod 7)
-        uint32_t o[4];
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-          f2x v = t3 * w[(g + 4) % 7][j];
-          v = __builtin_elementwise_fma(t2, w[(g + 3) % 7][j] + w[(g + 5) % 7][j], v);
-          v = __builtin_elementwise_fma(t1, w[(g + 2) % 7][j] + w[(g + 6) % 7][j], v);
-          v = __builtin_elementwise_fma(t0, w[(g + 1) % 7][j] + w[g][j], v);
-          // (v + 32768) >> 16 = floor(v / 65536 + 0.5): both steps exact in float
-          const f2x q = __builtin_elementwise_fma(v, sc, half);
-          o[2 * j] = min((uint32_t)q.x, 255u);
-          o[2 * j + 1] = min((uint32_t)q.y, 255u);
-        }
-        uint8_t* dp = dst + (size_t)yo * L.w + x;
-        if (ncols == 4) {
-          const uint32_t packed = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
-          __builtin_memcpy(dp, &packed, 4);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-            if (j < ncols) dp[j] = (uint8_t)o[j];
-        }
-      }
+      row(d[g], g);
+      load_row(min(r + 7, r_end - 1), d[g]);
+      if (r - 3 >= t.y0) emit(g, r - 3);
     }
   }
 }
@@ -1719,6 +1800,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   ncells_ = (int)cells_.size();
   ntiles_ = (int)tiles.size();
   if (const char* e = getenv("MMT_ORB_SCHED")) sched_ = atoi(e);
+  if (const char* e = getenv("MMT_FAST_CPW")) fast_cpw_ = std::max(1, std::min(64, atoi(e)));
   total_slots_ = key_off;
   out_slots_ = out_off;
   cap_frame_ = out_off;
@@ -1859,8 +1941,9 @@ void OrbEngine::run_part(int f0, int nframes, hipStream_t stream, hipStream_t si
   const int fast_lds = 4 * fast_wave_lds(fs, fast_rows_max_, fast_win_max_);
   auto fast = [&](int c0, int c1, hipStream_t st) {
     if (c1 <= c0) return;
+    const int waves = (c1 - c0 + fast_cpw_ - 1) / fast_cpw_;  // fast_cpw_ cells per wave
     hipLaunchKernelGGL(fs == kFSSmall ? k_fast<kFSSmall> : k_fast<kFSMax>,
-                       dim3((c1 - c0 + 3) / 4, nframes), dim3(256), fast_lds, st, pyr,
+                       dim3((waves + 3) / 4, nframes), dim3(256), fast_lds, st, pyr,
                        pyr_stride_, d_lv_, d_cells_, ncells_, keys, total_slots_, cellcnt,
                        iniTh_, minTh_, fast_rows_max_, fast_win_max_, c0, c1);
   };

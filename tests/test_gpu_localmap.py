@@ -207,19 +207,20 @@ def test_keyframe_culling_and_reparenting_match_oracle(oracle_mod):
     """KeyFrameCulling (LocalMapping.cc:653-720) and KeyFrame::SetBadFlag's spanning-tree
     re-parenting (KeyFrame.cc:453-545) on the GPU path.  The reference's 0.9 redundancy ratio is
     never reached by the synthetic drives, so both sides lower it to 0.3 through the test knob
-    (mmt_set_keyframe_culling_ratio / oracle set_cull_ratio) on a slow half-resolution drive:
+    (mmt_set_keyframe_culling_ratio / oracle set_cull_ratio) on a slow drive at 3/4 resolution (the
+    smallest KITTI-shaped frame whose eighth pyramid level still holds a FAST cell):
     the product culls the same keyframes and re-parents the same children as the oracle, and the
     whole map graph equals the oracle's after every keyframe."""
     import multimot_track_amd as M
     from multimot_track_amd import scene
     from map_invariants import check_map, same_map
-    Kc = {k: v * 0.5 for k, v in scene.KITTI03.items()}
-    W, H = 621, 188
+    Kc = {k: v * 0.75 for k, v in scene.KITTI03.items()}
+    W, H = 931, 281
     R = scene.SequenceRenderer(scene.StreetScene(3, 1003, speed=0.3), W, H, K=Kc)
-    cfg = M.kitti03_config(W, H, 1000)
+    cfg = M.kitti03_config(W, H, 1500)
     cfg.fx, cfg.fy, cfg.cx, cfg.cy, cfg.bf = Kc["fx"], Kc["fy"], Kc["cx"], Kc["cy"], Kc["bf"]
     ctx = M.Context(cfg)
-    tr = oracle_mod.Tracker(W, H, (Kc["fx"], Kc["fy"], Kc["cx"], Kc["cy"]), Kc["bf"], 0, 1000)
+    tr = oracle_mod.Tracker(W, H, (Kc["fx"], Kc["fy"], Kc["cx"], Kc["cy"]), Kc["bf"], 0, 1500)
     ctx.set_keyframe_culling_ratio(0.3)
     tr.set_cull_ratio(0.3)
     try:

@@ -91,12 +91,14 @@ def test_oracle_keyframe_culling_reparents_and_keeps_invariants(oracle_mod):
     """KeyFrameCulling (LocalMapping.cc:653-720) with KeyFrame::SetBadFlag's re-parenting
     (KeyFrame.cc:453-545).  The synthetic sequences never reach the reference's 0.9 redundancy
     ratio, so the test lowers it (the test knob, oracle set_cull_ratio / the product's
-    mmt_set_keyframe_culling_ratio) on a slow drive: keyframes are culled, spanning-tree children
-    are re-parented, and the map passes every invariant after each LocalMapping."""
+    mmt_set_keyframe_culling_ratio) on a slow drive (the GPU test's 3/4-resolution sequence):
+    keyframes are culled, spanning-tree children are re-parented, and the map passes every
+    invariant after each LocalMapping."""
     from multimot_track_amd import scene
-    K, W, H = _half_res_camera()
+    K = {k: v * 0.75 for k, v in scene.KITTI03.items()}
+    W, H = 931, 281
     R = scene.SequenceRenderer(scene.StreetScene(3, 1003, speed=0.3), W, H, K=K)
-    tr = oracle_mod.Tracker(W, H, (K["fx"], K["fy"], K["cx"], K["cy"]), K["bf"], 0, 1000)
+    tr = oracle_mod.Tracker(W, H, (K["fx"], K["fy"], K["cx"], K["cy"]), K["bf"], 0, 1500)
     tr.set_cull_ratio(0.3)
     for i in range(60):
         b, d, f, m = R.frame(i)
