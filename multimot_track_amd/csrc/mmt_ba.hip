@@ -1199,85 +1199,87 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
     if (i > j) S[q] = S[(size_t)j * n6 + i];
   }
   __syncthreads();
-  // Blocked LDL^T over the 6 x 6 keyframe blocks, on the lower triangle (row-major).  Every entry
-  // receives exactly the scalar algorithm's operations in the scalar order (the subtraction of
-  // L(i, c) L(j, c) D(c) for c ascending, then for an off-diagonal the division by D(j)): the
-  // diagonal block is factored by one wave, the panel below it one row per thread, the trailing
-  // blocks one entry per thread, three barriers per block column.  L is also copied into the upper
-  // triangle (L(i, c) at (c, i)) for the forward substitution's coalesced reads.
+  // Right-looking LDL^T on the lower triangle (row-major), one column per step, one barrier per
+  // step.  At step c every thread has D(c) (Dg) and the column L(., c) (col[c & 1]).  Wave 0 looks
+  // one column ahead: it applies step c's update to column c + 1, takes the pivot D(c + 1) from its
+  // diagonal (lane 0), divides the column by it into col[(c + 1) & 1], and carries the forward
+  // substitution y(i) -= L(i, c) y(c); waves 1.. apply step c's update to the columns right of
+  // c + 1.  Every entry receives the scalar algorithm's operations in the scalar order (the
+  // subtraction of (L(i, c) L(j, c)) D(c) for c ascending, then the division by D(j)), as the CPU
+  // checker's left-looking loops, and so does y: the factors and y are bit-identical to it.
+  // Replaces a blocked version with a one-wave diagonal block and three barriers per keyframe.
+  __shared__ double s_col[2 * kLdsRows];
+  double* col = n6 <= kLdsRows ? s_col : w.vec + 3 * (size_t)n6;  // [2][n6]
   bool ok = true;
   pt[2] = wall_clock64();
-  for (int K = 0; K < d.n_opt; K++) {
-    const int k0 = 6 * K;
+  if (wave == 0) {  // column 0 and y = b
+    const double d0 = S[0];
+    for (int i = lane; i < n6; i += 64) {
+      yv[i] = bs[i];
+      if (i > 0) {
+        const double l = S[(size_t)i * n6] / d0;
+        col[i] = l;
+        S[(size_t)i * n6] = l;
+      }
+    }
+    if (lane == 0) {
+      Dg[0] = d0;
+      if (d0 == 0) s_ok = 0;
+    }
+  }
+  __syncthreads();
+  if (s_ok == 0) ok = false;
+  for (int c = 0; ok && c + 1 < n6; c++) {
+    const double dc = Dg[c];
+    const double* lc = col + (size_t)(c & 1) * n6;
     if (wave == 0) {
-      for (int c = 0; c < 6 && ok; c++) {
-        const int kc = k0 + c;
-        double dk = S[(size_t)kc * n6 + kc];
-        for (int m = k0; m < kc; m++) dk -= S[(size_t)kc * n6 + m] * S[(size_t)kc * n6 + m] * Dg[m];
-        if (dk == 0) {
-          ok = false;
-          break;
+      double* ln = col + (size_t)((c + 1) & 1) * n6;
+      const double lnc = lc[c + 1];  // L(c + 1, c)
+      const double yc = yv[c];
+      // rows c + 1 + lane (+ 64 ...): lane 0 of the first pass holds the new pivot
+      double piv = 0;
+      for (int k0 = 0; c + 1 + k0 < n6; k0 += 64) {
+        const int i = c + 1 + k0 + lane;
+        double v = 0, lic = 0;
+        if (i < n6) {
+          lic = lc[i];
+          v = S[(size_t)i * n6 + c + 1] - lic * lnc * dc;
+          yv[i] -= lic * yc;
         }
-        const int r = k0 + lane;
-        if (lane > c && lane < 6) {
-          double v = S[(size_t)r * n6 + kc];
-          for (int m = k0; m < kc; m++) v -= S[(size_t)r * n6 + m] * S[(size_t)kc * n6 + m] * Dg[m];
-          const double l = v / dk;
-          S[(size_t)r * n6 + kc] = l;
-          S[(size_t)kc * n6 + r] = l;
+        if (k0 == 0) piv = lane_value(v, 0);
+        if (i < n6 && i > c + 1) {
+          const double l = v / piv;
+          ln[i] = l;
+          S[(size_t)i * n6 + c + 1] = l;
         }
-        if (lane == 0) {
-          S[(size_t)kc * n6 + kc] = dk;
-          Dg[kc] = dk;
-        }
-        wave_sync_lds();
       }
-      if (!ok && lane == 0) s_ok = 0;
-    }
-    __syncthreads();
-    if (s_ok == 0) {
-      ok = false;
-      break;
-    }
-    // the panel: L(i, k0 + c) for the rows below the block, one row per thread
-    for (int i = k0 + 6 + tid; i < n6; i += kMkSolveThreads) {
-      double l[6];
-#pragma unroll
-      for (int c = 0; c < 6; c++) {
-        double v = S[(size_t)i * n6 + k0 + c];
-        for (int m = 0; m < c; m++) v -= l[m] * S[(size_t)(k0 + c) * n6 + k0 + m] * Dg[k0 + m];
-        l[c] = v / Dg[k0 + c];
-        S[(size_t)i * n6 + k0 + c] = l[c];
-        S[(size_t)(k0 + c) * n6 + i] = l[c];
+      if (lane == 0) {
+        S[(size_t)(c + 1) * n6 + c + 1] = piv;
+        Dg[c + 1] = piv;
+        if (piv == 0) s_ok = 0;
+      }
+    } else {
+      // step c's update of the trailing triangle c + 2 <= j <= i < n6, one entry per thread
+      const int m = n6 - c - 2, nq = m * (m + 1) / 2;
+      for (int q = tid - 64; q < nq; q += kMkSolveThreads - 64) {
+        int ii = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+        while (ii * (ii + 1) / 2 > q) ii--;
+        while ((ii + 1) * (ii + 2) / 2 <= q) ii++;
+        const int i = c + 2 + ii, j = c + 2 + (q - ii * (ii + 1) / 2);
+        S[(size_t)i * n6 + j] -= lc[i] * lc[j] * dc;
       }
     }
     __syncthreads();
-    // the trailing lower triangle: (i, j), k0 + 6 <= j <= i, minus the block's six terms in order
-    const int m0 = k0 + 6, mt = n6 - m0;
-    for (int q = tid; q < mt * mt; q += kMkSolveThreads) {
-      const int i = m0 + q / mt, jj = m0 + q % mt;
-      if (jj > i) continue;
-      double v = S[(size_t)i * n6 + jj];
-#pragma unroll
-      for (int c = 0; c < 6; c++)
-        v -= S[(size_t)i * n6 + k0 + c] * S[(size_t)jj * n6 + k0 + c] * Dg[k0 + c];
-      S[(size_t)i * n6 + jj] = v;
-    }
-    __syncthreads();
+    if (s_ok == 0) ok = false;
   }
   pt[3] = wall_clock64();
   if (!ok) {
     if (tid == 0) s_ok = 0;
   } else if (wave == 0) {
-    // substitutions with y in registers (lane i: rows i, i + 64), y[c] broadcast by readlane;
-    // forward reads L(i, c) at (c, i) (upper copy), backward L(r, i) at (r, i): coalesced rows
-    double y0 = lane < n6 ? bs[lane] : 0.0, y1 = lane + 64 < n6 ? bs[lane + 64] : 0.0;
+    // y / D and the backward substitution, y in registers (lane i: rows i, i + 64), y[r]
+    // broadcast by readlane, L(r, i) read at (r, i): coalesced rows
+    double y0 = lane < n6 ? yv[lane] : 0.0, y1 = lane + 64 < n6 ? yv[lane + 64] : 0.0;
     if (n6 <= 128) {
-      for (int c = 0; c < n6; c++) {
-        const double yc = c < 64 ? lane_value(y0, c) : lane_value(y1, c - 64);
-        if (lane > c && lane < n6) y0 -= S[(size_t)c * n6 + lane] * yc;
-        if (lane + 64 > c && lane + 64 < n6) y1 -= S[(size_t)c * n6 + lane + 64] * yc;
-      }
       if (lane < n6) y0 /= Dg[lane];
       if (lane + 64 < n6) y1 /= Dg[lane + 64];
       for (int r = n6 - 1; r > 0; r--) {
@@ -1288,13 +1290,6 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
       if (lane < n6) w.x[lane] = y0;
       if (lane + 64 < n6) w.x[lane + 64] = y1;
     } else {
-      for (int i = lane; i < n6; i += 64) yv[i] = bs[i];
-      wave_sync_lds();
-      for (int c = 0; c < n6; c++) {
-        const double yc = yv[c];
-        for (int i = c + 1 + lane; i < n6; i += 64) yv[i] -= S[(size_t)c * n6 + i] * yc;
-        wave_sync_lds();
-      }
       for (int i = lane; i < n6; i += 64) yv[i] /= Dg[i];
       wave_sync_lds();
       for (int r = n6 - 1; r > 0; r--) {
@@ -1877,7 +1872,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.cvpart = (double*)take(8 * 6 * kitem.size());
     w.x = (double*)take(8 * ((size_t)n6 + 3 * (size_t)nP));
     w.S = (double*)take(8 * (size_t)n6 * n6);
-    w.vec = (double*)take(8 * 3 * (size_t)n6);
+    w.vec = (double*)take(8 * 5 * (size_t)n6);  // b, D, y, two L columns (p3)
     w.linpart = (double*)take(8 * 2 * (size_t)gP);
     w.p4part = (double*)take(8 * 2 * (size_t)gP);
     w.p4cnt = (unsigned*)take(16);

@@ -22,7 +22,7 @@ rows = con.execute("select name, duration, grid_x, grid_y, grid_z from kernels o
 acc = collections.OrderedDict()
 seen = collections.Counter()
 for name, dur, gx, gy, gz in rows:
-    short = re.sub(r"\(.*", "", name).replace("void ", "")
+    short = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", "")).replace("void ", "")
     seen[short] += 1
     if seen[short] <= a.skip:
         continue
