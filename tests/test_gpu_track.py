@@ -266,9 +266,27 @@ def test_track_c5_eight_motions_long_matches_oracle(oracle_mod):
 @pytest.mark.parametrize("w,h,seed", [(1241, 376, 1000), (1226, 370, 1005)])
 def test_track_c4_sizes_long_matches_oracle(oracle_mod, w, h, seed):
     """BASELINE C4 geometries (KITTI 00 at 1241x376, 05/07 at 1226x370), 4000 features, ego + 3
-    moving boxes, over 100 frames (keyframes, local BA, fusion and culling included)."""
+    moving boxes, over 100 frames (keyframes, local BA and fusion; the cull branch is covered by
+    test_gpu_localmap.py::test_keyframe_culling_and_reparenting_match_oracle)."""
     got, rec = _long_parity(oracle_mod, w, h, 4000, 100, seed, 3)
     assert rec["frames"] == 100 and got[-1]["n_keyframes"] > 2
+
+
+def test_track_c4_400_frames_matches_oracle(oracle_mod):
+    """C4 depth: KITTI 00's geometry over 400 frames (about a tenth of a real C4 sequence),
+    tracked on the map in every frame, every frame within the bar."""
+    got, rec = _long_parity(oracle_mod, 1241, 376, 4000, 400, 1000, 3, chunk=64)
+    assert rec["frames"] == 400 and got[-1]["n_keyframes"] > 10
+    assert all(g["map_state"] == 1 for g in got)
+
+
+def test_track_c5_eight_motions_250_frames_matches_oracle(oracle_mod):
+    """C5 depth: the eight object motions at 1920x1080 and 8000 features over 250 frames."""
+    got, rec = _long_parity(oracle_mod, 1920, 1080, 8000, 250, 2000, 2,
+                            lanes=[(-3.0, 12.0), (3.4, 9.0)], parts=4)
+    assert rec["frames"] == 250
+    assert sum(len(g["objects"]) == 8 for g in got[1:]) >= 240
+    assert all(g["map_state"] == 1 for g in got)
 
 
 @pytest.mark.parametrize("seed,n,out,mono", [(0, 400, 0.15, 0.2), (1, 1500, 0.2, 0.1),
