@@ -68,6 +68,16 @@ struct ResizeY {
 struct BlurTile {
   int level, x0, y0, pad;
 };
+// k_pyramid: the rows [lo, hi) of every level one band computes (its own rows and the halo rows
+// the next level's rows read), and the per-level constants of the launch
+constexpr int kPyrMaxLevels = 12;
+struct PyrBand {
+  int lo[kPyrMaxLevels], hi[kPyrMaxLevels];
+};
+struct PyrArgs {
+  int nl, buf_bytes;
+  int pitch[kPyrMaxLevels], xoff[kPyrMaxLevels], yoff[kPyrMaxLevels];
+};
 
 // Batched ORB extraction engine for one image size.
 class OrbEngine {
@@ -127,6 +137,15 @@ class OrbEngine {
   std::vector<CellInfo> cells_;
   std::vector<int> xtab_off_, ytab_off_;
   std::vector<int> rs_pitch_, rs_lds_;  // k_resize LDS row pitch and bytes per level
+  // k_pyramid (MMT_PYR=0: the k_resize chain): bands per frame (0: the chain, e.g. when a band's
+  // rows do not fit the LDS), the band table and the launch constants
+  int pyr_bands_ = 0, pyr_lds_ = 0;
+  // batches up to this many frames take k_pyramid (MMT_PYR_MAX_FRAMES); window against the chain
+  // (round 5): batch 1 0.124 / 0.140 ms, 4 0.136 / 0.154, 16 0.202 / 0.218, 32 0.297 / 0.300,
+  // 64 0.544 / 0.503, 128 1.029 / 0.919
+  int pyr_max_frames_ = 32;
+  PyrBand* d_pyr_bands_ = nullptr;
+  PyrArgs pyr_args_{};
   int sched_ = 0;  // MMT_ORB_SCHED=2: one stream (standalone kernel times for profiling)
   // FAST cells per wave (MMT_FAST_CPW, default 1): with more, each wave's next tile loads are in
   // flight during its current cell; measured 0.918 / 0.928 / 0.940 / 0.951 ms per 128-frame window

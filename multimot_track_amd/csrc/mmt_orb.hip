@@ -190,6 +190,146 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
   }
 }
 
+// ---- the whole pyramid in one launch (levels 1.. from level 0, cv::resize as k_resize) ----
+// One 1024-thread workgroup per (band of rows, frame): band b owns rows [h b / nb, h (b + 1) / nb)
+// of every level and computes, level after level, its own rows plus the halo rows the next level's
+// computed rows read (PyrBand, from the host's backward pass over the row tables), each level from
+// the previous one in LDS (two alternating buffers), writing its own rows to the pyramid.  No
+// workgroup waits for another, so the seven launches of the k_resize chain (each one memory round
+// trip and a launch gap on the window's critical path) become one; halo rows are recomputed from
+// the same bytes with the same arithmetic, so every level is bit-identical to the chain's.
+constexpr int kPyrStage = 16;  // level-0 staging dwords per thread issued together
+
+__global__ __launch_bounds__(1024) void k_pyramid(uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                  const LevelInfo* __restrict__ lv,
+                                                  const ResizeX* __restrict__ xt,
+                                                  const ResizeY* __restrict__ yt,
+                                                  const PyrBand* __restrict__ bands, PyrArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t py_lds[];
+  const int tid = threadIdx.x, band = blockIdx.x, nb = gridDim.x;
+  uint8_t* base = pyr + (size_t)blockIdx.y * pyr_stride;
+  const PyrBand& B = bands[band];
+  // the band's row coefficients of every level, staged in LDS after the two level buffers
+  ResizeY* ylds = (ResizeY*)(py_lds + 2 * (size_t)a.buf_bytes);
+  // thread -> (row offset, dword column) of a level whose rows hold nq dwords: rstep rows per pass
+  auto lane_map = [&](int nq, int& q, int& rsub, int& rstep) {
+    const float inv = 1.0f / (float)nq;
+    rsub = (int)(((float)tid + 0.5f) * inv);  // exact: tid < 2^10, nq <= 1024
+    q = tid - rsub * nq;
+    rstep = (int)((1024.0f + 0.5f) * inv);
+  };
+  // this thread's four column coefficients of level l (issued a level ahead of their use)
+  auto load_cx = [&](int l, ResizeX (&cx)[4]) {
+    const LevelInfo D = lv[l];
+    int q, rsub, rstep;
+    lane_map((D.w + 3) >> 2, q, rsub, rstep);
+    const ResizeX* X = xt + a.xoff[l];
+#pragma unroll
+    for (int j = 0; j < 4; j++) cx[j] = X[min(4 * q + j, D.w - 1)];
+  };
+  ResizeX cx[4];
+  load_cx(1, cx);
+  {  // level 0 rows of the band into buffer 0, the row coefficients into ylds: loads all in flight
+    const LevelInfo L0 = lv[0];
+    const int lo = B.lo[0], hi = B.hi[0], nq = (L0.w + 3) >> 2, pitch = a.pitch[0];
+    int q, rsub, rstep;
+    lane_map(nq, q, rsub, rstep);
+    const bool act = rsub < rstep;
+    // unconditional loads (rows clamped into the band): a load on a conditional path makes the
+    // compiler drain every outstanding load where the paths join
+    const int rs = act ? rsub : 0;
+    const uint8_t* l0 = base + L0.off + 4 * q;
+    uint32_t v[kPyrStage];
+#pragma unroll
+    for (int k = 0; k < kPyrStage; k++)  // may read <= 3 bytes past the row: next row / slack
+      __builtin_memcpy(&v[k], l0 + (size_t)min(lo + rs + k * rstep, hi - 1) * L0.w, 4);
+    int yo = 0;
+    int ya[kPyrMaxLevels], yb[kPyrMaxLevels], yc[kPyrMaxLevels];  // ResizeY as three dwords
+#pragma unroll
+    for (int l = 1; l < kPyrMaxLevels; l++) {
+      const int* yp = (const int*)(yt + a.yoff[l] + B.lo[l] +
+                                   min(tid, max(B.hi[min(l, a.nl - 1)] - B.lo[l] - 1, 0)));
+      ya[l] = l < a.nl ? yp[0] : 0;
+      yb[l] = l < a.nl ? yp[1] : 0;
+      yc[l] = l < a.nl ? yp[2] : 0;
+    }
+    uint8_t* lp = py_lds + rsub * pitch + 4 * q;
+#pragma unroll
+    for (int k = 0; k < kPyrStage; k++)
+      if (act && lo + rsub + k * rstep < hi) *(uint32_t*)(lp + k * rstep * pitch) = v[k];
+    for (int y = lo + rsub + kPyrStage * rstep; act && y < hi; y += rstep) {  // tall bands only
+      uint32_t w;
+      __builtin_memcpy(&w, base + L0.off + (size_t)y * L0.w + 4 * q, 4);
+      *(uint32_t*)(py_lds + (y - lo) * pitch + 4 * q) = w;
+    }
+#pragma unroll
+    for (int l = 1; l < kPyrMaxLevels; l++)
+      if (l < a.nl) {
+        const int n = B.hi[l] - B.lo[l];
+        if (tid < n) {  // n <= 1024 (host)
+          int* yd = (int*)(ylds + yo + tid);
+          yd[0] = ya[l];
+          yd[1] = yb[l];
+          yd[2] = yc[l];
+        }
+        yo += n;
+      }
+  }
+  __syncthreads();
+  int ybase = 0;  // level l's rows start at ylds[ybase]
+  for (int l = 1; l < a.nl; l++) {
+    const LevelInfo D = lv[l];
+    const uint8_t* src = py_lds + (size_t)((l - 1) & 1) * a.buf_bytes;
+    uint8_t* dst = py_lds + (size_t)(l & 1) * a.buf_bytes;
+    const int slo = B.lo[l - 1], spitch = a.pitch[l - 1], dpitch = a.pitch[l];
+    const int lo = B.lo[l], hi = B.hi[l];
+    const int own_lo = D.h * band / nb, own_hi = D.h * (band + 1) / nb;
+    const bool keep = l + 1 < a.nl;  // the next level reads this one from LDS
+    int q, rsub, rstep;
+    lane_map((D.w + 3) >> 2, q, rsub, rstep);
+    ResizeX cn[4];
+    if (keep) load_cx(l + 1, cn);  // in flight during this level
+    if (rsub < rstep && lo < hi) {
+      const int dx = 4 * q, ncols = min(4, D.w - dx);
+      const int sx0 = cx[0].sx;
+      int lx[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) lx[j] = cx[j].sx - sx0;
+      for (int y = lo + rsub; y < hi; y += rstep) {
+        const ResizeY cy = ylds[ybase + y - lo];
+        const uint8_t* r0 = src + __umul24((unsigned)(cy.sy0 - slo), (unsigned)spitch) + sx0;
+        const uint8_t* r1 = src + __umul24((unsigned)(cy.sy1 - slo), (unsigned)spitch) + sx0;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          // a1 == 0 marks the clamped right edge: the byte at sx + 1 (inside the row pitch) is
+          // multiplied by 0.  24-bit multiplies as k_resize: |a|, |b| <= 2048, |h| < 2^20
+          const int h0 = __mul24(r0[lx[j]], cx[j].a0) + __mul24(r0[lx[j] + 1], cx[j].a1);
+          const int h1 = __mul24(r1[lx[j]], cx[j].a0) + __mul24(r1[lx[j] + 1], cx[j].a1);
+          int v = (__mul24(cy.b0, h0) + __mul24(cy.b1, h1) + (1 << 21)) >> 22;
+          v = v < 0 ? 0 : (v > 255 ? 255 : v);
+          packed |= (uint32_t)v << (8 * j);
+        }
+        if (keep) *(uint32_t*)(dst + __umul24((unsigned)(y - lo), (unsigned)dpitch) + dx) = packed;
+        if (y >= own_lo && y < own_hi) {
+          uint8_t* dp = base + D.off + (size_t)y * D.w + dx;
+          if (ncols == 4) {
+            __builtin_memcpy(dp, &packed, 4);
+          } else {
+            for (int j = 0; j < ncols; j++) dp[j] = (uint8_t)(packed >> (8 * j));
+          }
+        }
+      }
+    }
+    ybase += hi - lo;
+    if (keep) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) cx[j] = cn[j];
+    }
+    __syncthreads();
+  }
+}
+
 // ---- FAST arc strength: max over 9-arcs of min(v - p) (dark) and min(p - v) (bright). ----
 // A pixel is a FAST-9 corner at threshold t iff M > t, and OpenCV's cornerScore<16> returns
 // M - 1 for every corner (derivation in DESIGN.md), so one M per pixel serves both thresholds.
@@ -1625,8 +1765,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(
 OrbEngine::~OrbEngine() { release(); }
 
 void OrbEngine::release() {
-  void* ptrs[] = {d_lv_,   d_cells_,   d_xtab_,  d_ytab_,   d_tiles_, d_umax_, d_pyr_, d_blur_,
-                  d_keys_, d_lkeys_, d_knode_, d_cellcnt_, d_okeys_, d_ocount_, d_err_};
+  void* ptrs[] = {d_lv_,    d_cells_,  d_xtab_,  d_ytab_,    d_tiles_,  d_umax_,   d_pyr_,
+                  d_blur_,  d_keys_,   d_lkeys_, d_knode_,   d_cellcnt_, d_okeys_, d_ocount_,
+                  d_err_,   d_pyr_bands_};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   d_lv_ = nullptr;
@@ -1638,6 +1779,8 @@ void OrbEngine::release() {
   d_pyr_ = d_blur_ = nullptr;
   d_keys_ = d_lkeys_ = d_knode_ = d_okeys_ = nullptr;
   d_cellcnt_ = d_ocount_ = d_err_ = nullptr;
+  d_pyr_bands_ = nullptr;
+  pyr_bands_ = 0;
   for (hipEvent_t* e : {&ev_pyr_, &ev_blur_, &ev_gray_}) {
     if (*e) (void)hipEventDestroy(*e);
     *e = nullptr;
@@ -1801,6 +1944,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   ntiles_ = (int)tiles.size();
   if (const char* e = getenv("MMT_ORB_SCHED")) sched_ = atoi(e);
   if (const char* e = getenv("MMT_FAST_CPW")) fast_cpw_ = std::max(1, std::min(64, atoi(e)));
+  if (const char* e = getenv("MMT_PYR_MAX_FRAMES")) pyr_max_frames_ = atoi(e);
   total_slots_ = key_off;
   out_slots_ = out_off;
   cap_frame_ = out_off;
@@ -1852,6 +1996,59 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
     oct_two_per_cu_ = true;
     MMT_HIP(hipFuncSetAttribute((const void*)k_octree<8>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds1_));
+  }
+  // k_pyramid bands: the fewest (from 16) whose two level buffers fit 120 KB of LDS
+  pyr_bands_ = 0;
+  if (nlevels_ <= kPyrMaxLevels && nlevels_ > 1 && !(getenv("MMT_PYR") && atoi(getenv("MMT_PYR")) == 0)) {
+    for (int nb = 16; nb <= 256 && pyr_bands_ == 0; nb *= 2) {
+      std::vector<PyrBand> bands(nb);
+      PyrArgs pa{};
+      pa.nl = nlevels_;
+      for (int l = 0; l < nlevels_; l++) {
+        pa.pitch[l] = ((lv_[l].w + 3) & ~3) + 4;  // + the clamped edge's byte at sx + 1
+        pa.xoff[l] = xtab_off_[l];
+        pa.yoff[l] = ytab_off_[l];
+      }
+      bool fits = true;
+      int buf = 0;
+      for (int b = 0; b < nb && fits; b++) {
+        PyrBand& B = bands[b];
+        // backward from the last level: rows computed = own rows + the rows the next level reads
+        for (int l = nlevels_ - 1; l >= 0; l--) {
+          int lo = l > 0 ? lv_[l].h * b / nb : 0, hi = l > 0 ? lv_[l].h * (b + 1) / nb : 0;
+          if (l + 1 < nlevels_ && B.lo[l + 1] < B.hi[l + 1]) {
+            const ResizeY* Y = yt.data() + ytab_off_[l + 1];
+            const int slo = Y[B.lo[l + 1]].sy0, shi = Y[B.hi[l + 1] - 1].sy1 + 1;
+            if (lo < hi) {
+              lo = std::min(lo, slo);
+              hi = std::max(hi, shi);
+            } else {
+              lo = slo;
+              hi = shi;
+            }
+          }
+          B.lo[l] = lo;
+          B.hi[l] = std::max(lo, hi);
+          if (l + 1 < nlevels_) buf = std::max(buf, (B.hi[l] - B.lo[l]) * pa.pitch[l]);
+        }
+        fits = 2 * ((buf + 15) & ~15) <= 120 * 1024;
+        for (int l = 0; l < nlevels_; l++) fits = fits && B.hi[l] - B.lo[l] <= 1024;
+      }
+      if (!fits) continue;
+      pa.buf_bytes = (buf + 15) & ~15;
+      int yrows = 0;  // the largest band's row coefficients over levels 1..
+      for (const PyrBand& B : bands) {
+        int n = 0;
+        for (int l = 1; l < nlevels_; l++) n += B.hi[l] - B.lo[l];
+        yrows = std::max(yrows, n);
+      }
+      pyr_lds_ = 2 * pa.buf_bytes + (int)sizeof(ResizeY) * yrows;
+      pyr_bands_ = nb;
+      pyr_args_ = pa;
+      upload(&d_pyr_bands_, bands);
+      MMT_HIP(hipFuncSetAttribute((const void*)k_pyramid, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  pyr_lds_));
+    }
   }
   upload(&d_lv_, lv_);
   upload(&d_cells_, cells_);
@@ -1964,6 +2161,17 @@ void OrbEngine::run_part(int f0, int nframes, hipStream_t stream, hipStream_t si
                        S.w, L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l],
                        rs_pitch_[l]);
   };
+  auto pyramid = [&](hipStream_t st) {  // levels 1..: one k_pyramid launch, or the k_resize chain
+    // k_pyramid for small batches, where the chain's seven launches are pure latency; from 64
+    // frames on the chain is faster (at 128: 151 against 220 us standalone, the band workgroups'
+    // per-level barriers and halo rows cost more than the launches; mmt_internal.h)
+    if (pyr_bands_ > 0 && nframes <= pyr_max_frames_) {
+      hipLaunchKernelGGL(k_pyramid, dim3(pyr_bands_, nframes), dim3(1024), pyr_lds_,
+                         st, pyr, pyr_stride_, d_lv_, d_xtab_, d_ytab_, d_pyr_bands_, pyr_args_);
+    } else {
+      for (int l = 1; l < nlevels_; l++) resize(l, st);
+    }
+  };
   auto blur = [&](hipStream_t st) {
     hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, st, pyr,
                        blurb, pyr_stride_, d_lv_, d_tiles_, ntiles_);
@@ -1973,7 +2181,7 @@ void OrbEngine::run_part(int f0, int nframes, hipStream_t stream, hipStream_t si
   if (sched_ & 2) {  // one stream: standalone kernel times (profiling)
     fast(cells(0).first, cells(0).second, stream);
     octree(0, 1, stream);
-    for (int l = 1; l < NL; l++) resize(l, stream);
+    pyramid(stream);
     blur(stream);
     fast(cells(0).second, ncells_, stream);
     if (NL > 1) octree(1, NL, stream);
@@ -1989,7 +2197,7 @@ void OrbEngine::run_part(int f0, int nframes, hipStream_t stream, hipStream_t si
     MMT_HIP(hipStreamWaitEvent(side, e_gray, 0));
     fast(cells(0).first, cells(0).second, side);
     octree(0, 1, side);
-    for (int l = 1; l < NL; l++) resize(l, stream);
+    pyramid(stream);
     MMT_HIP(hipEventRecord(e_pyr, stream));
     MMT_HIP(hipStreamWaitEvent(side, e_pyr, 0));
     blur(side);
