@@ -11,7 +11,8 @@ OUT = os.path.join(HERE, "libmmt.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
-         "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+         "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+         "-Xarch_host", "-mpopcnt"]  # host: the popcount instruction (map-point descriptors)
 FLAGS += os.environ.get("MMT_EXTRA_FLAGS", "").split()  # e.g. -DMMT_LM_PROFILE (tools/)
 
 

@@ -322,6 +322,7 @@ void MapEngine::fuse_sequence(const std::vector<int>& kfl, const std::vector<int
 
 // ------------------------------------------------------------------ LocalMapping steps
 void MapEngine::search_in_neighbors(int kf) {  // LocalMapping::SearchInNeighbors (RGB-D: nn 10)
+  double tb = prof_on_ ? prof_now_us() : 0;
   const long cur = kfs_[kf].id;
   auto best = [&](int k, size_t n) {
     const std::vector<int>& o = kfs_[k].ordered;
@@ -340,7 +341,9 @@ void MapEngine::search_in_neighbors(int kf) {  // LocalMapping::SearchInNeighbor
     }
   }
   const std::vector<int> matches = kfs_[kf].mps;
+  blk_time(2, tb);
   fuse_sequence(targets, matches);
+  blk_time(3, tb);
   std::vector<int> cands;
   for (int t : targets) {
     const std::vector<int> mps = kfs_[t].mps;
@@ -352,14 +355,18 @@ void MapEngine::search_in_neighbors(int kf) {  // LocalMapping::SearchInNeighbor
       cands.push_back(h);
     }
   }
+  blk_time(4, tb);
   fuse_sequence(std::vector<int>{kf}, cands);
+  blk_time(5, tb);
   const std::vector<int> now = kfs_[kf].mps;
   for (int h : now) {
     if (h < 0 || mp(h).bad) continue;
     compute_distinctive(h);
     update_normal_depth(h);
   }
+  blk_time(6, tb);
   update_connections(kf);
+  blk_time(7, tb);
 }
 
 void MapEngine::local_bundle_adjustment(int kf) {  // Optimizer::LocalBundleAdjustment
@@ -439,9 +446,11 @@ void MapEngine::local_bundle_adjustment(int kf) {  // Optimizer::LocalBundleAdju
   std::vector<float> Tout(16 * (size_t)nK), Xout(3 * (size_t)nP);
   std::vector<uint8_t> er(std::max(nE, 1));
   int st[5];
-  const double tb = prof_on_ ? now_us() : 0;
+  double tb = prof_on_ ? now_us() : 0;
+  if (prof_on_) mstats_.blk_us[8] += tb - t0;
   ba_.run(P, lm_s_, Tout.data(), Xout.data(), er.data(), st);
   if (prof_on_) mstats_.basolve_us += now_us() - tb;
+  tb = prof_on_ ? now_us() : 0;
   mstats_.n_ba++;
   mstats_.ba_trials += st[2] + st[3];
   mstats_.ba_edges += nE;
@@ -466,6 +475,7 @@ void MapEngine::local_bundle_adjustment(int kf) {  // Optimizer::LocalBundleAdju
     mark_dirty(lpts[j]);
     update_normal_depth(lpts[j]);
   }
+  blk_time(9, tb);
   if (prof_on_) mstats_.ba_us += now_us() - t0;
 }
 

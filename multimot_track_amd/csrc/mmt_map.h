@@ -33,6 +33,7 @@
 #include <map>
 #include <set>
 #include <utility>
+#include <memory>
 #include <vector>
 
 #include "mmt_ba.h"
@@ -50,6 +51,29 @@ struct MapCamH {
   int nlevels = 0;
   float logScale = 0;
   std::vector<float> scale, invSigma2;
+};
+
+// An array in chunks of 2^kShift elements: indexing as a vector's (one more load), push_back never
+// moves the elements already stored (references stay valid)
+template <class T, int kShift = 13>
+class ChunkArray {
+ public:
+  T& operator[](size_t i) { return chunks_[i >> kShift][i & kMask]; }
+  const T& operator[](size_t i) const { return chunks_[i >> kShift][i & kMask]; }
+  size_t size() const { return n_; }
+  void push_back(const T& v) {
+    if ((n_ >> kShift) >= chunks_.size()) chunks_.emplace_back(new T[kChunk]);
+    (*this)[n_++] = v;
+  }
+  void clear() {
+    chunks_.clear();
+    n_ = 0;
+  }
+
+ private:
+  static constexpr size_t kChunk = (size_t)1 << kShift, kMask = kChunk - 1;
+  std::vector<std::unique_ptr<T[]>> chunks_;
+  size_t n_ = 0;
 };
 
 struct MPoint {
@@ -103,6 +127,8 @@ struct MappingStats {
   double lm_us = 0, ba_us = 0, fuse_us = 0;  // host wall time (MMT_MAP_PROFILE)
   // finer host wall times of the keyframe path (MMT_MAP_PROFILE; printed at destruction)
   double kfnew_us = 0, pnk_us = 0, sin_us = 0, basolve_us = 0, cull_us = 0, lmsync_us = 0;
+  static constexpr int kBlk = 10;  // finer blocks of the keyframe path (names in ~MapEngine)
+  double blk_us[kBlk] = {};
   long n_lm = 0;
 };
 
@@ -161,6 +187,14 @@ class MapEngine {
   // them into the keyframe store, where Fuse reads them
   void set_frame_grid(const GridFrame& G) { G_ = G; }
   const MappingStats& mapping_stats() const { return mstats_; }
+  // MMT_MAP_PROFILE: adds the time since t to block k and restarts t
+  void blk_time(int k, double& t) {
+    if (!prof_on_) return;
+    const double n = prof_now_us();
+    mstats_.blk_us[k] += n - t;
+    t = n;
+  }
+  static double prof_now_us();
   // test knob: KeyFrameCulling's redundancy ratio (0.9 in the reference, LocalMapping.cc:697)
   void set_cull_ratio(double r) { cull_ratio_ = r; }
   // the map as flat arrays (mmt_map_dump, include/mmt.h): sizes[7]; arrays written when out != 0
@@ -238,7 +272,14 @@ class MapEngine {
 
   MapCamH cam_;
   int kcap_ = 0;
-  std::vector<MPoint> pts_, temps_;
+  // map points in fixed chunks: growing the array never moves the existing points (a vector's
+  // reallocation moved all of them, 100k points at a time, inside a keyframe's point creation)
+#ifdef MMT_PTS_VECTOR  // A/B build (tools/build_prof_lib.sh)
+  std::vector<MPoint> pts_;
+#else
+  ChunkArray<MPoint> pts_;
+#endif
+  std::vector<MPoint> temps_;
   // the fields the per-frame local-map scans read, one compact record per real point (pts_ index):
   // UpdateLocalPoints walks ~13k point references and SearchLocalPoints ~4.4k, at random, and a
   // 12-byte record keeps them in cache where the 136-byte MPoint does not

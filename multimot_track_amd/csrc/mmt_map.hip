@@ -61,6 +61,8 @@ static double now_us() {
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+double MapEngine::prof_now_us() { return now_us(); }
+
 MapEngine::~MapEngine() {
   if (prof_on_ && prof_n_ > 0) {
     static const char* names[12] = {"C2 search", "D1 (motion model)", "local map update",
@@ -80,6 +82,13 @@ MapEngine::~MapEngine() {
               mstats_.sin_us / n, mstats_.fuse_us / n, mstats_.ba_us / n,
               mstats_.basolve_us / n, mstats_.cull_us / n, mstats_.lmsync_us / n,
               mstats_.lm_us / n, mstats_.kfnew_us / n);
+      static const char* bn[MappingStats::kBlk] = {
+          "new keyframe + store", "new points", "SIN targets", "SIN fuse 1", "SIN candidates",
+          "SIN fuse 2", "SIN point updates", "SIN connections", "BA graph", "BA apply"};
+      fprintf(stderr, "[mmt localmapping profile] per keyframe, us:");
+      for (int k = 0; k < MappingStats::kBlk; k++)
+        fprintf(stderr, " %s %.1f%s", bn[k], mstats_.blk_us[k] / n,
+                k + 1 < MappingStats::kBlk ? "," : "\n");
     }
     fprintf(stderr, "[mmt map profile] per frame: %.1f local keyframes, %.1f local points, "
             "%.1f C3 edges; %zu map points allocated, %d keyframes at the end\n",
@@ -143,7 +152,15 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
   d_esc_ = dev<double>(3 * (size_t)kcap);
   d_fsc_ = dev<int>(kcap);
   prof_on_ = getenv("MMT_MAP_PROFILE") != nullptr;
-  MMT_HIP(hipStreamCreateWithFlags(&lm_s_, hipStreamNonBlocking));
+  {
+    // LocalMapping's stream (A/B knob MMT_LM_PRIO: 1 high, 2 low, otherwise normal): its kernels
+    // (keyframe store copies, Fuse, the local BA) need nothing of the frame's flow solve
+    const char* e = getenv("MMT_LM_PRIO");
+    int lo = 0, hi = 0;
+    MMT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const int v = e ? atoi(e) : 0;
+    MMT_HIP(hipStreamCreateWithPriority(&lm_s_, hipStreamNonBlocking, v == 1 ? hi : (v == 2 ? lo : 0)));
+  }
   // keyframe store record: keys, descriptors, mvuRight, grid (cell starts + key lists)
   kf_rec_bytes_ = align16(sizeof(mmt_kp) * (size_t)kcap) + 32 * (size_t)kcap +
                   align16(4 * (size_t)kcap) + align16(4 * (size_t)(kGridCells + 1)) +
@@ -268,33 +285,51 @@ void MapEngine::set_bad(int h) {  // MapPoint::SetBadFlag
 void MapEngine::compute_distinctive(int h) {  // MapPoint::ComputeDistinctiveDescriptors
   MPoint& p = mp(h);
   if (p.bad || p.obs.empty()) return;
-  std::vector<const uint8_t*> Dv;
-  size_t N = 0;
+  // the descriptors of the good observing keyframes, their pairwise Hamming distances and each
+  // one's median distance (the (N - 1) / 2-th smallest, MapPoint.cc:295-313); up to 32
+  // observations on the stack (no allocation per call), beyond that on the heap
+  constexpr int kStack = 32;
+  const uint8_t* Ds[kStack];
+  std::vector<const uint8_t*> Dh;
+  int N = 0;
   for (const auto& kv : p.obs)
-    if (!kfs_[kv.first].bad) Dv.push_back(kfs_[kv.first].desc.data() + 32 * (size_t)kv.second);
-  N = Dv.size();
-  if (N == 0) return;
-  std::vector<int> dist(N * N, 0);
-  for (size_t i = 0; i < N; i++)
-    for (size_t j = i + 1; j < N; j++) {
-      int d = 0;
-      for (int w = 0; w < 8; w++) {
-        uint32_t a, b;
-        memcpy(&a, Dv[i] + 4 * w, 4);
-        memcpy(&b, Dv[j] + 4 * w, 4);
-        d += __builtin_popcount(a ^ b);
-      }
-      dist[i * N + j] = dist[j * N + i] = d;
+    if (!kfs_[kv.first].bad) {
+      const uint8_t* d = kfs_[kv.first].desc.data() + 32 * (size_t)kv.second;
+      if (N < kStack) Ds[N] = d;
+      if (N == kStack) Dh.assign(Ds, Ds + kStack);
+      if (N >= kStack) Dh.push_back(d);
+      N++;
     }
-  int best = INT_MAX;
-  size_t bi = 0;
-  std::vector<int> v(N);
-  for (size_t i = 0; i < N; i++) {
-    std::copy(dist.begin() + i * N, dist.begin() + (i + 1) * N, v.begin());
-    std::sort(v.begin(), v.end());
-    const int median = v[(size_t)(0.5 * (N - 1))];
-    if (median < best) {
-      best = median;
+  if (N == 0) return;
+  const uint8_t* const* Dv = N <= kStack ? Ds : Dh.data();
+  int dist_s[kStack * kStack], v_s[kStack];
+  std::vector<int> dist_h, v_h;
+  if (N > kStack) {
+    dist_h.assign((size_t)N * N, 0);
+    v_h.resize(N);
+  }
+  int* dist = N <= kStack ? dist_s : dist_h.data();
+  int* v = N <= kStack ? v_s : v_h.data();
+  for (int i = 0; i < N; i++) {
+    dist[(size_t)i * N + i] = 0;
+    for (int j = i + 1; j < N; j++) {
+      int d = 0;
+      for (int w = 0; w < 4; w++) {
+        uint64_t a, b;
+        memcpy(&a, Dv[i] + 8 * w, 8);
+        memcpy(&b, Dv[j] + 8 * w, 8);
+        d += __builtin_popcountll(a ^ b);
+      }
+      dist[(size_t)i * N + j] = dist[(size_t)j * N + i] = d;
+    }
+  }
+  const int m = (int)(0.5 * (N - 1));
+  int best = INT_MAX, bi = 0;
+  for (int i = 0; i < N; i++) {
+    std::copy(dist + (size_t)i * N, dist + (size_t)(i + 1) * N, v);
+    std::nth_element(v, v + m, v + N);
+    if (v[m] < best) {
+      best = v[m];
       bi = i;
     }
   }
@@ -641,7 +676,7 @@ void MapEngine::gpu_flush_pool(hipStream_t st) {
 // ------------------------------------------------------------------ map dump (tests)
 void MapEngine::dump(int32_t* sizes, const mmt_map_dump_arrays* out) const {
   long nobs = 0, nconn = 0, nord = 0, nchild = 0, nslots = 0;
-  for (const MPoint& p : pts_) nobs += (long)p.obs.size();
+  for (size_t j = 0; j < pts_.size(); j++) nobs += (long)pts_[j].obs.size();
   for (const KFrame& K : kfs_) {
     nconn += (long)K.conn.size();
     nord += (long)K.ordered.size();
@@ -1076,8 +1111,10 @@ bool MapEngine::need_new_keyframe(const MapFrameH& C) {  // Tracking::NeedNewKey
 }
 
 void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracking.cc:3333-3414
+  double tb = prof_on_ ? now_us() : 0;
   const int kf = new_keyframe(C, Tcw);
   kf_store_add(kf);
+  blk_time(0, tb);
   refKF_ = kf;
   C.refKF = kf;
   std::vector<std::pair<float, int>> v;
@@ -1110,6 +1147,7 @@ void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracki
       if (v[j].first > cam_.thDepth && nPoints > 200) break;
     }
   }
+  blk_time(1, tb);
   snapKF_ = kf;
   memcpy(snapTwc_, kfs_[kf].Twc, sizeof(snapTwc_));
   const double tp = prof_on_ ? now_us() : 0;
