@@ -200,7 +200,9 @@ void MapEngine::fuse_launch(const std::vector<int>& kft_kf, const std::vector<Fu
   const int nq = (int)q.size();
   if (nq == 0) return;
   const double t0 = prof_on_ ? now_us() : 0;
+  double tq = t0;
   gpu_flush_pool(lm_s_);
+  blk_time(10, tq);
   const size_t tb = al16(sizeof(FuseKF) * kft_kf.size());
   grow_dev(d_fup_, h_fup_, fup_cap_, tb + sizeof(FuseQuery) * (size_t)nq);
   {
@@ -238,7 +240,9 @@ void MapEngine::fuse_launch(const std::vector<int>& kft_kf, const std::vector<Fu
                    d_pool_desc_, c, d_fres_, lm_s_);
   MMT_HIP(hipMemcpyAsync(h_fres_, d_fres_, sizeof(int2) * (size_t)nq, hipMemcpyDeviceToHost,
                          lm_s_));
+  blk_time(11, tq);
   MMT_HIP(hipStreamSynchronize(lm_s_));
+  blk_time(12, tq);
   memcpy(res, h_fres_, sizeof(int2) * (size_t)nq);
   mstats_.fuse_launches++;
   mstats_.fuse_queries += nq;
@@ -284,7 +288,9 @@ void MapEngine::fuse_sequence(const std::vector<int>& kfl, const std::vector<int
       ver.push_back(mp(h).desc_ver);
     }
   std::vector<int2> res(q.size());
+  double tb = prof_on_ ? prof_now_us() : 0;
   fuse_launch(kfl, q, res.data());
+  tb = prof_on_ ? prof_now_us() : 0;
   for (int t = 0; t < nk; t++) {
     const int kf = kfl[t];
     for (int i = 0; i < np; i++) {
@@ -318,6 +324,7 @@ void MapEngine::fuse_sequence(const std::vector<int>& kfl, const std::vector<int
       fuse_apply(kf, h, res[qi].x, res[qi].y);
     }
   }
+  blk_time(13, tb);
 }
 
 // ------------------------------------------------------------------ LocalMapping steps

@@ -127,7 +127,7 @@ struct MappingStats {
   double lm_us = 0, ba_us = 0, fuse_us = 0;  // host wall time (MMT_MAP_PROFILE)
   // finer host wall times of the keyframe path (MMT_MAP_PROFILE; printed at destruction)
   double kfnew_us = 0, pnk_us = 0, sin_us = 0, basolve_us = 0, cull_us = 0, lmsync_us = 0;
-  static constexpr int kBlk = 10;  // finer blocks of the keyframe path (names in ~MapEngine)
+  static constexpr int kBlk = 14;  // finer blocks of the keyframe path (names in ~MapEngine)
   double blk_us[kBlk] = {};
   long n_lm = 0;
 };
@@ -297,6 +297,8 @@ class MapEngine {
   int refKF_ = -1;
   std::vector<int> localKFs_, localPts_, recent_, dirty_;
   std::vector<std::pair<float, int>> far_;  // UpdateLastFrame's far keys (scratch)
+  std::vector<uint32_t> sort_key_;  // CreateNewKeyFrame's depth sort (scratch)
+  std::vector<int> sort_idx_, sort_tmp_;
   float Tlr_[16];
   bool hasTlr_ = false;
   // the keyframe this frame created and its pose before its LocalMapping ran: the reference's

@@ -84,7 +84,8 @@ MapEngine::~MapEngine() {
               mstats_.lm_us / n, mstats_.kfnew_us / n);
       static const char* bn[MappingStats::kBlk] = {
           "new keyframe + store", "new points", "SIN targets", "SIN fuse 1", "SIN candidates",
-          "SIN fuse 2", "SIN point updates", "SIN connections", "BA graph", "BA apply"};
+          "SIN fuse 2", "SIN point updates", "SIN connections", "BA graph", "BA apply",
+          "Fuse pool flush", "Fuse enqueue", "Fuse wait", "Fuse apply (+ relaunches)"};
       fprintf(stderr, "[mmt localmapping profile] per keyframe, us:");
       for (int k = 0; k < MappingStats::kBlk; k++)
         fprintf(stderr, " %s %.1f%s", bn[k], mstats_.blk_us[k] / n,
@@ -1117,15 +1118,38 @@ void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracki
   blk_time(0, tb);
   refKF_ = kf;
   C.refKF = kf;
-  std::vector<std::pair<float, int>> v;
-  v.reserve(C.n);
+  // the keys with depth sorted by (depth, index): a stable LSD radix sort on the depths' bits
+  // (positive floats order as their bit patterns) over the keys in index order, 3 x 11 bits
+  std::vector<uint32_t>& key = sort_key_;
+  std::vector<int>& v = sort_idx_;
+  std::vector<int>& tmp = sort_tmp_;
+  key.clear();
+  v.clear();
   for (int i = 0; i < C.n; i++)
-    if (C.depth[i] > 0) v.push_back({C.depth[i], i});
+    if (C.depth[i] > 0) {
+      uint32_t b;
+      memcpy(&b, &C.depth[i], 4);
+      key.push_back(b);
+      v.push_back(i);
+    }
   if (!v.empty()) {
-    std::sort(v.begin(), v.end());
+    const int nv = (int)v.size();
+    std::vector<int> pos(nv);  // position of each entry's key
+    for (int k = 0; k < nv; k++) pos[k] = k;
+    tmp.resize(nv);
+    for (int pass = 0; pass < 3; pass++) {
+      uint32_t cnt[2049];
+      memset(cnt, 0, sizeof(cnt));
+      const int sh = 11 * pass;
+      for (int k = 0; k < nv; k++) cnt[((key[pos[k]] >> sh) & 0x7FF) + 1]++;
+      for (int b = 0; b < 2048; b++) cnt[b + 1] += cnt[b];
+      for (int k = 0; k < nv; k++) tmp[cnt[(key[pos[k]] >> sh) & 0x7FF]++] = pos[k];
+      pos.swap(tmp);
+    }
     int nPoints = 0;
-    for (size_t j = 0; j < v.size(); j++) {
-      const int i = v[j].second;
+    for (int j = 0; j < nv; j++) {
+      const int i = v[pos[j]];
+      const float depth_i = C.depth[i];
       bool create = false;
       if (C.mps[i] < 0) {
         create = true;
@@ -1144,7 +1168,7 @@ void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracki
         C.mps[i] = h;
       }
       nPoints++;
-      if (v[j].first > cam_.thDepth && nPoints > 200) break;
+      if (depth_i > cam_.thDepth && nPoints > 200) break;
     }
   }
   blk_time(1, tb);
