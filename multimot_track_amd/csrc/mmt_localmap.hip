@@ -281,6 +281,7 @@ void MapEngine::fuse_sequence(const std::vector<int>& kfl, const std::vector<int
   std::vector<int> ver;
   for (int t = 0; t < nk; t++)
     for (int i = 0; i < np; i++) {
+      if (t == 0 && i + 8 < np) prefetch_point(pts[i + 8]);
       const int h = pts[i];
       if (h < 0 || mp(h).bad || mp(h).obs_index(kfl[t]) >= 0) continue;
       qidx[(size_t)t * np + i] = (int)q.size();
@@ -366,7 +367,9 @@ void MapEngine::search_in_neighbors(int kf) {  // LocalMapping::SearchInNeighbor
   fuse_sequence(std::vector<int>{kf}, cands);
   blk_time(5, tb);
   const std::vector<int> now = kfs_[kf].mps;
-  for (int h : now) {
+  for (size_t j = 0; j < now.size(); j++) {
+    if (j + 8 < now.size()) prefetch_point(now[j + 8]);
+    const int h = now[j];
     if (h < 0 || mp(h).bad) continue;
     compute_distinctive(h);
     update_normal_depth(h);

@@ -195,6 +195,15 @@ class MapEngine {
     t = n;
   }
   static double prof_now_us();
+  // host prefetch of map point h's record (loops over point lists walk a 100k-point map in
+  // random order: one cache miss per record otherwise); MMT_NO_PREFETCH builds without it (A/B)
+  void prefetch_point(int h) const {
+#ifndef MMT_NO_PREFETCH
+    if (h >= 0 && h < kTemp && (size_t)h < pts_.size()) __builtin_prefetch(&pts_[h]);
+#else
+    (void)h;
+#endif
+  }
   // test knob: KeyFrameCulling's redundancy ratio (0.9 in the reference, LocalMapping.cc:697)
   void set_cull_ratio(double r) { cull_ratio_ = r; }
   // the map as flat arrays (mmt_map_dump, include/mmt.h): sizes[7]; arrays written when out != 0

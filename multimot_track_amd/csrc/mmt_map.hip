@@ -656,6 +656,7 @@ void MapEngine::gpu_flush_pool(hipStream_t st) {
     h_up_ = pinned<PoolUpdate>(up_cap_);
   }
   for (int q = 0; q < nd; q++) {
+    if (q + 8 < nd) prefetch_point(dirty_[q + 8]);
     const int h = dirty_[q];
     MPoint& p = pts_[h];
     PoolUpdate& u = h_up_[q];
