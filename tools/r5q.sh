@@ -1,0 +1,9 @@
+# Round-5 verification: full GPU suite, the default bench line, and its rocprofv3 kernel summary
+set -e
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > gpurun_out/r5q_suite.log 2>&1 || { tail -40 gpurun_out/r5q_suite.log; exit 1; }
+tail -2 gpurun_out/r5q_suite.log
+timeout -k 10 600 python bench.py > gpurun_out/r5q_bench.json 2> gpurun_out/r5q_bench.err || { tail -20 gpurun_out/r5q_bench.err; exit 1; }
+cat gpurun_out/r5q_bench.json
