@@ -144,6 +144,10 @@ class OrbEngine {
   // (round 5): batch 1 0.124 / 0.140 ms, 4 0.136 / 0.154, 16 0.202 / 0.218, 32 0.297 / 0.300,
   // 64 0.544 / 0.503, 128 1.029 / 0.919
   int pyr_max_frames_ = 32;
+  // XCD-contiguous workgroup order (MMT_ORB_XCD bits): 1 k_resize, 2 k_blur.  Blur only by
+  // default: its FETCH 131 -> 105 MB per 128-frame window at the same time; the resize chain
+  // fetches 101 -> 89 MB but runs 10 us slower (window 0.932 against 0.922 ms, round 5)
+  int xcd_order_ = 2;
   PyrBand* d_pyr_bands_ = nullptr;
   PyrArgs pyr_args_{};
   int sched_ = 0;  // MMT_ORB_SCHED=2: one stream (standalone kernel times for profiling)

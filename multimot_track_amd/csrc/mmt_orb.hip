@@ -110,13 +110,27 @@ constexpr int kResizeStage = 16;   // staging dwords per thread issued together
 __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                 int src_off, int sw, int dst_off, int dw, int dh,
                                                 const ResizeX* __restrict__ xt,
-                                                const ResizeY* __restrict__ yt, int lds_pitch) {
+                                                const ResizeY* __restrict__ yt, int lds_pitch,
+                                                int xcd_order) {
   extern __shared__ __attribute__((aligned(16))) uint8_t rs_lds[];
   const int tid = threadIdx.x;
-  uint8_t* base = pyr + (size_t)blockIdx.z * pyr_stride;
+  // (column block, band, frame) from the workgroup index with contiguous runs per XCD (as
+  // fast_job): vertically adjacent bands, which stage overlapping source rows, share an L2
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  {
+    const int gx = gridDim.x, gy = gridDim.y, total = gx * gy * gridDim.z;
+    if (xcd_order && (total & 7) == 0) {
+      const int lin = (bz * gy + by) * gx + bx;
+      const int j = (lin & 7) * (total >> 3) + (lin >> 3);
+      bx = j % gx;
+      by = (j / gx) % gy;
+      bz = j / (gx * gy);
+    }
+  }
+  uint8_t* base = pyr + (size_t)bz * pyr_stride;
   const uint8_t* src = base + src_off;
-  const int dx0 = blockIdx.x * kResizeCols, dx1 = min(dx0 + kResizeCols, dw);
-  const int y0 = blockIdx.y * kResizeRows, y1 = min(y0 + kResizeRows, dh);
+  const int dx0 = bx * kResizeCols, dx1 = min(dx0 + kResizeCols, dw);
+  const int y0 = by * kResizeRows, y1 = min(y0 + kResizeRows, dh);
   // source window (sx and sy are non-decreasing in dx and dy)
   const int sx_lo = xt[dx0].sx, sx_hi = min(xt[dx1 - 1].sx + 1, sw - 1);
   const int sy_lo = yt[y0].sy0, sy_hi = yt[y1 - 1].sy1;
@@ -1387,17 +1401,21 @@ typedef float f2x __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur, size_t pyr_stride,
                                               const LevelInfo* __restrict__ lv,
-                                              const BlurTile* __restrict__ tiles, int ntiles) {
+                                              const BlurTile* __restrict__ tiles, int ntiles, int xcd_order) {
   const uint32_t T0 = 18, T1 = 34, T2 = 48, T3 = 56;
   const uint32_t W1 = T0 | (T1 << 8) | (T2 << 16) | (T3 << 24);  // bytes x-3+j .. x+j
   const uint32_t W2 = T2 | (T1 << 8) | (T0 << 16);               // bytes x+1+j .. x+3+j, 0
   // wave-uniform (readfirstlane): the tile record, its level and the row arithmetic go to SALU
-  const int tile_id = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  // workgroups of one frame contiguous on one XCD (fast_job): vertically adjacent bands read the
+  // same halo rows from one L2
+  int xg = blockIdx.x, frame = blockIdx.y;
+  if (xcd_order) fast_job(xg, frame);
+  const int tile_id = __builtin_amdgcn_readfirstlane(xg * 4 + (threadIdx.x >> 6));
   if (tile_id >= ntiles) return;
   const int lane = threadIdx.x & 63;
   const BlurTile t = tiles[tile_id];
   const LevelInfo L = lv[t.level];
-  const size_t fo = (size_t)blockIdx.y * pyr_stride + L.off;
+  const size_t fo = (size_t)frame * pyr_stride + L.off;
   const uint8_t* img = pyr + fo;
   uint8_t* dst = blur + fo;
   // first of this lane's four columns; the lane that would hold the row's last 1-3 columns takes
@@ -1945,6 +1963,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   if (const char* e = getenv("MMT_ORB_SCHED")) sched_ = atoi(e);
   if (const char* e = getenv("MMT_FAST_CPW")) fast_cpw_ = std::max(1, std::min(64, atoi(e)));
   if (const char* e = getenv("MMT_PYR_MAX_FRAMES")) pyr_max_frames_ = atoi(e);
+  if (const char* e = getenv("MMT_ORB_XCD")) xcd_order_ = atoi(e);
   total_slots_ = key_off;
   out_slots_ = out_off;
   cap_frame_ = out_off;
@@ -2159,7 +2178,7 @@ void OrbEngine::run_part(int f0, int nframes, hipStream_t stream, hipStream_t si
               nframes);
     hipLaunchKernelGGL(k_resize, grid, dim3(256), rs_lds_[l], st, pyr, pyr_stride_, S.off,
                        S.w, L.off, L.w, L.h, d_xtab_ + xtab_off_[l], d_ytab_ + ytab_off_[l],
-                       rs_pitch_[l]);
+                       rs_pitch_[l], xcd_order_ & 1);
   };
   auto pyramid = [&](hipStream_t st) {  // levels 1..: one k_pyramid launch, or the k_resize chain
     // k_pyramid for small batches, where the chain's seven launches are pure latency; from 64
@@ -2174,7 +2193,7 @@ void OrbEngine::run_part(int f0, int nframes, hipStream_t stream, hipStream_t si
   };
   auto blur = [&](hipStream_t st) {
     hipLaunchKernelGGL(k_blur, dim3((ntiles_ + 3) / 4, nframes), dim3(256), 0, st, pyr,
-                       blurb, pyr_stride_, d_lv_, d_tiles_, ntiles_);
+                       blurb, pyr_stride_, d_lv_, d_tiles_, ntiles_, (xcd_order_ >> 1) & 1);
   };
   auto cells = [&](int l) { return std::make_pair(lv_[l].cell_begin, lv_[l].cell_end); };
   const int NL = nlevels_;
