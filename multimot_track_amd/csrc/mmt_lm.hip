@@ -2168,7 +2168,30 @@ void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, int n_max, hipStre
     const char* e = getenv("MMT_PO_VARIANT");
     return e ? atoi(e) : 2;
   }();
-  if (variant == 2 || variant == 3) {
+  // MMT_PO_WIDE_FIRST (default 1): the variants for the larger counts go first.  They normally
+  // return at once, but a workgroup of 512 threads and 132 KB of LDS that queues behind the
+  // object path's RANSAC grids waited for them to retire (the motion-model solve's no-op
+  // k_pose_opt_l<4> took 5-100 µs, median 64, after its k_pose_opt_l<2>); ahead of it, it is
+  // placed before those grids are launched
+  static const bool wide_first = [] {
+    const char* e = getenv("MMT_PO_WIDE_FIRST");
+    return !(e && atoi(e) == 0);
+  }();
+  if ((variant == 2 || variant == 3) && wide_first) {
+    if (n_max > 2 * kPoThreads)
+      hipLaunchKernelGGL(k_pose_opt_l<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
+                         2 * kPoThreads);
+    if (n_max > 4 * kPoThreads)
+      hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs, 4 * kPoThreads);
+    if (variant == 3) {
+      if (n_max > kPoThreads)
+        hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
+                           kPoThreads);
+      hipLaunchKernelGGL(k_pose_opt_l<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
+    } else {
+      hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
+    }
+  } else if (variant == 2 || variant == 3) {
     // the edge count is known on the device only: every variant whose range meets [0, n_max]
     // is launched and the ones outside the solve's count return at once (n_max is a bound)
     if (variant == 3) {
