@@ -1199,15 +1199,19 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
     if (i > j) S[q] = S[(size_t)j * n6 + i];
   }
   __syncthreads();
-  // Right-looking LDL^T on the lower triangle (row-major), one column per step, one barrier per
-  // step.  At step c every thread has D(c) (Dg) and the column L(., c) (col[c & 1]).  Wave 0 looks
-  // one column ahead: it applies step c's update to column c + 1, takes the pivot D(c + 1) from its
-  // diagonal (lane 0), divides the column by it into col[(c + 1) & 1], and carries the forward
-  // substitution y(i) -= L(i, c) y(c); waves 1.. apply step c's update to the columns right of
-  // c + 1.  Every entry receives the scalar algorithm's operations in the scalar order (the
-  // subtraction of (L(i, c) L(j, c)) D(c) for c ascending, then the division by D(j)), as the CPU
-  // checker's left-looking loops, and so does y: the factors and y are bit-identical to it.
-  // Replaces a blocked version with a one-wave diagonal block and three barriers per keyframe.
+  // Right-looking LDL^T on the lower triangle (row-major), TWO columns per step (n6 is a multiple
+  // of 6), one barrier per step.  At the step of the pair (a, a + 1) every thread has D(a), D(a + 1)
+  // (Dg) and the columns L(., a), L(., a + 1) (pair slot (a / 2) & 1 of colbuf).  Wave 0 looks one
+  // pair ahead: it applies the pair's updates to columns a + 2 and a + 3, takes their pivots,
+  // divides them into the other slot (column a + 3 also receiving column a + 2's update first), and
+  // carries the forward substitution y(i) -= L(i, c) y(c) for c = a, a + 1; waves 1.. apply the
+  // pair's updates to the columns right of a + 3.  Every entry receives the scalar algorithm's
+  // operations in the scalar order (the subtraction of (L(i, c) L(j, c)) D(c) for c ascending, then
+  // the division by D(j)), as the CPU checker's left-looking loops, and so does y: the factors and
+  // y are bit-identical to it.  Values every lane needs (pivots, L(a + 3, a + 2), y(a + 1)) are
+  // computed redundantly by every lane from the same operands (no cross-lane traffic).  Halves the
+  // barriers of the one-column version (MMT_BA_LDL1 builds keep that one).
+#ifdef MMT_BA_LDL1
   __shared__ double s_col[2 * kLdsRows];
   double* col = n6 <= kLdsRows ? s_col : w.vec + 3 * (size_t)n6;  // [2][n6]
   bool ok = true;
@@ -1236,7 +1240,6 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
       double* ln = col + (size_t)((c + 1) & 1) * n6;
       const double lnc = lc[c + 1];  // L(c + 1, c)
       const double yc = yv[c];
-      // rows c + 1 + lane (+ 64 ...): lane 0 of the first pass holds the new pivot
       double piv = 0;
       for (int k0 = 0; c + 1 + k0 < n6; k0 += 64) {
         const int i = c + 1 + k0 + lane;
@@ -1259,7 +1262,6 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
         if (piv == 0) s_ok = 0;
       }
     } else {
-      // step c's update of the trailing triangle c + 2 <= j <= i < n6, one entry per thread
       const int m = n6 - c - 2, nq = m * (m + 1) / 2;
       for (int q = tid - 64; q < nq; q += kMkSolveThreads - 64) {
         int ii = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
@@ -1272,13 +1274,112 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
     __syncthreads();
     if (s_ok == 0) ok = false;
   }
+  const bool y_last = false;
+#else
+  __shared__ double s_col[4 * kLdsRows];
+  double* colbuf = n6 <= kLdsRows ? s_col : w.vec + 3 * (size_t)n6;  // [2 slots][2 columns][n6]
+  bool ok = true;
+  pt[2] = wall_clock64();
+  if (wave == 0) {  // the first pair: columns 0 and 1, y = b
+    double* l0 = colbuf;
+    double* l1 = colbuf + n6;
+    const double d0 = S[0];
+    const double l10 = S[(size_t)n6] / d0;         // L(1, 0)
+    const double d1 = S[(size_t)n6 + 1] - l10 * l10 * d0;  // D(1)
+    for (int i = lane; i < n6; i += 64) {
+      yv[i] = bs[i];
+      if (i > 0) {
+        const double l = S[(size_t)i * n6] / d0;
+        l0[i] = l;
+        S[(size_t)i * n6] = l;
+        if (i > 1) {
+          const double l_1 = (S[(size_t)i * n6 + 1] - l * l10 * d0) / d1;
+          l1[i] = l_1;
+          S[(size_t)i * n6 + 1] = l_1;
+        }
+      }
+    }
+    if (lane == 0) {
+      Dg[0] = d0;
+      Dg[1] = d1;
+      S[(size_t)n6 + 1] = d1;
+      if (d0 == 0 || d1 == 0) s_ok = 0;
+    }
+  }
+  __syncthreads();
+  if (s_ok == 0) ok = false;
+  for (int a = 0; ok && a + 2 < n6; a += 2) {
+    const double da = Dg[a], da1 = Dg[a + 1];
+    const double* la = colbuf + (size_t)((a >> 1) & 1) * 2 * n6;  // L(., a)
+    const double* la1 = la + n6;                                  // L(., a + 1)
+    if (wave == 0) {
+      double* lb = colbuf + (size_t)(((a >> 1) + 1) & 1) * 2 * n6;  // L(., a + 2)
+      double* lb1 = lb + n6;                                        // L(., a + 3)
+      const int b = a + 2, b1 = a + 3;
+      // the uniform operands: the pair's entries in rows b, b1 and the two new pivots
+      const double lba = la[b], lb1a = la[b1], lba1 = la1[b], lb1a1 = la1[b1];
+      const double piv2 = (S[(size_t)b * n6 + b] - lba * lba * da) - lba1 * lba1 * da1;
+      const double l32 = ((S[(size_t)b1 * n6 + b] - lb1a * lba * da) - lb1a1 * lba1 * da1) / piv2;
+      const double piv3 =
+          ((S[(size_t)b1 * n6 + b1] - lb1a * lb1a * da) - lb1a1 * lb1a1 * da1) - l32 * l32 * piv2;
+      // forward substitution: y(a + 1) -= L(a + 1, a) y(a); rows > a + 1 take both columns
+      const double ya = yv[a];
+      const double ya1 = yv[a + 1] - la[a + 1] * ya;
+      if (lane == 0) yv[a + 1] = ya1;
+      for (int i = b + lane; i < n6; i += 64) {
+        const double lia = la[i], lia1 = la1[i];
+        yv[i] = (yv[i] - lia * ya) - lia1 * ya1;
+        if (i > b) {
+          const double l2 = ((S[(size_t)i * n6 + b] - lia * lba * da) - lia1 * lba1 * da1) / piv2;
+          lb[i] = l2;
+          S[(size_t)i * n6 + b] = l2;
+          if (i > b1) {
+            const double l3 =
+                (((S[(size_t)i * n6 + b1] - lia * lb1a * da) - lia1 * lb1a1 * da1) - l2 * l32 * piv2) /
+                piv3;
+            lb1[i] = l3;
+            S[(size_t)i * n6 + b1] = l3;
+          }
+        }
+      }
+      if (lane == 0) {
+        S[(size_t)b * n6 + b] = piv2;
+        S[(size_t)b1 * n6 + b1] = piv3;
+        Dg[b] = piv2;
+        Dg[b1] = piv3;
+        if (piv2 == 0 || piv3 == 0) s_ok = 0;
+      }
+    } else {
+      // the pair's update of the trailing triangle a + 4 <= j <= i < n6, one entry per thread
+      const int m = n6 - a - 4, nq = m * (m + 1) / 2;
+      for (int q = tid - 64; q < nq; q += kMkSolveThreads - 64) {
+        int ii = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+        while (ii * (ii + 1) / 2 > q) ii--;
+        while ((ii + 1) * (ii + 2) / 2 <= q) ii++;
+        const int i = a + 4 + ii, j = a + 4 + (q - ii * (ii + 1) / 2);
+        double v = S[(size_t)i * n6 + j];
+        v -= la[i] * la[j] * da;
+        v -= la1[i] * la1[j] * da1;
+        S[(size_t)i * n6 + j] = v;
+      }
+    }
+    __syncthreads();
+    if (s_ok == 0) ok = false;
+  }
+  // the last pair's column n6 - 2 still owes y(n6 - 1) its term (the loop's last step carried
+  // columns n6 - 4 and n6 - 3; no optimised keyframe: n6 = 0)
+  const bool y_last = n6 >= 2;
+#endif
   pt[3] = wall_clock64();
   if (!ok) {
     if (tid == 0) s_ok = 0;
   } else if (wave == 0) {
     // y / D and the backward substitution, y in registers (lane i: rows i, i + 64), y[r]
     // broadcast by readlane, L(r, i) read at (r, i): coalesced rows
-    double y0 = lane < n6 ? yv[lane] : 0.0, y1 = lane + 64 < n6 ? yv[lane + 64] : 0.0;
+    // (every lane computes the last row's final y, the lane of that row takes it)
+    const double ylast = y_last ? yv[n6 - 1] - S[(size_t)(n6 - 1) * n6 + n6 - 2] * yv[n6 - 2] : 0.0;
+    auto y_at = [&](int i) { return y_last && i == n6 - 1 ? ylast : yv[i]; };
+    double y0 = lane < n6 ? y_at(lane) : 0.0, y1 = lane + 64 < n6 ? y_at(lane + 64) : 0.0;
     if (n6 <= 128) {
       if (lane < n6) y0 /= Dg[lane];
       if (lane + 64 < n6) y1 /= Dg[lane + 64];
@@ -1290,7 +1391,7 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
       if (lane < n6) w.x[lane] = y0;
       if (lane + 64 < n6) w.x[lane + 64] = y1;
     } else {
-      for (int i = lane; i < n6; i += 64) yv[i] /= Dg[i];
+      for (int i = lane; i < n6; i += 64) yv[i] = y_at(i) / Dg[i];
       wave_sync_lds();
       for (int r = n6 - 1; r > 0; r--) {
         const double yr = yv[r];
@@ -1640,7 +1741,7 @@ size_t ba2_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt, int n_blk,
          a(8 * 3 * (size_t)n_edge) + a(8 * 36 * (size_t)n_edge) + a(8 * 54 * (size_t)n_edge) +
          a(8 * 18 * (size_t)n_edge) + a(8 * 6 * (size_t)n_edge) + a(8 * 36 * (size_t)n_opt) +
          a(8 * 6 * (size_t)n_opt) + a(8 * 6 * (size_t)n_opt) + a(8 * 36 * (size_t)n_blk) +
-         a(8 * (n6 + 3 * (size_t)n_pt)) + a(8 * n6 * n6) + a(8 * 3 * n6) + 2 * a(8 * 2 * (size_t)gP) +
+         a(8 * (n6 + 3 * (size_t)n_pt)) + a(8 * n6 * n6) + a(8 * 7 * n6) + 2 * a(8 * 2 * (size_t)gP) +
          a((size_t)n_edge) + a(4 * (size_t)n_edge) + a((size_t)n_kf) + a((size_t)n_pt) + a(16) + 64;
 }
 
@@ -1872,7 +1973,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.cvpart = (double*)take(8 * 6 * kitem.size());
     w.x = (double*)take(8 * ((size_t)n6 + 3 * (size_t)nP));
     w.S = (double*)take(8 * (size_t)n6 * n6);
-    w.vec = (double*)take(8 * 5 * (size_t)n6);  // b, D, y, two L columns (p3)
+    w.vec = (double*)take(8 * 7 * (size_t)n6);  // b, D, y, four L columns (p3)
     w.linpart = (double*)take(8 * 2 * (size_t)gP);
     w.p4part = (double*)take(8 * 2 * (size_t)gP);
     w.p4cnt = (unsigned*)take(16);
