@@ -1383,10 +1383,26 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
     if (n6 <= 128) {
       if (lane < n6) y0 /= Dg[lane];
       if (lane + 64 < n6) y1 /= Dg[lane + 64];
-      for (int r = n6 - 1; r > 0; r--) {
-        const double yr = r < 64 ? lane_value(y0, r) : lane_value(y1, r - 64);
-        if (lane < r) y0 -= S[(size_t)r * n6 + lane] * yr;
-        if (lane + 64 < r) y1 -= S[(size_t)r * n6 + lane + 64] * yr;
+      // rows in blocks of 4: the block's L loads (clamped, unconditional) go out together ahead
+      // of its four dependent readlane + update steps
+      const int c0 = min(lane, n6 - 1), c1 = min(lane + 64, n6 - 1);
+      for (int r = n6 - 1; r > 0; r -= 4) {
+        double l0[4], l1[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int rr = max(r - k, 0);
+          l0[k] = S[(size_t)rr * n6 + c0];
+          l1[k] = S[(size_t)rr * n6 + c1];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int rr = r - k;
+          if (rr > 0) {
+            const double yr = rr < 64 ? lane_value(y0, rr) : lane_value(y1, rr - 64);
+            if (lane < rr) y0 -= l0[k] * yr;
+            if (lane + 64 < rr) y1 -= l1[k] * yr;
+          }
+        }
       }
       if (lane < n6) w.x[lane] = y0;
       if (lane + 64 < n6) w.x[lane + 64] = y1;
