@@ -255,6 +255,8 @@ class Tracker {
     FlowSolveDesc descs[kMaxObj];
     ObjResults r;
   };
+  static constexpr size_t kObjStatsBytes = sizeof(LabelStats) * kMaxLabel + sizeof(int) * kMaxLabel * kMaxLabel;
+  static constexpr size_t kObjPnpBytes = sizeof(PnPObject) * kMaxObj + sizeof(int) * kMaxObj * 5 * kRansacIters;
   ObjHost* oh_[kObjSlots] = {};
   ObjResults* d_r_[kObjSlots] = {};
   double* d_Rt_[kObjSlots] = {};
@@ -295,7 +297,6 @@ class Tracker {
   // inlier counts and masks), shared by the object slots: only the RANSAC kernels touch it, and
   // they all run on oa_, so stream order keeps one frame's RANSAC off another's scratch.
   struct PnPScratch {
-    int* subsets;
     double* models;
     double* hrec;
     double* hout;

@@ -226,11 +226,19 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     MMT_HIP(hipMemset(F.st.count, 0, sizeof(int)));
     MMT_HIP(hipMemset(F.ob.count, 0, sizeof(int)));
   }
+  static_assert(offsetof(ObjHost, hist) == offsetof(ObjHost, stats) + sizeof(LabelStats) * kMaxLabel &&
+                    offsetof(ObjHost, err) - offsetof(ObjHost, stats) == kObjStatsBytes,
+                "ObjHost: stats, hist contiguous (one download)");
+  static_assert(offsetof(ObjHost, subsets) == offsetof(ObjHost, po) + sizeof(PnPObject) * kMaxObj &&
+                    sizeof(ObjHost::subsets) == sizeof(int) * kMaxObj * 5 * kRansacIters,
+                "ObjHost: po, subsets contiguous (one upload)");
   for (int q = 0; q < kObjSlots; q++) {
     d_obj_label_[q] = alloc<int32_t>(ocap_);
     d_members_[q] = alloc<int>((size_t)kMaxLabel * ocap_);
-    d_stats_[q] = alloc<LabelStats>(kMaxLabel);
-    d_hist_[q] = alloc<int>(kMaxLabel * kMaxLabel);
+    // the grouping statistics and the label histogram in one block laid out as ObjHost's, brought
+    // back by one copy
+    d_stats_[q] = (LabelStats*)alloc<uint8_t>(kObjStatsBytes);
+    d_hist_[q] = (int*)((uint8_t*)d_stats_[q] + sizeof(LabelStats) * kMaxLabel);
   }
   d_err_ = alloc<int>(1);
   MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
@@ -251,7 +259,9 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // PnP
   mask_words_ = (ocap_ + 63) / 64;
   for (int q = 0; q < kObjSlots; q++) {
-  d_pnp_[q] = alloc<PnPObject>(kMaxObj);
+  // the PnP records and the RANSAC subset draws in one block laid out as ObjHost's po / subsets,
+  // uploaded by one copy
+  d_pnp_[q] = (PnPObject*)alloc<uint8_t>(kObjPnpBytes);
   d_r_[q] = alloc<ObjResults>(1);
   d_Rt_[q] = alloc<double>(12 * kMaxObj);
   d_descs3_[q] = alloc<FlowSolveDesc>(kMaxObj);
@@ -274,7 +284,6 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   }
   for (int o = 0; o < kMaxObj; o++) {
     PnPScratch& r = pnp_scr_[o];
-    r.subsets = alloc<int>(5 * kRansacIters);
     r.models = alloc<double>(6 * kRansacIters);
     r.hrec = alloc<double>((size_t)kHypRec * kRansacIters);
     r.hout = alloc<double>((size_t)3 * kHypOut * kRansacIters);
@@ -1090,8 +1099,7 @@ void Tracker::obj_stage_a_launch(ObjFrame& F) {
   g.err = d_err_;
   launch_obj_group(g, st);
   ObjHost& H = *oh_[q];
-  MMT_HIP(hipMemcpyAsync(H.stats, d_stats_[q], sizeof(H.stats), hipMemcpyDeviceToHost, st));
-  MMT_HIP(hipMemcpyAsync(H.hist, d_hist_[q], sizeof(H.hist), hipMemcpyDeviceToHost, st));
+  MMT_HIP(hipMemcpyAsync(H.stats, d_stats_[q], kObjStatsBytes, hipMemcpyDeviceToHost, st));
   MMT_HIP(hipMemcpyAsync(&H.err, d_err_, sizeof(int), hipMemcpyDeviceToHost, st));
   MMT_HIP(hipEventRecord(ev_grp_[q], st));
 }
@@ -1176,6 +1184,7 @@ void Tracker::obj_stage_a_decide(ObjFrame& F) {
     PnPBuf& b = pnp_[q][i];
     const PnPScratch& r = pnp_scr_[i];
     PnPObject& o = F.po[i];
+    int* d_sub = (int*)((uint8_t*)d_pnp_[q] + sizeof(PnPObject) * kMaxObj) + (size_t)i * 5 * kRansacIters;
     memset(&o, 0, sizeof(o));
     o.n = &d_stats_[q][l].members;
     o.members = d_members_[q] + (size_t)l * ocap_;
@@ -1189,9 +1198,7 @@ void Tracker::obj_stage_a_decide(ObjFrame& F) {
     F.members[i] = stats[l].members;
     const std::vector<int>& sub = cached_subsets(std::max(stats[l].members, 1));
     memcpy(H.subsets[i], sub.data(), sizeof(H.subsets[i]));
-    MMT_HIP(hipMemcpyAsync(r.subsets, H.subsets[i], sizeof(H.subsets[i]), hipMemcpyHostToDevice,
-                           st));
-    o.subsets = r.subsets;
+    o.subsets = d_sub;
     for (size_t k = 0; k < Ls.nModLabel.size(); k++)
       if (Ls.nModLabel[k] == LabId[i]) {
         F.PreObjID[i] = (int)k;
@@ -1213,7 +1220,9 @@ void Tracker::obj_stage_a_decide(ObjFrame& F) {
     o.result = b.result;
     o.Rt = b.Rt;
   }
-  MMT_HIP(hipMemcpyAsync(d_pnp_[q], F.po, sizeof(PnPObject) * nobj, hipMemcpyHostToDevice, st));
+  // the records (all kMaxObj) and the first nobj subset draws behind them
+  MMT_HIP(hipMemcpyAsync(d_pnp_[q], H.po, sizeof(PnPObject) * kMaxObj + sizeof(H.subsets[0]) * nobj,
+                         hipMemcpyHostToDevice, st));
   launch_pnp(d_pnp_[q], nobj, kRansacIters, st);
   // ev_ransac_[q] is recorded by stage B, behind the D3 descriptors' copy on this stream
 }
