@@ -836,10 +836,24 @@ __device__ __forceinline__ int ba2_diag_q(int r) { return 6 * r - r * (r - 1) / 
 
 // keyframe a's sum of pose term q over its items, in item order (k_ba2_p1 and k_ba2_p3 both
 // compute H_pp this way: the same bits)
-__device__ __forceinline__ double ba2_hsum(const BAWork2& w, int a, int q) {
+// base[stride * b] + ... + base[stride * (e - 1)] added in index order from 0 (the scalar sum's
+// rounding), the loads of U items issued together (clamped indices, no branch between them)
+template <int U = 8>
+__device__ __forceinline__ double ordered_sum(const double* base, size_t stride, int b, int e) {
   double s = 0;
-  for (int it = w.kitem_start[a]; it < w.kitem_start[a + 1]; it++) s += w.Hpart[27 * (size_t)it + q];
+  for (int it = b; it < e; it += U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = base[stride * (size_t)min(it + u, e - 1)];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (it + u < e) s += v[u];
+  }
   return s;
+}
+
+__device__ __forceinline__ double ba2_hsum(const BAWork2& w, int a, int q) {
+  return ordered_sum(w.Hpart + q, 27, w.kitem_start[a], w.kitem_start[a + 1]);
 }
 
 // computed by wave 0 (lanes over the point workgroups and the (keyframe, diagonal) pairs) and
@@ -1171,15 +1185,11 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
   }
   for (int q = tid; q < d.n_opt * 6; q += kMkSolveThreads) {
     const int a = q / 6, k = q % 6;
-    double v = 0;
-    for (int it = w.kitem_start[a]; it < w.kitem_start[a + 1]; it++) v += w.cvpart[6 * (size_t)it + k];
-    w.cvs[q] = v;
+    w.cvs[q] = ordered_sum(w.cvpart + k, 6, w.kitem_start[a], w.kitem_start[a + 1]);
   }
   for (int q = tid; q < d.n_blk * 36; q += kMkSolveThreads) {
     const int bk = q / 36, k = q % 36;
-    double v = 0;
-    for (int it = w.bitem_start[bk]; it < w.bitem_start[bk + 1]; it++) v += w.Spart[36 * (size_t)it + k];
-    w.Sblk[q] = v;
+    w.Sblk[q] = ordered_sum(w.Spart + k, 36, w.bitem_start[bk], w.bitem_start[bk + 1]);
   }
   for (int q = tid; q < n6 * n6; q += kMkSolveThreads) S[q] = 0;
   __syncthreads();
