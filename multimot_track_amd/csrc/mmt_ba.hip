@@ -1433,7 +1433,8 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
   // the trial poses: exp(x_p) * pose for the round's optimised keyframes, the others unchanged
   const DSE3* cur = w.pose + (size_t)cb * d.n_kf;
   DSE3* tri = w.pose + (size_t)(1 - cb) * d.n_kf;
-  for (int k = tid; k < d.n_kf; k += kMkSolveThreads) {
+  // (waves 1..: the exponentials run beside wave 0's sums below)
+  for (int k = tid - 64; tid >= 64 && k < d.n_kf; k += kMkSolveThreads - 64) {
     const int a = d.opt_of[k];
     if (a >= 0 && w.kf_act[k]) {
       double u[6];
