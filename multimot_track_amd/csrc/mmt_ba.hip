@@ -1199,15 +1199,16 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
     const int a = d.blk_ab[2 * bk], b = d.blk_ab[2 * bk + 1];
     double base = 0;
     if (a == b) base = w.Hpp[36 * (size_t)a + k] + (r == c ? lambda : 0.0);
-    if (a < b || r <= c) S[(size_t)(6 * a + r) * n6 + 6 * b + c] = base - w.Sblk[36 * (size_t)bk + k];
+    // the upper triangle's entry and its mirror in the lower triangle, which the factorisation reads
+    if (a < b || r <= c) {
+      const double v = base - w.Sblk[36 * (size_t)bk + k];
+      const int i = 6 * a + r, j = 6 * b + c;
+      S[(size_t)i * n6 + j] = v;
+      S[(size_t)j * n6 + i] = v;
+    }
   }
   for (int i = tid; i < n6; i += kMkSolveThreads) bs[i] = w.bp[i] - w.cvs[i];
   if (tid == 0) s_ok = 1;
-  __syncthreads();
-  for (int q = tid; q < n6 * n6; q += kMkSolveThreads) {
-    const int i = q / n6, j = q % n6;
-    if (i > j) S[q] = S[(size_t)j * n6 + i];
-  }
   __syncthreads();
   // Right-looking LDL^T on the lower triangle (row-major), TWO columns per step (n6 is a multiple
   // of 6), one barrier per step.  At the step of the pair (a, a + 1) every thread has D(a), D(a + 1)
@@ -1393,19 +1394,20 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
     if (n6 <= 128) {
       if (lane < n6) y0 /= Dg[lane];
       if (lane + 64 < n6) y1 /= Dg[lane + 64];
-      // rows in blocks of 4: the block's L loads (clamped, unconditional) go out together ahead
-      // of its four dependent readlane + update steps
+      // rows in blocks of kSb: the block's L loads (clamped, unconditional) go out together ahead
+      // of its dependent readlane + update steps
+      constexpr int kSb = 4;  // 8 measured no faster
       const int c0 = min(lane, n6 - 1), c1 = min(lane + 64, n6 - 1);
-      for (int r = n6 - 1; r > 0; r -= 4) {
-        double l0[4], l1[4];
+      for (int r = n6 - 1; r > 0; r -= kSb) {
+        double l0[kSb], l1[kSb];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < kSb; k++) {
           const int rr = max(r - k, 0);
           l0[k] = S[(size_t)rr * n6 + c0];
           l1[k] = S[(size_t)rr * n6 + c1];
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < kSb; k++) {
           const int rr = r - k;
           if (rr > 0) {
             const double yr = rr < 64 ? lane_value(y0, rr) : lane_value(y1, rr - 64);
