@@ -1639,13 +1639,15 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
     double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
     if (w.pt_act[j]) {
       double* xl = &w.x[n6 + 3 * (size_t)j];
+      const double bl3[3] = {bl_c[3 * (size_t)j], bl_c[3 * (size_t)j + 1], bl_c[3 * (size_t)j + 2]};
+      double xv3[3];  // the increment, kept in registers (no read-back of the store)
       if (ok2) {
         // the loads that depend on j alone first (D^-1); an edge's H_pl block only for the edges
         // of the level to an optimised keyframe (ba2_lin_point writes no block for the others)
         double Di[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) Di[q] = w.Dinv[9 * (size_t)j + q];
-        double cl[3] = {bl_c[3 * (size_t)j], bl_c[3 * (size_t)j + 1], bl_c[3 * (size_t)j + 2]};
+        double cl[3] = {bl3[0], bl3[1], bl3[2]};
         for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
           const int a = w.eopt[e];
           if (w.level[e] || a < 0) continue;
@@ -1658,12 +1660,18 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
             for (int r = 0; r < 6; r++) cl[c] += B[3 * r + c] * (-w.x[6 * a + r]);
         }
 #pragma unroll
-        for (int a = 0; a < 3; a++) xl[a] = Di[3 * a] * cl[0] + Di[3 * a + 1] * cl[1] + Di[3 * a + 2] * cl[2];
+        for (int a = 0; a < 3; a++) {
+          xv3[a] = Di[3 * a] * cl[0] + Di[3 * a + 1] * cl[1] + Di[3 * a + 2] * cl[2];
+          xl[a] = xv3[a];
+        }
+      } else {
+#pragma unroll
+        for (int a = 0; a < 3; a++) xv3[a] = xl[a];  // stale (g2o re-applies its _x)
       }
 #pragma unroll
       for (int r = 0; r < 3; r++) {
-        const double xv = xl[r];
-        sc += xv * (lambda * xv + bl_c[3 * (size_t)j + r]);
+        const double xv = xv3[r];
+        sc += xv * (lambda * xv + bl3[r]);
         X[r] += xv;
       }
       if (SPEC) {
