@@ -40,6 +40,11 @@
  *   mmt_local_bundle_adjustment
  *                       <- Optimizer::LocalBundleAdjustment's two optimisation rounds and inlier
  *                          test, Optimizer.cc:3394-3631 (LocalMapping.cc:81-84)
+ *   mmt_load_vocabulary <- System::System's mpVocabulary->loadFromTextFile(strVocFile)
+ *                          System.cc:63-73 (TemplatedVocabulary::loadFromTextFile,
+ *                          Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1424)
+ *   mmt_bow_transform   <- TemplatedVocabulary::transform(feature, word, weight, &node, levelsup)
+ *                          TemplatedVocabulary.h:1218-1259 (Frame::ComputeBoW, Frame.cc:778-786)
  *   mmt_destroy         <- System::Shutdown / delete
  */
 #ifndef MMT_H
@@ -445,6 +450,33 @@ int mmt_map_counters_read(mmt_ctx* ctx, mmt_map_counters* out);
  * (0.9 in the reference, LocalMapping.cc:697; the default).  The synthetic sequences never reach
  * 0.9, so the culling tests lower it to exercise KeyFrame::SetBadFlag. */
 int mmt_set_keyframe_culling_ratio(mmt_ctx* ctx, double ratio);
+
+/* ---- ORB vocabulary ------------------------------------------------------------
+ * System(voc, ...) loads DBoW2's text vocabulary (System.cc:63-73): the header "k L scoring
+ * weighting", then one line per node "parent is_leaf d0 .. d31 weight".  With a vocabulary the
+ * tracker runs the reference's TrackReferenceKeyFrame (SearchByBoW against the reference
+ * keyframe, Tracking.cc:2836-2892), Relocalization (KeyFrameDatabase candidates, SearchByBoW,
+ * PnPsolver, the SearchByProjection(F, KF, ...) rounds; Tracking.cc:3614-3776) and LocalMapping's
+ * CreateNewMapPoints (SearchForTriangulation, LocalMapping.cc:210-456), and keeps the keyframe
+ * database; without one it runs the documented substitutes.  Load it before
+ * the first frame (MMT_ESTATE afterwards).  Scorings L1 / L2 (ORBvoc.txt: L1, TF-IDF); errors:
+ * MMT_EINVAL with mmt_last_error (unreadable file, the reference's header check). */
+int mmt_load_vocabulary(mmt_ctx* ctx, const char* path);
+
+/* Probe of TemplatedVocabulary::transform(feature, id, w, &nid, levelsup) over n descriptors (host
+ * n x 32) on the GPU: word id, word weight (0: stopped) and the node at level L - levelsup. */
+int mmt_bow_transform(mmt_ctx* ctx, const uint8_t* desc, int n, int levelsup, uint32_t* word,
+                      double* weight, uint32_t* node);
+
+/* Counters of the vocabulary path (tests): BoW conversions of frames, TrackReferenceKeyFrame calls
+ * and successes, Relocalization calls and successes, candidate keyframes, PnPsolver poses,
+ * SearchByProjection(F, KF) rounds, triangulated points, SearchForTriangulation matches, database
+ * insertions. */
+typedef struct mmt_bow_counters {
+  int64_t bow_frames, trk, trk_ok, reloc, reloc_ok, reloc_cands, pnp_found, sbp_rounds,
+      triangulated, sft_matches, kfdb;
+} mmt_bow_counters;
+int mmt_bow_counters_read(mmt_ctx* ctx, mmt_bow_counters* out);
 
 /* The tracker's map as flat arrays (no reference counterpart: the map invariant tests and the
  * map-graph parity against the CPU oracle read it).  Keyframes and map points are numbered in

@@ -115,6 +115,12 @@ class MmtMapCounters(ctypes.Structure):
         [("d2_split_fallbacks", ctypes.c_int64), ("n_reparent", ctypes.c_int64)]
 
 
+class MmtBowCounters(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in ("bow_frames", "trk", "trk_ok", "reloc", "reloc_ok",
+                                               "reloc_cands", "pnp_found", "sbp_rounds",
+                                               "triangulated", "sft_matches", "kfdb")]
+
+
 MAP_DUMP_FIELDS = (("kf_i", np.int64, 4), ("kf_T", np.float32, 16), ("kf_mps_start", np.int32, 1),
                    ("kf_mps", np.int32, 1), ("pt_f", np.float32, 5), ("pt_i", np.int32, 5),
                    ("obs_start", np.int32, 1), ("obs_i", np.int32, 3), ("obs_f", np.float32, 4),
@@ -255,6 +261,9 @@ def lib():
         L.mmt_map_counters_read.argtypes = [vp, ctypes.POINTER(MmtMapCounters)]
         L.mmt_map_dump.argtypes = [vp, vp, ctypes.POINTER(MmtMapDumpArrays)]
         L.mmt_set_keyframe_culling_ratio.argtypes = [vp, ctypes.c_double]
+        L.mmt_load_vocabulary.argtypes = [vp, ctypes.c_char_p]
+        L.mmt_bow_transform.argtypes = [vp, vp, i32, i32, vp, vp, vp]
+        L.mmt_bow_counters_read.argtypes = [vp, ctypes.POINTER(MmtBowCounters)]
         L.mmt_set_deferred_objects.argtypes = [vp, i32]
         L.mmt_flush_objects.argtypes = [vp, vp, vp, i32, i32, vp]
         _LIB = L
@@ -618,6 +627,28 @@ class Context:
         self._check(lib().mmt_map_dump(self._h, _p(sz), ctypes.byref(st)))
         del keep
         return out
+
+    def load_vocabulary(self, path):
+        """System(voc, ...): DBoW2 text vocabulary; with it the tracker runs the reference's
+        TrackReferenceKeyFrame, Relocalization and CreateNewMapPoints (mmt_load_vocabulary)."""
+        self._check(lib().mmt_load_vocabulary(self._h, path.encode()))
+
+    def bow_transform(self, desc, levelsup=4):
+        """Per descriptor (word, weight, node at level L - levelsup) on the GPU."""
+        desc = np.ascontiguousarray(desc, np.uint8)
+        n = len(desc)
+        w = np.zeros(max(n, 1), np.uint32)
+        x = np.zeros(max(n, 1), np.float64)
+        nd = np.zeros(max(n, 1), np.uint32)
+        self._check(lib().mmt_bow_transform(self._h, _p(desc), n, levelsup, _p(w), _p(x),
+                                            _p(nd)))
+        return w[:n], x[:n], nd[:n]
+
+    def bow_counters(self):
+        """Counters of the vocabulary path (mmt_bow_counters_read)."""
+        c = MmtBowCounters()
+        self._check(lib().mmt_bow_counters_read(self._h, ctypes.byref(c)))
+        return {k: int(getattr(c, k)) for k, _ in MmtBowCounters._fields_}
 
     def map_counters(self):
         """LocalMapping counters of the context's tracker (mmt_map_counters_read)."""

@@ -1220,78 +1220,13 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
   // operations in the scalar order (the subtraction of (L(i, c) L(j, c)) D(c) for c ascending, then
   // the division by D(j)), as the CPU checker's left-looking loops, and so does y: the factors and
   // y are bit-identical to it.  Values every lane needs (pivots, L(a + 3, a + 2), y(a + 1)) are
-  // computed redundantly by every lane from the same operands (no cross-lane traffic).  Halves the
-  // barriers of the one-column version (MMT_BA_LDL1 builds keep that one).
-#ifdef MMT_BA_LDL1
-  __shared__ double s_col[2 * kLdsRows];
-  double* col = n6 <= kLdsRows ? s_col : w.vec + 3 * (size_t)n6;  // [2][n6]
-  bool ok = true;
-  pt[2] = wall_clock64();
-  if (wave == 0) {  // column 0 and y = b
-    const double d0 = S[0];
-    for (int i = lane; i < n6; i += 64) {
-      yv[i] = bs[i];
-      if (i > 0) {
-        const double l = S[(size_t)i * n6] / d0;
-        col[i] = l;
-        S[(size_t)i * n6] = l;
-      }
-    }
-    if (lane == 0) {
-      Dg[0] = d0;
-      if (d0 == 0) s_ok = 0;
-    }
-  }
-  __syncthreads();
-  if (s_ok == 0) ok = false;
-  for (int c = 0; ok && c + 1 < n6; c++) {
-    const double dc = Dg[c];
-    const double* lc = col + (size_t)(c & 1) * n6;
-    if (wave == 0) {
-      double* ln = col + (size_t)((c + 1) & 1) * n6;
-      const double lnc = lc[c + 1];  // L(c + 1, c)
-      const double yc = yv[c];
-      double piv = 0;
-      for (int k0 = 0; c + 1 + k0 < n6; k0 += 64) {
-        const int i = c + 1 + k0 + lane;
-        double v = 0, lic = 0;
-        if (i < n6) {
-          lic = lc[i];
-          v = S[(size_t)i * n6 + c + 1] - lic * lnc * dc;
-          yv[i] -= lic * yc;
-        }
-        if (k0 == 0) piv = lane_value(v, 0);
-        if (i < n6 && i > c + 1) {
-          const double l = v / piv;
-          ln[i] = l;
-          S[(size_t)i * n6 + c + 1] = l;
-        }
-      }
-      if (lane == 0) {
-        S[(size_t)(c + 1) * n6 + c + 1] = piv;
-        Dg[c + 1] = piv;
-        if (piv == 0) s_ok = 0;
-      }
-    } else {
-      const int m = n6 - c - 2, nq = m * (m + 1) / 2;
-      for (int q = tid - 64; q < nq; q += kMkSolveThreads - 64) {
-        int ii = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
-        while (ii * (ii + 1) / 2 > q) ii--;
-        while ((ii + 1) * (ii + 2) / 2 <= q) ii++;
-        const int i = c + 2 + ii, j = c + 2 + (q - ii * (ii + 1) / 2);
-        S[(size_t)i * n6 + j] -= lc[i] * lc[j] * dc;
-      }
-    }
-    __syncthreads();
-    if (s_ok == 0) ok = false;
-  }
-  const bool y_last = false;
-#else
+  // computed redundantly by every lane from the same operands (no cross-lane traffic).  With no
+  // optimised keyframe (n6 = 0, every keyframe fixed) nothing is factored and s_ok stays 1.
   __shared__ double s_col[4 * kLdsRows];
   double* colbuf = n6 <= kLdsRows ? s_col : w.vec + 3 * (size_t)n6;  // [2 slots][2 columns][n6]
   bool ok = true;
   pt[2] = wall_clock64();
-  if (wave == 0) {  // the first pair: columns 0 and 1, y = b
+  if (wave == 0 && n6 >= 2) {  // the first pair: columns 0 and 1, y = b (n6 = 0: nothing)
     double* l0 = colbuf;
     double* l1 = colbuf + n6;
     const double d0 = S[0];
@@ -1380,7 +1315,6 @@ __global__ __launch_bounds__(kMkSolveThreads) void k_ba2_p3(BADesc d, BAWork2 w)
   // the last pair's column n6 - 2 still owes y(n6 - 1) its term (the loop's last step carried
   // columns n6 - 4 and n6 - 3; no optimised keyframe: n6 = 0)
   const bool y_last = n6 >= 2;
-#endif
   pt[3] = wall_clock64();
   if (!ok) {
     if (tid == 0) s_ok = 0;
@@ -1702,6 +1636,7 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
     s_part[2 * wave] = a;
     s_part[2 * wave + 1] = b;
   }
+  __threadfence();  // release this thread's err / Xt stores to the deciding workgroup
   __syncthreads();
   if (threadIdx.x == 0) {
     double t0 = 0, t1 = 0;
@@ -1713,8 +1648,9 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
     w.p4part[2 * blockIdx.x] = t0;
     w.p4part[2 * blockIdx.x + 1] = t1;
     // the last workgroup to finish takes the trial's decision (k_ba2_p5's work, one launch fewer
-    // per trial): its partials published by an agent-scope release, the count, and the last
-    // one's acquire before it reads every partial
+    // per trial): its partials published by an agent-scope release (every thread's err / Xt
+    // stores were released by their own fence before the barrier above), the count, and the
+    // last one's acquire before it reads every partial
     __threadfence();
     const unsigned done = atomicAdd(w.p4cnt, 1u);
     s_last = done == (unsigned)gridDim.x - 1;

@@ -873,6 +873,69 @@ int mmt_set_keyframe_culling_ratio(mmt_ctx* ctx, double ratio) {
   });
 }
 
+int mmt_load_vocabulary(mmt_ctx* ctx, const char* path) {
+  if (!ctx || !path) return MMT_EINVAL;
+  bool late = false;
+  const int rc = guard(ctx, [&] {
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    ensure_tracker(ctx);
+    if (ctx->tracker.map().n_keyframes() > 0 || ctx->tracker.map().state() != 0) {
+      late = true;
+      return;
+    }
+    std::unique_ptr<mmt::Vocabulary> v(new mmt::Vocabulary());
+    v->load_text(path);
+    ctx->tracker.set_vocabulary(v.get());
+    ctx->voc = std::move(v);
+  });
+  if (rc == MMT_OK && late) {
+    ctx->err = "mmt_load_vocabulary: load the vocabulary before the first frame";
+    return MMT_ESTATE;
+  }
+  return rc;
+}
+
+int mmt_bow_transform(mmt_ctx* ctx, const uint8_t* desc, int n, int levelsup, uint32_t* word,
+                      double* weight, uint32_t* node) {
+  if (!ctx || n < 0 || (n > 0 && (!desc || !word || !weight || !node))) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    if (!ctx->voc) throw mmt::ArgError("mmt_bow_transform: no vocabulary loaded");
+    MMT_HIP(hipSetDevice(ctx->cfg.device_id));
+    if (n == 0) return;
+    ctx->voc->upload();
+    hipStream_t s = ctx->stream;
+    DevBuf<uint8_t> d(32 * (size_t)n);
+    DevBuf<uint32_t> w(n), nd(n);
+    DevBuf<double> x(n);
+    MMT_HIP(hipMemcpyAsync(d.p, desc, 32 * (size_t)n, hipMemcpyHostToDevice, s));
+    mmt::launch_bow_transform(ctx->voc->dev, d.p, n, levelsup, w.p, x.p, nd.p, s);
+    MMT_HIP(hipMemcpyAsync(word, w.p, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(weight, x.p, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(node, nd.p, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int mmt_bow_counters_read(mmt_ctx* ctx, mmt_bow_counters* out) {
+  if (!ctx || !out) return MMT_EINVAL;
+  return guard(ctx, [&] {
+    memset(out, 0, sizeof(*out));
+    if (!ctx->tracker_ready) return;
+    const mmt::BowStatsH& b = ctx->tracker.bow_stats();
+    out->bow_frames = b.n_bow_frames;
+    out->trk = b.n_trk;
+    out->trk_ok = b.n_trk_ok;
+    out->reloc = b.n_reloc;
+    out->reloc_ok = b.n_reloc_ok;
+    out->reloc_cands = b.n_reloc_cands;
+    out->pnp_found = b.n_pnp_found;
+    out->sbp_rounds = b.n_sbp_rounds;
+    out->triangulated = b.n_triangulated;
+    out->sft_matches = b.n_sft_matches;
+    out->kfdb = b.n_kfdb;
+  });
+}
+
 int mmt_map_dump(mmt_ctx* ctx, int32_t* sizes, const mmt_map_dump_arrays* out) {
   if (!ctx || !sizes) return MMT_EINVAL;
   return guard(ctx, [&] {
@@ -1059,6 +1122,171 @@ int mmt_pnp_ransac(mmt_ctx* ctx, const float* pts3, const float* pts2, int n, fl
 // iteration this call can run are built and scored on the GPU in one batch (k_pnp_hyp<4>,
 // k_pnp_beta<4>, k_p4p_check); the host replays iterate()'s loop over their inlier counts, and
 // every Refine() it reaches runs on the GPU (EPnP over the best inliers + CheckInliers).
+}  // extern "C"
+
+// PnPsolver::iterate on the GPU (the C-ABI probe mmt_pnpsolver_iterate and the tracker's
+// Relocalization): SetRansacParameters' arithmetic, every hypothesis the call can run scored in
+// one launch, the host replaying iterate()'s loop and Refine() on the GPU
+void mmt::pnpsolver_iterate_gpu(hipStream_t s, const mmt_pnpsolver_problem* pr,
+                                const int32_t* randi, int n_draw_iters, int n_iterations,
+                                mmt_pnpsolver_state* st, float* Tcw_out, uint8_t* inliers_out,
+                                int* n_inliers, int* pose_found, int* no_more) {
+  if (pr->min_set != 4) throw mmt::ArgError("PnPsolver: min_set must be 4 (P4P)");
+  const int N = pr->n;
+  // ---- SetRansacParameters (PnPsolver.cc:119-152), the reference's int/float arithmetic
+  float eps = pr->epsilon;
+  int minInl = pr->min_inliers;
+  int nMinInliers = (int)(N * eps);
+  if (nMinInliers < minInl) nMinInliers = minInl;
+  if (nMinInliers < pr->min_set) nMinInliers = pr->min_set;
+  minInl = nMinInliers;
+  if (N > 0 && eps < (float)minInl / N) eps = (float)minInl / N;
+  int nIt;
+  if (minInl == N)
+    nIt = 1;
+  else
+    nIt = (int)ceil(log(1 - pr->probability) / log(1 - pow(eps, 3)));
+  const int maxIts = std::max(1, std::min(nIt, pr->max_iterations));
+  // ---- iterate() (PnPsolver.cc:160-264)
+  *no_more = 0;
+  *pose_found = 0;
+  *n_inliers = 0;
+  memset(inliers_out, 0, (size_t)N);
+  if (N < minInl) {
+    *no_more = 1;
+    return;
+  }
+  const int it0 = st->iterations;
+  const int K = std::max(maxIts - it0, n_iterations);  // while (its < max || cur < nIt)
+  if (K > n_draw_iters) throw mmt::ArgError("PnPsolver: randi covers fewer iterations than the call runs");
+  const int words = (N + 63) / 64;
+  // minimal sets: RandomInt draws through vAvailableIndices' swap-with-last removal
+  std::vector<int> sub(4 * (size_t)std::max(K, 1));
+  std::vector<int> avail(N);
+  for (int k = 0; k < K; k++) {
+    for (int i = 0; i < N; i++) avail[i] = i;
+    int sz = N;
+    for (int j = 0; j < 4; j++) {
+      const int r = randi[4 * (size_t)k + j];
+      if (r < 0 || r >= sz) throw mmt::ArgError("PnPsolver: randi value outside [0, n-1-j]");
+      sub[4 * (size_t)k + j] = avail[r];
+      avail[r] = avail[sz - 1];
+      sz--;
+    }
+  }
+  std::vector<float> maxErr(N);
+  for (int i = 0; i < N; i++) maxErr[i] = pr->sigma2[i] * pr->th2;
+  const int rows = K + 2;  // hypothesis masks, then the refine's input and output rows
+  DevBuf<float> p3(3 * (size_t)N + 1), merr((size_t)N + 1);
+  DevBuf<float2> p2((size_t)N + 1);
+  DevBuf<int> dn(1), dsub(sub.size()), good((size_t)K + 1), inl((size_t)N + 1), res(8);
+  DevBuf<double> hrec((size_t)mmt::kHypRec * std::max(K, 1)),
+      hout((size_t)3 * mmt::kHypOut * std::max(K, 1)), hrt(12 * (size_t)std::max(K, 1)), Rt(12);
+  DevBuf<unsigned long long> masks((size_t)rows * words + 1);
+  DevBuf<mmt::PnPObject> po(1);
+  MMT_HIP(hipMemcpyAsync(p3.p, pr->pts3, 12 * (size_t)N, hipMemcpyHostToDevice, s));
+  MMT_HIP(hipMemcpyAsync(p2.p, pr->pts2, 8 * (size_t)N, hipMemcpyHostToDevice, s));
+  MMT_HIP(hipMemcpyAsync(merr.p, maxErr.data(), 4 * (size_t)N, hipMemcpyHostToDevice, s));
+  MMT_HIP(hipMemcpyAsync(dn.p, &N, 4, hipMemcpyHostToDevice, s));
+  MMT_HIP(hipMemcpyAsync(dsub.p, sub.data(), 4 * sub.size(), hipMemcpyHostToDevice, s));
+  mmt::PnPObject o;
+  memset(&o, 0, sizeof(o));
+  o.n = dn.p;
+  o.fx = pr->fx; o.fy = pr->fy; o.cx = pr->cx; o.cy = pr->cy;
+  o.subsets = dsub.p;
+  o.pts3 = p3.p;
+  o.pts2 = p2.p;
+  o.hrec = hrec.p;
+  o.hout = hout.p;
+  o.good = good.p;
+  o.masks = masks.p;
+  o.mask_words = words;
+  o.inliers = inl.p;
+  o.result = res.p;
+  o.Rt = Rt.p;
+  o.raw_pixels = 1;
+  o.rt_raw = 1;
+  o.max_err = merr.p;
+  o.hrt = hrt.p;
+  MMT_HIP(hipMemcpyAsync(po.p, &o, sizeof(o), hipMemcpyHostToDevice, s));
+  std::vector<int> h_good(std::max(K, 1));
+  if (K > 0) {
+    mmt::launch_p4p_hypotheses(po.p, K, s);
+    MMT_HIP(hipMemcpyAsync(h_good.data(), good.p, 4 * (size_t)K, hipMemcpyDeviceToHost, s));
+  }
+  MMT_HIP(hipStreamSynchronize(s));
+  auto fetch_mask = [&](int row, uint8_t* out) {
+    std::vector<unsigned long long> w(words);
+    MMT_HIP(hipMemcpy(w.data(), masks.p + (size_t)row * words, 8 * (size_t)words,
+                      hipMemcpyDeviceToHost));
+    for (int i = 0; i < N; i++) out[i] = (uint8_t)((w[i >> 6] >> (i & 63)) & 1ull);
+  };
+  auto pose_to_Tcw = [](const double* Rt12, float* T) {  // cv::Mat(R, t).convertTo(CV_32F)
+    for (int r = 0; r < 4; r++)
+      for (int c = 0; c < 4; c++) T[4 * r + c] = (r == c) ? 1.f : 0.f;
+    for (int r = 0; r < 3; r++) {
+      for (int c = 0; c < 3; c++) T[4 * r + c] = (float)Rt12[3 * r + c];
+      T[4 * r + 3] = (float)Rt12[9 + r];
+    }
+  };
+  // Refine() of the current best set (st->best_mask), cached while the best set is unchanged
+  bool refined_valid = false;
+  int refined_n = 0;
+  float refined_T[16];
+  std::vector<uint8_t> refined_mask(N);
+  auto refine = [&]() {
+    if (refined_valid) return;
+    std::vector<unsigned long long> w(words, 0ull);
+    for (int i = 0; i < N; i++)
+      if (st->best_mask[i]) w[i >> 6] |= 1ull << (i & 63);
+    MMT_HIP(hipMemcpyAsync(masks.p + (size_t)K * words, w.data(), 8 * (size_t)words,
+                           hipMemcpyHostToDevice, s));
+    mmt::launch_p4p_refine(po.p, K, K + 1, s);
+    int r[8];
+    double rt[12];
+    MMT_HIP(hipMemcpyAsync(r, res.p, sizeof(r), hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipMemcpyAsync(rt, Rt.p, sizeof(rt), hipMemcpyDeviceToHost, s));
+    MMT_HIP(hipStreamSynchronize(s));
+    refined_n = r[6];
+    pose_to_Tcw(rt, refined_T);
+    fetch_mask(K + 1, refined_mask.data());
+    refined_valid = true;
+  };
+  for (int k = 0; k < K; k++) {
+    st->iterations = it0 + k + 1;
+    const int g = h_good[k];
+    if (g >= minInl) {
+      if (g > st->best_inliers) {
+        fetch_mask(k, st->best_mask);
+        st->best_inliers = g;
+        double rt[12];
+        MMT_HIP(hipMemcpy(rt, hrt.p + 12 * (size_t)k, sizeof(rt), hipMemcpyDeviceToHost));
+        pose_to_Tcw(rt, st->best_Tcw);
+        refined_valid = false;
+      }
+      refine();
+      if (refined_n > minInl) {  // Refine() succeeded: return the refined pose
+        *pose_found = 1;
+        *n_inliers = refined_n;
+        memcpy(inliers_out, refined_mask.data(), (size_t)N);
+        memcpy(Tcw_out, refined_T, sizeof(refined_T));
+        return;
+      }
+    }
+  }
+  if (st->iterations >= maxIts) {
+    *no_more = 1;
+    if (st->best_inliers >= minInl) {
+      *pose_found = 1;
+      *n_inliers = st->best_inliers;
+      memcpy(inliers_out, st->best_mask, (size_t)N);
+      memcpy(Tcw_out, st->best_Tcw, sizeof(st->best_Tcw));
+    }
+  }
+}
+
+extern "C" {
+
 int mmt_pnpsolver_iterate(mmt_ctx* ctx, const mmt_pnpsolver_problem* pr, const int32_t* randi,
                           int n_draw_iters, int n_iterations, mmt_pnpsolver_state* st,
                           float* Tcw_out, uint8_t* inliers_out, int* n_inliers, int* pose_found,
@@ -1068,160 +1296,9 @@ int mmt_pnpsolver_iterate(mmt_ctx* ctx, const mmt_pnpsolver_problem* pr, const i
     return MMT_EINVAL;
   if (pr->n > 0 && (!pr->pts3 || !pr->pts2 || !pr->sigma2)) return MMT_EINVAL;
   return guard(ctx, [&] {
-    if (pr->min_set != 4) throw mmt::ArgError("PnPsolver: min_set must be 4 (P4P)");
-    const int N = pr->n;
-    // ---- SetRansacParameters (PnPsolver.cc:119-152), the reference's int/float arithmetic
-    float eps = pr->epsilon;
-    int minInl = pr->min_inliers;
-    int nMinInliers = (int)(N * eps);
-    if (nMinInliers < minInl) nMinInliers = minInl;
-    if (nMinInliers < pr->min_set) nMinInliers = pr->min_set;
-    minInl = nMinInliers;
-    if (N > 0 && eps < (float)minInl / N) eps = (float)minInl / N;
-    int nIt;
-    if (minInl == N)
-      nIt = 1;
-    else
-      nIt = (int)ceil(log(1 - pr->probability) / log(1 - pow(eps, 3)));
-    const int maxIts = std::max(1, std::min(nIt, pr->max_iterations));
-    // ---- iterate() (PnPsolver.cc:160-264)
-    *no_more = 0;
-    *pose_found = 0;
-    *n_inliers = 0;
-    memset(inliers_out, 0, (size_t)N);
-    if (N < minInl) {
-      *no_more = 1;
-      return;
-    }
-    const int it0 = st->iterations;
-    const int K = std::max(maxIts - it0, n_iterations);  // while (its < max || cur < nIt)
-    if (K > n_draw_iters) throw mmt::ArgError("PnPsolver: randi covers fewer iterations than the call runs");
     MMT_HIP(hipSetDevice(ctx->cfg.device_id));
-    hipStream_t s = ctx->stream;
-    const int words = (N + 63) / 64;
-    // minimal sets: RandomInt draws through vAvailableIndices' swap-with-last removal
-    std::vector<int> sub(4 * (size_t)std::max(K, 1));
-    std::vector<int> avail(N);
-    for (int k = 0; k < K; k++) {
-      for (int i = 0; i < N; i++) avail[i] = i;
-      int sz = N;
-      for (int j = 0; j < 4; j++) {
-        const int r = randi[4 * (size_t)k + j];
-        if (r < 0 || r >= sz) throw mmt::ArgError("PnPsolver: randi value outside [0, n-1-j]");
-        sub[4 * (size_t)k + j] = avail[r];
-        avail[r] = avail[sz - 1];
-        sz--;
-      }
-    }
-    std::vector<float> maxErr(N);
-    for (int i = 0; i < N; i++) maxErr[i] = pr->sigma2[i] * pr->th2;
-    const int rows = K + 2;  // hypothesis masks, then the refine's input and output rows
-    DevBuf<float> p3(3 * (size_t)N + 1), merr((size_t)N + 1);
-    DevBuf<float2> p2((size_t)N + 1);
-    DevBuf<int> dn(1), dsub(sub.size()), good((size_t)K + 1), inl((size_t)N + 1), res(8);
-    DevBuf<double> hrec((size_t)mmt::kHypRec * std::max(K, 1)),
-        hout((size_t)3 * mmt::kHypOut * std::max(K, 1)), hrt(12 * (size_t)std::max(K, 1)), Rt(12);
-    DevBuf<unsigned long long> masks((size_t)rows * words + 1);
-    DevBuf<mmt::PnPObject> po(1);
-    MMT_HIP(hipMemcpyAsync(p3.p, pr->pts3, 12 * (size_t)N, hipMemcpyHostToDevice, s));
-    MMT_HIP(hipMemcpyAsync(p2.p, pr->pts2, 8 * (size_t)N, hipMemcpyHostToDevice, s));
-    MMT_HIP(hipMemcpyAsync(merr.p, maxErr.data(), 4 * (size_t)N, hipMemcpyHostToDevice, s));
-    MMT_HIP(hipMemcpyAsync(dn.p, &N, 4, hipMemcpyHostToDevice, s));
-    MMT_HIP(hipMemcpyAsync(dsub.p, sub.data(), 4 * sub.size(), hipMemcpyHostToDevice, s));
-    mmt::PnPObject o;
-    memset(&o, 0, sizeof(o));
-    o.n = dn.p;
-    o.fx = pr->fx; o.fy = pr->fy; o.cx = pr->cx; o.cy = pr->cy;
-    o.subsets = dsub.p;
-    o.pts3 = p3.p;
-    o.pts2 = p2.p;
-    o.hrec = hrec.p;
-    o.hout = hout.p;
-    o.good = good.p;
-    o.masks = masks.p;
-    o.mask_words = words;
-    o.inliers = inl.p;
-    o.result = res.p;
-    o.Rt = Rt.p;
-    o.raw_pixels = 1;
-    o.rt_raw = 1;
-    o.max_err = merr.p;
-    o.hrt = hrt.p;
-    MMT_HIP(hipMemcpyAsync(po.p, &o, sizeof(o), hipMemcpyHostToDevice, s));
-    std::vector<int> h_good(std::max(K, 1));
-    if (K > 0) {
-      mmt::launch_p4p_hypotheses(po.p, K, s);
-      MMT_HIP(hipMemcpyAsync(h_good.data(), good.p, 4 * (size_t)K, hipMemcpyDeviceToHost, s));
-    }
-    MMT_HIP(hipStreamSynchronize(s));
-    auto fetch_mask = [&](int row, uint8_t* out) {
-      std::vector<unsigned long long> w(words);
-      MMT_HIP(hipMemcpy(w.data(), masks.p + (size_t)row * words, 8 * (size_t)words,
-                        hipMemcpyDeviceToHost));
-      for (int i = 0; i < N; i++) out[i] = (uint8_t)((w[i >> 6] >> (i & 63)) & 1ull);
-    };
-    auto pose_to_Tcw = [](const double* Rt12, float* T) {  // cv::Mat(R, t).convertTo(CV_32F)
-      for (int r = 0; r < 4; r++)
-        for (int c = 0; c < 4; c++) T[4 * r + c] = (r == c) ? 1.f : 0.f;
-      for (int r = 0; r < 3; r++) {
-        for (int c = 0; c < 3; c++) T[4 * r + c] = (float)Rt12[3 * r + c];
-        T[4 * r + 3] = (float)Rt12[9 + r];
-      }
-    };
-    // Refine() of the current best set (st->best_mask), cached while the best set is unchanged
-    bool refined_valid = false;
-    int refined_n = 0;
-    float refined_T[16];
-    std::vector<uint8_t> refined_mask(N);
-    auto refine = [&]() {
-      if (refined_valid) return;
-      std::vector<unsigned long long> w(words, 0ull);
-      for (int i = 0; i < N; i++)
-        if (st->best_mask[i]) w[i >> 6] |= 1ull << (i & 63);
-      MMT_HIP(hipMemcpyAsync(masks.p + (size_t)K * words, w.data(), 8 * (size_t)words,
-                             hipMemcpyHostToDevice, s));
-      mmt::launch_p4p_refine(po.p, K, K + 1, s);
-      int r[8];
-      double rt[12];
-      MMT_HIP(hipMemcpyAsync(r, res.p, sizeof(r), hipMemcpyDeviceToHost, s));
-      MMT_HIP(hipMemcpyAsync(rt, Rt.p, sizeof(rt), hipMemcpyDeviceToHost, s));
-      MMT_HIP(hipStreamSynchronize(s));
-      refined_n = r[6];
-      pose_to_Tcw(rt, refined_T);
-      fetch_mask(K + 1, refined_mask.data());
-      refined_valid = true;
-    };
-    for (int k = 0; k < K; k++) {
-      st->iterations = it0 + k + 1;
-      const int g = h_good[k];
-      if (g >= minInl) {
-        if (g > st->best_inliers) {
-          fetch_mask(k, st->best_mask);
-          st->best_inliers = g;
-          double rt[12];
-          MMT_HIP(hipMemcpy(rt, hrt.p + 12 * (size_t)k, sizeof(rt), hipMemcpyDeviceToHost));
-          pose_to_Tcw(rt, st->best_Tcw);
-          refined_valid = false;
-        }
-        refine();
-        if (refined_n > minInl) {  // Refine() succeeded: return the refined pose
-          *pose_found = 1;
-          *n_inliers = refined_n;
-          memcpy(inliers_out, refined_mask.data(), (size_t)N);
-          memcpy(Tcw_out, refined_T, sizeof(refined_T));
-          return;
-        }
-      }
-    }
-    if (st->iterations >= maxIts) {
-      *no_more = 1;
-      if (st->best_inliers >= minInl) {
-        *pose_found = 1;
-        *n_inliers = st->best_inliers;
-        memcpy(inliers_out, st->best_mask, (size_t)N);
-        memcpy(Tcw_out, st->best_Tcw, sizeof(st->best_Tcw));
-      }
-    }
+    mmt::pnpsolver_iterate_gpu(ctx->stream, pr, randi, n_draw_iters, n_iterations, st, Tcw_out,
+                               inliers_out, n_inliers, pose_found, no_more);
   });
 }
 

@@ -1,8 +1,10 @@
 // multimot_track_amd/csrc/mmt_ctx.h -- the opaque mmt_ctx behind include/mmt.h.
 #pragma once
 #include <deque>
+#include <memory>
 
 #include "mmt_ba.h"
+#include "mmt_bow.h"
 #include "mmt_internal.h"
 #include "mmt_tracker.h"
 
@@ -29,4 +31,5 @@ struct mmt_ctx {
   int32_t* t_mask = nullptr;
   int t_frames = 0;  // frames the t_* staging buffers hold
   std::deque<mmt::FrameOut> flushed;  // mmt_flush_objects records not yet handed out
+  std::unique_ptr<mmt::Vocabulary> voc;  // mmt_load_vocabulary (System's ORB vocabulary)
 };

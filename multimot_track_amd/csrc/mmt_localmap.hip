@@ -190,6 +190,7 @@ void MapEngine::kf_set_bad(int kf) {  // KeyFrame::SetBadFlag (mbNotErase is nev
     kfs_[K.parent].children.erase(kf);
   }
   K.bad = true;
+  kfdb_erase(kf);  // mpKeyFrameDB->erase(this) (KeyFrame.cc:544)
 }
 
 // ------------------------------------------------------------------ Fuse
@@ -525,7 +526,9 @@ void MapEngine::keyframe_culling(int kf) {  // LocalMapping::KeyFrameCulling (RG
 
 void MapEngine::local_mapping(int kf) {
   const double t0 = prof_on_ ? now_us() : 0;
-  // CreateNewMapPoints: SearchForTriangulation needs the BoW vocabulary (skipped, see above)
+  // CreateNewMapPoints: SearchForTriangulation needs the vocabulary's FeatureVectors (without one
+  // it is skipped, see mmt_map.h); mmt_bowmap.hip
+  if (voc_) create_new_map_points(kf);
   search_in_neighbors(kf);
   const double t1 = prof_on_ ? now_us() : 0;
   if (n_keyframes() > 2) local_bundle_adjustment(kf);

@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "mmt_ba.h"
+#include "mmt_bow.h"
 #include "mmt_internal.h"
 #include "mmt_match.h"
 #include "mmt_track.h"
@@ -117,6 +118,26 @@ struct KFrame {
   bool bad = false;
   long fuseTarget = 0, baLocal = 0, baFixed = 0;  // mnFuseTargetForKF, mnBALocalForKF, mnBAFixedForKF
   FuseKF dev{};  // the keyframe's keys, descriptors, mvuRight and grid on the device (KF store)
+  // with a vocabulary: mBowVec, mFeatVec, and the KeyFrameDatabase query fields (KeyFrame.h:146-149;
+  // mRelocScore uninitialised in the reference: pinned 0)
+  BowVecH bow;
+  FeatVecH fv;
+  bool hasBow = false;
+  long relocQuery = 0;
+  int relocWords = 0;
+  float relocScore = 0;
+};
+
+// glibc's rand() (random_r TYPE_3, srand(1) for an unseeded process): the stream
+// DUtils::Random::RandomInt draws PnPsolver's minimal sets from (Random.cpp:47-50)
+class GlibcRandH {
+ public:
+  GlibcRandH();
+  int next();
+  int random_int(int min, int max);
+
+ private:
+  std::vector<int32_t> r_;
 };
 
 // LocalMapping counters (tests, profiling)
@@ -144,6 +165,15 @@ struct MapFrameH {
   std::vector<int> mps;          // mvpMapPoints (point handle or -1)
   std::vector<uint8_t> outlier;  // mvbOutlier
   int refKF = -1;                // mpReferenceKF
+  BowVecH bow;                   // mBowVec / mFeatVec (Frame::ComputeBoW, with a vocabulary)
+  FeatVecH fv;
+  bool hasBow = false;
+};
+
+// counters of the vocabulary path (tests, mmt_map_counters)
+struct BowStatsH {
+  long n_bow_frames = 0, n_trk = 0, n_trk_ok = 0, n_reloc = 0, n_reloc_ok = 0, n_reloc_cands = 0,
+       n_pnp_found = 0, n_sbp_rounds = 0, n_triangulated = 0, n_sft_matches = 0, n_kfdb = 0;
 };
 
 struct MapStatsH {
@@ -154,6 +184,9 @@ struct MapStatsH {
   int new_keyframe = 0;
   float Tcw_map[16];       // the map branch's pose: PoseOptimizationFlow2Cam's initial estimate
 };
+
+constexpr size_t kDescBytes = 256;  // D1's descriptor at the head of an upload block
+constexpr size_t kOutHdr = 128;     // [nm][ninl][pad][pose] at the head of the download block
 
 class MapEngine {
  public:
@@ -208,6 +241,10 @@ class MapEngine {
   void set_cull_ratio(double r) { cull_ratio_ = r; }
   // the map as flat arrays (mmt_map_dump, include/mmt.h): sizes[7]; arrays written when out != 0
   void dump(int32_t* sizes, const mmt_map_dump_arrays* out) const;
+  // System's vocabulary (System.cc:67): with one, TrackReferenceKeyFrame, Relocalization and
+  // CreateNewMapPoints run as the reference's (mmt_bowmap.hip); without, the substitutes above
+  void set_vocabulary(Vocabulary* v);
+  const BowStatsH& bow_stats() const { return bstats_; }
 
  private:
   std::function<void()> overlap_;
@@ -262,6 +299,29 @@ class MapEngine {
   void erase_connection(int kf, int other);
   void set_pose(int kf, const float* Tcw);
   void kf_store_add(int kf);
+  // ---- vocabulary path (mmt_bowmap.hip)
+  void bow_transform(const uint8_t* d_desc, int n, hipStream_t st, BowVecH& v, FeatVecH& fv);
+  void frame_bow(MapFrameH& C, const GridFrame& G);
+  void kf_bow(int kf);
+  void kfdb_add(int kf);
+  void kfdb_erase(int kf);
+  std::vector<int> detect_relocalization_candidates(const MapFrameH& C);
+  int search_by_bow_kf(int kf, const MapFrameH& C, const GridFrame& G, float nnratio,
+                       std::vector<int>& match);
+  int gpu_pose_optimization(MapFrameH& C, float* Tcw);
+  bool track_reference_kf(MapFrameH& C, const GridFrame& G, float* Tcw, const float* Tlast);
+  bool relocalization(MapFrameH& C, const GridFrame& G, float* Tcw);
+  int search_by_projection_kf(MapFrameH& C, const GridFrame& G, const float* Tcw, int kf,
+                              const std::set<int>& found, float th, int orbDist);
+  void create_new_map_points(int kf);
+  void bw_grow(size_t need);
+  Vocabulary* voc_ = nullptr;
+  std::vector<std::vector<int>> invfile_;  // KeyFrameDatabase::mvInvertedFile
+  GlibcRandH rand_;
+  BowStatsH bstats_;
+  uint8_t* d_bw_ = nullptr;  // the vocabulary path's upload / download scratch
+  uint8_t* h_bw_ = nullptr;
+  size_t bw_cap_ = 0;
   void fuse_launch(const std::vector<int>& kft_kf, const std::vector<FuseQuery>& q, int2* res);
   // GPU stages (synchronous on s_)
   // retry_below (-1: min_matches): the retry at retry_th runs below this many matches

@@ -108,9 +108,7 @@ MapEngine::~MapEngine() {
 static size_t last_bytes(int n) { return (size_t)n * (sizeof(mmt_kp) + 12 + 32 + 2); }
 
 // every chain (C2 -> D1, C3 -> D1) moves one block up and one block down
-constexpr size_t kDescBytes = 256;  // D1's descriptor at the head of an upload block
 static_assert(sizeof(PoseOptDesc) <= kDescBytes, "PoseOptDesc outgrew its slot");
-constexpr size_t kOutHdr = 128;     // [nm][ninl][pad][pose] at the head of the download block
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // C3's upload block for m local points and n keys: offsets of taken (after ids, skip), the base
@@ -219,6 +217,7 @@ void MapEngine::reset() {
   hasTlr_ = false;
   snapKF_ = -1;
   n_good_ = 0;
+  for (auto& l : invfile_) l.clear();  // mpKeyFrameDB->clear() (Tracking.cc:3801)
 }
 
 int MapEngine::n_keyframes() const {
@@ -231,6 +230,10 @@ void MapEngine::prepare(MapFrameH& F) const {
   F.mps.assign(F.n, -1);
   F.outlier.assign(F.n, 0);
   F.refKF = -1;
+  F.hasBow = false;
+  F.bow.word.clear();
+  F.bow.value.clear();
+  F.fv = FeatVecH();
 }
 
 // ------------------------------------------------------------------ MapPoint
@@ -456,7 +459,8 @@ int MapEngine::tracked_map_points(int kf, int minObs) {  // KeyFrame::TrackedMap
   return n;
 }
 
-void MapEngine::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFrame, no BoW
+void MapEngine::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFrame
+  if (voc_) kf_bow(kf);  // mpCurrentKeyFrame->ComputeBoW() (without a vocabulary: none)
   const std::vector<int> mps = kfs_[kf].mps;
   for (size_t i = 0; i < mps.size(); i++) {
     const int h = mps[i];
@@ -752,7 +756,7 @@ void MapEngine::initialize(MapFrameH& C, const float* Tcw) {
   }
   process_new_keyframe(kf);
   map_point_culling(kf);
-  local_mapping(kf);
+  local_mapping(kf);  // keyframe 0 never enters the database (LoopClosing.cc:95)
   lastKFFrameId_ = C.id;
   localKFs_.assign(1, kf);
   localPts_.clear();
@@ -1180,6 +1184,9 @@ void MapEngine::create_new_keyframe(MapFrameH& C, const float* Tcw) {  // Tracki
   map_point_culling(kf);
   if (prof_on_) mstats_.pnk_us += now_us() - tp;
   local_mapping(kf);
+  // mpLoopCloser->InsertKeyFrame: LoopClosing::DetectLoop adds every keyframe but the first to
+  // the database (LoopClosing.cc:92-121); loop detection itself is out of scope
+  if (voc_ && kfs_[kf].id != 0 && !kfs_[kf].bad) kfdb_add(kf);
   lastKFFrameId_ = C.id;
 }
 
@@ -1197,15 +1204,20 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
         L.mps[i] = pts_[L.mps[i]].replaced;
     if (!has_vel || C.id < lastRelocFrameId_ + 2) {
       bSecondFrame = true;
-      bOK = track_reference_subst(C, G, Tcw, L, Tlast);
+      bOK = voc_ ? track_reference_kf(C, G, Tcw, Tlast) : track_reference_subst(C, G, Tcw, L, Tlast);
     } else {
       bSecondFrame = false;
       bOK = track_with_motion_model(C, G, Tcw, L, Tlast, vel, st);
       if (!bOK) {
         bSecondFrame = true;
-        bOK = track_reference_subst(C, G, Tcw, L, Tlast);
+        bOK = voc_ ? track_reference_kf(C, G, Tcw, Tlast)
+                   : track_reference_subst(C, G, Tcw, L, Tlast);
       }
     }
+  } else if (voc_) {  // Relocalization (Tracking.cc:3614-3776)
+    mat4_mul(vel, Tlast, Tcw);  // no pose computed: the motion model's prediction (pinned)
+    bOK = relocalization(C, G, Tcw);
+    if (bOK) lastRelocFrameId_ = C.id;
   } else {
     bOK = relocalization_subst(C, G, Tcw, Tlast, vel);  // Relocalization (substitute)
     if (bOK) lastRelocFrameId_ = C.id;

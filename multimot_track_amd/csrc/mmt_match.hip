@@ -28,6 +28,7 @@
 #include <climits>
 #include <cmath>
 
+#include "mmt_bow.h"
 #include "mmt_internal.h"
 #include "mmt_match.h"
 #include "mmt_track.h"
@@ -1310,6 +1311,86 @@ void launch_fuse_cand(const FuseKF* kfs, const FuseQuery* q, int nq, const Local
   if (nq <= 0) return;
   FuseArgs a{kfs, q, nq, pool, pool_desc, cam, out};
   hipLaunchKernelGGL(k_fuse_cand, dim3((nq + 3) / 4), dim3(256), 0, st, a);
+  MMT_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------ relocalisation
+// SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist) (ORBmatcher.cc:2104-2231):
+// one wave per keyframe map point (those not bad and not found, listed by the host): projection
+// (no depth test, as the reference), image bounds, distance invariance, PredictScale, then the
+// window's candidates in GetFeaturesInArea order with the level gate [p - 1, p + 1] and no stereo
+// test (er = inf); keys bound when the call starts are skipped, the rest is the host's replay.
+struct BoundKeys {
+  const uint8_t* b;
+  __device__ bool operator()(int k) const { return b[k] != 0; }
+};
+
+__global__ __launch_bounds__(256) void k_sbp_kf(SbpKfArgs a) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= a.m) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const GridFrame& C = a.C;
+  const SbpKfPoint p = a.pts[j];
+  float x3Dc[3];
+  pose_xform(a.Tcw, p.Xw, x3Dc);
+  const float invzc = (float)(1.0 / (double)x3Dc[2]);
+  const float u = C.fx * x3Dc[0] * invzc + C.cx;
+  const float v = C.fy * x3Dc[1] * invzc + C.cy;
+  bool ok = !(u < C.minX || u > C.maxX) && !(v < C.minY || v > C.maxY);
+  int npl = 0;
+  if (ok) {
+    float Ow[3];
+    pose_centre(a.Tcw, Ow);
+    double n2 = 0;
+    for (int k = 0; k < 3; k++) {
+      const float d = p.Xw[k] - Ow[k];
+      n2 += (double)d * (double)d;
+    }
+    const float dist3D = (float)sqrt(n2);
+    const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+    ok = !(dist3D < minDistance || dist3D > maxDistance);
+    if (ok) {  // MapPoint::PredictScale(dist3D, &CurrentFrame)
+      const float ratio = p.max_dist / dist3D;
+      const float ls = (float)log((double)ratio) / C.logScale;
+      npl = isfinite(ls) ? (int)ceilf(ls) : INT_MIN;
+      if (npl < 0) npl = 0;
+      else if (npl >= C.nlevels) npl = C.nlevels - 1;
+    }
+  }
+  if (!ok) {
+    if (lane < kSbpKfCand) {
+      a.cand_key[(size_t)j * kSbpKfCand + lane] = kNoCand;
+      a.cand_idx[(size_t)j * kSbpKfCand + lane] = -1;
+    }
+    if (lane == 0) a.n_cand[j] = -1;
+    return;
+  }
+  PointWin w = {};
+  w.x = u;
+  w.y = v;
+  w.r = a.th * C.scale[npl];
+  w.ur = 0.f;
+  w.er = INFINITY;
+  w.minLevel = npl - 1;
+  w.maxLevel = npl + 1;
+  uint32_t dmp[8];
+  load_desc8(p.desc, dmp);
+  uint32_t tk;
+  int ti;
+  const int passed = wave_topk<kSbpKfCand>(C, w, dmp, BoundKeys{a.bound}, tk, ti);
+  if (lane < kSbpKfCand) {
+    a.cand_key[(size_t)j * kSbpKfCand + lane] = tk;
+    a.cand_idx[(size_t)j * kSbpKfCand + lane] = ti;
+  }
+  if (lane == 0) {
+    a.n_cand[j] = passed;
+    a.win[j] = w;
+  }
+}
+
+void launch_sbp_kf(const SbpKfArgs& a, hipStream_t st) {
+  if (a.m <= 0) return;
+  hipLaunchKernelGGL(k_sbp_kf, dim3((a.m + 3) / 4), dim3(256), 0, st, a);
   MMT_HIP(hipGetLastError());
 }
 

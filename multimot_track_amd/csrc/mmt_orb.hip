@@ -2052,6 +2052,9 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
         }
         fits = 2 * ((buf + 15) & ~15) <= 120 * 1024;
         for (int l = 0; l < nlevels_; l++) fits = fits && B.hi[l] - B.lo[l] <= 1024;
+        // k_pyramid stages level-0 rows clamped to [lo, hi - 1]: an empty level-0 range would
+        // read row -1, so such a band count is rejected (the k_resize chain takes over)
+        fits = fits && B.lo[0] < B.hi[0];
       }
       if (!fits) continue;
       pa.buf_bytes = (buf + 15) & ~15;

@@ -4,6 +4,8 @@
 
 #include <cstdint>
 
+#include "../../include/mmt.h"
+
 namespace mmt {
 
 struct PnPObject {
@@ -57,6 +59,12 @@ void launch_p4p_hypotheses(PnPObject* d_obj, int K, hipStream_t st);
 // D6: PnPsolver::Refine on the inliers of masks row `row` (EPnP over them, CheckInliers of the
 // refined pose: count in result[6], mask in row `row_out`, pose in Rt)
 void launch_p4p_refine(PnPObject* d_obj, int row, int row_out, hipStream_t st);
+// PnPsolver::SetRansacParameters + iterate(n_iterations) on the GPU (mmt_pnpsolver_iterate's
+// semantics, include/mmt.h; throws ArgError on bad arguments)
+void pnpsolver_iterate_gpu(hipStream_t s, const mmt_pnpsolver_problem* pr, const int32_t* randi,
+                           int n_draw_iters, int n_iterations, mmt_pnpsolver_state* st,
+                           float* Tcw_out, uint8_t* inliers_out, int* n_inliers, int* pose_found,
+                           int* no_more);
 
 
 #ifdef __HIPCC__

@@ -89,6 +89,8 @@ class Tracker {
   const MappingStats& mapping_stats() const { return map_.mapping_stats(); }
   const MapEngine& map() const { return map_; }
   void set_cull_ratio(double r) { map_.set_cull_ratio(r); }
+  void set_vocabulary(Vocabulary* v) { map_.set_vocabulary(v); }
+  const BowStatsH& bow_stats() const { return map_.bow_stats(); }
   long split_fallbacks() const { return split_fallbacks_; }
   // the last tracked frame's static samples (mvSiftKeys) and object samples (mvObjKeys,
   // vSemObjLabel), copied to the host (visualisation hook); counts clipped to the caps

@@ -6,6 +6,7 @@
 // double rounded to float; cv::norm is the double sqrt of the double sum of squares.
 
 #include <algorithm>
+#include <cstdlib>
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -41,6 +42,7 @@ void MapTracker::reset() {
   temporal_.clear();
   recent_.clear();
   hasTlr_ = false;
+  for (auto& l : invfile_) l.clear();  // mpKeyFrameDB->clear() (Tracking.cc:3801)
 }
 
 int MapTracker::n_keyframes() const {
@@ -69,6 +71,9 @@ void MapTracker::prepare_frame(const std::vector<Key>& keys, const float* depth,
   F.mps.assign(keys.size(), -1);
   F.outlier.assign(keys.size(), 0);
   F.refKF = -1;
+  F.hasBow = false;
+  F.bow = BowVec();
+  F.fv = FeatVecO();
   depth_ = depth;
 }
 
@@ -271,7 +276,8 @@ int MapTracker::tracked_map_points(int kf, int minObs) {  // KeyFrame::TrackedMa
 }
 
 // ------------------------------------------------------------------ LocalMapping (synchronous)
-void MapTracker::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFrame, no BoW
+void MapTracker::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFrame
+  if (voc_) kf_compute_bow(kf);  // mpCurrentKeyFrame->ComputeBoW() (without a vocabulary: none)
   const std::vector<int> mps = kfs[kf].mps;
   for (size_t i = 0; i < mps.size(); i++) {
     const int h = mps[i];
@@ -341,7 +347,13 @@ void MapTracker::initialize(const std::vector<Key>& keys, const std::vector<uint
 void MapTracker::insert_keyframe(int kf) { pendingKF_ = kf; }
 
 void MapTracker::frame_done(const MapFrame& C, const float* Tcw) {
-  if (C.refKF >= 0) {
+  // ORACLE_ABLATE (diagnostics only, tools/drift_ablation.py; default 0): bit 1 skips
+  // MapPointCulling, bit 2 computes Tlr after the keyframe's LocalMapping (round 4's order)
+  static const int ablate = [] {
+    const char* e = getenv("ORACLE_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  if (C.refKF >= 0 && !(ablate & 2)) {
     m4_mul(Tcw, kfs[C.refKF].Twc, Tlr_);  // Tcr = mTcw * mpReferenceKF->GetPoseInverse()
     hasTlr_ = true;
   }
@@ -351,8 +363,15 @@ void MapTracker::frame_done(const MapFrame& C, const float* Tcw) {
     const int kf = pendingKF_;
     pendingKF_ = -1;
     process_new_keyframe(kf);
-    map_point_culling(kf);
+    if (!(ablate & 1)) map_point_culling(kf);
     local_mapping(kf);
+    // mpLoopCloser->InsertKeyFrame: LoopClosing::DetectLoop adds it to the database (but
+    // keyframe 0, LoopClosing.cc:95); loop detection itself is out of scope
+    if (voc_ && kfs[kf].id != 0 && !kfs[kf].bad) kfdb_add(kf);
+  }
+  if (C.refKF >= 0 && (ablate & 2)) {
+    m4_mul(Tcw, kfs[C.refKF].Twc, Tlr_);
+    hasTlr_ = true;
   }
 }
 
@@ -789,17 +808,25 @@ int MapTracker::track(const std::vector<Key>& keys, const std::vector<uint8_t>& 
         L.mps[i] = mp(L.mps[i]).replaced;
     if (!has_vel || C.id < lastRelocFrameId_ + 2) {
       bSecondFrame = true;
-      bOK = track_reference_subst(keys, desc, C, Tcw, lkeys, L, Tlast);
+      bOK = voc_ ? track_reference_kf(keys, desc, C, Tcw, Tlast)
+                 : track_reference_subst(keys, desc, C, Tcw, lkeys, L, Tlast);
     } else {
       bSecondFrame = false;
       bOK = track_with_motion_model(keys, desc, C, Tcw, lkeys, ldesc, L, Tlast, vel, st);
       if (!bOK) {
         bSecondFrame = true;
-        bOK = track_reference_subst(keys, desc, C, Tcw, lkeys, L, Tlast);
+        bOK = voc_ ? track_reference_kf(keys, desc, C, Tcw, Tlast)
+                   : track_reference_subst(keys, desc, C, Tcw, lkeys, L, Tlast);
       }
     }
+  } else if (voc_) {  // Relocalization (Tracking.cc:3614-3776)
+    float Tpred[16];
+    m4_mul(vel, Tlast, Tpred);
+    memcpy(Tcw, Tpred, 64);  // no pose computed: the motion model's prediction (pinned)
+    bOK = relocalization(keys, desc, C, Tcw);
+    if (bOK) lastRelocFrameId_ = C.id;
   } else {
-    bOK = relocalization_subst(keys, desc, C, Tcw, Tlast, vel);  // Relocalization
+    bOK = relocalization_subst(keys, desc, C, Tcw, Tlast, vel);  // Relocalization substitute
     if (bOK) lastRelocFrameId_ = C.id;
   }
   C.refKF = refKF_;

@@ -217,6 +217,7 @@ void MapTracker::kf_set_bad(int kf) {  // KeyFrame::SetBadFlag (mbNotErase is ne
     kfs[K.parent].children.erase(kf);
   }
   K.bad = true;
+  kfdb_erase(kf);  // mpKeyFrameDB->erase(this) (KeyFrame.cc:544)
 }
 
 // ------------------------------------------------------------------ ORBmatcher::Fuse
@@ -419,12 +420,14 @@ void MapTracker::keyframe_culling(int kf) {  // LocalMapping::KeyFrameCulling (R
 
 void MapTracker::local_mapping(int kf) {
   // ORACLE_LM_STEPS (diagnostics only, default 7): bit 1 SearchInNeighbors, 2 the local BA,
-  // 4 KeyFrameCulling
+  // 4 KeyFrameCulling; bit 8 set skips CreateNewMapPoints
   static const int steps = [] {
     const char* e = getenv("ORACLE_LM_STEPS");
     return e ? atoi(e) : 7;
   }();
-  // CreateNewMapPoints: needs SearchForTriangulation (BoW), skipped (oracle_map.h)
+  // CreateNewMapPoints (with a vocabulary: SearchForTriangulation needs FeatureVectors;
+  // bowmap_ref.cpp), then the rest of LocalMapping::Run (LocalMapping.cc:68-87)
+  if (voc_ && (steps & 8) == 0) create_new_map_points(kf);
   if (steps & 1) search_in_neighbors(kf);
   if ((steps & 2) && n_keyframes() > 2) local_bundle_adjustment(kf);
   if (steps & 4) keyframe_culling(kf);

@@ -252,6 +252,55 @@ def _map_dump_arrays(sizes):
     return {k: D[k][:rows[k]] for k in D}, D, st
 
 
+BOW_STAT_KEYS = ("bow_frames", "trk", "trk_ok", "reloc", "reloc_ok", "reloc_cands", "pnp_found",
+                 "sbp_rounds", "triangulated", "sft_matches", "kfdb")
+
+
+class Vocabulary:
+    """DBoW2 TemplatedVocabulary restated (oracle/bow_ref.cpp): loadFromTextFile, transform,
+    score."""
+
+    def __init__(self, path):
+        L = lib()
+        L.oracle_voc_load.restype = ctypes.c_void_p
+        L.oracle_voc_load.argtypes = [ctypes.c_char_p]
+        L.oracle_voc_free.argtypes = [ctypes.c_void_p]
+        self._h = L.oracle_voc_load(path.encode())
+        if not self._h:
+            raise RuntimeError("oracle: cannot load vocabulary %s" % path)
+        info = np.zeros(6, np.int32)
+        L.oracle_voc_info(ctypes.c_void_p(self._h), _p(info))
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = (int(v) for v in info)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.oracle_voc_free(self._h)
+            self._h = None
+
+    def transform(self, desc, levelsup=4):
+        """-> dict(word, weight, node per feature; bow_word, bow_value; fv (ids, start, feat))."""
+        desc = np.ascontiguousarray(desc, np.uint8)
+        n = len(desc)
+        m = max(n, 1)
+        fw = np.zeros(m, np.uint32); fx = np.zeros(m, np.float64); fn = np.zeros(m, np.uint32)
+        bw = np.zeros(m, np.uint32); bv = np.zeros(m, np.float64)
+        fvn = np.zeros(m, np.uint32); fvs = np.zeros(m + 1, np.int32); fvf = np.zeros(m, np.int32)
+        cnt = np.zeros(2, np.int32)
+        lib().oracle_voc_transform(ctypes.c_void_p(self._h), _p(desc), n, levelsup, _p(fw), _p(fx),
+                                   _p(fn), _p(bw), _p(bv), _p(fvn), _p(fvs), _p(fvf), _p(cnt))
+        nb, nn = int(cnt[0]), int(cnt[1])
+        return dict(word=fw[:n], weight=fx[:n], node=fn[:n], bow_word=bw[:nb], bow_value=bv[:nb],
+                    fv=(fvn[:nn], fvs[:nn + 1], fvf[:fvs[nn]]))
+
+    def score(self, a_word, a_value, b_word, b_value):
+        L = lib()
+        L.oracle_voc_score.restype = ctypes.c_double
+        a_word = np.ascontiguousarray(a_word, np.uint32); b_word = np.ascontiguousarray(b_word, np.uint32)
+        a_value = np.ascontiguousarray(a_value, np.float64); b_value = np.ascontiguousarray(b_value, np.float64)
+        return float(L.oracle_voc_score(ctypes.c_void_p(self._h), _p(a_word), _p(a_value), len(a_word),
+                                        _p(b_word), _p(b_value), len(b_word)))
+
+
 class Tracker:
     """CPU restatement of System::TrackRGBD (oracle/track_ref.cpp)."""
 
@@ -276,6 +325,19 @@ class Tracker:
         keys = ("n_ba", "n_fused", "n_culled", "n_ba_erased", "ba_trials", "ba_edges", "ba_kfs",
                 "ba_pts", "ba_max_opt_kfs", "n_reparent")
         return {k: int(v) for k, v in zip(keys, out)}
+
+    def set_vocabulary(self, path):
+        """System(voc, ...): run the reference's BoW steps (TrackReferenceKeyFrame,
+        Relocalization, CreateNewMapPoints) with this DBoW2 text vocabulary."""
+        L = lib()
+        L.oracle_tracker_set_vocabulary.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        if L.oracle_tracker_set_vocabulary(self._h, path.encode()) != 0:
+            raise RuntimeError("oracle: cannot load vocabulary %s" % path)
+
+    def bow_stats(self):
+        out = np.zeros(11, np.int64)
+        lib().oracle_tracker_bow_stats(ctypes.c_void_p(self._h), _p(out))
+        return dict(zip(BOW_STAT_KEYS, (int(v) for v in out)))
 
     def set_cull_ratio(self, r):
         """Test knob: KeyFrameCulling's redundancy ratio (0.9 in the reference)."""

@@ -253,6 +253,85 @@ void* oracle_tracker_create(int w, int h, float fx, float fy, float cx, float cy
 
 void oracle_tracker_destroy(void* t) { delete (OTracker*)t; }
 
+// System(voc, ...): the tracker runs the reference's BoW steps with this vocabulary (0 / -1)
+int oracle_tracker_set_vocabulary(void* tp, const char* path) {
+  OTracker* t = (OTracker*)tp;
+  std::unique_ptr<Vocabulary> v(new Vocabulary());
+  std::string err;
+  if (v->load_text(path, &err) != 0) return -1;
+  t->voc = std::move(v);
+  t->map.set_vocabulary(t->voc.get());
+  return 0;
+}
+
+// the BoW path's counters: [BoW frames, TrackReferenceKeyFrame calls, ok, Relocalization calls,
+// ok, candidates, PnP poses, SearchByProjection(F, KF) rounds, triangulated points,
+// SearchForTriangulation matches, database insertions]
+void oracle_tracker_bow_stats(void* tp, long long* out) {
+  const MapTracker::BowStats& b = ((OTracker*)tp)->map.bstats;
+  const long v[11] = {b.n_bow_frames, b.n_trk, b.n_trk_ok, b.n_reloc, b.n_reloc_ok,
+                      b.n_reloc_cands, b.n_pnp_found, b.n_sbp_rounds, b.n_triangulated,
+                      b.n_sft_matches, b.n_kfdb};
+  for (int i = 0; i < 11; i++) out[i] = v[i];
+}
+
+// ---- DBoW2 vocabulary probes (tests)
+void* oracle_voc_load(const char* path) {
+  Vocabulary* v = new Vocabulary();
+  std::string err;
+  if (v->load_text(path, &err) != 0) {
+    delete v;
+    return nullptr;
+  }
+  return v;
+}
+void oracle_voc_free(void* v) { delete (Vocabulary*)v; }
+// sizes: [k, L, scoring, weighting, nodes, words]
+void oracle_voc_info(void* vp, int* out) {
+  const Vocabulary* v = (const Vocabulary*)vp;
+  out[0] = v->k; out[1] = v->L; out[2] = v->scoring; out[3] = v->weighting;
+  out[4] = (int)v->parent.size(); out[5] = (int)v->words.size();
+}
+// transform(features, BowVector, FeatureVector, levelsup): per feature its word, weight and node
+// (feat_*: n each); the BowVector (words ascending, values) into bow_word / bow_value (cap n) and
+// the FeatureVector flattened (fv_node, fv_start n + 1, fv_feat n); counts[0..1] = entries, nodes
+int oracle_voc_transform(void* vp, const uint8_t* desc, int n, int levelsup, uint32_t* feat_word,
+                         double* feat_weight, uint32_t* feat_node, uint32_t* bow_word,
+                         double* bow_value, uint32_t* fv_node, int* fv_start, int* fv_feat,
+                         int* counts) {
+  const Vocabulary* v = (const Vocabulary*)vp;
+  for (int i = 0; i < n; i++) {
+    uint32_t w = 0, nd = 0;
+    double x = 0;
+    v->transform1(desc + 32 * (size_t)i, levelsup, w, x, nd);
+    feat_word[i] = w;
+    feat_weight[i] = x;
+    feat_node[i] = nd;
+  }
+  BowVec b;
+  FeatVecO f;
+  v->transform(desc, n, levelsup, b, f);
+  counts[0] = (int)b.word.size();
+  counts[1] = (int)f.node.size();
+  for (size_t i = 0; i < b.word.size(); i++) {
+    bow_word[i] = b.word[i];
+    bow_value[i] = b.value[i];
+  }
+  for (size_t i = 0; i < f.node.size(); i++) fv_node[i] = f.node[i];
+  for (size_t i = 0; i < f.start.size(); i++) fv_start[i] = f.start[i];
+  for (size_t i = 0; i < f.feat.size(); i++) fv_feat[i] = f.feat[i];
+  return 0;
+}
+double oracle_voc_score(void* vp, const uint32_t* wa, const double* va, int na,
+                        const uint32_t* wb, const double* vb, int nb) {
+  BowVec a, b;
+  a.word.assign(wa, wa + na);
+  a.value.assign(va, va + na);
+  b.word.assign(wb, wb + nb);
+  b.value.assign(vb, vb + nb);
+  return ((const Vocabulary*)vp)->score(a, b);
+}
+
 // LocalMapping counters: [BAs, fused, culled keyframes, BA-erased observations, BA trials, BA
 // edges, BA keyframe vertices, BA points, largest count of optimised keyframes, re-parented
 // spanning-tree children]

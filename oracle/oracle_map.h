@@ -49,6 +49,7 @@
 #include <set>
 #include <vector>
 
+#include "oracle_bow.h"
 #include "oracle_common.h"
 #include "oracle_match.h"
 #include "oracle_solve.h"
@@ -100,6 +101,14 @@ struct OKeyFrame {
   bool bad = false;
   long fuseTargetForKF = 0, baLocalForKF = 0, baFixedForKF = 0;
   std::vector<std::vector<int>> grid;  // mGrid (the frame's, copied), [ix * kGridRows + iy]
+  // BoW (with a vocabulary): mBowVec, mFeatVec; KeyFrameDatabase query fields (KeyFrame.h:146-149;
+  // mRelocScore is uninitialised in the reference: pinned 0)
+  BowVec bow;
+  FeatVecO fv;
+  bool hasBow = false;
+  long relocQuery = 0;
+  int relocWords = 0;
+  float relocScore = 0;
 };
 
 // Map-path fields of one Frame (Frame.h): its keys and descriptors live in OFrame.
@@ -109,6 +118,9 @@ struct MapFrame {
   std::vector<int> mps;          // mvpMapPoints
   std::vector<uint8_t> outlier;  // mvbOutlier
   int refKF = -1;                // mpReferenceKF
+  BowVec bow;                    // mBowVec / mFeatVec (Frame::ComputeBoW, with a vocabulary)
+  FeatVecO fv;
+  bool hasBow = false;
 };
 
 // What the parity tests compare besides the poses.
@@ -209,6 +221,16 @@ class MapTracker {
   } mstats;
   OMapPoint& mp(int h) { return h >= kTemp ? temps[h - kTemp] : pts[h]; }
   double cullRatio = 0.9;  // KeyFrameCulling's redundancy ratio (test knob; LocalMapping.cc:697)
+  // the vocabulary System is given (System.cc:67): with one, TrackReferenceKeyFrame,
+  // Relocalization and CreateNewMapPoints run as the reference's (bowmap_ref.cpp); without, the
+  // substitutes of the header comment
+  void set_vocabulary(const Vocabulary* v);
+  const Vocabulary* voc() const { return voc_; }
+  struct BowStats {
+    long n_bow_frames = 0, n_trk = 0, n_trk_ok = 0, n_reloc = 0, n_reloc_ok = 0,
+         n_reloc_cands = 0, n_pnp_found = 0, n_sbp_rounds = 0, n_triangulated = 0,
+         n_sft_matches = 0, n_kfdb = 0;
+  } bstats;
 
  private:
   bool track_with_motion_model(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
@@ -263,6 +285,25 @@ class MapTracker {
   int tracked_map_points(int kf, int minObs);
   void build_grid(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
                   const MapFrame& C, MatchFrame& G);
+  // ---- vocabulary path (bowmap_ref.cpp)
+  void compute_bow(const std::vector<uint8_t>& desc, MapFrame& C);
+  void kf_compute_bow(int kf);
+  void kfdb_add(int kf);
+  void kfdb_erase(int kf);
+  std::vector<int> detect_relocalization_candidates(const MapFrame& C);
+  bool track_reference_kf(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                          MapFrame& C, float* Tcw, const float* Tlast);
+  bool relocalization(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                      MapFrame& C, float* Tcw);
+  int search_by_projection_kf(const std::vector<Key>& keys, const std::vector<uint8_t>& desc,
+                              MapFrame& C, const float* Tcw, int kf, const std::set<int>& found,
+                              float th, int orbDist);
+  void create_new_map_points(int kf);
+  int search_for_triangulation(int kf1, int kf2, const float* F12,
+                               std::vector<std::pair<int, int>>& pairs);
+  const Vocabulary* voc_ = nullptr;
+  std::vector<std::vector<int>> invfile_;  // KeyFrameDatabase::mvInvertedFile
+  GlibcRand rand_{1};                      // the process's rand() (PnPsolver's draws)
 
   int state_ = 0;
   long frameNextId_ = 0;

@@ -1,5 +1,6 @@
 // oracle/oracle_track.h -- TEST INFRASTRUCTURE ONLY (see orb_ref.cpp header).
 #pragma once
+#include <memory>
 #include <array>
 #include <cstdint>
 #include <functional>
@@ -73,6 +74,7 @@ class OTracker {
   bool bFirstFrame = false, bSecondFrame = false, hasVelocity = false;
   bool reset_pending = false;  // System::Reset requested (LOST with <= 5 keyframes)
   MapTracker map;
+  std::unique_ptr<Vocabulary> voc;  // System's vocabulary (null: the substitutes, oracle_map.h)
   float V[16] = {0};
   float g0 = 0;
   OFrame L;  // mLastFrame

@@ -1,0 +1,135 @@
+"""GPU parity of the vocabulary-driven path against the CPU oracle.
+
+The DBoW2 vocabulary is tests/golden/test_voc_k10l6.txt (the reference's ORBvoc.txt is missing;
+tools/make_test_vocabulary.py writes this one in the same text format).  With it the tracker runs
+the reference's TrackReferenceKeyFrame (SearchByBoW against the reference keyframe),
+Relocalization (keyframe database, SearchByBoW, PnPsolver, the SearchByProjection(F, KF) rounds)
+and LocalMapping's CreateNewMapPoints (SearchForTriangulation), on the GPU kernels of
+mmt_bow.hip / mmt_match.hip / mmt_pnp.hip / mmt_lm.hip.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_kitti_frame
+from synth_problems import K_KITTI
+
+pytestmark = pytest.mark.gpu
+
+VOC = os.path.join(GOLDEN, "test_voc_k10l6.txt")
+BOW_KEYS = ("bow_frames", "trk", "trk_ok", "reloc", "reloc_ok", "reloc_cands", "pnp_found",
+            "sbp_rounds", "triangulated", "sft_matches", "kfdb")
+
+
+def test_bow_transform_bit_exact(oracle_mod):
+    """k_bow_transform (one descent per descriptor) against the oracle's transform over the
+    kitti_sample frames' descriptors: word ids, weights and level-2 nodes identical."""
+    import multimot_track_amd as M
+    ov = oracle_mod.Vocabulary(VOC)
+    ctx = M.Context(M.kitti03_config(1242, 375, 2000))
+    try:
+        ctx.load_vocabulary(VOC)
+        for i in range(5):
+            g = oracle_mod.gray_from_bgr(load_kitti_frame(i)["bgr"])
+            _, d = oracle_mod.orb_extract(g, 2000)
+            for levelsup in (4, 3, 6):
+                w, x, nd = ctx.bow_transform(d, levelsup)
+                r = ov.transform(d, levelsup)
+                assert np.array_equal(w, r["word"]), (i, levelsup)
+                assert np.array_equal(x, r["weight"]), (i, levelsup)
+                assert np.array_equal(nd, r["node"]), (i, levelsup)
+        # random descriptors (far from every training descriptor: ties at every level)
+        d = np.random.default_rng(5).integers(0, 256, (3000, 32), dtype=np.uint8)
+        w, x, nd = ctx.bow_transform(d, 4)
+        r = ov.transform(d, 4)
+        assert np.array_equal(w, r["word"]) and np.array_equal(nd, r["node"])
+    finally:
+        ctx.close()
+
+
+def test_load_vocabulary_errors(tmp_path):
+    import multimot_track_amd as M
+    ctx = M.Context(M.kitti03_config(1242, 375, 2000))
+    try:
+        with pytest.raises(RuntimeError):
+            ctx.load_vocabulary(str(tmp_path / "missing.txt"))
+        p = tmp_path / "bad.txt"
+        p.write_text("10 12 0 0\n")  # L > 10 (TemplatedVocabulary.h:1359)
+        with pytest.raises(RuntimeError):
+            ctx.load_vocabulary(str(p))
+        ctx.load_vocabulary(VOC)
+    finally:
+        ctx.close()
+
+
+def _run_pair(oracle_mod, W, H, K, bf, nfeat, n, lost, chunk=16, seed=1003):
+    import torch
+    import multimot_track_amd as M
+    from multimot_track_amd import scene
+    dev = torch.device("cuda:0")
+    R = scene.SequenceRenderer(scene.StreetScene(3, seed), W, H, K=K, device=dev)
+    seq = R.sequence(n)
+    for i in lost:
+        seq["bgr"][i] = 128
+    cfg = M.kitti03_config(W, H, nfeat, max_batch=chunk)
+    cfg.fx, cfg.fy, cfg.cx, cfg.cy, cfg.bf = K["fx"], K["fy"], K["cx"], K["cy"], bf
+    ctx = M.Context(cfg)
+    got = []
+    try:
+        ctx.load_vocabulary(VOC)
+        for s0 in range(0, n, chunk):
+            sl = slice(s0, min(n, s0 + chunk))
+            got += ctx.track_chunk_device(seq["bgr"][sl], seq["disp"][sl], seq["flow"][sl],
+                                          seq["mask"][sl])
+        gb = ctx.bow_counters()
+        gm = ctx.map_dump()
+    finally:
+        ctx.close()
+    tr = oracle_mod.Tracker(W, H, (K["fx"], K["fy"], K["cx"], K["cy"]), bf, 0, nfeat)
+    tr.set_vocabulary(VOC)
+    ora = []
+    for i in range(n):
+        f = scene.to_numpy_frames({k: seq[k][i:i + 1] for k in ("bgr", "disp", "flow", "mask")})[0]
+        ora.append(tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]))
+    return got, ora, gb, tr.bow_stats(), gm, tr.map_dump()
+
+
+def _check_maps(gm, om):
+    for k in ("kf_i", "kf_mps_start", "kf_mps", "pt_i", "obs_start", "obs_i", "conn", "ord",
+              "child"):
+        assert np.array_equal(gm[k], om[k]), k
+    assert np.abs(gm["kf_T"] - om["kf_T"]).max() < 1e-4
+    assert np.abs(gm["pt_f"] - om["pt_f"]).max() < 1e-3
+
+
+def test_vocabulary_tracking_half_res_matches_oracle(oracle_mod):
+    """Half-resolution C3 drive, one textureless frame: the GPU tracker takes the oracle's
+    TrackReferenceKeyFrame / Relocalization / CreateNewMapPoints path frame by frame (poses within
+    the bar, integers exact), its vocabulary counters equal the oracle's, and the final map graph
+    is the oracle's."""
+    from multimot_track_amd import scene
+    from oracle import compare
+    K = {k: v * 0.5 for k, v in scene.KITTI03.items()}
+    got, ora, gb, ob, gm, om = _run_pair(oracle_mod, 621, 187, K, K["bf"], 1000, 40, [24])
+    rec = compare.parity_record(got, ora)
+    assert rec["first_divergent_frame"] is None, rec
+    assert {k: gb[k] for k in BOW_KEYS} == {k: ob[k] for k in BOW_KEYS}
+    assert ob["trk_ok"] >= 1 and ob["reloc"] >= 1 and ob["triangulated"] > 0
+    _check_maps(gm, om)
+
+
+def test_vocabulary_tracking_c3_300_frames_matches_oracle(oracle_mod):
+    """The C3 workload (1242x375, 2000 features, ego + 3 objects) over 300 frames with the
+    vocabulary and two textureless frames: every frame matches the oracle, reference-keyframe
+    tracking, relocalisation (with its SearchByProjection rounds) and triangulation all taken."""
+    from multimot_track_amd import scene
+    from oracle import compare
+    K = dict(scene.KITTI03)
+    got, ora, gb, ob, gm, om = _run_pair(oracle_mod, 1242, 375, K, 387.5744, 2000, 300,
+                                         [120, 230], chunk=32)
+    rec = compare.parity_record(got, ora)
+    assert rec["first_divergent_frame"] is None, rec
+    assert {k: gb[k] for k in BOW_KEYS} == {k: ob[k] for k in BOW_KEYS}, (gb, ob)
+    assert ob["trk_ok"] >= 1 and ob["reloc"] >= 2 and ob["triangulated"] > 100
+    _check_maps(gm, om)

@@ -1,0 +1,176 @@
+"""CPU checks of the vocabulary restatement (oracle/bow_ref.cpp, oracle/bowmap_ref.cpp).
+
+The reference's ORBvoc.txt is missing (.MISSING_LARGE_BLOBS); tests/golden/test_voc_k10l6.txt is
+a vocabulary in the same DBoW2 text format (tools/make_test_vocabulary.py).  The oracle's
+loadFromTextFile / transform / L1 score are pinned here against an independent pure-Python
+restatement of TemplatedVocabulary.h:1127-1259, 1338-1424 and ScoringObject.cpp, over the
+kitti_sample frames' ORB descriptors.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_kitti_frame
+
+VOC = os.path.join(GOLDEN, "test_voc_k10l6.txt")
+
+
+def py_vocabulary(path):
+    """loadFromTextFile, restated in Python: (k, L, scoring, weighting, parent, children,
+    descriptors (n x 32 u8), weight, word id per node)."""
+    lines = open(path).read().split("\n")
+    k, L, n1, n2 = (int(v) for v in lines[0].split())
+    parent, children, desc, weight, word = [-1], [[]], [np.zeros(32, np.uint8)], [0.0], [-1]
+    nw = 0
+    for ln in lines[1:]:
+        if not ln.strip():
+            continue
+        t = ln.split()
+        pid, leaf = int(t[0]), int(t[1])
+        nid = len(parent)
+        parent.append(pid)
+        children[pid].append(nid)
+        children.append([])
+        desc.append(np.array([int(v) for v in t[2:34]], np.uint8))
+        weight.append(float(t[34]))
+        word.append(nw if leaf > 0 else -1)
+        nw += leaf > 0
+    return k, L, n1, n2, parent, children, np.stack(desc), np.array(weight), np.array(word)
+
+
+def py_transform(V, d, levelsup=4):
+    """transform(feature, word, weight, &nid, levelsup): strict-< descent, first child wins."""
+    k, L, _, _, _, children, desc, weight, word = V
+    bits = np.unpackbits(desc, axis=1)
+    fb = np.unpackbits(d)
+    nid_level = L - levelsup
+    nid = 0
+    cur, level = 0, 0
+    while True:
+        level += 1
+        ch = children[cur]
+        dist = (bits[ch] != fb).sum(1)
+        cur = ch[int(np.argmin(dist))]  # argmin returns the first of equal minima
+        if level == nid_level:
+            nid = cur
+        if not children[cur]:
+            break
+    return int(word[cur]), float(weight[cur]), nid
+
+
+def py_bow(V, descs, levelsup=4):
+    """TF-IDF BowVector (weights summed in feature order, L1-normalised) + FeatureVector."""
+    bow, fv = {}, {}
+    for i, d in enumerate(descs):
+        w, x, nd = py_transform(V, d, levelsup)
+        if not x > 0:
+            continue
+        bow[w] = bow.get(w, 0.0) + x
+        fv.setdefault(nd, []).append(i)
+    norm = 0.0
+    for w in sorted(bow):  # BowVector::normalize walks the map in word order
+        norm += abs(bow[w])
+    if norm > 0:
+        bow = {w: v / norm for w, v in bow.items()}
+    return bow, fv
+
+
+def py_l1(a, b):
+    s = 0.0
+    for w in sorted(set(a) & set(b)):
+        s += abs(a[w] - b[w]) - abs(a[w]) - abs(b[w])
+    return -s / 2.0
+
+
+@pytest.fixture(scope="module")
+def kitti_desc(oracle_mod):
+    out = []
+    for i in range(5):
+        g = oracle_mod.gray_from_bgr(load_kitti_frame(i)["bgr"])
+        out.append(oracle_mod.orb_extract(g, 2000)[1])
+    return out
+
+
+def test_vocabulary_loader_matches_python_restatement(oracle_mod):
+    V = py_vocabulary(VOC)
+    o = oracle_mod.Vocabulary(VOC)
+    assert (o.k, o.L, o.scoring, o.weighting) == (10, 6, 0, 0) == V[:4]
+    assert o.n_nodes == len(V[4])
+    assert o.n_words == int((V[8] >= 0).sum())
+
+
+def test_transform_matches_python_restatement(oracle_mod, kitti_desc):
+    V = py_vocabulary(VOC)
+    o = oracle_mod.Vocabulary(VOC)
+    for d in kitti_desc[:2]:
+        r = o.transform(d, 4)
+        sel = np.arange(0, len(d), 7)  # the pure-Python descent is slow: a subset of features
+        for i in sel:
+            w, x, nd = py_transform(V, d[i])
+            assert (int(r["word"][i]), float(r["weight"][i]), int(r["node"][i])) == (w, x, nd)
+    d = kitti_desc[1]
+    r = o.transform(d, 4)
+    bow, fv = py_bow(V, d)
+    assert list(r["bow_word"]) == sorted(bow)
+    assert np.array_equal(r["bow_value"], np.array([bow[w] for w in sorted(bow)]))
+    ids, start, feat = r["fv"]
+    assert list(ids) == sorted(fv)
+    for q, nd in enumerate(ids):
+        assert list(feat[start[q]:start[q + 1]]) == fv[int(nd)]
+    # every feature listed once, at the level-2 node its descent passes (L - levelsup = 2)
+    assert len(set(feat.tolist())) == len(feat)
+    assert abs(sum(r["bow_value"]) - 1.0) < 1e-12
+
+
+def test_l1_score(oracle_mod, kitti_desc):
+    o = oracle_mod.Vocabulary(VOC)
+    V = py_vocabulary(VOC)
+    r = [o.transform(d, 4) for d in kitti_desc]
+    b = [py_bow(V, d)[0] for d in kitti_desc[:3]]
+    for i in range(3):
+        assert o.score(r[i]["bow_word"], r[i]["bow_value"], r[i]["bow_word"], r[i]["bow_value"]) \
+            == pytest.approx(1.0, abs=1e-12)
+        for j in range(3):
+            s = o.score(r[i]["bow_word"], r[i]["bow_value"], r[j]["bow_word"], r[j]["bow_value"])
+            assert s == pytest.approx(py_l1(b[i], b[j]), abs=1e-12)
+            assert 0.0 <= s <= 1.0 + 1e-12
+    # consecutive kitti frames share more words than frames four apart
+    s01 = o.score(r[0]["bow_word"], r[0]["bow_value"], r[1]["bow_word"], r[1]["bow_value"])
+    s04 = o.score(r[0]["bow_word"], r[0]["bow_value"], r[4]["bow_word"], r[4]["bow_value"])
+    assert s01 > s04
+
+
+def test_loader_rejects_bad_header(oracle_mod, tmp_path):
+    p = tmp_path / "bad.txt"
+    p.write_text("30 6 0 0\n0 1 " + " ".join(["0"] * 32) + " 1.0")  # k > 20 (TemplatedVocabulary.h:1359)
+    with pytest.raises(RuntimeError):
+        oracle_mod.Vocabulary(str(p))
+
+
+def test_oracle_tracker_with_vocabulary_runs_bow_paths(oracle_mod):
+    """The oracle tracker with the test vocabulary over a half-resolution C3 drive with one
+    textureless frame: TrackReferenceKeyFrame (second frame and after the relocalisation),
+    Relocalization through the keyframe database + SearchByBoW + PnPsolver, and
+    CreateNewMapPoints all run; the map passes the invariant checks."""
+    from map_invariants import check_map
+    from multimot_track_amd import scene
+    K = {k: v * 0.5 for k, v in scene.KITTI03.items()}
+    W, H = 621, 187
+    R = scene.SequenceRenderer(scene.StreetScene(3, 1003), W, H, K=K)
+    tr = oracle_mod.Tracker(W, H, (K["fx"], K["fy"], K["cx"], K["cy"]), K["bf"], 0, 1000)
+    tr.set_vocabulary(VOC)
+    states = []
+    for i in range(30):
+        b, d, f, m = R.frame(i)
+        b = b.numpy()
+        if i == 24:
+            b = np.full_like(b, 128)
+        states.append(tr.track(b, d.numpy().view(np.uint16), f.numpy(), m.numpy())["map_state"])
+    st = tr.bow_stats()
+    assert states[:24] == [1] * 24 and states[24] == 2, states
+    assert st["trk"] >= 1 and st["trk_ok"] >= 1
+    assert st["reloc"] >= 1 and st["reloc_cands"] >= 1
+    assert st["triangulated"] > 0 and st["sft_matches"] >= st["triangulated"]
+    assert st["kfdb"] > 0
+    assert check_map(tr.map_dump()) == []
