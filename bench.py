@@ -56,6 +56,15 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0
 METRIC = "KITTI RGB-D frames/sec (ego+object poses) at 1/2/4/8 GPUs; CPU ref fps"
+WORKLOADS = {
+    "C2": "C2: KITTI-03-like RGB-D, ego only (%d object motions), end-to-end TrackRGBD",
+    "C3": "C3: KITTI-03-like RGB-D, end-to-end TrackRGBD (ORB + association + ego + %d object "
+          "motions)",
+    "C4": "C4: KITTI 00/03/05/07-like RGB-D sequences, one per rank (their geometry, length and "
+          "seed), 4000 features, ego + %d object motions, end-to-end TrackRGBD",
+    "C5": "C5: 1920x1080 synthetic RGB-D streams, 8000 features, ego + %d rigid object motions, "
+          "end-to-end TrackRGBD",
+}
 
 
 def b_orb(w, h, nfeat, lw, lh):
@@ -89,6 +98,14 @@ def load_traffic(path, cfg_key):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=("C2", "C3", "C4", "C5"), default="C3",
+                    help="BASELINE.json workload per rank (multimot_track_amd/shard.py workload): "
+                         "C3 (default) KITTI-03 + 3 objects; C4 KITTI 00/03/05/07 geometry, "
+                         "length and seed per rank at 4000 features; C5 1920x1080, 8000 "
+                         "features, eight rigid object motions")
+    ap.add_argument("--dry-length-scale", type=float, default=1.0,
+                    help="(--dry) scale of the C4 sequence lengths: rehearses ranks whose "
+                         "sequences end before the timed steps do")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--chunk", type=int, default=128,
@@ -255,7 +272,27 @@ def cpu_multi_leg(args, render, W, H, NF, fps1):
                       "per-core rates" % (K, 2002 + K, args.cpu_seqs_seconds)}
 
 
-def rank_parity(args, seqs, seq_frames, rank, K, W, H, NF):
+def ego_rpe(frames, gt_tcw):
+    """Relative pose error of the ego track against the renderer's ground truth, over
+    consecutive frames (the reference's camera RPE, Tracking.cc:1319-1345, taken per frame step):
+    the translation (m) and rotation (deg) of (G_b G_a^-1)^-1 (T_b T_a^-1); median, p95 and max."""
+    te, re = [], []
+    for a in range(len(frames) - 1):
+        Ta = np.asarray(frames[a]["Tcw"], np.float64)
+        Tb = np.asarray(frames[a + 1]["Tcw"], np.float64)
+        Ga, Gb = np.asarray(gt_tcw[a], np.float64), np.asarray(gt_tcw[a + 1], np.float64)
+        E = np.linalg.inv(Gb @ np.linalg.inv(Ga)) @ (Tb @ np.linalg.inv(Ta))
+        te.append(float(np.linalg.norm(E[:3, 3])))
+        re.append(float(np.degrees(np.arccos(np.clip((np.trace(E[:3, :3]) - 1) / 2, -1, 1)))))
+    if not te:
+        return None
+    q = lambda v, p: round(float(np.percentile(v, p)), 6)  # noqa: E731
+    return {"frames": len(te) + 1, "trans_m_median": q(te, 50), "trans_m_p95": q(te, 95),
+            "trans_m_max": round(max(te), 6), "rot_deg_median": q(re, 50),
+            "rot_deg_p95": q(re, 95), "rot_deg_max": round(max(re), 6)}
+
+
+def rank_parity(args, seqs, seq_frames, rank, wls):
     """The oracle over the first --rank-parity-frames frames of each of this rank's sequences
     (one core each, after the timed region), compared with the GPU's frames: a compact parity
     record per sequence for multi-sequence and multi-rank lines."""
@@ -263,14 +300,17 @@ def rank_parity(args, seqs, seq_frames, rank, K, W, H, NF):
     from multimot_track_amd import shard
     from oracle import compare, oracle as O
     O.build()
-    n = min(args.rank_parity_frames, len(seq_frames[0]))
+    K = len(wls)
+    n = min([args.rank_parity_frames] + [len(f) for f in seq_frames])
     frames = [[seq_frame_numpy(seqs[k], i) for i in range(n)] for k in range(K)]
 
     def one(k):  # the oracle's C calls release the GIL: one thread per sequence
-        tr = O.Tracker(W, H, (721.5377, 721.5377, 609.5593, 172.8540), 387.5744, 0, NF)
+        wl = wls[k]
+        tr = O.Tracker(wl["width"], wl["height"], (721.5377, 721.5377, 609.5593, 172.8540),
+                       387.5744, 0, wl["nfeatures"])
         ofr = [tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]) for f in frames[k]]
         rec = compare.parity_record(seq_frames[k][:n], ofr)
-        return {"rank": rank, "sequence": k, "seed": shard.sequence_seed(1003, rank * K + k),
+        return {"rank": rank, "sequence": k, "workload": wl["name"], "seed": wl["seed"],
                 "frames": rec["frames"], "first_divergent_frame": rec["first_divergent_frame"],
                 "max_pose_diff": rec["max_pose_diff"],
                 "int_mismatch_frames": rec["int_mismatch_frames"],
@@ -289,31 +329,42 @@ def run_dry(args, rank, world):
     from multimot_track_amd import shard
     dev = torch.device("cpu")
     C, K = args.chunk, args.seqs_per_gpu
-    seeds = [shard.sequence_seed(1003, rank * K + k) for k in range(K)]
+    wls = [shard.workload(args.config, rank * K + k) for k in range(K)]
+    seeds = [wl["seed"] for wl in wls]
+    rsteps = []
+    for wl in wls:
+        n = None if wl["length"] is None else int(wl["length"] * args.dry_length_scale)
+        rsteps.append(shard.rank_steps(n, C, args.warmup, args.steps))
     step_s = 0.01 * (rank + 1)  # rank r's stand-in step cost
-    for _ in range(args.warmup):
+    for _ in range(max(w for w, _ in rsteps)):
         time.sleep(step_s)
     shard.barrier(world, dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(max(t for _, t in rsteps)):
         time.sleep(step_s)
     shard.barrier(world, dev)
     elapsed = shard.max_over_ranks(time.perf_counter() - t0, world, dev)
-    frames_all = shard.sum_over_ranks(args.steps * C * K, world, dev)
+    frames_all = shard.sum_over_ranks(sum(t for _, t in rsteps) * C, world, dev)
+    mine = [dict(name=wl["name"], seed=wl["seed"], width=wl["width"], height=wl["height"],
+                 timed_steps=t) for wl, (_, t) in zip(wls, rsteps)]
     all_seeds = [None] * world
+    all_wl = [None] * world
     if world > 1:
         dist.all_gather_object(all_seeds, seeds)
+        dist.all_gather_object(all_wl, mine)
     else:
         all_seeds = [seeds]
+        all_wl = [mine]
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(frames_all / elapsed, 2),
                           "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                           "dtype": "u8", "data": "dry run (no GPU work)",
-                          "config": {"workload": "dry", "chunk_frames": C, "sequences_per_gpu": K,
+                          "config": {"workload": "dry", "config": args.config,
+                                     "chunk_frames": C, "sequences_per_gpu": K,
                                      "parallelism": "dp%d" % world, "seeds": all_seeds,
-                                     "frames_all": frames_all}}), flush=True)
+                                     "ranks": all_wl, "frames_all": frames_all}}), flush=True)
 
 
 # ------------------------------------------------------------------ main
@@ -347,30 +398,44 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    W, H, NF, C, K = args.width, args.height, args.nfeatures, args.chunk, args.seqs_per_gpu
-    nframes = (args.warmup + args.steps) * C
+    C, K = args.chunk, args.seqs_per_gpu
+    # this rank's sequences (shard.workload: C3 by default; C4 / C5 per-rank geometry and length)
+    wls = [shard.workload(args.config, rank * K + k) for k in range(K)]
+    if args.config == "C3":  # the C3 knobs stay overridable
+        for wl in wls:
+            wl.update(width=args.width, height=args.height, nfeatures=args.nfeatures,
+                      objects=args.objects)
+    rsteps = [shard.rank_steps(wl["length"], C, args.warmup, args.steps) for wl in wls]
+    W, H, NF = wls[0]["width"], wls[0]["height"], wls[0]["nfeatures"]
     t_gen = time.perf_counter()
 
-    def render(seed, n, objects=args.objects):
+    def render(seed, n, objects=None, wl=None):
         # in pieces of 400 frames (each frame is rendered on its own, so the sequence is the
         # same), with a progress line on stderr for long runs under a profiler
+        wl = wl or wls[0]
+        objects = wl["objects"] if objects is None else objects
         parts = []
         for s0 in range(0, n, 400):
-            parts.append(scene.kitti_like_sequence(min(400, n - s0), W, H, n_objects=objects,
-                                                   seed=seed, device=dev, start=s0))
+            parts.append(scene.kitti_like_sequence(min(400, n - s0), wl["width"], wl["height"],
+                                                   n_objects=objects, seed=seed, device=dev,
+                                                   start=s0, lanes=wl["lanes"]))
             print("rank %d: rendered %d / %d frames" % (rank, s0 + len(parts[-1]["Tcw"]), n),
                   file=sys.stderr, flush=True)
         out = {k: torch.cat([p[k] for p in parts]) for k in ("bgr", "disp", "flow", "mask")}
         out["Tcw"] = np.concatenate([p["Tcw"] for p in parts])
+        if wl["parts"] > 1 and objects > 0:  # C5: rigid column bands of the boxes (8 motions)
+            out["mask"] = scene.split_label_bands(out["mask"], wl["parts"])
         return out
 
-    seqs = [render(shard.sequence_seed(1003, rank * K + k), nframes) for k in range(K)]
+    seqs = [render(wl["seed"], (w + t) * C, wl=wl) for wl, (w, t) in zip(wls, rsteps)]
     seq = seqs[0]
     torch.cuda.synchronize(dev)
     t_gen = time.perf_counter() - t_gen
 
-    cfg = M.kitti03_config(W, H, NF, max_batch=C, device_id=local)
-    ctxs = [M.Context(cfg) for _ in range(K)]
+    cfgs = [M.kitti03_config(wl["width"], wl["height"], wl["nfeatures"], max_batch=C,
+                             device_id=local) for wl in wls]
+    cfg = cfgs[0]
+    ctxs = [M.Context(c) for c in cfgs]
     ctx = ctxs[0]
     if not args.immediate:
         for c in ctxs:
@@ -393,18 +458,21 @@ def main(argv=None):
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(max_workers=K)
 
-    def step(i):  # the raw results of every sequence of this rank
+    def step(i, timed):  # the raw results of this rank's sequences that still have chunk i
+        ks = [k for k in range(K) if (i < rsteps[k][1] if timed else i < rsteps[k][0])]
+        idx = [(rsteps[k][0] + i) if timed else i for k in ks]
         if pool is None:
-            return [step_k(0, i)]
-        return [f.result() for f in [pool.submit(step_k, k, i) for k in range(K)]]
+            return {k: step_k(k, j) for k, j in zip(ks, idx)}
+        futs = {k: pool.submit(step_k, k, j) for k, j in zip(ks, idx)}
+        return {k: f.result() for k, f in futs.items()}
 
-    warm = [step(i) for i in range(args.warmup)]
+    warm = [step(i, False) for i in range(max(w for w, _ in rsteps))]
     torch.cuda.synchronize(dev)
     ctx.profile_enable(True)
     ctx.profile_read(reset=True)
     shard.barrier(world, dev)
     t0 = time.perf_counter()
-    results = [step(args.warmup + i) for i in range(args.steps)]
+    results = [step(i, True) for i in range(max(t for _, t in rsteps))]
     flushed = [[] for _ in range(K)]
     if not args.immediate:  # the timed frames' last object motions, inside the timed region
         if pool is None:
@@ -416,20 +484,31 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     prof = ctx.profile_read()
     elapsed = shard.max_over_ranks(elapsed, world, dev)
-    frames_all = shard.sum_over_ranks(args.steps * C * K, world, dev)
+    frames_all = shard.sum_over_ranks(sum(t for _, t in rsteps) * C, world, dev)
 
     # per-frame outputs of every sequence (sanity: every timed frame tracked by the map, objects
     # found); a line whose timed frames are not all tracked is marked invalid
-    seq_frames = [assemble([r[k] for r in warm + results], C, flushed[k]) for k in range(K)]
+    seq_frames = [assemble([r[k] for r in warm + results if k in r], C, flushed[k])
+                  for k in range(K)]
     all_frames = seq_frames[0]
-    timed_frames = all_frames[args.warmup * C:]
-    n_obj_last = len(timed_frames[-1]["objects"])
-    tracked_rank = sum(int(d["initialized"]) for f in seq_frames for d in f[args.warmup * C:])
+    timed_frames = all_frames[rsteps[0][0] * C:]
+    n_obj_last = len(timed_frames[-1]["objects"]) if timed_frames else 0
+    tracked_rank = sum(int(d["initialized"]) for k, f in enumerate(seq_frames)
+                       for d in f[rsteps[k][0] * C:])
     tracked = int(shard.sum_over_ranks(tracked_rank, world, dev))
-    lost_first = [next((args.warmup * C + i for i, d in enumerate(f[args.warmup * C:])
-                        if not d["initialized"]), None) for f in seq_frames]
-    gt = seq["Tcw"][-1]
-    ego_err = float(np.abs(timed_frames[-1]["Tcw"] - gt).max())
+    lost_first = [next((rsteps[k][0] * C + i for i, d in enumerate(f[rsteps[k][0] * C:])
+                        if not d["initialized"]), None) for k, f in enumerate(seq_frames)]
+    gt = seq["Tcw"][len(all_frames) - 1]
+    ego_err = float(np.abs(all_frames[-1]["Tcw"] - gt).max())
+    rpe = ego_rpe(all_frames[rsteps[0][0] * C:], seq["Tcw"][rsteps[0][0] * C:len(all_frames)])
+    rank_wl = [dict(name=wl["name"], seed=wl["seed"], width=wl["width"], height=wl["height"],
+                    orb_features=wl["nfeatures"], objects=wl["objects"] * wl["parts"],
+                    frames_timed=rsteps[k][1] * C, length=wl["length"])
+               for k, wl in enumerate(wls)]
+    if world > 1:
+        g = [None] * world
+        dist.all_gather_object(g, rank_wl)
+        rank_wl = [r for x in g for r in x]
     mc = ctx.map_counters()
     local_mapping = {k: int(mc[k]) for k in ("n_ba", "n_fused", "n_culled", "n_ba_erased",
                                              "ba_trials", "ba_edges", "ba_pts", "ba_max_opt",
@@ -448,7 +527,7 @@ def main(argv=None):
     # or ranks: the N = 1 line's CPU leg below checks the one sequence over more frames)
     rank_par = None
     if (world > 1 or K > 1) and args.rank_parity_frames > 0:
-        rank_par = rank_parity(args, seqs, seq_frames, rank, K, W, H, NF)
+        rank_par = rank_parity(args, seqs, seq_frames, rank, wls)
         if world > 1:
             gathered = [None] * world
             dist.all_gather_object(gathered, rank_par)
@@ -462,7 +541,7 @@ def main(argv=None):
         key = "%dx%d_n%d_b%d" % (W, H, NF, C)
         traffic = load_traffic(args.traffic_file, key)
         cpu, parity, c2, single = None, None, None, None
-        if world == 1 and args.single_frames > 0:
+        if world == 1 and args.single_frames > 0 and args.config == "C3":
             # the reference-shaped call pattern: one frame per call (rgbd_tum.cc's loop), objects
             # deferred; a fresh sequence context over the frames after the timed region
             ns = args.single_frames
@@ -489,7 +568,7 @@ def main(argv=None):
                                 "flush inside the timed region" % (7 + ns)}
             sctx.close()
             del s1
-        if world == 1 and args.c2_steps > 0:
+        if world == 1 and args.c2_steps > 0 and args.config == "C3":
             # C2 (ego only): same camera and sequence seed, mask == 0
             nc2 = (1 + args.c2_steps) * C
             s2 = render(shard.sequence_seed(1003, 0), nc2, objects=0)
@@ -506,7 +585,7 @@ def main(argv=None):
             c2ctx.close()
         if world == 1 and not args.no_cpu:
             gpu_frames = all_frames
-            timed_from = args.warmup * C
+            timed_from = rsteps[0][0] * C
             n_t, t_t, parity = cpu_leg(args, seq, gpu_frames, timed_from, W, H, NF)
             fps1 = n_t / t_t if t_t > 0 else 0.0
             cpu = {"value": round(fps1, 3), "unit": "frames/s", "cores": 1,
@@ -542,8 +621,8 @@ def main(argv=None):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic (seeded ray-cast street sequence, exact depth/flow/"
                                    "labels, KITTI-03 camera), resident in HBM",
-            "config": {"workload": "C3: KITTI-03-like RGB-D, end-to-end TrackRGBD (ORB + "
-                                   "association + ego + %d object motions)" % args.objects,
+            "config": {"workload": WORKLOADS[args.config] % (wls[0]["objects"] * wls[0]["parts"]),
+                       "config": args.config, "ranks": rank_wl, "ego_rpe": rpe,
                        "width": W, "height": H, "orb_features": NF, "chunk_frames": C,
                        "sequences_per_gpu": K, "parallelism": "dp%d" % world,
                        "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
@@ -560,7 +639,7 @@ def main(argv=None):
                          "launch_ms": round(launch_ms, 4), "bytes_per_launch": bytes_per_launch,
                          "orb_share_of_step": round(prof["orb_ms"] / (elapsed * 1e3), 4)},
             "cpu_baseline": cpu,
-            "parity": parity,
+            "parity": parity if parity is None else dict(parity, ego_rpe=rpe),
             "rank_parity": rank_par,
         }
         if tracked != frames_timed:

@@ -253,3 +253,25 @@ def to_numpy_frames(seq):
                         disp=seq["disp"][i].cpu().numpy().view(np.uint16),
                         flow=seq["flow"][i].cpu().numpy(), sem=seq["mask"][i].cpu().numpy()))
     return out
+
+
+def split_label_bands(mask, parts):
+    """Each box label (1..3) split into `parts` rigid column bands with labels of their own
+    (1 + (L - 1) parts + band), per frame, on the mask's device: BASELINE C5's eight rigid motions
+    from two boxes (parts = 4).  Same bands as tests/test_gpu_track.py's split_labels."""
+    import torch
+    out = torch.zeros_like(mask)
+    W = mask.shape[-1]
+    cols = torch.arange(W, device=mask.device)
+    for f in range(mask.shape[0]):
+        o = out[f]
+        for L in (1, 2, 3):
+            m = mask[f] == L
+            anyc = m.any(0).nonzero()
+            if anyc.numel() == 0:
+                continue
+            u0 = int(anyc.min())
+            w = int(anyc.max()) - u0 + 1
+            q = torch.clamp(torch.div((cols - u0) * parts, w, rounding_mode="floor"), max=parts - 1)
+            o[:] = torch.where(m, (1 + (L - 1) * parts + q)[None, :].to(mask.dtype), o)
+    return out

@@ -75,3 +75,37 @@ def test_bench_self_launches_ranks_dry():
     # the slower rank (2 x 10 ms per step) sets the time: 3 steps >= 60 ms
     assert d["ms_per_step"] >= 20.0
     assert d["value"] == pytest.approx(48 / (d["ms_per_step"] * 3 / 1000.0), rel=0.02)
+
+
+def test_bench_c4_per_rank_workloads_dry():
+    """bench.py --config C4: rank r tracks KITTI 00 / 03 / 05 / 07's geometry, length and seed
+    (shard.workload); a rank whose sequence ends early times fewer chunks, the job's time is still
+    the MAX over ranks and its frames the SUM of what every rank timed (dry gloo rehearsal with
+    the lengths scaled down so that rank 1's KITTI-03 runs out)."""
+    import json
+    import subprocess
+    import sys
+    from multimot_track_amd import shard
+    assert [shard.workload("C4", r)["name"] for r in range(4)] == \
+        ["C4/KITTI-00", "C4/KITTI-03", "C4/KITTI-05", "C4/KITTI-07"]
+    assert (shard.workload("C4", 2)["width"], shard.workload("C4", 2)["height"]) == (1226, 370)
+    assert shard.workload("C5", 3)["nfeatures"] == 8000 and shard.workload("C5", 3)["parts"] == 4
+    assert shard.rank_steps(801, 128, 5, 20) == (5, 1)
+    assert shard.rank_steps(None, 128, 5, 20) == (5, 20)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry",
+                        "--config", "C4", "--steps", "3", "--warmup", "1", "--chunk", "8",
+                        "--dry-length-scale", "0.02"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    ranks = d["config"]["ranks"]
+    assert [r[0]["name"] for r in ranks] == ["C4/KITTI-00", "C4/KITTI-03"]
+    assert d["config"]["seeds"] == [[1000], [1003]]
+    # KITTI-00 (90 frames after scaling): 1 warm-up + 3 timed chunks; KITTI-03 (16): 1 + 1
+    assert [r[0]["timed_steps"] for r in ranks] == [3, 1]
+    assert d["config"]["frames_all"] == (3 + 1) * 8
+    # MAX over ranks: rank 0's three 10 ms steps, not rank 1's single 20 ms step
+    assert d["ms_per_step"] * 3 >= 30.0
