@@ -39,7 +39,6 @@ struct BADesc {
 };
 
 size_t ba_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt);
-void launch_local_ba(const BADesc& d, hipStream_t st);
 
 // The graph as LocalBundleAdjustment builds it (Optimizer.cc:3408-3541): keyframe vertices (fixed
 // or not), points, and the edges listed point by point (e_pt non-decreasing), each point's

@@ -258,476 +258,14 @@ __device__ __forceinline__ void wave_sync_lds() {
 
 }  // namespace
 
-__global__ __launch_bounds__(kBAThreads) void k_local_ba(BADesc d) {
-  __shared__ double s_S[kLdsRows * kLdsRows];
-  __shared__ double s_vec[3 * kLdsRows];
-  __shared__ double s_part[2 * kBAWaves];
-  __shared__ int s_ok;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const BAWork w = carve(d);
-  const Cam cam{d.fx, d.fy, d.cx, d.cy, d.bf};
-  const int n6 = 6 * d.n_opt;
-  double* S = n6 <= kLdsRows ? s_S : w.S;
-  double* bs = n6 <= kLdsRows ? s_vec : w.vec;
-  double* Dg = bs + n6;
-  double* yv = Dg + n6;
-  const float dMonoF = sqrtf(5.991f), dStereoF = sqrtf(7.815f);
-  (void)dMonoF;
-  // thHuberMono = sqrt(5.991) stored as a float (Optimizer.cc:3457-3458)
-  const double dMono = (double)(float)sqrt(5.991), dStereo = (double)(float)sqrt(7.815);
-
-  // ---- vertices
-  for (int k = tid; k < d.n_kf; k += kBAThreads) w.pose[k] = dse3_from_float(d.Tcw + 16 * (size_t)k);
-  for (int q = tid; q < 3 * d.n_pt; q += kBAThreads) w.X[q] = (double)d.Xw[q];
-  for (int e = tid; e < d.n_edge; e += kBAThreads) {
-    w.level[e] = 0;
-    w.err[3 * (size_t)e] = w.err[3 * (size_t)e + 1] = w.err[3 * (size_t)e + 2] = 0;
-  }
-  __syncthreads();
-
-  for (int round = 0; round < 2; round++) {
-    const bool robust = round == 0;
-    const int iters = round == 0 ? 5 : 10;
-    // the solver's x starts at zero in each round (a failed first solve re-applies it)
-    for (int q = tid; q < n6 + 3 * d.n_pt; q += kBAThreads) w.x[q] = 0;
-    if (round == 1) {
-      // check inlier observations (Optimizer.cc:3559-3590): the last computed error, the current
-      // depth; every kernel dropped
-      for (int e = tid; e < d.n_edge; e += kBAThreads) {
-        const bool st = !(d.e_obs[3 * (size_t)e + 2] < 0);
-        const double chi = edge_chi2(&w.err[3 * (size_t)e], (double)d.e_s[e], st);
-        double pc[3];
-        se3_map(w.pose[d.e_kf[e]], &w.X[3 * (size_t)d.e_pt[e]], pc);
-        if (chi > (st ? 7.815 : 5.991) || !(pc[2] > 0.0)) w.level[e] = 1;
-      }
-      __syncthreads();
-    }
-    // the round's active graph: vertices with a level-0 edge (initializeOptimization(level))
-    for (int k = tid; k < d.n_kf; k += kBAThreads) w.kf_act[k] = 0;
-    __syncthreads();
-    int nact = 0;
-    for (int j = tid; j < d.n_pt; j += kBAThreads) {
-      uint8_t a = 0;
-      for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++)
-        if (w.level[e] == 0) {
-          a = 1;
-          w.kf_act[d.e_kf[e]] = 1;  // benign race: every writer stores 1
-        }
-      w.pt_act[j] = a;
-      nact += a;
-    }
-    nact = (int)wg_sum1((double)nact, s_part);  // also orders the kf_act stores
-    int it_done = 0, trials = 0;
-    if (nact > 0) {
-      double lambda = 0, ni = 2, chk = 0;
-      int nBad = 0;
-      // The errors and chi2 of the current estimate are those of the last trial when it was
-      // accepted: T5 computed them at that very state, in the same loop and reduction order as
-      // the pass below, so the pass is skipped then (bit-identical).
-      bool fresh = false;
-      double currentChi = 0;
-      for (int iter = 0; iter < iters; iter++) {
-        // ---- computeActiveErrors + activeRobustChi2
-        if (!fresh) {
-          double part = 0;
-          for (int e = tid; e < d.n_edge; e += kBAThreads) {
-            if (w.level[e]) continue;
-            const bool st = !(d.e_obs[3 * (size_t)e + 2] < 0);
-            const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], st,
-                                        w.pose[d.e_kf[e]], &w.X[3 * (size_t)d.e_pt[e]], cam,
-                                        &w.err[3 * (size_t)e]);
-            double r0 = c, r1;
-            if (robust) huber_rho(c, st ? dStereo : dMono, r0, r1);
-            part += r0;
-          }
-          currentChi = wg_sum1(part, s_part);
-        }
-        const double iniChi = currentChi;
-        // ---- buildSystem, point pass: H_ll, b_l per point; H_pl per edge
-        for (int j = tid; j < d.n_pt; j += kBAThreads) {
-          double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b3[3] = {0, 0, 0};
-          const double* X = &w.X[3 * (size_t)j];
-          for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
-            if (w.level[e]) continue;
-            const int k = d.e_kf[e];
-            const bool st = !(d.e_obs[3 * (size_t)e + 2] < 0);
-            const double s = (double)d.e_s[e];
-            const double* er = &w.err[3 * (size_t)e];
-            double Jp[3][6], Jl[3][3];
-            edge_jac<true>(st, w.pose[k], X, cam, Jp, Jl);
-            const int rows = st ? 3 : 2;
-            double r1 = 1.0;
-            if (robust) {
-              double r0;
-              huber_rho(edge_chi2(er, s, st), st ? dStereo : dMono, r0, r1);
-            }
-            const double wt = r1 * s;
-            double om[3];
-            for (int r = 0; r < 3; r++) om[r] = r < rows ? -(s * er[r]) * r1 : 0.0;
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-#pragma unroll
-              for (int b = 0; b < 3; b++) {
-                double acc = 0;
-                for (int r = 0; r < rows; r++) acc += Jl[r][a] * wt * Jl[r][b];
-                hl[3 * a + b] += acc;
-              }
-              double g = 0;
-              for (int r = 0; r < rows; r++) g += Jl[r][a] * om[r];
-              b3[a] += g;
-            }
-            if (d.opt_of[k] >= 0) {
-              double* hpl = &w.Hpl[18 * (size_t)e];
-#pragma unroll
-              for (int a = 0; a < 6; a++)
-#pragma unroll
-                for (int b = 0; b < 3; b++) {
-                  double acc = 0;
-                  for (int r = 0; r < rows; r++) acc += Jp[r][a] * wt * Jl[r][b];
-                  hpl[3 * a + b] = acc;
-                }
-            }
-          }
-#pragma unroll
-          for (int q = 0; q < 9; q++) w.Hll[9 * (size_t)j + q] = hl[q];
-#pragma unroll
-          for (int q = 0; q < 3; q++) w.bl[3 * (size_t)j + q] = b3[q];
-        }
-        // ---- buildSystem, keyframe pass: one wave per optimised keyframe
-        for (int a = wave; a < d.n_opt; a += kBAWaves) {
-          double acc[27];
-#pragma unroll
-          for (int q = 0; q < 27; q++) acc[q] = 0;
-          for (int t = d.kf_start[a] + lane; t < d.kf_start[a + 1]; t += 64) {
-            const int e = d.kf_edges[t];
-            if (w.level[e]) continue;
-            const bool st = !(d.e_obs[3 * (size_t)e + 2] < 0);
-            const double s = (double)d.e_s[e];
-            const double* er = &w.err[3 * (size_t)e];
-            double Jp[3][6], Jl[3][3];
-            edge_jac<false>(st, w.pose[d.e_kf[e]], &w.X[3 * (size_t)d.e_pt[e]], cam, Jp, Jl);
-            const int rows = st ? 3 : 2;
-            double r1 = 1.0;
-            if (robust) {
-              double r0;
-              huber_rho(edge_chi2(er, s, st), st ? dStereo : dMono, r0, r1);
-            }
-            const double wt = r1 * s;
-            int q = 0;
-#pragma unroll
-            for (int r0 = 0; r0 < 6; r0++)
-#pragma unroll
-              for (int c0 = r0; c0 < 6; c0++) {
-                double v = 0;
-                for (int r = 0; r < rows; r++) v += Jp[r][r0] * wt * Jp[r][c0];
-                acc[q++] += v;
-              }
-#pragma unroll
-            for (int r0 = 0; r0 < 6; r0++) {
-              double g = 0;
-              for (int r = 0; r < rows; r++) g += Jp[r][r0] * (-(s * er[r]) * r1);
-              acc[21 + r0] += g;
-            }
-          }
-          double mine = 0;
-#pragma unroll
-          for (int q = 0; q < 27; q++) {
-            const double v = wave_sum_dpp(acc[q]);
-            if (lane == q) mine = v;
-          }
-          if (lane < 21) {
-            int r0 = 0, q = lane;
-            while (q >= 6 - r0) {
-              q -= 6 - r0;
-              r0++;
-            }
-            const int c0 = r0 + q;
-            w.Hpp[36 * (size_t)a + 6 * r0 + c0] = mine;
-            w.Hpp[36 * (size_t)a + 6 * c0 + r0] = mine;
-          } else if (lane < 27) {
-            w.bp[6 * (size_t)a + lane - 21] = mine;
-          }
-        }
-        __syncthreads();
-        if (iter == 0) {  // computeLambdaInit over the round's vertices
-          double m = 0;
-          for (int a = tid; a < d.n_opt; a += kBAThreads)
-            if (w.kf_act[d.opt_kf[a]])
-              for (int r = 0; r < 6; r++) m = fmax(m, fabs(w.Hpp[36 * (size_t)a + 7 * r]));
-          for (int j = tid; j < d.n_pt; j += kBAThreads)
-            if (w.pt_act[j])
-              for (int r = 0; r < 3; r++) m = fmax(m, fabs(w.Hll[9 * (size_t)j + 4 * r]));
-          lambda = 1e-5 * wg_max1(m, s_part);
-          ni = 2;
-          nBad = 0;
-        }
-        double rho = 0, lastTrialChi = 0;
-        int qmax = 0;
-        do {
-          // ---- T1: backups, D^-1 per point, Y = H_pl D^-1 and H_pl D^-1 b_l per edge, S cleared
-          for (int k = tid; k < d.n_kf; k += kBAThreads) w.pose_b[k] = w.pose[k];
-          for (int q = tid; q < n6 * n6; q += kBAThreads) S[q] = 0;
-          for (int j = tid; j < d.n_pt; j += kBAThreads) {
-            double Dm[9], Di[9];
-#pragma unroll
-            for (int q = 0; q < 9; q++) Dm[q] = w.Hll[9 * (size_t)j + q] + ((q % 4) == 0 ? lambda : 0.0);
-            inverse3(Dm, Di);
-#pragma unroll
-            for (int q = 0; q < 9; q++) w.Dinv[9 * (size_t)j + q] = Di[q];
-#pragma unroll
-            for (int q = 0; q < 3; q++) w.Xb[3 * (size_t)j + q] = w.X[3 * (size_t)j + q];
-            const double* b3 = &w.bl[3 * (size_t)j];
-            double db[3];
-#pragma unroll
-            for (int a = 0; a < 3; a++) db[a] = Di[3 * a] * b3[0] + Di[3 * a + 1] * b3[1] + Di[3 * a + 2] * b3[2];
-            for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
-              if (w.level[e] || d.opt_of[d.e_kf[e]] < 0) continue;
-              const double* B = &w.Hpl[18 * (size_t)e];
-              double* Ye = &w.Y[18 * (size_t)e];
-              double* ce = &w.cv[6 * (size_t)e];
-#pragma unroll
-              for (int r = 0; r < 6; r++) {
-#pragma unroll
-                for (int c = 0; c < 3; c++)
-                  Ye[3 * r + c] = B[3 * r] * Di[c] + B[3 * r + 1] * Di[3 + c] + B[3 * r + 2] * Di[6 + c];
-                ce[r] = B[3 * r] * db[0] + B[3 * r + 1] * db[1] + B[3 * r + 2] * db[2];
-              }
-            }
-          }
-          __syncthreads();
-          // ---- T2: the reduced camera system, one wave per keyframe-pair block
-          for (int bk = wave; bk < d.n_blk; bk += kBAWaves) {
-            const int a = d.blk_ab[2 * bk], b = d.blk_ab[2 * bk + 1];
-            double acc[36];
-#pragma unroll
-            for (int q = 0; q < 36; q++) acc[q] = 0;
-            for (int t = d.blk_start[bk] + lane; t < d.blk_start[bk + 1]; t += 64) {
-              const int2 tr = d.trip[t];
-              if (w.level[tr.x] || w.level[tr.y]) continue;
-              const double* Ye = &w.Y[18 * (size_t)tr.x];
-              const double* B2 = &w.Hpl[18 * (size_t)tr.y];
-              double h2[18];
-#pragma unroll
-              for (int q = 0; q < 18; q++) h2[q] = B2[q];
-#pragma unroll
-              for (int r = 0; r < 6; r++) {
-                const double y0 = Ye[3 * r], y1 = Ye[3 * r + 1], y2 = Ye[3 * r + 2];
-#pragma unroll
-                for (int c = 0; c < 6; c++)
-                  acc[6 * r + c] += y0 * h2[3 * c] + y1 * h2[3 * c + 1] + y2 * h2[3 * c + 2];
-              }
-            }
-            double mine = 0;
-#pragma unroll
-            for (int q = 0; q < 36; q++) {
-              const double v = wave_sum_dpp(acc[q]);
-              if (lane == q) mine = v;
-            }
-            if (lane < 36) {
-              const int r = lane / 6, c = lane % 6;
-              double base = 0;
-              if (a == b) base = w.Hpp[36 * (size_t)a + lane] + (r == c ? lambda : 0.0);
-              S[(size_t)(6 * a + r) * n6 + 6 * b + c] = base - mine;
-            }
-            if (a == b) {  // b_schur = b_p - sum of H_pl D^-1 b_l over the keyframe's edges
-              double cs[6] = {0, 0, 0, 0, 0, 0};
-              for (int t = d.kf_start[a] + lane; t < d.kf_start[a + 1]; t += 64) {
-                const int e = d.kf_edges[t];
-                if (w.level[e]) continue;
-#pragma unroll
-                for (int r = 0; r < 6; r++) cs[r] += w.cv[6 * (size_t)e + r];
-              }
-              double mc = 0;
-#pragma unroll
-              for (int r = 0; r < 6; r++) {
-                const double v = wave_sum_dpp(cs[r]);
-                if (lane == r) mc = v;
-              }
-              if (lane < 6) bs[6 * a + lane] = w.bp[6 * (size_t)a + lane] - mc;
-            }
-          }
-          __syncthreads();
-          // ---- T3: LDL^T (left-looking, the checker's operation order) and the substitutions
-          if (tid == 0) s_ok = 1;
-          __syncthreads();
-          if (n6 <= 64) {
-            if (wave == 0) {
-              bool ok = true;
-              for (int k = 0; k < n6 && ok; k++) {
-                double dk = S[(size_t)k * n6 + k];
-                for (int c = 0; c < k; c++) dk -= S[(size_t)k * n6 + c] * S[(size_t)k * n6 + c] * Dg[c];
-                if (dk == 0) {
-                  ok = false;
-                  break;
-                }
-                if (lane == 0) Dg[k] = dk;
-                const int i = lane;
-                if (i > k && i < n6) {
-                  double s = S[(size_t)k * n6 + i];
-                  for (int c = 0; c < k; c++) s -= S[(size_t)i * n6 + c] * S[(size_t)k * n6 + c] * Dg[c];
-                  S[(size_t)i * n6 + k] = s / dk;
-                }
-                wave_sync_lds();
-              }
-              if (!ok && lane == 0) s_ok = 0;
-            }
-          } else {
-            for (int k = 0; k < n6; k++) {
-              double dk = S[(size_t)k * n6 + k];
-              for (int c = 0; c < k; c++) dk -= S[(size_t)k * n6 + c] * S[(size_t)k * n6 + c] * Dg[c];
-              if (dk == 0) {  // uniform: every thread reads the same values
-                if (tid == 0) s_ok = 0;
-                break;
-              }
-              if (tid == 0) Dg[k] = dk;
-              for (int i = k + 1 + tid; i < n6; i += kBAThreads) {
-                double s = S[(size_t)k * n6 + i];
-                for (int c = 0; c < k; c++) s -= S[(size_t)i * n6 + c] * S[(size_t)k * n6 + c] * Dg[c];
-                S[(size_t)i * n6 + k] = s / dk;
-              }
-              __syncthreads();
-            }
-          }
-          __syncthreads();
-          const bool ok2 = s_ok != 0;
-          if (ok2 && tid == 0) {
-            for (int i = 0; i < n6; i++) yv[i] = bs[i];
-            for (int i = 0; i < n6; i++)
-              for (int c = 0; c < i; c++) yv[i] -= S[(size_t)i * n6 + c] * yv[c];
-            for (int i = 0; i < n6; i++) yv[i] /= Dg[i];
-            for (int i = n6 - 1; i >= 0; i--)
-              for (int r = i + 1; r < n6; r++) yv[i] -= S[(size_t)r * n6 + i] * yv[r];
-            for (int i = 0; i < n6; i++) w.x[i] = yv[i];
-          }
-          __syncthreads();
-          // ---- T4: point increments (x_l = D^-1 (b_l - H_pl^T x_p)), update (stale x on failure)
-          for (int j = tid; j < d.n_pt; j += kBAThreads) {
-            if (!w.pt_act[j]) continue;
-            double* xl = &w.x[n6 + 3 * (size_t)j];
-            if (ok2) {
-              double cl[3] = {w.bl[3 * (size_t)j], w.bl[3 * (size_t)j + 1], w.bl[3 * (size_t)j + 2]};
-              for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
-                const int a = d.opt_of[d.e_kf[e]];
-                if (w.level[e] || a < 0) continue;
-                const double* B = &w.Hpl[18 * (size_t)e];
-#pragma unroll
-                for (int c = 0; c < 3; c++)
-#pragma unroll
-                  for (int r = 0; r < 6; r++) cl[c] += B[3 * r + c] * (-w.x[6 * a + r]);
-              }
-              const double* Di = &w.Dinv[9 * (size_t)j];
-#pragma unroll
-              for (int a = 0; a < 3; a++) xl[a] = Di[3 * a] * cl[0] + Di[3 * a + 1] * cl[1] + Di[3 * a + 2] * cl[2];
-            }
-#pragma unroll
-            for (int a = 0; a < 3; a++) w.X[3 * (size_t)j + a] += xl[a];
-          }
-          for (int a = tid; a < d.n_opt; a += kBAThreads) {
-            const int k = d.opt_kf[a];
-            if (!w.kf_act[k]) continue;
-            double u[6];
-#pragma unroll
-            for (int r = 0; r < 6; r++) u[r] = w.x[6 * a + r];
-            w.pose[k] = dse3_mul(dse3_exp(u), w.pose[k]);
-          }
-          __syncthreads();
-          // ---- T5: errors, chi2 and the scale term
-          double pc2 = 0, psc = 0;
-          for (int e = tid; e < d.n_edge; e += kBAThreads) {
-            if (w.level[e]) continue;
-            const bool st = !(d.e_obs[3 * (size_t)e + 2] < 0);
-            const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], st,
-                                        w.pose[d.e_kf[e]], &w.X[3 * (size_t)d.e_pt[e]], cam,
-                                        &w.err[3 * (size_t)e]);
-            double r0 = c, r1;
-            if (robust) huber_rho(c, st ? dStereo : dMono, r0, r1);
-            pc2 += r0;
-          }
-          for (int a = tid; a < d.n_opt; a += kBAThreads) {
-            if (!w.kf_act[d.opt_kf[a]]) continue;
-            for (int r = 0; r < 6; r++) {
-              const double xv = w.x[6 * a + r];
-              psc += xv * (lambda * xv + w.bp[6 * (size_t)a + r]);
-            }
-          }
-          for (int j = tid; j < d.n_pt; j += kBAThreads) {
-            if (!w.pt_act[j]) continue;
-            for (int r = 0; r < 3; r++) {
-              const double xv = w.x[n6 + 3 * (size_t)j + r];
-              psc += xv * (lambda * xv + w.bl[3 * (size_t)j + r]);
-            }
-          }
-          double tempChi, scale;
-          block_sum2(pc2, psc, s_part, kBAWaves, tempChi, scale);
-          __syncthreads();
-          lastTrialChi = tempChi;
-          if (!ok2) tempChi = DBL_MAX;
-          rho = currentChi - tempChi;
-          scale += 1e-3;
-          rho /= scale;
-          fresh = rho > 0 && isfinite(tempChi);
-          if (fresh) {
-            double alpha = 1. - pow((2 * rho - 1), 3);
-            alpha = fmin(alpha, 2. / 3.);
-            lambda *= fmax(1. / 3., alpha);
-            ni = 2;
-            currentChi = tempChi;
-          } else {
-            lambda *= ni;
-            ni *= 2;
-            for (int k = tid; k < d.n_kf; k += kBAThreads) w.pose[k] = w.pose_b[k];
-            for (int q = tid; q < 3 * d.n_pt; q += kBAThreads) w.X[q] = w.Xb[q];
-            __syncthreads();
-          }
-          qmax++;
-          trials++;
-        } while (rho < 0 && qmax < 10);
-        bool ok = true;
-        if (qmax == 10 || rho == 0) ok = false;
-        if (ok) {
-          if ((iniChi - currentChi) * 1e3 < iniChi)
-            nBad++;
-          else
-            nBad = 0;
-          if (nBad >= 3) ok = false;
-        }
-        if (chk < lastTrialChi && iter > 0) ok = false;
-        chk = lastTrialChi;
-        it_done = iter + 1;
-        if (!ok) break;
-      }
-    }
-    if (tid == 0) {
-      d.stats[round] = it_done;
-      d.stats[2 + round] = trials;
-    }
-    __syncthreads();
-  }
-  // ---- the erase test (Optimizer.cc:3603-3631) and the recovered estimates
-  int nerase = 0;
-  for (int e = tid; e < d.n_edge; e += kBAThreads) {
-    const bool st = !(d.e_obs[3 * (size_t)e + 2] < 0);
-    const double chi = edge_chi2(&w.err[3 * (size_t)e], (double)d.e_s[e], st);
-    double pc[3];
-    se3_map(w.pose[d.e_kf[e]], &w.X[3 * (size_t)d.e_pt[e]], pc);
-    const bool er = chi > (st ? 7.815 : 5.991) || !(pc[2] > 0.0);
-    d.erase[e] = er ? 1 : 0;
-    nerase += er;
-  }
-  for (int k = tid; k < d.n_kf; k += kBAThreads) dse3_to_float(w.pose[k], d.T_out + 16 * (size_t)k);
-  for (int q = tid; q < 3 * d.n_pt; q += kBAThreads) d.X_out[q] = (float)w.X[q];
-  nerase = (int)wg_sum1((double)nerase, s_part);
-  if (tid == 0) d.stats[4] = nerase;
-}
-
 namespace {
-// ================================================================== multi-kernel solve (default)
-// The same LM as k_local_ba spread over the chip: one LM trial is a chain of short kernels on the
+// ================================================================== multi-kernel solve
+// The local BA's LM spread over the chip: one LM trial is a chain of short kernels on the
 // caller's stream (points, keyframe-pair blocks and keyframes in parallel; the reduced camera
 // system and the LM decision in one workgroup each), with the LM state in device memory.  The host
 // enqueues trials in batches and reads the state's done flag after each batch; every kernel of a
-// finished solve returns at once.  k_local_ba ran the whole solve on one CU (10-11 ms per local
-// BA of the C3 sequence); spread, a trial costs a few microseconds per kernel.
+// finished solve returns at once.  Round 4's first version ran the whole solve in one workgroup
+// (10-11 ms per local BA of the C3 sequence); spread, a trial costs a few microseconds per kernel.
 //   per iteration (need_lin):  k_ba2_lin   one thread per point: errors, robust chi2, H_ll, b_l,
 //                                          H_pl and the edge's pose terms (J_p^T w J_p, J_p^T w e)
 //                              k_ba2_kfsum one workgroup per optimised keyframe: H_pp, b_p
@@ -1718,10 +1256,6 @@ size_t ba2_workspace_bytes(int n_kf, int n_pt, int n_edge, int n_opt, int n_blk,
          a((size_t)n_edge) + a(4 * (size_t)n_edge) + a((size_t)n_kf) + a((size_t)n_pt) + a(16) + 64;
 }
 
-void launch_local_ba(const BADesc& d, hipStream_t st) {
-  hipLaunchKernelGGL(k_local_ba, dim3(1), dim3(kBAThreads), 0, st, d);
-  MMT_HIP(hipGetLastError());
-}
 
 // ------------------------------------------------------------------ host side
 static size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -1895,13 +1429,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
   d.X_out = (float*)(d_dn_ + o_X);
   d.erase = d_dn_ + o_er;
   d.stats = (int*)(d_dn_ + o_st);
-  static const bool onewg = [] {  // MMT_BA_ONEWG=1: the one-workgroup kernel (A/B and fallback)
-    const char* e = getenv("MMT_BA_ONEWG");
-    return e && atoi(e) != 0;
-  }();
-  if (onewg) {
-    launch_local_ba(d, st);
-  } else {
+  {
     const int gP = std::max(1, (nP + kMkThreads - 1) / kMkThreads);
     const int n6 = 6 * nO, nblk = nblocks;
     const size_t wsb2 = ba2_workspace_bytes(nK, nP, nE, nO, nblk, gP) +
@@ -1955,11 +1483,8 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.kf_act = take((size_t)nK);
     w.pt_act = take((size_t)nP);
     w.gP = gP;
-    static const int spec = [] {
-      const char* e = getenv("MMT_BA_SPEC");
-      return e && atoi(e) != 0 ? 1 : 0;
-    }();
-    w.spec = spec;
+    w.spec = 0;  // k_ba2_lin linearises every trial (the trial kernel's own linearisation,
+                 // k_ba2_p4<true>, measured 1,509 against 1,549 us per BA but spills)
     const double tp1 = hp.on ? ba_now_us() : 0;
     double t_launch = 0, t_wait = 0;
     hipLaunchKernelGGL(k_ba2_init, dim3(gP), dim3(kMkThreads), 0, st, d, w);
@@ -1980,10 +1505,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
         if (w.n_bitem + w.n_kitem > 0)
           hipLaunchKernelGGL(k_ba2_p2, dim3(w.n_bitem + w.n_kitem), dim3(kMkThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p3, dim3(1), dim3(kMkSolveThreads), 0, st, d, w);
-        if (w.spec)
-          hipLaunchKernelGGL(k_ba2_p4<true>, dim3(gP), dim3(kMkThreads), 0, st, d, w);
-        else
-          hipLaunchKernelGGL(k_ba2_p4<false>, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p4<false>, dim3(gP), dim3(kMkThreads), 0, st, d, w);
       }
       MMT_HIP(hipGetLastError());
       slots += batch;

@@ -140,14 +140,8 @@ mmt_ctx* mmt_create(const mmt_config* cfg) {
     MMT_HIP(hipGetDeviceCount(&ndev));
     if (cfg->device_id < 0 || cfg->device_id >= ndev) throw ArgError("bad device_id");
     MMT_HIP(hipSetDevice(cfg->device_id));
-    {
-      // MMT_EGO_PRIO=1: the context stream (ORB window, ego chain) at high priority (A/B knob)
-      const char* ep = getenv("MMT_EGO_PRIO");
-      int lo = 0, hi = 0;
-      MMT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      MMT_HIP(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking,
-                                          ep && atoi(ep) == 1 ? hi : 0));
-    }
+    // the context stream (ORB window, ego chain) at normal priority (high measured within noise)
+    MMT_HIP(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, 0));
     ctx->orb.init(cfg->orb_nfeatures, cfg->orb_scale_factor, cfg->orb_nlevels,
                   cfg->orb_ini_th_fast, cfg->orb_min_th_fast);
     ctx->engine.setup(cfg->width, cfg->height, ctx->orb, cfg->max_batch > 0 ? cfg->max_batch : 1);

@@ -123,12 +123,6 @@ class OrbEngine {
   // (GPU_MAX_HW_QUEUES), and streams beyond them end up sharing the caller's queue.
   hipStream_t side_ = nullptr;
   hipEvent_t ev_pyr_ = nullptr, ev_blur_ = nullptr, ev_gray_ = nullptr;
-  // the batch split into parts with launch sequences of their own (MMT_ORB_PARTS, default 1: measured slower at 2 and 4, the window is throughput-bound):
-  // one part's latency-bound launches (resize chain, octree) overlap another's FAST / blur
-  static constexpr int kMaxParts = 4;
-  int parts_ = 1;
-  hipStream_t pstream_[kMaxParts][2] = {};
-  hipEvent_t pev_[kMaxParts][4] = {};  // gray, pyramid, blur, part done
   void run_part(int f0, int nf, hipStream_t st_main, hipStream_t st_side, hipEvent_t* ev,
                 mmt_kp* d_kps, uint8_t* d_desc, int cap_per_frame, int* d_n);
   int iniTh_ = 20, minTh_ = 7;
@@ -137,24 +131,22 @@ class OrbEngine {
   std::vector<CellInfo> cells_;
   std::vector<int> xtab_off_, ytab_off_;
   std::vector<int> rs_pitch_, rs_lds_;  // k_resize LDS row pitch and bytes per level
-  // k_pyramid (MMT_PYR=0: the k_resize chain): bands per frame (0: the chain, e.g. when a band's
-  // rows do not fit the LDS), the band table and the launch constants
+  // k_pyramid: bands per frame (0: the k_resize chain, e.g. when a band's rows do not fit the
+  // LDS), the band table and the launch constants
   int pyr_bands_ = 0, pyr_lds_ = 0;
-  // batches up to this many frames take k_pyramid (MMT_PYR_MAX_FRAMES); window against the chain
+  // batches up to this many frames take k_pyramid; window against the chain
   // (round 5): batch 1 0.124 / 0.140 ms, 4 0.136 / 0.154, 16 0.202 / 0.218, 32 0.297 / 0.300,
   // 64 0.544 / 0.503, 128 1.029 / 0.919
-  int pyr_max_frames_ = 32;
-  // XCD-contiguous workgroup order (MMT_ORB_XCD bits): 1 k_resize, 2 k_blur.  Blur only by
-  // default: its FETCH 131 -> 105 MB per 128-frame window at the same time; the resize chain
+  static constexpr int pyr_max_frames_ = 32;
+  // XCD-contiguous workgroup order (bits: 1 k_resize, 2 k_blur).  Blur only: its FETCH 131 -> 105 MB per 128-frame window at the same time; the resize chain
   // fetches 101 -> 89 MB but runs 10 us slower (window 0.932 against 0.922 ms, round 5)
-  int xcd_order_ = 2;
+  static constexpr int xcd_order_ = 2;
   PyrBand* d_pyr_bands_ = nullptr;
   PyrArgs pyr_args_{};
   int sched_ = 0;  // MMT_ORB_SCHED=2: one stream (standalone kernel times for profiling)
-  // FAST cells per wave (MMT_FAST_CPW, default 1): with more, each wave's next tile loads are in
-  // flight during its current cell; measured 0.918 / 0.928 / 0.940 / 0.951 ms per 128-frame window
-  // at 1 / 2 / 4 / 8 (round 5), so one cell per wave stays the default
-  int fast_cpw_ = 1;
+  // FAST cells per wave: with more, each wave's next tile loads are in flight during its current
+  // cell; measured 0.918 / 0.928 / 0.940 / 0.951 ms per 128-frame window at 1 / 2 / 4 / 8 (round 5)
+  static constexpr int fast_cpw_ = 1;
   LevelInfo* d_lv_ = nullptr;
   CellInfo* d_cells_ = nullptr;
   ResizeX* d_xtab_ = nullptr;

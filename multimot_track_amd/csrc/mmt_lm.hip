@@ -1243,21 +1243,12 @@ void launch_flow_lm(const FlowSolveDesc* d_descs, int nsolves, int n_hint, hipSt
   // items each (more register items spill: the 6x6 solve and the sums need the room); items
   // beyond go through the global item arrays.  Each workgroup picks its own item count
   // (k_flow_lm); n_hint (the largest edge count) only sizes the block.
-  static const int force = [] {  // MMT_LM_THREADS=<threads>: tuning knob for tools/
-    const char* e = getenv("MMT_LM_THREADS");
-    return e ? atoi(e) : 0;
-  }();
-  int threads = std::min(256, std::max(64, (n_hint + 63) / 64 * 64));
-  if (force) threads = force;
-  // MMT_LM_MAX_CAND=1..4 (read per launch; tests compare 1 against the default 4 bit for bit)
+  const int threads = std::min(256, std::max(64, (n_hint + 63) / 64 * 64));
+  // MMT_LM_MAX_CAND=1..4 (read per launch; tests compare 1 against the default 4 bit for bit);
+  // bit 256: the accepted trial's sums reduced in registers; bit 512: the fused trial pass
   int max_cand = 4;
   if (const char* e = getenv("MMT_LM_MAX_CAND")) max_cand = std::min(4, std::max(1, atoi(e)));
-  // MMT_LM_REGSUM=0: the accepted trial's sums through the LDS tile (A/B knob, read per launch)
-  const char* rs = getenv("MMT_LM_REGSUM");
-  if (!(rs && atoi(rs) == 0)) max_cand |= 256;
-  // MMT_LM_SPEC1=0: two passes and two reductions per trial instead of the fused pass (A/B knob)
-  const char* s1 = getenv("MMT_LM_SPEC1");
-  if (!(s1 && atoi(s1) == 0)) max_cand |= 512;
+  max_cand |= 256 | 512;
   hipLaunchKernelGGL(k_flow_lm<2>, dim3(nsolves), dim3(threads), 0, st, d_descs, max_cand);
 }
 
@@ -1276,10 +1267,8 @@ void launch_flow_lm_split(const FlowSolveDesc* d_desc, int groups, hipStream_t s
   int max_cand = 4;
   if (const char* e = getenv("MMT_LM_MAX_CAND")) max_cand = std::min(4, std::max(1, atoi(e)));
   groups = std::max(1, std::min(groups, kFlowSplitMax));
-  const char* e = getenv("MMT_LM_SPEC");  // 0: two passes and two exchanges per trial
-  const int spec = !(e && atoi(e) == 0);
-  const char* rs = getenv("MMT_LM_REGSUM");  // 0: the fused pass's sums through the LDS tile
-  if (!(rs && atoi(rs) == 0)) max_cand |= 256;
+  const int spec = 1;  // one fused pass and one exchange per trial
+  max_cand |= 256;     // its sums reduced in registers
   hipLaunchKernelGGL(k_flow_lm_split, dim3(groups), dim3(256), 0, st, d_desc, max_cand, spec);
 }
 
@@ -1559,13 +1548,6 @@ constexpr int kPoThreads = 512, kPoNone = 8;
 
 constexpr int kPoStride = 29;  // odd row stride of the reduction tile (28 sums)
 
-struct PoSmemR {
-  double tile[(kPoThreads / 64) * 64 * kPoStride];
-  double part[2][(kPoThreads / 64) * 32];  // wave partials, double-buffered across passes
-  double Hw[kPoThreads / 64][2][32];        // every wave's own copy of the current / trial sums
-  double red[16 * 32];
-  double H[32];
-};
 
 // po_linearise for the register path: the edge's contribution goes straight into the thread's
 // row of the reduction tile (stored by its first edge, FIRST, accumulated by the others; an
@@ -1634,193 +1616,6 @@ __device__ __forceinline__ void po_linearise_row(const PoEdgeR& E, const DSE3& T
     row[22 + a] = FIRST ? -(r1 * g) : row[22 + a] - r1 * g;
   }
   }
-}
-
-template <int IT>
-__device__ void pose_opt_reg(const PoseOptDesc& D, int N, PoSmemR& sm) {
-  const int tid = threadIdx.x, nw = kPoThreads >> 6;
-  const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
-  PoEdgeR Ed[IT];
-  double er[IT][3];
-#pragma unroll
-  for (int q = 0; q < IT; q++) {
-    const int i = tid + q * kPoThreads;
-    if (i < N) {
-      Ed[q] = po_load(D, nullptr, i, (D.obs[3 * i + 2] < 0 ? 0 : kPoStereo) | kPoRobust);
-    } else {
-      Ed[q] = PoEdgeR{};
-      Ed[q].flags = kPoNone | kPoOutlier;
-    }
-    er[q][0] = er[q][1] = er[q][2] = 0;
-  }
-  DSE3 P;
-  int nBad = 0;
-  double* row = tile_row<kPoStride>(sm.tile);
-#ifdef MMT_PO_PROFILE
-  long long pp[4] = {0, 0, 0, 0}, pt = clock64();
-#define PO_T(k)                     \
-  do {                              \
-    const long long _n = clock64(); \
-    pp[k] += _n - pt;               \
-    pt = _n;                        \
-  } while (0)
-#else
-#define PO_T(k) \
-  do {          \
-  } while (0)
-#endif
-  int npass = 0, nrej = 0;
-  const int lane = tid & 63, wave = tid >> 6;
-  // one pass: linearise into the tile rows, column sums per wave, one barrier, and every wave adds
-  // the wave partials itself (same order everywhere, so every wave holds the same bits) into its
-  // own LDS copy of the sums, read after a wave-level fence
-  auto pass = [&](const DSE3& T, int buf) {
-    PO_T(0);
-    po_linearise_row<true>(Ed[0], T, D, dM, dS, er[0], row);
-#pragma unroll
-    for (int q = 1; q < IT; q++) po_linearise_row<false>(Ed[q], T, D, dM, dS, er[q], row);
-    PO_T(1);
-    const double* t = sm.tile + (size_t)wave * 64 * kPoStride;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double* part = sm.part[npass & 1];
-    if (lane < kPoSums) {
-      double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int r0 = 0; r0 < 64; r0 += 16) {
-        double x[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) x[j] = t[(r0 + j) * kPoStride + lane];
-#pragma unroll
-        for (int j = 0; j < 16; j++) acc[j & 7] += x[j];
-      }
-      part[wave * 32 + lane] =
-          ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-    }
-    __syncthreads();
-    if (lane < kPoSums) {
-      double sum = 0;
-#pragma unroll
-      for (int w = 0; w < nw; w++) sum += part[w * 32 + lane];
-      sm.Hw[wave][buf][lane] = sum;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    PO_T(2);
-    npass++;
-  };
-  for (int it = 0; it < 4; it++) {
-    P = dse3_from_float(D.Tcw);  // every round restarts from the input pose
-    int hs = 0;
-    pass(P, 0);
-    double cur = sm.Hw[wave][0][0], lam, ni = 2, chk = 0;
-    {
-      double md = 0;
-#pragma unroll
-      for (int a = 0; a < 6; a++) md = fmax(md, fabs(sm.Hw[wave][0][1 + a * (a + 3) / 2]));
-      lam = 1e-5 * md;
-    }
-    int nRaul = 0;
-    double xb[6] = {0, 0, 0, 0, 0, 0};
-    for (int iter = 0; iter < 10; iter++) {
-      const double ini = cur;
-      int qmax = 0;
-      bool bad = false;
-      for (;;) {
-        const double* Hc = sm.Hw[wave][hs];
-        double A[21], bs[6];
-#pragma unroll
-        for (int q = 0; q < 21; q++) A[q] = Hc[1 + q];
-#pragma unroll
-        for (int a = 0; a < 6; a++) {
-          A[a * (a + 3) / 2] += lam;
-          bs[a] = Hc[22 + a];
-        }
-        const bool ok2 = ldlt6_packed(A, bs);
-#pragma unroll
-        for (int a = 0; a < 6; a++) xb[a] = ok2 ? bs[a] : xb[a];
-        const DSE3 PN = exp_mul(xb, P);
-        pass(PN, hs ^ 1);
-        const double* Ht = sm.Hw[wave][hs ^ 1];
-        const double lastTrialChi = Ht[0];
-        const double tempChi = ok2 ? Ht[0] : DBL_MAX;
-        double scale = 0;
-#pragma unroll
-        for (int a = 0; a < 6; a++) scale += xb[a] * (lam * xb[a] + Hc[22 + a]);
-        scale += 1e-3;
-        const double rho = (cur - tempChi) / scale;
-        const bool accept = rho > 0 && isfinite(tempChi);
-        if (accept) {
-          const double t = 2 * rho - 1;
-          double alpha = 1. - t * t * t;
-          alpha = fmin(alpha, 2. / 3.);
-          lam = lam * fmax(1. / 3., alpha);
-          ni = 2;
-          cur = tempChi;
-          P = PN;
-          hs ^= 1;
-        } else {
-          lam = lam * ni;
-          ni = ni * 2;
-          nrej++;
-        }
-        qmax++;
-        const bool again = (rho < 0 && qmax < 10);
-        if (!again) {
-          bool ok = true;
-          if (qmax == 10 || rho == 0) ok = false;
-          if (ok) {
-            if ((ini - cur) * 1e3 < ini)
-              nRaul++;
-            else
-              nRaul = 0;
-            if (nRaul >= 3) ok = false;
-          }
-          if (chk < lastTrialChi && iter > 0) ok = false;
-          chk = lastTrialChi;
-          bad = !ok;
-          break;
-        }
-      }
-      if (bad) break;
-    }
-    // re-classification (Optimizer.cc:3266-3322), as pose_opt_body
-    double nb[1] = {0};
-#pragma unroll
-    for (int q = 0; q < IT; q++) {
-      if (Ed[q].flags & kPoNone) continue;
-      if (Ed[q].flags & kPoOutlier) {
-        double x, y, z;
-        po_err(Ed[q], P, D, er[q], x, y, z);
-      }
-      const double c = po_chi2(Ed[q], er[q]);
-      const float thr = (Ed[q].flags & kPoStereo) ? 7.815f : 5.991f;
-      int f = c > (double)thr ? (Ed[q].flags | kPoOutlier) : (Ed[q].flags & ~kPoOutlier);
-      nb[0] += (f & kPoOutlier) ? 1.0 : 0.0;
-      if (it == 2) f &= ~kPoRobust;
-      Ed[q].flags = f;
-    }
-    block_sum<1>(nb, sm.red, sm.H, nw);
-    nBad = (int)sm.H[0];
-    __syncthreads();  // sm.H is rewritten by the next round's count
-    if (N < 10) break;
-  }
-#pragma unroll
-  for (int q = 0; q < IT; q++) {
-    const int i = tid + q * kPoThreads;
-    if (i < N) D.outlier[i] = (Ed[q].flags & kPoOutlier) ? 1 : 0;
-  }
-  if (tid == 0) {
-    dse3_to_float(P, D.pose_out);
-    *D.n_inliers = N - nBad;
-#ifdef MMT_PO_PROFILE
-    printf("[po profile] N %d passes %d (rejected trials %d) cycles: solve+ctl %lld linearise "
-           "%lld reduce %lld\n", N, npass, nrej, pp[0], pp[1], pp[2]);
-#endif
-  }
-#undef PO_T
 }
 
 }  // namespace
@@ -2145,80 +1940,21 @@ __global__ __launch_bounds__(kPoThreads) void k_pose_opt_l(const PoseOptDesc* __
   pose_opt_light<IT>(D, N, sm);
 }
 
-template <int IT>
-__global__ __launch_bounds__(kPoThreads) void k_pose_opt_r(const PoseOptDesc* __restrict__ descs) {
-  __shared__ PoSmemR sm;
-  const PoseOptDesc& D = descs[blockIdx.x];
-  const int N = D.n;
-  if (pose_opt_trivial(D, N)) return;
-  if (N > IT * kPoThreads) {  // the host sized the launch for the largest solve
-    if (threadIdx.x == 0) *D.n_inliers = -1;
-    return;
-  }
-  pose_opt_reg<IT>(D, N, sm);
-}
-
 void launch_pose_opt(const PoseOptDesc* d_descs, int nsolves, int n_max, hipStream_t st) {
-  // MMT_PO_VARIANT: 2 (default) light trial passes + lambda candidates, the two-edge variant for
-  // every count up to 2 * kPoThreads (one launch fewer: the map chains' bound n_max is always
-  // above kPoThreads); 3 the same with the one-edge variant for counts up to kPoThreads; 1
-  // register kernel with a full pass per trial; 0 the LDS kernel for every size (A/B knobs).
-  // One kernel holding several variants spills (580 B per lane), so each is a launch of its own.
-  static const int variant = [] {
-    const char* e = getenv("MMT_PO_VARIANT");
-    return e ? atoi(e) : 2;
-  }();
-  // MMT_PO_WIDE_FIRST (default 1): the variants for the larger counts go first.  They normally
-  // return at once, but a workgroup of 512 threads and 132 KB of LDS that queues behind the
-  // object path's RANSAC grids waited for them to retire (the motion-model solve's no-op
-  // k_pose_opt_l<4> took 5-100 µs, median 64, after its k_pose_opt_l<2>); ahead of it, it is
-  // placed before those grids are launched
-  static const bool wide_first = [] {
-    const char* e = getenv("MMT_PO_WIDE_FIRST");
-    return !(e && atoi(e) == 0);
-  }();
-  if ((variant == 2 || variant == 3) && wide_first) {
-    if (n_max > 2 * kPoThreads)
-      hipLaunchKernelGGL(k_pose_opt_l<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
-                         2 * kPoThreads);
-    if (n_max > 4 * kPoThreads)
-      hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs, 4 * kPoThreads);
-    if (variant == 3) {
-      if (n_max > kPoThreads)
-        hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
-                           kPoThreads);
-      hipLaunchKernelGGL(k_pose_opt_l<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
-    } else {
-      hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
-    }
-  } else if (variant == 2 || variant == 3) {
-    // the edge count is known on the device only: every variant whose range meets [0, n_max]
-    // is launched and the ones outside the solve's count return at once (n_max is a bound)
-    if (variant == 3) {
-      hipLaunchKernelGGL(k_pose_opt_l<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
-      if (n_max > kPoThreads)
-        hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
-                           kPoThreads);
-    } else {
-      hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
-    }
-    if (n_max > 2 * kPoThreads)
-      hipLaunchKernelGGL(k_pose_opt_l<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
-                         2 * kPoThreads);
-    if (n_max > 4 * kPoThreads) {
-      // beyond the register variants: the LDS kernel, for the solves above 4 * kPoThreads only
-      hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs,
-                         4 * kPoThreads);
-    }
-  } else if (variant == 1 && n_max <= kPoThreads) {
-    hipLaunchKernelGGL(k_pose_opt_r<1>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
-  } else if (variant == 1 && n_max <= 2 * kPoThreads) {
-    hipLaunchKernelGGL(k_pose_opt_r<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
-  } else if (variant == 1 && n_max <= 4 * kPoThreads) {
-    hipLaunchKernelGGL(k_pose_opt_r<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs);
-  } else {
-    hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs, -1);
-  }
+  // The edge count is known on the device only: every variant whose range meets [0, n_max] is
+  // launched and the ones outside the solve's count return at once (n_max is a bound).  Light
+  // trial passes + lambda candidates, two edges per thread up to 2 * kPoThreads, four up to
+  // 4 * kPoThreads, the LDS kernel beyond.  One kernel holding several variants spills (580 B per
+  // lane), so each is a launch of its own.  The variants for the larger counts go first: a
+  // 512-thread workgroup with 132 KB of LDS that queued behind the object path's RANSAC grids
+  // waited for them to retire (the motion-model solve's no-op k_pose_opt_l<4> took 5-100 µs,
+  // median 64, after its k_pose_opt_l<2>); ahead of it, it is placed before those grids.
+  if (n_max > 2 * kPoThreads)
+    hipLaunchKernelGGL(k_pose_opt_l<4>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs,
+                       2 * kPoThreads);
+  if (n_max > 4 * kPoThreads)
+    hipLaunchKernelGGL(k_pose_opt, dim3(nsolves), dim3(256), 0, st, d_descs, 4 * kPoThreads);
+  hipLaunchKernelGGL(k_pose_opt_l<2>, dim3(nsolves), dim3(kPoThreads), 0, st, d_descs, -1);
   MMT_HIP(hipGetLastError());
 }
 

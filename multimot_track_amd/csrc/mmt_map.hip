@@ -151,15 +151,9 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
   d_esc_ = dev<double>(3 * (size_t)kcap);
   d_fsc_ = dev<int>(kcap);
   prof_on_ = getenv("MMT_MAP_PROFILE") != nullptr;
-  {
-    // LocalMapping's stream (A/B knob MMT_LM_PRIO: 1 high, 2 low, otherwise normal): its kernels
-    // (keyframe store copies, Fuse, the local BA) need nothing of the frame's flow solve
-    const char* e = getenv("MMT_LM_PRIO");
-    int lo = 0, hi = 0;
-    MMT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    const int v = e ? atoi(e) : 0;
-    MMT_HIP(hipStreamCreateWithPriority(&lm_s_, hipStreamNonBlocking, v == 1 ? hi : (v == 2 ? lo : 0)));
-  }
+  // LocalMapping's stream, normal priority (high / low measured within noise / slower): its
+  // kernels (keyframe store copies, Fuse, the local BA) need nothing of the frame's flow solve
+  MMT_HIP(hipStreamCreateWithPriority(&lm_s_, hipStreamNonBlocking, 0));
   // keyframe store record: keys, descriptors, mvuRight, grid (cell starts + key lists)
   kf_rec_bytes_ = align16(sizeof(mmt_kp) * (size_t)kcap) + 32 * (size_t)kcap +
                   align16(4 * (size_t)kcap) + align16(4 * (size_t)(kGridCells + 1)) +
@@ -495,12 +489,6 @@ void MapEngine::map_point_culling(int kf) {  // LocalMapping::MapPointCulling (R
 }
 
 // ------------------------------------------------------------------ GPU stages
-// MMT_MAP_EDGES_FUSED=0: D1's edge list by a k_map_edges launch of its own (A/B knob, read per
-// call); by default the matcher kernel builds it
-static bool edges_fused() {
-  const char* e = getenv("MMT_MAP_EDGES_FUSED");
-  return !(e && atoi(e) == 0);
-}
 // D1's descriptor for an edge list that k_map_edges builds on the device (it writes n): the edge
 // arrays at a fixed capacity of kcap edges
 void MapEngine::pose_desc_fill(uint8_t* h_blk, uint8_t* d_blk, const float* Tcw) {
@@ -598,13 +586,9 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
   e.nm = d_nm_;
   e.min_matches = min_matches;
   e.src_X = LD.Xw;
-  const bool fused = edges_fused();
-  launch_sbp_frame(G, Tcw, LD, th, 0, 1, c2_, d_match_, d_nm_, s_, nullptr, 0,
-                   fused ? &e : nullptr);
+  launch_sbp_frame(G, Tcw, LD, th, 0, 1, c2_, d_match_, d_nm_, s_, nullptr, 0, &e);
   if (retry_th > 0)
-    launch_sbp_frame(G, Tcw, LD, retry_th, 0, 1, c2_, d_match_, d_nm_, s_, d_nm_, retry_below,
-                     fused ? &e : nullptr);
-  if (!fused) launch_map_edges(e, s_);
+    launch_sbp_frame(G, Tcw, LD, retry_th, 0, 1, c2_, d_match_, d_nm_, s_, d_nm_, retry_below, &e);
   launch_pose_opt(d_pod_, 1, std::min(C.n, nact), s_);
   MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
   run_overlap();
@@ -1054,10 +1038,8 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
   e.ids = (const int*)(d_sel_ + sl.ids);
   e.has_base = d_sel_ + sl.bHas;
   e.base_X = (const float*)(d_sel_ + sl.bX);
-  const bool fused = edges_fused();
   launch_search_local(G, Tcw, d_pool_, d_pool_desc_, m, th, d_sel_ + sl.taken, nullptr, c3_,
-                      d_match_, d_nm_, s_, &sel, fused ? &e : nullptr);
-  if (!fused) launch_map_edges(e, s_);
+                      d_match_, d_nm_, s_, &sel, &e);
   launch_pose_opt(d_pod_, 1, std::min(C.n, nbase + m), s_);
   MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
   if (m > 0) MMT_HIP(hipMemcpyAsync(h_inview_, d_inview_, (size_t)m, hipMemcpyDeviceToHost, s_));

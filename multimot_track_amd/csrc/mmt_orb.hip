@@ -1805,16 +1805,6 @@ void OrbEngine::release() {
   }
   if (side_) (void)hipStreamDestroy(side_);
   side_ = nullptr;
-  for (int q = 0; q < kMaxParts; q++) {
-    for (int k = 0; k < 2; k++) {
-      if (pstream_[q][k]) (void)hipStreamDestroy(pstream_[q][k]);
-      pstream_[q][k] = nullptr;
-    }
-    for (int k = 0; k < 4; k++) {
-      if (pev_[q][k]) (void)hipEventDestroy(pev_[q][k]);
-      pev_[q][k] = nullptr;
-    }
-  }
 }
 
 template <typename T>
@@ -1960,10 +1950,9 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   }
   ncells_ = (int)cells_.size();
   ntiles_ = (int)tiles.size();
+  // MMT_ORB_SCHED=2 (profiling switch, tools/orb_sched.sh): every ORB launch on the caller's
+  // stream, so a kernel trace gives standalone kernel times
   if (const char* e = getenv("MMT_ORB_SCHED")) sched_ = atoi(e);
-  if (const char* e = getenv("MMT_FAST_CPW")) fast_cpw_ = std::max(1, std::min(64, atoi(e)));
-  if (const char* e = getenv("MMT_PYR_MAX_FRAMES")) pyr_max_frames_ = atoi(e);
-  if (const char* e = getenv("MMT_ORB_XCD")) xcd_order_ = atoi(e);
   total_slots_ = key_off;
   out_slots_ = out_off;
   cap_frame_ = out_off;
@@ -2005,7 +1994,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
     }
   int max_key_cap1 = 0;  // keys any level 1.. can hold at most (its FAST slot capacity)
   for (int l = 1; l < nlevels_; l++) max_key_cap1 = std::max(max_key_cap1, lv_[l].key_cap);
-  if (key_cap1_ < 256 || getenv("MMT_OCT_ONE_PER_CU")) {
+  if (key_cap1_ < 256) {
     key_cap1_ = key_cap_;  // the node arrays alone fill half the LDS: one workgroup per CU
     octree_lds1_ = octree_lds_;
     oct_two_per_cu_ = false;
@@ -2018,7 +2007,7 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   }
   // k_pyramid bands: the fewest (from 16) whose two level buffers fit 120 KB of LDS
   pyr_bands_ = 0;
-  if (nlevels_ <= kPyrMaxLevels && nlevels_ > 1 && !(getenv("MMT_PYR") && atoi(getenv("MMT_PYR")) == 0)) {
+  if (nlevels_ <= kPyrMaxLevels && nlevels_ > 1) {
     for (int nb = 16; nb <= 256 && pyr_bands_ == 0; nb *= 2) {
       std::vector<PyrBand> bands(nb);
       PyrArgs pa{};
@@ -2092,14 +2081,6 @@ void OrbEngine::setup(int w, int h, const OrbTables& t, int max_batch) {
   MMT_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&ev_pyr_, &ev_blur_, &ev_gray_})
     MMT_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  if (const char* e = getenv("MMT_ORB_PARTS")) parts_ = atoi(e);
-  parts_ = std::max(1, std::min(kMaxParts, parts_));
-  if (parts_ > 1)
-    for (int q = 0; q < parts_; q++) {
-      for (int k = 0; k < 2; k++)
-        MMT_HIP(hipStreamCreateWithFlags(&pstream_[q][k], hipStreamNonBlocking));
-      for (int k = 0; k < 4; k++) MMT_HIP(hipEventCreateWithFlags(&pev_[q][k], hipEventDisableTiming));
-    }
   MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));
 }
 
@@ -2112,24 +2093,9 @@ void OrbEngine::run(const uint8_t* d_gray, int nframes, size_t frame_pitch, mmt_
   if (d_gray != d_pyr_ || frame_pitch != pyr_stride_)
     MMT_HIP(hipMemcpy2DAsync(d_pyr_, pyr_stride_, d_gray, frame_pitch, lvl0, nframes,
                              hipMemcpyDeviceToDevice, stream));
-  // the batch in parts of at least 16 frames, each on a stream pair of its own once the gray
-  // frames are in; the caller's stream waits for every part
-  const int np = (sched_ & 2) ? 1 : std::max(1, std::min(parts_, nframes / 16));
-  if (np == 1) {
-    run_part(0, nframes, stream, side_, nullptr, d_kps, d_desc, cap_per_frame, d_n);
-    MMT_HIP(hipGetLastError());
-    return;
-  }
-  MMT_HIP(hipEventRecord(ev_gray_, stream));
-  int f0 = 0;
-  for (int q = 0; q < np; q++) {
-    const int nf = nframes / np + (q < nframes % np ? 1 : 0);
-    MMT_HIP(hipStreamWaitEvent(pstream_[q][0], ev_gray_, 0));
-    run_part(f0, nf, pstream_[q][0], pstream_[q][1], pev_[q], d_kps, d_desc, cap_per_frame, d_n);
-    MMT_HIP(hipEventRecord(pev_[q][3], pstream_[q][0]));
-    f0 += nf;
-  }
-  for (int q = 0; q < np; q++) MMT_HIP(hipStreamWaitEvent(stream, pev_[q][3], 0));
+  // the whole batch in one launch sequence (splitting it into parts on stream pairs of their own
+  // measured slower at 2 and 4 parts: the window is throughput-bound)
+  run_part(0, nframes, stream, side_, nullptr, d_kps, d_desc, cap_per_frame, d_n);
   MMT_HIP(hipGetLastError());
 }
 

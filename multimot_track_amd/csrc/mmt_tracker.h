@@ -2,12 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <condition_variable>
 #include <cstdint>
 #include <deque>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "mmt_internal.h"
@@ -121,7 +118,6 @@ class Tracker {
   struct ObjFrame {
     bool active = false;
     bool a_launched = false;  // obj_stage_a_launch ran
-    long seq = 0;  // job number (obj_submit)
     int cur = 0, last = 0, slot = 0, nobj = 0;
     FrameOut* out = nullptr;
     std::vector<int> labels, LabId, PreObjID, members;
@@ -159,23 +155,10 @@ class Tracker {
   void obj_stage_a(ObjFrame& F);    // grouping + B7/B8 + PnP-RANSAC launch (stream oa_)
   void obj_stage_a_launch(ObjFrame& F);  // its first half: the grouping kernel and its read-back
   void obj_stage_a_decide(ObjFrame& F);  // its second half: B7/B8 on the host, the RANSAC launch
-  void obj_advance_launch();        // obj_advance's first step (stage A's launch), on its own
   void obj_stage_b(ObjFrame& F);    // MM matrix, MM check, model choice, D3 (stream ob_, no wait)
   void obj_finish(ObjFrame& F);     // waits for the frame's D3, object motions, results
   void obj_advance();               // enqueue the queued frame's object path, finish old frames
   void obj_flush();
-  // The object worker (MMT_OBJ_THREAD, default on): the host side of the object path (stage A's
-  // wait for the grouping and its B7/B8 decisions, stage B's enqueue, the finish's wait for D3)
-  // runs on a thread of its own, beside the ego chain.  The main thread hands it each frame's
-  // job after ego_finish; before the ego path rewrites a frame slot it waits until every job
-  // that read the slot is finished on the host (slot_job_) and orders its stream behind the
-  // job's device work (ev_slot_).  The worker's first error is rethrown on the main thread.
-  void obj_worker_main();
-  void obj_submit(const ObjFrame& F);
-  void slot_wait(int s, hipStream_t st);
-  void obj_drain(bool discard);  // every handed job staged and finished (or dropped)
-  void obj_check();              // rethrows the worker's error
-  void obj_job(ObjFrame& F);     // stage A + B of one job, then its slot events
 
   mmt_config cfg_{};
   OrbEngine* engine_ = nullptr;
@@ -313,25 +296,8 @@ class Tracker {
   double hprof_us_[7] = {0, 0, 0, 0, 0, 0, 0};  // + map finish, stage A, stage B, obj finish
   long hprof_n_ = 0;
   hipEvent_t ev_orb_[2] = {nullptr, nullptr};
-  // the previous frame's object path inside the first map chain of the frame (MMT_OBJ_OVERLAP)
-  bool overlap_obj_ = true;
-  bool obj_split_ = false;  // MMT_OBJ_SPLIT
-  bool b3_host_ = true;    // MMT_B3_HOST
   bool obj_ran_ = false;
-  // object worker
-  bool ow_on_ = false;
   int device_ = 0;
-  std::thread ow_;
-  std::mutex om_;
-  std::condition_variable ocv_;   // work or requests for the worker
-  std::condition_variable odone_;  // worker progress for the main thread
-  std::deque<ObjFrame> oq_;       // handed jobs not yet staged (worker side: inflight_)
-  long o_handed_ = 0, o_finished_ = 0, o_need_fin_ = 0;
-  bool o_stop_ = false, o_discard_ = false;
-  int o_err_kind_ = 0;  // 1 DeviceError, 2 ArgError
-  std::string o_err_;
-  long slot_job_[kSlots] = {};  // (main thread) last job that reads each frame slot
-  hipEvent_t ev_slot_[kSlots][2] = {};
   double orb_ms_ = 0;
   long long orb_launches_ = 0, orb_frames_ = 0;
 };

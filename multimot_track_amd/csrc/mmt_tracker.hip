@@ -118,18 +118,6 @@ static T* dalloc(size_t n) {
 }
 
 Tracker::~Tracker() {
-  if (ow_.joinable()) {
-    obj_drain(true);
-    {
-      std::lock_guard<std::mutex> lk(om_);
-      o_stop_ = true;
-    }
-    ocv_.notify_all();
-    ow_.join();
-  }
-  for (auto& e : ev_slot_)
-    for (hipEvent_t& x : e)
-      if (x) (void)hipEventDestroy(x);
   if (hprof_ && hprof_n_ > 0)
     fprintf(stderr, "[mmt tracker profile] %ld frames, host wall us per frame: map finish + obj_advance %.1f, "
             "ego_launch %.1f, ego_finish %.1f\n", hprof_n_, hprof_us_[0] / hprof_n_,
@@ -345,39 +333,18 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
     for (int l = 0; l < t.nlevels; l++) G.scale[l] = t.scale[l];
     G.logScale = mc.logScale;
   }
-  // The two object stages run on streams of their own (streams beyond the runtime's
-  // GPU_MAX_HW_QUEUES share hardware queues; a priority class other than normal gets a queue of
-  // its own: the RANSAC stream is low priority).
+  // The two object stages run on streams of their own, both at low priority (a priority class
+  // other than normal gets a hardware queue of its own; a normal-priority D3 stream shares the ego
+  // chain's queue and halves C3).  Measured alternatives (round 3-4): the RANSAC
+  // stream confined to every 4th CU and D3 at high priority, chunked C3 895 against 896 frames/s,
+  // one frame per call 1.77 against 1.49 ms.
   int lo = 0, hi = 0;
   MMT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  // MMT_RANSAC_CU_MASK=1: the RANSAC stream confined to every 4th CU (otherwise every CU, low
-  // priority).  Its kernels are grids of hundreds of one-wave workgroups at 256 VGPRs; spread over
-  // the whole chip they can leave no CU with a free SIMD for the ego chain's workgroups.
-  // MMT_D3_PRIO: the D3 stream's priority, 0 or unset low (the default), 1 high, 2 normal (the
-  // measured worst: a normal-priority stream shares the ego chain's queue).  Round 3 chose both for the
-  // chunked bench; measured again with LocalMapping (interleaved A/B, tools/ab_interleave.py and
-  // tools/one_frame_bench.py): chunked C3 895 (both on) against 896 frames/s (both off), one frame
-  // per call 1.77 against 1.49 ms (the high-priority D3 queue and the masked RANSAC grids delay
-  // the ego chain's one-workgroup solves: k_pose_opt_l<4> 5 -> 100+ µs beside k_pnp_hyp)
-  const char* cm = getenv("MMT_RANSAC_CU_MASK");
-  if (cm && atoi(cm) == 1) {
-    int ncu = 0;
-    MMT_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg.device_id));
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; c += 4) mask[c / 32] |= 1u << (c % 32);
-    MMT_HIP(hipExtStreamCreateWithCUMask(&oa_, (uint32_t)mask.size(), mask.data()));
-  } else {
-    MMT_HIP(hipStreamCreateWithPriority(&oa_, hipStreamNonBlocking, lo));
-  }
-  const char* dp = getenv("MMT_D3_PRIO");  // 1 high, 2 normal, otherwise (0, unset) low
-  const int d3v = dp ? atoi(dp) : 0;
-  const int d3p = d3v == 1 ? hi : (d3v == 2 ? 0 : lo);
-  MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, d3p));
+  (void)hi;
+  MMT_HIP(hipStreamCreateWithPriority(&oa_, hipStreamNonBlocking, lo));
+  MMT_HIP(hipStreamCreateWithPriority(&ob_, hipStreamNonBlocking, lo));
   MMT_HIP(hipHostMalloc((void**)&eh_, sizeof(EgoHost), hipHostMallocDefault));
   memset(eh_, 0, sizeof(EgoHost));
-  for (auto& e : ev_slot_)
-    for (hipEvent_t& x : e)
-      if (!x) MMT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
   reset();
   device_ = cfg.device_id;
   // MMT_OBJ_THREAD=1: the object path's host side on a worker thread (903 against 895 fps
@@ -390,189 +357,12 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   // above 16 and the "flat to 32" sweep were measured with more object slots than this build's
   // kObjSlots = 18, which caps the lag at 16)
   static_assert(kSlots > kObjLagMax + 2, "frame slots too few for the object lag");
-  if (const char* ol = getenv("MMT_OBJ_LAG")) obj_lag_ = std::max(1, std::min(kObjLagMax, atoi(ol)));
-  // MMT_DEBUG_D3_ITERS: caps D3's LM iterations (the reference's 200), for bottleneck analysis
-  // only: it changes the object results
-  if (const char* di = getenv("MMT_DEBUG_D3_ITERS")) d3_iters_ = std::max(1, atoi(di));
   // MMT_DEBUG_SPLIT_SPIN: the split ego solve's exchange spin bound in wall-clock ticks (test
   // hook: a tiny bound forces the not-resident status and so the one-workgroup re-run)
   if (const char* ss = getenv("MMT_DEBUG_SPLIT_SPIN")) split_spin_ = strtoull(ss, nullptr, 10);
-  // MMT_OBJ_SPLIT=1: the overlap above in two steps (C2: the grouping launch; C3: the rest);
-  // measured slower, off by default (interleaved A/B: C3 888 against 903 frames/s, one frame per
-  // call 1.90-1.93 against 1.77-1.83 ms).  MMT_B3_HOST (default 1): k_stereo_grid writes the
-  // chunk's host copies itself (one frame per call 1.90-1.93 against 2.01-2.22 ms with the
-  // capacity-sized copies; C3 within noise, 888 against 894)
-  const char* os = getenv("MMT_OBJ_SPLIT");
-  obj_split_ = os && atoi(os) == 1;
-  const char* bh = getenv("MMT_B3_HOST");
-  b3_host_ = !(bh && atoi(bh) == 0);
-  const char* oo = getenv("MMT_OBJ_OVERLAP");
-  overlap_obj_ = !(oo && atoi(oo) == 0);
-  const char* ot = getenv("MMT_OBJ_THREAD");
-  ow_on_ = ot && atoi(ot) == 1;
-  if (ow_on_ && !ow_.joinable()) ow_ = std::thread([this] { obj_worker_main(); });
-}
-
-// ------------------------------------------------------------------ object worker
-void Tracker::obj_job(ObjFrame& F) {
-  auto now = [] {
-    return std::chrono::duration<double, std::micro>(
-               std::chrono::steady_clock::now().time_since_epoch()).count();
-  };
-  const double t0 = hprof_ ? now() : 0;
-  obj_stage_a(F);
-  const double t1 = hprof_ ? now() : 0;
-  obj_stage_b(F);
-  if (hprof_) {
-    hprof_us_[4] += t1 - t0;
-    hprof_us_[5] += now() - t1;
-  }
-  // everything this job enqueued that reads its two frame slots
-  for (int s : {F.cur, F.last}) {
-    MMT_HIP(hipEventRecord(ev_slot_[s][0], oa_));
-    MMT_HIP(hipEventRecord(ev_slot_[s][1], ob_));
-  }
-}
-
-void Tracker::obj_worker_main() {
-  (void)hipSetDevice(device_);
-  auto guarded = [this](auto&& fn) {
-    int kind = 0;
-    std::string msg;
-    try {
-      fn();
-    } catch (const DeviceError& e) {
-      kind = 1;
-      msg = e.msg;
-    } catch (const ArgError& e) {
-      kind = 2;
-      msg = e.msg;
-    } catch (const std::exception& e) {
-      kind = 1;
-      msg = e.what();
-    } catch (...) {
-      kind = 1;
-      msg = "object worker: unknown exception";
-    }
-    if (kind) {
-      std::lock_guard<std::mutex> lk(om_);
-      if (!o_err_kind_) {
-        o_err_kind_ = kind;
-        o_err_ = msg;
-      }
-    }
-  };
-  auto now = [] {
-    return std::chrono::duration<double, std::micro>(
-               std::chrono::steady_clock::now().time_since_epoch()).count();
-  };
-  std::unique_lock<std::mutex> lk(om_);
-  for (;;) {
-    ocv_.wait(lk, [&] {
-      return o_stop_ || !oq_.empty() ||
-             (!inflight_.empty() && (inflight_.front().seq <= o_need_fin_ || o_discard_));
-    });
-    if (o_stop_ && oq_.empty()) return;
-    if (!oq_.empty()) {
-      ObjFrame F = oq_.front();
-      oq_.pop_front();
-      if (!o_discard_ && !o_err_kind_) {
-        lk.unlock();
-        guarded([&] { obj_job(F); });
-        lk.lock();
-      }
-      inflight_.push_back(F);
-    }
-    // finish in order: beyond the lag, what the main thread waits for, or everything when the
-    // jobs are dropped
-    while (!inflight_.empty() &&
-           ((int)inflight_.size() > obj_lag_ || inflight_.front().seq <= o_need_fin_ ||
-            o_discard_ || o_err_kind_)) {
-      ObjFrame G = inflight_.front();
-      inflight_.pop_front();
-      if (!o_discard_ && !o_err_kind_) {
-        lk.unlock();
-        const double t0 = hprof_ ? now() : 0;
-        guarded([&] { obj_finish(G); });
-        if (hprof_) hprof_us_[6] += now() - t0;
-        lk.lock();
-      }
-      o_finished_ = G.seq;
-      odone_.notify_all();
-    }
-  }
-}
-
-void Tracker::obj_check() {
-  int kind = 0;
-  std::string msg;
-  {
-    std::lock_guard<std::mutex> lk(om_);
-    kind = o_err_kind_;
-    msg = o_err_;
-    o_err_kind_ = 0;
-    o_err_.clear();
-  }
-  if (kind == 1) throw DeviceError(msg);
-  if (kind == 2) throw ArgError(msg);
-}
-
-void Tracker::obj_submit(const ObjFrame& F0) {
-  obj_check();
-  ObjFrame F = F0;
-  {
-    std::lock_guard<std::mutex> lk(om_);
-    F.seq = ++o_handed_;
-    oq_.push_back(F);
-  }
-  slot_job_[F.cur] = slot_job_[F.last] = F.seq;
-  ocv_.notify_one();
-}
-
-void Tracker::slot_wait(int s, hipStream_t st) {
-  const long k = slot_job_[s];
-  if (k == 0) return;
-  {
-    std::unique_lock<std::mutex> lk(om_);
-    if (o_finished_ < k) {
-      o_need_fin_ = std::max(o_need_fin_, k);
-      ocv_.notify_one();
-      odone_.wait(lk, [&] { return o_finished_ >= k; });
-    }
-  }
-  obj_check();
-  // the job is frames old: its device work has normally finished, and a wait would put a barrier
-  // packet on the ego queue for nothing
-  for (hipEvent_t e : ev_slot_[s]) {
-    const hipError_t q = hipEventQuery(e);
-    if (q == hipErrorNotReady)
-      MMT_HIP(hipStreamWaitEvent(st, e, 0));
-    else if (q != hipSuccess)
-      MMT_HIP(q);
-  }
-  slot_job_[s] = 0;
-}
-
-void Tracker::obj_drain(bool discard) {
-  if (!ow_.joinable()) return;
-  {
-    std::unique_lock<std::mutex> lk(om_);
-    if (discard) o_discard_ = true;
-    o_need_fin_ = o_handed_;
-    ocv_.notify_one();
-    odone_.wait(lk, [&] { return o_finished_ >= o_handed_; });
-    o_discard_ = false;
-    if (discard) {
-      o_err_kind_ = 0;
-      o_err_.clear();
-    }
-  }
-  if (!discard) obj_check();
 }
 
 void Tracker::reset() {
-  obj_drain(true);
-  for (long& k : slot_job_) k = 0;
   if (oa_) MMT_HIP(hipStreamSynchronize(oa_));
   if (ob_) MMT_HIP(hipStreamSynchronize(ob_));
   if (d_err_) MMT_HIP(hipMemset(d_err_, 0, sizeof(int)));  // a bad label does not outlive a reset
@@ -584,10 +374,7 @@ void Tracker::reset() {
   last_ = kSlots - 1;
   ego_pending_ = false;
   qa_ = ObjFrame();
-  {
-    std::lock_guard<std::mutex> lk(om_);  // the worker is idle (drained), its queue empty
-    inflight_.clear();
-  }
+  inflight_.clear();
   obj_slot_next_ = 0;
   dq_.clear();
   frame_seq_ = 0;
@@ -629,7 +416,7 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   const int nbuf = chunk_buf_ ^ 1;
   const HostChunk& hc = hc_[nbuf];
   std::vector<int> nkp(nframes);
-  if (b3_host_) {
+  {
     B3HostOut ho = hc.dev;
     ho.ddesc = d_desc_;
     ho.err_src = engine_->err_word();
@@ -638,20 +425,6 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
                        &ho);
     MMT_HIP(hipStreamSynchronize(st));
     engine_->check_flags_value(hc.nkp[nframes], st);  // throws on a tripped octree guard
-    std::copy(hc.nkp, hc.nkp + nframes, nkp.begin());
-  } else {  // MMT_B3_HOST=0: capacity-sized copies after the kernel (A/B)
-    launch_stereo_grid(d_kps_, d_nkp_, kcap_, d_depth_, npix, W_, H_, cfg_.bf, grid0_.invW,
-                       grid0_.invH, d_uR_, d_kdepth_, d_cell_start_, d_cell_idx_, nframes, st);
-    MMT_HIP(hipMemcpyAsync(hc.kps, d_kps_, sizeof(mmt_kp) * (size_t)kcap_ * nframes,
-                           hipMemcpyDeviceToHost, st));
-    MMT_HIP(hipMemcpyAsync(hc.desc, d_desc_, 32 * (size_t)kcap_ * nframes,
-                           hipMemcpyDeviceToHost, st));
-    MMT_HIP(hipMemcpyAsync(hc.uR, d_uR_, sizeof(float) * (size_t)kcap_ * nframes,
-                           hipMemcpyDeviceToHost, st));
-    MMT_HIP(hipMemcpyAsync(hc.kdepth, d_kdepth_, sizeof(float) * (size_t)kcap_ * nframes,
-                           hipMemcpyDeviceToHost, st));
-    MMT_HIP(hipMemcpyAsync(hc.nkp, d_nkp_, sizeof(int) * nframes, hipMemcpyDeviceToHost, st));
-    engine_->check_flags(st);  // synchronises st; throws on a tripped octree guard
     std::copy(hc.nkp, hc.nkp + nframes, nkp.begin());
   }
   chunk_buf_ = nbuf;
@@ -668,7 +441,6 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
   // on ost_.  Frame f's ego solve runs on the GPU while the host drives frame f-1's object path.
   try {
   for (int f = 0; f < nframes; f++) {
-    if (ow_on_) slot_wait(cur_, st);  // the slot this frame's ego path writes
     obj_ran_ = false;
     FrameArgs a;
     a.depth = d_depth_ + npix * f;
@@ -689,13 +461,9 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
       const double t1 = now();
       ego_map_finish(outs[f]);
       hprof_us_[3] += now() - t1;
-      if (!ow_on_ && !obj_ran_) obj_advance();
+      if (!obj_ran_) obj_advance();
       const double t2 = now();
       ego_finish(outs[f], st);
-      if (ow_on_ && qa_.active) {
-        obj_submit(qa_);
-        qa_ = ObjFrame();
-      }
       hprof_us_[0] += t2 - t1;
       hprof_us_[1] += t1 - t0;
       hprof_us_[2] += now() - t2;
@@ -706,32 +474,21 @@ void Tracker::track_chunk(const uint8_t* d_bgr, size_t bgr_pitch, const uint16_t
     // host finishes the map branch (keyframes) and drives frame f-1's object path
     ego_launch(a, outs[f], st);
     ego_map_finish(outs[f]);
-    if (!ow_on_ && !obj_ran_) obj_advance();  // when no map chain took it
+    if (!obj_ran_) obj_advance();  // when no map chain took it
     ego_finish(outs[f], st);
-    if (ow_on_ && qa_.active) {  // the frame's object path, on the worker
-      obj_submit(qa_);
-      qa_ = ObjFrame();
-    }
   }
   } catch (...) {
-    obj_drain(true);  // no job may outlive the call (they write into `outs`)
     // the inline path: frames still in flight (and the queued one) point into `outs`, which dies
     // with this call; let their device work finish and drop them (the object pipeline restarts)
     if (oa_) (void)hipStreamSynchronize(oa_);
     if (ob_) (void)hipStreamSynchronize(ob_);
-    {
-      std::lock_guard<std::mutex> lk(om_);
-      inflight_.clear();
-    }
+    inflight_.clear();
     qa_ = ObjFrame();
     dq_.clear();  // deferred records of frames whose pipeline was dropped
     throw;
   }
   // the chunk's results are complete on return (deferred mode: the finished object records)
-  if (ow_on_)
-    obj_drain(false);
-  else if (!defer_)
-    obj_flush();
+  if (!defer_) obj_flush();
   if (defer_) {
     deliver_deferred(outs, false);
   } else {
@@ -762,7 +519,6 @@ void Tracker::frame_samples(float* sxy, int scap, int* ns, float* oxy, int32_t* 
 }
 
 void Tracker::set_deferred(bool on) {
-  if (on && ow_on_) throw ArgError("deferred object results need the inline object path (MMT_OBJ_THREAD=0)");
   if (on == defer_) return;
   if (!on) {  // results still owed are lost to a caller who turns the mode off: finish them first
     std::vector<FrameOut> drop;
@@ -798,10 +554,6 @@ void Tracker::flush_deferred(std::vector<FrameOut>& outs) {
 // Enqueue the queued frame's whole object path (stage A's host decisions need one wait for the
 // grouping statistics; stage B is device-ordered), then read the results of frames older than
 // obj_lag_.  Called while the next ego solve runs.
-void Tracker::obj_advance_launch() {
-  if (qa_.active) obj_stage_a_launch(qa_);
-}
-
 void Tracker::obj_advance() {
   obj_ran_ = true;
   auto now = [] {
@@ -897,17 +649,9 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   // may reset mLastFrame's pose (UpdateLastFrame), which the rest of this frame reads
   {
     MapStatsH& ms = out.map;
-    // the previous frame's object path runs while the first map chain is on the GPU
-    // in two steps: the grouping kernel goes out inside the first map chain (C2), the host
-    // decisions, the RANSAC, D3 and the old frames' results inside the second (C3), whose kernels
-    // then run while the host works; a frame without C3 finishes them after the map branch
-    if (!ow_on_ && overlap_obj_ && obj_split_)
-      map_.set_overlap([this] {
-        obj_advance_launch();
-        map_.set_overlap([this] { obj_advance(); });
-      });
-    else if (!ow_on_ && overlap_obj_)  // MMT_OBJ_SPLIT=0: all of it inside the first chain
-      map_.set_overlap([this] { obj_advance(); });
+    // the previous frame's object path runs while the first map chain is on the GPU (splitting
+    // it over the two map chains measured slower: C3 888 against 903 frames/s)
+    map_.set_overlap([this] { obj_advance(); });
     const int rr = map_.track(C.m, G, ego_Tinit_, Ls.m, Ls.Tview, V_, hasVelocity_,
                               bSecondFrame_, ms, st);
     map_.set_overlap(nullptr);  // not taken (no chain ran): the loop runs it
