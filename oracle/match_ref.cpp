@@ -9,6 +9,7 @@
 // logf is within 0.52 ulp of that).
 
 #include <algorithm>
+#include <cstdlib>
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -28,9 +29,17 @@ static inline float logf_pinned(float x) { return (float)std::log((double)x); }
 void frame_stereo_grid(MatchFrame& F, const float* depth, int W, int H) {
   F.uR.assign(F.n, -1.f);
   F.depth.assign(F.n, -1.f);
+  // ORACLE_ABLATE bit 4 (diagnostics only, tools/drift_ablation.py): the depth at the nearest
+  // pixel instead of the truncated one
+  static const bool nearest = [] {
+    const char* e = getenv("ORACLE_ABLATE");
+    return e && (atoi(e) & 4);
+  }();
   for (int i = 0; i < F.n; i++) {
     const float v = F.keys[i].y, u = F.keys[i].x;
-    const float d = depth[(size_t)(int)v * W + (int)u];  // at<float>(v,u): float -> int truncation
+    const int iv = nearest ? std::min(H - 1, (int)std::lround(v)) : (int)v;
+    const int iu = nearest ? std::min(W - 1, (int)std::lround(u)) : (int)u;
+    const float d = depth[(size_t)iv * W + iu];  // at<float>(v,u): float -> int truncation
     if (d > 0) {
       F.depth[i] = d;
       F.uR[i] = F.keys[i].x - F.bf / d;

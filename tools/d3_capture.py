@@ -49,7 +49,7 @@ def main():
     np.savez(os.path.join(ROOT, "gpurun_out", "d3_f%d_o%d.npz" % (a.frame, a.obj)), **P)
     if torch.cuda.is_available():
         ctx = M.Context(M.kitti03_config(a.w, a.h, a.nfeat))
-        for env in ({}, {"MMT_LM_SPLIT": "0"}, {"MMT_LM_SPLIT": "0", "MMT_LM_SPEC1": "0"},
+        for env in ({}, {"MMT_LM_SPLIT": "0"},
                     {"MMT_LM_MAX_CAND": "1"}):
             old = {k: os.environ.get(k) for k in env}
             os.environ.update(env)

@@ -8,6 +8,9 @@ ablation per process and logs the per-frame pose error against the renderer's gr
   no_lm     ORACLE_LM_STEPS=0: ProcessNewKeyFrame + MapPointCulling only
   no_cull   ORACLE_ABLATE=1: no MapPointCulling
   tlr_post  ORACLE_ABLATE=2: Tlr taken after the keyframe's LocalMapping (round 4's order)
+  depth_nearest        ORACLE_ABLATE=4: the keys' depth (mvDepth, mvuRight) read at the nearest
+                       pixel instead of the truncated one (Frame.cc:1041-1062's at<float>(v, u))
+  no_ba_depth_nearest  both
 Frames are rendered on the GPU (scene.py) and copied to the host; the oracle runs on the host
 cores, one process per configuration.  Output: one JSON per configuration with, every 100 frames,
 the camera-centre error of the final pose (after the flow solve) and of the map-branch pose, the
@@ -36,6 +39,8 @@ CONFIGS = {
     "no_lm": {"ORACLE_LM_STEPS": "0"},
     "no_cull": {"ORACLE_ABLATE": "1"},
     "tlr_post": {"ORACLE_ABLATE": "2"},
+    "depth_nearest": {"ORACLE_ABLATE": "4"},
+    "no_ba_depth_nearest": {"ORACLE_ABLATE": "4", "ORACLE_LM_STEPS": "5"},
 }
 
 
