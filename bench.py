@@ -23,7 +23,9 @@ Multi-GPU: one process per GPU, independent sequences, no data-path collective; 
 sync bracket the timed region; time = MAX over ranks; value = frames of all ranks / that time
 ("scaling": "weak").  `--gpus N` without a torchrun environment launches the N ranks itself
 (torch.distributed.run as a child process; this parent never touches the GPU); n_gpus is the
-world size the process group was initialised with.
+world size the process group was initialised with.  --ranks-per-gpu R runs R such processes per
+GPU (each its own sequences, contexts and hardware queues; gloo for the barrier and reductions):
+the rate of several sequences per GPU without one process's shared queues.
 
 roofline: the batched ORB window -- k_gray_depth (A1 + A2) and the ORB launch sequence (A3-A9) --
 with SURVEY 8(d)'s B_orb = 3WH + 4P + 60N plus A2's 6WH algorithmic bytes per frame x frames per
@@ -130,6 +132,10 @@ def parse_args(argv=None):
                          "pipeline at each chunk boundary)")
     ap.add_argument("--single-frames", type=int, default=256,
                     help="frames of the one-frame-per-call leg (0: skip)")
+    ap.add_argument("--ranks-per-gpu", type=int, default=1,
+                    help="processes per GPU, each with its own sequence(s), contexts and the "
+                         "HIP runtime's hardware queues (gloo for the barrier and the reductions; "
+                         "n_gpus stays the GPU count)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="GPU_MAX_HW_QUEUES for this process (0: leave it; more queues measured "
                          "slower: K=8 1461 / 733 / 299 frames/s at 4 / 16 / 32)")
@@ -154,7 +160,7 @@ def self_launch(args):
     torch.distributed.run as a child process and return its exit code.  Nothing here touches the
     GPU, so the ranks own their devices from the start."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--nproc-per-node", str(args.gpus * args.ranks_per_gpu), "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -335,6 +341,7 @@ def run_dry(args, rank, world):
     for wl in wls:
         n = None if wl["length"] is None else int(wl["length"] * args.dry_length_scale)
         rsteps.append(shard.rank_steps(n, C, args.warmup, args.steps))
+    R = max(1, args.ranks_per_gpu)
     step_s = 0.01 * (rank + 1)  # rank r's stand-in step cost
     for _ in range(max(w for w, _ in rsteps)):
         time.sleep(step_s)
@@ -357,20 +364,21 @@ def run_dry(args, rank, world):
         all_wl = [mine]
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(frames_all / elapsed, 2),
-                          "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                          "unit": "frames/s", "n_gpus": world // R, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                           "dtype": "u8", "data": "dry run (no GPU work)",
                           "config": {"workload": "dry", "config": args.config,
-                                     "chunk_frames": C, "sequences_per_gpu": K,
-                                     "parallelism": "dp%d" % world, "seeds": all_seeds,
+                                     "chunk_frames": C, "sequences_per_gpu": K * R,
+                                     "parallelism": "dp%d" % (world // R), "seeds": all_seeds,
                                      "ranks": all_wl, "frames_all": frames_all}}), flush=True)
 
 
 # ------------------------------------------------------------------ main
 def main(argv=None):
     args = parse_args(argv)
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    R = max(1, args.ranks_per_gpu)
+    if (args.gpus > 1 or R > 1) and "WORLD_SIZE" not in os.environ:
         return self_launch(args)
 
     # GPU_MAX_HW_QUEUES (hardware queues the HIP runtime multiplexes a process's streams onto,
@@ -384,7 +392,9 @@ def main(argv=None):
 
     rank, world, local = shard.rank_env()
     if world > 1:
-        dist.init_process_group("gloo" if args.dry else "nccl", init_method="env://")
+        # several ranks on one GPU: RCCL wants one rank per device, so the (tiny) barrier and
+        # reductions go through gloo on host tensors
+        dist.init_process_group("gloo" if args.dry or R > 1 else "nccl", init_method="env://")
         world = dist.get_world_size()
     if args.dry:
         run_dry(args, rank, world)
@@ -395,8 +405,11 @@ def main(argv=None):
     import multimot_track_amd as M
     from multimot_track_amd import scene
 
+    local //= R  # the GPU of this rank (R ranks per GPU)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    rdev = torch.device("cpu") if R > 1 else dev  # where the cross-rank reductions run
+    n_gpus = world // R
 
     C, K = args.chunk, args.seqs_per_gpu
     # this rank's sequences (shard.workload: C3 by default; C4 / C5 per-rank geometry and length)
@@ -483,8 +496,8 @@ def main(argv=None):
     shard.barrier(world, dev)
     elapsed = time.perf_counter() - t0
     prof = ctx.profile_read()
-    elapsed = shard.max_over_ranks(elapsed, world, dev)
-    frames_all = shard.sum_over_ranks(sum(t for _, t in rsteps) * C, world, dev)
+    elapsed = shard.max_over_ranks(elapsed, world, rdev)
+    frames_all = shard.sum_over_ranks(sum(t for _, t in rsteps) * C, world, rdev)
 
     # per-frame outputs of every sequence (sanity: every timed frame tracked by the map, objects
     # found); a line whose timed frames are not all tracked is marked invalid
@@ -495,7 +508,7 @@ def main(argv=None):
     n_obj_last = len(timed_frames[-1]["objects"]) if timed_frames else 0
     tracked_rank = sum(int(d["initialized"]) for k, f in enumerate(seq_frames)
                        for d in f[rsteps[k][0] * C:])
-    tracked = int(shard.sum_over_ranks(tracked_rank, world, dev))
+    tracked = int(shard.sum_over_ranks(tracked_rank, world, rdev))
     lost_first = [next((rsteps[k][0] * C + i for i, d in enumerate(f[rsteps[k][0] * C:])
                         if not d["initialized"]), None) for k, f in enumerate(seq_frames)]
     gt = seq["Tcw"][len(all_frames) - 1]
@@ -613,7 +626,7 @@ def main(argv=None):
         frames_timed = int(frames_all)
         out = {
             "metric": METRIC,
-            "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": n_gpus,
             "frames_timed": frames_timed, "frames_tracked": tracked,
             "valid": tracked == frames_timed,
             "steps": args.steps, "warmup": args.warmup,
@@ -624,7 +637,9 @@ def main(argv=None):
             "config": {"workload": WORKLOADS[args.config] % (wls[0]["objects"] * wls[0]["parts"]),
                        "config": args.config, "ranks": rank_wl, "ego_rpe": rpe,
                        "width": W, "height": H, "orb_features": NF, "chunk_frames": C,
-                       "sequences_per_gpu": K, "parallelism": "dp%d" % world,
+                       "sequences_per_gpu": K * R, "ranks_per_gpu": R,
+                       "parallelism": "dp%d" % n_gpus if R == 1 else "dp%d x %d ranks per GPU" % (
+                           n_gpus, R),
                        "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "frames_tracked": tracked, "objects_last_frame": n_obj_last,
                        "ego_abs_err_last_frame": round(ego_err, 5),

@@ -26,8 +26,9 @@
 // object centroids are ObjCentre3D_pre (the solve's last-frame centroid, which mmt_motion
 // carries) instead of vObjCentre3D.
 //
-// Differences from the reference binary: the vocabulary is not read (this path
-// never uses BoW); no viewer, no imshow/waitKey; the usleep pacing to the timestamps is off
+// Differences from the reference binary: a vocabulary that does not load (the
+// reference's ORBvoc.txt is missing from its tree) is a warning, and tracking goes on with the
+// substitutes of DESIGN.md §2 instead of the reference's exit(-1) (System.cc:62-66); no viewer, no imshow/waitKey; the usleep pacing to the timestamps is off
 // unless --realtime; a sequence whose times.txt lists more frames than exist on disk stops
 // cleanly after the last frame (the reference fails at the first missing image).
 #include <chrono>
@@ -298,6 +299,12 @@ int main(int argc, char** argv) {
     fprintf(stderr, "mmt_create failed: %s\n", mmt_last_error(nullptr));
     return 1;
   }
+  // System::System: "Loading ORB Vocabulary" (System.cc:57-67)
+  if (mmt_load_vocabulary(ctx, pos[0].c_str()) == MMT_OK)
+    printf("Vocabulary loaded!\n\n");
+  else
+    fprintf(stderr, "warning: vocabulary %s not loaded (%s): tracking without BoW\n",
+            pos[0].c_str(), mmt_last_error(ctx));
   const int W = cfg.width, H = cfg.height;
   const size_t npix = (size_t)W * H;
   const int F = chunk;

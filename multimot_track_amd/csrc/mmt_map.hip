@@ -1179,6 +1179,12 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
   curId_ = C.id;
   const double t_track = prof_on_ ? now_us() : 0;
   bool bOK;
+  // a branch that computes no pose leaves the motion model's prediction, or the last pose
+  // (pinned as in the oracle: the reference's mCurrentFrame.mTcw stays empty there)
+  if (has_vel)
+    mat4_mul(vel, Tlast, Tcw);
+  else
+    memcpy(Tcw, Tlast, 64);
   if (state_ == 1) {
     // CheckReplacedInLastFrame (Tracking.cc:2766-2781): one level of MapPoint::GetReplaced
     for (int i = 0; i < L.n; i++)
@@ -1197,8 +1203,7 @@ int MapEngine::track(MapFrameH& C, const GridFrame& G, float* Tcw, MapFrameH& L,
       }
     }
   } else if (voc_) {  // Relocalization (Tracking.cc:3614-3776)
-    mat4_mul(vel, Tlast, Tcw);  // no pose computed: the motion model's prediction (pinned)
-    bOK = relocalization(C, G, Tcw);
+    bOK = relocalization(C, G, Tcw);  // from the prediction set above
     if (bOK) lastRelocFrameId_ = C.id;
   } else {
     bOK = relocalization_subst(C, G, Tcw, Tlast, vel);  // Relocalization (substitute)

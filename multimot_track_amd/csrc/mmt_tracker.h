@@ -195,7 +195,7 @@ class Tracker {
   // object-pipeline buffers: at least the frames in flight (obj_lag_ + 1) plus one
   static constexpr int kObjSlots = 18;
   static constexpr int kObjLagMax = kObjSlots - 2;
-  // frames between enqueueing a frame's D3 and reading it (MMT_OBJ_LAG, 1..kObjLagMax)
+  // frames between enqueueing a frame's D3 and reading it (1..kObjLagMax)
   int obj_lag_ = 16;
   int d3_iters_ = 200;  // PoseOptimizationFlow2's optimize(200) (Optimizer.cc:2292)
   FrameSlot slot_[kSlots];

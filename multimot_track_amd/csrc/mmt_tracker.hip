@@ -347,15 +347,11 @@ void Tracker::setup(const mmt_config& cfg, OrbEngine* engine, int max_chunk) {
   memset(eh_, 0, sizeof(EgoHost));
   reset();
   device_ = cfg.device_id;
-  // MMT_OBJ_THREAD=1: the object path's host side on a worker thread (903 against 895 fps
-  // inline, 905 with the overlap above, which needs no thread: off by default)
-  // MMT_OBJ_OVERLAP (default 1): the previous frame's object path inside the first map chain of
-  // the frame, while its kernels run (C3 895 -> 905 fps, tools/ab_interleave.py, 4 rounds)
-  // MMT_OBJ_LAG: frames between enqueueing a frame's object path and reading its results (default
-  // 16: the D3 chain's slow stretches no longer stall the host; interleaved A/B 905 / 915 / 920 fps
-  // at 2 / 3 / 4, then 932 / 937 / 944 / 950 / 956 / 964 at 4 / 6 / 8 / 10 / 14 / 18; the lags
-  // above 16 and the "flat to 32" sweep were measured with more object slots than this build's
-  // kObjSlots = 18, which caps the lag at 16)
+  // The previous frame's object path runs on this thread inside the first map chain of the frame,
+  // while its kernels run (C3 895 -> 905 fps; a worker thread measured slower).
+  // obj_lag_ = 16 frames between enqueueing a frame's object path and reading its results: the D3
+  // chain's slow stretches no longer stall the host (interleaved A/B 905 / 915 / 920 fps at 2 / 3 /
+  // 4, then 932 / 937 / 944 / 950 / 956 at 4 / 6 / 8 / 10 / 14; kObjSlots = 18 caps it at 16)
   static_assert(kSlots > kObjLagMax + 2, "frame slots too few for the object lag");
   // MMT_DEBUG_SPLIT_SPIN: the split ego solve's exchange spin bound in wall-clock ticks (test
   // hook: a tiny bound forces the not-resident status and so the one-workgroup re-run)

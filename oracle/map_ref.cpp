@@ -801,6 +801,13 @@ int MapTracker::track(const std::vector<Key>& keys, const std::vector<uint8_t>& 
                       bool& has_vel, bool& bSecondFrame, MapStats& st) {
   curId_ = C.id;
   bool bOK;
+  // A branch that computes no pose (TrackReferenceKeyFrame below 15 BoW matches, a relocalisation
+  // without a hypothesis) leaves mCurrentFrame.mTcw empty in the reference, and the flow solve
+  // then starts from it (undefined).  Pinned: the motion model's prediction, or the last pose.
+  if (has_vel)
+    m4_mul(vel, Tlast, Tcw);
+  else
+    memcpy(Tcw, Tlast, 64);
   if (state_ == 1) {
     // CheckReplacedInLastFrame (Tracking.cc:2766-2781): one level of MapPoint::GetReplaced
     for (size_t i = 0; i < L.mps.size(); i++)
@@ -820,10 +827,7 @@ int MapTracker::track(const std::vector<Key>& keys, const std::vector<uint8_t>& 
       }
     }
   } else if (voc_) {  // Relocalization (Tracking.cc:3614-3776)
-    float Tpred[16];
-    m4_mul(vel, Tlast, Tpred);
-    memcpy(Tcw, Tpred, 64);  // no pose computed: the motion model's prediction (pinned)
-    bOK = relocalization(keys, desc, C, Tcw);
+    bOK = relocalization(keys, desc, C, Tcw);  // from the prediction set above
     if (bOK) lastRelocFrameId_ = C.id;
   } else {
     bOK = relocalization_subst(keys, desc, C, Tcw, Tlast, vel);  // Relocalization substitute

@@ -109,3 +109,23 @@ def test_bench_c4_per_rank_workloads_dry():
     assert d["config"]["frames_all"] == (3 + 1) * 8
     # MAX over ranks: rank 0's three 10 ms steps, not rank 1's single 20 ms step
     assert d["ms_per_step"] * 3 >= 30.0
+
+
+def test_bench_ranks_per_gpu_dry():
+    """bench.py --ranks-per-gpu 2 on one GPU: two processes (gloo), each with its own sequence;
+    n_gpus stays 1, the time is the MAX over the ranks and the frames their SUM."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--ranks-per-gpu", "2",
+                        "--dry", "--steps", "3", "--warmup", "1", "--chunk", "8"], cwd=root,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["config"]["sequences_per_gpu"] == 2
+    assert d["config"]["seeds"] == [[1003], [1004]]
+    assert d["config"]["frames_all"] == 2 * 3 * 8
+    assert d["ms_per_step"] >= 20.0

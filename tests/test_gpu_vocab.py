@@ -103,15 +103,16 @@ def _check_maps(gm, om):
     assert np.abs(gm["pt_f"] - om["pt_f"]).max() < 1e-3
 
 
-def test_vocabulary_tracking_half_res_matches_oracle(oracle_mod):
-    """Half-resolution C3 drive, one textureless frame: the GPU tracker takes the oracle's
+def test_vocabulary_tracking_three_quarter_res_matches_oracle(oracle_mod):
+    """3/4-resolution C3 drive (the smallest the 8-level pyramid's cell grid takes), one
+    textureless frame: the GPU tracker takes the oracle's
     TrackReferenceKeyFrame / Relocalization / CreateNewMapPoints path frame by frame (poses within
     the bar, integers exact), its vocabulary counters equal the oracle's, and the final map graph
     is the oracle's."""
     from multimot_track_amd import scene
     from oracle import compare
-    K = {k: v * 0.5 for k, v in scene.KITTI03.items()}
-    got, ora, gb, ob, gm, om = _run_pair(oracle_mod, 621, 187, K, K["bf"], 1000, 40, [24])
+    K = {k: v * 0.75 for k, v in scene.KITTI03.items()}
+    got, ora, gb, ob, gm, om = _run_pair(oracle_mod, 931, 281, K, K["bf"], 1000, 40, [24])
     rec = compare.parity_record(got, ora)
     assert rec["first_divergent_frame"] is None, rec
     assert {k: gb[k] for k in BOW_KEYS} == {k: ob[k] for k in BOW_KEYS}

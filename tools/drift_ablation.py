@@ -11,6 +11,9 @@ ablation per process and logs the per-frame pose error against the renderer's gr
   depth_nearest        ORACLE_ABLATE=4: the keys' depth (mvDepth, mvuRight) read at the nearest
                        pixel instead of the truncated one (Frame.cc:1041-1062's at<float>(v, u))
   no_ba_depth_nearest  both
+  static, static_no_ba the same sequence without its three moving boxes (the ego motion, the
+                       street and the seed unchanged): do the map points that the moving boxes'
+                       keys create drive the drift through the local BA?
 Frames are rendered on the GPU (scene.py) and copied to the host; the oracle runs on the host
 cores, one process per configuration.  Output: one JSON per configuration with, every 100 frames,
 the camera-centre error of the final pose (after the flow solve) and of the map-branch pose, the
@@ -41,7 +44,10 @@ CONFIGS = {
     "tlr_post": {"ORACLE_ABLATE": "2"},
     "depth_nearest": {"ORACLE_ABLATE": "4"},
     "no_ba_depth_nearest": {"ORACLE_ABLATE": "4", "ORACLE_LM_STEPS": "5"},
+    "static": {},
+    "static_no_ba": {"ORACLE_LM_STEPS": "5"},
 }
+N_OBJECTS = {"static": 0, "static_no_ba": 0}
 
 
 def centre(T):
@@ -72,7 +78,8 @@ def worker(args):
     lost = []
     for s0 in range(0, args.frames, 200):
         n = min(200, args.frames - s0)
-        seq = scene.kitti_like_sequence(n, W, H, n_objects=3, seed=args.seed, device=dev, start=s0)
+        seq = scene.kitti_like_sequence(n, W, H, n_objects=N_OBJECTS.get(args.config, 3),
+                                        seed=args.seed, device=dev, start=s0)
         fr = scene.to_numpy_frames(seq)
         for i in range(n):
             f = fr[i]
@@ -101,7 +108,7 @@ def worker(args):
                              "wall_s": round(time.time() - t0, 1)})
                 print(args.config, json.dumps(rows[-1]), flush=True)
         del seq, fr
-    sc = scene.StreetScene(n_objects=3, seed=args.seed)  # the keyframes' ground truth
+    sc = scene.StreetScene(n_objects=N_OBJECTS.get(args.config, 3), seed=args.seed)  # the keyframes' ground truth
     m = tr.map_dump()
     kf_err = []
     for k in range(len(m["kf_i"])):
