@@ -10,7 +10,9 @@ host thread each; SURVEY 8(e) allows several sequences per device), seeds 1003 +
 A "step" = System::TrackRGBD over one chunk of `--chunk` consecutive frames of the sequence:
 batched ORB extraction for the chunk, then per frame everything the reference does on this path
 (mmt_track_rgbd_chunk_device), including the synchronous LocalMapping of every new keyframe
-(SearchInNeighbors + Fuse, local bundle adjustment, keyframe culling).  Frames are processed in
+(ComputeBoW, CreateNewMapPoints, SearchInNeighbors + Fuse, local bundle adjustment, keyframe
+culling) with the DBoW2 vocabulary loaded as System loads it (--vocabulary: the committed test
+vocabulary; the reference's ORBvoc.txt is missing).  Frames are processed in
 order, so the tracker state carries across steps exactly as in rgbd_mmt.  By default the object
 results are deferred (mmt_set_deferred_objects): the object pipeline keeps running across steps
 instead of draining at every chunk boundary, each frame's object motions arrive with a later
@@ -132,6 +134,12 @@ def parse_args(argv=None):
                          "pipeline at each chunk boundary)")
     ap.add_argument("--single-frames", type=int, default=256,
                     help="frames of the one-frame-per-call leg (0: skip)")
+    ap.add_argument("--vocabulary", default=os.path.join(ROOT, "tests", "golden",
+                                                          "test_voc_k10l6.txt"),
+                    help="DBoW2 vocabulary (text format) every context and oracle tracker loads, as "
+                         "System does (System.cc:57-67): TrackReferenceKeyFrame, Relocalization and "
+                         "LocalMapping's BoW steps + CreateNewMapPoints run; '' for none (the "
+                         "substitutes of DESIGN.md section 2)")
     ap.add_argument("--ranks-per-gpu", type=int, default=1,
                     help="processes per GPU, each with its own sequence(s), contexts and the "
                          "HIP runtime's hardware queues (gloo for the barrier and the reductions; "
@@ -206,6 +214,8 @@ def cpu_leg(args, seq, gpu_frames, timed_from, W, H, NF):
     O.build()
     K = (721.5377, 721.5377, 609.5593, 172.8540)
     tr = O.Tracker(W, H, K, 387.5744, 0, NF)
+    if args.vocabulary:
+        tr.set_vocabulary(args.vocabulary)
     affinity = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
     if affinity:
         os.sched_setaffinity(0, {min(affinity)})
@@ -259,7 +269,8 @@ def cpu_multi_leg(args, render, W, H, NF, fps1):
         for k in range(K):
             procs.append(subprocess.Popen(
                 [sys.executable, "-m", "oracle.cpu_worker", os.path.join(tmp, "s%d" % k),
-                 str(cores[k]), str(args.cpu_seqs_seconds), str(W), str(H), str(NF)],
+                 str(cores[k]), str(args.cpu_seqs_seconds), str(W), str(H), str(NF),
+                 args.vocabulary or ""],
                 cwd=ROOT, stdout=subprocess.PIPE, text=True))
         outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
         wall = time.perf_counter() - t0
@@ -314,6 +325,8 @@ def rank_parity(args, seqs, seq_frames, rank, wls):
         wl = wls[k]
         tr = O.Tracker(wl["width"], wl["height"], (721.5377, 721.5377, 609.5593, 172.8540),
                        387.5744, 0, wl["nfeatures"])
+        if args.vocabulary:
+            tr.set_vocabulary(args.vocabulary)
         ofr = [tr.track(f["bgr"], f["disp"], f["flow"], f["sem"]) for f in frames[k]]
         rec = compare.parity_record(seq_frames[k][:n], ofr)
         return {"rank": rank, "sequence": k, "workload": wl["name"], "seed": wl["seed"],
@@ -449,6 +462,9 @@ def main(argv=None):
                              device_id=local) for wl in wls]
     cfg = cfgs[0]
     ctxs = [M.Context(c) for c in cfgs]
+    for c in ctxs:
+        if args.vocabulary:
+            c.load_vocabulary(args.vocabulary)
     ctx = ctxs[0]
     if not args.immediate:
         for c in ctxs:
@@ -527,6 +543,9 @@ def main(argv=None):
                                              "ba_trials", "ba_edges", "ba_pts", "ba_max_opt",
                                              "fuse_launches", "fuse_queries", "fuse_relaunches",
                                              "d2_split_fallbacks")}
+    local_mapping["vocabulary"] = os.path.basename(args.vocabulary) if args.vocabulary else None
+    if args.vocabulary:  # the BoW steps inside the timed region (TRK, relocalisation, CNMP)
+        local_mapping["bow"] = ctx.bow_counters()
     if mc["lm_us"] > 0:  # host wall times, collected with MMT_MAP_PROFILE=1
         for k in ("lm_us", "ba_us", "fuse_us"):
             local_mapping[k] = round(float(mc[k]), 1)
@@ -560,6 +579,8 @@ def main(argv=None):
             ns = args.single_frames
             s1 = render(shard.sequence_seed(1003, 0), ns + 8)
             sctx = M.Context(M.kitti03_config(W, H, NF, max_batch=8, device_id=local))
+            if args.vocabulary:
+                sctx.load_vocabulary(args.vocabulary)
             sctx.set_deferred_objects(True)
             for i in range(8):  # initialisation and warm-up
                 sctx.track_chunk_device(s1["bgr"][i:i + 1], s1["disp"][i:i + 1],
@@ -586,6 +607,8 @@ def main(argv=None):
             nc2 = (1 + args.c2_steps) * C
             s2 = render(shard.sequence_seed(1003, 0), nc2, objects=0)
             c2ctx = M.Context(cfg)
+            if args.vocabulary:
+                c2ctx.load_vocabulary(args.vocabulary)
             step_k(0, 0, s2, c2ctx)
             torch.cuda.synchronize(dev)
             t2 = time.perf_counter()
@@ -611,6 +634,8 @@ def main(argv=None):
             if c2 is not None:
                 from oracle import oracle as O
                 tr2 = O.Tracker(W, H, (721.5377, 721.5377, 609.5593, 172.8540), 387.5744, 0, NF)
+                if args.vocabulary:
+                    tr2.set_vocabulary(args.vocabulary)
                 n2, tt2 = 0, 0.0
                 while tt2 < 5.0 and n2 < nc2:
                     f = seq_frame_numpy(s2, n2)

@@ -352,7 +352,11 @@ typedef short short2v __attribute__((ext_vector_type(2)));
 // LDS row stride of a FAST tile (template parameter FS): a compile-time constant, so every
 // circle / compass / NMS neighbour read is one ds_read with an immediate offset from the pixel's
 // address.  40 covers the ~31-pixel cells of any image (tile = cell + 6); 72 is the general case.
-constexpr int kFSSmall = 40, kFSMax = 72;
+#ifndef MMT_FAST_FS
+#define MMT_FAST_FS 40  // A/B builds: tools/ab_build.sh <tag> -DMMT_FAST_FS=..
+#endif
+constexpr int kFSSmall = MMT_FAST_FS, kFSMax = 72;
+static_assert(kFSSmall % 4 == 0 && kFSSmall >= 40 && kFSSmall <= 128, "FAST tile stride");
 
 // Circle differences as packed f16 pairs (v - q, q - v): every value is an integer of
 // magnitude <= 255, exact in f16, and min / max are exact, so the result equals the integer

@@ -4,7 +4,7 @@ oracle on one pinned core for about `seconds` of CPU time, and prints one JSON l
 {"frames", "seconds", "core"}.  It never touches the GPU (no torch import): the parent renders
 the frames on the GPU and starts the workers as child processes.
 
-usage: python -m oracle.cpu_worker DIR CORE SECONDS W H NFEAT"""
+usage: python -m oracle.cpu_worker DIR CORE SECONDS W H NFEAT [VOCABULARY]"""
 import json
 import os
 import sys
@@ -26,6 +26,8 @@ def main():
     mask = np.load(os.path.join(d, "mask.npy"), mmap_mode="r")
     K = (721.5377, 721.5377, 609.5593, 172.8540)
     tr = O.Tracker(W, H, K, 387.5744, 0, nfeat)
+    if len(sys.argv) > 7 and sys.argv[7]:
+        tr.set_vocabulary(sys.argv[7])
     n, t = 0, 0.0
     while t < seconds and n < len(bgr):
         f = (np.ascontiguousarray(bgr[n]), np.ascontiguousarray(disp[n]),

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <vector>
@@ -163,6 +164,20 @@ int OTracker::track(const uint8_t* bgr, const uint16_t* disp, const float* flow,
   }
   OFrame C;
   build_frame(P, orbc, bgr, disp, flow, mask, C);
+  // ORACLE_ABLATE bit 8 (diagnostics only, tools/drift_ablation.py): a level-l keypoint at the
+  // level-0 position of its pixel's centre, (x_l + 0.5) s - 0.5, instead of x_l s
+  // (ORBextractor.cc:1100-1104 scales the corner, not the centre)
+  static const bool centre = [] {
+    const char* e = getenv("ORACLE_ABLATE");
+    return e && (atoi(e) & 8);
+  }();
+  if (centre)
+    for (Key& k : C.keys)
+      if (k.octave > 0) {
+        const float d = 0.5f * (orbc.scale[k.octave] - 1.f);
+        k.x += d;
+        k.y += d;
+      }
   C.m.id = map.next_frame_id();
   map.prepare_frame(C.keys, C.depth.data(), C.m);
   std::vector<P2> mvTmpObjKeys;

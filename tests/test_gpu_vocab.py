@@ -96,11 +96,13 @@ def _run_pair(oracle_mod, W, H, K, bf, nfeat, n, lost, chunk=16, seed=1003):
 
 
 def _check_maps(gm, om):
-    for k in ("kf_i", "kf_mps_start", "kf_mps", "pt_i", "obs_start", "obs_i", "conn", "ord",
-              "child"):
-        assert np.array_equal(gm[k], om[k]), k
+    """Integer structure exact, poses / points / observations within 1e-3 (same_map; a key whose
+    truncated pixel holds disparity 0 has depth bf / 0 = inf in the reference, Tracking.cc:447-456,
+    and its point a non-finite position in both maps)."""
+    from map_invariants import same_map
+    diff, fmax = same_map(gm, om)
+    assert diff == [] and fmax < 1e-3, (diff, fmax)
     assert np.abs(gm["kf_T"] - om["kf_T"]).max() < 1e-4
-    assert np.abs(gm["pt_f"] - om["pt_f"]).max() < 1e-3
 
 
 def test_vocabulary_tracking_three_quarter_res_matches_oracle(oracle_mod):
@@ -130,6 +132,7 @@ def test_vocabulary_tracking_c3_300_frames_matches_oracle(oracle_mod):
     got, ora, gb, ob, gm, om = _run_pair(oracle_mod, 1242, 375, K, 387.5744, 2000, 300,
                                          [120, 230], chunk=32)
     rec = compare.parity_record(got, ora)
+    print("parity", rec, "\nbow counters", gb, "\nmap states", [g["map_state"] for g in got])
     assert rec["first_divergent_frame"] is None, rec
     assert {k: gb[k] for k in BOW_KEYS} == {k: ob[k] for k in BOW_KEYS}, (gb, ob)
     assert ob["trk_ok"] >= 1 and ob["reloc"] >= 2 and ob["triangulated"] > 100

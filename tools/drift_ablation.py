@@ -11,6 +11,8 @@ ablation per process and logs the per-frame pose error against the renderer's gr
   depth_nearest        ORACLE_ABLATE=4: the keys' depth (mvDepth, mvuRight) read at the nearest
                        pixel instead of the truncated one (Frame.cc:1041-1062's at<float>(v, u))
   no_ba_depth_nearest  both
+  level_centre         ORACLE_ABLATE=8: level-l keypoints at their pixel centre's level-0 position
+                       ((x + 0.5) s - 0.5) instead of x s (ORBextractor.cc:1100-1104)
   static, static_no_ba the same sequence without its three moving boxes (the ego motion, the
                        street and the seed unchanged): do the map points that the moving boxes'
                        keys create drive the drift through the local BA?
@@ -44,6 +46,7 @@ CONFIGS = {
     "tlr_post": {"ORACLE_ABLATE": "2"},
     "depth_nearest": {"ORACLE_ABLATE": "4"},
     "no_ba_depth_nearest": {"ORACLE_ABLATE": "4", "ORACLE_LM_STEPS": "5"},
+    "level_centre": {"ORACLE_ABLATE": "8"},
     "static": {},
     "static_no_ba": {"ORACLE_LM_STEPS": "5"},
 }
