@@ -529,6 +529,7 @@ void MapEngine::local_mapping(int kf) {
   // CreateNewMapPoints: SearchForTriangulation needs the vocabulary's FeatureVectors (without one
   // it is skipped, see mmt_map.h); mmt_bowmap.hip
   if (voc_) create_new_map_points(kf);
+  if (prof_on_) mstats_.cnmp_us += now_us() - t0;
   search_in_neighbors(kf);
   const double t1 = prof_on_ ? now_us() : 0;
   if (n_keyframes() > 2) local_bundle_adjustment(kf);

@@ -75,11 +75,12 @@ MapEngine::~MapEngine() {
     if (mstats_.n_lm > 0) {
       const double n = (double)mstats_.n_lm;
       fprintf(stderr, "[mmt localmapping profile] %ld keyframes, host wall us per keyframe: "
-              "ProcessNewKeyFrame+MapPointCulling %.1f, SearchInNeighbors %.1f (Fuse launches "
+              "ProcessNewKeyFrame+MapPointCulling %.1f, CreateNewMapPoints + SearchInNeighbors %.1f "
+              "(CreateNewMapPoints %.1f, Fuse launches "
               "%.1f), LocalBundleAdjustment %.1f (solve %.1f), KeyFrameCulling %.1f, final sync "
               "%.1f, LocalMapping total %.1f; CreateNewKeyFrame with all of it %.1f\n", mstats_.n_lm,
               mstats_.pnk_us / n,
-              mstats_.sin_us / n, mstats_.fuse_us / n, mstats_.ba_us / n,
+              mstats_.sin_us / n, mstats_.cnmp_us / n, mstats_.fuse_us / n, mstats_.ba_us / n,
               mstats_.basolve_us / n, mstats_.cull_us / n, mstats_.lmsync_us / n,
               mstats_.lm_us / n, mstats_.kfnew_us / n);
       static const char* bn[MappingStats::kBlk] = {
