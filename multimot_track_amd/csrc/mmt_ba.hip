@@ -327,7 +327,10 @@ struct BAWork2 {
   int* eopt;        // n_edge: the edge's optimised-keyframe index, -1 for a fixed keyframe
   uint8_t* kf_act;  // n_kf: optimised keyframe with an active edge this round
   uint8_t* pt_act;  // n_pt
-  int gP;           // point workgroups
+  int gP;           // partial sums: point workgroups + heavy-point workgroups
+  int gPp;          // point workgroups (one thread per point)
+  const int* heavy; // the points with more than kBaHeavy edges, one wave each
+  int n_heavy;
   int spec;         // k_ba2_p4<true>: the trial kernel linearises at the trial state
 };
 
@@ -454,14 +457,123 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_init(BADesc d, BAWork2 w) {
   }
 }
 
+// Points with more edges than this are linearised and tried by a wave each (lane = edge) instead
+// of one thread: a point seen from far away by every keyframe (a key at disparity 0 has depth
+// bf / 0 = inf, and CreateNewMapPoints triangulates such keys into far points) collects a hundred
+// or more edges, and its thread's serial edge loop set k_ba2_lin / k_ba2_p4 at 100-160 us.
+constexpr int kBaHeavy = 24;
+
+__device__ __forceinline__ bool ba2_heavy(const BADesc& d, int j) {
+  return d.pt_start[j + 1] - d.pt_start[j] > kBaHeavy;
+}
+
+// one active edge e of the point at X: its error (stored), robust rho (returned: r0), H_pl and the
+// pose terms (stored for an edge to an optimised keyframe), and its share of the point's H_ll
+// (acc9) and b_l (g3)
+__device__ __forceinline__ double ba2_lin_edge(const BADesc& d, const BAWork2& w, int e,
+                                               const DSE3* pose, const double (&X)[3], bool robust,
+                                               double* Hpl_b, double* Hpe_b, double (&acc9)[9],
+                                               double (&g3)[3]) {
+  const Cam cam = ba_cam(d);
+  const double dMono = huber_mono(), dStereo = huber_stereo();
+  const int k = d.e_kf[e];
+  const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
+  const double s = (double)d.e_s[e];
+  double er[3];
+  const double c = edge_error(d.e_obs + 3 * (size_t)e, s, stereo, pose[k], X, cam, er);
+#pragma unroll
+  for (int r = 0; r < 3; r++) w.err[3 * (size_t)e + r] = er[r];
+  double r0 = c, r1 = 1.0;
+  if (robust) huber_rho(c, stereo ? dStereo : dMono, r0, r1);
+  double Jp[3][6], Jl[3][3];
+  edge_jac<true>(stereo, pose[k], X, cam, Jp, Jl);
+  const int rows = stereo ? 3 : 2;
+  const double wt = r1 * s;
+  double om[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) om[r] = r < rows ? -(s * er[r]) * r1 : 0.0;
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+      double acc = 0;
+      _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) acc += Jl[r][a] * wt * Jl[r][b];
+      acc9[3 * a + b] = acc;
+    }
+    double g = 0;
+    _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) g += Jl[r][a] * om[r];
+    g3[a] = g;
+  }
+  if (d.opt_of[k] >= 0) {
+    double* hpl = &Hpl_b[18 * (size_t)e];
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+      for (int b = 0; b < 3; b++) {
+        double acc = 0;
+        _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) acc += Jp[r][a] * wt * Jl[r][b];
+        hpl[3 * a + b] = acc;
+      }
+    double* hpe = &Hpe_b[27 * (size_t)e];
+    int q = 0;
+#pragma unroll
+    for (int r0i = 0; r0i < 6; r0i++)
+#pragma unroll
+      for (int c0 = r0i; c0 < 6; c0++) {
+        double v = 0;
+        _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) v += Jp[r][r0i] * wt * Jp[r][c0];
+        hpe[q++] = v;
+      }
+#pragma unroll
+    for (int r0i = 0; r0i < 6; r0i++) {
+      double g = 0;
+      _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) g += Jp[r][r0i] * (-(s * er[r]) * r1);
+      hpe[21 + r0i] = g;
+    }
+  }
+  return r0;
+}
+
+// the trial error of active edge e at (pose, X) (stored) and its robust rho
+__device__ __forceinline__ double ba2_trial_edge(const BADesc& d, const BAWork2& w, int e,
+                                                 const DSE3* tri, const double (&X)[3],
+                                                 bool robust) {
+  const Cam cam = ba_cam(d);
+  const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
+  const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], stereo, tri[d.e_kf[e]],
+                              X, cam, &w.err[3 * (size_t)e]);
+  double r0 = c, r1;
+  if (robust) huber_rho(c, stereo ? huber_stereo() : huber_mono(), r0, r1);
+  return r0;
+}
+
+// A heavy point's wave: lane l takes edge e0 + l of each 64-edge chunk, stages its shares in the
+// wave's LDS rows, and every lane then adds them up in edge order (uniform broadcast reads): the
+// point's H_ll, b_l and chi2 carry the one-thread loop's bits.  K values per edge.
+template <int K>
+__device__ __forceinline__ void ba2_wave_ordered_add(double* sh, int lane, int n, const bool valid,
+                                                     const double (&v)[K], double (&sum)[K]) {
+#pragma unroll
+  for (int q = 0; q < K; q++) sh[K * lane + q] = valid ? v[q] : 0.0;
+  const unsigned long long vb = __ballot(valid);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int k = 0; k < n; k++) {
+    if (!((vb >> k) & 1ull)) continue;  // an inactive edge adds nothing (skipped, as the loop does)
+#pragma unroll
+    for (int q = 0; q < K; q++) sum[q] += sh[K * k + q];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // computeActiveErrors + activeRobustChi2 + buildSystem's point side for point j at (pose, X):
 // its active edges' errors (stored), robust chi2 (returned), H_ll and b_l of the point, H_pl and
 // the pose terms of each edge, into linearisation buffer `lb`; *mx = the largest H_ll diagonal
 __device__ __forceinline__ double ba2_lin_point(const BADesc& d, const BAWork2& w, int j,
                                                const DSE3* pose, const double (&X)[3], bool robust,
                                                int lb, double* mx) {
-  const Cam cam = ba_cam(d);
-  const double dMono = huber_mono(), dStereo = huber_stereo();
   double* Hpl_b = w.Hpl + (size_t)lb * 18 * d.n_edge;
   double* Hpe_b = w.Hpe + (size_t)lb * 27 * d.n_edge;
   double chi = 0;
@@ -469,62 +581,12 @@ __device__ __forceinline__ double ba2_lin_point(const BADesc& d, const BAWork2& 
     double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b3[3] = {0, 0, 0};
     for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
       if (w.level[e]) continue;
-      const int k = d.e_kf[e];
-      const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
-      const double s = (double)d.e_s[e];
-      double er[3];
-      const double c = edge_error(d.e_obs + 3 * (size_t)e, s, stereo, pose[k], X, cam, er);
+      double acc9[9], g3[3];
+      chi += ba2_lin_edge(d, w, e, pose, X, robust, Hpl_b, Hpe_b, acc9, g3);
 #pragma unroll
-      for (int r = 0; r < 3; r++) w.err[3 * (size_t)e + r] = er[r];
-      double r0 = c, r1 = 1.0;
-      if (robust) huber_rho(c, stereo ? dStereo : dMono, r0, r1);
-      chi += r0;
-      double Jp[3][6], Jl[3][3];
-      edge_jac<true>(stereo, pose[k], X, cam, Jp, Jl);
-      const int rows = stereo ? 3 : 2;
-      const double wt = r1 * s;
-      double om[3];
+      for (int q = 0; q < 9; q++) hl[q] += acc9[q];
 #pragma unroll
-      for (int r = 0; r < 3; r++) om[r] = r < rows ? -(s * er[r]) * r1 : 0.0;
-#pragma unroll
-      for (int a = 0; a < 3; a++) {
-#pragma unroll
-        for (int b = 0; b < 3; b++) {
-          double acc = 0;
-          _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) acc += Jl[r][a] * wt * Jl[r][b];
-          hl[3 * a + b] += acc;
-        }
-        double g = 0;
-        _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) g += Jl[r][a] * om[r];
-        b3[a] += g;
-      }
-      if (d.opt_of[k] >= 0) {
-        double* hpl = &Hpl_b[18 * (size_t)e];
-#pragma unroll
-        for (int a = 0; a < 6; a++)
-#pragma unroll
-          for (int b = 0; b < 3; b++) {
-            double acc = 0;
-            _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) acc += Jp[r][a] * wt * Jl[r][b];
-            hpl[3 * a + b] = acc;
-          }
-        double* hpe = &Hpe_b[27 * (size_t)e];
-        int q = 0;
-#pragma unroll
-        for (int r0 = 0; r0 < 6; r0++)
-#pragma unroll
-          for (int c0 = r0; c0 < 6; c0++) {
-            double v = 0;
-            _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) v += Jp[r][r0] * wt * Jp[r][c0];
-            hpe[q++] = v;
-          }
-#pragma unroll
-        for (int r0 = 0; r0 < 6; r0++) {
-          double g = 0;
-          _Pragma("unroll") for (int r = 0; r < 3; r++) if (r < rows) g += Jp[r][r0] * (-(s * er[r]) * r1);
-          hpe[21 + r0] = g;
-        }
-      }
+      for (int a = 0; a < 3; a++) b3[a] += g3[a];
     }
     double* Hll_b = w.Hll + (size_t)lb * 9 * d.n_pt;
     double* bl_b = w.bl + (size_t)lb * 3 * d.n_pt;
@@ -537,6 +599,42 @@ __device__ __forceinline__ double ba2_lin_point(const BADesc& d, const BAWork2& 
   return chi;
 }
 
+// ba2_lin_point by the wave of a heavy point (every lane returns the point's chi2 and *mx; sh: the
+// wave's 64 x 13 LDS staging rows)
+__device__ __forceinline__ double ba2_lin_point_wave(const BADesc& d, const BAWork2& w, int j,
+                                                    const DSE3* pose, const double (&X)[3],
+                                                    bool robust, int lb, double* mx, double* sh) {
+  const int lane = threadIdx.x & 63;
+  double* Hpl_b = w.Hpl + (size_t)lb * 18 * d.n_edge;
+  double* Hpe_b = w.Hpe + (size_t)lb * 27 * d.n_edge;
+  double sum[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // chi2, H_ll (9), b_l (3)
+  const int e1 = d.pt_start[j + 1];
+  for (int e0 = d.pt_start[j]; e0 < e1; e0 += 64) {
+    const int e = e0 + lane;
+    const bool valid = e < e1 && !w.level[e];
+    double v[13];
+    if (valid) {
+      double acc9[9], g3[3];
+      v[0] = ba2_lin_edge(d, w, e, pose, X, robust, Hpl_b, Hpe_b, acc9, g3);
+#pragma unroll
+      for (int q = 0; q < 9; q++) v[1 + q] = acc9[q];
+#pragma unroll
+      for (int q = 0; q < 3; q++) v[10 + q] = g3[q];
+    }
+    ba2_wave_ordered_add<13>(sh, lane, min(64, e1 - e0), valid, v, sum);
+  }
+  if (lane == 0) {
+    double* Hll_b = w.Hll + (size_t)lb * 9 * d.n_pt;
+    double* bl_b = w.bl + (size_t)lb * 3 * d.n_pt;
+#pragma unroll
+    for (int q = 0; q < 9; q++) Hll_b[9 * (size_t)j + q] = sum[1 + q];
+#pragma unroll
+    for (int q = 0; q < 3; q++) bl_b[3 * (size_t)j + q] = sum[10 + q];
+  }
+  *mx = fmax(fabs(sum[1]), fmax(fabs(sum[5]), fabs(sum[9])));
+  return sum[0];
+}
+
 // the linearisation at the current estimate, one thread per point (the start of each round, and an
 // iteration that follows a rejected trial; after an accepted one k_ba2_p4 has linearised already)
 __global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
@@ -547,13 +645,29 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
   const int cb = st->cb;
   const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
   const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
-  const int j = blockIdx.x * kMkThreads + threadIdx.x;
   double chi = 0, mx = 0;
-  if (j < d.n_pt) {
-    const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
-    double m = 0;
-    chi = ba2_lin_point(d, w, j, pose, X, robust, cb, &m);
-    if (w.pt_act[j]) mx = m;
+  if ((int)blockIdx.x < w.gPp) {  // one thread per point (the heavy ones are the waves' below)
+    const int j = blockIdx.x * kMkThreads + threadIdx.x;
+    if (j < d.n_pt && !ba2_heavy(d, j)) {
+      const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
+      double m = 0;
+      chi = ba2_lin_point(d, w, j, pose, X, robust, cb, &m);
+      if (w.pt_act[j]) mx = m;
+    }
+  } else {
+    __shared__ double s_stage[kMkWaves][64 * 13];
+    const int wave = threadIdx.x >> 6;
+    const int hi = ((int)blockIdx.x - w.gPp) * kMkWaves + wave;
+    if (hi < w.n_heavy) {
+      const int j = w.heavy[hi];
+      const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
+      double m = 0;
+      const double c = ba2_lin_point_wave(d, w, j, pose, X, robust, cb, &m, s_stage[wave]);
+      if ((threadIdx.x & 63) == 0) {
+        chi = c;
+        if (w.pt_act[j]) mx = m;
+      }
+    }
   }
   const double cs = wave_sum_dpp(chi);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1085,12 +1199,11 @@ __device__ void ba2_decide(const BADesc& d, const BAWork2& w) {
   }
 }
 
-// trial step 4, one thread per point: x_l = D^-1 (b_l - H_pl^T x_p) (stale on a failed solve),
-// the trial point, the errors of its active edges at the trial state, chi2 and the scale term
-// SPEC (MMT_BA_SPEC=1): also linearise at the trial state, so an accepted trial needs no
-// k_ba2_lin; measured slower (the linearisation's registers slow every trial more than the launch
-// it saves), off by default
-template <bool SPEC>
+// trial step 4, one thread per point (a wave per heavy point): x_l = D^-1 (b_l - H_pl^T x_p) (stale
+// on a failed solve), the trial point, the errors of its active edges at the trial state, chi2 and
+// the scale term.  (Linearising at the trial state here as well, so that an accepted trial needs no
+// k_ba2_lin, measured slower in round 5: its registers slowed every trial more than the launch it
+// saved.)
 __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
   __shared__ double s_part[2 * kMkWaves];
   __shared__ int s_last;
@@ -1105,7 +1218,16 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
   double* Xt = w.X + (size_t)nb * 3 * d.n_pt;
   const double* bl_c = w.bl + (size_t)cb * 3 * d.n_pt;
   const double* Hpl_c = w.Hpl + (size_t)cb * 18 * d.n_edge;
-  const int j = blockIdx.x * kMkThreads + threadIdx.x;
+  __shared__ double s_stage[kMkWaves][64];
+  const bool heavy_wg = (int)blockIdx.x >= w.gPp;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int j = blockIdx.x * kMkThreads + threadIdx.x;
+  if (heavy_wg) {  // a wave per heavy point: every lane runs the point's increment (uniform)
+    const int hi = ((int)blockIdx.x - w.gPp) * kMkWaves + wave;
+    j = hi < w.n_heavy ? w.heavy[hi] : d.n_pt;
+  } else if (j < d.n_pt && ba2_heavy(d, j)) {
+    j = d.n_pt;  // the heavy point's wave does it
+  }
   double chi = 0, sc = 0;
   if (j < d.n_pt) {
     double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
@@ -1146,30 +1268,29 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
         sc += xv * (lambda * xv + bl3[r]);
         X[r] += xv;
       }
-      if (SPEC) {
-        // the trial's errors and chi2, and the linearisation at the trial state (the next
-        // iteration's system if the trial is accepted) into the other buffer
-        double m;
-        chi = ba2_lin_point(d, w, j, tri, X, robust, nb, &m);
-      } else {  // the trial's errors and chi2
-        const Cam cam = ba_cam(d);
-        const double dMono = huber_mono(), dStereo = huber_stereo();
-        for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
-          if (w.level[e]) continue;
-          const bool stereo = !(d.e_obs[3 * (size_t)e + 2] < 0);
-          const double c = edge_error(d.e_obs + 3 * (size_t)e, (double)d.e_s[e], stereo,
-                                      tri[d.e_kf[e]], X, cam, &w.err[3 * (size_t)e]);
-          double r0 = c, r1;
-          if (robust) huber_rho(c, stereo ? dStereo : dMono, r0, r1);
-          chi += r0;
+      if (!heavy_wg) {  // the trial's errors and chi2
+        for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++)
+          if (!w.level[e]) chi += ba2_trial_edge(d, w, e, tri, X, robust);
+      } else {  // the same by the point's wave, added in edge order
+        double sum[1] = {0};
+        const int e1 = d.pt_start[j + 1];
+        for (int e0 = d.pt_start[j]; e0 < e1; e0 += 64) {
+          const int e = e0 + lane;
+          const bool valid = e < e1 && !w.level[e];
+          double v[1] = {0};
+          if (valid) v[0] = ba2_trial_edge(d, w, e, tri, X, robust);
+          ba2_wave_ordered_add<1>(s_stage[wave], lane, min(64, e1 - e0), valid, v, sum);
         }
+        chi = sum[0];
       }
     }
+    if (!heavy_wg || lane == 0) {
 #pragma unroll
-    for (int r = 0; r < 3; r++) Xt[3 * (size_t)j + r] = X[r];
+      for (int r = 0; r < 3; r++) Xt[3 * (size_t)j + r] = X[r];
+    }
+    if (heavy_wg && lane != 0) chi = sc = 0;  // the point counts once
   }
   const double a = wave_sum_dpp(chi), b = wave_sum_dpp(sc);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
     s_part[2 * wave] = a;
     s_part[2 * wave + 1] = b;
@@ -1368,6 +1489,11 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
       bitem.push_back(make_int4((int)bk, t, std::min(t + 256, blk_start[bk + 1]), 0));
     bitem_start.push_back((int)bitem.size());
   }
+  // the heavy points (more than kBaHeavy edges): a wave each, in the point kernels' workgroups
+  // after the thread-per-point ones
+  std::vector<int> heavy;
+  for (int j = 0; j < nP; j++)
+    if (pt_start[j + 1] - pt_start[j] > kBaHeavy) heavy.push_back(j);
   struct Seg {
     size_t bytes;
     const void* src;
@@ -1380,7 +1506,8 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
                       {4 * kf_edges.size(), kf_edges.data()}, {4 * blk_ab.size(), blk_ab.data()},
                       {4 * blk_start.size(), blk_start.data()}, {8 * trip.size(), trip.data()},
                       {16 * kitem.size(), kitem.data()}, {4 * kitem_start.size(), kitem_start.data()},
-                      {16 * bitem.size(), bitem.data()}, {4 * bitem_start.size(), bitem_start.data()}};
+                      {16 * bitem.size(), bitem.data()}, {4 * bitem_start.size(), bitem_start.data()},
+                      {4 * heavy.size(), heavy.data()}};
   constexpr int nseg = sizeof(segs) / sizeof(segs[0]);
   size_t off[nseg], tot = 0;
   for (int i = 0; i < nseg; i++) {
@@ -1430,7 +1557,9 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
   d.erase = d_dn_ + o_er;
   d.stats = (int*)(d_dn_ + o_st);
   {
-    const int gP = std::max(1, (nP + kMkThreads - 1) / kMkThreads);
+    const int gPp = std::max(1, (nP + kMkThreads - 1) / kMkThreads);
+    const int gH = ((int)heavy.size() + kMkWaves - 1) / kMkWaves;
+    const int gP = gPp + gH;
     const int n6 = 6 * nO, nblk = nblocks;
     const size_t wsb2 = ba2_workspace_bytes(nK, nP, nE, nO, nblk, gP) +
                         8 * (27 + 6) * kitem.size() + 8 * 36 * bitem.size() + 64 * 3;
@@ -1483,11 +1612,14 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.kf_act = take((size_t)nK);
     w.pt_act = take((size_t)nP);
     w.gP = gP;
+    w.gPp = gPp;
+    w.heavy = (const int*)(u + off[18]);
+    w.n_heavy = (int)heavy.size();
     w.spec = 0;  // k_ba2_lin linearises every trial (the trial kernel's own linearisation,
                  // k_ba2_p4<true>, measured 1,509 against 1,549 us per BA but spills)
     const double tp1 = hp.on ? ba_now_us() : 0;
     double t_launch = 0, t_wait = 0;
-    hipLaunchKernelGGL(k_ba2_init, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+    hipLaunchKernelGGL(k_ba2_init, dim3(gPp), dim3(kMkThreads), 0, st, d, w);
     MMT_HIP(hipGetLastError());
     // A trial is at most 6 launches; a solve at most 5 x 10 + 10 x 10 trials.  The first batch
     // covers a typical solve (about 15 trials on the C3 sequence), later ones are short.
@@ -1501,11 +1633,11 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
         hipLaunchKernelGGL(k_ba2_lin, dim3(gP), dim3(kMkThreads), 0, st, d, w);
         if (w.n_kitem > 0)
           hipLaunchKernelGGL(k_ba2_kfsum, dim3(w.n_kitem), dim3(kMkThreads), 0, st, d, w);
-        hipLaunchKernelGGL(k_ba2_p1, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p1, dim3(gPp), dim3(kMkThreads), 0, st, d, w);
         if (w.n_bitem + w.n_kitem > 0)
           hipLaunchKernelGGL(k_ba2_p2, dim3(w.n_bitem + w.n_kitem), dim3(kMkThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p3, dim3(1), dim3(kMkSolveThreads), 0, st, d, w);
-        hipLaunchKernelGGL(k_ba2_p4<false>, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p4, dim3(gP), dim3(kMkThreads), 0, st, d, w);
       }
       MMT_HIP(hipGetLastError());
       slots += batch;

@@ -12,6 +12,7 @@
 // its vocabulary node in keyframe 2): the descriptor distances, the epipole test for mono pairs
 // and CheckDistEpipolarLine in float in the reference's operation order (-ffp-contract=off).
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <fstream>
@@ -144,26 +145,37 @@ void Vocabulary::build(const uint32_t* word, const double* w, const uint32_t* no
   fv.feat.clear();
   if (empty()) return;
   const bool add = weighting == 0 || weighting == 1;
-  std::vector<std::vector<int>> fl;
+  // features by (word, feature) and by (node, feature): a word's weights are then added in feature
+  // order and a node's features listed in feature order, as the map insertions of the reference do
+  std::vector<uint64_t> kw, kn;
+  kw.reserve(n);
+  kn.reserve(n);
   for (int i = 0; i < n; i++) {
     if (!(w[i] > 0)) continue;
-    const uint32_t id = word[i];
-    const size_t p = (size_t)(std::lower_bound(v.word.begin(), v.word.end(), id) - v.word.begin());
-    if (p < v.word.size() && v.word[p] == id) {
-      if (add) v.value[p] += w[i];
+    kw.push_back(((uint64_t)word[i] << 32) | (uint32_t)i);
+    kn.push_back(((uint64_t)node[i] << 32) | (uint32_t)i);
+  }
+  std::sort(kw.begin(), kw.end());
+  std::sort(kn.begin(), kn.end());
+  for (size_t k = 0; k < kw.size(); k++) {
+    const uint32_t id = (uint32_t)(kw[k] >> 32);
+    const double x = w[(uint32_t)kw[k]];
+    if (!v.word.empty() && v.word.back() == id) {
+      if (add) v.value.back() += x;
     } else {
-      v.word.insert(v.word.begin() + p, id);
-      v.value.insert(v.value.begin() + p, w[i]);
-    }
-    const uint32_t nid = node[i];
-    const size_t q = (size_t)(std::lower_bound(fv.node.begin(), fv.node.end(), nid) - fv.node.begin());
-    if (q < fv.node.size() && fv.node[q] == nid) {
-      fl[q].push_back(i);
-    } else {
-      fv.node.insert(fv.node.begin() + q, nid);
-      fl.insert(fl.begin() + q, std::vector<int>{i});
+      v.word.push_back(id);
+      v.value.push_back(x);
     }
   }
+  for (size_t k = 0; k < kn.size(); k++) {
+    const uint32_t nid = (uint32_t)(kn[k] >> 32);
+    if (fv.node.empty() || fv.node.back() != nid) {
+      if (!fv.node.empty()) fv.start.push_back((int)fv.feat.size());
+      fv.node.push_back(nid);
+    }
+    fv.feat.push_back((int)(uint32_t)kn[k]);
+  }
+  if (!fv.node.empty()) fv.start.push_back((int)fv.feat.size());
   double norm = 0.0;
   if (scoring != 1) {
     for (double x : v.value) norm += std::fabs(x);
@@ -173,10 +185,6 @@ void Vocabulary::build(const uint32_t* word, const double* w, const uint32_t* no
   }
   if (norm > 0.0)
     for (double& x : v.value) x /= norm;
-  for (const auto& l : fl) {
-    fv.feat.insert(fv.feat.end(), l.begin(), l.end());
-    fv.start.push_back((int)fv.feat.size());
-  }
 }
 
 double Vocabulary::score(const BowVecH& a, const BowVecH& b) const {
