@@ -327,10 +327,11 @@ struct BAWork2 {
   int* eopt;        // n_edge: the edge's optimised-keyframe index, -1 for a fixed keyframe
   uint8_t* kf_act;  // n_kf: optimised keyframe with an active edge this round
   uint8_t* pt_act;  // n_pt
-  int gP;           // partial sums: point workgroups + heavy-point workgroups
-  int gPp;          // point workgroups (one thread per point)
+  int gP;           // partial sums: one per point workgroup
+  int gPp;          // point workgroups (one thread per point; k_ba2_p1's heavy waves follow them)
   const int* heavy; // the points with more than kBaHeavy edges, one wave each
   int n_heavy;
+  double* hres;     // 2 n_pt: a heavy point's (chi2, H_ll diagonal max) or (trial chi2, scale)
   int spec;         // k_ba2_p4<true>: the trial kernel linearises at the trial state
 };
 
@@ -457,11 +458,11 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_init(BADesc d, BAWork2 w) {
   }
 }
 
-// Points with more edges than this are linearised and tried by a wave each (lane = edge) instead
-// of one thread: a point seen from far away by every keyframe (a key at disparity 0 has depth
+// Points with more edges than this are linearised, solved and tried by a wave each (lane = edge)
+// instead of one thread: a point seen from far away by every keyframe (a key at disparity 0 has depth
 // bf / 0 = inf, and CreateNewMapPoints triangulates such keys into far points) collects a hundred
 // or more edges, and its thread's serial edge loop set k_ba2_lin / k_ba2_p4 at 100-160 us.
-constexpr int kBaHeavy = 24;
+constexpr int kBaHeavy = 8;
 
 __device__ __forceinline__ bool ba2_heavy(const BADesc& d, int j) {
   return d.pt_start[j + 1] - d.pt_start[j] > kBaHeavy;
@@ -645,29 +646,18 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
   const int cb = st->cb;
   const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
   const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
+  const int j = blockIdx.x * kMkThreads + threadIdx.x;
   double chi = 0, mx = 0;
-  if ((int)blockIdx.x < w.gPp) {  // one thread per point (the heavy ones are the waves' below)
-    const int j = blockIdx.x * kMkThreads + threadIdx.x;
-    if (j < d.n_pt && !ba2_heavy(d, j)) {
+  if (j < d.n_pt) {
+    double m = 0;
+    if (ba2_heavy(d, j)) {  // linearised by its wave in k_ba2_lin_heavy: its results
+      chi = w.hres[2 * (size_t)j];
+      m = w.hres[2 * (size_t)j + 1];
+    } else {
       const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
-      double m = 0;
       chi = ba2_lin_point(d, w, j, pose, X, robust, cb, &m);
-      if (w.pt_act[j]) mx = m;
     }
-  } else {
-    __shared__ double s_stage[kMkWaves][64 * 13];
-    const int wave = threadIdx.x >> 6;
-    const int hi = ((int)blockIdx.x - w.gPp) * kMkWaves + wave;
-    if (hi < w.n_heavy) {
-      const int j = w.heavy[hi];
-      const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
-      double m = 0;
-      const double c = ba2_lin_point_wave(d, w, j, pose, X, robust, cb, &m, s_stage[wave]);
-      if ((threadIdx.x & 63) == 0) {
-        chi = c;
-        if (w.pt_act[j]) mx = m;
-      }
-    }
+    if (w.pt_act[j]) mx = m;
   }
   const double cs = wave_sum_dpp(chi);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -679,6 +669,29 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_lin(BADesc d, BAWork2 w) {
     for (int q = 0; q < kMkWaves; q++) t += s_part[q];
     w.linpart[2 * blockIdx.x] = t;
     w.linpart[2 * blockIdx.x + 1] = m;
+  }
+}
+
+// the heavy points' linearisation, a wave each, before k_ba2_lin (which takes their chi2 and
+// H_ll diagonal maximum from hres into its sums at the point's own place: the sums' order is the
+// one-thread-per-point kernel's)
+__global__ __launch_bounds__(kMkThreads) void k_ba2_lin_heavy(BADesc d, BAWork2 w) {
+  __shared__ double s_stage[kMkWaves][64 * 13];
+  const BAState* st = w.st;
+  if (st->done || !st->need_lin || st->spec_ok) return;
+  const int wave = threadIdx.x >> 6;
+  const int hi = (int)blockIdx.x * kMkWaves + wave;
+  if (hi >= w.n_heavy) return;
+  const int cb = st->cb;
+  const DSE3* pose = w.pose + (size_t)cb * d.n_kf;
+  const double* Xc = w.X + (size_t)cb * 3 * d.n_pt;
+  const int j = w.heavy[hi];
+  const double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
+  double m = 0;
+  const double c = ba2_lin_point_wave(d, w, j, pose, X, st->round == 0, cb, &m, s_stage[wave]);
+  if ((threadIdx.x & 63) == 0) {
+    w.hres[2 * (size_t)j] = c;
+    w.hres[2 * (size_t)j + 1] = m;
   }
 }
 
@@ -713,7 +726,15 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p1(BADesc d, BAWork2 w) {
   if (st->done) return;
   __shared__ double s_lam;
   const double lambda = st->lam_init ? ba2_lambda_init(d, w, &s_lam) : st->lambda;
-  const int j = blockIdx.x * kMkThreads + threadIdx.x;
+  const bool heavy_wg = (int)blockIdx.x >= w.gPp;
+  const int lane = threadIdx.x & 63;
+  int j = blockIdx.x * kMkThreads + threadIdx.x;
+  if (heavy_wg) {  // a wave per heavy point, lanes over its edges (each edge's Y and cv alone)
+    const int hi = ((int)blockIdx.x - w.gPp) * kMkWaves + (int)(threadIdx.x >> 6);
+    j = hi < w.n_heavy ? w.heavy[hi] : d.n_pt;
+  } else if (j < d.n_pt && ba2_heavy(d, j)) {
+    return;
+  }
   if (j >= d.n_pt || !w.pt_act[j]) return;
   const int cb = st->cb;
   const double* Hll_c = w.Hll + (size_t)cb * 9 * d.n_pt;
@@ -723,13 +744,16 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p1(BADesc d, BAWork2 w) {
 #pragma unroll
   for (int q = 0; q < 9; q++) Dm[q] = Hll_c[9 * (size_t)j + q] + ((q % 4) == 0 ? lambda : 0.0);
   inverse3(Dm, Di);
+  if (!heavy_wg || lane == 0) {
 #pragma unroll
-  for (int q = 0; q < 9; q++) w.Dinv[9 * (size_t)j + q] = Di[q];
+    for (int q = 0; q < 9; q++) w.Dinv[9 * (size_t)j + q] = Di[q];
+  }
   const double* b3 = &bl_c[3 * (size_t)j];
   double db[3];
 #pragma unroll
   for (int a = 0; a < 3; a++) db[a] = Di[3 * a] * b3[0] + Di[3 * a + 1] * b3[1] + Di[3 * a + 2] * b3[2];
-  for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
+  const int eb = d.pt_start[j] + (heavy_wg ? lane : 0), es = heavy_wg ? 64 : 1;
+  for (int e = eb; e < d.pt_start[j + 1]; e += es) {
     if (w.level[e] || w.eopt[e] < 0) continue;
     const double* B = &Hpl_c[18 * (size_t)e];
     double* Ye = &w.Y[18 * (size_t)e];
@@ -1204,11 +1228,13 @@ __device__ void ba2_decide(const BADesc& d, const BAWork2& w) {
 // the scale term.  (Linearising at the trial state here as well, so that an accepted trial needs no
 // k_ba2_lin, measured slower in round 5: its registers slowed every trial more than the launch it
 // saved.)
-__global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
-  __shared__ double s_part[2 * kMkWaves];
-  __shared__ int s_last;
+// point j's trial: x_l, the trial point (stored to Xt), its active edges' trial errors (stored),
+// chi2 and the scale term.  WAVE: the heavy point's wave (every lane returns the same values;
+// edges 64 at a time, the chi2 added in edge order from the staging row sh)
+template <bool WAVE>
+__device__ __forceinline__ void ba2_trial_point(const BADesc& d, const BAWork2& w, int j,
+                                                double* sh, double* chi_out, double* sc_out) {
   const BAState* st = w.st;
-  if (st->done) return;
   const int cb = st->cb, nb = 1 - cb;
   const bool ok2 = st->ok2 != 0, robust = st->round == 0;
   const double lambda = st->lambda;
@@ -1218,77 +1244,121 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
   double* Xt = w.X + (size_t)nb * 3 * d.n_pt;
   const double* bl_c = w.bl + (size_t)cb * 3 * d.n_pt;
   const double* Hpl_c = w.Hpl + (size_t)cb * 18 * d.n_edge;
-  __shared__ double s_stage[kMkWaves][64];
-  const bool heavy_wg = (int)blockIdx.x >= w.gPp;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int j = blockIdx.x * kMkThreads + threadIdx.x;
-  if (heavy_wg) {  // a wave per heavy point: every lane runs the point's increment (uniform)
-    const int hi = ((int)blockIdx.x - w.gPp) * kMkWaves + wave;
-    j = hi < w.n_heavy ? w.heavy[hi] : d.n_pt;
-  } else if (j < d.n_pt && ba2_heavy(d, j)) {
-    j = d.n_pt;  // the heavy point's wave does it
-  }
+  const int lane = threadIdx.x & 63;
   double chi = 0, sc = 0;
-  if (j < d.n_pt) {
-    double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
-    if (w.pt_act[j]) {
-      double* xl = &w.x[n6 + 3 * (size_t)j];
-      const double bl3[3] = {bl_c[3 * (size_t)j], bl_c[3 * (size_t)j + 1], bl_c[3 * (size_t)j + 2]};
-      double xv3[3];  // the increment, kept in registers (no read-back of the store)
-      if (ok2) {
-        // the loads that depend on j alone first (D^-1); an edge's H_pl block only for the edges
-        // of the level to an optimised keyframe (ba2_lin_point writes no block for the others)
-        double Di[9];
+  double X[3] = {Xc[3 * (size_t)j], Xc[3 * (size_t)j + 1], Xc[3 * (size_t)j + 2]};
+  if (w.pt_act[j]) {
+    double* xl = &w.x[n6 + 3 * (size_t)j];
+    const double bl3[3] = {bl_c[3 * (size_t)j], bl_c[3 * (size_t)j + 1], bl_c[3 * (size_t)j + 2]};
+    double xv3[3];  // the increment, kept in registers (no read-back of the store)
+    if (ok2) {
+      // the loads that depend on j alone first (D^-1); an edge's H_pl block only for the edges
+      // of the level to an optimised keyframe (ba2_lin_point writes no block for the others)
+      double Di[9];
 #pragma unroll
-        for (int q = 0; q < 9; q++) Di[q] = w.Dinv[9 * (size_t)j + q];
-        double cl[3] = {bl3[0], bl3[1], bl3[2]};
+      for (int q = 0; q < 9; q++) Di[q] = w.Dinv[9 * (size_t)j + q];
+      double cl[3] = {bl3[0], bl3[1], bl3[2]};
+      auto add_edge = [&](int e, int a) {
+        double B[18];
+#pragma unroll
+        for (int q = 0; q < 18; q++) B[q] = Hpl_c[18 * (size_t)e + q];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+#pragma unroll
+          for (int r = 0; r < 6; r++) cl[c] += B[3 * r + c] * (-w.x[6 * a + r]);
+      };
+      if (!WAVE) {
         for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++) {
           const int a = w.eopt[e];
           if (w.level[e] || a < 0) continue;
-          double B[18];
-#pragma unroll
-          for (int q = 0; q < 18; q++) B[q] = Hpl_c[18 * (size_t)e + q];
-#pragma unroll
-          for (int c = 0; c < 3; c++)
-#pragma unroll
-            for (int r = 0; r < 6; r++) cl[c] += B[3 * r + c] * (-w.x[6 * a + r]);
+          add_edge(e, a);
         }
-#pragma unroll
-        for (int a = 0; a < 3; a++) {
-          xv3[a] = Di[3 * a] * cl[0] + Di[3 * a + 1] * cl[1] + Di[3 * a + 2] * cl[2];
-          xl[a] = xv3[a];
-        }
-      } else {
-#pragma unroll
-        for (int a = 0; a < 3; a++) xv3[a] = xl[a];  // stale (g2o re-applies its _x)
-      }
-#pragma unroll
-      for (int r = 0; r < 3; r++) {
-        const double xv = xv3[r];
-        sc += xv * (lambda * xv + bl3[r]);
-        X[r] += xv;
-      }
-      if (!heavy_wg) {  // the trial's errors and chi2
-        for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++)
-          if (!w.level[e]) chi += ba2_trial_edge(d, w, e, tri, X, robust);
-      } else {  // the same by the point's wave, added in edge order
-        double sum[1] = {0};
+      } else {  // the active edges to optimised keyframes found 64 at a time, taken in edge order
         const int e1 = d.pt_start[j + 1];
         for (int e0 = d.pt_start[j]; e0 < e1; e0 += 64) {
           const int e = e0 + lane;
-          const bool valid = e < e1 && !w.level[e];
-          double v[1] = {0};
-          if (valid) v[0] = ba2_trial_edge(d, w, e, tri, X, robust);
-          ba2_wave_ordered_add<1>(s_stage[wave], lane, min(64, e1 - e0), valid, v, sum);
+          const bool take = e < e1 && !w.level[e] && w.eopt[e] >= 0;
+          unsigned long long m = __ballot(take);
+          while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            add_edge(e0 + k, w.eopt[e0 + k]);
+          }
         }
-        chi = sum[0];
       }
-    }
-    if (!heavy_wg || lane == 0) {
 #pragma unroll
-      for (int r = 0; r < 3; r++) Xt[3 * (size_t)j + r] = X[r];
+      for (int a = 0; a < 3; a++)
+        xv3[a] = Di[3 * a] * cl[0] + Di[3 * a + 1] * cl[1] + Di[3 * a + 2] * cl[2];
+      if (!WAVE || lane == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; a++) xl[a] = xv3[a];
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < 3; a++) xv3[a] = xl[a];  // stale (g2o re-applies its _x)
     }
-    if (heavy_wg && lane != 0) chi = sc = 0;  // the point counts once
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      const double xv = xv3[r];
+      sc += xv * (lambda * xv + bl3[r]);
+      X[r] += xv;
+    }
+    if (!WAVE) {  // the trial's errors and chi2
+      for (int e = d.pt_start[j]; e < d.pt_start[j + 1]; e++)
+        if (!w.level[e]) chi += ba2_trial_edge(d, w, e, tri, X, robust);
+    } else {
+      double sum[1] = {0};
+      const int e1 = d.pt_start[j + 1];
+      for (int e0 = d.pt_start[j]; e0 < e1; e0 += 64) {
+        const int e = e0 + lane;
+        const bool valid = e < e1 && !w.level[e];
+        double v[1] = {0};
+        if (valid) v[0] = ba2_trial_edge(d, w, e, tri, X, robust);
+        ba2_wave_ordered_add<1>(sh, lane, min(64, e1 - e0), valid, v, sum);
+      }
+      chi = sum[0];
+    }
+  }
+  if (!WAVE || lane == 0) {
+#pragma unroll
+    for (int r = 0; r < 3; r++) Xt[3 * (size_t)j + r] = X[r];
+  }
+  *chi_out = chi;
+  *sc_out = sc;
+}
+
+// the heavy points' trials, a wave each, before k_ba2_p4 (which adds their chi2 and scale terms
+// from hres at the point's own place)
+__global__ __launch_bounds__(kMkThreads) void k_ba2_p4_heavy(BADesc d, BAWork2 w) {
+  __shared__ double s_stage[kMkWaves][64];
+  if (w.st->done) return;
+  const int wave = threadIdx.x >> 6;
+  const int hi = (int)blockIdx.x * kMkWaves + wave;
+  if (hi >= w.n_heavy) return;
+  const int j = w.heavy[hi];
+  double chi, sc;
+  ba2_trial_point<true>(d, w, j, s_stage[wave], &chi, &sc);
+  if ((threadIdx.x & 63) == 0) {
+    w.hres[2 * (size_t)j] = chi;
+    w.hres[2 * (size_t)j + 1] = sc;
+  }
+}
+
+__global__ __launch_bounds__(kMkThreads) void k_ba2_p4(BADesc d, BAWork2 w) {
+  __shared__ double s_part[2 * kMkWaves];
+  __shared__ int s_last;
+  const BAState* st = w.st;
+  if (st->done) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * kMkThreads + threadIdx.x;
+  double chi = 0, sc = 0;
+  if (j < d.n_pt) {
+    if (ba2_heavy(d, j)) {  // tried by its wave in k_ba2_p4_heavy
+      chi = w.hres[2 * (size_t)j];
+      sc = w.hres[2 * (size_t)j + 1];
+    } else {
+      ba2_trial_point<false>(d, w, j, nullptr, &chi, &sc);
+    }
   }
   const double a = wave_sum_dpp(chi), b = wave_sum_dpp(sc);
   if (lane == 0) {
@@ -1559,10 +1629,11 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
   {
     const int gPp = std::max(1, (nP + kMkThreads - 1) / kMkThreads);
     const int gH = ((int)heavy.size() + kMkWaves - 1) / kMkWaves;
-    const int gP = gPp + gH;
+    const int gP = gPp;  // the partial sums: one per point workgroup
     const int n6 = 6 * nO, nblk = nblocks;
     const size_t wsb2 = ba2_workspace_bytes(nK, nP, nE, nO, nblk, gP) +
-                        8 * (27 + 6) * kitem.size() + 8 * 36 * bitem.size() + 64 * 3;
+                        8 * (27 + 6) * kitem.size() + 8 * 36 * bitem.size() + 16 * (size_t)nP +
+                        64 * 4;
     if (wsb2 > ws2_cap_ || !d_ws2_) {
       MMT_HIP(hipStreamSynchronize(st));
       if (d_ws2_) (void)hipFree(d_ws2_);
@@ -1615,6 +1686,7 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
     w.gPp = gPp;
     w.heavy = (const int*)(u + off[18]);
     w.n_heavy = (int)heavy.size();
+    w.hres = (double*)take(16 * (size_t)nP);
     w.spec = 0;  // k_ba2_lin linearises every trial (the trial kernel's own linearisation,
                  // k_ba2_p4<true>, measured 1,509 against 1,549 us per BA but spills)
     const double tp1 = hp.on ? ba_now_us() : 0;
@@ -1630,14 +1702,16 @@ void BARunner::run(const BAHostProblem& P, hipStream_t st, float* T_out, float* 
       const int batch = slots == 0 ? 15 : 4;
       const double tl = hp.on ? ba_now_us() : 0;
       for (int b = 0; b < batch; b++) {
-        hipLaunchKernelGGL(k_ba2_lin, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        if (gH > 0) hipLaunchKernelGGL(k_ba2_lin_heavy, dim3(gH), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_lin, dim3(gPp), dim3(kMkThreads), 0, st, d, w);
         if (w.n_kitem > 0)
           hipLaunchKernelGGL(k_ba2_kfsum, dim3(w.n_kitem), dim3(kMkThreads), 0, st, d, w);
-        hipLaunchKernelGGL(k_ba2_p1, dim3(gPp), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p1, dim3(gPp + gH), dim3(kMkThreads), 0, st, d, w);
         if (w.n_bitem + w.n_kitem > 0)
           hipLaunchKernelGGL(k_ba2_p2, dim3(w.n_bitem + w.n_kitem), dim3(kMkThreads), 0, st, d, w);
         hipLaunchKernelGGL(k_ba2_p3, dim3(1), dim3(kMkSolveThreads), 0, st, d, w);
-        hipLaunchKernelGGL(k_ba2_p4, dim3(gP), dim3(kMkThreads), 0, st, d, w);
+        if (gH > 0) hipLaunchKernelGGL(k_ba2_p4_heavy, dim3(gH), dim3(kMkThreads), 0, st, d, w);
+        hipLaunchKernelGGL(k_ba2_p4, dim3(gPp), dim3(kMkThreads), 0, st, d, w);
       }
       MMT_HIP(hipGetLastError());
       slots += batch;

@@ -149,7 +149,7 @@ struct MappingStats {
   // finer host wall times of the keyframe path (MMT_MAP_PROFILE; printed at destruction)
   double kfnew_us = 0, pnk_us = 0, sin_us = 0, basolve_us = 0, cull_us = 0, lmsync_us = 0;
   double cnmp_us = 0;  // CreateNewMapPoints (vocabulary path), inside sin_us
-  static constexpr int kBlk = 14;  // finer blocks of the keyframe path (names in ~MapEngine)
+  static constexpr int kBlk = 15;  // finer blocks of the keyframe path (names in ~MapEngine)
   double blk_us[kBlk] = {};
   long n_lm = 0;
 };

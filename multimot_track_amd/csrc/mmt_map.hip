@@ -86,7 +86,8 @@ MapEngine::~MapEngine() {
       static const char* bn[MappingStats::kBlk] = {
           "new keyframe + store", "new points", "SIN targets", "SIN fuse 1", "SIN candidates",
           "SIN fuse 2", "SIN point updates", "SIN connections", "BA graph", "BA apply",
-          "Fuse pool flush", "Fuse enqueue", "Fuse wait", "Fuse apply (+ relaunches)"};
+          "Fuse pool flush", "Fuse enqueue", "Fuse wait", "Fuse apply (+ relaunches)",
+          "ComputeDistinctiveDescriptors (inside the others)"};
       fprintf(stderr, "[mmt localmapping profile] per keyframe, us:");
       for (int k = 0; k < MappingStats::kBlk; k++)
         fprintf(stderr, " %s %.1f%s", bn[k], mstats_.blk_us[k] / n,
@@ -284,6 +285,13 @@ void MapEngine::set_bad(int h) {  // MapPoint::SetBadFlag
 void MapEngine::compute_distinctive(int h) {  // MapPoint::ComputeDistinctiveDescriptors
   MPoint& p = mp(h);
   if (p.bad || p.obs.empty()) return;
+  struct Timer {  // MMT_MAP_PROFILE: this function's share of the keyframe path
+    MapEngine* m;
+    double t;
+    ~Timer() {
+      if (m) m->mstats_.blk_us[14] += now_us() - t;
+    }
+  } timer{prof_on_ ? this : nullptr, prof_on_ ? now_us() : 0};
   // the descriptors of the good observing keyframes, their pairwise Hamming distances and each
   // one's median distance (the (N - 1) / 2-th smallest, MapPoint.cc:295-313); up to 32
   // observations on the stack (no allocation per call), beyond that on the heap
