@@ -32,6 +32,7 @@
 #include <functional>
 #include <map>
 #include <set>
+#include <unordered_map>
 #include <utility>
 #include <memory>
 #include <vector>
@@ -250,6 +251,13 @@ class MapEngine {
  private:
   std::function<void()> overlap_;
   std::vector<int> kf_count_, kf_touched_;  // update_local_keyframes' counter
+  // compute_distinctive's pairwise descriptor distances of points with more than 32 good
+  // observations, by observation ((keyframe << 32) | key, keyframe order)
+  struct DistCache {
+    std::vector<uint64_t> ids;
+    std::vector<uint16_t> d;
+  };
+  std::unordered_map<int, DistCache> dcache_;
   void run_overlap() {
     if (!overlap_) return;
     std::function<void()> fn = std::move(overlap_);

@@ -199,6 +199,7 @@ void MapEngine::grow_local(int m) {
 void MapEngine::reset() {
   pts_.clear();
   hot_.clear();
+  dcache_.clear();
   temps_.clear();
   kfs_.clear();
   state_ = 0;
@@ -294,10 +295,12 @@ void MapEngine::compute_distinctive(int h) {  // MapPoint::ComputeDistinctiveDes
   } timer{prof_on_ ? this : nullptr, prof_on_ ? now_us() : 0};
   // the descriptors of the good observing keyframes, their pairwise Hamming distances and each
   // one's median distance (the (N - 1) / 2-th smallest, MapPoint.cc:295-313); up to 32
-  // observations on the stack (no allocation per call), beyond that on the heap
+  // observations on the stack (no allocation per call), beyond that on the heap with the
+  // distances kept per point (dcache_: a new observation costs N distances, not N^2 / 2)
   constexpr int kStack = 32;
   const uint8_t* Ds[kStack];
   std::vector<const uint8_t*> Dh;
+  std::vector<uint64_t> ids;
   int N = 0;
   for (const auto& kv : p.obs)
     if (!kfs_[kv.first].bad) {
@@ -305,10 +308,21 @@ void MapEngine::compute_distinctive(int h) {  // MapPoint::ComputeDistinctiveDes
       if (N < kStack) Ds[N] = d;
       if (N == kStack) Dh.assign(Ds, Ds + kStack);
       if (N >= kStack) Dh.push_back(d);
+      ids.push_back(((uint64_t)(uint32_t)kv.first << 32) | (uint32_t)kv.second);
       N++;
     }
   if (N == 0) return;
   const uint8_t* const* Dv = N <= kStack ? Ds : Dh.data();
+  auto hamming = [](const uint8_t* x, const uint8_t* y) {
+    int d = 0;
+    for (int w = 0; w < 4; w++) {
+      uint64_t a, b;
+      memcpy(&a, x + 8 * w, 8);
+      memcpy(&b, y + 8 * w, 8);
+      d += __builtin_popcountll(a ^ b);
+    }
+    return d;
+  };
   int dist_s[kStack * kStack], v_s[kStack];
   std::vector<int> dist_h, v_h;
   if (N > kStack) {
@@ -317,23 +331,46 @@ void MapEngine::compute_distinctive(int h) {  // MapPoint::ComputeDistinctiveDes
   }
   int* dist = N <= kStack ? dist_s : dist_h.data();
   int* v = N <= kStack ? v_s : v_h.data();
-  for (int i = 0; i < N; i++) {
-    dist[(size_t)i * N + i] = 0;
-    for (int j = i + 1; j < N; j++) {
-      int d = 0;
-      for (int w = 0; w < 4; w++) {
-        uint64_t a, b;
-        memcpy(&a, Dv[i] + 8 * w, 8);
-        memcpy(&b, Dv[j] + 8 * w, 8);
-        d += __builtin_popcountll(a ^ b);
-      }
-      dist[(size_t)i * N + j] = dist[(size_t)j * N + i] = d;
+  if (N <= kStack) {
+    dcache_.erase(h);
+    for (int i = 0; i < N; i++) {
+      dist[(size_t)i * N + i] = 0;
+      for (int j = i + 1; j < N; j++)
+        dist[(size_t)i * N + j] = dist[(size_t)j * N + i] = hamming(Dv[i], Dv[j]);
     }
+  } else {
+    // old index of every current observation (both lists in keyframe order), -1 for a new one
+    DistCache& c = dcache_[h];
+    std::vector<int> old(N, -1);
+    for (size_t i = 0, o = 0; i < (size_t)N; i++) {
+      while (o < c.ids.size() && c.ids[o] < ids[i]) o++;
+      if (o < c.ids.size() && c.ids[o] == ids[i]) old[i] = (int)o;
+    }
+    const size_t M = c.ids.size();
+    for (int i = 0; i < N; i++) {
+      dist[(size_t)i * N + i] = 0;
+      for (int j = i + 1; j < N; j++) {
+        const int d = old[i] >= 0 && old[j] >= 0 ? (int)c.d[(size_t)old[i] * M + old[j]]
+                                                  : hamming(Dv[i], Dv[j]);
+        dist[(size_t)i * N + j] = dist[(size_t)j * N + i] = d;
+      }
+    }
+    c.ids = ids;
+    c.d.resize((size_t)N * N);
+    for (size_t q = 0; q < (size_t)N * N; q++) c.d[q] = (uint16_t)dist[q];
   }
+  // the row with the smallest median (the first on ties): a row's median is below the best so
+  // far iff more than m of its distances are, so most rows cost one counting pass
   const int m = (int)(0.5 * (N - 1));
   int best = INT_MAX, bi = 0;
   for (int i = 0; i < N; i++) {
-    std::copy(dist + (size_t)i * N, dist + (size_t)(i + 1) * N, v);
+    const int* row = dist + (size_t)i * N;
+    if (best != INT_MAX) {
+      int below = 0;
+      for (int k = 0; k < N; k++) below += row[k] < best;
+      if (below <= m) continue;
+    }
+    std::copy(row, row + N, v);
     std::nth_element(v, v + m, v + N);
     if (v[m] < best) {
       best = v[m];

@@ -108,8 +108,12 @@ def _texture(s, t, salt):
 
 
 class SequenceRenderer:
-    def __init__(self, scene, width=1242, height=375, K=KITTI03, device="cpu"):
+    def __init__(self, scene, width=1242, height=375, K=KITTI03, device="cpu", aa=1):
+        """aa > 1: the colour of a pixel is the mean of aa x aa sub-pixel rays (box-filtered
+        texture, diagnostics of aliasing: tools/drift_ablation.py); depth, flow and labels stay
+        the pixel centre's.  aa = 1 (default) is the sequence every test and the bench use."""
         self.scene, self.W, self.H, self.K = scene, width, height, K
+        self.aa = int(aa)
         self.dev = torch.device(device)
         v, u = torch.meshgrid(torch.arange(height, dtype=torch.float64, device=self.dev),
                               torch.arange(width, dtype=torch.float64, device=self.dev),
@@ -121,12 +125,18 @@ class SequenceRenderer:
     def _t(self, a):
         return torch.as_tensor(np.asarray(a), dtype=torch.float64, device=self.dev)
 
-    def _cast(self, t):
-        """Depth Z (camera z), surface id, world hit point for frame t."""
+    def _cast(self, t, du=0.0, dv=0.0):
+        """Depth Z (camera z), surface id, world hit point for frame t (rays through the pixel
+        centres shifted by (du, dv) pixels)."""
         sc = self.scene
         Twc = self._t(sc.Twc(t))
         o = Twc[:3, 3]
-        dw = self.ray @ Twc[:3, :3].T  # world direction per unit camera depth
+        ray = self.ray
+        if du or dv:
+            ray = torch.stack([(self.u + du - self.K["cx"]) / self.K["fx"],
+                               (self.v + dv - self.K["cy"]) / self.K["fy"],
+                               torch.ones_like(self.u)], -1)
+        dw = ray @ Twc[:3, :3].T  # world direction per unit camera depth
         inf = torch.full_like(self.u, float("inf"))
         Z = inf.clone()
         sid = torch.zeros_like(self.u, dtype=torch.int32)  # 0 sky
@@ -167,10 +177,9 @@ class SequenceRenderer:
         return pc[..., 0] / z * self.K["fx"] + self.K["cx"], pc[..., 1] / z * self.K["fy"] + \
             self.K["cy"]
 
-    def frame(self, t):
+    def _colour(self, t, sid, Pw):
+        """Gray texture value and tint of every pixel from its ray's surface and hit point."""
         sc = self.scene
-        Z, sid, Pw = self._cast(t)
-        # ---- colour
         g = torch.full_like(self.u, 200.0, dtype=torch.float64).to(torch.float32)
         tint = torch.zeros(self.H, self.W, 3, dtype=torch.float32, device=self.dev)
         P32 = Pw.to(torch.float32)
@@ -199,7 +208,24 @@ class SequenceRenderer:
         sky = sid == 0
         tint = torch.where(sky.unsqueeze(-1), torch.tensor((1.05, 1.0, 0.95), device=self.dev),
                            tint)
-        bgr = torch.clamp(g.unsqueeze(-1) * tint + 0.5, 0, 255).to(torch.uint8)
+        return g, tint
+
+    def frame(self, t):
+        sc = self.scene
+        Z, sid, Pw = self._cast(t)
+        # ---- colour
+        if self.aa <= 1:
+            g, tint = self._colour(t, sid, Pw)
+            bgr = torch.clamp(g.unsqueeze(-1) * tint + 0.5, 0, 255).to(torch.uint8)
+        else:
+            acc = torch.zeros(self.H, self.W, 3, dtype=torch.float32, device=self.dev)
+            offs = [(k + 0.5) / self.aa - 0.5 for k in range(self.aa)]
+            for dv in offs:
+                for du in offs:
+                    _, sid_s, Pw_s = self._cast(t, du, dv)
+                    g_s, tint_s = self._colour(t, sid_s, Pw_s)
+                    acc = acc + g_s.unsqueeze(-1) * tint_s
+            bgr = torch.clamp(acc / (self.aa * self.aa) + 0.5, 0, 255).to(torch.uint8)
         # ---- disparity (KITTI u16 = disp * 256), exact depth where finite
         valid = torch.isfinite(Z) & (Z > 0.1)
         dq = torch.where(valid, torch.round(256.0 * self.K["bf"] / Z.clamp(min=0.1)),
@@ -238,11 +264,11 @@ class SequenceRenderer:
 
 
 def kitti_like_sequence(nframes, width=1242, height=375, n_objects=3, seed=1003, device="cpu",
-                        start=0, lanes=None):
+                        start=0, lanes=None, aa=1):
     """C2 (n_objects=0) / C3 (n_objects=3) / C5 (1920x1080, n_objects=8) sequences; `lanes`
     (x, distance ahead) per object overrides the default street layout."""
     return SequenceRenderer(StreetScene(n_objects, seed, lanes=lanes), width, height,
-                            device=device).sequence(nframes, start)
+                            device=device, aa=aa).sequence(nframes, start)
 
 
 def to_numpy_frames(seq):

@@ -13,6 +13,10 @@ ablation per process and logs the per-frame pose error against the renderer's gr
   no_ba_depth_nearest  both
   level_centre         ORACLE_ABLATE=8: level-l keypoints at their pixel centre's level-0 position
                        ((x + 0.5) s - 0.5) instead of x s (ORBextractor.cc:1100-1104)
+  aa3, aa3_no_ba       the same sequence with box-filtered colour (3 x 3 sub-pixel rays per pixel,
+                       scene.SequenceRenderer aa): does texture aliasing (the fbm's finest octaves
+                       are above the pixel Nyquist rate beyond about 20 m) feed the BA keypoints
+                       that do not stay on one surface point?
   static, static_no_ba the same sequence without its three moving boxes (the ego motion, the
                        street and the seed unchanged): do the map points that the moving boxes'
                        keys create drive the drift through the local BA?
@@ -47,10 +51,13 @@ CONFIGS = {
     "depth_nearest": {"ORACLE_ABLATE": "4"},
     "no_ba_depth_nearest": {"ORACLE_ABLATE": "4", "ORACLE_LM_STEPS": "5"},
     "level_centre": {"ORACLE_ABLATE": "8"},
+    "aa3": {},
+    "aa3_no_ba": {"ORACLE_LM_STEPS": "5"},
     "static": {},
     "static_no_ba": {"ORACLE_LM_STEPS": "5"},
 }
 N_OBJECTS = {"static": 0, "static_no_ba": 0}
+AA = {"aa3": 3, "aa3_no_ba": 3}
 
 
 def centre(T):
@@ -82,7 +89,8 @@ def worker(args):
     for s0 in range(0, args.frames, 200):
         n = min(200, args.frames - s0)
         seq = scene.kitti_like_sequence(n, W, H, n_objects=N_OBJECTS.get(args.config, 3),
-                                        seed=args.seed, device=dev, start=s0)
+                                        seed=args.seed, device=dev, start=s0,
+                                        aa=AA.get(args.config, 1))
         fr = scene.to_numpy_frames(seq)
         for i in range(n):
             f = fr[i]
