@@ -150,7 +150,7 @@ struct MappingStats {
   // finer host wall times of the keyframe path (MMT_MAP_PROFILE; printed at destruction)
   double kfnew_us = 0, pnk_us = 0, sin_us = 0, basolve_us = 0, cull_us = 0, lmsync_us = 0;
   double cnmp_us = 0;  // CreateNewMapPoints (vocabulary path), inside sin_us
-  static constexpr int kBlk = 15;  // finer blocks of the keyframe path (names in ~MapEngine)
+  static constexpr int kBlk = 18;  // finer blocks of the keyframe path (names in ~MapEngine)
   double blk_us[kBlk] = {};
   long n_lm = 0;
 };
@@ -251,6 +251,7 @@ class MapEngine {
  private:
   std::function<void()> overlap_;
   std::vector<int> kf_count_, kf_touched_;  // update_local_keyframes' counter
+  std::vector<int> lp_buf_;                  // update_local_points' compacted slots
   // compute_distinctive's pairwise descriptor distances of points with more than 32 good
   // observations, by observation ((keyframe << 32) | key, keyframe order)
   struct DistCache {

@@ -87,7 +87,8 @@ MapEngine::~MapEngine() {
           "new keyframe + store", "new points", "SIN targets", "SIN fuse 1", "SIN candidates",
           "SIN fuse 2", "SIN point updates", "SIN connections", "BA graph", "BA apply",
           "Fuse pool flush", "Fuse enqueue", "Fuse wait", "Fuse apply (+ relaunches)",
-          "ComputeDistinctiveDescriptors (inside the others)"};
+          "ComputeDistinctiveDescriptors (inside the others)", "PNK ComputeBoW",
+          "PNK observations", "PNK UpdateConnections"};
       fprintf(stderr, "[mmt localmapping profile] per keyframe, us:");
       for (int k = 0; k < MappingStats::kBlk; k++)
         fprintf(stderr, " %s %.1f%s", bn[k], mstats_.blk_us[k] / n,
@@ -500,7 +501,9 @@ int MapEngine::tracked_map_points(int kf, int minObs) {  // KeyFrame::TrackedMap
 }
 
 void MapEngine::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFrame
+  double tb = prof_on_ ? now_us() : 0;
   if (voc_) kf_bow(kf);  // mpCurrentKeyFrame->ComputeBoW() (without a vocabulary: none)
+  blk_time(15, tb);
   const std::vector<int> mps = kfs_[kf].mps;
   for (size_t i = 0; i < mps.size(); i++) {
     const int h = mps[i];
@@ -513,7 +516,9 @@ void MapEngine::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFr
       recent_.push_back(h);
     }
   }
+  blk_time(16, tb);
   update_connections(kf);
+  blk_time(17, tb);
 }
 
 void MapEngine::map_point_culling(int kf) {  // LocalMapping::MapPointCulling (RGB-D: 3 obs)
@@ -1013,10 +1018,20 @@ void MapEngine::update_local_keyframes(MapFrameH& C) {  // Tracking::UpdateLocal
 
 void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
   localPts_.clear();
-  for (int kf : localKFs_)
-    for (int h : kfs_[kf].mps) {
+  // a keyframe's slots are about half empty (-1) in no predictable pattern: its handles are first
+  // compacted without a branch, then visited in slot order (the same points in the same order)
+  std::vector<int>& buf = lp_buf_;
+  for (int kf : localKFs_) {
+    const std::vector<int>& mps = kfs_[kf].mps;
+    buf.resize(mps.size());
+    size_t n = 0;
+    for (int h : mps) {
+      buf[n] = h;
       // keyframes hold real points only (Track clears the VO points before a keyframe is made)
-      if (h < 0 || h >= kTemp) continue;
+      n += (unsigned)h < (unsigned)kTemp;
+    }
+    for (size_t i = 0; i < n; i++) {
+      const int h = buf[i];
       PtHot& q = hot_[h];
       if (q.trackRef == (int)curId_) continue;
       if (!q.bad) {
@@ -1024,6 +1039,7 @@ void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
         q.trackRef = (int)curId_;
       }
     }
+  }
 }
 
 void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const float* Tcw) {
