@@ -252,6 +252,7 @@ class MapEngine {
   std::function<void()> overlap_;
   std::vector<int> kf_count_, kf_touched_;  // update_local_keyframes' counter
   std::vector<int> lp_buf_;                  // update_local_points' compacted slots
+  std::vector<uint64_t> lp_seen_;            // update_local_points' per-point marks (bits)
   // compute_distinctive's pairwise descriptor distances of points with more than 32 good
   // observations, by observation ((keyframe << 32) | key, keyframe order)
   struct DistCache {

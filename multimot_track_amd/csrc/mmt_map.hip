@@ -1019,8 +1019,13 @@ void MapEngine::update_local_keyframes(MapFrameH& C) {  // Tracking::UpdateLocal
 void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
   localPts_.clear();
   // a keyframe's slots are about half empty (-1) in no predictable pattern: its handles are first
-  // compacted without a branch, then visited in slot order (the same points in the same order)
+  // compacted without a branch, then visited in slot order (the same points in the same order).
+  // mnTrackReferenceForFrame is a bit per point here (lp_seen_, tens of kB: the 70k slot visits
+  // of a dense local map stay in cache), cleared again for the points this call marked; the one
+  // call per frame (TrackLocalMap) makes it equal to the per-point frame id.
   std::vector<int>& buf = lp_buf_;
+  const size_t words = (hot_.size() + 63) / 64;
+  if (lp_seen_.size() < words) lp_seen_.resize(words, 0);
   for (int kf : localKFs_) {
     const std::vector<int>& mps = kfs_[kf].mps;
     buf.resize(mps.size());
@@ -1032,14 +1037,16 @@ void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
     }
     for (size_t i = 0; i < n; i++) {
       const int h = buf[i];
-      PtHot& q = hot_[h];
-      if (q.trackRef == (int)curId_) continue;
-      if (!q.bad) {
+      uint64_t& wd = lp_seen_[(size_t)h >> 6];
+      const uint64_t bit = 1ull << (h & 63);
+      if (wd & bit) continue;
+      if (!hot_[h].bad) {  // a bad point stays unmarked and is skipped again, as the reference
         localPts_.push_back(h);
-        q.trackRef = (int)curId_;
+        wd |= bit;
       }
     }
   }
+  for (int h : localPts_) lp_seen_[(size_t)h >> 6] &= ~(1ull << (h & 63));
 }
 
 void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const float* Tcw) {
@@ -1107,12 +1114,10 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
   if (m > 0) MMT_HIP(hipMemcpyAsync(h_inview_, d_inview_, (size_t)m, hipMemcpyDeviceToHost, s_));
   run_overlap();
   MMT_HIP(hipStreamSynchronize(s_));
-  for (int j = 0; j < m; j++) {
-    if (skip[j]) continue;
-    MPoint& p = mp(localPts_[j]);
-    p.trackInView = h_inview_[j] != 0;
-    if (p.trackInView) p.visible++;
-  }
+  // IncreaseVisible for the points in view (mbTrackInView itself is read by the GPU search only,
+  // from h_inview_: the host's copy of the flag is not kept, so only the points in view are touched)
+  for (int j = 0; j < m; j++)
+    if (!skip[j] && h_inview_[j]) mp(localPts_[j]).visible++;
   for (int i = 0; i < C.n; i++)
     if (h_match_[i] >= 0) C.mps[i] = localPts_[h_match_[i]];
 }
