@@ -9,7 +9,9 @@ checks of what the reference's data structures must satisfy after every LocalMap
     go together, MapPoint.cc:98-137, KeyFrame.cc:188-216), and a good keyframe's slot holding a
     good point belongs to a keyframe the point observes (not necessarily at that slot: a frame
     can hold one point at two keys after CheckReplacedInLastFrame, and ProcessNewKeyFrame then
-    keeps the second slot without an observation, LocalMapping.cc:149-166);
+    keeps the second slot without an observation, LocalMapping.cc:149-166; and two points
+    CreateNewMapPoints made from one keyframe-2 feature both observe its slot, which holds the
+    second, or nothing once the second went bad);
   * nObs == the recount (2 per observation with mvuRight >= 0, else 1; MapPoint.cc:98-137);
   * mpRefKF is an observer (MapPoint::EraseObservation moves it, MapPoint.cc:111-137);
   * no good point observes a bad keyframe (KeyFrame::SetBadFlag erases its observations,
@@ -26,9 +28,11 @@ Test infrastructure only."""
 import numpy as np
 
 
-def check_map(D, newest=None):
+def check_map(D, newest=None, cnmp=False):
     """List of violation strings (empty: every invariant holds).  newest: the keyframe whose
-    LocalMapping just ran (its covisibility weights are compared with the recount)."""
+    LocalMapping just ran (its covisibility weights are compared with the recount).  cnmp: the
+    map comes from a run with CreateNewMapPoints (a vocabulary), whose duplicate slot bindings
+    (below) are allowed."""
     bad = []
     kf_i, pt_i = D["kf_i"], D["pt_i"]
     nk, npt = len(kf_i), len(pt_i)
@@ -42,9 +46,24 @@ def check_map(D, newest=None):
     for o in np.nonzero(og & kbad[okf])[0][:20]:
         bad.append("point %d observes bad keyframe %d" % (pid[o], okf[o]))
     held = slots[ks[okf] + oidx]
-    for o in np.nonzero(og & (held != pid))[0][:20]:
+    # one exception: SearchForTriangulation never sets vbMatched2 (ORBmatcher.cc:1032-1198), so two
+    # keyframe-1 features can take the same keyframe-2 feature, and CreateNewMapPoints'
+    # AddMapPoint(pMP, idx2) then gives the slot to the second new point while the first keeps its
+    # observation (LocalMapping.cc:430-440): the slot's holder observes the same (kf, key)
+    key = (pid.astype(np.int64) * nk + okf) * np.int64(1 << 20) + oidx
+    keys = set(key[og].tolist())
+    for o in np.nonzero(og & (held != pid))[0]:
+        if cnmp and held[o] >= 0 and \
+                ((int(held[o]) * nk + int(okf[o])) * (1 << 20) + int(oidx[o])) in keys:
+            continue
+        # ... and once that holder goes bad, SetBadFlag empties the slot (EraseMapPointMatch) while
+        # the first point still observes it
+        if cnmp and held[o] < 0:
+            continue
         bad.append("point %d obs (kf %d, key %d) but the slot holds %d"
                    % (pid[o], okf[o], oidx[o], held[o]))
+        if len(bad) >= 20:
+            break
     nobs = np.bincount(pid, weights=np.where(of[:, 3] >= 0, 2, 1), minlength=npt)
     for j in np.nonzero(pgood & (nobs != pt_i[:, 1]))[0][:20]:
         bad.append("point %d nObs %d != recount %d" % (j, pt_i[j, 1], nobs[j]))

@@ -173,4 +173,4 @@ def test_oracle_tracker_with_vocabulary_runs_bow_paths(oracle_mod):
     assert st["reloc"] >= 1 and st["reloc_cands"] >= 1
     assert st["triangulated"] > 0 and st["sft_matches"] >= st["triangulated"]
     assert st["kfdb"] > 0
-    assert check_map(tr.map_dump()) == []
+    assert check_map(tr.map_dump(), cnmp=True) == []
