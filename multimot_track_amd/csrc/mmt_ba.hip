@@ -462,7 +462,10 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_init(BADesc d, BAWork2 w) {
 // instead of one thread: a point seen from far away by every keyframe (a key at disparity 0 has depth
 // bf / 0 = inf, and CreateNewMapPoints triangulates such keys into far points) collects a hundred
 // or more edges, and its thread's serial edge loop set k_ba2_lin / k_ba2_p4 at 100-160 us.
-constexpr int kBaHeavy = 8;
+#ifndef MMT_BA_HEAVY
+#define MMT_BA_HEAVY 8  // A/B builds: tools/ab_build.sh <tag> --src mmt_ba.hip -DMMT_BA_HEAVY=..
+#endif
+constexpr int kBaHeavy = MMT_BA_HEAVY;
 
 __device__ __forceinline__ bool ba2_heavy(const BADesc& d, int j) {
   return d.pt_start[j + 1] - d.pt_start[j] > kBaHeavy;

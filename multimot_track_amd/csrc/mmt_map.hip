@@ -154,9 +154,15 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
   d_esc_ = dev<double>(3 * (size_t)kcap);
   d_fsc_ = dev<int>(kcap);
   prof_on_ = getenv("MMT_MAP_PROFILE") != nullptr;
-  // LocalMapping's stream, normal priority (high / low measured within noise / slower): its
-  // kernels (keyframe store copies, Fuse, the local BA) need nothing of the frame's flow solve
-  MMT_HIP(hipStreamCreateWithPriority(&lm_s_, hipStreamNonBlocking, 0));
+  // LocalMapping's stream, normal priority (high / low measured within noise / slower in round 5,
+  // without the vocabulary): its kernels (keyframe store copies, the BoW transform, Fuse,
+  // SearchForTriangulation, the local BA) need nothing of the frame's flow solve.  MMT_LM_PRIO=high
+  // (A/B): the greatest priority
+  int prio_lo = 0, prio_hi = 0;
+  MMT_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  const char* lmp = getenv("MMT_LM_PRIO");
+  const int lm_prio = lmp && strcmp(lmp, "high") == 0 ? prio_hi : 0;
+  MMT_HIP(hipStreamCreateWithPriority(&lm_s_, hipStreamNonBlocking, lm_prio));
   // keyframe store record: keys, descriptors, mvuRight, grid (cell starts + key lists)
   kf_rec_bytes_ = align16(sizeof(mmt_kp) * (size_t)kcap) + 32 * (size_t)kcap +
                   align16(4 * (size_t)kcap) + align16(4 * (size_t)(kGridCells + 1)) +
