@@ -463,9 +463,9 @@ __global__ __launch_bounds__(kMkThreads) void k_ba2_init(BADesc d, BAWork2 w) {
 // bf / 0 = inf, and CreateNewMapPoints triangulates such keys into far points) collects a hundred
 // or more edges, and its thread's serial edge loop set k_ba2_lin / k_ba2_p4 at 100-160 us.
 #ifndef MMT_BA_HEAVY
-#define MMT_BA_HEAVY 8  // A/B builds: tools/ab_build.sh <tag> --src mmt_ba.hip -DMMT_BA_HEAVY=..
+#define MMT_BA_HEAVY 2  // A/B builds: tools/ab_build.sh <tag> --src mmt_ba.hip -DMMT_BA_HEAVY=..
 #endif
-constexpr int kBaHeavy = MMT_BA_HEAVY;
+constexpr int kBaHeavy = MMT_BA_HEAVY;  // 2: BA 2,060 -> 1,800 us per keyframe against 8 (profiles/r06_ab_lmprio_baheavy.txt)
 
 __device__ __forceinline__ bool ba2_heavy(const BADesc& d, int j) {
   return d.pt_start[j + 1] - d.pt_start[j] > kBaHeavy;
