@@ -279,6 +279,7 @@ void MapEngine::mark_bad(int h) {
   if (!p.bad && h < kTemp) n_good_--;
   p.bad = true;
   if (h < kTemp) hot_[h].bad = 1;
+  if (!dcache_.empty()) dcache_.erase(h);  // a bad point's descriptor is never recomputed
 }
 
 void MapEngine::set_bad(int h) {  // MapPoint::SetBadFlag
