@@ -222,9 +222,9 @@ void MapEngine::bw_grow(size_t need) {
 }
 
 // transform(descriptors, BowVector, FeatureVector, 4): the descent on the GPU, the vectors built
-// on the host in feature order (Vocabulary::build)
-void MapEngine::bow_transform(const uint8_t* d_desc, int n, hipStream_t st, BowVecH& v,
-                              FeatVecH& fv) {
+// on the host in feature order (Vocabulary::build).  bow_launch queues the descent and the copy
+// back on st; bow_finish waits for them and builds (nothing may touch d_bw_ / h_bw_ between)
+void MapEngine::bow_launch(const uint8_t* d_desc, int n, hipStream_t st) {
   const size_t bytes = 16 * (size_t)std::max(n, 1);
   bw_grow(bytes);
   uint32_t* dw = (uint32_t*)d_bw_;
@@ -232,6 +232,9 @@ void MapEngine::bow_transform(const uint8_t* d_desc, int n, hipStream_t st, BowV
   double* dx = (double*)(d_bw_ + 8 * (size_t)n);
   launch_bow_transform(voc_->dev, d_desc, n, 4, dw, dx, dn, st);
   if (n > 0) MMT_HIP(hipMemcpyAsync(h_bw_, d_bw_, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
+}
+
+void MapEngine::bow_finish(int n, hipStream_t st, BowVecH& v, FeatVecH& fv) {
   MMT_HIP(hipStreamSynchronize(st));
   const uint32_t* hw = (const uint32_t*)h_bw_;
   voc_->build(hw, (const double*)(h_bw_ + 8 * (size_t)n), hw + n, n, v, fv);
@@ -239,15 +242,23 @@ void MapEngine::bow_transform(const uint8_t* d_desc, int n, hipStream_t st, BowV
 
 void MapEngine::frame_bow(MapFrameH& C, const GridFrame& G) {  // Frame::ComputeBoW
   if (C.hasBow) return;
-  bow_transform(G.desc, C.n, s_, C.bow, C.fv);
+  bow_launch(G.desc, C.n, s_);
+  bow_finish(C.n, s_, C.bow, C.fv);
   C.hasBow = true;
   bstats_.n_bow_frames++;
 }
 
-void MapEngine::kf_bow(int kf) {  // KeyFrame::ComputeBoW (the keyframe-store copy on lm_s_)
+// KeyFrame::ComputeBoW on the keyframe-store copy (lm_s_), in two halves: ProcessNewKeyFrame's
+// host work runs between them (it does not read the vectors)
+void MapEngine::kf_bow_launch(int kf) {
+  const KFrame& K = kfs_[kf];
+  if (!K.hasBow) bow_launch(K.dev.desc, (int)K.keys.size(), lm_s_);
+}
+
+void MapEngine::kf_bow_finish(int kf) {
   KFrame& K = kfs_[kf];
   if (K.hasBow) return;
-  bow_transform(K.dev.desc, (int)K.keys.size(), lm_s_, K.bow, K.fv);
+  bow_finish((int)K.keys.size(), lm_s_, K.bow, K.fv);
   K.hasBow = true;
 }
 

@@ -311,9 +311,11 @@ class MapEngine {
   void set_pose(int kf, const float* Tcw);
   void kf_store_add(int kf);
   // ---- vocabulary path (mmt_bowmap.hip)
-  void bow_transform(const uint8_t* d_desc, int n, hipStream_t st, BowVecH& v, FeatVecH& fv);
+  void bow_launch(const uint8_t* d_desc, int n, hipStream_t st);
+  void bow_finish(int n, hipStream_t st, BowVecH& v, FeatVecH& fv);
   void frame_bow(MapFrameH& C, const GridFrame& G);
-  void kf_bow(int kf);
+  void kf_bow_launch(int kf);
+  void kf_bow_finish(int kf);
   void kfdb_add(int kf);
   void kfdb_erase(int kf);
   std::vector<int> detect_relocalization_candidates(const MapFrameH& C);

@@ -509,7 +509,9 @@ int MapEngine::tracked_map_points(int kf, int minObs) {  // KeyFrame::TrackedMap
 
 void MapEngine::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFrame
   double tb = prof_on_ ? now_us() : 0;
-  if (voc_) kf_bow(kf);  // mpCurrentKeyFrame->ComputeBoW() (without a vocabulary: none)
+  // mpCurrentKeyFrame->ComputeBoW() (without a vocabulary: none): the descent runs on the GPU
+  // while the observations and connections below are updated on the host (they do not read it)
+  if (voc_) kf_bow_launch(kf);
   blk_time(15, tb);
   const std::vector<int> mps = kfs_[kf].mps;
   for (size_t i = 0; i < mps.size(); i++) {
@@ -526,6 +528,8 @@ void MapEngine::process_new_keyframe(int kf) {  // LocalMapping::ProcessNewKeyFr
   blk_time(16, tb);
   update_connections(kf);
   blk_time(17, tb);
+  if (voc_) kf_bow_finish(kf);
+  blk_time(15, tb);
 }
 
 void MapEngine::map_point_culling(int kf) {  // LocalMapping::MapPointCulling (RGB-D: 3 obs)
