@@ -253,6 +253,22 @@ class MapEngine {
   std::vector<int> kf_count_, kf_touched_;  // update_local_keyframes' counter
   std::vector<int> lp_buf_;                  // update_local_points' compacted slots
   std::vector<uint64_t> lp_seen_;            // update_local_points' per-point marks (bits)
+  // TrackLocalMap's local keyframes and points, computed from C2's matches while D1 runs on the
+  // GPU (speculate_local_map) and taken by track_local_map when D1's outliers leave every counted
+  // keyframe with a count (commit_local_map); MMT_LOCALMAP_SPEC=0 turns it off (A/B)
+  bool spec_on_ = true, spec_valid_ = false;
+  bool overlap_c3_ = false;  // MMT_OVERLAP_C3=1: the overlap work waits for the C3 chain (A/B)
+  long spec_frame_ = -1, spec_stamp_ = 0, spec_hits_ = 0, spec_tries_ = 0;
+  std::vector<int> spec_mps_, spec_cnt_, spec_touched_, spec_kfs_, spec_pts_;
+  std::vector<long> spec_mark_;
+  uint8_t* h_early_ = nullptr;  // C2's match count and matches, copied before D1
+  hipEvent_t ev_early_ = nullptr;
+  void speculate_local_map(const MapFrameH& L, int n);
+  bool commit_local_map(MapFrameH& C);
+  void spec_discard();
+  template <class Marked, class Mark>
+  void expand_local_kfs(std::vector<int>& kfl, Marked marked, Mark mark);
+  void collect_local_points(const std::vector<int>& kfl, std::vector<int>& out);
   // compute_distinctive's pairwise descriptor distances of points with more than 32 good
   // observations, by observation ((keyframe << 32) | key, keyframe order)
   struct DistCache {
@@ -340,7 +356,7 @@ class MapEngine {
   // retry_below (-1: min_matches): the retry at retry_th runs below this many matches
   int gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
                       const float* Tlast, float th, float retry_th, int min_matches,
-                      int retry_below = -1);
+                      int retry_below = -1, bool spec = false);
   void pose_desc_fill(uint8_t* h_blk, uint8_t* d_blk, const float* Tcw);
   size_t out_bytes(int n) const;
   MapEdgeArgs edge_args(const GridFrame& G) const;

@@ -95,15 +95,17 @@ MapEngine::~MapEngine() {
                 k + 1 < MappingStats::kBlk ? "," : "\n");
     }
     fprintf(stderr, "[mmt map profile] per frame: %.1f local keyframes, %.1f local points, "
-            "%.1f C3 edges; %zu map points allocated, %d keyframes at the end\n",
+            "%.1f C3 edges; %zu map points allocated, %d keyframes at the end; local map "
+            "speculated %ld times, taken %ld\n",
             prof_cnt_[0] / prof_n_, prof_cnt_[1] / prof_n_, prof_cnt_[2] / prof_n_, pts_.size(),
-            n_keyframes());
+            n_keyframes(), spec_tries_, spec_hits_);
   }
   if (s_) (void)hipStreamSynchronize(s_);
   if (lm_s_) {
     (void)hipStreamSynchronize(lm_s_);
     (void)hipStreamDestroy(lm_s_);
   }
+  if (ev_early_) (void)hipEventDestroy(ev_early_);
   for (void* p : dallocs_) (void)hipFree(p);
   for (void* p : hallocs_) (void)hipHostFree(p);
 }
@@ -154,6 +156,10 @@ void MapEngine::setup(const MapCamH& cam, int kcap) {
   d_esc_ = dev<double>(3 * (size_t)kcap);
   d_fsc_ = dev<int>(kcap);
   prof_on_ = getenv("MMT_MAP_PROFILE") != nullptr;
+  if (const char* e = getenv("MMT_LOCALMAP_SPEC")) spec_on_ = atoi(e) != 0;
+  if (const char* e = getenv("MMT_OVERLAP_C3")) overlap_c3_ = atoi(e) != 0;
+  h_early_ = pinned<uint8_t>(kOutHdr + 4 * (size_t)kcap);
+  MMT_HIP(hipEventCreateWithFlags(&ev_early_, hipEventDisableTiming));
   // LocalMapping's stream, normal priority (high / low measured within noise / slower in round 5,
   // without the vocabulary): its kernels (keyframe store copies, the BoW transform, Fuse,
   // SearchForTriangulation, the local BA) need nothing of the frame's flow solve.  MMT_LM_PRIO=high
@@ -207,6 +213,7 @@ void MapEngine::reset() {
   pts_.clear();
   hot_.clear();
   dcache_.clear();
+  spec_discard();
   temps_.clear();
   kfs_.clear();
   state_ = 0;
@@ -608,7 +615,7 @@ void MapEngine::apply_pose_opt(MapFrameH& C, float* Tcw) {
 // Returns nmatches; the pose and outliers are applied when D1 ran.
 int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, const MapFrameH& L,
                                const float* Tlast, float th, float retry_th, int min_matches,
-                               int retry_below) {
+                               int retry_below, bool spec) {
   if (retry_below < 0) retry_below = min_matches;
   const double t_pack = prof_on_ ? now_us() : 0;
   const int n1 = L.n;
@@ -651,9 +658,18 @@ int MapEngine::gpu_frame_chain(MapFrameH& C, const GridFrame& G, float* Tcw, con
   launch_sbp_frame(G, Tcw, LD, th, 0, 1, c2_, d_match_, d_nm_, s_, nullptr, 0, &e);
   if (retry_th > 0)
     launch_sbp_frame(G, Tcw, LD, retry_th, 0, 1, c2_, d_match_, d_nm_, s_, d_nm_, retry_below, &e);
+  spec = spec && spec_on_;
+  if (spec) {  // the final matches (D1 does not change them) ahead of D1, for speculate_local_map
+    MMT_HIP(hipMemcpyAsync(h_early_, d_out_, kOutHdr + 4 * (size_t)C.n, hipMemcpyDeviceToHost, s_));
+    MMT_HIP(hipEventRecord(ev_early_, s_));
+  }
   launch_pose_opt(d_pod_, 1, std::min(C.n, nact), s_);
   MMT_HIP(hipMemcpyAsync(h_out_, d_out_, out_bytes(C.n), hipMemcpyDeviceToHost, s_));
-  run_overlap();
+  if (!spec || !overlap_c3_) run_overlap();
+  if (spec) {
+    MMT_HIP(hipEventSynchronize(ev_early_));
+    if (*(const int*)h_early_ >= min_matches) speculate_local_map(L, C.n);
+  }
   MMT_HIP(hipStreamSynchronize(s_));
   std::fill(C.mps.begin(), C.mps.end(), -1);
   for (int i2 = 0; i2 < C.n; i2++)
@@ -889,7 +905,7 @@ bool MapEngine::track_with_motion_model(MapFrameH& C, const GridFrame& G, float*
   const float th = 15;
   int nmatches;
   // C2 at th, again at 2 th below 20 matches, then D1 at 20 or more (Tracking.cc:2962-2990)
-  MAP_PROF(0, nmatches = gpu_frame_chain(C, G, Tcw, L, Tlast, th, 2 * th, 20));
+  MAP_PROF(0, nmatches = gpu_frame_chain(C, G, Tcw, L, Tlast, th, 2 * th, 20, -1, true));
   st.matches_mm = nmatches;
   if (nmatches < 20) return false;
   int nmatchesMap = 0;
@@ -960,6 +976,39 @@ bool MapEngine::relocalization_subst(MapFrameH& C, const GridFrame& G, float* Tc
   return false;
 }
 
+// UpdateLocalKeyFrames' second part (Tracking.cc:3555-3604): per keyframe of the counted set, its
+// first unmarked good covisible among the best 10, its first unmarked good child, and its parent
+// (which ends the loop), up to 80 keyframes
+template <class Marked, class Mark>
+void MapEngine::expand_local_kfs(std::vector<int>& kfl, Marked marked, Mark mark) {
+  const size_t n0 = kfl.size();
+  for (size_t q = 0; q < n0; q++) {
+    if (kfl.size() > 80) break;
+    const KFrame& K = kfs_[kfl[q]];
+    const size_t nn = std::min<size_t>(10, K.ordered.size());
+    for (size_t a = 0; a < nn; a++) {
+      const int id = K.ordered[a];
+      if (!kfs_[id].bad && !marked(id)) {
+        kfl.push_back(id);
+        mark(id);
+        break;
+      }
+    }
+    for (int ch : K.children) {
+      if (!kfs_[ch].bad && !marked(ch)) {
+        kfl.push_back(ch);
+        mark(ch);
+        break;
+      }
+    }
+    if (K.parent >= 0 && !marked(K.parent)) {
+      kfl.push_back(K.parent);
+      mark(K.parent);
+      break;  // leaves the keyframe loop (Tracking.cc:3601)
+    }
+  }
+}
+
 void MapEngine::update_local_keyframes(MapFrameH& C) {  // Tracking::UpdateLocalKeyFrames
   // keyframeCounter (a std::map keyed by KeyFrame*, here by keyframe id): counts in a flat array,
   // then the touched ids in ascending order, as the map would iterate them
@@ -991,44 +1040,20 @@ void MapEngine::update_local_keyframes(MapFrameH& C) {  // Tracking::UpdateLocal
     localKFs_.push_back(id);
     K.trackRef = curId_;
   }
-  const size_t n0 = localKFs_.size();
-  for (size_t q = 0; q < n0; q++) {
-    if (localKFs_.size() > 80) break;
-    const KFrame& K = kfs_[localKFs_[q]];
-    const size_t nn = std::min<size_t>(10, K.ordered.size());
-    for (size_t a = 0; a < nn; a++) {
-      KFrame& N = kfs_[K.ordered[a]];
-      if (!N.bad && N.trackRef != curId_) {
-        localKFs_.push_back(K.ordered[a]);
-        N.trackRef = curId_;
-        break;
-      }
-    }
-    for (int ch : K.children) {
-      KFrame& N = kfs_[ch];
-      if (!N.bad && N.trackRef != curId_) {
-        localKFs_.push_back(ch);
-        N.trackRef = curId_;
-        break;
-      }
-    }
-    if (K.parent >= 0) {
-      KFrame& Pa = kfs_[K.parent];
-      if (Pa.trackRef != curId_) {
-        localKFs_.push_back(K.parent);
-        Pa.trackRef = curId_;
-        break;  // leaves the keyframe loop (Tracking.cc:3601)
-      }
-    }
-  }
+  expand_local_kfs(
+      localKFs_, [&](int id) { return kfs_[id].trackRef == curId_; },
+      [&](int id) { kfs_[id].trackRef = curId_; });
   if (kmax >= 0) {
     refKF_ = kmax;
     C.refKF = kmax;
   }
 }
 
-void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
-  localPts_.clear();
+void MapEngine::update_local_points() { collect_local_points(localKFs_, localPts_); }
+
+void MapEngine::collect_local_points(const std::vector<int>& kfl, std::vector<int>& out) {
+  // Tracking::UpdateLocalPoints over the keyframes kfl
+  out.clear();
   // a keyframe's slots are about half empty (-1) in no predictable pattern: its handles are first
   // compacted without a branch, then visited in slot order (the same points in the same order).
   // mnTrackReferenceForFrame is a bit per point here (lp_seen_, tens of kB: the 70k slot visits
@@ -1037,7 +1062,7 @@ void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
   std::vector<int>& buf = lp_buf_;
   const size_t words = (hot_.size() + 63) / 64;
   if (lp_seen_.size() < words) lp_seen_.resize(words, 0);
-  for (int kf : localKFs_) {
+  for (int kf : kfl) {
     const std::vector<int>& mps = kfs_[kf].mps;
     buf.resize(mps.size());
     size_t n = 0;
@@ -1052,12 +1077,109 @@ void MapEngine::update_local_points() {  // Tracking::UpdateLocalPoints
       const uint64_t bit = 1ull << (h & 63);
       if (wd & bit) continue;
       if (!hot_[h].bad) {  // a bad point stays unmarked and is skipped again, as the reference
-        localPts_.push_back(h);
+        out.push_back(h);
         wd |= bit;
       }
     }
   }
-  for (int h : localPts_) lp_seen_[(size_t)h >> 6] &= ~(1ull << (h & 63));
+  for (int h : out) lp_seen_[(size_t)h >> 6] &= ~(1ull << (h & 63));
+}
+
+// UpdateLocalMap from C2's final matches while D1 runs (track_with_motion_model; L: the last frame
+// whose points the matches index).  Nothing of the map changes between here and TrackLocalMap but
+// the frame's bindings, which D1's outliers can only remove: commit_local_map checks that every
+// counted keyframe keeps a count (the same keyframe set, so the same expansion and points) and
+// recomputes the best-counted keyframe.  Marks are private (spec_mark_), so a speculation that is
+// never taken leaves no trace.
+void MapEngine::speculate_local_map(const MapFrameH& L, int n) {
+  spec_discard();
+  const int* match = (const int*)(h_early_ + kOutHdr);
+  if (spec_cnt_.size() < kfs_.size()) spec_cnt_.resize(kfs_.size(), 0);
+  if (spec_mark_.size() < kfs_.size()) spec_mark_.resize(kfs_.size(), 0);
+  spec_mps_.assign(n, -1);
+  spec_touched_.clear();
+  for (int i = 0; i < n; i++) {
+    if (match[i] < 0) continue;
+    const int h = L.mps[match[i]];
+    spec_mps_[i] = h;
+    if (h < 0) continue;
+    const MPoint& p = mp(h);
+    if (p.bad) continue;
+    for (const auto& kv : p.obs)
+      if (spec_cnt_[kv.first]++ == 0) spec_touched_.push_back(kv.first);
+  }
+  std::sort(spec_touched_.begin(), spec_touched_.end());
+  const long stamp = ++spec_stamp_;
+  spec_kfs_.clear();
+  for (const int id : spec_touched_)
+    if (!kfs_[id].bad) {
+      spec_kfs_.push_back(id);
+      spec_mark_[id] = stamp;
+    }
+  spec_frame_ = curId_;
+  if (spec_kfs_.empty()) return;  // (the reference's early return keeps the last local map)
+  expand_local_kfs(
+      spec_kfs_, [&](int id) { return spec_mark_[id] == stamp; },
+      [&](int id) { spec_mark_[id] = stamp; });
+  collect_local_points(spec_kfs_, spec_pts_);
+  spec_valid_ = true;
+  spec_tries_++;
+}
+
+void MapEngine::spec_discard() {
+  for (const int id : spec_touched_) spec_cnt_[id] = 0;
+  spec_touched_.clear();
+  spec_valid_ = false;
+}
+
+bool MapEngine::commit_local_map(MapFrameH& C) {
+  if (!spec_valid_ || spec_frame_ != curId_ || (int)spec_mps_.size() != C.n) {
+    spec_discard();
+    return false;
+  }
+  // the bindings now: a subset of the speculated ones; the dropped ones' counts come off
+  bool ok = true;
+  for (int i = 0; i < C.n && ok; i++) {
+    const int h = C.mps[i], s0 = spec_mps_[i];
+    if (h >= 0 && h != s0) {
+      ok = false;
+    } else if (s0 >= 0 && h < 0) {
+      const MPoint& p = mp(s0);
+      if (!p.bad)
+        for (const auto& kv : p.obs) spec_cnt_[kv.first]--;
+    }
+  }
+  for (size_t q = 0; q < spec_touched_.size() && ok; q++) {
+    const int id = spec_touched_[q];
+    ok = kfs_[id].bad || spec_cnt_[id] > 0;
+  }
+  if (!ok) {
+    spec_discard();
+    return false;
+  }
+  for (int i = 0; i < C.n; i++)
+    if (C.mps[i] >= 0 && mp(C.mps[i]).bad) C.mps[i] = -1;
+  int mx = 0, kmax = -1;
+  for (const int id : spec_touched_) {
+    const int cnt = spec_cnt_[id];
+    spec_cnt_[id] = 0;
+    if (kfs_[id].bad) continue;
+    if (cnt > mx) {
+      mx = cnt;
+      kmax = id;
+    }
+  }
+  spec_touched_.clear();
+  spec_valid_ = false;
+  for (const int id : spec_kfs_) kfs_[id].trackRef = curId_;
+  localKFs_.swap(spec_kfs_);
+  localPts_.swap(spec_pts_);
+  if (kmax >= 0) {
+    refKF_ = kmax;
+    C.refKF = kmax;
+  }
+  spec_hits_++;
+  return true;
 }
 
 void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const float* Tcw) {
@@ -1134,7 +1256,10 @@ void MapEngine::search_local_points(MapFrameH& C, const GridFrame& G, const floa
 }
 
 bool MapEngine::track_local_map(MapFrameH& C, const GridFrame& G, float* Tcw) {
-  MAP_PROF(2, update_local_keyframes(C); update_local_points());
+  MAP_PROF(2, if (!commit_local_map(C)) {
+    update_local_keyframes(C);
+    update_local_points();
+  });
   if (prof_on_) {
     prof_cnt_[0] += localKFs_.size();
     prof_cnt_[1] += localPts_.size();
