@@ -257,7 +257,9 @@ class MapEngine {
   // GPU (speculate_local_map) and taken by track_local_map when D1's outliers leave every counted
   // keyframe with a count (commit_local_map); MMT_LOCALMAP_SPEC=0 turns it off (A/B)
   bool spec_on_ = true, spec_valid_ = false;
-  bool overlap_c3_ = false;  // MMT_OVERLAP_C3=1: the overlap work waits for the C3 chain (A/B)
+  // the overlap work runs while the C3 chain executes when the C2 chain's wait holds the local
+  // map speculation (MMT_OVERLAP_C3=0: in the C2 chain as before, A/B)
+  bool overlap_c3_ = true;
   long spec_frame_ = -1, spec_stamp_ = 0, spec_hits_ = 0, spec_tries_ = 0;
   std::vector<int> spec_mps_, spec_cnt_, spec_touched_, spec_kfs_, spec_pts_;
   std::vector<long> spec_mark_;

@@ -645,8 +645,10 @@ void Tracker::ego_launch(const FrameArgs& a, FrameOut& out, hipStream_t st) {
   // may reset mLastFrame's pose (UpdateLastFrame), which the rest of this frame reads
   {
     MapStatsH& ms = out.map;
-    // the previous frame's object path runs while the first map chain is on the GPU (splitting
-    // it over the two map chains measured slower: C3 888 against 903 frames/s)
+    // the previous frame's object path runs while a map chain is on the GPU: the C3 chain when the
+    // C2 chain's wait holds the local map speculation (8-step bench 722 against 737 frames/s,
+    // medians of 5, profiles/r06_ab_overlap_c3.txt), else the first chain (splitting it over the
+    // two chains measured slower in round 4: 888 against 903 frames/s)
     map_.set_overlap([this] { obj_advance(); });
     const int rr = map_.track(C.m, G, ego_Tinit_, Ls.m, Ls.Tview, V_, hasVelocity_,
                               bSecondFrame_, ms, st);
