@@ -140,3 +140,62 @@ def test_vocabulary_tracking_c3_300_frames_matches_oracle(oracle_mod):
     assert {k: gb[k] for k in BOW_KEYS} == {k: ob[k] for k in BOW_KEYS}, (gb, ob)
     assert ob["trk_ok"] >= 1 and ob["reloc"] >= 2 and ob["triangulated"] > 100
     _check_maps(gm, om)
+
+
+def _run_gpu(seq, n, chunk, W, H, K, bf, nfeat):
+    import multimot_track_amd as M
+    cfg = M.kitti03_config(W, H, nfeat, max_batch=chunk)
+    cfg.fx, cfg.fy, cfg.cx, cfg.cy, cfg.bf = K["fx"], K["fy"], K["cx"], K["cy"], bf
+    ctx = M.Context(cfg)
+    got = []
+    try:
+        ctx.load_vocabulary(VOC)
+        for s0 in range(0, n, chunk):
+            sl = slice(s0, min(n, s0 + chunk))
+            got += ctx.track_chunk_device(seq["bgr"][sl], seq["disp"][sl], seq["flow"][sl],
+                                          seq["mask"][sl])
+        return got, ctx.bow_counters(), ctx.map_dump()
+    finally:
+        ctx.close()
+
+
+def _same(a, b):
+    if isinstance(a, dict):
+        return a.keys() == b.keys() and all(_same(a[k], b[k]) for k in a)
+    if isinstance(a, (list, tuple)):
+        return len(a) == len(b) and all(_same(x, y) for x, y in zip(a, b))
+    if isinstance(a, np.ndarray):
+        return a.shape == b.shape and np.array_equal(a, b, equal_nan=a.dtype.kind == "f")
+    if isinstance(a, (float, np.floating)) and np.isnan(a):
+        return isinstance(b, (float, np.floating)) and np.isnan(b)
+    return a == b
+
+
+def test_local_map_speculation_changes_nothing(monkeypatch, capfd):
+    """UpdateLocalMap built from C2's matches while D1 runs (taken when D1's outliers leave the
+    counted keyframe set unchanged, mmt_map.hip speculate_local_map / commit_local_map) and the
+    object path beside the C3 chain: every frame's output, the vocabulary counters and the final
+    map bit-identical to the build-as-you-go order (MMT_LOCALMAP_SPEC=0, MMT_OVERLAP_C3=0) over a
+    C3 drive with a textureless frame (a relocalisation)."""
+    import torch
+    from multimot_track_amd import scene
+    K = dict(scene.KITTI03)
+    R = scene.SequenceRenderer(scene.StreetScene(3, 1003), 1242, 375, K=K,
+                               device=torch.device("cuda:0"))
+    n = 160
+    seq = R.sequence(n)
+    seq["bgr"][90] = 128
+    args = (seq, n, 32, 1242, 375, K, 387.5744, 2000)
+    monkeypatch.setenv("MMT_MAP_PROFILE", "1")  # the speculation counters, at destruction
+    spec = _run_gpu(*args)
+    import re
+    m = re.search(r"speculated (\d+) times, taken (\d+)", capfd.readouterr().err)
+    tries, hits = int(m.group(1)), int(m.group(2))
+    print("local map speculated", tries, "taken", hits)
+    assert tries > hits > 0  # both the taken and the discarded path ran
+    monkeypatch.delenv("MMT_MAP_PROFILE")
+    monkeypatch.setenv("MMT_LOCALMAP_SPEC", "0")
+    monkeypatch.setenv("MMT_OVERLAP_C3", "0")
+    base = _run_gpu(*args)
+    assert spec[1]["reloc"] >= 1 and spec[1]["kfdb"] > 5
+    assert _same(spec, base)
